@@ -1,0 +1,150 @@
+"""Headline benchmark: images/sec of 2D UNet training on BraTS-shaped 128x128x4
+synthetic slices (BASELINE.json metric), one process per GPU.
+
+    python bench.py --gpus 1 --steps 20 --warmup 5
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29511 bench.py --gpus 8 --steps 20 --warmup 5
+
+Each timed step is a complete training step of the flagship configuration:
+device-side batch load, UNet forward (bf16 HIP kernels), Dice loss, backward,
+bucketed RCCL allreduce (overlapped with backward), fused TF-Adam update.
+Weak scaling: the per-GPU micro-batch is fixed (default 256 = the reference's
+per-worker shard of its 1024 global batch, `settings_dist.py:17`,
+`test_dist.py:390`), so the global batch is 256*N.  Random-init weights
+(he_uniform / glorot as the reference), synthetic data.
+
+Rank 0 prints ONE JSON line; ``value`` is whole-job images/sec computed from the
+MAX over ranks of the timed wall time.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--per_gpu_batch", type=int, default=256)
+    p.add_argument("--img_size", type=int, default=128)
+    p.add_argument("--in_channels", type=int, default=4)
+    p.add_argument("--dims", type=int, default=2)
+    p.add_argument("--use_upsampling", action="store_true")
+    p.add_argument("--backend", default="auto", choices=["auto", "native", "torch"])
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp16"])
+    p.add_argument("--bucket_mb", type=float, default=8.0)
+    p.add_argument("--no_overlap", action="store_true")
+    p.add_argument("--profile_dir", default="")
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    from unet_distributed_amd.config import Config
+    from unet_distributed_amd.data.datasets import synthetic_brats
+    from unet_distributed_amd.models import reference
+    from unet_distributed_amd.models.spec import spec_from_config
+    from unet_distributed_amd.parallel import dist as D
+    from unet_distributed_amd.parallel.grad_sync import GradSync, plan_buckets
+    from unet_distributed_amd.runtime.backends import make_backend
+    from unet_distributed_amd.runtime.optim import TFAdam
+    from unet_distributed_amd.runtime.params import FlatParams
+    from unet_distributed_amd.runtime.trainer import _NativeOpt
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    ctx = D.init("auto", "auto", 600.0)
+    N = ctx.world_size
+    if world_env != a.gpus and ctx.rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (a.gpus, world_env), file=sys.stderr)
+    cfg = Config(batch_size=a.per_gpu_batch * N, in_channels=a.in_channels, img_size=a.img_size,
+                 dims=a.dims, use_upsampling=a.use_upsampling, backend=a.backend, dtype=a.dtype,
+                 synthetic=True, no_checkpoint=True, bucket_mb=a.bucket_mb, overlap_comm=not a.no_overlap)
+    dev = ctx.device
+    spec = spec_from_config(cfg)
+    flat = FlatParams(spec, device=dev)
+    flat.load_dict(reference.init_params(spec, seed=cfg.seed))
+    D.broadcast_(flat.master, 0)
+    bounds = plan_buckets(flat, cfg.bucket_mb)
+    backend = make_backend(spec, flat, cfg, dev, a.per_gpu_batch, bounds)
+    if hasattr(backend, "engine"):
+        backend.engine.repack()
+    sync = GradSync(flat, bounds, ctx, overlap=cfg.overlap_comm)
+    opt = TFAdam(flat, cfg, native=_NativeOpt(backend) if hasattr(backend, "adam_step") else None)
+
+    # two distinct synthetic batches resident on the device (per-rank shards)
+    B = a.per_gpu_batch
+    xs, ys = [], []
+    for k in range(2):
+        x, y = synthetic_brats(B, a.img_size, a.in_channels, a.dims, seed=1000 * ctx.rank + k)
+        xs.append(torch.from_numpy(x).to(dev))
+        ys.append(torch.from_numpy(y).to(dev))
+
+    def step(i):
+        backend.fwd_bwd(xs[i % 2], ys[i % 2], seed=12345 + i, on_segment=sync.on_segment)
+        sync.finish()
+        opt.step()
+
+    for i in range(a.warmup):
+        step(i)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    D.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    prof = None
+    if a.profile_dir and ctx.rank == 0:
+        prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU,
+                                                  torch.profiler.ProfilerActivity.CUDA])
+        prof.__enter__()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + i)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    D.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        os.makedirs(a.profile_dir, exist_ok=True)
+        prof.export_chrome_trace(os.path.join(a.profile_dir, "trace.json"))
+    dt = D.allreduce_max_scalar(dt, dev)
+    imgs = a.steps * B * N
+    s = backend.sums()
+    i_, st, sp = [float(v) for v in s[:3].tolist()]
+    dice = (2 * i_ + 1) / (st + sp + 1)
+    if ctx.rank == 0:
+        rec = {
+            "metric": "images/sec (whole node) 2D UNet BraTS 128x128x4 training",
+            "value": round(imgs / dt, 2),
+            "unit": "images/sec",
+            "n_gpus": N,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * dt / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.dtype,
+            "data": "synthetic (BraTS-shaped %dx%dx%d slices, random-init weights)"
+                    % (a.img_size, a.img_size, a.in_channels),
+            "config": {"model": "unet2d-%s (base 32, depth 4, %d params)"
+                                % ("upsampling" if a.use_upsampling else "transposed", spec.num_params()),
+                       "global_batch": B * N, "per_gpu_batch": B, "seq_len": None,
+                       "img_size": a.img_size, "in_channels": a.in_channels,
+                       "parallelism": "dp%d" % N, "backend": backend.name},
+            "train_dice_last_batch": round(dice, 5),
+        }
+        print(json.dumps(rec), flush=True)
+    D.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,296 @@
+"""Numerics of the gfx950 HIP kernels against fp32 PyTorch references of the same op.
+
+Inputs are bf16-rounded first so the reference sees exactly what the kernel
+reads; tolerances cover fp32-accumulate vs bf16 output rounding.
+"""
+
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def C():
+    from unet_distributed_amd import native
+    return native.require()
+
+
+def ptr(t):
+    return int(t.data_ptr())
+
+
+def stream():
+    return int(torch.cuda.current_stream().cuda_stream)
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1)
+
+
+def pack_fwd(w_hwio):          # [kh][kw][ci][co] -> [co][kh*kw*ci]
+    kh, kw, ci, co = w_hwio.shape
+    return w_hwio.permute(3, 0, 1, 2).reshape(co, kh * kw * ci).contiguous()
+
+
+def pack_dgrad(w_hwio):        # -> [ci][taps flipped][co]
+    kh, kw, ci, co = w_hwio.shape
+    return w_hwio.flip(0, 1).permute(2, 0, 1, 3).reshape(ci, kh * kw * co).contiguous()
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout", [(2, 16, 32, 32), (2, 8, 64, 128), (1, 32, 32, 64), (4, 8, 128, 256)])
+def test_conv3x3_fwd_bias_relu(cuda_dev, N, H, Cin, Cout):
+    torch.manual_seed(0)
+    x = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, Cin, Cout, device=cuda_dev) * 0.1).bfloat16()
+    b = torch.randn(Cout, device=cuda_dev)
+    out = torch.empty(N, H, H, Cout, device=cuda_dev, dtype=torch.bfloat16)
+    wp = pack_fwd(w)
+    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(x), wgt=ptr(wp),
+                      bias=ptr(b), Cout=Cout, relu=1, dst1=ptr(out)), stream())
+    ref = nhwc(F.relu(F.conv2d(nchw(x.float()), w.float().permute(3, 2, 0, 1), b, padding=1)))
+    assert rel_err(out, ref) < 1e-2
+
+
+def test_conv3x3_concat_dual_source_and_upsample(cuda_dev):
+    torch.manual_seed(1)
+    N, H, C1, C2, Co = 2, 16, 32, 64, 64
+    lo = torch.randn(N, H // 2, H // 2, C1, device=cuda_dev).bfloat16()   # upsampled source
+    skip = torch.randn(N, H, H, C2, device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, C1 + C2, Co, device=cuda_dev) * 0.05).bfloat16()
+    out = torch.empty(N, H, H, Co, device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=C1, C2=C2, up1=2, src1=ptr(lo),
+                      src2=ptr(skip), wgt=ptr(pack_fwd(w)), Cout=Co, relu=0, dst1=ptr(out)), stream())
+    up = F.interpolate(nchw(lo.float()), scale_factor=2, mode="nearest")
+    ref = nhwc(F.conv2d(torch.cat([up, nchw(skip.float())], 1), w.float().permute(3, 2, 0, 1), padding=1))
+    assert rel_err(out, ref) < 1e-2
+
+
+def test_conv_dgrad_dual_dest_mask(cuda_dev):
+    """dgrad of a concat conv: flipped weights, channel split into two tensors, ReLU mask on the skip half."""
+    torch.manual_seed(2)
+    N, H, C1, C2, Co = 2, 16, 32, 32, 32
+    xin = torch.randn(N, H, H, C1 + C2, device=cuda_dev)
+    skip = F.relu(torch.randn(N, H, H, C2, device=cuda_dev)).bfloat16()
+    w = (torch.randn(3, 3, C1 + C2, Co, device=cuda_dev) * 0.1).bfloat16()
+    dy = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
+    d1 = torch.empty(N, H, H, C1, device=cuda_dev, dtype=torch.bfloat16)
+    d2 = torch.empty(N, H, H, C2, device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Co, src1=ptr(dy),
+                      wgt=ptr(pack_dgrad(w)), Cout=C1 + C2, D1=C1, dst1=ptr(d1), dst2=ptr(d2),
+                      mask2=ptr(skip), mask_scale2=1.25), stream())
+    xr = nchw(xin).requires_grad_(True)
+    y = F.conv2d(xr, w.float().permute(3, 2, 0, 1), padding=1)
+    (g,) = torch.autograd.grad(y, xr, nchw(dy.float()))
+    g = nhwc(g)
+    ref1 = g[..., :C1]
+    ref2 = g[..., C1:] * (skip.float() > 0) * 1.25
+    assert rel_err(d1, ref1) < 1e-2
+    assert rel_err(d2, ref2) < 1e-2
+
+
+def test_conv_first_layer_smallc(cuda_dev):
+    torch.manual_seed(3)
+    N, H, Cin, Co = 2, 32, 4, 32
+    x = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, Cin, Co, device=cuda_dev) * 0.2).bfloat16()
+    b = torch.randn(Co, device=cuda_dev)
+    wp = torch.zeros(Co, 64, device=cuda_dev, dtype=torch.bfloat16)
+    wp[:, :36] = pack_fwd(w)
+    out = torch.empty(N, H, H, Co, device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(x), wgt=ptr(wp),
+                      bias=ptr(b), Cout=Co, relu=1, dst1=ptr(out)), stream())
+    ref = nhwc(F.relu(F.conv2d(nchw(x.float()), w.float().permute(3, 2, 0, 1), b, padding=1)))
+    assert rel_err(out, ref) < 1e-2
+
+
+def test_tconv_fwd_shuffle_and_dgrad(cuda_dev):
+    torch.manual_seed(4)
+    N, H, Ci, Co = 2, 8, 64, 32
+    x = F.relu(torch.randn(N, H, H, Ci, device=cuda_dev)).bfloat16()
+    k = (torch.randn(2, 2, Co, Ci, device=cuda_dev) * 0.1).bfloat16()   # Keras (kh,kw,Cout,Cin)
+    b = torch.randn(Co, device=cuda_dev)
+    out = torch.empty(N, 2 * H, 2 * H, Co, device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, C1=Ci, src1=ptr(x), wgt=ptr(k.reshape(4 * Co, Ci)),
+                      bias=ptr(b), Cout=4 * Co, shuffle=2, dst1=ptr(out)), stream())
+    wt = k.float().permute(3, 2, 0, 1)      # (Cin, Cout, kh, kw)
+    ref = nhwc(F.conv_transpose2d(nchw(x.float()), wt, b, stride=2))
+    assert rel_err(out, ref) < 1e-2
+    # dgrad: 2x2 stride-2 conv of dOut with weights [ci][tap][co], masked by x > 0
+    dout = torch.randn(N, 2 * H, 2 * H, Co, device=cuda_dev).bfloat16()
+    wdg = k.permute(3, 0, 1, 2).reshape(Ci, 4 * Co).contiguous()
+    dx = torch.empty(N, H, H, Ci, device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=2 * H, IW=2 * H, KH=2, KW=2, stride=2, pad=0, C1=Co,
+                      src1=ptr(dout), wgt=ptr(wdg), Cout=Ci, dst1=ptr(dx), mask1=ptr(x)), stream())
+    xr = nchw(x.float()).requires_grad_(True)
+    (g,) = torch.autograd.grad(F.conv_transpose2d(xr, wt, stride=2), xr, nchw(dout.float()))
+    ref = nhwc(g) * (x.float() > 0)
+    assert rel_err(dx, ref) < 1e-2
+
+
+def _wgrad(d, splits, taps, Mtot, Mout, Nc, out_numel, bias_w=None, rows=None):
+    dev = torch.device("cuda")
+    slab = torch.zeros(splits * taps * Mtot * Nc, device=dev)
+    bslab = torch.zeros(splits * 8 * max(Mtot, Nc), device=dev)
+    d = dict(d, splits=splits, slab=ptr(slab), bias_slab=ptr(bslab))
+    C().wgrad(d, stream())
+    out = torch.zeros(out_numel, device=dev)
+    ints = [splits, taps, Mtot, Mout, Nc] + (list(rows) if rows else [])
+    C().generic("wgrad_reduce", [ptr(slab), ptr(out)], ints, [1.0], stream())
+    bout = None
+    if bias_w is not None:
+        nrows, w = bias_w
+        bout = torch.zeros(w, device=dev)
+        C().generic("wgrad_reduce", [ptr(bslab), ptr(bout)], [nrows, 1, 1, 1, w], [1.0], stream())
+    return out, bout
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,splits", [(4, 16, 32, 32, 3), (2, 16, 64, 128, 2), (2, 8, 128, 128, 4),
+                                                  (2, 8, 256, 512, 2)])
+def test_conv_wgrad_and_bias(cuda_dev, N, H, Cin, Cout, splits):
+    torch.manual_seed(5)
+    x = F.relu(torch.randn(N, H, H, Cin, device=cuda_dev)).bfloat16()
+    dy = torch.randn(N, H, H, Cout, device=cuda_dev).bfloat16()
+    BM, BN, NTAP, smallc = C().wgrad_pick(Cin, 0, Cout, 9)
+    d = dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=Cin, a1=ptr(x), b=ptr(dy), Nc=Cout,
+             bias_mode=1)
+    gw, gb = _wgrad(d, splits, 9, Cin, Cin, Cout, 9 * Cin * Cout, bias_w=(splits, Cout))
+    w = torch.zeros(Cout, Cin, 3, 3, device=cuda_dev, requires_grad=True)
+    bb = torch.zeros(Cout, device=cuda_dev, requires_grad=True)
+    y = F.conv2d(nchw(x.float()), w, bb, padding=1)
+    gwr, gbr = torch.autograd.grad(y, [w, bb], nchw(dy.float()))
+    ref = gwr.permute(2, 3, 1, 0).reshape(-1)        # HWIO
+    assert rel_err(gw, ref) < 2e-3
+    assert rel_err(gb, gbr) < 2e-3
+
+
+def test_wgrad_concat_upsample(cuda_dev):
+    torch.manual_seed(6)
+    N, H, C1, C2, Co = 2, 16, 32, 32, 32
+    lo = F.relu(torch.randn(N, H // 2, H // 2, C1, device=cuda_dev)).bfloat16()
+    skip = F.relu(torch.randn(N, H, H, C2, device=cuda_dev)).bfloat16()
+    dy = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
+    d = dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=C1, M2=C2, upA=2, a1=ptr(lo),
+             a2=ptr(skip), b=ptr(dy), Nc=Co)
+    gw, _ = _wgrad(d, 2, 9, C1 + C2, C1 + C2, Co, 9 * (C1 + C2) * Co)
+    inp = torch.cat([F.interpolate(nchw(lo.float()), scale_factor=2, mode="nearest"), nchw(skip.float())], 1)
+    w = torch.zeros(Co, C1 + C2, 3, 3, device=cuda_dev, requires_grad=True)
+    (gwr,) = torch.autograd.grad(F.conv2d(inp, w, padding=1), [w], nchw(dy.float()))
+    assert rel_err(gw, gwr.permute(2, 3, 1, 0).reshape(-1)) < 2e-3
+
+
+def test_wgrad_first_layer_smallc(cuda_dev):
+    torch.manual_seed(7)
+    N, H, Creal, Cpad, Co = 2, 32, 1, 4, 32
+    x = torch.zeros(N, H, H, Cpad, device=cuda_dev)
+    x[..., :Creal] = torch.randn(N, H, H, Creal, device=cuda_dev)
+    x = x.bfloat16()
+    dy = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
+    d = dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=Cpad, a1=ptr(x), b=ptr(dy), Nc=Co,
+             bias_mode=1)
+    gw, gb = _wgrad(d, 3, 1, 64, 9 * Creal, Co, 9 * Creal * Co, bias_w=(3, Co), rows=(Cpad, Creal))
+    w = torch.zeros(Co, Creal, 3, 3, device=cuda_dev, requires_grad=True)
+    bb = torch.zeros(Co, device=cuda_dev, requires_grad=True)
+    gwr, gbr = torch.autograd.grad(F.conv2d(nchw(x.float()[..., :Creal]), w, bb, padding=1), [w, bb],
+                                   nchw(dy.float()))
+    assert rel_err(gw, gwr.permute(2, 3, 1, 0).reshape(-1)) < 2e-3
+    assert rel_err(gb, gbr) < 2e-3
+
+
+def test_tconv_wgrad_bias_mode2(cuda_dev):
+    torch.manual_seed(8)
+    N, H, Ci, Co = 2, 8, 64, 32
+    x = F.relu(torch.randn(N, H, H, Ci, device=cuda_dev)).bfloat16()
+    dout = torch.randn(N, 2 * H, 2 * H, Co, device=cuda_dev).bfloat16()
+    d = dict(N=N, QH=H, QW=H, AH=2 * H, AW=2 * H, KH=2, KW=2, stride=2, pad=0, M1=Co, a1=ptr(dout),
+             b=ptr(x), Nc=Ci, bias_mode=2)
+    BM, BN, NTAP, _ = C().wgrad_pick(Co, 0, Ci, 4)
+    tg = 4 // NTAP
+    gw, gb = _wgrad(d, 2, 4, Co, Co, Ci, 4 * Co * Ci, bias_w=(2 * tg, Co))
+    k = torch.zeros(Ci, Co, 2, 2, device=cuda_dev, requires_grad=True)
+    bb = torch.zeros(Co, device=cuda_dev, requires_grad=True)
+    gk, gbr = torch.autograd.grad(F.conv_transpose2d(nchw(x.float()), k, bb, stride=2), [k, bb],
+                                  nchw(dout.float()))
+    ref = gk.permute(2, 3, 1, 0).reshape(-1)     # (kh, kw, Cout, Cin)
+    assert rel_err(gw, ref) < 2e-3
+    assert rel_err(gb, gbr) < 2e-3
+
+
+def test_maxpool_fwd_bwd_with_skip(cuda_dev):
+    torch.manual_seed(9)
+    N, H, Cc = 2, 16, 32
+    x = F.relu(torch.randn(N, H, H, Cc, device=cuda_dev)).bfloat16()
+    y = torch.empty(N, H // 2, H // 2, Cc, device=cuda_dev, dtype=torch.bfloat16)
+    C().generic("pool_fwd", [ptr(x), ptr(y)], [N, 1, H, H, Cc, 0], [], stream())
+    ref = nhwc(F.max_pool2d(nchw(x.float()), 2))
+    assert (y.float() - ref).abs().max().item() == 0
+    dy = torch.randn_like(y.float()).bfloat16()
+    skip = torch.randn_like(x.float()).bfloat16()
+    dx = torch.empty_like(x)
+    C().generic("pool_bwd", [ptr(x), ptr(dy), ptr(skip), ptr(dx)], [N, 1, H, H, Cc, 0], [], stream())
+    xr = nchw(x.float()).requires_grad_(True)
+    (g,) = torch.autograd.grad(F.max_pool2d(xr, 2), xr, nchw(dy.float()))
+    assert rel_err(dx, nhwc(g) + skip.float()) < 1e-2
+
+
+def test_head_fwd_bwd(cuda_dev):
+    torch.manual_seed(10)
+    P, Cc = 4096, 32
+    x = F.relu(torch.randn(P, Cc, device=cuda_dev)).bfloat16()
+    w = torch.randn(Cc, device=cuda_dev) * 0.3
+    b = torch.randn(1, device=cuda_dev)
+    t = (torch.rand(P, device=cuda_dev) > 0.7).bfloat16()
+    prob = torch.empty(P, device=cuda_dev)
+    nb = C().head_blocks(P)
+    part = torch.empty(nb * (Cc + 1) + 4 * nb, device=cuda_dev)
+    sums = torch.empty(4, device=cuda_dev)
+    C().generic("head_fwd", [ptr(x), ptr(w), ptr(b), ptr(t), ptr(prob), ptr(part), ptr(sums)], [P, Cc], [],
+                stream())
+    xr = x.float().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    z = xr @ wr + br
+    p = torch.sigmoid(z)
+    tf = t.float()
+    I, St, Sp = (tf * p).sum(), tf.sum(), p.sum()
+    bce = F.binary_cross_entropy_with_logits(z, tf, reduction="sum")
+    assert rel_err(prob, p) < 1e-4
+    assert rel_err(sums, torch.stack([I, St, Sp, bce])) < 1e-4
+    loss = -torch.log(2 * I + 1) + torch.log(St + Sp + 1) + 0.5 * bce / P
+    gx, gw, gb = torch.autograd.grad(loss, [xr, wr, br])
+    dx = torch.empty_like(x)
+    ow = torch.empty(Cc, device=cuda_dev)
+    ob = torch.empty(1, device=cuda_dev)
+    C().generic("head_bwd", [ptr(x), ptr(w), ptr(prob), ptr(t), ptr(sums), ptr(dx), ptr(part), ptr(ow),
+                             ptr(ob)], [P, Cc], [1.0 / P, 0.5, 1.0], stream())
+    assert rel_err(dx, gx * (x.float() > 0)) < 1e-2
+    assert rel_err(ow, gw) < 1e-3
+    assert rel_err(ob, gb) < 1e-3
+
+
+def test_dropout_matches_reference_hash(cuda_dev):
+    from unet_distributed_amd.models.reference import dropout_keep_mask
+    torch.manual_seed(11)
+    N, H, Cin, Co = 2, 8, 32, 64
+    x = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, Cin, Co, device=cuda_dev) * 0.1).bfloat16()
+    out = torch.empty(N, H, H, Co, device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(x),
+                      wgt=ptr(pack_fwd(w)), Cout=Co, relu=1, dst1=ptr(out), drop_rate=0.2, seed=1234, salt=7),
+                 stream())
+    keep = dropout_keep_mask(1234, 7, out.shape, 0.2, cuda_dev)
+    ref = nhwc(F.relu(F.conv2d(nchw(x.float()), w.float().permute(3, 2, 0, 1), padding=1))) * keep / 0.8
+    assert rel_err(out, ref) < 1e-2
+    frac = keep.float().mean().item()
+    assert 0.75 < frac < 0.85

@@ -1,0 +1,75 @@
+// Host/device parameter blocks of the conv kernels (POD, passed by value).
+#pragma once
+#include <stdint.h>
+
+namespace unet {
+
+// Implicit-GEMM "NT" convolution: out[q][n] = epilogue(sum_{tap,c} X[q*s + tap - pad][c] * W[n][tap][c])
+// GEMM M = output pixels q over [N][OD][OH][OW], GEMM N = Cout, K = taps * Cin.
+// One kernel serves: conv forward, conv dgrad (flipped/transposed weights),
+// transposed-conv forward (1x1 GEMM + pixel-shuffle store) and transposed-conv
+// dgrad (2x2 stride-2 conv).
+struct ConvFwdParams {
+  int N, OD, OH, OW;          // output grid (GEMM rows)
+  int ID, IH, IW;             // input grid, full-resolution coordinates
+  int KD, KH, KW, stride, pad;
+  int C1, C2;                 // input channels read from src1 / src2 (concat-free skip)
+  int up1;                    // src1 is stored at 1/up1 resolution (nearest upsample fold)
+  const void* src1;
+  const void* src2;
+  const void* wgt;            // bf16 [Cout][KD*KH*KW][C1+C2]
+  const float* bias;          // [Cout] or nullptr
+  int Cout;
+  int relu;
+  float out_scale;
+  float drop_rate;            // >0: inverted dropout on the output
+  uint32_t seed, salt;
+  void* dst1;                 // channels [0, D1)
+  void* dst2;                 // channels [D1, Cout)
+  int D1;
+  const void* mask1;          // nullptr or tensor shaped like dst1: out *= (mask1 > 0)
+  const void* mask2;
+  float mask_scale1, mask_scale2;
+  int shuffle;                // 0, or number of upsampled dims (2/3): tconv pixel shuffle
+  float* stats;               // nullptr or [2][Cout] per-channel sum / sum of squares (BN)
+};
+
+// "TN" weight-gradient GEMM with split-K over pixels:
+//   slab[split][tap][m][n] = sum_{q in split} A[q*s + tap - pad][m] * B[q][n]
+// conv 3x3:  A = layer input X (m = Cin), B = dY_pre (n = Cout)  -> HWIO
+// tconv 2x2: A = dOut (m = Cout),         B = layer input (n = Cin) -> (kh,kw,Cout,Cin)
+struct WgradParams {
+  int N, QD, QH, QW;          // pixel grid of B (the K dimension)
+  int AD, AH, AW;             // spatial grid of A
+  int KD, KH, KW, stride, pad;
+  int M1, M2;                 // A channels from a1 / a2 (concat input of decoder convs)
+  int upA;                    // a1 stored at 1/upA resolution
+  const void* a1;
+  const void* a2;
+  const void* b;              // [Q][Nc]
+  int Nc;
+  int splits;                 // K splits (grid dim)
+  int tap_groups;             // taps handled per WG = (KD*KH*KW)/tap_groups
+  float* slab;                // [splits][taps][M][Nc] fp32
+  // fused bias gradient: 0 = off, 1 = column sums of B (conv: dY -> n),
+  // 2 = column sums of A over the WG's taps (tconv: dOut -> m)
+  int bias_mode;
+  float* bias_slab;           // [splits][tap_groups][M or Nc] fp32
+};
+
+// Tile configuration chosen for a wgrad problem (shared with the host planner).
+struct WgradCfg {
+  int BM, BN, NTAP, smallc;
+};
+
+// Segment descriptor of the fused Adam + bf16 repack kernel (adam.hip).
+struct PackSeg {
+  int off, n;          // element range in the flat master buffer
+  int kind;            // 0 = none (bias / fp32-only), 1 = conv, 2 = tconv
+  int T, Ci, Co;       // taps, input/output channels (TF kernel semantics)
+  int Ci_pad, rowstride;
+  long long fwd_off;   // element offset into the bf16 weight arena, -1 = none
+  long long dg_off;    // dgrad copy, -1 = none
+};
+
+}  // namespace unet

@@ -1,0 +1,206 @@
+// Memory-bound kernels of the UNet step on gfx950: all 16-byte vectorised
+// (8 x bf16 per lane, cdna_hip_programming.md §6 Guideline 13).
+//
+//  * cast_input: fp32 NHWC image -> bf16 with channel padding (first layer reads 4/8 channels)
+//  * maxpool2_fwd / maxpool2_bwd: 2x2(x2) max-pool (`model.py:53-69`); the backward
+//    routes to the FIRST maximum of each window (TF MaxPoolGrad tie rule) and
+//    fuses the add of the skip-connection gradient coming from the decoder
+//    (the concat's dgrad), so the encoder output gradient is written once.
+//  * upsample2_bwd: 2x2(x2) sum of the full-res gradient of the folded nearest
+//    upsample (`model.py:76-109` upsampling variant), masked by the source's ReLU.
+#include "common.h"
+
+namespace unet {
+
+namespace {
+
+__device__ __forceinline__ uint32_t bf_pos_mask(uint32_t w) {
+  const uint32_t lo = w & 0xffffu, hi = w >> 16;
+  return ((lo != 0u && !(lo & 0x8000u)) ? 0xffffu : 0u) | ((hi != 0u && !(hi & 0x8000u)) ? 0xffff0000u : 0u);
+}
+
+__global__ void __launch_bounds__(256) cast_input_kernel(const float* __restrict__ x, int P, int Cin, int Cpad,
+                                                         bf16* __restrict__ y) {
+  const int total = P * Cpad;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int p = i / Cpad, c = i - p * Cpad;
+    y[i] = (bf16)(c < Cin ? x[(size_t)p * Cin + c] : 0.f);
+  }
+}
+
+// one thread = one pooled pixel x 8 channels
+__global__ void __launch_bounds__(256) maxpool2_fwd_kernel(const bf16* __restrict__ x, int N, int D, int H, int W,
+                                                           int C, int dims3, bf16* __restrict__ y) {
+  const int OD = dims3 ? D / 2 : 1, OH = H / 2, OW = W / 2;
+  const int cpp = C / 8;
+  const long long total = (long long)N * OD * OH * OW * cpp;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cc = i % cpp;
+    long long r = i / cpp;
+    const int ow = r % OW;
+    r /= OW;
+    const int oh = r % OH;
+    r /= OH;
+    const int od = r % OD;
+    const int n = r / OD;
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+    const int nz = dims3 ? 2 : 1;
+    for (int dz = 0; dz < nz; ++dz)
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 2; ++dx) {
+          const int id = dims3 ? 2 * od + dz : 0;
+          const size_t pix = (((size_t)n * D + id) * H + 2 * oh + dy) * W + 2 * ow + dx;
+          const u32x4 v = *(const u32x4*)(x + pix * C + cc * 8);
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
+        }
+    *(u32x4*)(y + (size_t)i * 8) = pack8(m);
+  }
+}
+
+// dx[window] = (first argmax ? dy : 0) + skip_grad (optional)
+__global__ void __launch_bounds__(256) maxpool2_bwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                           const bf16* __restrict__ skip, int N, int D, int H, int W,
+                                                           int C, int dims3, bf16* __restrict__ dx) {
+  const int OD = dims3 ? D / 2 : 1, OH = H / 2, OW = W / 2;
+  const int cpp = C / 8;
+  const long long total = (long long)N * OD * OH * OW * cpp;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cc = i % cpp;
+    long long r = i / cpp;
+    const int ow = r % OW;
+    r /= OW;
+    const int oh = r % OH;
+    r /= OH;
+    const int od = r % OD;
+    const int n = r / OD;
+    const int nz = dims3 ? 2 : 1;
+    float g[8];
+    unpack8(*(const u32x4*)(dy + (size_t)i * 8), g);
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      best[e] = -INFINITY;
+      arg[e] = 0;
+    }
+    size_t pix[8];
+    int k = 0;
+    for (int dz = 0; dz < nz; ++dz)
+#pragma unroll
+      for (int dyy = 0; dyy < 2; ++dyy)
+#pragma unroll
+        for (int dxx = 0; dxx < 2; ++dxx) {
+          const int id = dims3 ? 2 * od + dz : 0;
+          pix[k] = (((size_t)n * D + id) * H + 2 * oh + dyy) * W + 2 * ow + dxx;
+          float f[8];
+          unpack8(*(const u32x4*)(x + pix[k] * C + cc * 8), f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (f[e] > best[e]) {
+              best[e] = f[e];
+              arg[e] = k;
+            }
+          ++k;
+        }
+    for (int kk = 0; kk < k; ++kk) {
+      float o[8];
+      if (skip) {
+        unpack8(*(const u32x4*)(skip + pix[kk] * C + cc * 8), o);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (arg[e] == kk) o[e] += g[e];
+      *(u32x4*)(dx + pix[kk] * C + cc * 8) = pack8(o);
+    }
+  }
+}
+
+// dlow[p] = sum_{2x2(x2) children} dup[child] * (mask[p] > 0)
+__global__ void __launch_bounds__(256) upsample2_bwd_kernel(const bf16* __restrict__ dup, const bf16* __restrict__ mask,
+                                                            int N, int D, int H, int W, int C, int dims3,
+                                                            bf16* __restrict__ dlow) {
+  // D, H, W: LOW resolution dims
+  const int cpp = C / 8;
+  const int FD = dims3 ? 2 : 1;
+  const long long total = (long long)N * D * H * W * cpp;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int cc = i % cpp;
+    long long r = i / cpp;
+    const int w = r % W;
+    r /= W;
+    const int h = r % H;
+    r /= H;
+    const int d = r % D;
+    const int n = r / D;
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int dz = 0; dz < FD; ++dz)
+      for (int dy = 0; dy < 2; ++dy)
+        for (int dx = 0; dx < 2; ++dx) {
+          const size_t pix = (((size_t)n * (D * FD) + d * FD + dz) * (2 * H) + 2 * h + dy) * (2 * W) + 2 * w + dx;
+          float f[8];
+          unpack8(*(const u32x4*)(dup + pix * C + cc * 8), f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s[e] += f[e];
+        }
+    u32x4 v = pack8(s);
+    if (mask) {
+      const u32x4 mv = *(const u32x4*)(mask + (size_t)i * 8);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] &= bf_pos_mask(mv[e]);
+    }
+    *(u32x4*)(dlow + (size_t)i * 8) = v;
+  }
+}
+
+inline int grid_for(long long work, int per_block = 256) {
+  long long g = (work + per_block - 1) / per_block;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+hipError_t cast_input_launch(const float* x, int P, int Cin, int Cpad, void* y, hipStream_t s) {
+  hipLaunchKernelGGL(cast_input_kernel, dim3(grid_for((long long)P * Cpad)), dim3(256), 0, s, x, P, Cin, Cpad,
+                     (bf16*)y);
+  return hipGetLastError();
+}
+
+hipError_t maxpool2_fwd_launch(const void* x, int N, int D, int H, int W, int C, int dims3, void* y, hipStream_t s) {
+  const long long work = (long long)N * (dims3 ? D / 2 : 1) * (H / 2) * (W / 2) * (C / 8);
+  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const bf16*)x, N, D, H, W, C,
+                     dims3, (bf16*)y);
+  return hipGetLastError();
+}
+
+hipError_t maxpool2_bwd_launch(const void* x, const void* dy, const void* skip, int N, int D, int H, int W, int C,
+                               int dims3, void* dx, hipStream_t s) {
+  const long long work = (long long)N * (dims3 ? D / 2 : 1) * (H / 2) * (W / 2) * (C / 8);
+  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const bf16*)x, (const bf16*)dy,
+                     (const bf16*)skip, N, D, H, W, C, dims3, (bf16*)dx);
+  return hipGetLastError();
+}
+
+hipError_t upsample2_bwd_launch(const void* dup, const void* mask, int N, int D, int H, int W, int C, int dims3,
+                                void* dlow, hipStream_t s) {
+  const long long work = (long long)N * D * H * W * (C / 8);
+  hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const bf16*)dup,
+                     (const bf16*)mask, N, D, H, W, C, dims3, (bf16*)dlow);
+  return hipGetLastError();
+}
+
+}  // namespace unet

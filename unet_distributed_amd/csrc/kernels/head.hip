@@ -1,0 +1,225 @@
+// Fused segmentation head + loss on gfx950.
+//
+// Forward (`model.py:119-120` Mask 1x1 conv + sigmoid, `model.py:4-21` Dice):
+//   z_p = sum_c x[p][c] w[c] + b;   prob_p = sigmoid(z_p)
+//   per-block partials of {I = sum t*p, St = sum t, Sp = sum p, BCE = sum bce(z, t)}
+//   then ONE deterministic block reduces the partials -> sums[4] on device
+//   (no host sync; metrics are read lazily by the logger).
+// Backward:
+//   dL/dp = -2 t / (2I + 1) + 1 / (St + Sp + 1)              (-log Dice)
+//   dz    = g * (dL/dp * p (1 - p) + bce_w * (p - t) / P_total)
+//   dx[p][c] = dz w[c] * (x[p][c] > 0)   (ReLU of conv9b folded in)
+//   dW[c] = sum dz x[p][c], db = sum dz   -> per-block partials, reduced deterministically.
+#include "common.h"
+
+namespace unet {
+
+namespace {
+
+constexpr int HT = 256;
+
+template <int C>
+__global__ void __launch_bounds__(HT) head_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+                                                      const float* __restrict__ b, const bf16* __restrict__ t,
+                                                      int P, float* __restrict__ prob, float* __restrict__ partial) {
+  __shared__ float red[4][HT / 64];
+  float wr[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) wr[c] = w[c];
+  const float bias = b[0];
+  float sI = 0.f, sT = 0.f, sP = 0.f, sB = 0.f;
+  for (int p = blockIdx.x * HT + threadIdx.x; p < P; p += gridDim.x * HT) {
+    float z = bias;
+#pragma unroll
+    for (int c8 = 0; c8 < C / 8; ++c8) {
+      float f[8];
+      unpack8(*(const u32x4*)(x + (size_t)p * C + c8 * 8), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z += f[e] * wr[c8 * 8 + e];
+    }
+    const float pr = 1.f / (1.f + __expf(-z));
+    prob[p] = pr;
+    if (t) {
+      const float tv = (float)t[p];
+      sI += tv * pr;
+      sT += tv;
+      sP += pr;
+      sB += fmaxf(z, 0.f) - z * tv + log1pf(__expf(-fabsf(z)));
+    } else {
+      sP += pr;
+    }
+  }
+  sI = wave_sum(sI);
+  sT = wave_sum(sT);
+  sP = wave_sum(sP);
+  sB = wave_sum(sB);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][wv] = sI;
+    red[1][wv] = sT;
+    red[2][wv] = sP;
+    red[3][wv] = sB;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    float s = 0.f;
+    for (int k = 0; k < HT / 64; ++k) s += red[threadIdx.x][k];
+    partial[blockIdx.x * 4 + threadIdx.x] = s;
+  }
+}
+
+// out[j] = sum_b partial[b][j], j < width   (single block, fixed order)
+__global__ void __launch_bounds__(256) partial_reduce_kernel(const float* __restrict__ partial, int nb, int width,
+                                                             float* __restrict__ out) {
+  __shared__ float red[256];
+  for (int j = 0; j < width; ++j) {
+    float s = 0.f;
+    for (int k = threadIdx.x; k < nb; k += 256) s += partial[(size_t)k * width + j];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) out[j] = red[0];
+    __syncthreads();
+  }
+}
+
+template <int C>
+__global__ void __launch_bounds__(HT) head_bwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+                                                      const float* __restrict__ prob, const bf16* __restrict__ t,
+                                                      const float* __restrict__ sums, int P, float inv_total,
+                                                      float bce_w, float gscale, bf16* __restrict__ dx,
+                                                      float* __restrict__ partial) {
+  __shared__ float red[C + 1][HT / 64];
+  float wr[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) wr[c] = w[c];
+  const float I = sums[0], St = sums[1], Sp = sums[2];
+  const float a = -2.f / (2.f * I + 1.f);
+  const float bb = 1.f / (St + Sp + 1.f);
+  float gw[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) gw[c] = 0.f;
+  float gb = 0.f;
+  for (int p = blockIdx.x * HT + threadIdx.x; p < P; p += gridDim.x * HT) {
+    const float pr = prob[p];
+    const float tv = (float)t[p];
+    float dz = (a * tv + bb) * pr * (1.f - pr);
+    dz += bce_w * (pr - tv) * inv_total;
+    dz *= gscale;
+    gb += dz;
+#pragma unroll
+    for (int c8 = 0; c8 < C / 8; ++c8) {
+      const u32x4 xv = *(const u32x4*)(x + (size_t)p * C + c8 * 8);
+      float f[8], o[8];
+      unpack8(xv, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        gw[c8 * 8 + e] += dz * f[e];
+        o[e] = f[e] > 0.f ? dz * wr[c8 * 8 + e] : 0.f;
+      }
+      *(u32x4*)(dx + (size_t)p * C + c8 * 8) = pack8(o);
+    }
+  }
+  const int wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float s = wave_sum(gw[c]);
+    if ((threadIdx.x & 63) == 0) red[c][wv] = s;
+  }
+  gb = wave_sum(gb);
+  if ((threadIdx.x & 63) == 0) red[C][wv] = gb;
+  __syncthreads();
+  for (int j = threadIdx.x; j <= C; j += HT) {
+    float s = 0.f;
+    for (int k = 0; k < HT / 64; ++k) s += red[j][k];
+    partial[(size_t)blockIdx.x * (C + 1) + j] = s;
+  }
+}
+
+// grad_w[c] = sum_b partial[b][c], grad_b = sum_b partial[b][C]
+__global__ void __launch_bounds__(256) head_grad_reduce_kernel(const float* __restrict__ partial, int nb, int C,
+                                                               float* __restrict__ gw, float* __restrict__ gb) {
+  __shared__ float red[256];
+  for (int j = 0; j <= C; ++j) {
+    float s = 0.f;
+    for (int k = threadIdx.x; k < nb; k += 256) s += partial[(size_t)k * (C + 1) + j];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      if (j < C)
+        gw[j] = red[0];
+      else
+        gb[0] = red[0];
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+int head_blocks(int P) {
+  int nb = (P + HT * 4 - 1) / (HT * 4);
+  if (nb > 1024) nb = 1024;
+  if (nb < 1) nb = 1;
+  return nb;
+}
+
+const char* head_check(int C) {
+  if (C != 32 && C != 64 && C != 16) return "head: feature channels must be 16, 32 or 64";
+  return nullptr;
+}
+
+hipError_t head_fwd_launch(const void* x, const float* w, const float* b, const void* t, int P, int C, float* prob,
+                           float* partial, float* sums, hipStream_t s) {
+  const int nb = head_blocks(P);
+  switch (C) {
+    case 16:
+      hipLaunchKernelGGL(head_fwd_kernel<16>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, b, (const bf16*)t, P,
+                         prob, partial);
+      break;
+    case 32:
+      hipLaunchKernelGGL(head_fwd_kernel<32>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, b, (const bf16*)t, P,
+                         prob, partial);
+      break;
+    default:
+      hipLaunchKernelGGL(head_fwd_kernel<64>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, b, (const bf16*)t, P,
+                         prob, partial);
+  }
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3(1), dim3(256), 0, s, partial, nb, 4, sums);
+  return hipGetLastError();
+}
+
+hipError_t head_bwd_launch(const void* x, const float* w, const float* prob, const void* t, const float* sums, int P,
+                           int C, float inv_total, float bce_w, float gscale, void* dx, float* partial, float* gw,
+                           float* gb, hipStream_t s) {
+  const int nb = head_blocks(P);
+  switch (C) {
+    case 16:
+      hipLaunchKernelGGL(head_bwd_kernel<16>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, prob, (const bf16*)t,
+                         sums, P, inv_total, bce_w, gscale, (bf16*)dx, partial);
+      break;
+    case 32:
+      hipLaunchKernelGGL(head_bwd_kernel<32>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, prob, (const bf16*)t,
+                         sums, P, inv_total, bce_w, gscale, (bf16*)dx, partial);
+      break;
+    default:
+      hipLaunchKernelGGL(head_bwd_kernel<64>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, prob, (const bf16*)t,
+                         sums, P, inv_total, bce_w, gscale, (bf16*)dx, partial);
+  }
+  hipLaunchKernelGGL(head_grad_reduce_kernel, dim3(1), dim3(256), 0, s, partial, nb, C, gw, gb);
+  return hipGetLastError();
+}
+
+hipError_t partial_reduce_launch(const float* partial, int nb, int width, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3(1), dim3(256), 0, s, partial, nb, width, out);
+  return hipGetLastError();
+}
+
+}  // namespace unet

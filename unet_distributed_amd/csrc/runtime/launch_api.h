@@ -1,0 +1,45 @@
+// Host-side entry points of the HIP kernels (implemented in csrc/kernels/*.hip).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../kernels/conv_params.h"
+
+namespace unet {
+
+const char* conv_fwd_check(const ConvFwdParams& p);
+hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s);
+
+const char* wgrad_check(const WgradParams& p);
+WgradCfg wgrad_pick(const WgradParams& p);
+hipError_t wgrad_launch(const WgradParams& p, hipStream_t s);
+hipError_t wgrad_reduce_launch(const float* slab, int splits, int taps, int Mtot, int Mout, int Nc, int rg, int rkeep,
+                               float scale, float* out, hipStream_t s);
+hipError_t colsum_launch(const void* x, int rows, int C, int blocks, float* partial, hipStream_t s);
+
+hipError_t cast_input_launch(const float* x, int P, int Cin, int Cpad, void* y, hipStream_t s);
+hipError_t maxpool2_fwd_launch(const void* x, int N, int D, int H, int W, int C, int dims3, void* y, hipStream_t s);
+hipError_t maxpool2_bwd_launch(const void* x, const void* dy, const void* skip, int N, int D, int H, int W, int C,
+                               int dims3, void* dx, hipStream_t s);
+hipError_t upsample2_bwd_launch(const void* dup, const void* mask, int N, int D, int H, int W, int C, int dims3,
+                                void* dlow, hipStream_t s);
+
+int head_blocks(int P);
+const char* head_check(int C);
+hipError_t head_fwd_launch(const void* x, const float* w, const float* b, const void* t, int P, int C, float* prob,
+                           float* partial, float* sums, hipStream_t s);
+hipError_t head_bwd_launch(const void* x, const float* w, const float* prob, const void* t, const float* sums, int P,
+                           int C, float inv_total, float bce_w, float gscale, void* dx, float* partial, float* gw,
+                           float* gb, hipStream_t s);
+hipError_t partial_reduce_launch(const float* partial, int nb, int width, float* out, hipStream_t s);
+
+const char* adam_check(int nseg);
+hipError_t adam_pack_launch(float* w, const float* g, float* m, float* v, int n_total, const void* segs, int nseg,
+                            float lr_t, float b1, float b2, float eps, float gscale, int do_adam, void* arena,
+                            hipStream_t s);
+
+uint32_t crc32c_extend(uint32_t crc, const uint8_t* p, size_t n);
+void gather_rows(const uint8_t* src, const int64_t* idx, int64_t n, int64_t row_bytes, uint8_t* dst, int threads);
+
+}  // namespace unet

@@ -1,0 +1,121 @@
+"""Process-group lifecycle (one process per GPU, torch.distributed over RCCL).
+
+Replaces the reference's TF gRPC cluster (`test_dist.py:14-25` host tables,
+`test_dist.py:93-103` role-by-IP, `test_dist.py:130-131` ClusterSpec/Server):
+
+* rendezvous is env:// (``MASTER_ADDR``/``MASTER_PORT``/``RANK``/``WORLD_SIZE``
+  as set by ``torch.distributed.run`` or our ``launch.py``); the reference's
+  chief is rank 0;
+* backend ``nccl`` (= RCCL on ROCm, over xGMI inside an MI355X node) for GPU
+  tensors, ``gloo`` for the CPU plumbing configuration;
+* a finite collective timeout plus async error handling make a dead rank fail
+  the job fast instead of blocking forever like the reference's done-queue
+  (`test_dist.py:158-160`).
+"""
+
+import datetime
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+class DistContext:
+    def __init__(self):
+        self.rank = 0
+        self.world_size = 1
+        self.local_rank = 0
+        self.backend = None
+        self.initialized = False
+        self.device = torch.device("cpu")
+
+    @property
+    def is_chief(self) -> bool:
+        return self.rank == 0
+
+
+_CTX = DistContext()
+
+
+def context() -> DistContext:
+    return _CTX
+
+
+def init(device_pref: str = "auto", backend: str = "auto", timeout_s: float = 300.0) -> DistContext:
+    ctx = _CTX
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_cuda = (device_pref == "cuda") or (device_pref == "auto" and torch.cuda.is_available())
+    if use_cuda:
+        ndev = torch.cuda.device_count()
+        torch.cuda.set_device(local % max(ndev, 1))
+        ctx.device = torch.device("cuda", local % max(ndev, 1))
+    else:
+        ctx.device = torch.device("cpu")
+    ctx.rank, ctx.world_size, ctx.local_rank = rank, world, local
+    if world > 1 and not dist.is_initialized():
+        if backend == "auto":
+            backend = "nccl" if use_cuda else "gloo"
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = ctx.device
+        dist.init_process_group(**kw)
+        ctx.backend = backend
+        ctx.initialized = True
+    elif dist.is_initialized():
+        ctx.backend = dist.get_backend()
+        ctx.initialized = True
+    return ctx
+
+
+def barrier():
+    if _CTX.initialized:
+        if _CTX.backend == "nccl":
+            dist.barrier(device_ids=[_CTX.device.index])
+        else:
+            dist.barrier()
+
+
+def broadcast_(t: torch.Tensor, src: int = 0):
+    """In-place broadcast (rank 0 -> all); used for initial parameters and
+    restored checkpoints (replaces `prepare_or_wait_for_session`, test_dist.py:361)."""
+    if _CTX.initialized and _CTX.world_size > 1:
+        dist.broadcast(t, src)
+
+
+def allreduce_sum_(t: torch.Tensor):
+    if _CTX.initialized and _CTX.world_size > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
+def allreduce_avg_(t: torch.Tensor):
+    if _CTX.initialized and _CTX.world_size > 1:
+        if _CTX.backend == "nccl":
+            dist.all_reduce(t, op=dist.ReduceOp.AVG)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            t.div_(_CTX.world_size)
+    return t
+
+
+def allreduce_max_scalar(x: float, device=None) -> float:
+    if not (_CTX.initialized and _CTX.world_size > 1):
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device or _CTX.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def destroy():
+    """Orderly teardown (replaces the done-queue shutdown, test_dist.py:498-502)."""
+    if _CTX.initialized and dist.is_initialized():
+        try:
+            barrier()
+        finally:
+            dist.destroy_process_group()
+        _CTX.initialized = False

@@ -1,0 +1,165 @@
+"""Step backends: one forward + backward of the local micro-batch into the flat
+gradient buffer.
+
+* ``NativeBackend`` -- the MI355X path: the planned HIP executor
+  (``runtime.native_engine.NativeUNet``).  Mandatory on GPU for the configs
+  it supports; never silently replaced by ATen.
+* ``TorchBackend`` -- ATen reference (CPU plumbing config, fp32 runs, and the
+  numerical oracle for the kernels).
+
+Both expose ``fwd_bwd(x, y, seed, on_segment)``, ``sums()`` (device tensor
+{I, St, Sp, BCE_sum} of the last forward) and ``eval_sums(x, y)``.
+"""
+
+from typing import Callable, Optional
+
+import torch
+
+from ..models import reference
+from ..ops import losses
+from .params import FlatParams
+
+
+class TorchBackend:
+    name = "torch"
+
+    def __init__(self, spec, flat: FlatParams, cfg, device, per_rank_batch: int):
+        self.spec = spec
+        self.flat = flat
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[cfg.dtype]
+        if self.device.type == "cpu" and self.dtype == torch.float16:
+            self.dtype = torch.float32
+        self._sums = torch.zeros(4, device=self.device)
+        self.state = {}
+        if spec.norm == "batch":
+            for l in spec.param_layers():
+                if l.kind == "conv":
+                    self.state[l.name + "/norm/moving_mean"] = torch.zeros(l.cout, device=self.device)
+                    self.state[l.name + "/norm/moving_variance"] = torch.ones(l.cout, device=self.device)
+        self.bounds = [flat.numel]
+
+    def set_buckets(self, bounds):
+        self.bounds = list(bounds)
+
+    def _forward_logits(self, params, x, train, seed, dropout):
+        with torch.autocast(self.device.type, dtype=self.dtype, enabled=self.dtype != torch.float32):
+            return reference.forward(self.spec, params, x.to(self.device), train=train, dropout=dropout,
+                                     seed=seed, state=self.state, return_logits=True)
+
+    def fwd_bwd(self, x, y, seed: int, on_segment: Optional[Callable[[int], None]] = None,
+                grad_scale: float = 1.0):
+        names = [e[0] for e in self.flat.entries]
+        leaves = {n: self.flat.view(self.flat.master, n).detach().requires_grad_(True) for n in names}
+        logits = self._forward_logits(leaves, x, True, seed, True).float()
+        t = y.to(self.device).float()
+        loss, p = losses.total_loss(t, logits, self.cfg.loss, self.cfg.bce_weight)
+        grads = torch.autograd.grad(loss * grad_scale, [leaves[n] for n in names], allow_unused=True)
+        for n, g in zip(names, grads):
+            gv = self.flat.view(self.flat.grad, n)
+            if g is None:
+                gv.zero_()
+            else:
+                gv.copy_(g)
+        with torch.no_grad():
+            i, st, sp = losses.dice_sums(t, p)
+            bce = torch.nn.functional.binary_cross_entropy_with_logits(logits, t, reduction="sum")
+            self._sums = torch.stack([i, st, sp, bce]).detach()
+        if on_segment is not None:
+            for k in range(len(self.bounds)):
+                on_segment(k)
+
+    def sums(self) -> torch.Tensor:
+        return self._sums
+
+    @torch.no_grad()
+    def eval_sums(self, x, y) -> torch.Tensor:
+        logits = self._forward_logits(self.flat.params(), x, False, 0, self.cfg.eval_dropout).float()
+        t = y.to(self.device).float()
+        p = torch.sigmoid(logits)
+        i, st, sp = losses.dice_sums(t, p)
+        bce = torch.nn.functional.binary_cross_entropy_with_logits(logits, t, reduction="sum")
+        return torch.stack([i, st, sp, bce])
+
+    @torch.no_grad()
+    def predict(self, x) -> torch.Tensor:
+        logits = self._forward_logits(self.flat.params(), x, False, 0, self.cfg.eval_dropout).float()
+        return torch.sigmoid(logits)
+
+    def after_optimizer(self):
+        pass
+
+
+class NativeBackend:
+    name = "native"
+
+    def __init__(self, spec, flat: FlatParams, cfg, device, per_rank_batch: int, bounds=None):
+        from .native_engine import NativeUNet
+        self.cfg = cfg
+        self.flat = flat
+        self.engine = NativeUNet(spec, flat, per_rank_batch, cfg.img_size, device, loss=cfg.loss,
+                                 bce_weight=cfg.bce_weight, bucket_bounds=bounds,
+                                 eval_dropout=cfg.eval_dropout)
+        self.B = per_rank_batch
+
+    def set_buckets(self, bounds):
+        self.engine.set_buckets(bounds)
+
+    def fwd_bwd(self, x, y, seed: int, on_segment=None, grad_scale: float = 1.0):
+        e = self.engine
+        e.load_batch(x, y)
+        e.forward(seed)
+        e.backward(on_segment)
+
+    def sums(self) -> torch.Tensor:
+        return self.engine.sums
+
+    @torch.no_grad()
+    def eval_sums(self, x, y) -> torch.Tensor:
+        e = self.engine
+        if x.shape[0] != e.B:
+            raise ValueError("native eval batch must equal the per-rank batch")
+        e.load_batch(x, y)
+        e.evaluate_batch()
+        return e.sums.clone()
+
+    @torch.no_grad()
+    def predict(self, x) -> torch.Tensor:
+        e = self.engine
+        e.load_batch(x, torch.zeros(x.shape[:-1] + (1,), device=x.device))
+        e.evaluate_batch()
+        return e.probs().clone()
+
+    def adam_step(self, lr, b1p, b2p, grad_scale=1.0):
+        self.engine.adam_step(lr, b1p, b2p, grad_scale)
+
+
+def native_supported(spec, cfg, device) -> Optional[str]:
+    """None if the native executor supports this config, else the reason."""
+    if torch.device(device).type != "cuda":
+        return "not on a GPU"
+    if cfg.dtype != "bf16":
+        return "native kernels are bf16 (dtype=%s)" % cfg.dtype
+    if spec.norm != "none":
+        return "norm=%s not in the native executor yet" % spec.norm
+    if spec.n_cl_out != 1:
+        return "n_cl_out != 1"
+    if spec.base % 32:
+        return "base filters must be a multiple of 32"
+    cin = spec.in_channels
+    if not (cin <= 8 or cin % 32 == 0):
+        return "in_channels=%d" % cin
+    return None
+
+
+def make_backend(spec, flat, cfg, device, per_rank_batch, bounds=None):
+    want = cfg.backend
+    reason = native_supported(spec, cfg, device)
+    if want == "native" or (want == "auto" and reason is None):
+        if reason is not None:
+            raise RuntimeError("--backend native requested but unsupported: " + reason)
+        from .. import native
+        native.require()
+        return NativeBackend(spec, flat, cfg, device, per_rank_batch, bounds)
+    return TorchBackend(spec, flat, cfg, device, per_rank_batch)

@@ -1,0 +1,516 @@
+"""Native (HIP/gfx950) static-graph executor for the UNet training step.
+
+The executor plays the role of the reference's TF graph + session
+(`test_dist.py:183-298` graph construction, `test_dist.py:396-398` one
+``sess.run`` per step), designed for MI355X:
+
+* every activation / gradient buffer of the step is allocated ONCE for the
+  per-GPU micro-batch (channels-last bf16, sized for 288 GB HBM3E) and
+  reused every step — no allocator traffic in the hot loop;
+* every kernel launch of forward + backward is recorded once into a native
+  ``_C.Plan`` (shapes, pointers, epilogue flags resolved at plan time) and
+  replayed from C++;
+* cross-layer fusions that autograd cannot express are planned here:
+  - ReLU backward is folded into the CONSUMER's dgrad epilogue (every tensor
+    produced by a ReLU is masked by ``x > 0`` by whoever reads it), and the
+    dropout keep-mask needs no storage: ``z > 0`` of the dropout output is
+    exactly "kept and active", the 1/(1-rate) rescale rides on the same
+    epilogue (`model.py:60,66`);
+  - the decoder skip concat is never materialised: conv{j}a reads two
+    sources in its K loop, its dgrad writes two destinations and the skip
+    half is added to the max-pool backward in one kernel;
+  - nearest upsampling is folded into the next conv's address generation;
+  - bias gradients are column sums fused into the weight-gradient kernel;
+  - the Mask 1x1 conv + sigmoid + Dice/BCE partial sums is one kernel.
+* the backward plan is split into segments at allreduce-bucket boundaries so
+  the trainer can start RCCL allreduces of finished buckets on a side stream
+  while later layers' backward still runs.
+"""
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import native
+from ..models.spec import UNetSpec
+from .params import FlatParams
+
+BF16 = torch.bfloat16
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else int(t.data_ptr())
+
+
+class NativeUNet:
+    """Plans and runs forward + backward of one UNet micro-batch on the GPU."""
+
+    def __init__(self, spec: UNetSpec, flat: FlatParams, batch: int, img: int,
+                 device, loss: str = "dice", bce_weight: float = 1.0,
+                 bucket_bounds: Optional[Sequence[int]] = None, eval_dropout: bool = False,
+                 dry_run: bool = False):
+        self.C = native.require()
+        if spec.norm != "none":
+            raise NotImplementedError("native executor: norm=%s not implemented" % spec.norm)
+        if spec.n_cl_out != 1:
+            raise NotImplementedError("native executor: n_cl_out must be 1")
+        self.spec = spec
+        self.flat = flat
+        self.B = batch
+        self.img = img
+        self.dims = spec.dims
+        self.device = torch.device(device)
+        self.loss = loss
+        self.bce_weight = float(bce_weight) if loss == "dice_bce" else 0.0
+        cin = spec.in_channels
+        if cin <= 4:
+            self.cpad = 4
+        elif cin <= 8:
+            self.cpad = 8
+        elif cin % 32 == 0:
+            self.cpad = cin
+        else:
+            raise NotImplementedError("native executor: in_channels=%d" % cin)
+        self.bufs: Dict[str, torch.Tensor] = {}
+        self._grad_ptr_cache = {}
+        self._alloc_weights()
+        self._alloc_activations()
+        self.plan = self.C.Plan()
+        self.eval_plan = self.C.Plan()
+        self._build_forward(self.plan, dropout=True)
+        self.fwd_end = self.plan.size()
+        self.seg_ends: List[int] = []
+        self._layer_done_at: Dict[str, int] = {}
+        self._build_backward(self.plan)
+        self.bwd_end = self.plan.size()
+        self._build_forward(self.eval_plan, dropout=eval_dropout)
+        self.set_buckets(bucket_bounds)
+        if not dry_run:          # dry_run: plan construction only (CPU tests, no GPU launches)
+            self.repack()
+
+    # ------------------------------------------------------------------ shapes
+    def sdims(self, level: int) -> Tuple[int, int, int]:
+        s = self.img >> (level - 1)
+        return (s, s, s) if self.dims == 3 else (1, s, s)
+
+    def npix(self, level: int) -> int:
+        d, h, w = self.sdims(level)
+        return self.B * d * h * w
+
+    def _buf(self, name, level, ch, dtype=BF16):
+        d, h, w = self.sdims(level)
+        shape = (self.B, h, w, ch) if self.dims == 2 else (self.B, d, h, w, ch)
+        t = torch.empty(shape, dtype=dtype, device=self.device)
+        self.bufs[name] = t
+        return t
+
+    # ------------------------------------------------------------------ weights
+    def _alloc_weights(self):
+        """bf16 arena with the conv kernels in their compute layouts + Adam pack segments."""
+        spec, flat = self.spec, self.flat
+        T = 3 ** self.dims
+        Tt = 2 ** self.dims
+        off = 0
+        self.w_fwd_off: Dict[str, int] = {}
+        self.w_dg_off: Dict[str, int] = {}
+        layouts = {}
+        for l in spec.param_layers():
+            if l.kind == "conv":
+                first = l.name == spec.layers[0].name
+                ci_pad = self.cpad if first else l.cin
+                if first and self.cpad < 32:
+                    row = ((T * ci_pad + 31) // 32) * 32
+                else:
+                    row = T * ci_pad
+                self.w_fwd_off[l.name] = off
+                off += l.cout * row
+                off = (off + 63) // 64 * 64
+                if not first:
+                    self.w_dg_off[l.name] = off
+                    off += l.cin * T * l.cout
+                    off = (off + 63) // 64 * 64
+                layouts[l.name] = (1, T, l.cin, l.cout, ci_pad, row)
+            elif l.kind == "tconv":
+                self.w_fwd_off[l.name] = off
+                off += Tt * l.cout * l.cin
+                off = (off + 63) // 64 * 64
+                self.w_dg_off[l.name] = off
+                off += Tt * l.cout * l.cin
+                off = (off + 63) // 64 * 64
+                layouts[l.name] = (2, Tt, l.cin, l.cout, l.cin, 0)
+        self.arena = torch.zeros(max(off, 64), dtype=BF16, device=self.device)
+        segs = []
+        for name, shape, foff, n in flat.entries:
+            lname, var = name.split("/", 1)
+            if var == "kernel" and lname in layouts:
+                kind, t, ci, co, ci_pad, row = layouts[lname]
+                segs.append((foff, n, kind, t, ci, co, ci_pad, row,
+                             self.w_fwd_off[lname], self.w_dg_off.get(lname, -1)))
+            else:
+                segs.append((foff, n, 0, 0, 0, 0, 0, 0, -1, -1))
+        dt = np.dtype([("off", "<i4"), ("n", "<i4"), ("kind", "<i4"), ("T", "<i4"), ("Ci", "<i4"),
+                       ("Co", "<i4"), ("Ci_pad", "<i4"), ("rowstride", "<i4"),
+                       ("fwd_off", "<i8"), ("dg_off", "<i8")])
+        assert dt.itemsize == self.C.packseg_bytes()
+        arr = np.array(segs, dtype=dt)
+        self.nseg = len(segs)
+        self.segs = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
+
+    def wptr(self, lname, which="fwd"):
+        off = self.w_fwd_off[lname] if which == "fwd" else self.w_dg_off[lname]
+        return int(self.arena.data_ptr()) + 2 * off
+
+    def master_ptr(self, varname):
+        return int(self.flat.view(self.flat.master, varname).data_ptr())
+
+    def grad_ptr(self, varname):
+        return int(self.flat.view(self.flat.grad, varname).data_ptr())
+
+    def repack(self, stream=None):
+        """Refresh the bf16 compute copies from the fp32 master (no Adam)."""
+        f = self.flat
+        self.C.adam_pack(_ptr(f.master), _ptr(f.grad), _ptr(f.m), _ptr(f.v), f.numel,
+                         _ptr(self.segs), self.nseg, 0.0, 0.9, 0.999, 1e-8, 1.0, 0,
+                         _ptr(self.arena), native.stream_handle(stream))
+
+    def adam_step(self, lr, beta1_power, beta2_power, grad_scale=1.0, stream=None,
+                  beta1=0.9, beta2=0.999, eps=1e-8):
+        f = self.flat
+        lr_t = lr * math.sqrt(1.0 - beta2_power) / (1.0 - beta1_power)
+        self.C.adam_pack(_ptr(f.master), _ptr(f.grad), _ptr(f.m), _ptr(f.v), f.numel,
+                         _ptr(self.segs), self.nseg, lr_t, beta1, beta2, eps, grad_scale, 1,
+                         _ptr(self.arena), native.stream_handle(stream))
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc_activations(self):
+        spec = self.spec
+        self.x_f32 = torch.zeros((self.npix(1), spec.in_channels), dtype=torch.float32,
+                                 device=self.device)
+        self._buf("x", 1, self.cpad)
+        self.target = torch.zeros(self.npix(1), dtype=BF16, device=self.device)
+        # tensor graph: name -> (level, channels, produced_by_relu, dropout)
+        self.tinfo: Dict[str, Tuple[int, int, bool, bool]] = {"x": (1, self.cpad, False, False)}
+        self.inputs: Dict[str, Tuple] = {}
+        cur = "x"
+        pending_up = None
+        for l in spec.layers:
+            if l.kind == "conv":
+                if l.skip_from is not None:
+                    if pending_up is not None:
+                        src1, up1 = pending_up, 2
+                    else:
+                        src1, up1 = cur, 1
+                    self.inputs[l.name] = (src1, up1, l.skip_from)
+                    pending_up = None
+                else:
+                    self.inputs[l.name] = (cur, 1, None)
+                self._buf(l.name, l.level, l.cout)
+                self.tinfo[l.name] = (l.level, l.cout, True, l.dropout and spec.dropout > 0)
+                cur = l.name
+            elif l.kind == "pool":
+                self.inputs[l.name] = (cur, 1, None)
+                self._buf(l.name, l.level + 1, l.cout)
+                self.tinfo[l.name] = (l.level + 1, l.cout, True, False)
+                cur = l.name
+            elif l.kind == "tconv":
+                self.inputs[l.name] = (cur, 1, None)
+                self._buf(l.name, l.level, l.cout)
+                self.tinfo[l.name] = (l.level, l.cout, False, False)
+                cur = l.name
+            elif l.kind == "up":
+                pending_up = cur
+            elif l.kind == "mask":
+                self.inputs[l.name] = (cur, 1, None)
+                self.head_in = cur
+        P = self.npix(1)
+        self.prob = torch.zeros(P, dtype=torch.float32, device=self.device)
+        nb = self.C.head_blocks(P)
+        self.head_nb = nb
+        hc = self.tinfo[self.head_in][1]
+        self.head_partial = torch.zeros(nb * (hc + 1) + nb * 4, dtype=torch.float32, device=self.device)
+        self.sums = torch.zeros(4, dtype=torch.float32, device=self.device)
+        # gradient buffers: d:<tensor>, dskip:<tensor>, dfull:<tensor> (upsample fold)
+        for name, (lvl, ch, _, _) in list(self.tinfo.items()):
+            if name == "x":
+                continue
+            self.bufs["d:" + name] = torch.empty_like(self.bufs[name])
+        for l in spec.layers:
+            if l.kind == "conv" and l.skip_from is not None:
+                self.bufs["dskip:" + l.skip_from] = torch.empty_like(self.bufs[l.skip_from])
+                src1, up1, _ = self.inputs[l.name]
+                if up1 == 2:
+                    lvl, ch = self.tinfo[src1][0], self.tinfo[src1][1]
+                    d, h, w = self.sdims(l.level)
+                    shape = (self.B, h, w, ch) if self.dims == 2 else (self.B, d, h, w, ch)
+                    self.bufs["dfull:" + src1] = torch.empty(shape, dtype=BF16, device=self.device)
+        self.slab = None
+        self.bias_slab = None
+
+    # ------------------------------------------------------------------ plans
+    def _conv_common(self, level, K, stride, pad, out_level=None, in_level=None):
+        od, oh, ow = self.sdims(out_level or level)
+        idd, ih, iw = self.sdims(in_level or level)
+        kd = K if self.dims == 3 else 1
+        return dict(N=self.B, OD=od, OH=oh, OW=ow, ID=idd, IH=ih, IW=iw, KD=kd, KH=K, KW=K,
+                    stride=stride, pad=pad)
+
+    def _salt(self, lname):
+        return [l.name for l in self.spec.layers].index(lname)
+
+    def _build_forward(self, plan, dropout):
+        spec = self.spec
+        b = self.bufs
+        P1 = self.npix(1)
+        plan.add_generic("cast_input", [_ptr(self.x_f32), _ptr(b["x"])],
+                         [P1, spec.in_channels, self.cpad], [], "cast_input")
+        for l in spec.layers:
+            if l.kind == "conv":
+                src1, up1, skip = self.inputs[l.name]
+                c1 = self.tinfo[src1][1]
+                d = self._conv_common(l.level, 3, 1, 1)
+                d.update(name="fwd:" + l.name, C1=c1, C2=self.tinfo[skip][1] if skip else 0, up1=up1,
+                         src1=_ptr(b[src1]), src2=_ptr(b[skip]) if skip else None,
+                         wgt=self.wptr(l.name), bias=self.master_ptr(l.name + "/bias"),
+                         Cout=l.cout, relu=1, dst1=_ptr(b[l.name]),
+                         drop_rate=spec.dropout if (l.dropout and dropout) else 0.0,
+                         salt=self._salt(l.name))
+                plan.add_conv_fwd(d)
+            elif l.kind == "pool":
+                src = self.inputs[l.name][0]
+                dd, hh, ww = self.sdims(l.level)
+                plan.add_generic("pool_fwd", [_ptr(b[src]), _ptr(b[l.name])],
+                                 [self.B, dd, hh, ww, l.cout, int(self.dims == 3)], [], "fwd:" + l.name)
+            elif l.kind == "tconv":
+                src = self.inputs[l.name][0]
+                d = self._conv_common(l.level + 1, 1, 1, 0)
+                d.update(name="fwd:" + l.name, C1=l.cin, src1=_ptr(b[src]), wgt=self.wptr(l.name),
+                         bias=self.master_ptr(l.name + "/bias"), Cout=(2 ** self.dims) * l.cout,
+                         relu=0, shuffle=self.dims, dst1=_ptr(b[l.name]))
+                plan.add_conv_fwd(d)
+            elif l.kind == "mask":
+                hc = self.tinfo[self.head_in][1]
+                nb = self.head_nb
+                part = self.head_partial
+                plan.add_generic("head_fwd", [_ptr(b[self.head_in]), self.master_ptr("Mask/kernel"),
+                                              self.master_ptr("Mask/bias"), _ptr(self.target),
+                                              _ptr(self.prob), _ptr(part), _ptr(self.sums)],
+                                 [P1, hc], [], "fwd:Mask")
+
+    def _wgrad_splits(self, M1, M2, Nc, KT, Q):
+        BM, BN, NTAP, smallc = self.C.wgrad_pick(M1, M2, Nc, KT)
+        Mtot = ((KT * M1 + BM - 1) // BM) * BM if smallc else M1 + M2
+        tg = 1 if smallc else KT // NTAP
+        tiles = (Mtot // BM) * (Nc // BN) * tg
+        splits = max(1, min(-(-2048 // tiles), max(1, Q // (32 * 16))))
+        taps = 1 if smallc else KT
+        return splits, Mtot, taps, tg, smallc
+
+    def _build_backward(self, plan):
+        """Backward ops are first collected as closures (slab sizes are only known
+        after every wgrad is sized), then emitted in order."""
+        ops = []  # list of callables(plan) in emission order, plus layer-complete markers
+        spec = self.spec
+        b = self.bufs
+        P1 = self.npix(1)
+        layers = spec.layers
+        KT3 = 3 ** self.dims
+        KT2 = 2 ** self.dims
+        inv_total = 1.0 / float(P1)
+
+        def emit_generic(kind, ptrs, ints, floats, name):
+            ops.append(lambda pl: pl.add_generic(kind, ptrs(), ints, floats, name))
+
+        def emit_conv(d):
+            ops.append(lambda pl: pl.add_conv_fwd(d()))
+
+        wg_specs = []
+
+        def emit_wgrad(args):
+            wg_specs.append(args)
+            idx = len(wg_specs) - 1
+            ops.append(("wgrad", idx))
+
+        def done(lname):
+            ops.append(("done", lname))
+
+        for li in range(len(layers) - 1, -1, -1):
+            l = layers[li]
+            if l.kind == "mask":
+                hc = self.tinfo[self.head_in][1]
+                nb = self.head_nb
+                emit_generic("head_bwd",
+                             lambda hc=hc: [_ptr(b[self.head_in]), self.master_ptr("Mask/kernel"), _ptr(self.prob),
+                                            _ptr(self.target), _ptr(self.sums), _ptr(b["d:" + self.head_in]),
+                                            _ptr(self.head_partial), self.grad_ptr("Mask/kernel"),
+                                            self.grad_ptr("Mask/bias")],
+                             [P1, hc], [inv_total, self.bce_weight, 1.0], "bwd:Mask")
+                done("Mask")
+            elif l.kind == "conv":
+                src1, up1, skip = self.inputs[l.name]
+                first = src1 == "x"
+                c1 = self.tinfo[src1][1]
+                c2 = self.tinfo[skip][1] if skip else 0
+                dy = b["d:" + l.name]
+                Q = self.npix(l.level)
+                # --- weight + bias gradient (fused column sums)
+                kd = dict(N=self.B, QD=self.sdims(l.level)[0], QH=self.sdims(l.level)[1],
+                          QW=self.sdims(l.level)[2], AD=self.sdims(l.level)[0], AH=self.sdims(l.level)[1],
+                          AW=self.sdims(l.level)[2], KD=3 if self.dims == 3 else 1, KH=3, KW=3, stride=1,
+                          pad=1, upA=up1, a1=_ptr(b[src1]), a2=_ptr(b[skip]) if skip else None,
+                          b=_ptr(dy))
+                emit_wgrad(dict(lname=l.name, kd=kd, M1=c1, M2=c2, Nc=l.cout, KT=KT3, Q=Q,
+                                kernel=l.name + "/kernel", bias=l.name + "/bias", bias_mode=1,
+                                bias_width=l.cout,
+                                real_rows=(self.cpad, spec.in_channels) if first else None))
+                # --- data gradient
+                if not first:
+                    def mk(l=l, src1=src1, up1=up1, skip=skip, c1=c1, c2=c2, dy=dy):
+                        d = self._conv_common(l.level, 3, 1, 1)
+                        d.update(name="dgrad:" + l.name, C1=l.cout, src1=_ptr(dy),
+                                 wgt=self.wptr(l.name, "dg"), Cout=l.cin, relu=0)
+                        if skip is None:
+                            lvl, ch, relu_src, drop = self.tinfo[src1]
+                            d.update(dst1=_ptr(b["d:" + src1]), D1=l.cin,
+                                     mask1=_ptr(b[src1]) if relu_src else None,
+                                     mask_scale1=(1.0 / (1.0 - spec.dropout)) if drop else 1.0)
+                        else:
+                            if up1 == 2:
+                                dst1 = b["dfull:" + src1]          # full-res grad of the folded upsample
+                            else:
+                                dst1 = b["d:" + src1]              # tconv output: linear, no mask
+                            d.update(dst1=_ptr(dst1), D1=c1, dst2=_ptr(b["dskip:" + skip]),
+                                     mask2=_ptr(b[skip]))
+                        return d
+                    emit_conv(mk)
+                    if up1 == 2:
+                        lvl = self.tinfo[src1][0]
+                        dd, hh, ww = self.sdims(lvl)
+                        emit_generic("ups_bwd",
+                                     lambda src1=src1: [_ptr(b["dfull:" + src1]), _ptr(b[src1]),
+                                                        _ptr(b["d:" + src1])],
+                                     [self.B, dd, hh, ww, c1, int(self.dims == 3)], [], "bwd:up:" + src1)
+                done(l.name)
+            elif l.kind == "pool":
+                src = self.inputs[l.name][0]
+                dd, hh, ww = self.sdims(l.level)
+                emit_generic("pool_bwd",
+                             lambda src=src, l=l: [_ptr(b[src]), _ptr(b["d:" + l.name]),
+                                                   _ptr(b["dskip:" + src]) if ("dskip:" + src) in b else 0,
+                                                   _ptr(b["d:" + src])],
+                             [self.B, dd, hh, ww, l.cout, int(self.dims == 3)], [], "bwd:" + l.name)
+            elif l.kind == "tconv":
+                src = self.inputs[l.name][0]
+                du = b["d:" + l.name]
+                lo = self.sdims(l.level + 1)
+                hi = self.sdims(l.level)
+                kd = dict(N=self.B, QD=lo[0], QH=lo[1], QW=lo[2], AD=hi[0], AH=hi[1], AW=hi[2],
+                          KD=2 if self.dims == 3 else 1, KH=2, KW=2, stride=2, pad=0, upA=1,
+                          a1=_ptr(du), b=_ptr(b[src]))
+                emit_wgrad(dict(lname=l.name, kd=kd, M1=l.cout, M2=0, Nc=l.cin, KT=KT2,
+                                Q=self.npix(l.level + 1), kernel=l.name + "/kernel",
+                                bias=l.name + "/bias", bias_mode=2, bias_width=l.cout, real_rows=None))
+
+                def mk(l=l, src=src, du=du):
+                    d = self._conv_common(l.level + 1, 2, 2, 0, out_level=l.level + 1, in_level=l.level)
+                    d.update(name="dgrad:" + l.name, C1=l.cout, src1=_ptr(du),
+                             wgt=self.wptr(l.name, "dg"), Cout=l.cin, relu=0,
+                             dst1=_ptr(b["d:" + src]), mask1=_ptr(b[src]))
+                    return d
+                emit_conv(mk)
+                done(l.name)
+            elif l.kind == "up":
+                pass
+
+        # size the wgrad workspaces
+        sized = []
+        smax, bmax = 1, 1
+        for w in wg_specs:
+            splits, Mtot, taps, tg, smallc = self._wgrad_splits(w["M1"], w["M2"], w["Nc"], w["KT"], w["Q"])
+            sized.append((splits, Mtot, taps, tg, smallc))
+            smax = max(smax, splits * taps * Mtot * w["Nc"])
+            bw = w["bias_width"] if w["bias_mode"] == 1 else Mtot
+            bmax = max(bmax, splits * tg * bw)
+        self.slab = torch.empty(smax, dtype=torch.float32, device=self.device)
+        self.bias_slab = torch.empty(bmax, dtype=torch.float32, device=self.device)
+
+        for op in ops:
+            if callable(op):
+                op(plan)
+            elif op[0] == "done":
+                self._layer_done_at[op[1]] = plan.size()
+            else:
+                w = wg_specs[op[1]]
+                splits, Mtot, taps, tg, smallc = sized[op[1]]
+                d = dict(w["kd"])
+                d.update(name="wgrad:" + w["lname"], M1=w["M1"], M2=w["M2"], Nc=w["Nc"], splits=splits,
+                         slab=_ptr(self.slab), bias_mode=w["bias_mode"], bias_slab=_ptr(self.bias_slab))
+                plan.add_wgrad(d)
+                rr = w["real_rows"]
+                KT = w["KT"]
+                if smallc:
+                    cpad, creal = rr
+                    plan.add_generic("wgrad_reduce", [_ptr(self.slab), self.grad_ptr(w["kernel"])],
+                                     [splits, 1, Mtot, KT * creal, w["Nc"], cpad, creal], [1.0],
+                                     "wred:" + w["lname"])
+                else:
+                    plan.add_generic("wgrad_reduce", [_ptr(self.slab), self.grad_ptr(w["kernel"])],
+                                     [splits, taps, Mtot, Mtot, w["Nc"]], [1.0], "wred:" + w["lname"])
+                bw = w["bias_width"]
+                if w["bias_mode"] == 1:
+                    plan.add_generic("wgrad_reduce", [_ptr(self.bias_slab), self.grad_ptr(w["bias"])],
+                                     [splits, 1, 1, 1, bw], [1.0], "bred:" + w["lname"])
+                else:
+                    # [splits*tg][Mtot] rows -> bias (Mtot == cout for tconv)
+                    plan.add_generic("wgrad_reduce", [_ptr(self.bias_slab), self.grad_ptr(w["bias"])],
+                                     [splits * tg, 1, 1, 1, bw], [1.0], "bred:" + w["lname"])
+
+    # ------------------------------------------------------------------ buckets
+    def set_buckets(self, bounds: Optional[Sequence[int]]):
+        """bounds: flat-buffer element offsets ending each allreduce bucket.  A
+        segment ends at the first plan op after which every layer whose
+        variables lie below the bound has finished its gradient."""
+        self.seg_ends = []
+        self.seg_bounds = []
+        if not bounds:
+            self.seg_ends = [self.bwd_end]
+            self.seg_bounds = [self.flat.numel]
+            return
+        for bound in bounds:
+            last = self.fwd_end
+            for name, shape, off, n in self.flat.entries:
+                if off < bound:
+                    last = max(last, self._layer_done_at[name.split("/")[0]])
+            self.seg_ends.append(last)
+            self.seg_bounds.append(bound)
+        self.seg_ends[-1] = self.bwd_end
+
+    # ------------------------------------------------------------------ running
+    def load_batch(self, x: torch.Tensor, y: torch.Tensor, stream=None):
+        """x: [B, (D,) H, W, Cin] float, y: [B, (D,) H, W, 1] float/bool."""
+        self.x_f32.view(-1).copy_(x.reshape(-1), non_blocking=True)
+        self.target.copy_(y.reshape(-1), non_blocking=True)
+
+    def forward(self, seed: int, stream=None):
+        self.plan.set_seed(seed & 0xFFFFFFFF)
+        self.plan.run(0, self.fwd_end, native.stream_handle(stream))
+
+    def backward(self, on_segment=None, stream=None):
+        s = native.stream_handle(stream)
+        begin = self.fwd_end
+        for i, end in enumerate(self.seg_ends):
+            self.plan.run(begin, end, s)
+            begin = end
+            if on_segment is not None:
+                on_segment(i)
+
+    def evaluate_batch(self, stream=None):
+        """Inference forward (eval plan) of the loaded batch; sums -> self.sums."""
+        self.eval_plan.set_seed(0)
+        self.eval_plan.run(0, self.eval_plan.size(), native.stream_handle(stream))
+
+    def probs(self) -> torch.Tensor:
+        d, h, w = self.sdims(1)
+        shape = (self.B, h, w, 1) if self.dims == 2 else (self.B, d, h, w, 1)
+        return self.prob.view(shape)

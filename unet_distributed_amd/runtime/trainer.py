@@ -1,0 +1,245 @@
+"""Training runtime: the reference's worker ``main()`` re-designed for MI355X.
+
+Reference flow (`test_dist.py:121-508`): build the graph,
+SyncReplicasOptimizer over a parameter server, Supervisor-managed session with
+auto-restore, a hot loop that shards each global batch over the workers, chief
+duties (summaries, per-epoch evaluation, ``last_good_model`` save, TensorBoard,
+SavedModel export), and a done-queue shutdown.
+
+Here: one process per GPU; full replicas; bucketed RCCL allreduce overlapped
+with the native backward; fused TF-Adam on every rank; rank 0 does logging,
+evaluation reporting, checkpoints and export; checkpoints auto-resume; a dead
+rank fails the job through collective timeouts.  Fixes of reference quirks are
+listed in SURVEY.md Appendix Q and noted inline.
+"""
+
+import json
+import math
+import os
+import sys
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import settings
+from ..data import datasets
+from ..models import reference
+from ..models.spec import spec_from_config
+from ..ops import losses
+from ..parallel import dist as D
+from ..parallel.grad_sync import GradSync, plan_buckets
+from ..utils import checkpoint as ckpt
+from ..utils.metrics import MetricLogger
+from .backends import make_backend
+from .optim import TFAdam, learning_rate
+from .params import FlatParams
+
+
+class FaultInjected(RuntimeError):
+    pass
+
+
+def metrics_from_sums(s: torch.Tensor, npix: int, cfg) -> dict:
+    i, st, sp, bce = [float(v) for v in s.tolist()]
+    m = losses.metrics_from_sums(i, st, sp)
+    if cfg.loss == "dice_bce":
+        m["loss"] += cfg.bce_weight * bce / max(npix, 1)
+    return m
+
+
+class Trainer:
+    def __init__(self, cfg):
+        self.cfg = cfg
+        self.ctx = D.init(cfg.device, cfg.dist_backend, cfg.dist_timeout_s)
+        self.device = self.ctx.device
+        self.rank, self.world = self.ctx.rank, self.ctx.world_size
+        self.is_chief = self.ctx.is_chief
+        if cfg.batch_size % self.world:
+            raise SystemExit("--batch_size %d must be divisible by the world size %d"
+                             % (cfg.batch_size, self.world))
+        self.per_rank = cfg.batch_size // self.world
+        torch.manual_seed(cfg.seed)
+        self.spec = spec_from_config(cfg)
+        self.flat = FlatParams(self.spec, device=self.device)
+        self.flat.load_dict(reference.init_params(self.spec, seed=cfg.seed))
+        self.bounds = plan_buckets(self.flat, cfg.bucket_mb)
+        self.backend = make_backend(self.spec, self.flat, cfg, self.device, self.per_rank, self.bounds)
+        extra = getattr(self.backend, "state", {}) or {}
+        self.ckpt = ckpt.CheckpointManager(cfg, self.flat, self.is_chief, extra_state=extra)
+        self.restored = False
+        if cfg.resume and self.is_chief and not cfg.no_checkpoint:
+            self.restored = self.ckpt.restore_latest()
+        self._broadcast_state()
+        self.sync = GradSync(self.flat, self.bounds, self.ctx, overlap=cfg.overlap_comm)
+        native_opt = self.backend if hasattr(self.backend, "adam_step") else None
+        self.opt = TFAdam(self.flat, cfg, native=_NativeOpt(native_opt) if native_opt else None)
+        self.log = MetricLogger(cfg, self.is_chief, self.ckpt.logdir)
+        self._load_data()
+
+    # ------------------------------------------------------------------ setup
+    def _broadcast_state(self):
+        f = self.flat
+        for t in (f.master, f.m, f.v):
+            D.broadcast_(t, 0)
+        meta = torch.tensor([f.global_step, f.beta1_power, f.beta2_power, int(self.restored)],
+                            dtype=torch.float64, device=self.device)
+        D.broadcast_(meta, 0)
+        f.global_step = int(meta[0].item())
+        f.beta1_power = float(meta[1].item())
+        f.beta2_power = float(meta[2].item())
+        self.restored = bool(meta[3].item())
+        if hasattr(self.backend, "engine"):
+            self.backend.engine.repack()
+
+    def _load_data(self):
+        cfg = self.cfg
+        if cfg.synthetic:
+            n_tr = max(cfg.synthetic_train, cfg.batch_size)
+            self.x_train, self.y_train = datasets.synthetic_brats(n_tr, cfg.img_size, cfg.in_channels,
+                                                                  cfg.dims, seed=cfg.seed)
+            self.x_test, self.y_test = datasets.synthetic_brats(cfg.synthetic_test, cfg.img_size,
+                                                                cfg.in_channels, cfg.dims, seed=cfg.seed + 1)
+        else:
+            xi, yi = datasets.load_data(cfg.data_path, "_train")
+            self.x_train, self.y_train = datasets.update_channels(xi, yi, cfg.in_channels, cfg.out_channels, cfg.mode)
+            xi, yi = datasets.load_data(cfg.data_path, "_test")
+            self.x_test, self.y_test = datasets.update_channels(xi, yi, cfg.in_channels, cfg.out_channels, cfg.mode)
+        if self.is_chief:
+            print("Training images shape: {}".format(self.x_train.shape))
+            print("Training masks shape:  {}".format(self.y_train.shape))
+            print("Testing images shape:  {}".format(self.x_test.shape))
+            print("Testing masks shape:   {}".format(self.y_test.shape))
+        self.sampler = datasets.EpochSampler(len(self.x_train), cfg.batch_size, self.rank, self.world, cfg.seed)
+        self.num_batches = self.sampler.num_batches
+        pin = self.device.type == "cuda"
+        self._stage_x = torch.empty((self.per_rank,) + self.x_train.shape[1:], dtype=torch.float32,
+                                    pin_memory=pin)
+        self._stage_y = torch.empty((self.per_rank,) + self.y_train.shape[1:], dtype=torch.float32,
+                                    pin_memory=pin)
+
+    def _batch(self, idx: np.ndarray):
+        idx = np.sort(idx)
+        self._stage_x.numpy()[...] = self.x_train[idx]
+        self._stage_y.numpy()[...] = self.y_train[idx]
+        return (self._stage_x.to(self.device, non_blocking=True),
+                self._stage_y.to(self.device, non_blocking=True))
+
+    # ------------------------------------------------------------------ eval
+    def evaluate(self) -> dict:
+        """Per-epoch test metrics: every full per-rank batch, sharded over ranks,
+        batch metrics averaged over ALL batches (fixes the under-count of Q7)."""
+        n = len(self.x_test)
+        B = self.per_rank
+        nbatches = n // B
+        acc = torch.zeros(5, dtype=torch.float64, device=self.device)
+        for b in range(self.rank, nbatches, self.world):
+            x = torch.from_numpy(np.ascontiguousarray(self.x_test[b * B:(b + 1) * B])).to(self.device)
+            y = torch.from_numpy(np.ascontiguousarray(self.y_test[b * B:(b + 1) * B])).to(self.device)
+            m = metrics_from_sums(self.backend.eval_sums(x, y), y.numel(), self.cfg)
+            acc += torch.tensor([m["loss"], m["dice"], m["sensitivity"], m["specificity"], 1.0],
+                                dtype=torch.float64, device=self.device)
+        D.allreduce_sum_(acc)
+        cnt = max(acc[4].item(), 1.0)
+        return {"loss": acc[0].item() / cnt, "dice": acc[1].item() / cnt,
+                "sensitivity": acc[2].item() / cnt, "specificity": acc[3].item() / cnt,
+                "batches": int(acc[4].item())}
+
+    # ------------------------------------------------------------------ step
+    def train_step(self, x, y, seed: int) -> None:
+        self.backend.fwd_bwd(x, y, seed, on_segment=self.sync.on_segment)
+        self.sync.finish()
+        self.opt.step()
+
+    def check_sync(self):
+        """Cross-rank parameter checksum (detects DP divergence)."""
+        if self.world == 1:
+            return
+        s = self.flat.master.double().sum().reshape(1)
+        mx, mn = s.clone(), s.clone()
+        import torch.distributed as dist
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+        if (mx - mn).abs().item() > 1e-6 * max(1.0, abs(mx.item())):
+            raise RuntimeError("replica divergence detected at step %d: %g vs %g"
+                               % (self.flat.global_step, mn.item(), mx.item()))
+
+    def run(self) -> dict:
+        cfg = self.cfg
+        total = cfg.steps if cfg.steps > 0 else self.num_batches * cfg.epochs
+        step = self.flat.global_step
+        if self.is_chief:
+            print("I am chief worker with task #0 (world size %d, backend %s, device %s)"
+                  % (self.world, self.backend.name, self.device))
+            if self.restored:
+                print("Restored checkpoint at global_step %d" % step)
+        epoch = step // self.num_batches
+        epoch_idx = self.sampler.epoch_indices(epoch)
+        t_last = time.time()
+        imgs_since = 0
+        last_metrics = {}
+        while step < total:
+            batch_idx = step % self.num_batches
+            if batch_idx == 0 and step // self.num_batches != epoch:
+                epoch = step // self.num_batches
+                epoch_idx = self.sampler.epoch_indices(epoch)     # reshuffle (test_dist.py:449-452)
+            x, y = self._batch(epoch_idx[batch_idx])
+            if cfg.fault_inject_step >= 0 and step == cfg.fault_inject_step and \
+                    (cfg.fault_inject_rank < 0 or cfg.fault_inject_rank == self.rank):
+                raise FaultInjected("fault injected at step %d on rank %d" % (step, self.rank))
+            self.train_step(x, y, seed=cfg.seed * 1000003 + step)
+            step = self.flat.global_step
+            imgs_since += cfg.batch_size
+            if cfg.check_sync_every and step % cfg.check_sync_every == 0:
+                self.check_sync()
+            if step % cfg.log_every == 0 or step == total:
+                if self.device.type == "cuda":
+                    torch.cuda.synchronize()
+                dt = time.time() - t_last
+                m = metrics_from_sums(self.backend.sums(), y.numel(), cfg)
+                m["images_per_sec"] = imgs_since / max(dt, 1e-9)
+                m["lr"] = learning_rate(cfg, step)
+                m["percent_complete"] = 100.0 * step / total
+                self.log.train(step, m, total)
+                last_metrics = m
+                t_last, imgs_since = time.time(), 0
+            if step % self.num_batches == 0:
+                # end of an epoch: evaluate, report, keep last_good_model (test_dist.py:407-446)
+                tm = self.evaluate()
+                self.log.test(step, tm, step // self.num_batches, cfg.epochs)
+                if self.is_chief:
+                    self.ckpt.save_last_good()
+            self.ckpt.maybe_save()
+        final = self.evaluate()
+        self.log.test(step, final, step // max(self.num_batches, 1), cfg.epochs, final=True)
+        if self.is_chief:
+            self.ckpt.save(); self.ckpt.save_last_good()
+            if cfg.export:
+                d = ckpt.export_model(cfg, self.spec, self.flat)
+                print("Saved final model to directory: {}".format(d))
+        self.log.close()
+        return {"train": last_metrics, "test": final, "global_step": step}
+
+
+class _NativeOpt:
+    def __init__(self, backend):
+        self.backend = backend
+
+    def adam_step(self, lr, b1p, b2p, grad_scale):
+        self.backend.adam_step(lr, b1p, b2p, grad_scale)
+
+
+def main(argv=None) -> int:
+    from ..config import parse_args
+    cfg = parse_args(argv)
+    for k in ("http_proxy", "https_proxy"):
+        os.environ.pop(k, None)                 # Q5: the reference del's these unconditionally
+    tr = Trainer(cfg)
+    try:
+        tr.run()
+    finally:
+        D.destroy()
+    if tr.is_chief:
+        print("\n\nFinished work on this node.")
+    return 0
