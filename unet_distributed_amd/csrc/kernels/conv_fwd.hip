@@ -81,7 +81,8 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
   const int nk = SMALLC ? (Kpad >> 5) : KT * cblocks;
   const size_t Ktot = SMALLC ? (size_t)Kpad : (size_t)KT * Cin;
   const int ccol = tid & 3;
-  const int ID1 = p.ID / p.up1, IH1 = p.IH / p.up1, IW1 = p.IW / p.up1;
+  const int upd = p.ID > 1 ? p.up1 : 1;  // 2D: depth is never upsampled
+  const int ID1 = p.ID / upd, IH1 = p.IH / p.up1, IW1 = p.IW / p.up1;
 
   // ---- per-thread A rows (fixed for the whole K loop)
   int a_n[A_PER_T], a_d[A_PER_T], a_h[A_PER_T], a_w[A_PER_T];
@@ -93,7 +94,7 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
     a_ok[i] = (r < BM) && (q < M);
     PixCoord c = decompose(a_ok[i] ? q : 0, p.OD, p.OH, p.OW);
     a_n[i] = c.n;
-    a_d[i] = c.d * p.stride - p.pad;
+    a_d[i] = c.d * p.stride - (p.KD > 1 ? p.pad : 0);   // 2D: depth is not padded
     a_h[i] = c.h * p.stride - p.pad;
     a_w[i] = c.w * p.stride - p.pad;
   }
@@ -157,7 +158,7 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
       if (ok) {
         const bf16* src;
         if (from1) {
-          const size_t pix = (((size_t)a_n[i] * ID1 + id / p.up1) * IH1 + ih / p.up1) * IW1 + iw / p.up1;
+          const size_t pix = (((size_t)a_n[i] * ID1 + id / upd) * IH1 + ih / p.up1) * IW1 + iw / p.up1;
           src = (const bf16*)p.src1 + pix * p.C1 + c0 + ccol * 8;
         } else {
           const size_t pix = (((size_t)a_n[i] * p.ID + id) * p.IH + ih) * p.IW + iw;

@@ -56,13 +56,11 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, int lane, int cbase) 
       LDS_PTR(short4v, img + tr_off<W>(8 * g + q, cbase + 4 * pp)));
   const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       LDS_PTR(short4v, img + tr_off<W>(8 * g + 4 + q, cbase + 4 * pp)));
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    r[j] = __builtin_bit_cast(bf16, lo[j]);
-    r[j + 4] = __builtin_bit_cast(bf16, hi[j]);
-  }
-  return r;
+  // whole-vector bit casts: per-element short->bf16 casts miscompile (only the
+  // first dword of each 64-bit transposed read survived in ROCm 7.2 hipcc)
+  const u32x2 a = __builtin_bit_cast(u32x2, lo), b = __builtin_bit_cast(u32x2, hi);
+  const u32x4 v = {a[0], a[1], b[0], b[1]};
+  return __builtin_bit_cast(bf16x8, v);
 }
 
 template <int BM, int BN, int NTAP, int WAVES_M, int WAVES_N, bool SMALLC, bool BIAS>
@@ -96,8 +94,10 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
   const int kend = min(Q, kbeg + per);
   const int nks = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   const int upA = p.upA;
-  const int AD1 = p.AD / upA, AH1 = p.AH / upA, AW1 = p.AW / upA;
+  const int upAd = p.AD > 1 ? upA : 1;  // 2D: depth is never upsampled
+  const int AD1 = p.AD / upAd, AH1 = p.AH / upA, AW1 = p.AW / upA;
   const int Cin_s = p.M1;  // SMALLC: channels of the first-layer input
+  const int padd = p.KD > 1 ? p.pad : 0;  // 2D: depth is not padded
 
   const int krow = tid >> 3, sub = tid & 7;
   // bias partial sums: mode 1 once per (n-tile, split) [tm == 0, tg == 0]; mode 2 once per (m-tile, tg, split) [tn == 0]
@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
             const int tap = mm / Cin_s + e;
             if (tap >= KT) continue;
             const int kw = tap % p.KW, kh = (tap / p.KW) % p.KH, kd = tap / (p.KW * p.KH);
-            const int ad = qd * p.stride + kd - p.pad, ah = qh * p.stride + kh - p.pad,
+            const int ad = qd * p.stride + kd - padd, ah = qh * p.stride + kh - p.pad,
                       aw = qw * p.stride + kw - p.pad;
             if ((unsigned)ad >= (unsigned)p.AD || (unsigned)ah >= (unsigned)p.AH || (unsigned)aw >= (unsigned)p.AW)
               continue;
@@ -149,13 +149,13 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
         } else {
           const int tap = tg * NTAP + tl;
           const int kw = tap % p.KW, kh = (tap / p.KW) % p.KH, kd = tap / (p.KW * p.KH);
-          const int ad = qd * p.stride + kd - p.pad, ah = qh * p.stride + kh - p.pad,
+          const int ad = qd * p.stride + kd - padd, ah = qh * p.stride + kh - p.pad,
                     aw = qw * p.stride + kw - p.pad;
           if ((unsigned)ad < (unsigned)p.AD && (unsigned)ah < (unsigned)p.AH && (unsigned)aw < (unsigned)p.AW) {
             const int m = m0 + col * 8;
             const bf16* src;
             if (m < p.M1) {
-              const size_t pix = (((size_t)qn * AD1 + ad / upA) * AH1 + ah / upA) * AW1 + aw / upA;
+              const size_t pix = (((size_t)qn * AD1 + ad / upAd) * AH1 + ah / upA) * AW1 + aw / upA;
               src = (const bf16*)p.a1 + pix * p.M1 + m;
             } else {
               const size_t pix = (((size_t)qn * p.AD + ad) * p.AH + ah) * p.AW + aw;
