@@ -39,14 +39,22 @@ def nhwc(x):
     return x.permute(0, 2, 3, 1)
 
 
-def pack_fwd(w_hwio):          # [kh][kw][ci][co] -> [co][kh*kw*ci]
-    kh, kw, ci, co = w_hwio.shape
-    return w_hwio.permute(3, 0, 1, 2).reshape(co, kh * kw * ci).contiguous()
+def pad64(m):                   # rows zero-padded to a multiple of 64 (the kernels' K step)
+    k = m.shape[1]
+    kp = (k + 63) // 64 * 64
+    out = torch.zeros(m.shape[0], kp, dtype=m.dtype, device=m.device)
+    out[:, :k] = m
+    return out
 
 
-def pack_dgrad(w_hwio):        # -> [ci][taps flipped][co]
+def pack_fwd(w_hwio):          # [kh][kw][ci][co] -> [co][kh*kw*ci (pad 64)]
     kh, kw, ci, co = w_hwio.shape
-    return w_hwio.flip(0, 1).permute(2, 0, 1, 3).reshape(ci, kh * kw * co).contiguous()
+    return pad64(w_hwio.permute(3, 0, 1, 2).reshape(co, kh * kw * ci))
+
+
+def pack_dgrad(w_hwio):        # -> [ci][taps flipped][co] (pad 64)
+    kh, kw, ci, co = w_hwio.shape
+    return pad64(w_hwio.flip(0, 1).permute(2, 0, 1, 3).reshape(ci, kh * kw * co))
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout", [(2, 16, 32, 32), (2, 8, 64, 128), (1, 32, 32, 64), (4, 8, 128, 256)])
@@ -106,8 +114,7 @@ def test_conv_first_layer_smallc(cuda_dev):
     x = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
     w = (torch.randn(3, 3, Cin, Co, device=cuda_dev) * 0.2).bfloat16()
     b = torch.randn(Co, device=cuda_dev)
-    wp = torch.zeros(Co, 64, device=cuda_dev, dtype=torch.bfloat16)
-    wp[:, :36] = pack_fwd(w)
+    wp = pack_fwd(w)
     out = torch.empty(N, H, H, Co, device=cuda_dev, dtype=torch.bfloat16)
     C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(x), wgt=ptr(wp),
                       bias=ptr(b), Cout=Co, relu=1, dst1=ptr(out)), stream())
@@ -122,14 +129,14 @@ def test_tconv_fwd_shuffle_and_dgrad(cuda_dev):
     k = (torch.randn(2, 2, Co, Ci, device=cuda_dev) * 0.1).bfloat16()   # Keras (kh,kw,Cout,Cin)
     b = torch.randn(Co, device=cuda_dev)
     out = torch.empty(N, 2 * H, 2 * H, Co, device=cuda_dev, dtype=torch.bfloat16)
-    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, C1=Ci, src1=ptr(x), wgt=ptr(k.reshape(4 * Co, Ci)),
+    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, C1=Ci, src1=ptr(x), wgt=ptr(pad64(k.reshape(4 * Co, Ci))),
                       bias=ptr(b), Cout=4 * Co, shuffle=2, dst1=ptr(out)), stream())
     wt = k.float().permute(3, 2, 0, 1)      # (Cin, Cout, kh, kw)
     ref = nhwc(F.conv_transpose2d(nchw(x.float()), wt, b, stride=2))
     assert rel_err(out, ref) < 1e-2
     # dgrad: 2x2 stride-2 conv of dOut with weights [ci][tap][co], masked by x > 0
     dout = torch.randn(N, 2 * H, 2 * H, Co, device=cuda_dev).bfloat16()
-    wdg = k.permute(3, 0, 1, 2).reshape(Ci, 4 * Co).contiguous()
+    wdg = pad64(k.permute(3, 0, 1, 2).reshape(Ci, 4 * Co))
     dx = torch.empty(N, H, H, Ci, device=cuda_dev, dtype=torch.bfloat16)
     C().conv_fwd(dict(N=N, OH=H, OW=H, IH=2 * H, IW=2 * H, KH=2, KW=2, stride=2, pad=0, C1=Co,
                       src1=ptr(dout), wgt=ptr(wdg), Cout=Ci, dst1=ptr(dx), mask1=ptr(x)), stream())
@@ -146,17 +153,18 @@ def _wgrad(d, splits, taps, Mtot, Mout, Nc, out_numel, bias_w=None, rows=None):
     d = dict(d, splits=splits, slab=ptr(slab), bias_slab=ptr(bslab))
     C().wgrad(d, stream())
     out = torch.zeros(out_numel, device=dev)
+    stage = torch.zeros(C().wgrad_reduce_stage_floats(max(splits, 64), taps, Mtot, Nc) + 4096, device=dev)
     ints = [splits, taps, Mtot, Mout, Nc] + (list(rows) if rows else [])
-    C().generic("wgrad_reduce", [ptr(slab), ptr(out)], ints, [1.0], stream())
+    C().generic("wgrad_reduce", [ptr(slab), ptr(out), ptr(stage)], ints, [1.0], stream())
     bout = None
     if bias_w is not None:
         nrows, w = bias_w
         bout = torch.zeros(w, device=dev)
-        C().generic("wgrad_reduce", [ptr(bslab), ptr(bout)], [nrows, 1, 1, 1, w], [1.0], stream())
+        C().generic("wgrad_reduce", [ptr(bslab), ptr(bout), ptr(stage)], [nrows, 1, 1, 1, w], [1.0], stream())
     return out, bout
 
 
-@pytest.mark.parametrize("N,H,Cin,Cout,splits", [(4, 16, 32, 32, 3), (2, 16, 64, 128, 2), (2, 8, 128, 128, 4),
+@pytest.mark.parametrize("N,H,Cin,Cout,splits", [(4, 16, 32, 32, 3), (8, 32, 32, 32, 40), (2, 16, 64, 128, 2), (2, 8, 128, 128, 4),
                                                   (2, 8, 256, 512, 2)])
 def test_conv_wgrad_and_bias(cuda_dev, N, H, Cin, Cout, splits):
     torch.manual_seed(5)

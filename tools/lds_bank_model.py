@@ -108,3 +108,27 @@ if __name__ == "__main__":
     print("fwd b128 read/write worst ways:", check_fwd())
     for BM in (32, 64, 128, 256):
         print("tr BM=%d read/write ways:" % BM, check_tr(BM))
+
+
+# ---------------------------------------------------------------- 128-byte rows (BK = 64)
+def find_swz128():
+    """Search XOR swizzles chunk' = chunk ^ (A . bits(row & 15)) over GF(2) for
+    conflict-free ds_read_b128 16x16x32 fragment reads on [row][64 bf16] tiles."""
+    import itertools
+    best = None
+    for cols in itertools.product(range(8), repeat=4):     # images of row bits 0..3
+        def f(r):
+            v = 0
+            for b in range(4):
+                if (r >> b) & 1:
+                    v ^= cols[b]
+            return v
+        worst = 1
+        for kh2 in range(2):
+            addrs = [(l & 15) * 128 + 16 * (((l >> 4) + 4 * kh2) ^ f(l & 15)) for l in range(64)]
+            worst = max(worst, read_b128(addrs))
+        if worst == 1:
+            return cols
+        if best is None or worst < best[0]:
+            best = (worst, cols)
+    return best

@@ -7,10 +7,10 @@
 // UNcorrected sqrt(v), lr_t = lr sqrt(1-b2^t)/(1-b1^t) computed on the host),
 // then writes the updated weight, rounded to bf16, into the compute layouts
 // the conv kernels read:
-//   conv  kernel HWIO [T][Ci][Co] -> fwd  [Co][T*Ci_pad (+pad to Kpad)]
-//                                 -> dgrad [Ci][T][Co] with the taps flipped
-//   tconv kernel [T][Co][Ci]      -> fwd  = same layout (GEMM rows (tap, co))
-//                                 -> dgrad [Ci][T][Co]
+//   conv  kernel HWIO [T][Ci][Co] -> fwd  [Co][T*Ci_pad, padded to Kpad = 64k]
+//                                 -> dgrad [Ci][T*Co padded] with the taps flipped
+//   tconv kernel [T][Co][Ci]      -> fwd  [(T, Co)][Ci padded]  (GEMM rows (tap, co))
+//                                 -> dgrad [Ci][T*Co padded]
 // With do_adam = 0 the kernel only repacks (initialisation / checkpoint load).
 #include "common.h"
 #include "conv_params.h"
@@ -57,14 +57,14 @@ __global__ void __launch_bounds__(256) adam_pack_kernel(float* __restrict__ w, c
       const int ci = r % sg.Ci;
       const int t = r / sg.Ci;
       if (sg.fwd_off >= 0) arena[sg.fwd_off + (long long)co * sg.rowstride + t * sg.Ci_pad + ci] = wb;
-      if (sg.dg_off >= 0) arena[sg.dg_off + ((long long)ci * sg.T + (sg.T - 1 - t)) * sg.Co + co] = wb;
+      if (sg.dg_off >= 0) arena[sg.dg_off + (long long)ci * sg.dg_rowstride + (sg.T - 1 - t) * sg.Co + co] = wb;
     } else {
       const int ci = e % sg.Ci;
       const int r = e / sg.Ci;
       const int co = r % sg.Co;
       const int t = r / sg.Co;
-      if (sg.fwd_off >= 0) arena[sg.fwd_off + e] = wb;
-      if (sg.dg_off >= 0) arena[sg.dg_off + ((long long)ci * sg.T + t) * sg.Co + co] = wb;
+      if (sg.fwd_off >= 0) arena[sg.fwd_off + ((long long)t * sg.Co + co) * sg.rowstride + ci] = wb;
+      if (sg.dg_off >= 0) arena[sg.dg_off + (long long)ci * sg.dg_rowstride + t * sg.Co + co] = wb;
     }
   }
 }

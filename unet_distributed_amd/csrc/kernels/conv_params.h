@@ -17,7 +17,7 @@ struct ConvFwdParams {
   int up1;                    // src1 is stored at 1/up1 resolution (nearest upsample fold)
   const void* src1;
   const void* src2;
-  const void* wgt;            // bf16 [Cout][KD*KH*KW][C1+C2]
+  const void* wgt;            // bf16 [Cout][Kpad], row = (tap, channel), zero padded to a multiple of 64
   const float* bias;          // [Cout] or nullptr
   int Cout;
   int relu;
@@ -32,6 +32,10 @@ struct ConvFwdParams {
   float mask_scale1, mask_scale2;
   int shuffle;                // 0, or number of upsampled dims (2/3): tconv pixel shuffle
   float* stats;               // nullptr or [2][Cout] per-channel sum / sum of squares (BN)
+  // filled by conv_fwd_prepare (host): K padded to 64, per-tap pixel deltas / offsets
+  int Kpad;
+  int tap_delta[27];
+  signed char tap_d[27], tap_h[27], tap_w[27];
 };
 
 // "TN" weight-gradient GEMM with split-K over pixels:
@@ -67,7 +71,8 @@ struct PackSeg {
   int off, n;          // element range in the flat master buffer
   int kind;            // 0 = none (bias / fp32-only), 1 = conv, 2 = tconv
   int T, Ci, Co;       // taps, input/output channels (TF kernel semantics)
-  int Ci_pad, rowstride;
+  int Ci_pad, rowstride;  // fwd copy: row length (K padded to 64)
+  int dg_rowstride, pad_;  // dgrad copy: row length
   long long fwd_off;   // element offset into the bf16 weight arena, -1 = none
   long long dg_off;    // dgrad copy, -1 = none
 };

@@ -272,25 +272,48 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
 }
 
 // out[t][m][n] (m < Mout) = scale * sum_s slab[s][t][m][n]   (Mtot >= Mout rows in the slab)
-// Rows are remapped for the first layer whose input channels were padded:
-// output row o = grp * rkeep + j reads slab row grp * rg + j  (rg = rkeep = Mout: identity).
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int taps,
-                                                           int Mtot, int Mout, int Nc, int rg, int rkeep, float scale,
-                                                           float* __restrict__ out) {
-  const size_t n4 = (size_t)taps * Mout * Nc / 4;
-  const size_t sstride = (size_t)taps * Mtot * Nc;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
-    const size_t e = i * 4;
-    const int n = e % Nc;
-    const size_t r = e / Nc;
-    const int mo = r % Mout;
-    const int t = r / Mout;
-    const int m = (mo / rkeep) * rg + (mo % rkeep);
-    const float* src = slab + ((size_t)t * Mtot + m) * Nc + n;
-    f32x4 s = {0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < splits; ++k) s += *(const f32x4*)(src + k * sstride);
-    *(f32x4*)(out + e) = s * scale;
+// Deterministic two-level reduction of the split-K slabs.
+// Stage 1 (grid x = float4 chunks of a slab row, grid y = groups of G splits):
+//   stage[y][i] = sum_{s in group y} slab[s][i]          (8 loads in flight per thread)
+// Stage 2: out[o] = scale * sum_y stage[y][row_map(o)]   (rows remapped for the padded
+//   first-layer input: output row o = grp*rkeep + j reads slab row grp*rg + j).
+// With a single group, stage 1 writes the output directly (identity row map only).
+constexpr int RED_G = 16;
+
+__global__ void __launch_bounds__(256) slab_partial_kernel(const float* __restrict__ slab, int splits, size_t n4,
+                                                           float* __restrict__ stage, float scale) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const int s0 = blockIdx.y * RED_G, s1 = min(splits, s0 + RED_G);
+  const f32x4* src = (const f32x4*)slab + i;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  int s = s0;
+  for (; s + 4 <= s1; s += 4) {
+    const f32x4 a = src[(size_t)s * n4], b = src[(size_t)(s + 1) * n4];
+    const f32x4 c = src[(size_t)(s + 2) * n4], d = src[(size_t)(s + 3) * n4];
+    acc += (a + b) + (c + d);
   }
+  for (; s < s1; ++s) acc += src[(size_t)s * n4];
+  ((f32x4*)stage)[(size_t)blockIdx.y * n4 + i] = acc * scale;
+}
+
+__global__ void __launch_bounds__(256) slab_final_kernel(const float* __restrict__ stage, int groups, int taps, int Mtot,
+                                                         int Mout, int Nc, int rg, int rkeep,
+                                                         float* __restrict__ out) {
+  const size_t n4o = (size_t)taps * Mout * Nc / 4;
+  const size_t n4 = (size_t)taps * Mtot * Nc / 4;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n4o) return;
+  const size_t e = i * 4;
+  const int n = e % Nc;
+  const size_t r = e / Nc;
+  const int mo = r % Mout;
+  const int t = r / Mout;
+  const int m = (mo / rkeep) * rg + (mo % rkeep);
+  const size_t src = (((size_t)t * Mtot + m) * Nc + n) / 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int y = 0; y < groups; ++y) acc += ((const f32x4*)stage)[(size_t)y * n4 + src];
+  ((f32x4*)out)[i] = acc;
 }
 
 // partial[b][c] = sum over rows r of block b of x[r][c]   (bf16 [rows][C], C % 8 == 0, C <= 1024)
@@ -378,15 +401,28 @@ hipError_t wgrad_launch(const WgradParams& p, hipStream_t s) {
   return launch_wg<64, 64, 1, 2, 2>(p, s);
 }
 
+size_t wgrad_reduce_stage_floats(int splits, int taps, int Mtot, int Nc) {
+  const int groups = (splits + RED_G - 1) / RED_G;
+  return (size_t)groups * taps * Mtot * Nc;
+}
+
 hipError_t wgrad_reduce_launch(const float* slab, int splits, int taps, int Mtot, int Mout, int Nc, int rg, int rkeep,
-                               float scale, float* out, hipStream_t s) {
+                               float scale, float* out, float* stage, hipStream_t s) {
   if (rg <= 0) rg = Mout;
   if (rkeep <= 0) rkeep = rg;
-  const size_t n4 = (size_t)taps * Mout * Nc / 4;
-  int grid = (int)std::min<size_t>((n4 + 255) / 256, 4096);
-  if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(256), 0, s, slab, splits, taps, Mtot, Mout, Nc, rg, rkeep,
-                     scale, out);
+  const bool identity = (Mout == Mtot) && (rg == rkeep);
+  const int groups = (splits + RED_G - 1) / RED_G;
+  const size_t n4 = (size_t)taps * Mtot * Nc / 4;
+  const dim3 g1((unsigned)((n4 + 255) / 256), (unsigned)groups);
+  if (groups == 1 && identity) {
+    hipLaunchKernelGGL(slab_partial_kernel, g1, dim3(256), 0, s, slab, splits, n4, out, scale);
+    return hipGetLastError();
+  }
+  if (!stage) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(slab_partial_kernel, g1, dim3(256), 0, s, slab, splits, n4, stage, scale);
+  const size_t n4o = (size_t)taps * Mout * Nc / 4;
+  hipLaunchKernelGGL(slab_final_kernel, dim3((unsigned)((n4o + 255) / 256)), dim3(256), 0, s, stage, groups, taps,
+                     Mtot, Mout, Nc, rg, rkeep, out);
   return hipGetLastError();
 }
 

@@ -95,7 +95,7 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.shuffle = get<int>(d, "shuffle", 0);
   p.stats = (float*)getp(d, "stats");
   if (!p.src1 || !p.wgt || !p.dst1) throw std::invalid_argument("conv_fwd: src1/wgt/dst1 required");
-  check_msg(conv_fwd_check(p));
+  check_msg(conv_fwd_prepare(p));
   return p;
 }
 
@@ -170,15 +170,19 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     return [=](hipStream_t s) { return upsample2_bwd_launch(du, mk, n, d, h, w, c, d3, dl, s); };
   }
   if (kind == "wgrad_reduce") {
-    // ints: splits, taps, Mtot, Mout, Nc[, rg, rkeep]
+    // ptrs: slab, out[, stage]   ints: splits, taps, Mtot, Mout, Nc[, rg, rkeep]
     need(2, 5, 1);
     const float* slab = (const float*)vp(0);
     float* out = (float*)vp(1);
+    float* stage = P.size() > 2 ? (float*)vp(2) : nullptr;
     int sp = I[0], taps = I[1], mt = I[2], mo = I[3], nc = I[4];
     int rg = I.size() > 5 ? (int)I[5] : 0, rk = I.size() > 6 ? (int)I[6] : 0;
     float sc = (float)F[0];
     if (nc % 4) throw std::invalid_argument("wgrad_reduce: Nc % 4");
-    return [=](hipStream_t s) { return wgrad_reduce_launch(slab, sp, taps, mt, mo, nc, rg, rk, sc, out, s); };
+    const bool identity = (mo == mt) && (rg == rk);
+    if (!stage && !(identity && sp <= 16))
+      throw std::invalid_argument("wgrad_reduce: stage buffer required for >16 splits or row remap");
+    return [=](hipStream_t s) { return wgrad_reduce_launch(slab, sp, taps, mt, mo, nc, rg, rk, sc, out, stage, s); };
   }
   if (kind == "colsum") {
     need(2, 3, 0);
@@ -300,6 +304,7 @@ PYBIND11_MODULE(_C, m) {
           "adam_pack");
   });
   m.def("head_blocks", &head_blocks_py);
+  m.def("wgrad_reduce_stage_floats", &wgrad_reduce_stage_floats);
   m.def("wgrad_pick", [](int M1, int M2, int Nc, int KT) {
     WgradParams p{};
     p.M1 = M1;

@@ -8,14 +8,15 @@
 
 namespace unet {
 
-const char* conv_fwd_check(const ConvFwdParams& p);
+const char* conv_fwd_prepare(ConvFwdParams& p);
 hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s);
 
 const char* wgrad_check(const WgradParams& p);
 WgradCfg wgrad_pick(const WgradParams& p);
 hipError_t wgrad_launch(const WgradParams& p, hipStream_t s);
 hipError_t wgrad_reduce_launch(const float* slab, int splits, int taps, int Mtot, int Mout, int Nc, int rg, int rkeep,
-                               float scale, float* out, hipStream_t s);
+                               float scale, float* out, float* stage, hipStream_t s);
+size_t wgrad_reduce_stage_floats(int splits, int taps, int Mtot, int Nc);
 hipError_t colsum_launch(const void* x, int rows, int C, int blocks, float* partial, hipStream_t s);
 
 hipError_t cast_input_launch(const float* x, int P, int Cin, int Cpad, void* y, hipStream_t s);

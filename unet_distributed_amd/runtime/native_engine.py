@@ -44,6 +44,10 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else int(t.data_ptr())
 
 
+def _r64(k: int) -> int:
+    return (k + 63) // 64 * 64
+
+
 class NativeUNet:
     """Plans and runs forward + backward of one UNet micro-batch on the GPU."""
 
@@ -74,7 +78,7 @@ class NativeUNet:
         else:
             raise NotImplementedError("native executor: in_channels=%d" % cin)
         self.bufs: Dict[str, torch.Tensor] = {}
-        self._grad_ptr_cache = {}
+        self.wg_target = 512
         self._alloc_weights()
         self._alloc_activations()
         self.plan = self.C.Plan()
@@ -120,39 +124,35 @@ class NativeUNet:
             if l.kind == "conv":
                 first = l.name == spec.layers[0].name
                 ci_pad = self.cpad if first else l.cin
-                if first and self.cpad < 32:
-                    row = ((T * ci_pad + 31) // 32) * 32
-                else:
-                    row = T * ci_pad
+                row = _r64(T * ci_pad)                 # K padded to the 64-wide K step
+                dgrow = _r64(T * l.cout)
                 self.w_fwd_off[l.name] = off
                 off += l.cout * row
-                off = (off + 63) // 64 * 64
                 if not first:
                     self.w_dg_off[l.name] = off
-                    off += l.cin * T * l.cout
-                    off = (off + 63) // 64 * 64
-                layouts[l.name] = (1, T, l.cin, l.cout, ci_pad, row)
+                    off += l.cin * dgrow
+                layouts[l.name] = (1, T, l.cin, l.cout, ci_pad, row, dgrow)
             elif l.kind == "tconv":
+                row = _r64(l.cin)
+                dgrow = _r64(Tt * l.cout)
                 self.w_fwd_off[l.name] = off
-                off += Tt * l.cout * l.cin
-                off = (off + 63) // 64 * 64
+                off += Tt * l.cout * row
                 self.w_dg_off[l.name] = off
-                off += Tt * l.cout * l.cin
-                off = (off + 63) // 64 * 64
-                layouts[l.name] = (2, Tt, l.cin, l.cout, l.cin, 0)
+                off += l.cin * dgrow
+                layouts[l.name] = (2, Tt, l.cin, l.cout, l.cin, row, dgrow)
         self.arena = torch.zeros(max(off, 64), dtype=BF16, device=self.device)
         segs = []
         for name, shape, foff, n in flat.entries:
             lname, var = name.split("/", 1)
             if var == "kernel" and lname in layouts:
-                kind, t, ci, co, ci_pad, row = layouts[lname]
-                segs.append((foff, n, kind, t, ci, co, ci_pad, row,
+                kind, t, ci, co, ci_pad, row, dgrow = layouts[lname]
+                segs.append((foff, n, kind, t, ci, co, ci_pad, row, dgrow, 0,
                              self.w_fwd_off[lname], self.w_dg_off.get(lname, -1)))
             else:
-                segs.append((foff, n, 0, 0, 0, 0, 0, 0, -1, -1))
+                segs.append((foff, n, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1))
         dt = np.dtype([("off", "<i4"), ("n", "<i4"), ("kind", "<i4"), ("T", "<i4"), ("Ci", "<i4"),
-                       ("Co", "<i4"), ("Ci_pad", "<i4"), ("rowstride", "<i4"),
-                       ("fwd_off", "<i8"), ("dg_off", "<i8")])
+                       ("Co", "<i4"), ("Ci_pad", "<i4"), ("rowstride", "<i4"), ("dg_rowstride", "<i4"),
+                       ("pad_", "<i4"), ("fwd_off", "<i8"), ("dg_off", "<i8")])
         assert dt.itemsize == self.C.packseg_bytes()
         arr = np.array(segs, dtype=dt)
         self.nseg = len(segs)
@@ -303,7 +303,9 @@ class NativeUNet:
         Mtot = ((KT * M1 + BM - 1) // BM) * BM if smallc else M1 + M2
         tg = 1 if smallc else KT // NTAP
         tiles = (Mtot // BM) * (Nc // BN) * tg
-        splits = max(1, min(-(-2048 // tiles), max(1, Q // (32 * 16))))
+        # ~2 workgroups per CU: enough to fill 256 CUs, few enough that the fp32
+        # split-K slabs stay small next to the GEMM's own operand traffic
+        splits = max(1, min(-(-self.wg_target // tiles), max(1, Q // (32 * 32))))
         taps = 1 if smallc else KT
         return splits, Mtot, taps, tg, smallc
 
@@ -432,8 +434,14 @@ class NativeUNet:
             smax = max(smax, splits * taps * Mtot * w["Nc"])
             bw = w["bias_width"] if w["bias_mode"] == 1 else Mtot
             bmax = max(bmax, splits * tg * bw)
+        stmax = 1
+        for w, (splits, Mtot, taps, tg, smallc) in zip(wg_specs, sized):
+            stmax = max(stmax, self.C.wgrad_reduce_stage_floats(splits, taps, Mtot, w["Nc"]))
+            bw = w["bias_width"] if w["bias_mode"] == 1 else Mtot
+            stmax = max(stmax, self.C.wgrad_reduce_stage_floats(splits * tg, 1, 1, bw))
         self.slab = torch.empty(smax, dtype=torch.float32, device=self.device)
         self.bias_slab = torch.empty(bmax, dtype=torch.float32, device=self.device)
+        self.red_stage = torch.empty(stmax, dtype=torch.float32, device=self.device)
 
         for op in ops:
             if callable(op):
@@ -451,19 +459,19 @@ class NativeUNet:
                 KT = w["KT"]
                 if smallc:
                     cpad, creal = rr
-                    plan.add_generic("wgrad_reduce", [_ptr(self.slab), self.grad_ptr(w["kernel"])],
+                    plan.add_generic("wgrad_reduce", [_ptr(self.slab), self.grad_ptr(w["kernel"]), _ptr(self.red_stage)],
                                      [splits, 1, Mtot, KT * creal, w["Nc"], cpad, creal], [1.0],
                                      "wred:" + w["lname"])
                 else:
-                    plan.add_generic("wgrad_reduce", [_ptr(self.slab), self.grad_ptr(w["kernel"])],
+                    plan.add_generic("wgrad_reduce", [_ptr(self.slab), self.grad_ptr(w["kernel"]), _ptr(self.red_stage)],
                                      [splits, taps, Mtot, Mtot, w["Nc"]], [1.0], "wred:" + w["lname"])
                 bw = w["bias_width"]
                 if w["bias_mode"] == 1:
-                    plan.add_generic("wgrad_reduce", [_ptr(self.bias_slab), self.grad_ptr(w["bias"])],
+                    plan.add_generic("wgrad_reduce", [_ptr(self.bias_slab), self.grad_ptr(w["bias"]), _ptr(self.red_stage)],
                                      [splits, 1, 1, 1, bw], [1.0], "bred:" + w["lname"])
                 else:
                     # [splits*tg][Mtot] rows -> bias (Mtot == cout for tconv)
-                    plan.add_generic("wgrad_reduce", [_ptr(self.bias_slab), self.grad_ptr(w["bias"])],
+                    plan.add_generic("wgrad_reduce", [_ptr(self.bias_slab), self.grad_ptr(w["bias"]), _ptr(self.red_stage)],
                                      [splits * tg, 1, 1, 1, bw], [1.0], "bred:" + w["lname"])
 
     # ------------------------------------------------------------------ buckets
