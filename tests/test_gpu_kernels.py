@@ -73,7 +73,7 @@ def test_conv3x3_fwd_bias_relu(cuda_dev, N, H, Cin, Cout):
 
 def test_conv3x3_concat_dual_source_and_upsample(cuda_dev):
     torch.manual_seed(1)
-    N, H, C1, C2, Co = 2, 16, 32, 64, 64
+    N, H, C1, C2, Co = 2, 16, 64, 64, 64
     lo = torch.randn(N, H // 2, H // 2, C1, device=cuda_dev).bfloat16()   # upsampled source
     skip = torch.randn(N, H, H, C2, device=cuda_dev).bfloat16()
     w = (torch.randn(3, 3, C1 + C2, Co, device=cuda_dev) * 0.05).bfloat16()
@@ -82,6 +82,19 @@ def test_conv3x3_concat_dual_source_and_upsample(cuda_dev):
                       src2=ptr(skip), wgt=ptr(pack_fwd(w)), Cout=Co, relu=0, dst1=ptr(out)), stream())
     up = F.interpolate(nchw(lo.float()), scale_factor=2, mode="nearest")
     ref = nhwc(F.conv2d(torch.cat([up, nchw(skip.float())], 1), w.float().permute(3, 2, 0, 1), padding=1))
+    assert rel_err(out, ref) < 1e-2
+
+
+def test_conv3x3_concat_32_32(cuda_dev):
+    torch.manual_seed(12)
+    N, H, C1, C2, Co = 2, 16, 32, 32, 32
+    a = torch.randn(N, H, H, C1, device=cuda_dev).bfloat16()
+    b = torch.randn(N, H, H, C2, device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, C1 + C2, Co, device=cuda_dev) * 0.05).bfloat16()
+    out = torch.empty(N, H, H, Co, device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=C1, C2=C2, src1=ptr(a),
+                      src2=ptr(b), wgt=ptr(pack_fwd(w)), Cout=Co, relu=0, dst1=ptr(out)), stream())
+    ref = nhwc(F.conv2d(torch.cat([nchw(a.float()), nchw(b.float())], 1), w.float().permute(3, 2, 0, 1), padding=1))
     assert rel_err(out, ref) < 1e-2
 
 

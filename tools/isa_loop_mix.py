@@ -19,6 +19,8 @@ for i, l in enumerate(body):
         n_mf = sum(1 for j in mf if labels[m.group(1)] <= j <= i)
         if n_mf and (best is None or (n_mf, -(i - labels[m.group(1)])) > (best[2], -(best[1] - best[0]))):
             best = (labels[m.group(1)], i, n_mf)
+if best is None:
+    best = (mf[0], mf[-1], len(mf))
 s, e, _ = best
 ins = [l.strip().split()[0] for l in body[s:e + 1] if l.strip() and not l.strip().startswith((";", ".")) and not l.startswith(".")]
 cat = Counter()

@@ -102,16 +102,19 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
     a_pix[i] = ((c.n * p.ID + bd) * p.IH + bh) * p.IW + bw;
     a_pb1[i] = a_pix[i] * p.C1 * 2;
     a_pb2[i] = a_pix[i] * p.C2 * 2;
+    // in-bounds tap mask, taps ordered t = (kd*KH + kh)*KW + kw; kernel extents <= 3
     uint32_t m = 0;
-    if (ok) {
-      for (int t = 0; t < KT; ++t) {
-        const int kw = p.tap_w[t], kh = p.tap_h[t], kd = p.tap_d[t];
-        const int id = bd + kd, ih = bh + kh, iw = bw + kw;
-        if ((unsigned)id < (unsigned)p.ID && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW)
-          m |= 1u << t;
-      }
-    }
-    a_mask[i] = m;
+#pragma unroll
+    for (int kd = 0; kd < 3; ++kd)
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const bool in = kd < p.KD && kh < p.KH && kw < p.KW && (unsigned)(bd + kd) < (unsigned)p.ID &&
+                          (unsigned)(bh + kh) < (unsigned)p.IH && (unsigned)(bw + kw) < (unsigned)p.IW;
+          if (in) m |= 1u << ((kd * p.KH + kh) * p.KW + kw);
+        }
+    a_mask[i] = ok ? m : 0u;
     if (MODE == 1) {
       a_lo[i] = ((c.n * ID1 + c.d / upd) * IH1 + c.h / 2) * IW1 + c.w / 2;
       a_par[i] = ((c.d & 1) << 2) | ((c.h & 1) << 1) | (c.w & 1);
@@ -134,11 +137,14 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
   }
 
   int kt_tap = 0, kt_kk = 0;           // (tap, channel) at the start of the K step being loaded
+  const bool c32 = Cin == 32;
+  const int kk_c = c32 ? (cc & 3) * 8 : cc * 8;
+  const int hi_c = (c32 && cc >= 4) ? 1 : 0;
   auto load_stage = [&](int ks) {
     const int k0 = ks * BK;
     if constexpr (MODE == 2) {
       // first layer: chunk cc covers k = k0 + 8cc .. +7 = (8 / Cin) taps x Cin channels
-      const int t0 = (k0 + cc * 8) / Cin;
+      const int t0 = (k0 + cc * 8) / Cin;   // lane-varying; first layers have 1-2 K steps
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         u32x4 v = {0u, 0u, 0u, 0u};
@@ -158,26 +164,32 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
         ra[i] = v;
       }
     } else {
-      // K step = 64 consecutive k of the (tap, channel) index; with Cin == 32 the
-      // upper four chunk columns belong to the next tap.  (tap0, kk0) advance
-      // incrementally with the K loop; both taps' table entries are wave-uniform and
-      // each lane selects one.
-      const int tap0 = kt_tap, kk0 = kt_kk;
-      int kk = kk0 + cc * 8;
-      const bool hi = kk >= Cin;
-      kk -= hi ? Cin : 0;
-      const int tap = tap0 + (hi ? 1 : 0);
+      // K step = 64 consecutive k of the (tap, channel) index.  Cin == 32: the upper
+      // four chunk columns belong to the next tap (hi_c); Cin % 64 == 0: one tap per
+      // step.  hi_c / kk_c / the concat source are per-thread loop invariants, the
+      // tap (kt_tap) and channel base (kt_kk) are wave-uniform.
+      const int tap = kt_tap + hi_c;
+      const int kk = kt_kk + kk_c;
       const bool live = tap < KT;
-      const int t_a = tap0 < KT ? tap0 : 0, t_b = tap0 + 1 < KT ? tap0 + 1 : 0;
-      const int tdel = hi ? p.tap_delta[t_b] : p.tap_delta[t_a];
+      const int t_a = kt_tap < KT ? kt_tap : 0, t_b = kt_tap + 1 < KT ? kt_tap + 1 : 0;
+      // readfirstlane keeps both table reads scalar (s_load); a lane-indexed select
+      // would become a vector load from kernarg memory whose vmcnt(0) wait drains
+      // the whole prefetch pipeline every K step.
+      const int tdel_a = __builtin_amdgcn_readfirstlane(p.tap_delta[t_a]);
+      const int tdel_b = __builtin_amdgcn_readfirstlane(p.tap_delta[t_b]);
+      const int tdel = hi_c ? tdel_b : tdel_a;
       const bool from1 = !CONCAT || kk < p.C1;
       int dh = 0, dw = 0, dd = 0;
       if (MODE == 1) {
-        dh = hi ? p.tap_h[t_b] : p.tap_h[t_a];
-        dw = hi ? p.tap_w[t_b] : p.tap_w[t_a];
-        dd = hi ? p.tap_d[t_b] : p.tap_d[t_a];
+        const int ha = __builtin_amdgcn_readfirstlane(p.tap_h[t_a]), hb = __builtin_amdgcn_readfirstlane(p.tap_h[t_b]);
+        const int wa = __builtin_amdgcn_readfirstlane(p.tap_w[t_a]), wb = __builtin_amdgcn_readfirstlane(p.tap_w[t_b]);
+        const int da = __builtin_amdgcn_readfirstlane(p.tap_d[t_a]), db = __builtin_amdgcn_readfirstlane(p.tap_d[t_b]);
+        dh = hi_c ? hb : ha;
+        dw = hi_c ? wb : wa;
+        dd = hi_c ? db : da;
       }
-      const int td1 = tdel * p.C1 * 2 + kk * 2;
+      const int td1 = (tdel * p.C1 + kk) * 2;
+      const int td2 = (tdel * p.C2 + kk - p.C1) * 2;
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const bool ok = live && ((a_mask[i] >> tap) & 1u);
@@ -192,9 +204,8 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
           o1 = a_pb1[i] + td1;
         }
         if constexpr (CONCAT) {
-          const int o2 = a_pb2[i] + tdel * p.C2 * 2 + (kk - p.C1) * 2;
-          ra[i] = __builtin_amdgcn_raw_buffer_load_b128(rs1, (ok && from1) ? o1 : OOB, 0, 0) |
-                  __builtin_amdgcn_raw_buffer_load_b128(rs2, (ok && !from1) ? o2 : OOB, 0, 0);
+          const int o = from1 ? o1 : a_pb2[i] + td2;
+          ra[i] = __builtin_amdgcn_raw_buffer_load_b128(from1 ? rs1 : rs2, ok ? o : OOB, 0, 0);
         } else {
           ra[i] = __builtin_amdgcn_raw_buffer_load_b128(rs1, ok ? o1 : OOB, 0, 0);
         }
@@ -229,9 +240,9 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
   const int frag0 = fr * 128 + 16 * (((lane >> 4) + 0) ^ swz8(fr));
   const int frag1 = fr * 128 + 16 * (((lane >> 4) + 4) ^ swz8(fr));
 
-  auto advance = [&]() {   // Cin is 32 or a multiple of 64 (checked on the host)
-    if (Cin < BK) {
-      kt_tap += BK / 32;
+  auto advance = [&]() {   // Cin == 32 or a multiple of 64 (checked on the host)
+    if (c32) {
+      kt_tap += 2;
     } else {
       kt_kk += BK;
       if (kt_kk >= Cin) {
@@ -415,7 +426,7 @@ hipError_t launch_cfg(const ConvFwdParams& p, hipStream_t s) {
 // why the shape is unsupported.
 const char* conv_fwd_prepare(ConvFwdParams& p) {
   const int KT = p.KD * p.KH * p.KW;
-  if (KT < 1 || KT > 27) return "conv_fwd: 1..27 taps supported";
+  if (KT < 1 || KT > 27 || p.KD > 3 || p.KH > 3 || p.KW > 3) return "conv_fwd: kernel extents 1..3 supported";
   const bool smallc = (p.C1 == 4 || p.C1 == 8) && p.C2 == 0;
   if (smallc) {
     if (p.up1 != 1 || p.shuffle) return "conv_fwd: small-Cin mode supports plain convs only";
@@ -424,6 +435,9 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   }
   const int Cin = p.C1 + p.C2;
   if (!smallc && Cin != 32 && Cin % 64) return "conv_fwd: Cin must be 32 or a multiple of 64";
+  // the concat source must be constant per (thread, K step): split on a 64-channel
+  // boundary, or the 32 + 32 case where each thread's chunk column fixes the source
+  if (p.C2 > 0 && p.C1 % 64 && !(p.C1 == 32 && Cin == 64)) return "conv_fwd: concat split unsupported";
   if (p.Cout % 32) return "conv_fwd: Cout must be a multiple of 32";
   if (p.D1 <= 0 || p.D1 > p.Cout || (p.D1 % 8)) return "conv_fwd: bad channel split D1";
   if (p.D1 < p.Cout && !p.dst2) return "conv_fwd: dst2 missing for channel split";
@@ -435,6 +449,12 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.shuffle && ((p.Cout >> p.shuffle) % 8)) return "conv_fwd: shuffle channels must be multiples of 8";
   if (p.shuffle && p.D1 != p.Cout) return "conv_fwd: shuffle with channel split unsupported";
   if (p.stats && p.shuffle) return "conv_fwd: stats with shuffle unsupported";
+  if (p.tile < 0 || p.tile > 5) return "conv_fwd: bad tile id";
+  {
+    const int t = p.tile ? p.tile : 0;
+    const int bn = t == 1 ? 128 : (t == 2 || t == 5) ? 64 : 32;
+    if (t && p.Cout % bn) return "conv_fwd: forced tile does not divide Cout";
+  }
   if ((long long)p.N * p.ID * p.IH * p.IW >= (1LL << 31) || (long long)p.N * p.OD * p.OH * p.OW >= (1LL << 31))
     return "conv_fwd: too many pixels";
   // buffer loads use 32-bit byte offsets: every source tensor must stay below 2 GiB
@@ -455,11 +475,23 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   return nullptr;
 }
 
-hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
+// tile ids: 1 = 128x128, 2 = 128x64, 3 = 256x32, 4 = 128x32, 5 = 256x64 (4 waves each)
+int conv_fwd_pick(const ConvFwdParams& p) {
   const int M = p.N * p.OD * p.OH * p.OW;
-  if (p.Cout % 128 == 0 && M >= 8192) return launch_cfg<128, 128, 2, 2>(p, s);
-  if (p.Cout % 64 == 0) return launch_cfg<128, 64, 2, 2>(p, s);
-  return launch_cfg<256, 32, 4, 1>(p, s);
+  if (p.tile) return p.tile;
+  if (p.Cout % 128 == 0 && M >= 8192) return 1;
+  if (p.Cout % 64 == 0) return 2;
+  return 4;
+}
+
+hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
+  switch (conv_fwd_pick(p)) {
+    case 1: return launch_cfg<128, 128, 2, 2>(p, s);
+    case 2: return launch_cfg<128, 64, 2, 2>(p, s);
+    case 3: return launch_cfg<256, 32, 4, 1>(p, s);
+    case 5: return launch_cfg<256, 64, 4, 1>(p, s);
+    default: return launch_cfg<128, 32, 4, 1>(p, s);
+  }
 }
 
 }  // namespace unet

@@ -32,6 +32,7 @@ struct ConvFwdParams {
   float mask_scale1, mask_scale2;
   int shuffle;                // 0, or number of upsampled dims (2/3): tconv pixel shuffle
   float* stats;               // nullptr or [2][Cout] per-channel sum / sum of squares (BN)
+  int tile;                   // 0 = auto, else forced tile config id (tuning / A-B tests)
   // filled by conv_fwd_prepare (host): K padded to 64, per-tap pixel deltas / offsets
   int Kpad;
   int tap_delta[27];
@@ -59,6 +60,9 @@ struct WgradParams {
   // 2 = column sums of A over the WG's taps (tconv: dOut -> m)
   int bias_mode;
   float* bias_slab;           // [splits][tap_groups][M or Nc] fp32
+  // filled by the launcher
+  int lqw, lqh, lqd;          // log2 of the pixel grid (power-of-two fast path)
+  signed char tap_d[27], tap_h[27], tap_w[27];
 };
 
 // Tile configuration chosen for a wgrad problem (shared with the host planner).

@@ -63,16 +63,22 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, int lane, int cbase) 
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int BM, int BN, int NTAP, int WAVES_M, int WAVES_N, bool SMALLC, bool BIAS>
+// BK = 64 pixels per K step; 4 threads per pixel row (tid >> 2 = row, tid & 3 = sub).
+// With BM/8 a multiple of 4, the tap of chunk j = sub + 4i is j / (BM/8) = wave-uniform,
+// so tap deltas come from SGPRs.  Pixel coordinates use shifts when the grid is a
+// power of two (POW2), divisions otherwise.
+template <int BM, int BN, int NTAP, int WAVES_M, int WAVES_N, bool SMALLC, bool BIAS, bool POW2>
 __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
+  constexpr int BKW = 64;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int A_IMG = BK * BM * 2, B_IMG = BK * BN * 2;
+  constexpr int A_IMG = BKW * BM * 2, B_IMG = BKW * BN * 2;
   constexpr int STAGE = NTAP * A_IMG + B_IMG;
-  constexpr int NA = NTAP * BM / 8;          // A chunks per k row
-  constexpr int NCH = NA + BN / 8;           // chunks per k row
-  constexpr int CPT = (NCH + 7) / 8;         // chunks per thread (8 threads per row)
+  constexpr int NA = NTAP * BM / 8;          // A chunks per pixel row
+  constexpr int NCH = NA + BN / 8;           // chunks per pixel row
+  constexpr int CPT = NCH / 4;               // chunks per thread (4 threads per row)
   static_assert(WAVES_M * WAVES_N == 4, "4 waves");
+  static_assert((BM / 8) % 4 == 0 && NCH % 4 == 0, "chunk split");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -89,27 +95,40 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
   const int tn = t % tiles_n, tmi = t / tiles_n;
   const int m0 = tmi * BM, n0 = tn * BN;
   const int Q = p.N * p.QD * p.QH * p.QW;
-  const int per = ((Q + p.splits - 1) / p.splits + BK - 1) / BK * BK;
+  const int per = ((Q + p.splits - 1) / p.splits + BKW - 1) / BKW * BKW;
   const int kbeg = split * per;
   const int kend = min(Q, kbeg + per);
-  const int nks = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  const int nks = kend > kbeg ? (kend - kbeg + BKW - 1) / BKW : 0;
   const int upA = p.upA;
-  const int upAd = p.AD > 1 ? upA : 1;  // 2D: depth is never upsampled
+  const int upAd = p.AD > 1 ? upA : 1;       // 2D: depth is never upsampled
   const int AD1 = p.AD / upAd, AH1 = p.AH / upA, AW1 = p.AW / upA;
-  const int Cin_s = p.M1;  // SMALLC: channels of the first-layer input
-  const int padd = p.KD > 1 ? p.pad : 0;  // 2D: depth is not padded
+  const int padd = p.KD > 1 ? p.pad : 0;     // 2D: depth is not padded
+  const int Cin_s = p.M1;                    // SMALLC: channels of the first-layer input
 
-  const int krow = tid >> 3, sub = tid & 7;
+  const int krow = tid >> 2, sub = tid & 3;
   // bias partial sums: mode 1 once per (n-tile, split) [tm == 0, tg == 0]; mode 2 once per (m-tile, tg, split) [tn == 0]
   const bool bias_on = BIAS && ((p.bias_mode == 1 && tmi == 0 && tg == 0) || (p.bias_mode == 2 && tn == 0));
-  float bacc = 0.f;
+
+  constexpr int OOB = 0x7fffffff;
+  const __amdgpu_buffer_rsrc_t ra1 = __builtin_amdgcn_make_buffer_rsrc((void*)p.a1, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ra2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.a2 ? p.a2 : p.a1), (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rbb = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, OOB, 0x00020000);
+
   u32x4 reg[CPT];
 
   auto load = [&](int ks) {
-    const int q = kbeg + ks * BK + krow;
+    const int q = kbeg + ks * BKW + krow;
     const bool qok = q < kend;
-    int qn = 0, qd = 0, qh = 0, qw = 0;
-    if (qok) {
+    int qn, qd, qh, qw;
+    if (POW2) {
+      qw = q & (p.QW - 1);
+      int r = q >> p.lqw;
+      qh = r & (p.QH - 1);
+      r >>= p.lqh;
+      qd = r & (p.QD - 1);
+      qn = r >> p.lqd;
+    } else {
       qw = q % p.QW;
       int r = q / p.QW;
       qh = r % p.QH;
@@ -117,69 +136,92 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
       qd = r % p.QD;
       qn = r / p.QD;
     }
+    const int bd = qd * p.stride - padd, bh = qh * p.stride - p.pad, bw = qw * p.stride - p.pad;
+    const int pix0 = ((qn * p.AD + bd) * p.AH + bh) * p.AW + bw;     // window origin (full res)
+    int lo0 = 0, par = 0;
+    if (!SMALLC && upA == 2) {
+      const int cd = bd + padd, ch = bh + p.pad, cw = bw + p.pad;   // centre (stride 1 for the fold)
+      lo0 = ((qn * AD1 + cd / upAd) * AH1 + ch / 2) * AW1 + cw / 2;
+      par = ((cd & 1) << 2) | ((ch & 1) << 1) | (cw & 1);
+    }
+    if constexpr (SMALLC) {
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int j = sub + 8 * i;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (j < NA && qok) {
-        const int tl = j / (BM / 8), col = j % (BM / 8);
-        if constexpr (SMALLC) {
-          // m = tap*Cin + ci ; a chunk = 8/Cin taps
-          const int mm = m0 + col * 8;
+      for (int i = 0; i < NA / 4; ++i) {
+        const int col = sub + 4 * i;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        // m = tap*Cin + ci ; a chunk = 8/Cin taps (Cin in {4, 8})
+        const int mm = m0 + col * 8;
 #pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            if (e * Cin_s >= 8) break;
-            const int tap = mm / Cin_s + e;
-            if (tap >= KT) continue;
-            const int kw = tap % p.KW, kh = (tap / p.KW) % p.KH, kd = tap / (p.KW * p.KH);
-            const int ad = qd * p.stride + kd - padd, ah = qh * p.stride + kh - p.pad,
-                      aw = qw * p.stride + kw - p.pad;
-            if ((unsigned)ad >= (unsigned)p.AD || (unsigned)ah >= (unsigned)p.AH || (unsigned)aw >= (unsigned)p.AW)
-              continue;
-            const size_t pix = (((size_t)qn * p.AD + ad) * p.AH + ah) * p.AW + aw;
-            const bf16* src = (const bf16*)p.a1 + pix * Cin_s;
-            if (Cin_s == 8) {
-              v = *(const u32x4*)src;
-            } else {
-              const u32x2 h = *(const u32x2*)src;
-              v[2 * e] = h[0];
-              v[2 * e + 1] = h[1];
-            }
-          }
-        } else {
-          const int tap = tg * NTAP + tl;
-          const int kw = tap % p.KW, kh = (tap / p.KW) % p.KH, kd = tap / (p.KW * p.KH);
-          const int ad = qd * p.stride + kd - padd, ah = qh * p.stride + kh - p.pad,
-                    aw = qw * p.stride + kw - p.pad;
-          if ((unsigned)ad < (unsigned)p.AD && (unsigned)ah < (unsigned)p.AH && (unsigned)aw < (unsigned)p.AW) {
-            const int m = m0 + col * 8;
-            const bf16* src;
-            if (m < p.M1) {
-              const size_t pix = (((size_t)qn * AD1 + ad / upAd) * AH1 + ah / upA) * AW1 + aw / upA;
-              src = (const bf16*)p.a1 + pix * p.M1 + m;
-            } else {
-              const size_t pix = (((size_t)qn * p.AD + ad) * p.AH + ah) * p.AW + aw;
-              src = (const bf16*)p.a2 + pix * p.M2 + (m - p.M1);
-            }
-            v = *(const u32x4*)src;
+        for (int e = 0; e < 2; ++e) {
+          if (e * Cin_s >= 8) break;
+          const int tap = mm / Cin_s + e;
+          const int tt = tap < KT ? tap : 0;
+          const int kw = tt % p.KW, kh = (tt / p.KW) % p.KH, kd = tt / (p.KW * p.KH);
+          const bool ok = qok && tap < KT && (unsigned)(bd + kd) < (unsigned)p.AD &&
+                          (unsigned)(bh + kh) < (unsigned)p.AH && (unsigned)(bw + kw) < (unsigned)p.AW;
+          const int off = ((pix0 + (kd * p.AH + kh) * p.AW + kw) * Cin_s) * 2;
+          if (Cin_s == 8) {
+            v = __builtin_amdgcn_raw_buffer_load_b128(ra1, ok ? off : OOB, 0, 0);
+          } else {
+            const u32x2 h = __builtin_amdgcn_raw_buffer_load_b64(ra1, ok ? off : OOB, 0, 0);
+            v[2 * e] = h[0];
+            v[2 * e + 1] = h[1];
           }
         }
-      } else if (j >= NA && j < NCH && qok) {
-        const int col = j - NA;
-        v = *(const u32x4*)((const bf16*)p.b + (size_t)q * p.Nc + n0 + col * 8);
+        reg[i] = v;
       }
-      reg[i] = v;
+    } else {
+      constexpr int CPS = BM / 32;                  // chunks per thread per tap slot
+#pragma unroll
+      for (int tl = 0; tl < NTAP; ++tl) {
+        // per (K step, tap slot): scalar tap offsets, one validity test, one base offset
+        const int tap = tg * NTAP + tl;
+        const int kw = __builtin_amdgcn_readfirstlane(p.tap_w[tap]);
+        const int kh = __builtin_amdgcn_readfirstlane(p.tap_h[tap]);
+        const int kd = __builtin_amdgcn_readfirstlane(p.tap_d[tap]);
+        const bool ok = qok && (unsigned)(bd + kd) < (unsigned)p.AD && (unsigned)(bh + kh) < (unsigned)p.AH &&
+                        (unsigned)(bw + kw) < (unsigned)p.AW;
+        const int fpix = pix0 + (kd * p.AH + kh) * p.AW + kw;
+        int base1;
+        if (upA == 2) {
+          const int lh = (kh - p.pad + ((par >> 1) & 1)) >> 1;
+          const int lw = (kw - p.pad + (par & 1)) >> 1;
+          const int ld = p.AD > 1 ? ((kd - padd + ((par >> 2) & 1)) >> 1) : 0;
+          base1 = (lo0 + (ld * AH1 + lh) * AW1 + lw) * p.M1 * 2;
+        } else {
+          base1 = fpix * p.M1 * 2;
+        }
+        const int base2 = (fpix * p.M2 - p.M1) * 2;
+#pragma unroll
+        for (int ci = 0; ci < CPS; ++ci) {
+          const int m = m0 + (sub + 4 * ci) * 8;
+          const int i = tl * CPS + ci;
+          if (p.M2 == 0) {
+            reg[i] = __builtin_amdgcn_raw_buffer_load_b128(ra1, ok ? base1 + m * 2 : OOB, 0, 0);
+          } else {
+            const bool f1 = m < p.M1;
+            reg[i] = __builtin_amdgcn_raw_buffer_load_b128(ra1, (ok && f1) ? base1 + m * 2 : OOB, 0, 0) |
+                     __builtin_amdgcn_raw_buffer_load_b128(ra2, (ok && !f1) ? base2 + m * 2 : OOB, 0, 0);
+          }
+        }
+      }
+    }
+    const int bbase = q * p.Nc * 2 + n0 * 2;
+#pragma unroll
+    for (int i = NA / 4; i < CPT; ++i) {
+      const int col = sub + 4 * (i - NA / 4);
+      reg[i] = __builtin_amdgcn_raw_buffer_load_b128(rbb, qok ? bbase + col * 16 : OOB, 0, 0);
     }
   };
   auto store = [&](int buf) {
     char* S = smem + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
-      const int j = sub + 8 * i;
+      const int j = sub + 4 * i;
       if (j < NA) {
-        const int tl = j / (BM / 8), col = j % (BM / 8);
+        const int tl = (4 * i) / (BM / 8), col = j - tl * (BM / 8);
         *(u32x4*)(S + tl * A_IMG + tr_off<BM>(krow, col * 8)) = reg[i];
-      } else if (j < NCH) {
+      } else {
         const int col = j - NA;
         *(u32x4*)(S + NTAP * A_IMG + tr_off<BN>(krow, col * 8)) = reg[i];
       }
@@ -193,6 +235,18 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[a][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // bias column sums ride on the MFMA pipe: one extra MFMA per fragment against a
+  // constant all-ones operand (C[n][*] = sum_k B[k][n], or C[*][m] = sum_k A[k][m])
+  constexpr int NF = BIAS ? (TN > TM ? TN : TM) : 1;
+  f32x4 bacc[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) bacc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const u32x4 ones_u = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+  // wave-uniform scalar branches (readfirstlane) so the compiler does not predicate
+  // the extra MFMAs with exec masks
+  const bool do_b1 = BIAS && __builtin_amdgcn_readfirstlane((int)(bias_on && p.bias_mode == 1 && wm == 0));
+  const bool do_b2 = BIAS && __builtin_amdgcn_readfirstlane((int)(bias_on && p.bias_mode == 2 && wn == 0));
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_u);
 
   if (nks > 0) {
     load(0);
@@ -203,30 +257,27 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
     const int buf = ks & 1;
     if (ks + 1 < nks) load(ks + 1);
     const char* S = smem + buf * STAGE;
-    bf16x8 bfr[TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) bfr[j] = tr_frag<BN>(S + NTAP * A_IMG, lane, wn * WN + j * 16);
+    for (int h = 0; h < 2; ++h) {      // two k32 halves of the 64-pixel step
+      bf16x8 bfr[TN];
 #pragma unroll
-    for (int a = 0; a < NTAP; ++a) {
+      for (int j = 0; j < TN; ++j) bfr[j] = tr_frag<BN>(S + NTAP * A_IMG + h * 32 * BN * 2, lane, wn * WN + j * 16);
+      if constexpr (BIAS) {
+        if (do_b1) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const bf16x8 af = tr_frag<BM>(S + a * A_IMG, lane, wm * WM + i * 16);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[a][i][j] = mfma16(bfr[j], af, acc[a][i][j]);
+          for (int j = 0; j < TN; ++j) bacc[j] = mfma16(bfr[j], ones, bacc[j]);
+        }
       }
-    }
-    if constexpr (BIAS) {
-      // column sums of the staged B image (mode 1) or of the WG's A images (mode 2)
-      if (bias_on) {
-        if (p.bias_mode == 1) {
-          const int c = tid % BN;
-          for (int k = tid / BN; k < BK; k += NTHR / BN)
-            bacc += (float)*(const bf16*)(S + NTAP * A_IMG + tr_off<BN>(k, c));
-        } else {
-          const int c = tid % BM;
 #pragma unroll
-          for (int a = 0; a < NTAP; ++a)
-            for (int k = tid / BM; k < BK; k += NTHR / BM) bacc += (float)*(const bf16*)(S + a * A_IMG + tr_off<BM>(k, c));
+      for (int a = 0; a < NTAP; ++a) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const bf16x8 af = tr_frag<BM>(S + a * A_IMG + h * 32 * BM * 2, lane, wm * WM + i * 16);
+          if constexpr (BIAS) {
+            if (do_b2) bacc[i] = mfma16(ones, af, bacc[i]);
+          }
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[a][i][j] = mfma16(bfr[j], af, acc[a][i][j]);
         }
       }
     }
@@ -236,19 +287,19 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
 
   if constexpr (BIAS) {
     if (bias_on) {
-      // reduce bacc over the threads sharing a column (deterministic order through LDS)
-      float* red = (float*)smem;
-      red[tid] = bacc;
-      __syncthreads();
-      const int W = p.bias_mode == 1 ? BN : BM;
-      if (tid < W) {
-        float s = 0.f;
-        for (int k = tid; k < NTHR; k += W) s += red[k];
-        const int base = p.bias_mode == 1 ? n0 : m0;
-        const int Wtot = p.bias_mode == 1 ? p.Nc : Mtot;
-        const int tgi = p.bias_mode == 1 ? 0 : tg;
-        const int tgn = p.bias_mode == 1 ? 1 : p.tap_groups;
-        p.bias_slab[((size_t)split * tgn + tgi) * Wtot + base + tid] = s;
+      // mode 1: bacc[j] = C[n = 4g + r][*], g = lane >> 4 -> lanes 0,16,32,48 hold 4 columns each
+      // mode 2: bacc[i] = C[*][m = lane & 15]          -> lanes 0..15, register 0
+      const int Wtot = p.bias_mode == 1 ? p.Nc : Mtot;
+      const int tgi = p.bias_mode == 1 ? 0 : tg;
+      const int tgn = p.bias_mode == 1 ? 1 : p.tap_groups;
+      float* bs = p.bias_slab + ((size_t)split * tgn + tgi) * Wtot;
+      if (p.bias_mode == 1 && wm == 0 && (lane & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) *(f32x4*)(bs + n0 + wn * WN + j * 16 + (lane >> 4) * 4) = bacc[j];
+      }
+      if (p.bias_mode == 2 && wn == 0 && lane < 16) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) bs[m0 + wm * WM + i * 16 + lane] = bacc[i][0];
       }
     }
   }
@@ -271,7 +322,6 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
   }
 }
 
-// out[t][m][n] (m < Mout) = scale * sum_s slab[s][t][m][n]   (Mtot >= Mout rows in the slab)
 // Deterministic two-level reduction of the split-K slabs.
 // Stage 1 (grid x = float4 chunks of a slab row, grid y = groups of G splits):
 //   stage[y][i] = sum_{s in group y} slab[s][i]          (8 loads in flight per thread)
@@ -350,14 +400,33 @@ __global__ void __launch_bounds__(256) colsum_kernel(const bf16* __restrict__ x,
 template <int BM, int BN, int NTAP, int WAVES_M, int WAVES_N, bool SMALLC = false>
 hipError_t launch_wg(WgradParams p, hipStream_t s) {
   const int KT = p.KD * p.KH * p.KW;
+  for (int t = 0; t < 27; ++t) p.tap_d[t] = p.tap_h[t] = p.tap_w[t] = 0;
+  for (int t = 0; t < KT && t < 27; ++t) {
+    p.tap_w[t] = (signed char)(t % p.KW);
+    p.tap_h[t] = (signed char)((t / p.KW) % p.KH);
+    p.tap_d[t] = (signed char)(t / (p.KW * p.KH));
+  }
   const int Mtot = SMALLC ? (((KT * p.M1 + BM - 1) / BM) * BM) : (p.M1 + p.M2);
   p.tap_groups = SMALLC ? 1 : KT / NTAP;
   const int ntile = (Mtot / BM) * (p.Nc / BN) * p.tap_groups;
   const int grid = ntile * p.splits;
-  if (p.bias_mode)
-    hipLaunchKernelGGL((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, true>), dim3(grid), dim3(NTHR), 0, s, p);
-  else
-    hipLaunchKernelGGL((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, false>), dim3(grid), dim3(NTHR), 0, s, p);
+  auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
+  auto lg = [](int v) { int l = 0; while ((1 << l) < v) ++l; return l; };
+  const bool p2 = pow2(p.QW) && pow2(p.QH) && pow2(p.QD);
+  p.lqw = lg(p.QW);
+  p.lqh = lg(p.QH);
+  p.lqd = lg(p.QD);
+  if (p.bias_mode) {
+    if (p2)
+      hipLaunchKernelGGL((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, true, true>), dim3(grid), dim3(NTHR), 0, s, p);
+    else
+      hipLaunchKernelGGL((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, true, false>), dim3(grid), dim3(NTHR), 0, s, p);
+  } else {
+    if (p2)
+      hipLaunchKernelGGL((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, false, true>), dim3(grid), dim3(NTHR), 0, s, p);
+    else
+      hipLaunchKernelGGL((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, false, false>), dim3(grid), dim3(NTHR), 0, s, p);
+  }
   return hipGetLastError();
 }
 

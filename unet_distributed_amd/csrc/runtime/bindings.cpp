@@ -94,6 +94,7 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.mask_scale2 = get<float>(d, "mask_scale2", 1.f);
   p.shuffle = get<int>(d, "shuffle", 0);
   p.stats = (float*)getp(d, "stats");
+  p.tile = get<int>(d, "tile", 0);
   if (!p.src1 || !p.wgt || !p.dst1) throw std::invalid_argument("conv_fwd: src1/wgt/dst1 required");
   check_msg(conv_fwd_prepare(p));
   return p;

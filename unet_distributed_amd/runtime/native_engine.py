@@ -298,6 +298,10 @@ class NativeUNet:
                                               _ptr(self.prob), _ptr(part), _ptr(self.sums)],
                                  [P1, hc], [], "fwd:Mask")
 
+    @staticmethod
+    def _colsum_blocks(rows, C):
+        return max(1, min(512, rows // 256))
+
     def _wgrad_splits(self, M1, M2, Nc, KT, Q):
         BM, BN, NTAP, smallc = self.C.wgrad_pick(M1, M2, Nc, KT)
         Mtot = ((KT * M1 + BM - 1) // BM) * BM if smallc else M1 + M2
@@ -305,7 +309,7 @@ class NativeUNet:
         tiles = (Mtot // BM) * (Nc // BN) * tg
         # ~2 workgroups per CU: enough to fill 256 CUs, few enough that the fp32
         # split-K slabs stay small next to the GEMM's own operand traffic
-        splits = max(1, min(-(-self.wg_target // tiles), max(1, Q // (32 * 32))))
+        splits = max(1, min(-(-self.wg_target // tiles), max(1, Q // (64 * 16))))
         taps = 1 if smallc else KT
         return splits, Mtot, taps, tg, smallc
 
@@ -364,7 +368,7 @@ class NativeUNet:
                           b=_ptr(dy))
                 emit_wgrad(dict(lname=l.name, kd=kd, M1=c1, M2=c2, Nc=l.cout, KT=KT3, Q=Q,
                                 kernel=l.name + "/kernel", bias=l.name + "/bias", bias_mode=1,
-                                bias_width=l.cout,
+                                bias_width=l.cout, bias_src=(dy, Q),
                                 real_rows=(self.cpad, spec.in_channels) if first else None))
                 # --- data gradient
                 if not first:
@@ -412,7 +416,8 @@ class NativeUNet:
                           a1=_ptr(du), b=_ptr(b[src]))
                 emit_wgrad(dict(lname=l.name, kd=kd, M1=l.cout, M2=0, Nc=l.cin, KT=KT2,
                                 Q=self.npix(l.level + 1), kernel=l.name + "/kernel",
-                                bias=l.name + "/bias", bias_mode=2, bias_width=l.cout, real_rows=None))
+                                bias=l.name + "/bias", bias_mode=2, bias_width=l.cout, real_rows=None,
+                                bias_src=(du, self.npix(l.level))))
 
                 def mk(l=l, src=src, du=du):
                     d = self._conv_common(l.level + 1, 2, 2, 0, out_level=l.level + 1, in_level=l.level)
@@ -434,11 +439,14 @@ class NativeUNet:
             smax = max(smax, splits * taps * Mtot * w["Nc"])
             bw = w["bias_width"] if w["bias_mode"] == 1 else Mtot
             bmax = max(bmax, splits * tg * bw)
+            bmax = max(bmax, self._colsum_blocks(w["bias_src"][1], w["bias_width"]) * w["bias_width"])
         stmax = 1
         for w, (splits, Mtot, taps, tg, smallc) in zip(wg_specs, sized):
             stmax = max(stmax, self.C.wgrad_reduce_stage_floats(splits, taps, Mtot, w["Nc"]))
             bw = w["bias_width"] if w["bias_mode"] == 1 else Mtot
             stmax = max(stmax, self.C.wgrad_reduce_stage_floats(splits * tg, 1, 1, bw))
+            stmax = max(stmax, self.C.wgrad_reduce_stage_floats(
+                self._colsum_blocks(w["bias_src"][1], w["bias_width"]), 1, 1, w["bias_width"]))
         self.slab = torch.empty(smax, dtype=torch.float32, device=self.device)
         self.bias_slab = torch.empty(bmax, dtype=torch.float32, device=self.device)
         self.red_stage = torch.empty(stmax, dtype=torch.float32, device=self.device)
@@ -452,8 +460,13 @@ class NativeUNet:
                 w = wg_specs[op[1]]
                 splits, Mtot, taps, tg, smallc = sized[op[1]]
                 d = dict(w["kd"])
+                BM = self.C.wgrad_pick(w["M1"], w["M2"], w["Nc"], w["KT"])[0]
+                # the 128x128 tile has no register room for the fused ones-MFMA bias sums:
+                # those (level >= 3, small dY) use a separate column-sum pass instead
+                fused_bias = BM < 128
                 d.update(name="wgrad:" + w["lname"], M1=w["M1"], M2=w["M2"], Nc=w["Nc"], splits=splits,
-                         slab=_ptr(self.slab), bias_mode=w["bias_mode"], bias_slab=_ptr(self.bias_slab))
+                         slab=_ptr(self.slab), bias_mode=w["bias_mode"] if fused_bias else 0,
+                         bias_slab=_ptr(self.bias_slab))
                 plan.add_wgrad(d)
                 rr = w["real_rows"]
                 KT = w["KT"]
@@ -466,7 +479,15 @@ class NativeUNet:
                     plan.add_generic("wgrad_reduce", [_ptr(self.slab), self.grad_ptr(w["kernel"]), _ptr(self.red_stage)],
                                      [splits, taps, Mtot, Mtot, w["Nc"]], [1.0], "wred:" + w["lname"])
                 bw = w["bias_width"]
-                if w["bias_mode"] == 1:
+                if not fused_bias:
+                    src, rows = w["bias_src"]
+                    nb = self._colsum_blocks(rows, bw)
+                    plan.add_generic("colsum", [_ptr(src), _ptr(self.bias_slab)], [rows, bw, nb], [],
+                                     "bsum:" + w["lname"])
+                    plan.add_generic("wgrad_reduce", [_ptr(self.bias_slab), self.grad_ptr(w["bias"]),
+                                                      _ptr(self.red_stage)],
+                                     [nb, 1, 1, 1, bw], [1.0], "bred:" + w["lname"])
+                elif w["bias_mode"] == 1:
                     plan.add_generic("wgrad_reduce", [_ptr(self.bias_slab), self.grad_ptr(w["bias"]), _ptr(self.red_stage)],
                                      [splits, 1, 1, 1, bw], [1.0], "bred:" + w["lname"])
                 else:
