@@ -18,7 +18,7 @@ for r in rows:
     if i >= 0:
         n = n[n.rfind("::", 0, i) + 2: n.find(">", i) + 1]
     else:
-        n = n.split("(")[0].replace("unet::(anonymous namespace)::", "")[:70]
+        n = n.replace("unet::(anonymous namespace)::", "").split("(")[0][:70]
     pct = 100 * float(r["TotalDurationNs"]) / tot
     if pct < 0.1:
         continue
