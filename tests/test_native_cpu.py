@@ -1,0 +1,61 @@
+"""Native extension checks that need no GPU: the gfx950 build, the launch-plan
+construction of the executor (pointers only, no launches), host-side shape
+validation, bucket planning."""
+import pytest
+import torch
+
+from unet_distributed_amd import native
+from unet_distributed_amd.models.spec import UNetSpec
+from unet_distributed_amd.parallel.grad_sync import plan_buckets
+from unet_distributed_amd.runtime.params import FlatParams
+
+
+def test_extension_builds_and_imports():
+    native.build_if_needed()
+    C = native.require()
+    assert C.packseg_bytes() == 56
+    assert C.crc32c(b"123456789") == 0xE3069283
+
+
+@pytest.mark.parametrize("kw,img", [(dict(in_channels=4), 64), (dict(in_channels=1, use_upsampling=True), 64),
+                                    (dict(in_channels=4, dims=3), 32), (dict(in_channels=8), 64)])
+def test_plan_construction_dry_run(kw, img):
+    from unet_distributed_amd.runtime.native_engine import NativeUNet
+    spec = UNetSpec(**kw)
+    flat = FlatParams(spec)
+    b = plan_buckets(flat, 4.0)
+    e = NativeUNet(spec, flat, 2, img, "cpu", bucket_bounds=b, dry_run=True)
+    names = e.plan.names()
+    assert names[0] == "cast_input" and names[e.fwd_end - 1] == "fwd:Mask"
+    assert names[e.fwd_end] == "bwd:Mask"
+    # every parameter gradient is produced by exactly one reduce op
+    produced = [n for n in names if n.startswith(("wred:", "bred:")) or n == "bwd:Mask"]
+    assert len([n for n in names if n.startswith("wred:")]) == len(spec.param_layers()) - 1
+    assert e.seg_ends[-1] == e.plan.size() and sorted(e.seg_ends) == e.seg_ends
+    # dgrad of the first conv is never planned
+    assert "dgrad:conv1a" not in names
+
+
+def test_host_side_shape_validation_rejects_bad_shapes():
+    C = native.require()
+    base = dict(N=1, OH=8, OW=8, IH=8, IW=8, KH=3, KW=3, pad=1, src1=1, wgt=1, dst1=1, Cout=32)
+    with pytest.raises(ValueError):
+        C.conv_fwd(dict(base, C1=48), 0)            # Cin must be 32 / 64k
+    with pytest.raises(ValueError):
+        C.conv_fwd(dict(base, C1=32, Cout=40), 0)   # Cout % 32
+    with pytest.raises(ValueError):
+        C.wgrad(dict(N=1, QH=8, QW=8, AH=8, AW=8, KH=3, KW=3, M1=36, Nc=32, a1=1, b=1, slab=1), 0)
+    with pytest.raises(ValueError):
+        C.generic("pool_fwd", [1, 1], [1, 1, 8, 8, 12, 0], [], 0)
+
+
+def test_bucket_plan_is_layer_aligned_and_covers_buffer():
+    spec = UNetSpec()
+    flat = FlatParams(spec)
+    b = plan_buckets(flat, 8.0)
+    assert b[-1] == flat.numel and b == sorted(b)
+    starts = {off for _, _, off, _ in flat.entries}
+    for x in b[:-1]:
+        assert x in starts                          # cut at a variable boundary
+    # the exposed tail bucket (encoder grads, ready last) stays small
+    assert (flat.numel - b[-2]) * 4 / 2 ** 20 <= 8.0

@@ -70,6 +70,6 @@ def total_loss(t, logits, kind="dice", bce_weight=1.0):
 def sanity_dice(a, b):
     """The post-hoc check's Dice (`sanity_check_trained_model.py:30-35`):
     2*(sum(a*b) + 1) / (sum(a + b) + 1) -- a different smoothing."""
-    a = a.reshape(-1).double()
-    b = b.reshape(-1).double()
+    a = torch.as_tensor(a).reshape(-1).double()
+    b = torch.as_tensor(b).reshape(-1).double()
     return float(2.0 * ((a * b).sum() + 1.0) / ((a + b).sum() + 1.0))

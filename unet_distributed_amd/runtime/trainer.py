@@ -25,6 +25,7 @@ import torch
 
 from .. import settings
 from ..data import datasets
+from ..data.loader import BatchLoader
 from ..models import reference
 from ..models.spec import spec_from_config
 from ..ops import losses
@@ -114,17 +115,13 @@ class Trainer:
         self.sampler = datasets.EpochSampler(len(self.x_train), cfg.batch_size, self.rank, self.world, cfg.seed)
         self.num_batches = self.sampler.num_batches
         pin = self.device.type == "cuda"
-        self._stage_x = torch.empty((self.per_rank,) + self.x_train.shape[1:], dtype=torch.float32,
-                                    pin_memory=pin)
-        self._stage_y = torch.empty((self.per_rank,) + self.y_train.shape[1:], dtype=torch.float32,
-                                    pin_memory=pin)
+        self.loader = BatchLoader(np.ascontiguousarray(self.x_train, dtype=np.float32),
+                                  np.ascontiguousarray(self.y_train, dtype=np.float32),
+                                  self.per_rank, threads=min(cfg.num_threads, 16), pin=pin)
 
     def _batch(self, idx: np.ndarray):
-        idx = np.sort(idx)
-        self._stage_x.numpy()[...] = self.x_train[idx]
-        self._stage_y.numpy()[...] = self.y_train[idx]
-        return (self._stage_x.to(self.device, non_blocking=True),
-                self._stage_y.to(self.device, non_blocking=True))
+        bx, by = self.loader.gather(idx)
+        return bx.to(self.device, non_blocking=True), by.to(self.device, non_blocking=True)
 
     # ------------------------------------------------------------------ eval
     def evaluate(self) -> dict:

@@ -187,7 +187,9 @@ def write_bundle(prefix: str, tensors: Dict[str, np.ndarray]) -> None:
     with open(tmp_data, "wb") as f:
         off = 0
         for n in names:
-            a = np.ascontiguousarray(tensors[n])
+            a = np.asarray(tensors[n])          # (ascontiguousarray would promote 0-d to 1-d)
+            if not a.flags.c_contiguous:
+                a = a.copy()
             if a.dtype not in _DT:
                 raise TypeError("unsupported dtype %s for %s" % (a.dtype, n))
             raw = a.astype(a.dtype.newbyteorder("<"), copy=False).tobytes()
