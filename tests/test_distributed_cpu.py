@@ -111,3 +111,83 @@ def test_rank_failure_fails_fast(tmp_path):
                               "--dist_timeout_s", "60", "--no_checkpoint"], timeout=300)
     assert r.returncode != 0
     assert "fault injected" in r.stdout
+
+
+def test_parameter_server_applies_tf_adam_in_arrival_order():
+    sys.path.insert(0, ROOT)
+    from unet_distributed_amd.config import Config
+    from unet_distributed_amd.models import reference
+    from unet_distributed_amd.models.spec import spec_from_config
+    from unet_distributed_amd.parallel.async_ps import ParameterServer
+    from unet_distributed_amd.runtime.optim import TFAdam
+    from unet_distributed_amd.runtime.params import FlatParams
+    cfg = Config(img_size=32, in_channels=1, const_learningrate=False, decay_steps=3)
+    spec = spec_from_config(cfg)
+    a, b = FlatParams(spec), FlatParams(spec)
+    a.load_dict(reference.init_params(spec, seed=0))
+    b.master.copy_(a.master)
+    ps = ParameterServer(a, cfg)
+    opt = TFAdam(b, cfg)
+    out = torch.zeros_like(a.master)
+    g = torch.Generator().manual_seed(0)
+    for k in range(4):                         # four "workers'" gradients in arrival order
+        grad = torch.randn(a.numel, generator=g)
+        step = ps.apply(grad, out)
+        b.grad.copy_(grad)
+        opt.step()
+        assert step == b.global_step == k + 1
+    assert torch.allclose(out, b.master, atol=1e-7)
+    assert abs(ps.b1p - b.beta1_power) < 1e-12
+
+
+@pytest.mark.slow
+def test_async_ps_mode_two_ranks(tmp_path):
+    r = _run_train(tmp_path, ["--is_sync", "0", "--steps", "6", "--no_checkpoint"])
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert "Worker #1 reports job finished." in r.stdout
+    recs = [json.loads(l) for l in open(tmp_path / "m.jsonl")]
+    steps = [x["step"] for x in recs if x["kind"] == "train"]
+    assert len(steps) == 3 and steps[-1] <= 6           # 3 local steps; PS global_step advances per worker step
+    assert [x["step"] for x in recs if x["kind"] == "test_final"] == [6]   # PS global_step at the end
+
+
+def _run_launcher(tmp_path, extra, timeout=600):
+    port = _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, os.path.join(ROOT, "launch.py"), "--nproc_per_node", "2", "--master_port", str(port),
+           "--log_dir", str(tmp_path / "logs"), "--grace_s", "5", "--", os.path.join(ROOT, "train.py"),
+           "--synthetic", "--device", "cpu", "--dtype", "fp32", "--img_size", "32", "--in_channels", "4",
+           "--batch_size", "4", "--synthetic_train", "8", "--synthetic_test", "4",
+           "--checkpoint_dir", str(tmp_path / "ck"), "--no_checkpoint"] + extra
+    return subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                          timeout=timeout)
+
+
+@pytest.mark.slow
+def test_launcher_runs_ranks_and_stops_node_on_failure(tmp_path):
+    r = _run_launcher(tmp_path, ["--steps", "2"])
+    assert r.returncode == 0, r.stdout[-3000:]
+    log0 = open(tmp_path / "logs" / "training.rank0.log").read()
+    assert "Finished work on this node." in log0
+    assert os.path.exists(tmp_path / "logs" / "training.rank1.log")
+    # rank 1 dies at step 1 while rank 0 would block in the allreduce: the launcher
+    # must tear rank 0 down long before the 600 s collective timeout
+    import time
+    t0 = time.time()
+    r = _run_launcher(tmp_path, ["--steps", "50", "--fault_inject_step", "1", "--fault_inject_rank", "1"])
+    assert r.returncode != 0
+    assert time.time() - t0 < 120
+    assert "rank 1 exited" in r.stdout
+
+
+def test_inventory_roundtrip_and_remote_commands(tmp_path):
+    sys.path.insert(0, ROOT)
+    from unet_distributed_amd import launch
+    p = str(tmp_path / "inv.yml")
+    launch.write_inventory(p, ["10.0.0.1", "10.0.0.2"])
+    hosts = launch.read_inventory(p)
+    assert hosts == ["10.0.0.1", "10.0.0.2"]
+    cmds = launch.remote_commands(hosts, "/w", 8, 29500, ["train.py", "--epochs", "2"])
+    assert len(cmds) == 2 and "--node_rank 1" in cmds[1][-1] and "--master_addr 10.0.0.1" in cmds[1][-1]
+    env = launch.child_env({}, 9, 1, 16, 8, "10.0.0.1", 29500)
+    assert env["RANK"] == "9" and env["LOCAL_RANK"] == "1" and env["WORLD_SIZE"] == "16"

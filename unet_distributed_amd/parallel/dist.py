@@ -111,11 +111,14 @@ def allreduce_max_scalar(x: float, device=None) -> float:
     return float(t.item())
 
 
-def destroy():
-    """Orderly teardown (replaces the done-queue shutdown, test_dist.py:498-502)."""
+def destroy(orderly: bool = True):
+    """Teardown.  ``orderly``: barrier first (replaces the done-queue shutdown,
+    test_dist.py:498-502).  On an error path the barrier is skipped -- peers may
+    already be gone and waiting for them would turn a crash into a hang."""
     if _CTX.initialized and dist.is_initialized():
         try:
-            barrier()
+            if orderly:
+                barrier()
         finally:
             dist.destroy_process_group()
         _CTX.initialized = False

@@ -30,6 +30,7 @@ from ..models import reference
 from ..models.spec import spec_from_config
 from ..ops import losses
 from ..parallel import dist as D
+from ..parallel.async_ps import AsyncPS
 from ..parallel.grad_sync import GradSync, plan_buckets
 from ..utils import checkpoint as ckpt
 from ..utils.metrics import MetricLogger
@@ -73,6 +74,14 @@ class Trainer:
         if cfg.resume and self.is_chief and not cfg.no_checkpoint:
             self.restored = self.ckpt.restore_latest()
         self._broadcast_state()
+        # --is_sync=0: Hogwild updates through a parameter server (test_dist.py:264-267)
+        self.async_ps = None
+        if cfg.is_sync == 0 and self.world > 1:
+            engine = getattr(self.backend, "engine", None)
+            self.async_ps = AsyncPS(self.flat, cfg, self.ctx,
+                                    repack=engine.repack if engine is not None else None)
+        if self.async_ps is not None and self.is_chief:
+            self.ckpt.pre_save = self.async_ps.snapshot_into_flat
         self.sync = GradSync(self.flat, self.bounds, self.ctx, overlap=cfg.overlap_comm)
         native_opt = self.backend if hasattr(self.backend, "adam_step") else None
         self.opt = TFAdam(self.flat, cfg, native=_NativeOpt(native_opt) if native_opt else None)
@@ -145,6 +154,10 @@ class Trainer:
 
     # ------------------------------------------------------------------ step
     def train_step(self, x, y, seed: int) -> None:
+        if self.async_ps is not None:
+            self.backend.fwd_bwd(x, y, seed, on_segment=None)
+            self.async_ps.push_pull()
+            return
         self.backend.fwd_bwd(x, y, seed, on_segment=self.sync.on_segment)
         self.sync.finish()
         self.opt.step()
@@ -166,6 +179,12 @@ class Trainer:
         cfg = self.cfg
         total = cfg.steps if cfg.steps > 0 else self.num_batches * cfg.epochs
         step = self.flat.global_step
+        if self.async_ps is not None:
+            # async: the PS global_step advances once per WORKER step, so each rank
+            # runs its share of the remaining steps; the loop below then counts
+            # local iterations (identical on every rank -> collectives line up).
+            total = -(-(total - step) // self.world)
+            step = 0
         if self.is_chief:
             print("I am chief worker with task #0 (world size %d, backend %s, device %s)"
                   % (self.world, self.backend.name, self.device))
@@ -185,10 +204,11 @@ class Trainer:
             if cfg.fault_inject_step >= 0 and step == cfg.fault_inject_step and \
                     (cfg.fault_inject_rank < 0 or cfg.fault_inject_rank == self.rank):
                 raise FaultInjected("fault injected at step %d on rank %d" % (step, self.rank))
-            self.train_step(x, y, seed=cfg.seed * 1000003 + step)
-            step = self.flat.global_step
+            self.train_step(x, y, seed=cfg.seed * 1000003 + step * self.world + self.rank
+                            if self.async_ps is not None else cfg.seed * 1000003 + step)
+            step = self.async_ps.local_steps if self.async_ps is not None else self.flat.global_step
             imgs_since += cfg.batch_size
-            if cfg.check_sync_every and step % cfg.check_sync_every == 0:
+            if cfg.check_sync_every and step % cfg.check_sync_every == 0 and self.async_ps is None:
                 self.check_sync()
             if step % cfg.log_every == 0 or step == total:
                 if self.device.type == "cuda":
@@ -198,7 +218,7 @@ class Trainer:
                 m["images_per_sec"] = imgs_since / max(dt, 1e-9)
                 m["lr"] = learning_rate(cfg, step)
                 m["percent_complete"] = 100.0 * step / total
-                self.log.train(step, m, total)
+                self.log.train(self.flat.global_step, m, total)
                 last_metrics = m
                 t_last, imgs_since = time.time(), 0
             if step % self.num_batches == 0:
@@ -208,6 +228,13 @@ class Trainer:
                 if self.is_chief:
                     self.ckpt.save_last_good()
             self.ckpt.maybe_save()
+        if self.async_ps is not None:
+            self.async_ps.finish()              # done-queue: PS waits for every worker
+            D.barrier()
+            D.broadcast_(self.flat.master, 0)   # final PS weights to every replica
+            if hasattr(self.backend, "engine"):
+                self.backend.engine.repack()
+            step = self.flat.global_step
         final = self.evaluate()
         self.log.test(step, final, step // max(self.num_batches, 1), cfg.epochs, final=True)
         if self.is_chief:
@@ -235,8 +262,10 @@ def main(argv=None) -> int:
     tr = Trainer(cfg)
     try:
         tr.run()
-    finally:
-        D.destroy()
+    except BaseException:
+        D.destroy(orderly=False)
+        raise
+    D.destroy()
     if tr.is_chief:
         print("\n\nFinished work on this node.")
     return 0

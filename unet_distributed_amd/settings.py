@@ -60,6 +60,8 @@ PS_HOSTS = []
 PS_PORTS = []
 WORKER_HOSTS = ["127.0.0.1"]
 WORKER_PORTS = ["29500"]
+GPUS_PER_NODE = int(os.environ.get("UNET_GPUS_PER_NODE", "8"))   # MI355X node: 8 GPUs on xGMI
+MASTER_PORT = 29500
 
 CHECKPOINT_DIRECTORY = os.environ.get(
     "UNET_CHECKPOINT_DIRECTORY", os.path.join(os.getcwd(), "checkpoints"))

@@ -85,6 +85,7 @@ class CheckpointManager:
         self.logdir = logdir_name(cfg)
         self.max_to_keep = max_to_keep
         self.last_save = time.time()
+        self.pre_save = None
         self.extra_state = extra_state or {}
         if is_chief and not cfg.no_checkpoint:
             os.makedirs(self.logdir, exist_ok=True)
@@ -100,6 +101,8 @@ class CheckpointManager:
     def save(self) -> Optional[str]:
         if self.cfg.no_checkpoint or not self.is_chief:
             return None
+        if self.pre_save is not None:
+            self.pre_save()                 # e.g. async PS: pull server state into flat
         step = self.flat.global_step
         prefix = os.path.join(self.logdir, "model.ckpt-%d" % step)
         tf_bundle.write_bundle(prefix, flat_to_tensors(self.flat, extra_state=self.extra_state))
