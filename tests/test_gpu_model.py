@@ -83,3 +83,30 @@ def test_native_training_reduces_loss(cuda_dev):
         s = nb.sums().cpu()
         losses.append((-torch.log(2 * s[0] + 1) + torch.log(s[1] + s[2] + 1)).item())
     assert losses[-1] < 0.7 * losses[0], losses
+
+
+def test_native_inference_export_roundtrip(cuda_dev, tmp_path):
+    """export -> load_saved_model on the GPU runs the native eval plan; probabilities
+    match the fp32 reference forward (dropout off), short tail batch padded."""
+    import numpy as np
+    from unet_distributed_amd.config import Config
+    from unet_distributed_amd.data.datasets import synthetic_brats
+    from unet_distributed_amd.inference import load_saved_model
+    from unet_distributed_amd.models import reference
+    from unet_distributed_amd.models.spec import spec_from_config
+    from unet_distributed_amd.runtime.params import FlatParams
+    from unet_distributed_amd.utils.checkpoint import export_model
+    cfg = Config(img_size=64, in_channels=4, checkpoint_dir=str(tmp_path))
+    spec = spec_from_config(cfg)
+    flat = FlatParams(spec)
+    flat.load_dict(reference.init_params(spec, seed=3))
+    d = export_model(cfg, spec, flat)
+    model = load_saved_model(d, device=cuda_dev, batch=4)
+    assert model.name == "native"
+    x, _ = synthetic_brats(6, 64, 4, seed=2)
+    p = model.predict(x)
+    with torch.no_grad():
+        ref = reference.forward(spec, {k: v.to(cuda_dev) for k, v in flat.params().items()},
+                                torch.from_numpy(x).to(cuda_dev), train=False, dropout=False).cpu().numpy()
+    assert p.shape == ref.shape
+    assert np.abs(p - ref).max() < 0.05, np.abs(p - ref).max()

@@ -1,0 +1,99 @@
+"""Inference on an exported model (the reference's ``tf.saved_model.loader``
+flow, `sanity_check_trained_model.py:38-44`).
+
+:func:`load_saved_model` reads ``saved_model/saved_model.json`` (architecture +
+signature) and ``saved_model/variables/variables.{index,data-*}`` (TF bundle)
+written by :func:`utils.checkpoint.export_model`, and returns a
+:class:`Predictor` whose ``predict(x)`` maps NHWC(/NDHWC) float images to
+sigmoid probabilities -- the ``Placeholder:0 -> Mask/Sigmoid:0`` signature.
+
+On a GPU the native HIP executor's inference plan runs (forward only, dropout
+off, fused head+sigmoid) at a fixed micro-batch; a short last batch is padded.
+Elsewhere, or for configs the native executor does not cover, the ATen
+reference forward runs.
+"""
+
+import json
+import os
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .models.spec import UNetSpec
+from .runtime.params import FlatParams
+from .utils import tf_bundle
+from .utils.checkpoint import tensors_to_flat
+
+
+class _Cfg:
+    """Minimal config for the backends (inference needs no optimiser flags)."""
+
+    def __init__(self, img_size, dtype, eval_dropout=False):
+        self.img_size = img_size
+        self.dtype = dtype
+        self.loss = "dice"
+        self.bce_weight = 1.0
+        self.eval_dropout = eval_dropout
+        self.backend = "auto"
+
+
+class Predictor:
+    def __init__(self, spec: UNetSpec, flat: FlatParams, img_size: int, device, batch: int,
+                 dtype: str = "bf16", backend: str = "auto", state=None):
+        from .runtime.backends import NativeBackend, TorchBackend, native_supported
+        self.spec, self.flat, self.batch, self.img_size = spec, flat, batch, img_size
+        self.device = torch.device(device)
+        cfg = _Cfg(img_size, dtype if self.device.type == "cuda" else "fp32")
+        reason = native_supported(spec, cfg, self.device)
+        if backend == "native" or (backend == "auto" and reason is None):
+            if reason is not None:
+                raise RuntimeError("native inference unsupported: " + reason)
+            from . import native
+            native.require()
+            self.backend = NativeBackend(spec, flat, cfg, self.device, batch)
+            self.backend.engine.repack()
+        else:
+            self.backend = TorchBackend(spec, flat, cfg, self.device, batch)
+            for k, v in (state or {}).items():
+                if k in self.backend.state:
+                    self.backend.state[k].copy_(torch.as_tensor(v))
+        self.name = self.backend.name
+
+    @torch.no_grad()
+    def predict(self, x) -> np.ndarray:
+        """Probabilities for a batch of any length (native: chunks of ``batch``)."""
+        x = torch.as_tensor(np.ascontiguousarray(x, dtype=np.float32))
+        n = x.shape[0]
+        if self.backend.name != "native":
+            return self.backend.predict(x.to(self.device)).float().cpu().numpy()
+        outs = []
+        for s in range(0, n, self.batch):
+            xb = x[s:s + self.batch]
+            m = xb.shape[0]
+            if m < self.batch:
+                xb = torch.cat([xb, xb.new_zeros((self.batch - m,) + tuple(xb.shape[1:]))])
+            p = self.backend.predict(xb.to(self.device))
+            outs.append(p[:m].float().cpu())
+        return torch.cat(outs).numpy()
+
+
+def load_saved_model(export_dir: str, device=None, batch: int = 128, dtype: str = "bf16",
+                     backend: str = "auto") -> Predictor:
+    with open(os.path.join(export_dir, "saved_model.json")) as f:
+        meta = json.load(f)
+    if "serve" not in meta.get("tags", []):
+        raise ValueError("export in %s has no 'serve' tag" % export_dir)
+    m = meta["model"]
+    spec = UNetSpec(in_channels=m["in_channels"], n_cl_out=m["n_cl_out"], base=m["base"], depth=m["depth"],
+                    use_upsampling=m["use_upsampling"], dims=m["dims"], dropout=m["dropout"],
+                    norm=m.get("norm", "none"), groups=m.get("groups", 8))
+    sig = next(iter(meta["signature_def"].values()))
+    img_size = meta.get("img_size") or sig["inputs"]["image"]["shape"][1]
+    if device is None:
+        device = "cuda:0" if torch.cuda.is_available() else "cpu"
+    flat = FlatParams(spec, device=device)
+    tensors = tf_bundle.read_bundle(os.path.join(export_dir, "variables", "variables"))
+    tensors_to_flat(flat, tensors, strict=True)
+    state = {k: v for k, v in tensors.items() if k.endswith("moving_mean") or k.endswith("moving_variance")}
+    return Predictor(spec, flat, int(img_size), device, batch, dtype=dtype, backend=backend, state=state)

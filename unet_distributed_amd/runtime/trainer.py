@@ -240,7 +240,8 @@ class Trainer:
         if self.is_chief:
             self.ckpt.save(); self.ckpt.save_last_good()
             if cfg.export:
-                d = ckpt.export_model(cfg, self.spec, self.flat)
+                d = ckpt.export_model(cfg, self.spec, self.flat,
+                                         extra_state=getattr(self.backend, "state", None))
                 print("Saved final model to directory: {}".format(d))
         self.log.close()
         return {"train": last_metrics, "test": final, "global_step": step}

@@ -145,12 +145,13 @@ class CheckpointManager:
         return True
 
 
-def export_model(cfg, spec, flat, directory: Optional[str] = None) -> str:
-    """SavedModel-style export (C19): weights bundle + graph/signature description."""
+def export_model(cfg, spec, flat, directory: Optional[str] = None, extra_state=None) -> str:
+    """SavedModel-style export (C19): weights bundle + graph/signature description.
+    ``extra_state``: non-trainable inference state (BatchNorm moving statistics)."""
     d = directory or os.path.join(cfg.checkpoint_dir, "saved_model")
     os.makedirs(os.path.join(d, "variables"), exist_ok=True)
     tf_bundle.write_bundle(os.path.join(d, "variables", "variables"),
-                           flat_to_tensors(flat, include_optimizer=False))
+                           flat_to_tensors(flat, include_optimizer=False, extra_state=extra_state))
     meta = {
         "tags": ["serve"],
         "signature_def": {"intel_unet_brats_model": {
@@ -159,6 +160,7 @@ def export_model(cfg, spec, flat, directory: Optional[str] = None) -> str:
             "outputs": {"prediction": {"name": "Mask/Sigmoid:0", "dtype": "float32",
                                        "shape": [-1] + [cfg.img_size] * spec.dims + [spec.n_cl_out]}},
             "method_name": "tensorflow/serving/predict"}},
+        "img_size": cfg.img_size,
         "model": {"in_channels": spec.in_channels, "n_cl_out": spec.n_cl_out, "base": spec.base,
                   "depth": spec.depth, "use_upsampling": spec.use_upsampling, "dims": spec.dims,
                   "dropout": spec.dropout, "norm": spec.norm, "groups": spec.groups},
