@@ -70,6 +70,7 @@ class Config:
     synthetic: bool = False
     synthetic_train: int = 2048
     synthetic_test: int = 256
+    data_on_device: str = "auto"     # auto | on | off: keep the train set resident in HBM
     data_path: str = settings.OUT_PATH
     steps: int = 0                   # >0 overrides epochs*num_batches
     seed: int = 816
@@ -92,7 +93,9 @@ class Config:
     fault_inject_step: int = -1
     fault_inject_rank: int = -1
     check_sync_every: int = 0        # cross-rank parameter checksum every K steps
-    deterministic: bool = False
+    deterministic: bool = False      # torch path: deterministic algorithms (native path always is)
+    serialize_kernels: bool = False  # debug: AMD_SERIALIZE_KERNEL=3 + HIP_LAUNCH_BLOCKING=1
+    launch_tensorboard: bool = False # start `tensorboard --logdir` on the chief if installed
     hip_graph: bool = False
     progress: bool = True
     loss_scale: float = 0.0          # fp16 static loss scale (0 = dynamic)
@@ -115,6 +118,7 @@ _CHOICES = {
     "backend": ("auto", "native", "torch"),
     "device": ("auto", "cuda", "cpu"),
     "dist_backend": ("auto", "nccl", "gloo"),
+    "data_on_device": ("auto", "on", "off"),
 }
 
 

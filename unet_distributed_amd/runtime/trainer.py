@@ -25,7 +25,7 @@ import torch
 
 from .. import settings
 from ..data import datasets
-from ..data.loader import BatchLoader
+from ..data.loader import DeviceFeeder
 from ..models import reference
 from ..models.spec import spec_from_config
 from ..ops import losses
@@ -41,6 +41,62 @@ from .params import FlatParams
 
 class FaultInjected(RuntimeError):
     pass
+
+
+class _Ranges:
+    """roctx ranges (torch.cuda.nvtx is backed by roctx on ROCm builds) plus
+    torch.profiler record_function labels, so rocprofv3 --marker-trace and the
+    Chrome trace both show forward_backward / grad_sync / optimizer."""
+
+    def __init__(self, on: bool):
+        self.on = on
+
+    class _R:
+        def __init__(self, name, on):
+            self.name, self.on, self.rf = name, on, None
+
+        def __enter__(self):
+            if self.on:
+                try:
+                    torch.cuda.nvtx.range_push(self.name)
+                except Exception:
+                    pass
+                self.rf = torch.autograd.profiler.record_function(self.name)
+                self.rf.__enter__()
+
+        def __exit__(self, *a):
+            if self.on:
+                self.rf.__exit__(*a)
+                try:
+                    torch.cuda.nvtx.range_pop()
+                except Exception:
+                    pass
+
+    def __call__(self, name):
+        return self._R(name, self.on)
+
+
+def _make_profiler(cfg, rank, logdir):
+    """--profile: torch.profiler (roctracer-backed HIP kernel trace) over local
+    steps [a, b) of --profile_steps a,b; Chrome trace per rank in logdir/profile."""
+    a, b = [int(v) for v in cfg.profile_steps.split(",")]
+    out = os.path.join(logdir, "profile")
+    os.makedirs(out, exist_ok=True)
+
+    def ready(prof):
+        path = os.path.join(out, "trace_rank%d.json" % rank)
+        prof.export_chrome_trace(path)
+        if rank == 0:
+            print("profiler: wrote %s" % path, flush=True)
+            print(prof.key_averages().table(sort_by="self_device_time_total", row_limit=25), flush=True)
+
+    acts = [torch.profiler.ProfilerActivity.CPU]
+    if torch.cuda.is_available():
+        acts.append(torch.profiler.ProfilerActivity.CUDA)
+    return torch.profiler.profile(activities=acts,
+                                  schedule=torch.profiler.schedule(wait=max(a - 1, 0), warmup=1 if a > 0 else 0,
+                                                                   active=max(b - a, 1), repeat=1),
+                                  on_trace_ready=ready)
 
 
 def metrics_from_sums(s: torch.Tensor, npix: int, cfg) -> dict:
@@ -86,6 +142,16 @@ class Trainer:
         native_opt = self.backend if hasattr(self.backend, "adam_step") else None
         self.opt = TFAdam(self.flat, cfg, native=_NativeOpt(native_opt) if native_opt else None)
         self.log = MetricLogger(cfg, self.is_chief, self.ckpt.logdir)
+        self.ranges = _Ranges(cfg.profile)
+        self.tb_proc = None
+        if cfg.launch_tensorboard and self.is_chief:
+            import shutil
+            import subprocess
+            exe = shutil.which("tensorboard")
+            if exe:     # test_dist.py:375-378
+                self.tb_proc = subprocess.Popen([exe, "--logdir", self.ckpt.logdir])
+            else:
+                print("tensorboard is not installed; event files are in %s" % self.ckpt.logdir)
         self._load_data()
 
     # ------------------------------------------------------------------ setup
@@ -123,14 +189,14 @@ class Trainer:
             print("Testing masks shape:   {}".format(self.y_test.shape))
         self.sampler = datasets.EpochSampler(len(self.x_train), cfg.batch_size, self.rank, self.world, cfg.seed)
         self.num_batches = self.sampler.num_batches
-        pin = self.device.type == "cuda"
-        self.loader = BatchLoader(np.ascontiguousarray(self.x_train, dtype=np.float32),
-                                  np.ascontiguousarray(self.y_train, dtype=np.float32),
-                                  self.per_rank, threads=min(cfg.num_threads, 16), pin=pin)
+        self.feeder = DeviceFeeder(self.x_train, self.y_train, self.per_rank, self.device,
+                                   threads=min(cfg.num_threads, 16), mode=cfg.data_on_device)
+        if self.is_chief:
+            print("Training data: %s" % ("resident in device memory" if self.feeder.resident
+                                         else "streamed from host (pinned, double-buffered)"))
 
     def _batch(self, idx: np.ndarray):
-        bx, by = self.loader.gather(idx)
-        return bx.to(self.device, non_blocking=True), by.to(self.device, non_blocking=True)
+        return self.feeder.get(idx)
 
     # ------------------------------------------------------------------ eval
     def evaluate(self) -> dict:
@@ -154,13 +220,19 @@ class Trainer:
 
     # ------------------------------------------------------------------ step
     def train_step(self, x, y, seed: int) -> None:
+        R = self.ranges
         if self.async_ps is not None:
-            self.backend.fwd_bwd(x, y, seed, on_segment=None)
-            self.async_ps.push_pull()
+            with R("forward_backward"):
+                self.backend.fwd_bwd(x, y, seed, on_segment=None)
+            with R("ps_push_pull"):
+                self.async_ps.push_pull()
             return
-        self.backend.fwd_bwd(x, y, seed, on_segment=self.sync.on_segment)
-        self.sync.finish()
-        self.opt.step()
+        with R("forward_backward"):
+            self.backend.fwd_bwd(x, y, seed, on_segment=self.sync.on_segment)
+        with R("grad_sync"):
+            self.sync.finish()
+        with R("optimizer"):
+            self.opt.step()
 
     def check_sync(self):
         """Cross-rank parameter checksum (detects DP divergence)."""
@@ -195,6 +267,9 @@ class Trainer:
         t_last = time.time()
         imgs_since = 0
         last_metrics = {}
+        prof = _make_profiler(cfg, self.rank, self.ckpt.logdir) if cfg.profile else None
+        if prof is not None:
+            prof.start()
         while step < total:
             batch_idx = step % self.num_batches
             if batch_idx == 0 and step // self.num_batches != epoch:
@@ -206,6 +281,8 @@ class Trainer:
                 raise FaultInjected("fault injected at step %d on rank %d" % (step, self.rank))
             self.train_step(x, y, seed=cfg.seed * 1000003 + step * self.world + self.rank
                             if self.async_ps is not None else cfg.seed * 1000003 + step)
+            if prof is not None:
+                prof.step()
             step = self.async_ps.local_steps if self.async_ps is not None else self.flat.global_step
             imgs_since += cfg.batch_size
             if cfg.check_sync_every and step % cfg.check_sync_every == 0 and self.async_ps is None:
@@ -228,6 +305,8 @@ class Trainer:
                 if self.is_chief:
                     self.ckpt.save_last_good()
             self.ckpt.maybe_save()
+        if prof is not None:
+            prof.stop()
         if self.async_ps is not None:
             self.async_ps.finish()              # done-queue: PS waits for every worker
             D.barrier()
@@ -244,6 +323,8 @@ class Trainer:
                                          extra_state=getattr(self.backend, "state", None))
                 print("Saved final model to directory: {}".format(d))
         self.log.close()
+        if self.tb_proc is not None:
+            self.tb_proc.terminate()            # test_dist.py:496
         return {"train": last_metrics, "test": final, "global_step": step}
 
 
@@ -258,6 +339,11 @@ class _NativeOpt:
 def main(argv=None) -> int:
     from ..config import parse_args
     cfg = parse_args(argv)
+    if cfg.serialize_kernels:       # must precede the first HIP call
+        os.environ["AMD_SERIALIZE_KERNEL"] = "3"
+        os.environ["HIP_LAUNCH_BLOCKING"] = "1"
+    if cfg.deterministic:
+        torch.use_deterministic_algorithms(True, warn_only=True)
     for k in ("http_proxy", "https_proxy"):
         os.environ.pop(k, None)                 # Q5: the reference del's these unconditionally
     tr = Trainer(cfg)
