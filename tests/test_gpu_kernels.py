@@ -121,6 +121,50 @@ def test_conv_dgrad_dual_dest_mask(cuda_dev):
     assert rel_err(d2, ref2) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,C1,C2,Cout,tile", [
+    (2, 128, 32, 0, 32, 6), (3, 128, 32, 32, 32, 6), (2, 64, 64, 0, 64, 6), (3, 64, 64, 64, 64, 6),
+    (2, 64, 32, 0, 64, 6), (3, 16, 32, 0, 32, 6), (5, 16, 64, 0, 64, 6), (3, 32, 128, 0, 32, 6),
+    (1, 128, 32, 0, 64, 0), (2, 64, 64, 64, 64, 0), (2, 32, 64, 0, 128, 8)])
+def test_conv_row_window(cuda_dev, N, H, C1, C2, Cout, tile):
+    """Row-window kernel (tile 6, auto for 16 <= W <= 128): image boundaries inside a window,
+    row tails (N*H not a multiple of the window), concat sources, bias + ReLU + dropout."""
+    torch.manual_seed(N * 100 + H + C1 + C2)
+    a = torch.randn(N, H, H, C1, device=cuda_dev).bfloat16()
+    b2 = torch.randn(N, H, H, max(C2, 1), device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, C1 + C2, Cout, device=cuda_dev) * 0.08).bfloat16()
+    bias = torch.randn(Cout, device=cuda_dev) * 0.1
+    out = torch.empty(N, H, H, Cout, device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=C1, C2=C2, src1=ptr(a),
+                      src2=ptr(b2) if C2 else None, wgt=ptr(pack_fwd(w)), bias=ptr(bias), Cout=Cout, relu=1,
+                      dst1=ptr(out), tile=tile), stream())
+    xin = nchw(a.float()) if not C2 else torch.cat([nchw(a.float()), nchw(b2.float())], 1)
+    ref = nhwc(F.relu(F.conv2d(xin, w.float().permute(3, 2, 0, 1), bias, padding=1)))
+    assert rel_err(out, ref) < 1e-2
+
+
+def test_conv_row_window_dgrad_dual_dest_mask_dropout(cuda_dev):
+    """The row-window kernel as a concat dgrad (flipped weights, two destinations,
+    ReLU mask + dropout rescale) at the 128-wide level."""
+    torch.manual_seed(22)
+    N, H, C1, C2, Co = 2, 128, 32, 32, 32
+    skip = F.relu(torch.randn(N, H, H, C2, device=cuda_dev)).bfloat16()
+    m1 = torch.randn(N, H, H, C1, device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, C1 + C2, Co, device=cuda_dev) * 0.1).bfloat16()
+    dy = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
+    d1 = torch.empty(N, H, H, C1, device=cuda_dev, dtype=torch.bfloat16)
+    d2 = torch.empty(N, H, H, C2, device=cuda_dev, dtype=torch.bfloat16)
+    for tile in (6, 8):
+        C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Co, src1=ptr(dy),
+                          wgt=ptr(pack_dgrad(w)), Cout=C1 + C2, D1=C1, dst1=ptr(d1), dst2=ptr(d2),
+                          mask1=ptr(m1), mask2=ptr(skip), mask_scale2=1.25, tile=tile), stream())
+        xr = torch.zeros(N, C1 + C2, H, H, device=cuda_dev, requires_grad=True)
+        y = F.conv2d(xr, w.float().permute(3, 2, 0, 1), padding=1)
+        (g,) = torch.autograd.grad(y, xr, nchw(dy.float()))
+        g = nhwc(g)
+        assert rel_err(d1, g[..., :C1] * (m1.float() > 0)) < 1e-2
+        assert rel_err(d2, g[..., C1:] * (skip.float() > 0) * 1.25) < 1e-2
+
+
 def test_conv_first_layer_smallc(cuda_dev):
     torch.manual_seed(3)
     N, H, Cin, Co = 2, 32, 4, 32

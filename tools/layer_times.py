@@ -1,0 +1,120 @@
+"""Per-launch timing of the native training step (one HIP event pair per plan
+entry, each entry replayed ``--reps`` times in isolation) with achieved
+TFLOP/s for the conv / wgrad GEMMs.  Usage on the GPU box:
+
+    PYTHONPATH=. python tools/layer_times.py --batch 256 --img 128 --out profiles/layer_times.md
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from unet_distributed_amd.config import Config  # noqa: E402
+from unet_distributed_amd.data.datasets import synthetic_brats  # noqa: E402
+from unet_distributed_amd.models import reference  # noqa: E402
+from unet_distributed_amd.models.spec import spec_from_config  # noqa: E402
+from unet_distributed_amd.runtime.native_engine import NativeUNet  # noqa: E402
+from unet_distributed_amd.runtime.params import FlatParams  # noqa: E402
+
+
+def layer_flops(spec, B, img, dims):
+    """GEMM FLOPs per plan-entry name (fwd:, dgrad:, wgrad:)."""
+    out = {}
+    for l in spec.layers:
+        s = img >> (l.level - 1)
+        pix = B * s ** dims
+        if l.kind == "conv":
+            f = 2.0 * pix * l.cout * l.cin * 3 ** dims
+            out["fwd:" + l.name] = f
+            out["wgrad:" + l.name] = f
+            if l.level > 1 or l.skip_from is not None or l.cin > 8:
+                out["dgrad:" + l.name] = f
+        elif l.kind == "tconv":
+            f = 2.0 * pix * l.cout * l.cin      # pix at the output (finer) level... see below
+            s2 = img >> l.level
+            f = 2.0 * B * s2 ** dims * l.cin * l.cout * 2 ** dims
+            out["fwd:" + l.name] = f
+            out["wgrad:" + l.name] = f
+            out["dgrad:" + l.name] = f
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--img", type=int, default=128)
+    ap.add_argument("--in_channels", type=int, default=4)
+    ap.add_argument("--dims", type=int, default=2)
+    ap.add_argument("--upsampling", action="store_true")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    cfg = Config(batch_size=a.batch, img_size=a.img, in_channels=a.in_channels, dims=a.dims,
+                 use_upsampling=a.upsampling)
+    spec = spec_from_config(cfg)
+    flat = FlatParams(spec, device=dev)
+    flat.load_dict(reference.init_params(spec, seed=1))
+    e = NativeUNet(spec, flat, a.batch, a.img, dev)
+    x, y = synthetic_brats(min(a.batch, 64), a.img, a.in_channels, a.dims, seed=0)
+    reps = (a.batch + 63) // 64
+    x = torch.from_numpy(x).repeat((reps,) + (1,) * (x.ndim - 1))[:a.batch].to(dev)
+    y = torch.from_numpy(y).repeat((reps,) + (1,) * (y.ndim - 1))[:a.batch].to(dev)
+    e.load_batch(x, y)
+    for _ in range(3):
+        e.forward(1)
+        e.backward()
+    torch.cuda.synchronize()
+    names = e.plan.names()
+    fl = layer_flops(spec, a.batch, a.img, a.dims)
+    s = torch.cuda.current_stream().cuda_stream
+    rows = []
+    total = 0.0
+    for i, n in enumerate(names):
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e.plan.run(i, i + 1, s)
+        st.record()
+        for _ in range(a.reps):
+            e.plan.run(i, i + 1, s)
+        en.record()
+        torch.cuda.synchronize()
+        ms = st.elapsed_time(en) / a.reps
+        total += ms
+        f = fl.get(n)
+        rows.append((i, n, ms, f / ms / 1e9 if f else None))
+    # whole step for comparison
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(a.reps):
+        e.forward(1)
+        e.backward()
+    en.record()
+    torch.cuda.synchronize()
+    step = st.elapsed_time(en) / a.reps
+    lines = ["# Per-launch times, native step, %dD UNet %dx%d in_ch=%d, batch %d (1x MI355X)" %
+             (a.dims, a.img, a.img, a.in_channels, a.batch), "",
+             "sum of isolated launches %.3f ms; back-to-back step %.3f ms (%.0f img/s fwd+bwd only)"
+             % (total, step, a.batch / step * 1e3), "",
+             "| # | launch | ms | TFLOP/s |", "|---|---|---|---|"]
+    for i, n, ms, tf in rows:
+        lines.append("| %d | `%s` | %.4f | %s |" % (i, n, ms, "%.0f" % tf if tf else ""))
+    # per-kind rollup
+    kinds = {}
+    for _, n, ms, _ in rows:
+        k = n.split(":")[0]
+        kinds[k] = kinds.get(k, 0.0) + ms
+    lines += ["", "| kind | ms | % |", "|---|---|---|"]
+    for k, v in sorted(kinds.items(), key=lambda kv: -kv[1]):
+        lines.append("| %s | %.3f | %.1f |" % (k, v, 100 * v / total))
+    txt = "\n".join(lines)
+    print(txt)
+    if a.out:
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        open(a.out, "w").write(txt + "\n")
+
+
+if __name__ == "__main__":
+    main()

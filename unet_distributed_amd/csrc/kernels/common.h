@@ -36,10 +36,13 @@ __device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
   }
 }
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// one v_cvt_pk_bf16_f32 (round-to-nearest-even) for two values
 __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
-  bf16 x = (bf16)a, y = (bf16)b;
-  return (uint32_t)__builtin_bit_cast(uint16_t, x) |
-         ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+  const f32x2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
 }
 
 __device__ __forceinline__ u32x4 pack8(const float* f) {

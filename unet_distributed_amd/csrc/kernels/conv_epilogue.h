@@ -1,0 +1,182 @@
+// Shared epilogue of the implicit-GEMM conv kernels (conv_fwd.hip, conv_win.hip).
+//
+// Input: the MFMA accumulators of a BM x BN output tile issued as W x X^T, i.e.
+//   acc[i][j][r] = out[pixel = m0 + wm*WM + i*16 + (lane&15)]
+//                     [chan  = n0 + wn*WN + j*16 + (lane>>4)*4 + r].
+// Register phase: scale, bias, ReLU, inverted dropout (counter hash), BN statistics,
+// channel-split mask scale; packed to bf16 into an LDS staging tile.  Coalesced
+// phase: 16-byte chunks per thread to one of two destinations (concat dgrad),
+// optional consumer-side ReLU mask (out *= mask > 0) and transposed-conv pixel shuffle.
+#pragma once
+#include "common.h"
+#include "conv_params.h"
+
+namespace unet {
+
+struct PixCoord {
+  int n, d, h, w;
+};
+
+__device__ __forceinline__ PixCoord decompose(int q, int OD, int OH, int OW) {
+  PixCoord c;
+  c.w = q % OW;
+  int t = q / OW;
+  c.h = t % OH;
+  t /= OH;
+  c.d = t % OD;
+  c.n = t / OD;
+  return c;
+}
+
+// EPI selects a specialised epilogue (launch-time choice, conv_epi_mode below):
+//   0 generic (every feature read from p at run time), 1 forward (bias + ReLU only),
+//   2 data gradient (mask scales, consumer ReLU masks, optional channel split).
+enum { EPI_GENERIC = 0, EPI_FWD = 1, EPI_DGRAD = 2 };
+
+__host__ __device__ inline int conv_epi_mode(const ConvFwdParams& p) {
+  if (p.stats || p.shuffle || p.drop_rate > 0.f || p.out_scale != 1.f) return EPI_GENERIC;
+  if (p.relu && p.D1 == p.Cout && !p.mask1 && !p.mask2 && p.mask_scale1 == 1.f) return EPI_FWD;
+  if (!p.relu && !p.bias) return EPI_DGRAD;
+  return EPI_GENERIC;
+}
+
+template <int BM, int BN, int WM, int WN, int TM, int TN, int NTHR, int EPI = EPI_GENERIC>
+__device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc)[TM][TN], char* smem,
+                                              const int m0, const int n0, const int M, const int wm,
+                                              const int wn, const int lane, const int tid) {
+  constexpr int EPI_STRIDE = (BN + 4) * 2;          // bytes; 8B-aligned, conflict-free b64 writes
+  // register phase: acc[i][j][r] = out[pixel = m0 + wm*WM + i*16 + (lane&15)]
+  //                                   [chan  = n0 + wn*WN + j*16 + (lane>>4)*4 + r]
+  char* E = smem;
+  constexpr bool G = EPI == EPI_GENERIC;
+  const bool kRelu = G ? (p.relu != 0) : (EPI == EPI_FWD);
+  const bool kBias = EPI != EPI_DGRAD && p.bias;
+  const bool kDrop = G && p.drop_rate > 0.f;
+  const bool kStats = G && p.stats;
+  const bool kShuffle = G && p.shuffle;
+  constexpr bool kMaskScale = EPI != EPI_FWD;
+  const float inv_keep = p.drop_rate > 0.f ? 1.f / (1.f - p.drop_rate) : 1.f;
+  const uint32_t drop_thr = (uint32_t)(p.drop_rate * 4294967296.0);
+  const int Dtb = kShuffle ? (p.Cout >> p.shuffle) : p.Cout;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int nl = wn * WN + j * 16 + (lane >> 4) * 4;
+    const int n = n0 + nl;
+    float bsv[4], msc[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bsv[r] = kBias ? p.bias[kShuffle ? (n + r) % Dtb : n + r] : 0.f;
+      msc[r] = kMaskScale ? ((n + r < p.D1) ? p.mask_scale1 : p.mask_scale2) : 1.f;
+    }
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = wm * WM + i * 16 + (lane & 15);
+      const int q = m0 + ml;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = G ? acc[i][j][r] * p.out_scale + bsv[r] : acc[i][j][r] + bsv[r];
+        if (kRelu) x = fmaxf(x, 0.f);
+        if (kDrop) {
+          const uint32_t h = drop_hash((uint64_t)q * p.Cout + n + r, p.seed, p.salt);
+          x = (h >= drop_thr) ? x * inv_keep : 0.f;
+        }
+        if (kMaskScale) x *= msc[r];
+        v[r] = x;
+      }
+      if (kStats && q < M) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float xr = (float)(bf16)v[r];
+          s1[r] += xr;
+          s2[r] += xr * xr;
+        }
+      }
+      u32x2 pk;
+      pk[0] = pack2bf(v[0], v[1]);
+      pk[1] = pack2bf(v[2], v[3]);
+      *(u32x2*)(E + ml * EPI_STRIDE + nl * 2) = pk;
+    }
+    if (kStats) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float a = s1[r], b = s2[r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          a += __shfl_xor(a, o, 64);
+          b += __shfl_xor(b, o, 64);
+        }
+        if ((lane & 15) == 0) {
+          atomicAdd(p.stats + n + r, a);
+          atomicAdd(p.stats + p.Cout + n + r, b);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // coalesced phase: 16-byte chunks, consecutive threads -> consecutive channels
+  constexpr int CPR = BN / 8;
+  constexpr int NCHUNK = BM * CPR;
+  const int Dt = kShuffle ? (p.Cout >> p.shuffle) : 0;
+#pragma unroll 2
+  for (int c = tid; c < NCHUNK; c += NTHR) {
+    const int ml = c / CPR, cb = c % CPR;
+    const int q = m0 + ml;
+    if (q >= M) continue;
+    const int n = n0 + cb * 8;
+    const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
+    const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
+    u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
+    size_t off;
+    bf16* dst;
+    const void* mk;
+    if (EPI == EPI_FWD) {
+      off = (size_t)q * p.Cout + n;
+      dst = (bf16*)p.dst1;
+      mk = nullptr;
+    } else if (kShuffle) {
+      const int tap = n / Dt, co = n - tap * Dt;
+      const PixCoord pc = decompose(q, p.OD, p.OH, p.OW);
+      int td = 0, th, tw;
+      if (p.shuffle == 3) {
+        td = tap >> 2;
+        th = (tap >> 1) & 1;
+        tw = tap & 1;
+      } else {
+        th = tap >> 1;
+        tw = tap & 1;
+      }
+      const int dd = p.shuffle == 3 ? 2 : 1;
+      const size_t pix = (((size_t)pc.n * (p.OD * dd) + pc.d * dd + td) * (2 * p.OH) + 2 * pc.h + th) *
+                             (2 * p.OW) + 2 * pc.w + tw;
+      off = pix * Dt + co;
+      dst = (bf16*)p.dst1;
+      mk = p.mask1;
+    } else if (n < p.D1) {
+      off = (size_t)q * p.D1 + n;
+      dst = (bf16*)p.dst1;
+      mk = p.mask1;
+    } else {
+      off = (size_t)q * (p.Cout - p.D1) + (n - p.D1);
+      dst = (bf16*)p.dst2;
+      mk = p.mask2;
+    }
+    if (EPI != EPI_FWD && mk) {
+      const u32x4 mv = *(const u32x4*)((const bf16*)mk + off);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // bf16 > 0 <=> sign bit clear and not zero (-0 counts as not positive)
+        const uint32_t w = mv[e];
+        const uint32_t lo16 = w & 0xffffu, hi16 = w >> 16;
+        const uint32_t keep_lo = (lo16 != 0u && !(lo16 & 0x8000u)) ? 0xffffu : 0u;
+        const uint32_t keep_hi = (hi16 != 0u && !(hi16 & 0x8000u)) ? 0xffff0000u : 0u;
+        v[e] &= (keep_lo | keep_hi);
+      }
+    }
+    *(u32x4*)(dst + off) = v;
+  }
+}
+
+}  // namespace unet

@@ -29,6 +29,7 @@
 // UpSampling2D (`model.py:76-109`), Dropout(0.2) (`model.py:60,66`).
 #include "common.h"
 #include "conv_params.h"
+#include "conv_epilogue.h"
 
 namespace unet {
 
@@ -38,21 +39,6 @@ constexpr int NTHR = 256;
 constexpr int BK = 64;
 
 __device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
-
-struct PixCoord {
-  int n, d, h, w;
-};
-
-__device__ __forceinline__ PixCoord decompose(int q, int OD, int OH, int OW) {
-  PixCoord c;
-  c.w = q % OW;
-  int t = q / OW;
-  c.h = t % OH;
-  t /= OH;
-  c.d = t % OD;
-  c.n = t / OD;
-  return c;
-}
 
 // MODE 0: plain; MODE 1: src1 nearest-upsampled x2; MODE 2: first layer (Cin 4/8).
 // CONCAT: a second source supplies channels [C1, C1 + C2) (decoder skip concat).
@@ -64,8 +50,7 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
   constexpr int BR = (BN + 31) / 32;                // B rows per thread
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int EPI_STRIDE = (BN + 4) * 2;          // bytes; 8B-aligned, conflict-free b64 writes
-  constexpr int EPI_BYTES = BM * EPI_STRIDE;
+  constexpr int EPI_BYTES = BM * (BN + 4) * 2;
   constexpr int LDS_BYTES = (2 * STAGE > EPI_BYTES) ? 2 * STAGE : EPI_BYTES;
   static_assert(WAVES_M * WAVES_N == 4, "4 waves");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
@@ -280,128 +265,7 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
     __syncthreads();
   }
 
-  // ---------------------------------------------------------------- epilogue
-  // register phase: acc[i][j][r] = out[pixel = m0 + wm*WM + i*16 + (lane&15)]
-  //                                   [chan  = n0 + wn*WN + j*16 + (lane>>4)*4 + r]
-  char* E = smem;
-  const float inv_keep = p.drop_rate > 0.f ? 1.f / (1.f - p.drop_rate) : 1.f;
-  const uint32_t drop_thr = (uint32_t)(p.drop_rate * 4294967296.0);
-  const int Dtb = p.shuffle ? (p.Cout >> p.shuffle) : p.Cout;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int nl = wn * WN + j * 16 + (lane >> 4) * 4;
-    const int n = n0 + nl;
-    float bsv[4], msc[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      bsv[r] = p.bias ? p.bias[(n + r) % Dtb] : 0.f;
-      msc[r] = (n + r < p.D1) ? p.mask_scale1 : p.mask_scale2;
-    }
-    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int ml = wm * WM + i * 16 + (lane & 15);
-      const int q = m0 + ml;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float x = acc[i][j][r] * p.out_scale + bsv[r];
-        if (p.relu) x = fmaxf(x, 0.f);
-        if (p.drop_rate > 0.f) {
-          const uint32_t h = drop_hash((uint64_t)q * p.Cout + n + r, p.seed, p.salt);
-          x = (h >= drop_thr) ? x * inv_keep : 0.f;
-        }
-        x *= msc[r];
-        v[r] = x;
-      }
-      if (p.stats && q < M) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float xr = (float)(bf16)v[r];
-          s1[r] += xr;
-          s2[r] += xr * xr;
-        }
-      }
-      u32x2 pk;
-      pk[0] = pack2bf(v[0], v[1]);
-      pk[1] = pack2bf(v[2], v[3]);
-      *(u32x2*)(E + ml * EPI_STRIDE + nl * 2) = pk;
-    }
-    if (p.stats) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float a = s1[r], b = s2[r];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          a += __shfl_xor(a, o, 64);
-          b += __shfl_xor(b, o, 64);
-        }
-        if ((lane & 15) == 0) {
-          atomicAdd(p.stats + n + r, a);
-          atomicAdd(p.stats + p.Cout + n + r, b);
-        }
-      }
-    }
-  }
-  __syncthreads();
-
-  // coalesced phase: 16-byte chunks, consecutive threads -> consecutive channels
-  constexpr int CPR = BN / 8;
-  constexpr int NCHUNK = BM * CPR;
-  const int Dt = p.shuffle ? (p.Cout >> p.shuffle) : 0;
-#pragma unroll 2
-  for (int c = tid; c < NCHUNK; c += NTHR) {
-    const int ml = c / CPR, cb = c % CPR;
-    const int q = m0 + ml;
-    if (q >= M) continue;
-    const int n = n0 + cb * 8;
-    const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
-    const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
-    u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
-    size_t off;
-    bf16* dst;
-    const void* mk;
-    if (p.shuffle) {
-      const int tap = n / Dt, co = n - tap * Dt;
-      const PixCoord pc = decompose(q, p.OD, p.OH, p.OW);
-      int td = 0, th, tw;
-      if (p.shuffle == 3) {
-        td = tap >> 2;
-        th = (tap >> 1) & 1;
-        tw = tap & 1;
-      } else {
-        th = tap >> 1;
-        tw = tap & 1;
-      }
-      const int dd = p.shuffle == 3 ? 2 : 1;
-      const size_t pix = (((size_t)pc.n * (p.OD * dd) + pc.d * dd + td) * (2 * p.OH) + 2 * pc.h + th) *
-                             (2 * p.OW) + 2 * pc.w + tw;
-      off = pix * Dt + co;
-      dst = (bf16*)p.dst1;
-      mk = p.mask1;
-    } else if (n < p.D1) {
-      off = (size_t)q * p.D1 + n;
-      dst = (bf16*)p.dst1;
-      mk = p.mask1;
-    } else {
-      off = (size_t)q * (p.Cout - p.D1) + (n - p.D1);
-      dst = (bf16*)p.dst2;
-      mk = p.mask2;
-    }
-    if (mk) {
-      const u32x4 mv = *(const u32x4*)((const bf16*)mk + off);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        // bf16 > 0 <=> sign bit clear and not zero (-0 counts as not positive)
-        const uint32_t w = mv[e];
-        const uint32_t lo16 = w & 0xffffu, hi16 = w >> 16;
-        const uint32_t keep_lo = (lo16 != 0u && !(lo16 & 0x8000u)) ? 0xffffu : 0u;
-        const uint32_t keep_hi = (hi16 != 0u && !(hi16 & 0x8000u)) ? 0xffff0000u : 0u;
-        v[e] &= (keep_lo | keep_hi);
-      }
-    }
-    *(u32x4*)(dst + off) = v;
-  }
+  conv_epilogue<BM, BN, WM, WN, TM, TN, NTHR>(p, acc, smem, m0, n0, M, wm, wn, lane, tid);
 }
 
 template <int BM, int BN, int WAVES_M, int WAVES_N>
@@ -420,7 +284,204 @@ hipError_t launch_cfg(const ConvFwdParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------------
+// Row-window conv (fine UNet levels): 2D, 3x3, stride 1, 'same' padding, full-width rows.
+//
+// The implicit GEMM above re-gathers the input once per tap: at the 128^2 / 64^2
+// levels (Cin, Cout <= 64) that 9x L2->LDS traffic, not the MFMA, bounds it.  Here a
+// workgroup owns BM = 512 output pixels = R = 512/W whole rows of the flattened
+// (n, h) row space and BN output channels.  Per 32-channel input chunk it stages the
+// (R+2) x (W+2) halo image of those rows ONCE in LDS (zero columns at the left/right
+// border come free from out-of-range buffer loads), plus the chunk's 9 x BN weight
+// rows, and then runs all nine taps as MFMAs on shifted LDS addresses.  Rows that
+// cross an image boundary inside the window are handled by skipping the (wave-uniform)
+// MFMAs of taps whose input row falls outside the output row's image.
+//
+// LDS images: 64-byte pixel slots (32 bf16); the halo image has rows of HWP = W + 4
+// slots (a multiple of 4: every row starts on a 256-byte bank row) and stores 16-byte
+// chunk c of the pixel in column hc at c ^ ((hc >> 1) & 3).  Fragment reads are 16
+// consecutive columns from any start (any tap shift): conflict free, and because the
+// swizzle depends only on the column, a lane's address is one of three per-lane bases
+// (one per horizontal tap) plus a compile-time immediate (row, tile) -- no per-tap
+// address registers.  Weight rows (tap, n) use the same swizzle on the row index.
+template <int W, int BN, bool CONCAT, int EPI>
+__global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
+  static_assert(BN == 32, "row-window tile is 32 output channels wide");
+  constexpr int BM = W == 16 ? 256 : 512;       // window pixels (16-wide rows: 16 rows)
+  constexpr int R = BM / W, HR = R + 2;
+  constexpr int HWP = ((W + 2 + 15) / 16) * 16; // halo row pitch in 64-byte pixel slots
+  constexpr int IPR = HWP / 16;                 // LDS-DMA wave-instructions per halo row
+  constexpr int ROWB = HWP * 64;
+  constexpr int XI = HR * IPR, WI = 9 * BN / 16;
+  constexpr int XB = XI * 1024, WB = WI * 1024;
+  constexpr int EPIB = BM * (BN + 4) * 2;
+  constexpr int LDS_BYTES = (XB + WB > EPIB) ? XB + WB : EPIB;
+  constexpr int WMP = BM / 4;                   // pixels per wave
+  constexpr int TM = WMP / 16, TN = BN / 16;
+  constexpr int TPR = W / 16;                   // 16-pixel tiles per row
+  static_assert(W >= 16 && W <= 128 && BM % W == 0 && WMP % 16 == 0, "row width");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  char* Xs = smem;
+  char* Ws = smem + XB;
+
+  // wave index as a scalar: every per-wave quantity below (rows, DMA slots) stays in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = p.OH;
+  const int rows_total = p.N * H;
+  const int M = rows_total * W;
+  const int tiles_n = p.Cout / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int g0 = tm * R;
+  const int m0 = g0 * W, n0 = tn * BN;
+  const int Cin = p.C1 + p.C2;
+  const int nchunks = Cin >> 5;
+  constexpr int OOB = 0x7fffffff;
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)p.src1, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.src2 ? p.src2 : p.src1), (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
+
+  // wave w owns window pixels [WMP w, WMP (w + 1)): rows rw0 .. rw0 + WMP/W - 1
+  const int rw0 = (WMP * wave) / W;
+  uint32_t top_ok = 0, bot_ok = 0, live = 0;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int g = g0 + rw0 + (i / TPR);
+    const int h = g % H;
+    if (g < rows_total) live |= 1u << i;
+    if (h > 0) top_ok |= 1u << i;
+    if (h < H - 1) bot_ok |= 1u << i;
+  }
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int fsub = lane >> 4, fr = lane & 15;
+  // per-lane fragment bases: horizontal tap dw -> column fr + dw (+ the wave's first row)
+  int xbase[3];
+#pragma unroll
+  for (int dw = 0; dw < 3; ++dw) {
+    const int hc = fr + dw;
+    xbase[dw] = rw0 * ROWB + ((WMP * wave) % W) * 64 + hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3));
+  }
+  const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
+  // LDS-DMA lane roles: lane l fills physical 16-byte chunk (l & 3) of slot (l >> 2) of a
+  // 16-slot run; it loads logical chunk (l & 3) ^ swizzle(slot), which depends only on l
+  // because every run starts at a multiple of 16 slots.
+  const int lslot = lane >> 2;
+  const int lchunk = (lane & 3) ^ ((lslot >> 1) & 3);
+
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const bool from1 = !CONCAT || (kc << 5) < p.C1;
+    const int C = from1 ? p.C1 : p.C2;
+    const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
+    if (kc) __syncthreads();   // previous chunk's fragment reads are done
+    {
+      // halo image: row hr, slot hc holds pixel (g0 - 1 + hr, hc - 1); instruction
+      // (hr, j) covers slots 16j .. 16j + 15 of row hr.  Rows outside the tensor and
+      // columns outside [0, W) load zeros (out-of-range offsets).
+      const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
+      const int lofs = ((lslot - 1) * C + cb + lchunk * 8) * 2;
+#pragma unroll
+      for (int q = 0; q < (XI + 3) / 4; ++q) {
+        const int k = wave + 4 * q;
+        if (k < XI) {
+          const int hr = k / IPR, j = k - hr * IPR;      // wave-uniform
+          const int gr = g0 - 1 + hr;
+          const int col = 16 * j + lslot - 1;
+          const bool ok = (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+          const int off = ok ? (gr * W + 16 * j) * C * 2 + lofs : OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
+                                                   16, off, 0, 0, 0);
+        }
+      }
+      // weight image: row r = tap * 32 + n (64 bytes = this chunk's 32 input channels)
+      const int wl = (lslot * p.Kpad + (kc << 5) + lchunk * 8) * 2;
+#pragma unroll
+      for (int q = 0; q < (WI + 3) / 4; ++q) {
+        const int k = wave + 4 * q;
+        if (k < WI) {
+          const int tap = k >> 1, nb = (k & 1) * 16;     // wave-uniform
+          const int off = ((n0 + nb) * p.Kpad + tap * Cin) * 2 + wl;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024),
+                                                   16, off, 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dh = t / 3, dw = t % 3;
+      bf16x8 wf[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) wf[j] = *(const bf16x8*)(Ws + (t * BN + 16 * j) * 64 + wbase);
+      const uint32_t okm = (dh == 0 ? top_ok : (dh == 2 ? bot_ok : 0xffffffffu)) & live;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if ((okm >> i) & 1u) {
+          const bf16x8 xf =
+              *(const bf16x8*)(Xs + xbase[dw] + ((i / TPR) + dh) * ROWB + (i % TPR) * 16 * 64);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[j], xf, acc[i][j]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI>(p, acc, smem, m0, n0, M, wave, 0, lane, tid);
+}
+
+template <int BN>
+hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
+  const int W = p.OW;
+  const int rows = p.N * p.OH;
+  const int R = (W == 16 ? 256 : 512) / W;
+  const int grid = ((rows + R - 1) / R) * (p.Cout / BN);
+  const bool cc = p.C2 > 0;
+  const int epi = conv_epi_mode(p);
+#define WIN_EPI(WW, CC)                                                                                   \
+  if (epi == EPI_FWD)                                                                                     \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p);         \
+  else if (epi == EPI_DGRAD)                                                                              \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_DGRAD>), dim3(grid), dim3(NTHR), 0, s, p);       \
+  else                                                                                                    \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p);
+#define WIN_CASE(WW)                                                                                      \
+  case WW:                                                                                                \
+    if (cc) {                                                                                             \
+      WIN_EPI(WW, true)                                                                                   \
+    } else {                                                                                              \
+      WIN_EPI(WW, false)                                                                                  \
+    }                                                                                                     \
+    break;
+  switch (W) {
+    WIN_CASE(16)
+    WIN_CASE(32)
+    WIN_CASE(64)
+    WIN_CASE(128)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef WIN_CASE
+#undef WIN_EPI
+  return hipGetLastError();
+}
+
 }  // namespace
+
+// True when the row-window kernel can run this conv (2D, 3x3 s1 p1, plain / concat
+// source at full resolution, full rows of width 16..128).
+static bool win_eligible(const ConvFwdParams& p) {
+  const bool w_ok = p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128;
+  return p.KD == 1 && p.OD == 1 && p.ID == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.pad == 1 &&
+         p.up1 == 1 && !p.shuffle && !p.stats && w_ok && p.IW == p.OW && p.IH == p.OH &&
+         (p.C1 % 32) == 0 && (p.C2 % 32) == 0 && p.C1 > 0;
+}
 
 // Fills the tap tables and Kpad; returns nullptr on success or a message describing
 // why the shape is unsupported.
@@ -449,11 +510,13 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.shuffle && ((p.Cout >> p.shuffle) % 8)) return "conv_fwd: shuffle channels must be multiples of 8";
   if (p.shuffle && p.D1 != p.Cout) return "conv_fwd: shuffle with channel split unsupported";
   if (p.stats && p.shuffle) return "conv_fwd: stats with shuffle unsupported";
-  if (p.tile < 0 || p.tile > 5) return "conv_fwd: bad tile id";
+  if (p.tile < 0 || p.tile > 8) return "conv_fwd: bad tile id";
   {
     const int t = p.tile ? p.tile : 0;
     const int bn = t == 1 ? 128 : (t == 2 || t == 5) ? 64 : 32;
+    if (t == 7) return "conv_fwd: tile 7 (row-window 512x64) was removed: 1 wave/SIMD, never faster";
     if (t && p.Cout % bn) return "conv_fwd: forced tile does not divide Cout";
+    if (t == 6 && !win_eligible(p)) return "conv_fwd: row-window tile not applicable";
   }
   if ((long long)p.N * p.ID * p.IH * p.IW >= (1LL << 31) || (long long)p.N * p.OD * p.OH * p.OW >= (1LL << 31))
     return "conv_fwd: too many pixels";
@@ -475,10 +538,15 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   return nullptr;
 }
 
-// tile ids: 1 = 128x128, 2 = 128x64, 3 = 256x32, 4 = 128x32, 5 = 256x64 (4 waves each)
+// tile ids: 1 = 128x128, 2 = 128x64, 3 = 256x32, 4 = 128x32, 5 = 256x64 (4 waves each);
+// 6 = row-window 512 x 32; 8 = auto but never row-window (A/B tests)
 int conv_fwd_pick(const ConvFwdParams& p) {
   const int M = p.N * p.OD * p.OH * p.OW;
-  if (p.tile) return p.tile;
+  if (p.tile && p.tile != 8) return p.tile;
+  // row-window 512x32 wins at every level it applies to (16..128 wide), measured
+  // 1.1-2.1x over the implicit-GEMM tiles (profiles/r1_conv_tiles.md); the 512x64
+  // variant needs 287 registers (1 wave/SIMD) and never wins
+  if (p.tile != 8 && win_eligible(p)) return 6;
   if (p.Cout % 128 == 0 && M >= 8192) return 1;
   if (p.Cout % 64 == 0) return 2;
   return 4;
@@ -490,6 +558,7 @@ hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
     case 2: return launch_cfg<128, 64, 2, 2>(p, s);
     case 3: return launch_cfg<256, 32, 4, 1>(p, s);
     case 5: return launch_cfg<256, 64, 4, 1>(p, s);
+    case 6: return launch_win<32>(p, s);
     default: return launch_cfg<128, 32, 4, 1>(p, s);
   }
 }

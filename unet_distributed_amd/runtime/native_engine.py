@@ -28,6 +28,7 @@ The executor plays the role of the reference's TF graph + session
 """
 
 import math
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -253,8 +254,9 @@ class NativeUNet:
         od, oh, ow = self.sdims(out_level or level)
         idd, ih, iw = self.sdims(in_level or level)
         kd = K if self.dims == 3 else 1
+        # UNET_CONV_TILE: force a conv tile id for A/B measurements (8 = no row-window)
         return dict(N=self.B, OD=od, OH=oh, OW=ow, ID=idd, IH=ih, IW=iw, KD=kd, KH=K, KW=K,
-                    stride=stride, pad=pad)
+                    stride=stride, pad=pad, tile=int(os.environ.get("UNET_CONV_TILE", "0")))
 
     def _salt(self, lname):
         return [l.name for l in self.spec.layers].index(lname)
