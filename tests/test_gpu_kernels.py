@@ -240,6 +240,29 @@ def test_conv_wgrad_and_bias(cuda_dev, N, H, Cin, Cout, splits):
     assert rel_err(gb, gbr) < 2e-3
 
 
+@pytest.mark.parametrize("N,H,C1,C2,Cout,splits,win", [
+    (3, 128, 32, 0, 32, 5, 0), (2, 128, 32, 32, 32, 7, 0), (4, 64, 64, 0, 64, 3, 0), (3, 64, 64, 64, 64, 9, 0),
+    (2, 64, 32, 0, 64, 2, 0), (5, 32, 64, 0, 128, 4, 0), (2, 32, 128, 128, 128, 3, 0), (3, 32, 32, 0, 32, 40, 0),
+    (2, 64, 64, 0, 64, 3, -1)])
+def test_wgrad_row_window(cuda_dev, N, H, C1, C2, Cout, splits, win):
+    """Row-window wgrad (auto for 2D 3x3 on 32..128-wide rows): concat sources, 32/64-wide
+    output-channel blocks, more splits than windows, fused bias sums; win=-1 = tiled kernel."""
+    torch.manual_seed(N + H + C1 + C2 + Cout)
+    a = F.relu(torch.randn(N, H, H, C1, device=cuda_dev)).bfloat16()
+    b2 = F.relu(torch.randn(N, H, H, max(C2, 1), device=cuda_dev)).bfloat16()
+    dy = torch.randn(N, H, H, Cout, device=cuda_dev).bfloat16()
+    Mt = C1 + C2
+    d = dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=C1, M2=C2, a1=ptr(a),
+             a2=ptr(b2) if C2 else None, b=ptr(dy), Nc=Cout, bias_mode=1, win=win)
+    gw, gb = _wgrad(d, splits, 9, Mt, Mt, Cout, 9 * Mt * Cout, bias_w=(splits, Cout))
+    inp = nchw(a.float()) if not C2 else torch.cat([nchw(a.float()), nchw(b2.float())], 1)
+    w = torch.zeros(Cout, Mt, 3, 3, device=cuda_dev, requires_grad=True)
+    bb = torch.zeros(Cout, device=cuda_dev, requires_grad=True)
+    gwr, gbr = torch.autograd.grad(F.conv2d(inp, w, bb, padding=1), [w, bb], nchw(dy.float()))
+    assert rel_err(gw, gwr.permute(2, 3, 1, 0).reshape(-1)) < 2e-3
+    assert rel_err(gb, gbr) < 2e-3
+
+
 def test_wgrad_concat_upsample(cuda_dev):
     torch.manual_seed(6)
     N, H, C1, C2, Co = 2, 16, 32, 32, 32

@@ -60,6 +60,7 @@ struct WgradParams {
   // 2 = column sums of A over the WG's taps (tconv: dOut -> m)
   int bias_mode;
   float* bias_slab;           // [splits][tap_groups][M or Nc] fp32
+  int win;                    // 0 = row-window kernel when eligible, -1 = never (A/B tests)
   // filled by the launcher
   int lqw, lqh, lqd;          // log2 of the pixel grid (power-of-two fast path)
   signed char tap_d[27], tap_h[27], tap_w[27];

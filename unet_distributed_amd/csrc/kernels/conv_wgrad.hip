@@ -430,11 +430,222 @@ hipError_t launch_wg(WgradParams p, hipStream_t s) {
   return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------------
+// Row-window weight gradient (2D 3x3 stride 1 'same', full rows of W in {32,64,128}).
+//
+// The tiled kernel above stages one A image per tap (9 copies of the input tile):
+// at the fine levels, where Cin and Cout are 32..64, that LDS traffic bounds it at
+// ~160 TF.  Here a workgroup walks a contiguous range of 256-pixel windows (R = 256/W
+// whole rows of the flattened (n, h) row space) and, per window, LDS-DMAs ONE halo
+// image of the input rows (32 channels) plus the dY rows of its 32*QO output
+// channels.  Every tap then reads its shifted A fragments from that single image
+// with the hardware transpose read (ds_read_b64_tr_b16 -> 8 pixels of one channel
+// per lane), the dY fragments are read once per 32-pixel step and reused by all nine
+// taps, and the partial dW (9 x 32 x 32 per wave) stays in registers across windows.
+// Waves split output channels (QO) and pixel steps (4 / QO); pixel-split partials are
+// summed through LDS and each workgroup writes one fp32 slab (deterministic reduce).
+// Images: 64-byte pixel slots; 16-byte chunk c of the slot in column col is stored at
+// c ^ (((col >> 3) & 1) << 1), which makes the transposed fragment reads conflict free
+// (tools/lds_bank_model.py) and depends only on col mod 16 (DMA lane roles fixed).
+template <int W, int QO, bool CONCAT>
+__global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p) {
+  constexpr int BMW = 256, R = BMW / W, HR = R + 2;
+  constexpr int HWP = ((W + 2 + 15) / 16) * 16, IPR = HWP / 16, ROWB = HWP * 64;
+  constexpr int XI = HR * IPR, YI = QO * BMW / 16;
+  constexpr int XB = XI * 1024, YB = YI * 1024;
+  constexpr int PS = 4 / QO, KS = BMW / 32;
+  constexpr int REDB = 4 * 64 * 16 * 4;                 // one tap of every wave's partials
+  constexpr int LDS_BYTES = (XB + YB > REDB) ? XB + YB : REDB;
+  static_assert(W >= 32 && W <= 128 && (QO == 1 || QO == 2), "window wgrad shape");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  char* Xs = smem;
+  char* Ys = smem + XB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qo = wave % QO, ps = wave / QO;
+  const int H = p.QH;
+  const int rows_total = p.N * H;
+  const int Mq = rows_total * W;
+  const int nwin = (rows_total + R - 1) / R;
+  const int Mtot = p.M1 + p.M2;
+  const int cob = p.Nc / (32 * QO);
+  const int ntile = (Mtot / 32) * cob;
+  const int split = blockIdx.x / ntile, tile = blockIdx.x - split * ntile;
+  const int ci_blk = tile / cob, co_blk = tile - ci_blk * cob;
+  const int ci0 = ci_blk * 32, co0 = co_blk * 32 * QO;
+  const bool from1 = !CONCAT || ci0 < p.M1;
+  const int CA = from1 ? p.M1 : p.M2, ca0 = from1 ? ci0 : ci0 - p.M1;
+  constexpr int OOB = 0x7fffffff;
+  const __amdgpu_buffer_rsrc_t rsa =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(from1 ? p.a1 : p.a2), (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, OOB, 0x00020000);
+  const int w_begin = (int)((long long)split * nwin / p.splits);
+  const int w_end = (int)((long long)(split + 1) * nwin / p.splits);
+  const bool do_bias = p.bias_mode == 1 && ci_blk == 0;
+
+  f32x4 acc[9][2][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 bacc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+  const u32x4 ones_u = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_u);
+
+  // LDS-DMA lane roles (slot 16k + lslot, physical chunk lane & 3)
+  const int lslot = lane >> 2;
+  const int lchunk = (lane & 3) ^ (((lslot >> 3) & 1) << 1);
+  const int xl = ((lslot - 1) * CA + ca0 + lchunk * 8) * 2;
+  const int yl = (lslot * p.Nc + co0 + lchunk * 8) * 2;
+  // transposed-read lane roles: group G = lane >> 4 covers pixels 8G .. 8G + 7 of a
+  // 32-pixel step; lane 4q + pp addresses pixel 8G + 4hh + q, channels 4pp .. 4pp + 3
+  const int G = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+
+  auto tr_addr = [&](int slot, int col, int ch) -> int {   // ch: channel within the 32-ch slot
+    return slot * 64 + ((((ch >> 3) ^ (((col >> 3) & 1) << 1))) << 4) + ((ch & 7) << 1);
+  };
+  auto tr8 = [&](const char* base0, const char* base1) -> bf16x8 {
+    const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base0));
+    const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base1));
+    const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+    const u32x4 v = {l2[0], l2[1], h2[0], h2[1]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+  for (int win = w_begin; win < w_end; ++win) {
+    const int g0 = win * R;
+    __syncthreads();   // the previous window's fragment reads are done
+#pragma unroll
+    for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
+      const int k = wave + 4 * qq;
+      if (k < XI) {
+        const int hr = k / IPR, j = k - hr * IPR;
+        const int gr = g0 - 1 + hr;
+        const int col = 16 * j + lslot - 1;
+        const bool ok = (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+        const int off = ok ? (gr * W + 16 * j) * CA * 2 + xl : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int qq = 0; qq < (YI + 3) / 4; ++qq) {
+      const int k = wave + 4 * qq;
+      if (k < YI) {
+        const int o = k / (BMW / 16), sb = (k - o * (BMW / 16)) * 16;   // image o, first slot
+        const int pix = g0 * W + sb;
+        const int off = (pix + lslot < Mq) ? (pix * p.Nc + 32 * o) * 2 + yl : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (__attribute__((address_space(3))) void*)(Ys + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    const char* Yq = Ys + qo * (BMW * 64);
+#pragma unroll 1
+    for (int kk = ps; kk < KS; kk += PS) {
+      const int px0 = kk * 32;
+      const int rr = px0 / W, c0 = px0 - rr * W;
+      const int g = g0 + rr;
+      if (g >= rows_total) break;
+      const int h = g % H;
+      // dY fragments (B operand: k = pixels, n = output channels)
+      bf16x8 bf[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int s0 = px0 + 8 * G + q, s1 = s0 + 4;
+        bf[j] = tr8(Yq + tr_addr(s0, s0, 16 * j + 4 * pp), Yq + tr_addr(s1, s1, 16 * j + 4 * pp));
+      }
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bacc[j] = mfma16(ones, bf[j], bacc[j]);
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int dh = t / 3, dw = t % 3;
+        if ((dh == 0 && h == 0) || (dh == 2 && h == H - 1)) continue;   // zero-padding rows
+        const int colA = c0 + dw + 8 * G + q;       // halo column of this lane's first pixel
+        const int slotA = (rr + dh) * HWP + colA;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bf16x8 af = tr8(Xs + tr_addr(slotA, colA, 16 * i + 4 * pp),
+                                Xs + tr_addr(slotA + 4, colA + 4, 16 * i + 4 * pp));
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[t][i][j] = mfma16(af, bf[j], acc[t][i][j]);
+        }
+      }
+    }
+  }
+
+  // ---- reduce the pixel-split partials (waves with the same qo) and write the slab
+  // acc[t][i][j][r] = dW[t][ci0 + 16i + 4(lane>>4) + r][co0 + 32qo + 16j + (lane&15)]
+  float* red = (float*)smem;
+  const int n_base = co0 + 32 * qo + (lane & 15);
+  const int m_base = ci0 + 4 * (lane >> 4);
+  auto reduce_store = [&](const f32x4 (&v4)[2][2], const int t) {
+    __syncthreads();
+    if (PS > 1 && ps > 0) {
+      float* dst = red + (wave * 64 + lane) * 16;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) *(f32x4*)(dst + (i * 2 + j) * 4) = v4[i][j];
+    }
+    __syncthreads();
+    if (ps == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 v = v4[i][j];
+#pragma unroll
+          for (int o = 1; o < PS; ++o) v += *(const f32x4*)(red + ((qo + QO * o) * 64 + lane) * 16 + (i * 2 + j) * 4);
+          if (t < 9) {
+            float* dst = p.slab + (((size_t)split * 9 + t) * Mtot + m_base + 16 * i) * p.Nc + n_base + 16 * j;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dst[(size_t)r * p.Nc] = v[r];
+          } else if (i == 0 && lane < 16) {
+            p.bias_slab[(size_t)split * p.Nc + n_base + 16 * j] = v[0];
+          }
+        }
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < 9; ++t) reduce_store(acc[t], t);
+  if (do_bias) {
+    const f32x4 z = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const f32x4 bv[2][2] = {{bacc[0], bacc[1]}, {z, z}};
+    reduce_store(bv, 9);
+  }
+}
+
+template <int W, int QO>
+hipError_t launch_wgrad_win(const WgradParams& p, hipStream_t s) {
+  const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.splits;
+  if (p.M2 > 0)
+    hipLaunchKernelGGL((wgrad_win_kernel<W, QO, true>), dim3(grid), dim3(NTHR), 0, s, p);
+  else
+    hipLaunchKernelGGL((wgrad_win_kernel<W, QO, false>), dim3(grid), dim3(NTHR), 0, s, p);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+// Row-window wgrad applies to 2D 3x3 stride-1 'same' convs on full rows 32..128 wide
+// (p.win < 0 disables it for A/B tests).
+static bool wgrad_win_eligible(const WgradParams& p) {
+  const bool w_ok = p.QW == 32 || p.QW == 64 || p.QW == 128;
+  return p.win >= 0 && w_ok && p.QD == 1 && p.KD == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 &&
+         p.pad == 1 && p.upA == 1 && p.AW == p.QW && p.AH == p.QH && (p.M1 % 32) == 0 && (p.M2 % 32) == 0 &&
+         p.M1 > 0 && (p.Nc % 32) == 0 && p.bias_mode != 2;
+}
 
 WgradCfg wgrad_pick(const WgradParams& p) {
   const int KT = p.KD * p.KH * p.KW;
   const int M = p.M1 + p.M2;
+  if (wgrad_win_eligible(p)) return {32, (p.Nc % 64 == 0) ? 64 : 32, 9, 0};   // row-window tile
   if ((p.M1 == 4 || p.M1 == 8) && p.M2 == 0) return {64, 32, 1, 1};
   if (M <= 64 && p.Nc <= 64 && KT % 9 == 0) return {32, 32, 9, 0};
   if (M <= 64 && p.Nc <= 64 && KT % 4 == 0) return {32, 32, 4, 0};
@@ -462,6 +673,14 @@ const char* wgrad_check(const WgradParams& p) {
 
 hipError_t wgrad_launch(const WgradParams& p, hipStream_t s) {
   const WgradCfg c = wgrad_pick(p);
+  if (wgrad_win_eligible(p)) {
+    const bool q2 = c.BN == 64;
+    switch (p.QW) {
+      case 32: return q2 ? launch_wgrad_win<32, 2>(p, s) : launch_wgrad_win<32, 1>(p, s);
+      case 64: return q2 ? launch_wgrad_win<64, 2>(p, s) : launch_wgrad_win<64, 1>(p, s);
+      default: return q2 ? launch_wgrad_win<128, 2>(p, s) : launch_wgrad_win<128, 1>(p, s);
+    }
+  }
   if (c.smallc) return launch_wg<64, 32, 1, 2, 2, true>(p, s);
   if (c.BM == 32 && c.NTAP == 9) return launch_wg<32, 32, 9, 2, 2>(p, s);
   if (c.BM == 32 && c.NTAP == 4) return launch_wg<32, 32, 4, 2, 2>(p, s);

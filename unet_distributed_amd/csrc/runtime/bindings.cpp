@@ -126,6 +126,7 @@ WgradParams wgrad_params(const py::dict& d) {
   p.slab = (float*)getp(d, "slab");
   p.bias_mode = get<int>(d, "bias_mode", 0);
   p.bias_slab = (float*)getp(d, "bias_slab");
+  p.win = get<int>(d, "win", 0);
   if (p.bias_mode && !p.bias_slab) throw std::invalid_argument("wgrad: bias_slab required");
   if (!p.a1 || !p.b || !p.slab) throw std::invalid_argument("wgrad: a1/b/slab required");
   check_msg(wgrad_check(p));
@@ -306,17 +307,32 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("head_blocks", &head_blocks_py);
   m.def("wgrad_reduce_stage_floats", &wgrad_reduce_stage_floats);
-  m.def("wgrad_pick", [](int M1, int M2, int Nc, int KT) {
-    WgradParams p{};
-    p.M1 = M1;
-    p.M2 = M2;
-    p.Nc = Nc;
-    p.KD = 1;
-    p.KH = 1;
-    p.KW = KT;
-    WgradCfg c = wgrad_pick(p);
-    return py::make_tuple(c.BM, c.BN, c.NTAP, c.smallc);
-  });
+  // QW > 0 describes a 2D 3x3 stride-1 'same' conv on QW-wide rows (row-window candidate)
+  m.def(
+      "wgrad_pick",
+      [](int M1, int M2, int Nc, int KT, int QW, int upA, int win) {
+        WgradParams p{};
+        p.M1 = M1;
+        p.M2 = M2;
+        p.Nc = Nc;
+        p.KD = 1;
+        p.KH = 1;
+        p.KW = KT;
+        p.upA = upA;
+        p.win = win;
+        p.bias_mode = 1;
+        if (QW > 0 && KT == 9) {
+          p.KH = p.KW = 3;
+          p.QD = p.AD = 1;
+          p.QW = p.QH = p.AW = p.AH = QW;
+          p.stride = 1;
+          p.pad = 1;
+        }
+        WgradCfg c = wgrad_pick(p);
+        return py::make_tuple(c.BM, c.BN, c.NTAP, c.smallc);
+      },
+      py::arg("M1"), py::arg("M2"), py::arg("Nc"), py::arg("KT"), py::arg("QW") = 0, py::arg("upA") = 1,
+      py::arg("win") = -1);
   m.def("packseg_bytes", []() { return (int)sizeof(PackSeg); });
   m.def("crc32c", [](py::buffer b, uint32_t crc) {
     py::buffer_info info = b.request();

@@ -80,6 +80,8 @@ class NativeUNet:
             raise NotImplementedError("native executor: in_channels=%d" % cin)
         self.bufs: Dict[str, torch.Tensor] = {}
         self.wg_target = 512
+        # UNET_WGRAD_WIN=-1: never use the row-window wgrad kernel (A/B measurements)
+        self.wgrad_win = int(os.environ.get("UNET_WGRAD_WIN", "0"))
         self._alloc_weights()
         self._alloc_activations()
         self.plan = self.C.Plan()
@@ -304,8 +306,14 @@ class NativeUNet:
     def _colsum_blocks(rows, C):
         return max(1, min(512, rows // 256))
 
-    def _wgrad_splits(self, M1, M2, Nc, KT, Q):
-        BM, BN, NTAP, smallc = self.C.wgrad_pick(M1, M2, Nc, KT)
+    def _wgrad_pick(self, w):
+        """Tile config of a wgrad spec; QW marks 2D 3x3 convs (row-window candidates)."""
+        return self.C.wgrad_pick(w["M1"], w["M2"], w["Nc"], w["KT"], QW=w.get("QW", 0), upA=w.get("upA", 1),
+                                 win=self.wgrad_win)
+
+    def _wgrad_splits(self, w):
+        M1, M2, Nc, KT, Q = w["M1"], w["M2"], w["Nc"], w["KT"], w["Q"]
+        BM, BN, NTAP, smallc = self._wgrad_pick(w)
         Mtot = ((KT * M1 + BM - 1) // BM) * BM if smallc else M1 + M2
         tg = 1 if smallc else KT // NTAP
         tiles = (Mtot // BM) * (Nc // BN) * tg
@@ -369,6 +377,7 @@ class NativeUNet:
                           pad=1, upA=up1, a1=_ptr(b[src1]), a2=_ptr(b[skip]) if skip else None,
                           b=_ptr(dy))
                 emit_wgrad(dict(lname=l.name, kd=kd, M1=c1, M2=c2, Nc=l.cout, KT=KT3, Q=Q,
+                                QW=self.sdims(l.level)[2] if self.dims == 2 else 0, upA=up1,
                                 kernel=l.name + "/kernel", bias=l.name + "/bias", bias_mode=1,
                                 bias_width=l.cout, bias_src=(dy, Q),
                                 real_rows=(self.cpad, spec.in_channels) if first else None))
@@ -436,7 +445,7 @@ class NativeUNet:
         sized = []
         smax, bmax = 1, 1
         for w in wg_specs:
-            splits, Mtot, taps, tg, smallc = self._wgrad_splits(w["M1"], w["M2"], w["Nc"], w["KT"], w["Q"])
+            splits, Mtot, taps, tg, smallc = self._wgrad_splits(w)
             sized.append((splits, Mtot, taps, tg, smallc))
             smax = max(smax, splits * taps * Mtot * w["Nc"])
             bw = w["bias_width"] if w["bias_mode"] == 1 else Mtot
@@ -462,11 +471,12 @@ class NativeUNet:
                 w = wg_specs[op[1]]
                 splits, Mtot, taps, tg, smallc = sized[op[1]]
                 d = dict(w["kd"])
-                BM = self.C.wgrad_pick(w["M1"], w["M2"], w["Nc"], w["KT"])[0]
+                BM = self._wgrad_pick(w)[0]
                 # the 128x128 tile has no register room for the fused ones-MFMA bias sums:
                 # those (level >= 3, small dY) use a separate column-sum pass instead
                 fused_bias = BM < 128
                 d.update(name="wgrad:" + w["lname"], M1=w["M1"], M2=w["M2"], Nc=w["Nc"], splits=splits,
+                         win=self.wgrad_win,
                          slab=_ptr(self.slab), bias_mode=w["bias_mode"] if fused_bias else 0,
                          bias_slab=_ptr(self.bias_slab))
                 plan.add_wgrad(d)
