@@ -43,7 +43,9 @@ for name, H, Cin, Co, C2 in shapes:
 # ---- wgrad: row-window (win=0) vs tiled (win=-1) on the fine-level shapes
 wshapes = [("L1 32x32", 128, 32, 0, 32), ("L1 concat 32+32 -> 32", 128, 32, 32, 32), ("L2 32->64", 64, 32, 0, 64),
            ("L2 64x64", 64, 64, 0, 64), ("L2 concat 64+64 -> 64", 64, 64, 64, 64), ("L3 64->128", 32, 64, 0, 128),
-           ("L3 128x128", 32, 128, 0, 128), ("L3 concat 128+128 -> 128", 32, 128, 128, 128)]
+           ("L3 128x128", 32, 128, 0, 128), ("L3 concat 128+128 -> 128", 32, 128, 128, 128),
+           ("L4 256x256", 16, 256, 0, 256), ("L4 concat 256+256 -> 256", 16, 256, 256, 256),
+           ("L5 256->512", 8, 256, 0, 512), ("L5 512x512", 8, 512, 0, 512)]
 for name, H, C1, C2, Co in wshapes:
     a = torch.randn(B, H, H, C1, device=dev).bfloat16()
     a2 = torch.randn(B, H, H, max(C2, 1), device=dev).bfloat16()

@@ -243,7 +243,8 @@ def test_conv_wgrad_and_bias(cuda_dev, N, H, Cin, Cout, splits):
 @pytest.mark.parametrize("N,H,C1,C2,Cout,splits,win", [
     (3, 128, 32, 0, 32, 5, 0), (2, 128, 32, 32, 32, 7, 0), (4, 64, 64, 0, 64, 3, 0), (3, 64, 64, 64, 64, 9, 0),
     (2, 64, 32, 0, 64, 2, 0), (5, 32, 64, 0, 128, 4, 0), (2, 32, 128, 128, 128, 3, 0), (3, 32, 32, 0, 32, 40, 0),
-    (2, 64, 64, 0, 64, 3, -1)])
+    (2, 64, 64, 0, 64, 3, -1), (4, 16, 64, 0, 64, 3, 0), (3, 16, 128, 128, 128, 5, 0), (4, 8, 256, 0, 256, 2, 0),
+    (3, 8, 32, 0, 32, 7, 0)])
 def test_wgrad_row_window(cuda_dev, N, H, C1, C2, Cout, splits, win):
     """Row-window wgrad (auto for 2D 3x3 on 32..128-wide rows): concat sources, 32/64-wide
     output-channel blocks, more splits than windows, fused bias sums; win=-1 = tiled kernel."""

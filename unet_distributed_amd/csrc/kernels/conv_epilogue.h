@@ -119,6 +119,47 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
   // coalesced phase: 16-byte chunks, consecutive threads -> consecutive channels
   constexpr int CPR = BN / 8;
   constexpr int NCHUNK = BM * CPR;
+  if constexpr (EPI == EPI_DGRAD && NCHUNK % NTHR == 0 && NTHR % CPR == 0) {
+    // a thread's channel chunk (hence destination tensor, row stride and mask) is the
+    // same for all its rows: issue every ReLU-mask load first, then mask and store
+    constexpr int NIT = NCHUNK / NTHR, RPI = NTHR / CPR;
+    const int cb = tid % CPR, ml0 = tid / CPR;
+    const int n = n0 + cb * 8;
+    const bool side1 = n < p.D1;
+    const int rs = side1 ? p.D1 : p.Cout - p.D1;
+    const int co = side1 ? n : n - p.D1;
+    bf16* dst = (bf16*)(side1 ? p.dst1 : p.dst2);
+    const bf16* mk = (const bf16*)(side1 ? p.mask1 : p.mask2);
+    u32x4 mv[NIT];
+    if (mk) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int q = m0 + ml0 + it * RPI;
+        if (q < M) mv[it] = *(const u32x4*)(mk + (size_t)q * rs + co);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int ml = ml0 + it * RPI;
+      const int q = m0 + ml;
+      if (q >= M) continue;
+      const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
+      const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
+      u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
+      if (mk) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t w = mv[it][e];
+          const uint32_t lo16 = w & 0xffffu, hi16 = w >> 16;
+          const uint32_t keep_lo = (lo16 != 0u && !(lo16 & 0x8000u)) ? 0xffffu : 0u;
+          const uint32_t keep_hi = (hi16 != 0u && !(hi16 & 0x8000u)) ? 0xffff0000u : 0u;
+          v[e] &= (keep_lo | keep_hi);
+        }
+      }
+      *(u32x4*)(dst + (size_t)q * rs + co) = v;
+    }
+    return;
+  }
   const int Dt = kShuffle ? (p.Cout >> p.shuffle) : 0;
 #pragma unroll 2
   for (int c = tid; c < NCHUNK; c += NTHR) {

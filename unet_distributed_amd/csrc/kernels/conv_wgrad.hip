@@ -432,7 +432,7 @@ hipError_t launch_wg(WgradParams p, hipStream_t s) {
 
 
 // ---------------------------------------------------------------------------------
-// Row-window weight gradient (2D 3x3 stride 1 'same', full rows of W in {32,64,128}).
+// Row-window weight gradient (2D 3x3 stride 1 'same', full rows of W in {8,16,32,64,128}).
 //
 // The tiled kernel above stages one A image per tap (9 copies of the input tile):
 // at the fine levels, where Cin and Cout are 32..64, that LDS traffic bounds it at
@@ -457,7 +457,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   constexpr int PS = 4 / QO, KS = BMW / 32;
   constexpr int REDB = 4 * 64 * 16 * 4;                 // one tap of every wave's partials
   constexpr int LDS_BYTES = (XB + YB > REDB) ? XB + YB : REDB;
-  static_assert(W >= 32 && W <= 128 && (QO == 1 || QO == 2), "window wgrad shape");
+  static_assert(W >= 8 && W <= 128 && (QO == 1 || QO == 2), "window wgrad shape");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   char* Xs = smem;
   char* Ys = smem + XB;
@@ -562,16 +562,23 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
 #pragma unroll
         for (int j = 0; j < 2; ++j) bacc[j] = mfma16(ones, bf[j], bacc[j]);
       }
+      // lane pixel 8G + q (+4 for the second transposed read): for rows narrower than
+      // a 32-pixel step it lies lr rows below the step's first row, at column lc
+      const int lp = 8 * G + q;
+      const int lr = W >= 32 ? 0 : lp / W, lc = W >= 32 ? lp : lp - (lp / W) * W;
+      const int hl = W >= 32 ? h : (g + lr) % H;
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int dh = t / 3, dw = t % 3;
-        if ((dh == 0 && h == 0) || (dh == 2 && h == H - 1)) continue;   // zero-padding rows
-        const int colA = c0 + dw + 8 * G + q;       // halo column of this lane's first pixel
-        const int slotA = (rr + dh) * HWP + colA;
+        if (W >= 32 && ((dh == 0 && h == 0) || (dh == 2 && h == H - 1))) continue;   // zero-padding rows
+        const bool lane_ok = W >= 32 || !((dh == 0 && hl == 0) || (dh == 2 && hl == H - 1));
+        const int colA = c0 + dw + lc;              // halo column of this lane's first pixel
+        const int slotA = (rr + lr + dh) * HWP + colA;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const bf16x8 af = tr8(Xs + tr_addr(slotA, colA, 16 * i + 4 * pp),
-                                Xs + tr_addr(slotA + 4, colA + 4, 16 * i + 4 * pp));
+          bf16x8 af = tr8(Xs + tr_addr(slotA, colA, 16 * i + 4 * pp),
+                          Xs + tr_addr(slotA + 4, colA + 4, 16 * i + 4 * pp));
+          if (W < 32 && !lane_ok) af = __builtin_bit_cast(bf16x8, (u32x4){0u, 0u, 0u, 0u});
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[t][i][j] = mfma16(af, bf[j], acc[t][i][j]);
         }
@@ -633,10 +640,10 @@ hipError_t launch_wgrad_win(const WgradParams& p, hipStream_t s) {
 
 }  // namespace
 
-// Row-window wgrad applies to 2D 3x3 stride-1 'same' convs on full rows 32..128 wide
+// Row-window wgrad applies to 2D 3x3 stride-1 'same' convs on full rows 8..128 wide
 // (p.win < 0 disables it for A/B tests).
 static bool wgrad_win_eligible(const WgradParams& p) {
-  const bool w_ok = p.QW == 32 || p.QW == 64 || p.QW == 128;
+  const bool w_ok = p.QW == 8 || p.QW == 16 || p.QW == 32 || p.QW == 64 || p.QW == 128;
   return p.win >= 0 && w_ok && p.QD == 1 && p.KD == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 &&
          p.pad == 1 && p.upA == 1 && p.AW == p.QW && p.AH == p.QH && (p.M1 % 32) == 0 && (p.M2 % 32) == 0 &&
          p.M1 > 0 && (p.Nc % 32) == 0 && p.bias_mode != 2;
@@ -676,6 +683,8 @@ hipError_t wgrad_launch(const WgradParams& p, hipStream_t s) {
   if (wgrad_win_eligible(p)) {
     const bool q2 = c.BN == 64;
     switch (p.QW) {
+      case 8: return q2 ? launch_wgrad_win<8, 2>(p, s) : launch_wgrad_win<8, 1>(p, s);
+      case 16: return q2 ? launch_wgrad_win<16, 2>(p, s) : launch_wgrad_win<16, 1>(p, s);
       case 32: return q2 ? launch_wgrad_win<32, 2>(p, s) : launch_wgrad_win<32, 1>(p, s);
       case 64: return q2 ? launch_wgrad_win<64, 2>(p, s) : launch_wgrad_win<64, 1>(p, s);
       default: return q2 ? launch_wgrad_win<128, 2>(p, s) : launch_wgrad_win<128, 1>(p, s);
