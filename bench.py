@@ -122,7 +122,10 @@ def main():
     dice = (2 * i_ + 1) / (st + sp + 1)
     if ctx.rank == 0:
         rec = {
-            "metric": "images/sec (whole node) 2D UNet BraTS 128x128x4 training",
+            "metric": ("images/sec (whole node) 2D UNet BraTS 128x128x4 training"
+                       if (a.dims, a.img_size, a.in_channels) == (2, 128, 4) else
+                       "images/sec (whole node) %dD UNet %s x%d training"
+                       % (a.dims, "x".join([str(a.img_size)] * a.dims), a.in_channels)),
             "value": round(imgs / dt, 2),
             "unit": "images/sec",
             "n_gpus": N,
@@ -133,10 +136,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": a.dtype,
-            "data": "synthetic (BraTS-shaped %dx%dx%d slices, random-init weights)"
-                    % (a.img_size, a.img_size, a.in_channels),
-            "config": {"model": "unet2d-%s (base 32, depth 4, %d params)"
-                                % ("upsampling" if a.use_upsampling else "transposed", spec.num_params()),
+            "data": "synthetic (BraTS-shaped %s x%d %s, random-init weights)"
+                    % ("x".join([str(a.img_size)] * a.dims), a.in_channels, "slices" if a.dims == 2 else "volumes"),
+            "config": {"model": "unet%dd-%s (base 32, depth 4, %d params)"
+                                % (a.dims, "upsampling" if a.use_upsampling else "transposed", spec.num_params()),
                        "global_batch": B * N, "per_gpu_batch": B, "seq_len": None,
                        "img_size": a.img_size, "in_channels": a.in_channels,
                        "parallelism": "dp%d" % N, "backend": backend.name},
