@@ -36,6 +36,8 @@ def parse():
     p.add_argument("--in_channels", type=int, default=4)
     p.add_argument("--dims", type=int, default=2)
     p.add_argument("--use_upsampling", action="store_true")
+    p.add_argument("--norm", default="none", choices=["none", "batch", "group"])
+    p.add_argument("--groups", type=int, default=8)
     p.add_argument("--backend", default="auto", choices=["auto", "native", "torch"])
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp16"])
     p.add_argument("--bucket_mb", type=float, default=8.0)
@@ -64,6 +66,7 @@ def main():
         print("warning: --gpus %d but WORLD_SIZE %d" % (a.gpus, world_env), file=sys.stderr)
     cfg = Config(batch_size=a.per_gpu_batch * N, in_channels=a.in_channels, img_size=a.img_size,
                  dims=a.dims, use_upsampling=a.use_upsampling, backend=a.backend, dtype=a.dtype,
+                 norm=a.norm, groups=a.groups,
                  synthetic=True, no_checkpoint=True, bucket_mb=a.bucket_mb, overlap_comm=not a.no_overlap)
     dev = ctx.device
     spec = spec_from_config(cfg)
@@ -138,8 +141,9 @@ def main():
             "dtype": a.dtype,
             "data": "synthetic (BraTS-shaped %s x%d %s, random-init weights)"
                     % ("x".join([str(a.img_size)] * a.dims), a.in_channels, "slices" if a.dims == 2 else "volumes"),
-            "config": {"model": "unet%dd-%s (base 32, depth 4, %d params)"
-                                % (a.dims, "upsampling" if a.use_upsampling else "transposed", spec.num_params()),
+            "config": {"model": "unet%dd-%s%s (base 32, depth 4, %d params)"
+                                % (a.dims, "upsampling" if a.use_upsampling else "transposed",
+                                   "" if a.norm == "none" else "-" + a.norm + "norm", spec.num_params()),
                        "global_batch": B * N, "per_gpu_batch": B, "seq_len": None,
                        "img_size": a.img_size, "in_channels": a.in_channels,
                        "parallelism": "dp%d" % N, "backend": backend.name},

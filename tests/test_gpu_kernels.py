@@ -383,3 +383,62 @@ def test_dropout_matches_reference_hash(cuda_dev):
     assert rel_err(out, ref) < 1e-2
     frac = keep.float().mean().item()
     assert 0.75 < frac < 0.85
+
+
+@pytest.mark.parametrize("norm,N,H,Cc,G", [("batch", 4, 16, 32, 0), ("batch", 3, 8, 64, 0), ("group", 4, 16, 64, 8),
+                                           ("group", 2, 8, 32, 4)])
+def test_norm_fwd_bwd_kernels(cuda_dev, norm, N, H, Cc, G):
+    """BN / GN forward (batch statistics, ReLU) and backward (dz, dgamma, dbeta) against
+    autograd of the fp32 ATen ops on the same bf16 inputs."""
+    torch.manual_seed(31)
+    dev = cuda_dev
+    P = H * H
+    z = (torch.randn(N, H, H, Cc, device=dev) * 2 + 0.5).bfloat16()
+    gam = torch.rand(Cc, device=dev) + 0.5
+    bet = torch.randn(Cc, device=dev) * 0.1
+    g = torch.randn(N, H, H, Cc, device=dev).bfloat16()
+    nbp = C().norm_blocks_per_sample(N, P)
+    part = torch.zeros(N * nbp * 2 * Cc, device=dev)
+    S = torch.zeros(N * 2 * Cc, device=dev)
+    rows = 1 if norm == "batch" else N
+    mean, rstd, ca, cb, cc = [torch.zeros(rows * Cc, device=dev) for _ in range(5)]
+    rm, rv = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
+    dg, db = torch.zeros(Cc, device=dev), torch.zeros(Cc, device=dev)
+    y = torch.empty_like(z)
+    dz = torch.empty_like(z)
+    st = stream()
+    C().generic("norm_moments", [ptr(z), ptr(z), ptr(part), ptr(S)], [N, P, Cc], [], st)
+    if norm == "batch":
+        C().generic("bn_finalize", [ptr(S), ptr(gam), ptr(rm), ptr(rv), ptr(mean), ptr(rstd), 0, 0, 0, 0, 0],
+                    [N, Cc, 0], [float(N * P), 1e-3, 0.01], st)
+        cs = 0
+    else:
+        C().generic("gn_finalize", [ptr(S), ptr(gam), ptr(mean), ptr(rstd), 0, 0, 0, 0, 0], [N, Cc, G, P, 0], [1e-3], st)
+        cs = Cc
+    C().generic("norm_apply", [ptr(z), ptr(mean), ptr(rstd), ptr(gam), ptr(bet), ptr(y)], [N, P, Cc, cs, 1, 0, 0],
+                [0.0], st)
+    C().generic("norm_moments", [ptr(g), ptr(z), ptr(part), ptr(S)], [N, P, Cc], [], st)
+    if norm == "batch":
+        C().generic("bn_finalize", [ptr(S), ptr(gam), 0, 0, ptr(mean), ptr(rstd), ptr(ca), ptr(cb), ptr(cc), ptr(dg),
+                                    ptr(db)], [N, Cc, 1], [float(N * P), 1e-3, 0.01], st)
+    else:
+        C().generic("gn_finalize", [ptr(S), ptr(gam), ptr(mean), ptr(rstd), ptr(ca), ptr(cb), ptr(cc), ptr(dg),
+                                    ptr(db)], [N, Cc, G, P, 1], [1e-3], st)
+    C().generic("norm_bwd_apply", [ptr(g), ptr(z), ptr(ca), ptr(cb), ptr(cc), ptr(dz)], [N, P, Cc, cs], [], st)
+    torch.cuda.synchronize()
+    zr = nchw(z.float()).requires_grad_(True)
+    gr = gam.clone().requires_grad_(True)
+    br = bet.clone().requires_grad_(True)
+    if norm == "batch":
+        rmr, rvr = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
+        o = F.batch_norm(zr, rmr, rvr, gr, br, training=True, momentum=0.01, eps=1e-3)
+    else:
+        o = F.group_norm(zr, G, gr, br, eps=1e-3)
+    # the kernel's bwd input g is dL/d(norm output) already ReLU-masked by the consumer
+    yref = F.relu(o)
+    dzr, dgr, dbr = torch.autograd.grad(o, [zr, gr, br], nchw(g.float()))
+    assert rel_err(y, nhwc(yref)) < 1e-2
+    assert rel_err(dz, nhwc(dzr)) < 2e-2
+    assert rel_err(dg, dgr) < 1e-3 and rel_err(db, dbr) < 1e-3
+    if norm == "batch":
+        assert torch.allclose(rm, rmr, atol=1e-5) and torch.allclose(rv, rvr, atol=1e-4)

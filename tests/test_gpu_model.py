@@ -52,11 +52,18 @@ def test_native_step_matches_reference(cuda_dev, kw):
     assert torch.allclose(sn[:3], st[:3], rtol=3e-2, atol=1.0), (sn, st)
     for name, shape, off, n in fn.entries:
         gn, gt = fn.grad[off:off + n], ft.grad[off:off + n]
+        if gt.norm() < 1e-6:          # conv bias under BatchNorm: exactly 0 in exact arithmetic
+            assert gn.norm() < 1e-3, (name, gn.norm().item())
+            continue
         c = _cos(gn, gt)
-        # bias grads are plain sums of bf16 dY over few pixels at the coarse levels
-        assert c > (0.95 if name.endswith("/bias") else 0.98), (name, c, gn.norm().item(), gt.norm().item())
+        # bias grads are plain sums of bf16 dY over few pixels at the coarse levels; the
+        # normalisation backward (g - mean g - x^ mean g x^) cancels terms, which amplifies
+        # the bf16 storage rounding of g and z
+        tol = 0.95 if name.endswith("/bias") else 0.98
+        assert c > tol, (name, c, gn.norm().item(), gt.norm().item())
         r = (gn.norm() / (gt.norm() + 1e-30)).item()
         assert 0.9 < r < 1.1, (name, r)
+    assert _cos(fn.grad, ft.grad) > 0.99
 
 
 def test_native_adam_matches_reference(cuda_dev):
@@ -113,3 +120,48 @@ def test_native_inference_export_roundtrip(cuda_dev, tmp_path):
                                 torch.from_numpy(x).to(cuda_dev), train=False, dropout=False).cpu().numpy()
     assert p.shape == ref.shape
     assert np.abs(p - ref).max() < 0.05, np.abs(p - ref).max()
+
+
+@pytest.mark.parametrize("norm", ["batch", "group"])
+def test_native_norm_state_and_eval(cuda_dev, norm):
+    """BatchNorm running statistics follow the ATen momentum update; eval-mode sums
+    (BN: running stats, GN: per-sample stats) match the fp32 reference."""
+    spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, batch_size=4, img_size=64, in_channels=4, norm=norm)
+    for k in range(2):
+        nb.fwd_bwd(x, y, seed=5 + k)
+        tb.fwd_bwd(x, y, seed=5 + k)
+    torch.cuda.synchronize()
+    if norm == "batch":
+        assert set(nb.state) == set(tb.state)
+        for k in tb.state:
+            a, b = nb.state[k].float(), tb.state[k].float()
+            assert torch.allclose(a, b, rtol=3e-2, atol=3e-2), (k, (a - b).abs().max().item())
+    en, et = nb.eval_sums(x, y).cpu(), tb.eval_sums(x, y).cpu()
+    assert torch.allclose(en[:3], et[:3], rtol=5e-2, atol=2.0), (en, et)
+
+
+@pytest.mark.parametrize("norm", ["batch", "group"])
+def test_native_norm_step_matches_bf16_noise_floor(cuda_dev, norm):
+    """With BatchNorm / GroupNorm the backward cancels large terms, so any bf16 storage
+    drifts from fp32 layer by layer (ATen's own bf16 autocast reaches cos ~0.93 at the
+    bottleneck).  The native step must track the fp32 gradients at least as well as
+    ATen bf16 does (per layer, within 0.02) and match fp32 overall."""
+    from unet_distributed_amd.config import Config
+    from unet_distributed_amd.runtime.backends import TorchBackend
+    from unet_distributed_amd.runtime.params import FlatParams
+    from unet_distributed_amd.models import reference
+    kw = dict(batch_size=4, img_size=64, in_channels=4, norm=norm, groups=8)
+    spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
+    fb = FlatParams(spec, device=cuda_dev)
+    fb.load_dict(reference.init_params(spec, seed=3))
+    bb = TorchBackend(spec, fb, Config(**dict(kw, dtype="bf16")), cuda_dev, 4)
+    for be in (nb, tb, bb):
+        be.fwd_bwd(x, y, seed=77)
+    torch.cuda.synchronize()
+    for name, shape, off, n in fn.entries:
+        g32 = ft.grad[off:off + n]
+        if g32.norm() < 1e-6:
+            continue
+        cn, cb = _cos(fn.grad[off:off + n], g32), _cos(fb.grad[off:off + n], g32)
+        assert cn > cb - 0.02, (name, cn, cb)
+    assert _cos(fn.grad, ft.grad) > 0.98

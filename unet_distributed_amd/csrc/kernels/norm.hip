@@ -1,0 +1,313 @@
+// BatchNorm / GroupNorm for the native executor (the [EXT] `--norm batch|group`
+// variants of the reference's conv blocks, models/reference.py::_norm:
+// torch F.batch_norm(momentum=0.01, eps=1e-3) / F.group_norm(eps=1e-3)).
+//
+// Layout: NHWC bf16, a conv layer's pre-norm output z[N][P][C] (P pixels per sample).
+// Every statistic the forward and backward need is a per-(sample, channel) pair of
+// sums over pixels, so one deterministic reduction kernel serves both:
+//   forward   S1 = sum z,   S2 = sum z^2
+//   backward  S1 = sum g,   S2 = sum g*z      (g = dL/d(norm output), ReLU-masked)
+// BatchNorm aggregates the pairs over samples per channel, GroupNorm over the
+// channels of a group per sample.  With x^ = (z - mu) r the backward is
+//   dz = a*g + b*z + c   with per-(n, c) coefficients
+//   BN: a = gamma r, b = -gamma r^2 m2, c = -gamma r m1 + gamma r^2 mu m2
+//       (m1 = mean g, m2 = mean g x^ over N*P),
+//   GN: a = gamma_c r, b = -r^2 M2, c = -r M1 + r^2 mu M2
+//       (M1 = mean gamma g, M2 = mean gamma g x^ over P * C/G of the group),
+// and dgamma_c = sum_n r (S2 - mu S1), dbeta_c = sum_n S1.
+// No float atomics anywhere: block partials are reduced in a fixed order.
+#include "common.h"
+
+namespace unet {
+
+namespace {
+
+constexpr int NT = 256;
+
+// partial[(n * nbp + blk)][2][C]: sums over this block's pixels of sample n
+__global__ void __launch_bounds__(NT) chan_moments_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                          int P, int C, int nbp, float* __restrict__ partial) {
+  extern __shared__ float red[];   // [NT][2][8]
+  const int n = blockIdx.x / nbp, blk = blockIdx.x - n * nbp;
+  const int cpr = C / 8;                       // 16-byte chunk columns
+  const int cc = threadIdx.x % cpr, rs = threadIdx.x / cpr, rstep = NT / cpr;
+  const int p0 = (int)((long long)blk * P / nbp), p1 = (int)((long long)(blk + 1) * P / nbp);
+  float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rs < rstep) {
+    const size_t base = (size_t)n * P * C + cc * 8;
+    for (int p = p0 + rs; p < p1; p += rstep) {
+      float a[8], b[8];
+      unpack8(*(const u32x4*)(A + base + (size_t)p * C), a);
+      unpack8(*(const u32x4*)(B + base + (size_t)p * C), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += a[e];
+        s2[e] += a[e] * b[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[(threadIdx.x * 2 + 0) * 8 + e] = s1[e];
+    red[(threadIdx.x * 2 + 1) * 8 + e] = s2[e];
+  }
+  __syncthreads();
+  // thread t < 2C sums its (moment, channel) over the row-threads in order
+  for (int t = threadIdx.x; t < 2 * C; t += NT) {
+    const int mom = t / C, c = t - mom * C;
+    const int col = c / 8, e = c & 7;
+    float s = 0.f;
+    for (int r = 0; r < rstep; ++r) s += red[((r * cpr + col) * 2 + mom) * 8 + e];
+    partial[((size_t)blockIdx.x * 2 + mom) * C + c] = s;
+  }
+}
+
+// S[n][2][C] = sum over the nbp block partials of sample n
+__global__ void __launch_bounds__(NT) moments_collect_kernel(const float* __restrict__ partial, int N, int C, int nbp,
+                                                             float* __restrict__ S) {
+  const int total = N * 2 * C;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const int n = i / (2 * C), r = i - n * 2 * C;
+    float s = 0.f;
+    for (int b = 0; b < nbp; ++b) s += partial[((size_t)n * nbp + b) * 2 * C + r];
+    S[i] = s;
+  }
+}
+
+// BatchNorm per channel (grid: C / 64 blocks of 64 channels x 4 sample slices).
+//   mode 0 (forward, training): mean/rstd[c] from the batch, running stats updated
+//   mode 1 (backward): coefficients a/b/c[c], dgamma/dbeta
+//   mode 2 (forward, inference): mean/rstd[c] from the running stats
+__global__ void __launch_bounds__(NT) bn_finalize_kernel(const float* __restrict__ S, int N, int C, float count,
+                                                         int mode, const float* __restrict__ gamma, float eps,
+                                                         float momentum, float* __restrict__ run_mean,
+                                                         float* __restrict__ run_var, float* __restrict__ mean,
+                                                         float* __restrict__ rstd, float* __restrict__ ca,
+                                                         float* __restrict__ cb, float* __restrict__ cc,
+                                                         float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float red[4][2][64];
+  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s1 = 0.f, s2 = 0.f;
+  if (c < C && mode != 2) {
+    for (int n = sl; n < N; n += 4) {
+      s1 += S[((size_t)n * 2 + 0) * C + c];
+      s2 += S[((size_t)n * 2 + 1) * C + c];
+    }
+  }
+  red[sl][0][cl] = s1;
+  red[sl][1][cl] = s2;
+  __syncthreads();
+  if (sl != 0 || c >= C) return;
+  s1 = red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl];
+  s2 = red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl];
+  if (mode == 0) {
+    const float mu = s1 / count;
+    const float var = fmaxf(s2 / count - mu * mu, 0.f);
+    mean[c] = mu;
+    rstd[c] = rsqrtf(var + eps);
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * (count / fmaxf(count - 1.f, 1.f));
+  } else if (mode == 2) {
+    mean[c] = run_mean[c];
+    rstd[c] = rsqrtf(run_var[c] + eps);
+  } else {
+    const float mu = mean[c], r = rstd[c], gm = gamma[c];
+    const float sgx = r * (s2 - mu * s1);       // sum g x^
+    dbeta[c] = s1;
+    dgamma[c] = sgx;
+    const float m1 = s1 / count, m2 = sgx / count;
+    ca[c] = gm * r;
+    cb[c] = -gm * r * r * m2;
+    cc[c] = -gm * r * m1 + gm * r * r * mu * m2;
+  }
+}
+
+// GroupNorm per (sample, group): one thread per (n, g).
+//   mode 0: mean/rstd[n][c] (training and inference are the same)
+//   mode 1: coefficients a/b/c[n][c]
+__global__ void __launch_bounds__(NT) gn_finalize_kernel(const float* __restrict__ S, int N, int C, int G, float P,
+                                                         int mode, const float* __restrict__ gamma, float eps,
+                                                         float* __restrict__ mean, float* __restrict__ rstd,
+                                                         float* __restrict__ ca, float* __restrict__ cb,
+                                                         float* __restrict__ cc) {
+  const int i = blockIdx.x * NT + threadIdx.x;
+  if (i >= N * G) return;
+  const int n = i / G, g = i - n * G;
+  const int Cg = C / G;
+  const float count = P * Cg;
+  const float* S1 = S + (size_t)n * 2 * C;
+  const float* S2 = S1 + C;
+  if (mode == 0) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+      s1 += S1[c];
+      s2 += S2[c];
+    }
+    const float mu = s1 / count;
+    const float r = rsqrtf(fmaxf(s2 / count - mu * mu, 0.f) + eps);
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+      mean[(size_t)n * C + c] = mu;
+      rstd[(size_t)n * C + c] = r;
+    }
+  } else {
+    const float mu = mean[(size_t)n * C + g * Cg], r = rstd[(size_t)n * C + g * Cg];
+    float M1 = 0.f, M2 = 0.f;
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+      M1 += gamma[c] * S1[c];
+      M2 += gamma[c] * r * (S2[c] - mu * S1[c]);
+    }
+    M1 /= count;
+    M2 /= count;
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+      ca[(size_t)n * C + c] = gamma[c] * r;
+      cb[(size_t)n * C + c] = -r * r * M2;
+      cc[(size_t)n * C + c] = -r * M1 + r * r * mu * M2;
+    }
+  }
+}
+
+// GroupNorm parameter gradients (per channel over samples), thread per channel
+__global__ void __launch_bounds__(NT) gn_param_grad_kernel(const float* __restrict__ S, int N, int C,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  float db = 0.f, dg = 0.f;
+  for (int n = 0; n < N; ++n) {
+    const float s1 = S[((size_t)n * 2 + 0) * C + c], s2 = S[((size_t)n * 2 + 1) * C + c];
+    db += s1;
+    dg += rstd[(size_t)n * C + c] * (s2 - mean[(size_t)n * C + c] * s1);
+  }
+  dgamma[c] = dg;
+  dbeta[c] = db;
+}
+
+// y = relu(gamma (z - mean) rstd + beta) with optional inverted dropout (counter hash,
+// same stream as the conv epilogue's); coefficient arrays are [C] (cstride 0) or [N][C]
+__global__ void __launch_bounds__(NT) norm_apply_kernel(const bf16* __restrict__ z, int N, int P, int C,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd, int cstride,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, int relu, float drop_rate,
+                                                        uint32_t seed, uint32_t salt, bf16* __restrict__ y) {
+  const int cpr = C / 8;
+  const long long total = (long long)N * P * cpr;
+  const float inv_keep = drop_rate > 0.f ? 1.f / (1.f - drop_rate) : 1.f;
+  const uint32_t thr = (uint32_t)(drop_rate * 4294967296.0);
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int cc = (int)(i % cpr);
+    const long long q = i / cpr;
+    const int n = (int)(q / P);
+    const int c0 = cc * 8;
+    float v[8];
+    unpack8(*(const u32x4*)(z + q * C + c0), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c0 + e;
+      const size_t k = (size_t)n * cstride + c;
+      float x = gamma[c] * (v[e] - mean[k]) * rstd[k] + beta[c];
+      if (relu) x = fmaxf(x, 0.f);
+      if (drop_rate > 0.f) {
+        const uint32_t h = drop_hash((uint64_t)q * C + c, seed, salt);
+        x = (h >= thr) ? x * inv_keep : 0.f;
+      }
+      v[e] = x;
+    }
+    *(u32x4*)(y + q * C + c0) = pack8(v);
+  }
+}
+
+// dz = a g + b z + c  (coefficients [C] or [N][C])
+__global__ void __launch_bounds__(NT) norm_bwd_apply_kernel(const bf16* __restrict__ g, const bf16* __restrict__ z,
+                                                            int N, int P, int C, const float* __restrict__ ca,
+                                                            const float* __restrict__ cb,
+                                                            const float* __restrict__ ccf, int cstride,
+                                                            bf16* __restrict__ dz) {
+  const int cpr = C / 8;
+  const long long total = (long long)N * P * cpr;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int cc = (int)(i % cpr);
+    const long long q = i / cpr;
+    const int n = (int)(q / P);
+    const int c0 = cc * 8;
+    float gv[8], zv[8];
+    unpack8(*(const u32x4*)(g + q * C + c0), gv);
+    unpack8(*(const u32x4*)(z + q * C + c0), zv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const size_t k = (size_t)n * cstride + c0 + e;
+      gv[e] = ca[k] * gv[e] + cb[k] * zv[e] + ccf[k];
+    }
+    *(u32x4*)(dz + q * C + c0) = pack8(gv);
+  }
+}
+
+int ew_grid(long long work) {
+  long long b = (work + NT - 1) / NT;
+  return (int)(b < 8192 ? (b < 1 ? 1 : b) : 8192);
+}
+
+}  // namespace
+
+int norm_blocks_per_sample(int N, int P) {
+  int nbp = (512 + N - 1) / N;
+  const int maxb = (P + 63) / 64;
+  if (nbp > maxb) nbp = maxb;
+  return nbp < 1 ? 1 : nbp;
+}
+
+const char* norm_check(int C, int G) {
+  if (C % 8) return "norm: channels must be a multiple of 8";
+  if (C > 2048) return "norm: at most 2048 channels";
+  if (G > 0 && C % G) return "norm: channels not divisible by groups";
+  return nullptr;
+}
+
+// stats over pixels per (sample, channel): partial [N*nbp][2][C], S [N][2][C]
+hipError_t norm_moments_launch(const void* A, const void* B, int N, int P, int C, float* partial, float* S,
+                               hipStream_t s) {
+  const int nbp = norm_blocks_per_sample(N, P);
+  hipLaunchKernelGGL(chan_moments_kernel, dim3(N * nbp), dim3(NT), NT * 2 * 8 * sizeof(float), s,
+                     (const bf16*)A, (const bf16*)B, P, C, nbp, partial);
+  hipLaunchKernelGGL(moments_collect_kernel, dim3(ew_grid((long long)N * 2 * C)), dim3(NT), 0, s, partial, N, C, nbp,
+                     S);
+  return hipGetLastError();
+}
+
+hipError_t bn_finalize_launch(const float* S, int N, int C, float count, int mode, const float* gamma, float eps,
+                              float momentum, float* run_mean, float* run_var, float* mean, float* rstd, float* ca,
+                              float* cb, float* cc, float* dgamma, float* dbeta, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(NT), 0, s, S, N, C, count, mode, gamma, eps,
+                     momentum, run_mean, run_var, mean, rstd, ca, cb, cc, dgamma, dbeta);
+  return hipGetLastError();
+}
+
+hipError_t gn_finalize_launch(const float* S, int N, int C, int G, int P, int mode, const float* gamma, float eps,
+                              float* mean, float* rstd, float* ca, float* cb, float* cc, float* dgamma, float* dbeta,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((N * G + NT - 1) / NT), dim3(NT), 0, s, S, N, C, G, (float)P, mode,
+                     gamma, eps, mean, rstd, ca, cb, cc);
+  if (mode == 1)
+    hipLaunchKernelGGL(gn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, S, N, C, mean, rstd, dgamma,
+                       dbeta);
+  return hipGetLastError();
+}
+
+hipError_t norm_apply_launch(const void* z, int N, int P, int C, const float* mean, const float* rstd, int cstride,
+                             const float* gamma, const float* beta, int relu, float drop_rate, uint32_t seed,
+                             uint32_t salt, void* y, hipStream_t s) {
+  hipLaunchKernelGGL(norm_apply_kernel, dim3(ew_grid((long long)N * P * (C / 8))), dim3(NT), 0, s, (const bf16*)z, N,
+                     P, C, mean, rstd, cstride, gamma, beta, relu, drop_rate, seed, salt, (bf16*)y);
+  return hipGetLastError();
+}
+
+hipError_t norm_bwd_apply_launch(const void* g, const void* z, int N, int P, int C, const float* ca, const float* cb,
+                                 const float* cc, int cstride, void* dz, hipStream_t s) {
+  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(ew_grid((long long)N * P * (C / 8))), dim3(NT), 0, s,
+                     (const bf16*)g, (const bf16*)z, N, P, C, ca, cb, cc, cstride, (bf16*)dz);
+  return hipGetLastError();
+}
+
+}  // namespace unet

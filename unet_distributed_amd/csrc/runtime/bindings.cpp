@@ -136,8 +136,10 @@ WgradParams wgrad_params(const py::dict& d) {
 using Launcher = std::function<hipError_t(hipStream_t)>;
 
 // generic memory-bound ops: (kind, pointer args, int args, float args)
+// seedp: the owning plan's per-step dropout seed (nullptr for immediate calls: the
+// seed is then the op's last int argument)
 Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, const std::vector<long long>& I,
-                      const std::vector<double>& F) {
+                      const std::vector<double>& F, const uint32_t* seedp = nullptr) {
   auto need = [&](size_t np, size_t ni, size_t nf) {
     if (P.size() < np || I.size() < ni || F.size() < nf)
       throw std::invalid_argument("generic op '" + kind + "': wrong argument count");
@@ -225,6 +227,66 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     check_msg(head_check(C));
     return [=](hipStream_t s) { return head_bwd_launch(x, w, prob, t, sums, P_, C, it, bw, gs, dx, part, gw, gb, s); };
   }
+  if (kind == "norm_moments") {
+    // ptrs: A, B, partial, S   ints: N, P, C    (S[n][2][C] = per-sample sums of A and A*B)
+    need(4, 3, 0);
+    void *a = vp(0), *b = vp(1);
+    float *part = (float*)vp(2), *S = (float*)vp(3);
+    int n = I[0], np = I[1], c = I[2];
+    check_msg(norm_check(c, 0));
+    return [=](hipStream_t s) { return norm_moments_launch(a, b, n, np, c, part, S, s); };
+  }
+  if (kind == "bn_finalize") {
+    // ptrs: S, gamma, run_mean, run_var, mean, rstd, ca, cb, cc, dgamma, dbeta  ints: N, C, mode
+    // floats: count, eps, momentum
+    need(11, 3, 3);
+    const float* S = (const float*)vp(0);
+    const float* gm = (const float*)vp(1);
+    float *rm = (float*)vp(2), *rv = (float*)vp(3), *mu = (float*)vp(4), *rs = (float*)vp(5);
+    float *ca = (float*)vp(6), *cb = (float*)vp(7), *cc = (float*)vp(8), *dg = (float*)vp(9), *db = (float*)vp(10);
+    int n = I[0], c = I[1], mode = I[2];
+    float cnt = (float)F[0], eps = (float)F[1], mom = (float)F[2];
+    return [=](hipStream_t s) {
+      return bn_finalize_launch(S, n, c, cnt, mode, gm, eps, mom, rm, rv, mu, rs, ca, cb, cc, dg, db, s);
+    };
+  }
+  if (kind == "gn_finalize") {
+    // ptrs: S, gamma, mean, rstd, ca, cb, cc, dgamma, dbeta   ints: N, C, G, P, mode   floats: eps
+    need(9, 5, 1);
+    const float* S = (const float*)vp(0);
+    const float* gm = (const float*)vp(1);
+    float *mu = (float*)vp(2), *rs = (float*)vp(3), *ca = (float*)vp(4), *cb = (float*)vp(5), *cc = (float*)vp(6);
+    float *dg = (float*)vp(7), *db = (float*)vp(8);
+    int n = I[0], c = I[1], g = I[2], np = I[3], mode = I[4];
+    float eps = (float)F[0];
+    check_msg(norm_check(c, g));
+    return [=](hipStream_t s) { return gn_finalize_launch(S, n, c, g, np, mode, gm, eps, mu, rs, ca, cb, cc, dg, db, s); };
+  }
+  if (kind == "norm_apply") {
+    // ptrs: z, mean, rstd, gamma, beta, y   ints: N, P, C, cstride, relu, salt[, seed]   floats: drop_rate
+    need(6, 6, 1);
+    void* z = vp(0);
+    const float *mu = (const float*)vp(1), *rs = (const float*)vp(2), *gm = (const float*)vp(3),
+                *bt = (const float*)vp(4);
+    void* y = vp(5);
+    int n = I[0], np = I[1], c = I[2], cs = I[3], relu = I[4];
+    uint32_t salt = (uint32_t)I[5], seed0 = I.size() > 6 ? (uint32_t)I[6] : 0u;
+    float dr = (float)F[0];
+    check_msg(norm_check(c, 0));
+    return [=](hipStream_t s) {
+      return norm_apply_launch(z, n, np, c, mu, rs, cs, gm, bt, relu, dr, seedp ? *seedp : seed0, salt, y, s);
+    };
+  }
+  if (kind == "norm_bwd_apply") {
+    // ptrs: g, z, ca, cb, cc, dz   ints: N, P, C, cstride
+    need(6, 4, 0);
+    void *g = vp(0), *z = vp(1);
+    const float *ca = (const float*)vp(2), *cb = (const float*)vp(3), *cc = (const float*)vp(4);
+    void* dz = vp(5);
+    int n = I[0], np = I[1], c = I[2], cs = I[3];
+    check_msg(norm_check(c, 0));
+    return [=](hipStream_t s) { return norm_bwd_apply_launch(g, z, n, np, c, ca, cb, cc, cs, dz, s); };
+  }
   if (kind == "memset") {
     need(1, 1, 0);
     void* p = vp(0);
@@ -257,7 +319,7 @@ class Plan {
   }
   int add_generic(const std::string& kind, const std::vector<uintptr_t>& P, const std::vector<long long>& I,
                   const std::vector<double>& F, const std::string& name) {
-    ops_.push_back(make_generic(kind, P, I, F));
+    ops_.push_back(make_generic(kind, P, I, F, &seed_));
     names_.push_back(name.empty() ? kind : name);
     return (int)ops_.size() - 1;
   }
@@ -306,6 +368,7 @@ PYBIND11_MODULE(_C, m) {
           "adam_pack");
   });
   m.def("head_blocks", &head_blocks_py);
+  m.def("norm_blocks_per_sample", &norm_blocks_per_sample);
   m.def("wgrad_reduce_stage_floats", &wgrad_reduce_stage_floats);
   // QW > 0 describes a 2D 3x3 stride-1 'same' conv on QW-wide rows (row-window candidate)
   m.def(

@@ -35,6 +35,22 @@ hipError_t head_bwd_launch(const void* x, const float* w, const float* prob, con
                            float* gb, hipStream_t s);
 hipError_t partial_reduce_launch(const float* partial, int nb, int width, float* out, hipStream_t s);
 
+int norm_blocks_per_sample(int N, int P);
+const char* norm_check(int C, int G);
+hipError_t norm_moments_launch(const void* A, const void* B, int N, int P, int C, float* partial, float* S,
+                               hipStream_t s);
+hipError_t bn_finalize_launch(const float* S, int N, int C, float count, int mode, const float* gamma, float eps,
+                              float momentum, float* run_mean, float* run_var, float* mean, float* rstd, float* ca,
+                              float* cb, float* cc, float* dgamma, float* dbeta, hipStream_t s);
+hipError_t gn_finalize_launch(const float* S, int N, int C, int G, int P, int mode, const float* gamma, float eps,
+                              float* mean, float* rstd, float* ca, float* cb, float* cc, float* dgamma, float* dbeta,
+                              hipStream_t s);
+hipError_t norm_apply_launch(const void* z, int N, int P, int C, const float* mean, const float* rstd, int cstride,
+                             const float* gamma, const float* beta, int relu, float drop_rate, uint32_t seed,
+                             uint32_t salt, void* y, hipStream_t s);
+hipError_t norm_bwd_apply_launch(const void* g, const void* z, int N, int P, int C, const float* ca, const float* cb,
+                                 const float* cc, int cstride, void* dz, hipStream_t s);
+
 const char* adam_check(int nseg);
 hipError_t adam_pack_launch(float* w, const float* g, float* m, float* v, int n_total, const void* segs, int nseg,
                             float lr_t, float b1, float b2, float eps, float gscale, int do_adam, void* arena,

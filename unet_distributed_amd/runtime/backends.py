@@ -102,6 +102,7 @@ class NativeBackend:
                                  bce_weight=cfg.bce_weight, bucket_bounds=bounds,
                                  eval_dropout=cfg.eval_dropout)
         self.B = per_rank_batch
+        self.state = self.engine.state        # BatchNorm running statistics (checkpointed)
 
     def set_buckets(self, bounds):
         self.engine.set_buckets(bounds)
@@ -141,8 +142,6 @@ def native_supported(spec, cfg, device) -> Optional[str]:
         return "not on a GPU"
     if cfg.dtype != "bf16":
         return "native kernels are bf16 (dtype=%s)" % cfg.dtype
-    if spec.norm != "none":
-        return "norm=%s not in the native executor yet" % spec.norm
     if spec.n_cl_out != 1:
         return "n_cl_out != 1"
     if spec.base % 32:

@@ -57,8 +57,8 @@ class NativeUNet:
                  bucket_bounds: Optional[Sequence[int]] = None, eval_dropout: bool = False,
                  dry_run: bool = False):
         self.C = native.require()
-        if spec.norm != "none":
-            raise NotImplementedError("native executor: norm=%s not implemented" % spec.norm)
+        if spec.norm not in ("none", "batch", "group"):
+            raise NotImplementedError("native executor: norm=%s" % spec.norm)
         if spec.n_cl_out != 1:
             raise NotImplementedError("native executor: n_cl_out must be 1")
         self.spec = spec
@@ -92,7 +92,7 @@ class NativeUNet:
         self._layer_done_at: Dict[str, int] = {}
         self._build_backward(self.plan)
         self.bwd_end = self.plan.size()
-        self._build_forward(self.eval_plan, dropout=eval_dropout)
+        self._build_forward(self.eval_plan, dropout=eval_dropout, train=False)
         self.set_buckets(bucket_bounds)
         if not dry_run:          # dry_run: plan construction only (CPU tests, no GPU launches)
             self.repack()
@@ -250,6 +250,94 @@ class NativeUNet:
                     self.bufs["dfull:" + src1] = torch.empty(shape, dtype=BF16, device=self.device)
         self.slab = None
         self.bias_slab = None
+        self._alloc_norm()
+
+    # ------------------------------------------------------------------ normalisation
+    NORM_EPS = 1e-3          # models/reference.py::_norm (Keras default epsilon)
+    BN_MOMENTUM = 0.01       # torch convention = Keras momentum 0.99
+
+    def _alloc_norm(self):
+        """Per normalised conv layer: the pre-norm conv output z:<L>, its gradient
+        dz:<L>, per-(sample|batch, channel) mean / rstd saved for the backward,
+        backward coefficients; BatchNorm running statistics (``self.state``, the
+        same names as the ATen backend so checkpoints are interchangeable)."""
+        self.state: Dict[str, torch.Tensor] = {}
+        self.norm_layers = []
+        if self.spec.norm == "none":
+            return
+        f32 = torch.float32
+        maxS = maxPart = 1
+        for l in self.spec.layers:
+            if l.kind != "conv":
+                continue
+            self.norm_layers.append(l.name)
+            self.bufs["z:" + l.name] = torch.empty_like(self.bufs[l.name])
+            self.bufs["dz:" + l.name] = torch.empty_like(self.bufs[l.name])
+            rows = 1 if self.spec.norm == "batch" else self.B
+            for k in ("mean", "rstd", "ca", "cb", "cc"):
+                self.bufs["%s:%s" % (k, l.name)] = torch.zeros(rows * l.cout, dtype=f32, device=self.device)
+            if self.spec.norm == "batch":
+                self.state[l.name + "/norm/moving_mean"] = torch.zeros(l.cout, dtype=f32, device=self.device)
+                self.state[l.name + "/norm/moving_variance"] = torch.ones(l.cout, dtype=f32, device=self.device)
+            P = self.npix(l.level) // self.B
+            nbp = self.C.norm_blocks_per_sample(self.B, P)
+            maxS = max(maxS, self.B * 2 * l.cout)
+            maxPart = max(maxPart, self.B * nbp * 2 * l.cout)
+        self.norm_S = torch.zeros(maxS, dtype=f32, device=self.device)
+        self.norm_part = torch.zeros(maxPart, dtype=f32, device=self.device)
+
+    def _norm_fwd(self, plan, l, dropout, train):
+        """z:<L> -> activation <L> = relu(norm(z)) (+ dropout)."""
+        b, spec = self.bufs, self.spec
+        C, P, N = l.cout, self.npix(l.level) // self.B, self.B
+        z = b["z:" + l.name]
+        mean, rstd = b["mean:" + l.name], b["rstd:" + l.name]
+        gamma, beta = self.master_ptr(l.name + "/norm/gamma"), self.master_ptr(l.name + "/norm/beta")
+        if spec.norm == "batch":
+            rm = self.state[l.name + "/norm/moving_mean"]
+            rv = self.state[l.name + "/norm/moving_variance"]
+            if train:
+                plan.add_generic("norm_moments", [_ptr(z), _ptr(z), _ptr(self.norm_part), _ptr(self.norm_S)],
+                                 [N, P, C], [], "bnstat:" + l.name)
+            plan.add_generic("bn_finalize", [_ptr(self.norm_S), gamma, _ptr(rm), _ptr(rv), _ptr(mean), _ptr(rstd),
+                                             0, 0, 0, 0, 0],
+                             [N, C, 0 if train else 2], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM],
+                             "bnfin:" + l.name)
+            cstride = 0
+        else:
+            plan.add_generic("norm_moments", [_ptr(z), _ptr(z), _ptr(self.norm_part), _ptr(self.norm_S)],
+                             [N, P, C], [], "gnstat:" + l.name)
+            plan.add_generic("gn_finalize", [_ptr(self.norm_S), gamma, _ptr(mean), _ptr(rstd), 0, 0, 0, 0, 0],
+                             [N, C, spec.groups, P, 0], [self.NORM_EPS], "gnfin:" + l.name)
+            cstride = C
+        plan.add_generic("norm_apply", [_ptr(z), _ptr(mean), _ptr(rstd), gamma, beta, _ptr(b[l.name])],
+                         [N, P, C, cstride, 1, self._salt(l.name)],
+                         [spec.dropout if (l.dropout and dropout) else 0.0], "norm:" + l.name)
+
+    def _norm_bwd_ops(self, l):
+        """(kind, ptrs, ints, floats, name) of d:<L> -> dz:<L> plus gamma/beta grads."""
+        b, spec = self.bufs, self.spec
+        C, P, N = l.cout, self.npix(l.level) // self.B, self.B
+        g, z, dz = b["d:" + l.name], b["z:" + l.name], b["dz:" + l.name]
+        mean, rstd = b["mean:" + l.name], b["rstd:" + l.name]
+        ca, cb, cc = b["ca:" + l.name], b["cb:" + l.name], b["cc:" + l.name]
+        gamma = self.master_ptr(l.name + "/norm/gamma")
+        dgam, dbet = self.grad_ptr(l.name + "/norm/gamma"), self.grad_ptr(l.name + "/norm/beta")
+        ops = [("norm_moments", [_ptr(g), _ptr(z), _ptr(self.norm_part), _ptr(self.norm_S)], [N, P, C], [],
+                "nstat_bwd:" + l.name)]
+        if spec.norm == "batch":
+            ops.append(("bn_finalize", [_ptr(self.norm_S), gamma, 0, 0, _ptr(mean), _ptr(rstd), _ptr(ca), _ptr(cb),
+                                        _ptr(cc), dgam, dbet],
+                        [N, C, 1], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM], "bnfin_bwd:" + l.name))
+            cstride = 0
+        else:
+            ops.append(("gn_finalize", [_ptr(self.norm_S), gamma, _ptr(mean), _ptr(rstd), _ptr(ca), _ptr(cb),
+                                        _ptr(cc), dgam, dbet],
+                        [N, C, spec.groups, P, 1], [self.NORM_EPS], "gnfin_bwd:" + l.name))
+            cstride = C
+        ops.append(("norm_bwd_apply", [_ptr(g), _ptr(z), _ptr(ca), _ptr(cb), _ptr(cc), _ptr(dz)],
+                    [N, P, C, cstride], [], "norm_bwd:" + l.name))
+        return ops
 
     # ------------------------------------------------------------------ plans
     def _conv_common(self, level, K, stride, pad, out_level=None, in_level=None):
@@ -263,7 +351,7 @@ class NativeUNet:
     def _salt(self, lname):
         return [l.name for l in self.spec.layers].index(lname)
 
-    def _build_forward(self, plan, dropout):
+    def _build_forward(self, plan, dropout, train=True):
         spec = self.spec
         b = self.bufs
         P1 = self.npix(1)
@@ -274,13 +362,17 @@ class NativeUNet:
                 src1, up1, skip = self.inputs[l.name]
                 c1 = self.tinfo[src1][1]
                 d = self._conv_common(l.level, 3, 1, 1)
+                normed = spec.norm != "none"
                 d.update(name="fwd:" + l.name, C1=c1, C2=self.tinfo[skip][1] if skip else 0, up1=up1,
                          src1=_ptr(b[src1]), src2=_ptr(b[skip]) if skip else None,
                          wgt=self.wptr(l.name), bias=self.master_ptr(l.name + "/bias"),
-                         Cout=l.cout, relu=1, dst1=_ptr(b[l.name]),
-                         drop_rate=spec.dropout if (l.dropout and dropout) else 0.0,
+                         Cout=l.cout, relu=0 if normed else 1,
+                         dst1=_ptr(b["z:" + l.name] if normed else b[l.name]),
+                         drop_rate=spec.dropout if (l.dropout and dropout and not normed) else 0.0,
                          salt=self._salt(l.name))
                 plan.add_conv_fwd(d)
+                if normed:
+                    self._norm_fwd(plan, l, dropout, train)
             elif l.kind == "pool":
                 src = self.inputs[l.name][0]
                 dd, hh, ww = self.sdims(l.level)
@@ -369,6 +461,10 @@ class NativeUNet:
                 c1 = self.tinfo[src1][1]
                 c2 = self.tinfo[skip][1] if skip else 0
                 dy = b["d:" + l.name]
+                if spec.norm != "none":
+                    for kind, P_, I_, F_, nm in self._norm_bwd_ops(l):
+                        ops.append(lambda pl, kind=kind, P_=P_, I_=I_, F_=F_, nm=nm: pl.add_generic(kind, P_, I_, F_, nm))
+                    dy = b["dz:" + l.name]
                 Q = self.npix(l.level)
                 # --- weight + bias gradient (fused column sums)
                 kd = dict(N=self.B, QD=self.sdims(l.level)[0], QH=self.sdims(l.level)[1],
