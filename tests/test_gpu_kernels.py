@@ -165,16 +165,19 @@ def test_conv_row_window_dgrad_dual_dest_mask_dropout(cuda_dev):
         assert rel_err(d2, g[..., C1:] * (skip.float() > 0) * 1.25) < 1e-2
 
 
-def test_conv_first_layer_smallc(cuda_dev):
+@pytest.mark.parametrize("N,H,Cin,Co,tile", [(2, 32, 4, 32, 0), (3, 128, 4, 32, 9), (5, 16, 4, 64, 9),
+                                             (2, 64, 8, 32, 9), (2, 32, 4, 32, 8), (2, 32, 8, 64, 8)])
+def test_conv_first_layer_smallc(cuda_dev, N, H, Cin, Co, tile):
+    """First layer (padded 4/8 channels): row-window kernel (tile 9, auto) and the
+    implicit-GEMM small-C mode (tile 8)."""
     torch.manual_seed(3)
-    N, H, Cin, Co = 2, 32, 4, 32
     x = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
     w = (torch.randn(3, 3, Cin, Co, device=cuda_dev) * 0.2).bfloat16()
     b = torch.randn(Co, device=cuda_dev)
     wp = pack_fwd(w)
     out = torch.empty(N, H, H, Co, device=cuda_dev, dtype=torch.bfloat16)
     C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(x), wgt=ptr(wp),
-                      bias=ptr(b), Cout=Co, relu=1, dst1=ptr(out)), stream())
+                      bias=ptr(b), Cout=Co, relu=1, dst1=ptr(out), tile=tile), stream())
     ref = nhwc(F.relu(F.conv2d(nchw(x.float()), w.float().permute(3, 2, 0, 1), b, padding=1)))
     assert rel_err(out, ref) < 1e-2
 
@@ -279,16 +282,23 @@ def test_wgrad_concat_upsample(cuda_dev):
     assert rel_err(gw, gwr.permute(2, 3, 1, 0).reshape(-1)) < 2e-3
 
 
-def test_wgrad_first_layer_smallc(cuda_dev):
+@pytest.mark.parametrize("N,H,Creal,Cpad,Co,splits,win", [(2, 32, 1, 4, 32, 3, -1), (2, 32, 1, 4, 32, 3, 0),
+                                                           (3, 128, 4, 4, 32, 7, 0), (2, 16, 3, 4, 64, 40, 0),
+                                                           (2, 64, 8, 8, 32, 5, 0), (2, 32, 5, 8, 32, 3, -1)])
+def test_wgrad_first_layer_smallc(cuda_dev, N, H, Creal, Cpad, Co, splits, win):
+    """First-layer weight gradient: row-window kernel (win=0) and the tiled small-C mode
+    (win=-1); padded channels dropped by the slab reduction's row remap."""
     torch.manual_seed(7)
-    N, H, Creal, Cpad, Co = 2, 32, 1, 4, 32
     x = torch.zeros(N, H, H, Cpad, device=cuda_dev)
     x[..., :Creal] = torch.randn(N, H, H, Creal, device=cuda_dev)
     x = x.bfloat16()
     dy = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
+    BM, BN, NTAP, smallc = C().wgrad_pick(Cpad, 0, Co, 9, QW=H, win=win)
+    assert smallc
+    Mtot = (9 * Cpad + BM - 1) // BM * BM
     d = dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=Cpad, a1=ptr(x), b=ptr(dy), Nc=Co,
-             bias_mode=1)
-    gw, gb = _wgrad(d, 3, 1, 64, 9 * Creal, Co, 9 * Creal * Co, bias_w=(3, Co), rows=(Cpad, Creal))
+             bias_mode=1, win=win)
+    gw, gb = _wgrad(d, splits, 1, Mtot, 9 * Creal, Co, 9 * Creal * Co, bias_w=(splits, Co), rows=(Cpad, Creal))
     w = torch.zeros(Co, Creal, 3, 3, device=cuda_dev, requires_grad=True)
     bb = torch.zeros(Co, device=cuda_dev, requires_grad=True)
     gwr, gbr = torch.autograd.grad(F.conv2d(nchw(x.float()[..., :Creal]), w, bb, padding=1), [w, bb],

@@ -436,6 +436,155 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI>(p, acc, smem, m0, n0, M, wave, 0, lane, tid);
 }
 
+
+// ---------------------------------------------------------------------------------
+// First-layer row-window conv (Cin = 4 or 8 after channel padding, 2D 3x3 'same').
+//
+// K = 9 taps x CIN is tiny, so the implicit GEMM above spends its time on per-tap
+// address generation and 64-wide K padding.  Here the workgroup stages the (R+2)-row
+// halo of its 512 output pixels once (8- or 16-byte pixel slots, LDS-DMA), keeps the
+// 32 x K weight fragments in registers, and builds each MFMA A fragment straight from
+// the halo: lane group G of K-step s covers k = 32 s + 8 G .. + 7, i.e. two taps x 4
+// channels (CIN 4: two 8-byte reads) or one tap x 8 channels (CIN 8: one 16-byte read).
+// Taps past the ninth and taps whose input row leaves the output row's image read the
+// always-zero slot 0.  Halo slot layout per row: [0] zero, [1] column -1 (zero),
+// [2 .. W+1] columns 0 .. W-1, [W+2] column W (zero), [W+3] pad.
+template <int W, int CIN, int EPI>
+__global__ void __launch_bounds__(NTHR) conv_win_first_kernel(const ConvFwdParams p) {
+  constexpr int BM = 512, R = BM / W, HR = R + 2, RS = W + 4;   // row pitch in slots
+  constexpr int SB = 2 * CIN;                                  // slot bytes
+  constexpr int ROWB = RS * SB;
+  constexpr int CPR = ROWB / 16;                               // 16-byte chunks per halo row
+  constexpr int XI = (HR * CPR + 63) / 64;                     // LDS-DMA wave-instructions
+  constexpr int XB = XI * 1024;
+  constexpr int BN = 32, TM = 8, TN = 2;
+  constexpr int KS = (9 * CIN + 31) / 32;                      // MFMA K-steps
+  constexpr int EPIB = BM * (BN + 4) * 2;
+  constexpr int LDS_BYTES = XB > EPIB ? XB : EPIB;
+  constexpr int TPR = W / 16;
+  static_assert((CIN == 4 || CIN == 8) && W >= 16 && W <= 128 && BM % W == 0, "first-layer window");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  char* Xs = smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = p.OH;
+  const int rows_total = p.N * H;
+  const int M = rows_total * W;
+  const int tiles_n = p.Cout / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int g0 = tm * R;
+  const int m0 = g0 * W, n0 = tn * BN;
+  constexpr int OOB = 0x7fffffff;
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)p.src1, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
+
+  // halo DMA: chunk u of the image = row u / CPR, 16 bytes = slots covering columns
+  // (CIN 4) 2c - 2, 2c - 1  or  (CIN 8) c - 2, c = u % CPR
+#pragma unroll
+  for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
+    const int k = wave + 4 * qq;
+    if (k < XI) {
+      const int u = 64 * k + lane;
+      const int hr = u / CPR, c = u - hr * CPR;
+      const int gr = g0 - 1 + hr;
+      const int col = CIN == 4 ? 2 * c - 2 : c - 2;
+      const bool ok = hr < HR && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+      const int off = ok ? ((gr * W + col) * CIN) * 2 : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs1, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16, off,
+                                               0, 0, 0);
+    }
+  }
+  // weight fragments (B operand: k = 32 s + 8 (lane >> 4) .. + 7, n = lane & 15), from global
+  const int fsub = lane >> 4, fr = lane & 15;
+  bf16x8 wf[KS][TN];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+          rsw, ((n0 + 16 * j + fr) * p.Kpad + 32 * s + 8 * fsub) * 2, 0, 0);
+      wf[s][j] = __builtin_bit_cast(bf16x8, v);
+    }
+
+  const int rw0 = (128 * wave) / W;
+  uint32_t top_ok = 0, bot_ok = 0, live = 0;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int g = g0 + rw0 + (i / TPR);
+    const int h = g % H;
+    if (g < rows_total) live |= 1u << i;
+    if (h > 0) top_ok |= 1u << i;
+    if (h < H - 1) bot_ok |= 1u << i;
+  }
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    if (!((live >> i) & 1u)) continue;
+    const int rr = rw0 + i / TPR;                       // window row of this 16-pixel tile
+    const int cw = ((128 * wave) % W) + (i % TPR) * 16 + fr;   // this lane's output column
+    const bool tok = (top_ok >> i) & 1u, bok = (bot_ok >> i) & 1u;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      u32x4 v;
+      if constexpr (CIN == 4) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int t = 8 * s + 2 * fsub + hh;            // tap of this 4-channel half
+          const int dh = t / 3, dw = t - 3 * dh;
+          const bool ok = t < 9 && (dh != 0 || tok) && (dh != 2 || bok);
+          const int slot = (rr + dh) * RS + cw + dw + 1;
+          const u32x2 h2 = *(const u32x2*)(Xs + (ok ? slot * SB : 0));
+          v[2 * hh] = h2[0];
+          v[2 * hh + 1] = h2[1];
+        }
+      } else {
+        const int t = 4 * s + fsub;
+        const int dh = t / 3, dw = t - 3 * dh;
+        const bool ok = t < 9 && (dh != 0 || tok) && (dh != 2 || bok);
+        const int slot = (rr + dh) * RS + cw + dw + 1;
+        v = *(const u32x4*)(Xs + (ok ? slot * SB : 0));
+      }
+      const bf16x8 xf = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[s][j], xf, acc[i][j]);
+    }
+  }
+  __syncthreads();
+  conv_epilogue<BM, BN, 128, BN, TM, TN, NTHR, EPI>(p, acc, smem, m0, n0, M, wave, 0, lane, tid);
+}
+
+template <int CIN>
+hipError_t launch_win_first(const ConvFwdParams& p, hipStream_t s) {
+  const int W = p.OW;
+  const int R = 512 / W;
+  const int grid = ((p.N * p.OH + R - 1) / R) * (p.Cout / 32);
+  const bool fwd = conv_epi_mode(p) == EPI_FWD;
+#define WF_CASE(WW)                                                                                        \
+  case WW:                                                                                                 \
+    if (fwd)                                                                                               \
+      hipLaunchKernelGGL((conv_win_first_kernel<WW, CIN, EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p);     \
+    else                                                                                                   \
+      hipLaunchKernelGGL((conv_win_first_kernel<WW, CIN, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p); \
+    break;
+  switch (W) {
+    WF_CASE(16)
+    WF_CASE(32)
+    WF_CASE(64)
+    WF_CASE(128)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef WF_CASE
+  return hipGetLastError();
+}
+
 template <int BN>
 hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
   const int W = p.OW;
@@ -483,6 +632,14 @@ static bool win_eligible(const ConvFwdParams& p) {
          (p.C1 % 32) == 0 && (p.C2 % 32) == 0 && p.C1 > 0;
 }
 
+// First layer (4/8 padded input channels) on full rows 16..128 wide.
+static bool win_first_eligible(const ConvFwdParams& p) {
+  const bool w_ok = p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128;
+  return p.KD == 1 && p.OD == 1 && p.ID == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.pad == 1 &&
+         p.up1 == 1 && !p.shuffle && !p.stats && w_ok && p.IW == p.OW && p.IH == p.OH && p.C2 == 0 &&
+         (p.C1 == 4 || p.C1 == 8) && p.Cout % 32 == 0 && p.D1 == p.Cout;
+}
+
 // Fills the tap tables and Kpad; returns nullptr on success or a message describing
 // why the shape is unsupported.
 const char* conv_fwd_prepare(ConvFwdParams& p) {
@@ -510,7 +667,8 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.shuffle && ((p.Cout >> p.shuffle) % 8)) return "conv_fwd: shuffle channels must be multiples of 8";
   if (p.shuffle && p.D1 != p.Cout) return "conv_fwd: shuffle with channel split unsupported";
   if (p.stats && p.shuffle) return "conv_fwd: stats with shuffle unsupported";
-  if (p.tile < 0 || p.tile > 8) return "conv_fwd: bad tile id";
+  if (p.tile < 0 || p.tile > 9) return "conv_fwd: bad tile id";
+  if (p.tile == 9 && !win_first_eligible(p)) return "conv_fwd: first-layer window tile not applicable";
   {
     const int t = p.tile ? p.tile : 0;
     const int bn = t == 1 ? 128 : (t == 2 || t == 5) ? 64 : 32;
@@ -547,6 +705,7 @@ int conv_fwd_pick(const ConvFwdParams& p) {
   // 1.1-2.1x over the implicit-GEMM tiles (profiles/r1_conv_tiles.md); the 512x64
   // variant needs 287 registers (1 wave/SIMD) and never wins
   if (p.tile != 8 && win_eligible(p)) return 6;
+  if (p.tile != 8 && win_first_eligible(p)) return 9;
   if (p.Cout % 128 == 0 && M >= 8192) return 1;
   if (p.Cout % 64 == 0) return 2;
   return 4;
@@ -559,6 +718,7 @@ hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
     case 3: return launch_cfg<256, 32, 4, 1>(p, s);
     case 5: return launch_cfg<256, 64, 4, 1>(p, s);
     case 6: return launch_win<32>(p, s);
+    case 9: return p.C1 == 4 ? launch_win_first<4>(p, s) : launch_win_first<8>(p, s);
     default: return launch_cfg<128, 32, 4, 1>(p, s);
   }
 }

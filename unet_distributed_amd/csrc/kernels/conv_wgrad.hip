@@ -628,6 +628,183 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   }
 }
 
+
+// ---------------------------------------------------------------------------------
+// First-layer row-window weight gradient (CIN = 4 or 8 padded input channels).
+// GEMM rows m = (tap, channel) (36 or 72, padded to MT x 16), columns = 32 output
+// channels, K = pixels.  The halo image uses the first-layer forward's slot layout
+// (8- or 16-byte slots, row pitch W + 4, slot 0 always zero).  A fragments come from
+// the transposed LDS read with per-lane addresses: lane 4q + pp of a 16-lane group
+// supplies pixel q's slot for tap 4mt + pp (CIN 4) or tap 2mt + pp/2 and channel half
+// pp & 1 (CIN 8), so the transpose hands lane i the (tap, channel) row 16 mt + i; taps
+// past the ninth and taps whose input row leaves the pixel's image address slot 0.
+template <int W, int CIN>
+__global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams p) {
+  constexpr int BMW = 256, R = BMW / W, HR = R + 2, RS = W + 4, SB = 2 * CIN, ROWB = RS * SB;
+  constexpr int CPR = ROWB / 16;
+  constexpr int XI = (HR * CPR + 63) / 64, YI = BMW / 16;
+  constexpr int XB = XI * 1024, YB = YI * 1024;
+  constexpr int MT = (9 * CIN + 15) / 16;
+  constexpr int KS = BMW / 32;
+  constexpr int REDB = 4 * 64 * (MT * 2 + 2) * 16;
+  constexpr int LDS_BYTES = (XB + YB > REDB) ? XB + YB : REDB;
+  static_assert(W >= 16 && W <= 128, "first-layer window wgrad");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  char* Xs = smem;
+  char* Ys = smem + XB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = p.QH;
+  const int rows_total = p.N * H;
+  const int Mq = rows_total * W;
+  const int nwin = (rows_total + R - 1) / R;
+  const int Mtot = MT * 16;
+  const int cot = p.Nc / 32;
+  const int split = blockIdx.x / cot, co_blk = blockIdx.x - split * cot;
+  const int co0 = co_blk * 32;
+  constexpr int OOB = 0x7fffffff;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.a1, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, OOB, 0x00020000);
+  const int w_begin = (int)((long long)split * nwin / p.splits);
+  const int w_end = (int)((long long)(split + 1) * nwin / p.splits);
+  const bool do_bias = p.bias_mode == 1;
+
+  f32x4 acc[MT][2];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) acc[i][0] = acc[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 bacc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+  const u32x4 ones_u = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_u);
+  const int lslot = lane >> 2;
+  const int lchunk = (lane & 3) ^ (((lslot >> 3) & 1) << 1);
+  const int yl = (lslot * p.Nc + co0 + lchunk * 8) * 2;
+  const int G = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+
+  auto tr_addr = [&](int slot, int col, int ch) -> int {
+    return slot * 64 + ((((ch >> 3) ^ (((col >> 3) & 1) << 1))) << 4) + ((ch & 7) << 1);
+  };
+  auto tr8 = [&](const char* base0, const char* base1) -> bf16x8 {
+    const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base0));
+    const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base1));
+    const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+    const u32x4 v = {l2[0], l2[1], h2[0], h2[1]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+  for (int win = w_begin; win < w_end; ++win) {
+    const int g0 = win * R;
+    __syncthreads();
+#pragma unroll
+    for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
+      const int k = wave + 4 * qq;
+      if (k < XI) {
+        const int u = 64 * k + lane;
+        const int hr = u / CPR, c = u - hr * CPR;
+        const int gr = g0 - 1 + hr;
+        const int col = CIN == 4 ? 2 * c - 2 : c - 2;
+        const bool ok = hr < HR && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+        const int off = ok ? ((gr * W + col) * CIN) * 2 : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int qq = 0; qq < (YI + 3) / 4; ++qq) {
+      const int k = wave + 4 * qq;
+      if (k < YI) {
+        const int pix = g0 * W + 16 * k;
+        const int off = (pix + lslot < Mq) ? pix * p.Nc * 2 + yl : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (__attribute__((address_space(3))) void*)(Ys + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int kk = wave; kk < KS; kk += 4) {
+      const int px0 = kk * 32;
+      if (g0 + px0 / W >= rows_total) break;
+      bf16x8 bf[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int s0 = px0 + 8 * G + q, s1 = s0 + 4;
+        bf[j] = tr8(Ys + tr_addr(s0, s0, 16 * j + 4 * pp), Ys + tr_addr(s1, s1, 16 * j + 4 * pp));
+      }
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bacc[j] = mfma16(ones, bf[j], bacc[j]);
+      }
+      // this lane's two pixels (second transposed read: +4)
+      int slotp[2], hlp[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int px = px0 + 8 * G + 4 * hh + q;
+        const int rr = px / W, cw = px - rr * W;
+        slotp[hh] = rr * RS + cw + 1;        // tap (dh, dw) adds dh * RS + dw
+        hlp[hh] = (g0 + rr) % H;
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int t = CIN == 4 ? 4 * mt + pp : 2 * mt + (pp >> 1);
+        const int chb = CIN == 4 ? 0 : (pp & 1) * 8;
+        const int dh = t / 3, dw = t - 3 * dh;
+        int a[2];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const bool ok = t < 9 && !(dh == 0 && hlp[hh] == 0) && !(dh == 2 && hlp[hh] == H - 1);
+          a[hh] = ok ? (slotp[hh] + dh * RS + dw) * SB + chb : 0;
+        }
+        const bf16x8 af = tr8(Xs + a[0], Xs + a[1]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mt][j] = mfma16(af, bf[j], acc[mt][j]);
+      }
+    }
+  }
+
+  // cross-wave reduce (all four waves split pixels), then one slab per workgroup:
+  // acc[mt][j][r] = dW[m = 16 mt + 4 (lane >> 4) + r][co0 + 16 j + (lane & 15)]
+  __syncthreads();
+  float* red = (float*)smem;
+  constexpr int NV = MT * 2 + 2;
+  {
+    float* dst = red + (wave * 64 + lane) * NV * 4;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) *(f32x4*)(dst + (mt * 2 + j) * 4) = acc[mt][j];
+    *(f32x4*)(dst + (MT * 2) * 4) = bacc[0];
+    *(f32x4*)(dst + (MT * 2 + 1) * 4) = bacc[1];
+  }
+  __syncthreads();
+  for (int idx = tid; idx < 64 * NV; idx += NTHR) {
+    const int ln = idx / NV, v = idx - ln * NV;
+    f32x4 sum = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) sum += *(const f32x4*)(red + ((w * 64 + ln) * NV + v) * 4);
+    const int n = co0 + (ln & 15);
+    if (v < MT * 2) {
+      const int mt = v >> 1, j = v & 1;
+      const int m = 16 * mt + 4 * (ln >> 4);
+      float* dst = p.slab + ((size_t)split * Mtot + m) * p.Nc + n + 16 * j;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dst[(size_t)r * p.Nc] = sum[r];
+    } else if (do_bias && ln < 16) {
+      p.bias_slab[(size_t)split * p.Nc + n + 16 * (v - MT * 2)] = sum[0];
+    }
+  }
+}
+
+template <int CIN>
+hipError_t launch_wgrad_win_first(const WgradParams& p, hipStream_t s) {
+  const int grid = (p.Nc / 32) * p.splits;
+  switch (p.QW) {
+    case 16: hipLaunchKernelGGL((wgrad_win_first_kernel<16, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 32: hipLaunchKernelGGL((wgrad_win_first_kernel<32, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 64: hipLaunchKernelGGL((wgrad_win_first_kernel<64, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    default: hipLaunchKernelGGL((wgrad_win_first_kernel<128, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
+  }
+  return hipGetLastError();
+}
+
 template <int W, int QO>
 hipError_t launch_wgrad_win(const WgradParams& p, hipStream_t s) {
   const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.splits;
@@ -649,10 +826,19 @@ static bool wgrad_win_eligible(const WgradParams& p) {
          p.M1 > 0 && (p.Nc % 32) == 0 && p.bias_mode != 2;
 }
 
+// First layer (CIN 4/8, padded channels) on full rows 16..128 wide.
+static bool wgrad_win_first_eligible(const WgradParams& p) {
+  const bool w_ok = p.QW == 16 || p.QW == 32 || p.QW == 64 || p.QW == 128;
+  return p.win >= 0 && w_ok && p.QD == 1 && p.KD == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.pad == 1 &&
+         p.upA == 1 && p.AW == p.QW && p.AH == p.QH && (p.M1 == 4 || p.M1 == 8) && p.M2 == 0 &&
+         (p.Nc % 32) == 0 && p.bias_mode != 2;
+}
+
 WgradCfg wgrad_pick(const WgradParams& p) {
   const int KT = p.KD * p.KH * p.KW;
   const int M = p.M1 + p.M2;
   if (wgrad_win_eligible(p)) return {32, (p.Nc % 64 == 0) ? 64 : 32, 9, 0};   // row-window tile
+  if (wgrad_win_first_eligible(p)) return {p.M1 == 4 ? 48 : 80, 32, 1, 1};      // first-layer window
   if ((p.M1 == 4 || p.M1 == 8) && p.M2 == 0) return {64, 32, 1, 1};
   if (M <= 64 && p.Nc <= 64 && KT % 9 == 0) return {32, 32, 9, 0};
   if (M <= 64 && p.Nc <= 64 && KT % 4 == 0) return {32, 32, 4, 0};
@@ -680,6 +866,7 @@ const char* wgrad_check(const WgradParams& p) {
 
 hipError_t wgrad_launch(const WgradParams& p, hipStream_t s) {
   const WgradCfg c = wgrad_pick(p);
+  if (wgrad_win_first_eligible(p)) return p.M1 == 4 ? launch_wgrad_win_first<4>(p, s) : launch_wgrad_win_first<8>(p, s);
   if (wgrad_win_eligible(p)) {
     const bool q2 = c.BN == 64;
     switch (p.QW) {

@@ -1,4 +1,4 @@
-// Fused segmentation head + loss on gfx950.
+// Fused segmentation head + loss on gfx950 (16-byte lanes: C/8 lanes per pixel).
 //
 // Forward (`model.py:119-120` Mask 1x1 conv + sigmoid, `model.py:4-21` Dice):
 //   z_p = sum_c x[p][c] w[c] + b;   prob_p = sigmoid(z_p)
@@ -18,6 +18,8 @@ namespace {
 
 constexpr int HT = 256;
 
+// Forward: one thread per pixel (the sigmoid / BCE transcendentals then run once per
+// pixel on full waves; a lane-per-chunk mapping measured 2x slower here).
 template <int C>
 __global__ void __launch_bounds__(HT) head_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                       const float* __restrict__ b, const bf16* __restrict__ t,
@@ -68,22 +70,20 @@ __global__ void __launch_bounds__(HT) head_fwd_kernel(const bf16* __restrict__ x
   }
 }
 
-// out[j] = sum_b partial[b][j], j < width   (single block, fixed order)
+// out[j] = sum_b partial[b][j]: one block per column j, fixed order
 __global__ void __launch_bounds__(256) partial_reduce_kernel(const float* __restrict__ partial, int nb, int width,
                                                              float* __restrict__ out) {
   __shared__ float red[256];
-  for (int j = 0; j < width; ++j) {
-    float s = 0.f;
-    for (int k = threadIdx.x; k < nb; k += 256) s += partial[(size_t)k * width + j];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) out[j] = red[0];
+  const int j = blockIdx.x;
+  float s = 0.f;
+  for (int k = threadIdx.x; k < nb; k += 256) s += partial[(size_t)k * width + j];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
+  if (threadIdx.x == 0) out[j] = red[0];
 }
 
 template <int C>
@@ -92,80 +92,80 @@ __global__ void __launch_bounds__(HT) head_bwd_kernel(const bf16* __restrict__ x
                                                       const float* __restrict__ sums, int P, float inv_total,
                                                       float bce_w, float gscale, bf16* __restrict__ dx,
                                                       float* __restrict__ partial) {
-  __shared__ float red[C + 1][HT / 64];
-  float wr[C];
+  constexpr int CP = C / 8;
+  __shared__ float red[HT / 64][C + 1];
+  const int cc = threadIdx.x % CP;
+  float wr[8];
 #pragma unroll
-  for (int c = 0; c < C; ++c) wr[c] = w[c];
+  for (int e = 0; e < 8; ++e) wr[e] = w[cc * 8 + e];
   const float I = sums[0], St = sums[1], Sp = sums[2];
   const float a = -2.f / (2.f * I + 1.f);
   const float bb = 1.f / (St + Sp + 1.f);
-  float gw[C];
-#pragma unroll
-  for (int c = 0; c < C; ++c) gw[c] = 0.f;
+  float gw[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float gb = 0.f;
-  for (int p = blockIdx.x * HT + threadIdx.x; p < P; p += gridDim.x * HT) {
+  const long long total = (long long)P * CP;
+  for (long long i = blockIdx.x * (long long)HT + threadIdx.x; i < total; i += (long long)gridDim.x * HT) {
+    const int p = (int)(i / CP);
     const float pr = prob[p];
     const float tv = (float)t[p];
     float dz = (a * tv + bb) * pr * (1.f - pr);
     dz += bce_w * (pr - tv) * inv_total;
     dz *= gscale;
-    gb += dz;
+    if (cc == 0) gb += dz;
+    float f[8], o[8];
+    unpack8(*(const u32x4*)(x + i * 8), f);
 #pragma unroll
-    for (int c8 = 0; c8 < C / 8; ++c8) {
-      const u32x4 xv = *(const u32x4*)(x + (size_t)p * C + c8 * 8);
-      float f[8], o[8];
-      unpack8(xv, f);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        gw[c8 * 8 + e] += dz * f[e];
-        o[e] = f[e] > 0.f ? dz * wr[c8 * 8 + e] : 0.f;
-      }
-      *(u32x4*)(dx + (size_t)p * C + c8 * 8) = pack8(o);
+    for (int e = 0; e < 8; ++e) {
+      gw[e] += dz * f[e];
+      o[e] = f[e] > 0.f ? dz * wr[e] : 0.f;      // ReLU of the head's input folded in
     }
+    *(u32x4*)(dx + i * 8) = pack8(o);
   }
-  const int wv = threadIdx.x >> 6;
+  // lanes l, l + CP, l + 2CP, ... hold the same channels: fold them, then across waves
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const float s = wave_sum(gw[c]);
-    if ((threadIdx.x & 63) == 0) red[c][wv] = s;
-  }
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int o = CP; o < 64; o <<= 1) gw[e] += __shfl_xor(gw[e], o, 64);
   gb = wave_sum(gb);
-  if ((threadIdx.x & 63) == 0) red[C][wv] = gb;
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  if (ln < CP) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[wv][ln * 8 + e] = gw[e];
+  }
+  if (ln == 0) red[wv][C] = gb;
   __syncthreads();
   for (int j = threadIdx.x; j <= C; j += HT) {
     float s = 0.f;
-    for (int k = 0; k < HT / 64; ++k) s += red[j][k];
+    for (int k = 0; k < HT / 64; ++k) s += red[k][j];
     partial[(size_t)blockIdx.x * (C + 1) + j] = s;
   }
 }
 
-// grad_w[c] = sum_b partial[b][c], grad_b = sum_b partial[b][C]
+// grad_w[c] = sum_b partial[b][c], grad_b = sum_b partial[b][C]: one block per column
 __global__ void __launch_bounds__(256) head_grad_reduce_kernel(const float* __restrict__ partial, int nb, int C,
                                                                float* __restrict__ gw, float* __restrict__ gb) {
   __shared__ float red[256];
-  for (int j = 0; j <= C; ++j) {
-    float s = 0.f;
-    for (int k = threadIdx.x; k < nb; k += 256) s += partial[(size_t)k * (C + 1) + j];
-    red[threadIdx.x] = s;
+  const int j = blockIdx.x;
+  float s = 0.f;
+  for (int k = threadIdx.x; k < nb; k += 256) s += partial[(size_t)k * (C + 1) + j];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      if (j < C)
-        gw[j] = red[0];
-      else
-        gb[0] = red[0];
-    }
-    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (j < C)
+      gw[j] = red[0];
+    else
+      gb[0] = red[0];
   }
 }
 
 }  // namespace
 
 int head_blocks(int P) {
-  int nb = (P + HT * 4 - 1) / (HT * 4);
+  int nb = (P + HT - 1) / HT;
   if (nb > 1024) nb = 1024;
   if (nb < 1) nb = 1;
   return nb;
@@ -192,7 +192,7 @@ hipError_t head_fwd_launch(const void* x, const float* w, const float* b, const 
       hipLaunchKernelGGL(head_fwd_kernel<64>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, b, (const bf16*)t, P,
                          prob, partial);
   }
-  hipLaunchKernelGGL(partial_reduce_kernel, dim3(1), dim3(256), 0, s, partial, nb, 4, sums);
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3(4), dim3(256), 0, s, partial, nb, 4, sums);
   return hipGetLastError();
 }
 
@@ -213,12 +213,12 @@ hipError_t head_bwd_launch(const void* x, const float* w, const float* prob, con
       hipLaunchKernelGGL(head_bwd_kernel<64>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, prob, (const bf16*)t,
                          sums, P, inv_total, bce_w, gscale, (bf16*)dx, partial);
   }
-  hipLaunchKernelGGL(head_grad_reduce_kernel, dim3(1), dim3(256), 0, s, partial, nb, C, gw, gb);
+  hipLaunchKernelGGL(head_grad_reduce_kernel, dim3(C + 1), dim3(256), 0, s, partial, nb, C, gw, gb);
   return hipGetLastError();
 }
 
 hipError_t partial_reduce_launch(const float* partial, int nb, int width, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(partial_reduce_kernel, dim3(1), dim3(256), 0, s, partial, nb, width, out);
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3(width), dim3(256), 0, s, partial, nb, width, out);
   return hipGetLastError();
 }
 
