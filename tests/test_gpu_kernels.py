@@ -182,15 +182,17 @@ def test_conv_first_layer_smallc(cuda_dev, N, H, Cin, Co, tile):
     assert rel_err(out, ref) < 1e-2
 
 
-def test_tconv_fwd_shuffle_and_dgrad(cuda_dev):
+@pytest.mark.parametrize("N,H,Ci,Co,tile", [(2, 8, 64, 32, 0), (2, 8, 64, 32, 8), (3, 64, 64, 32, 0),
+                                            (2, 32, 128, 64, 0), (5, 16, 256, 128, 0), (3, 8, 512, 256, 0)])
+def test_tconv_fwd_shuffle_and_dgrad(cuda_dev, N, H, Ci, Co, tile):
+    """2x2 stride-2 transposed conv: window kernels (auto) and the implicit-GEMM path (tile 8)."""
     torch.manual_seed(4)
-    N, H, Ci, Co = 2, 8, 64, 32
     x = F.relu(torch.randn(N, H, H, Ci, device=cuda_dev)).bfloat16()
     k = (torch.randn(2, 2, Co, Ci, device=cuda_dev) * 0.1).bfloat16()   # Keras (kh,kw,Cout,Cin)
     b = torch.randn(Co, device=cuda_dev)
     out = torch.empty(N, 2 * H, 2 * H, Co, device=cuda_dev, dtype=torch.bfloat16)
     C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, C1=Ci, src1=ptr(x), wgt=ptr(pad64(k.reshape(4 * Co, Ci))),
-                      bias=ptr(b), Cout=4 * Co, shuffle=2, dst1=ptr(out)), stream())
+                      bias=ptr(b), Cout=4 * Co, shuffle=2, dst1=ptr(out), tile=tile), stream())
     wt = k.float().permute(3, 2, 0, 1)      # (Cin, Cout, kh, kw)
     ref = nhwc(F.conv_transpose2d(nchw(x.float()), wt, b, stride=2))
     assert rel_err(out, ref) < 1e-2
@@ -199,7 +201,7 @@ def test_tconv_fwd_shuffle_and_dgrad(cuda_dev):
     wdg = pad64(k.permute(3, 0, 1, 2).reshape(Ci, 4 * Co))
     dx = torch.empty(N, H, H, Ci, device=cuda_dev, dtype=torch.bfloat16)
     C().conv_fwd(dict(N=N, OH=H, OW=H, IH=2 * H, IW=2 * H, KH=2, KW=2, stride=2, pad=0, C1=Co,
-                      src1=ptr(dout), wgt=ptr(wdg), Cout=Ci, dst1=ptr(dx), mask1=ptr(x)), stream())
+                      src1=ptr(dout), wgt=ptr(wdg), Cout=Ci, dst1=ptr(dx), mask1=ptr(x), tile=tile), stream())
     xr = nchw(x.float()).requires_grad_(True)
     (g,) = torch.autograd.grad(F.conv_transpose2d(xr, wt, stride=2), xr, nchw(dout.float()))
     ref = nhwc(g) * (x.float() > 0)
@@ -307,16 +309,19 @@ def test_wgrad_first_layer_smallc(cuda_dev, N, H, Creal, Cpad, Co, splits, win):
     assert rel_err(gb, gbr) < 2e-3
 
 
-def test_tconv_wgrad_bias_mode2(cuda_dev):
+@pytest.mark.parametrize("N,H,Ci,Co,splits,win", [(2, 8, 64, 32, 2, 0), (3, 64, 64, 32, 5, 0), (2, 32, 128, 64, 3, 0),
+                                                   (2, 32, 128, 64, 3, -1), (3, 64, 64, 32, 40, 0)])
+def test_tconv_wgrad_bias_mode2(cuda_dev, N, H, Ci, Co, splits, win):
+    """Transposed-conv weight + bias gradients: window kernel (coarse rows 32/64, auto) and
+    the tiled kernel; the slab / bias-slab layout comes from wgrad_pick like the engine."""
     torch.manual_seed(8)
-    N, H, Ci, Co = 2, 8, 64, 32
     x = F.relu(torch.randn(N, H, H, Ci, device=cuda_dev)).bfloat16()
     dout = torch.randn(N, 2 * H, 2 * H, Co, device=cuda_dev).bfloat16()
     d = dict(N=N, QH=H, QW=H, AH=2 * H, AW=2 * H, KH=2, KW=2, stride=2, pad=0, M1=Co, a1=ptr(dout),
-             b=ptr(x), Nc=Ci, bias_mode=2)
-    BM, BN, NTAP, _ = C().wgrad_pick(Co, 0, Ci, 4)
+             b=ptr(x), Nc=Ci, bias_mode=2, win=win)
+    BM, BN, NTAP, _ = C().wgrad_pick(Co, 0, Ci, 4, QW=H, win=win)
     tg = 4 // NTAP
-    gw, gb = _wgrad(d, 2, 4, Co, Co, Ci, 4 * Co * Ci, bias_w=(2 * tg, Co))
+    gw, gb = _wgrad(d, splits, 4, Co, Co, Ci, 4 * Co * Ci, bias_w=(splits * tg, Co))
     k = torch.zeros(Ci, Co, 2, 2, device=cuda_dev, requires_grad=True)
     bb = torch.zeros(Co, device=cuda_dev, requires_grad=True)
     gk, gbr = torch.autograd.grad(F.conv_transpose2d(nchw(x.float()), k, bb, stride=2), [k, bb],

@@ -307,7 +307,7 @@ hipError_t launch_cfg(const ConvFwdParams& p, hipStream_t s) {
 // address registers.  Weight rows (tap, n) use the same swizzle on the row index.
 template <int W, int BN, bool CONCAT, int EPI>
 __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
-  static_assert(BN == 32, "row-window tile is 32 output channels wide");
+  static_assert(BN == 32 || BN == 64, "row-window tile is 32 or 64 output channels wide");
   constexpr int BM = W == 16 ? 256 : 512;       // window pixels (16-wide rows: 16 rows)
   constexpr int R = BM / W, HR = R + 2;
   constexpr int HWP = ((W + 2 + 15) / 16) * 16; // halo row pitch in 64-byte pixel slots
@@ -406,7 +406,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
       for (int q = 0; q < (WI + 3) / 4; ++q) {
         const int k = wave + 4 * q;
         if (k < WI) {
-          const int tap = k >> 1, nb = (k & 1) * 16;     // wave-uniform
+          const int tap = k / (BN / 16), nb = (k % (BN / 16)) * 16;     // wave-uniform
           const int off = ((n0 + nb) * p.Kpad + tap * Cin) * 2 + wl;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024),
                                                    16, off, 0, 0, 0);
@@ -585,6 +585,252 @@ hipError_t launch_win_first(const ConvFwdParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------------
+// 2x2 stride-2 transposed convolution (2D), forward and data gradient, on windows of
+// whole coarse rows.  Coarse grid H x W (the transposed conv's input), fine grid 2H x 2W.
+//
+// Forward  out[2h+th][2w+tw][co] = b[co] + sum_ci x[h][w][ci] W[(th,tw)][co][ci]:
+//   a workgroup owns 128 coarse pixels (R = 128 / W coarse rows) and 32 output
+//   channels; wave t computes tap t for all 128 pixels (shared x image, per-tap weight
+//   rows), and the epilogue assembles the 2R x 2W fine tile in LDS so the stores are
+//   whole contiguous fine rows (the pixel shuffle costs nothing).
+// Data gradient dx[h][w][ci] = sum_{t,co} dy[2h+th][2w+tw][co] W[(th,tw)][co][ci]:
+//   256 coarse pixels x 32 input channels per workgroup; per 32-channel chunk of dy the
+//   2R fine rows are LDS-DMA'd once with even / odd columns de-interleaved, so the
+//   four taps' A fragments are 16 consecutive slots (conflict free) of the same image.
+template <int W, int EPI>
+__global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) {
+  constexpr int BMc = 128, R = BMc / W;
+  constexpr int XI = BMc / 16, WI = 4 * 32 / 16;   // 1 KB DMA instructions per chunk
+  constexpr int XB = XI * 1024, WB = WI * 1024;
+  constexpr int FST = 32 * 2 + 8;                   // fine staging row stride (bytes)
+  constexpr int EPIB = 4 * BMc * FST;
+  constexpr int LDS_BYTES = (XB + WB > EPIB) ? XB + WB : EPIB;
+  constexpr int TM = BMc / 16, TN = 2;
+  static_assert(BMc % W == 0 && W >= 8 && W <= 128, "tconv window");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  char* Xs = smem;
+  char* Ws = smem + XB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = p.OH;
+  const int rows_total = p.N * H;
+  const int Mc = rows_total * W;
+  const int cof = p.Cout >> 2;                   // fine output channels
+  const int tiles_n = cof / 32;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
+  const int g0 = tm * R, m0 = g0 * W, n0 = tn * 32;
+  const int Cin = p.C1;
+  constexpr int OOB = 0x7fffffff;
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc((void*)p.src1, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
+  const int lslot = lane >> 2;
+  const int lchunk = (lane & 3) ^ ((lslot >> 1) & 3);
+  const int fsub = lane >> 4, fr = lane & 15;
+  const int fbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) acc[i][0] = acc[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int kc = 0; kc < (Cin >> 5); ++kc) {
+    if (kc) __syncthreads();
+#pragma unroll
+    for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
+      const int k = wave + 4 * qq;
+      if (k < XI) {
+        const int pix = m0 + 16 * k + lslot;
+        const int off = pix < Mc ? (pix * Cin + (kc << 5) + lchunk * 8) * 2 : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsx, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int qq = 0; qq < (WI + 3) / 4; ++qq) {
+      const int k = wave + 4 * qq;
+      if (k < WI) {
+        const int t = k >> 1, nb = (k & 1) * 16;        // weight image row = t * 32 + co
+        const int row = t * cof + n0 + nb + lslot;
+        const int off = (row * p.Kpad + (kc << 5) + lchunk * 8) * 2;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    bf16x8 wf[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) wf[j] = *(const bf16x8*)(Ws + (wave * 32 + 16 * j) * 64 + fbase);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const bf16x8 xf = *(const bf16x8*)(Xs + (16 * i) * 64 + fbase);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[j], xf, acc[i][j]);
+    }
+  }
+  __syncthreads();
+  // register phase: acc[i][j][r] = out(coarse px 16i + (lane&15), tap = wave)[co = 16j + 4(lane>>4) + r]
+  char* E = smem;
+  const int th = wave >> 1, tw = wave & 1;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int nl = 16 * j + 4 * (lane >> 4);
+    float bs[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bs[r] = p.bias ? p.bias[n0 + nl + r] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int pl = 16 * i + (lane & 15);
+      const int rr = pl / W, w = pl - rr * W;
+      const int fp = (2 * rr + th) * (2 * W) + 2 * w + tw;
+      u32x2 pk;
+      pk[0] = pack2bf(acc[i][j][0] + bs[0], acc[i][j][1] + bs[1]);
+      pk[1] = pack2bf(acc[i][j][2] + bs[2], acc[i][j][3] + bs[3]);
+      *(u32x2*)(E + fp * FST + nl * 2) = pk;
+    }
+  }
+  __syncthreads();
+  // coalesced phase: the window's 2R fine rows are contiguous in the output
+  const size_t fine0 = (size_t)(2 * g0) * (2 * W);
+  const size_t fine_total = (size_t)(2 * rows_total) * (2 * W);
+#pragma unroll
+  for (int it = 0; it < (4 * BMc * 4) / NTHR; ++it) {
+    const int c = tid + it * NTHR;
+    const int fp = c >> 2, q = c & 3;
+    const size_t gp = fine0 + fp;
+    if (gp >= fine_total) continue;
+    const u32x2 lo = *(const u32x2*)(E + fp * FST + q * 16);
+    const u32x2 hi = *(const u32x2*)(E + fp * FST + q * 16 + 8);
+    const u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
+    *(u32x4*)((bf16*)p.dst1 + gp * cof + n0 + q * 8) = v;
+  }
+}
+
+template <int W, int BN, int EPI>
+__global__ void __launch_bounds__(NTHR) tconv_dgrad_kernel(const ConvFwdParams p) {
+  constexpr int BMc = 256, R = BMc / W, FW = 2 * W;     // coarse window; fine row width
+  constexpr int YI = (2 * R * FW) / 16;                 // dy image DMA instructions per chunk
+  constexpr int WI = 4 * BN / 16;
+  constexpr int YB = YI * 1024, WB = WI * 1024;
+  constexpr int EPIB = BMc * (BN + 4) * 2;
+  constexpr int LDS_BYTES = (YB + WB > EPIB) ? YB + WB : EPIB;
+  constexpr int TM = BMc / 4 / 16, TN = BN / 16;
+  static_assert(BMc % W == 0 && W >= 8 && W <= 128, "tconv window");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  char* Ys = smem;
+  char* Ws = smem + YB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = p.OH;                                    // coarse (output) grid
+  const int rows_total = p.N * H;
+  const int Mc = rows_total * W;
+  const int cof = p.C1;                                  // fine channels (dy)
+  const int tiles_n = p.Cout / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
+  const int g0 = tm * R, m0 = g0 * W, n0 = tn * BN;
+  constexpr int OOB = 0x7fffffff;
+  const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc((void*)p.src1, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
+  const int lslot = lane >> 2;
+  const int lchunk = (lane & 3) ^ ((lslot >> 1) & 3);
+  const int fsub = lane >> 4, fr = lane & 15;
+  const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
+  const int fine_rows_total = 2 * rows_total;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int kc = 0; kc < (cof >> 5); ++kc) {
+    if (kc) __syncthreads();
+    // dy image: fine row fr2 (of 2R), slot s in [0, 2W): s < W -> column 2s, else 2(s - W) + 1
+#pragma unroll
+    for (int qq = 0; qq < (YI + 3) / 4; ++qq) {
+      const int k = wave + 4 * qq;
+      if (k < YI) {
+        const int sl = 16 * k + lslot;
+        const int frr = sl / FW, s = sl - frr * FW;
+        const int col = s < W ? 2 * s : 2 * (s - W) + 1;
+        const int gf = 2 * g0 + frr;
+        const int off = gf < fine_rows_total ? ((gf * FW + col) * cof + (kc << 5) + lchunk * 8) * 2 : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsy, (__attribute__((address_space(3))) void*)(Ys + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+    // weight image [t][ci BN][co chunk 32]: row t * BN + ci, from the dgrad pack [ci][t*cof + co]
+#pragma unroll
+    for (int qq = 0; qq < (WI + 3) / 4; ++qq) {
+      const int k = wave + 4 * qq;
+      if (k < WI) {
+        const int t = k / (BN / 16), cb = (k % (BN / 16)) * 16;
+        const int off = ((n0 + cb + lslot) * p.Kpad + t * cof + (kc << 5) + lchunk * 8) * 2;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int th = t >> 1, tw = t & 1;
+      bf16x8 wf[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) wf[j] = *(const bf16x8*)(Ws + (t * BN + 16 * j) * 64 + wbase);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int pl = wave * (BMc / 4) + 16 * i + fr;     // this lane's coarse pixel
+        const int rr = pl / W, w = pl - rr * W;
+        const int slot = (2 * rr + th) * FW + tw * W + w;
+        const bf16x8 xf = *(const bf16x8*)(Ys + slot * 64 + 16 * (fsub ^ ((slot >> 1) & 3)));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[j], xf, acc[i][j]);
+      }
+    }
+  }
+  __syncthreads();
+  conv_epilogue<BMc, BN, BMc / 4, BN, TM, TN, NTHR, EPI>(p, acc, smem, m0, n0, Mc, wave, 0, lane, tid);
+}
+
+hipError_t launch_tconv_fwd(const ConvFwdParams& p, hipStream_t s) {
+  const int W = p.OW;
+  const int R = 128 / W;
+  const int grid = ((p.N * p.OH + R - 1) / R) * ((p.Cout >> 2) / 32);
+  switch (W) {
+    case 8: hipLaunchKernelGGL((tconv_fwd_kernel<8, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 16: hipLaunchKernelGGL((tconv_fwd_kernel<16, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 32: hipLaunchKernelGGL((tconv_fwd_kernel<32, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 64: hipLaunchKernelGGL((tconv_fwd_kernel<64, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// data gradient: 64 input channels per workgroup (one dy image feeds 4 MFMA columns)
+hipError_t launch_tconv_dgrad(const ConvFwdParams& p, hipStream_t s) {
+  const int W = p.OW;
+  const int R = 256 / W;
+  const int grid = ((p.N * p.OH + R - 1) / R) * (p.Cout / 64);
+  const bool dg = conv_epi_mode(p) == EPI_DGRAD;
+#define TD_CASE(WW)                                                                                          \
+  case WW:                                                                                                   \
+    if (dg)                                                                                                  \
+      hipLaunchKernelGGL((tconv_dgrad_kernel<WW, 64, EPI_DGRAD>), dim3(grid), dim3(NTHR), 0, s, p);       \
+    else                                                                                                     \
+      hipLaunchKernelGGL((tconv_dgrad_kernel<WW, 64, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p);     \
+    break;
+  switch (W) {
+    TD_CASE(32)
+    TD_CASE(64)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef TD_CASE
+  return hipGetLastError();
+}
+
 template <int BN>
 hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
   const int W = p.OW;
@@ -640,6 +886,23 @@ static bool win_first_eligible(const ConvFwdParams& p) {
          (p.C1 == 4 || p.C1 == 8) && p.Cout % 32 == 0 && p.D1 == p.Cout;
 }
 
+// 2D transposed-conv forward (1x1 GEMM + 2x2 pixel shuffle) on coarse rows 8..64 wide.
+static bool tconv_fwd_eligible(const ConvFwdParams& p) {
+  const bool w_ok = p.OW == 8 || p.OW == 16 || p.OW == 32 || p.OW == 64;
+  return p.shuffle == 2 && p.KD == 1 && p.KH == 1 && p.KW == 1 && p.OD == 1 && w_ok && p.IW == p.OW &&
+         p.IH == p.OH && p.C2 == 0 && (p.C1 % 32) == 0 && ((p.Cout >> 2) % 32) == 0 && !p.relu &&
+         p.drop_rate == 0.f && !p.mask1 && !p.stats && p.out_scale == 1.f;
+}
+
+// 2D transposed-conv data gradient (2x2 stride-2 conv of the fine gradient); coarse rows
+// 32 / 64 wide (narrower levels measured faster on the implicit-GEMM kernel).
+static bool tconv_dgrad_eligible(const ConvFwdParams& p) {
+  const bool w_ok = p.OW == 32 || p.OW == 64;
+  return !p.shuffle && p.KD == 1 && p.KH == 2 && p.KW == 2 && p.stride == 2 && p.pad == 0 && p.OD == 1 &&
+         p.ID == 1 && w_ok && p.IW == 2 * p.OW && p.IH == 2 * p.OH && p.up1 == 1 && p.C2 == 0 &&
+         (p.C1 % 32) == 0 && (p.Cout % 64) == 0 && !p.stats && p.drop_rate == 0.f;
+}
+
 // Fills the tap tables and Kpad; returns nullptr on success or a message describing
 // why the shape is unsupported.
 const char* conv_fwd_prepare(ConvFwdParams& p) {
@@ -667,13 +930,15 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.shuffle && ((p.Cout >> p.shuffle) % 8)) return "conv_fwd: shuffle channels must be multiples of 8";
   if (p.shuffle && p.D1 != p.Cout) return "conv_fwd: shuffle with channel split unsupported";
   if (p.stats && p.shuffle) return "conv_fwd: stats with shuffle unsupported";
-  if (p.tile < 0 || p.tile > 9) return "conv_fwd: bad tile id";
+  if (p.tile < 0 || p.tile > 11) return "conv_fwd: bad tile id";
+  if (p.tile == 10 && !tconv_fwd_eligible(p)) return "conv_fwd: transposed-conv window tile not applicable";
+  if (p.tile == 11 && !tconv_dgrad_eligible(p)) return "conv_fwd: transposed-conv dgrad tile not applicable";
   if (p.tile == 9 && !win_first_eligible(p)) return "conv_fwd: first-layer window tile not applicable";
   {
     const int t = p.tile ? p.tile : 0;
-    const int bn = t == 1 ? 128 : (t == 2 || t == 5) ? 64 : 32;
-    if (t == 7) return "conv_fwd: tile 7 (row-window 512x64) was removed: 1 wave/SIMD, never faster";
+    const int bn = t == 1 ? 128 : (t == 2 || t == 5 || t == 7) ? 64 : 32;
     if (t && p.Cout % bn) return "conv_fwd: forced tile does not divide Cout";
+    if (t == 7) return "conv_fwd: tile 7 (row-window 512x64: 268 registers, 92 KB LDS, 1 wave/SIMD) is not built";
     if (t == 6 && !win_eligible(p)) return "conv_fwd: row-window tile not applicable";
   }
   if ((long long)p.N * p.ID * p.IH * p.IW >= (1LL << 31) || (long long)p.N * p.OD * p.OH * p.OW >= (1LL << 31))
@@ -706,6 +971,8 @@ int conv_fwd_pick(const ConvFwdParams& p) {
   // variant needs 287 registers (1 wave/SIMD) and never wins
   if (p.tile != 8 && win_eligible(p)) return 6;
   if (p.tile != 8 && win_first_eligible(p)) return 9;
+  if (p.tile != 8 && tconv_fwd_eligible(p)) return 10;
+  if (p.tile != 8 && tconv_dgrad_eligible(p)) return 11;
   if (p.Cout % 128 == 0 && M >= 8192) return 1;
   if (p.Cout % 64 == 0) return 2;
   return 4;
@@ -719,6 +986,8 @@ hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
     case 5: return launch_cfg<256, 64, 4, 1>(p, s);
     case 6: return launch_win<32>(p, s);
     case 9: return p.C1 == 4 ? launch_win_first<4>(p, s) : launch_win_first<8>(p, s);
+    case 10: return launch_tconv_fwd(p, s);
+    case 11: return launch_tconv_dgrad(p, s);
     default: return launch_cfg<128, 32, 4, 1>(p, s);
   }
 }

@@ -805,6 +805,169 @@ hipError_t launch_wgrad_win_first(const WgradParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------------
+// 2x2 stride-2 transposed-conv weight gradient on windows of whole coarse rows:
+//   dW[t][co][ci] = sum_{coarse px} dy[fine(px, t)][co] * x[px][ci],  bias = sum dy.
+// Per window the workgroup LDS-DMAs the coarse x rows (32 input channels) and the 2R
+// fine dy rows (32 output channels, even / odd columns de-interleaved so a tap's
+// pixels are consecutive slots); both operands are read with ds_read_b64_tr_b16.
+// Slab contract of the tiled kernel: slab[split][tap][co][ci], bias_slab[split][co].
+template <int W, int QN>
+__global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams p) {
+  // QN 32-channel blocks of x per workgroup (one per wave); PS = 4 / QN waves split pixels.
+  // The fine dy slice of the co block is then staged once per window for all of them.
+  constexpr int BMc = 128, R = BMc / W, FW = 2 * W;
+  constexpr int PS = 4 / QN;
+  constexpr int XI = QN * BMc / 16, YI = 2 * R * FW / 16;
+  constexpr int XB = XI * 1024, YB = YI * 1024;
+  constexpr int KS = BMc / 32;
+  constexpr int REDB = 4 * 64 * 16 * 4;
+  constexpr int LDS_BYTES = (XB + YB > REDB) ? XB + YB : REDB;
+  static_assert(W >= 32 && W <= 64 && (QN == 1 || QN == 2 || QN == 4), "tconv window wgrad");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  char* Xs = smem;
+  char* Ys = smem + XB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qn = wave % QN, ps = wave / QN;
+  const int H = p.QH;                       // coarse grid
+  const int rows_total = p.N * H;
+  const int Mq = rows_total * W;
+  const int fine_rows_total = 2 * rows_total;
+  const int nwin = (rows_total + R - 1) / R;
+  const int Mtot = p.M1;                    // output channels of the transposed conv
+  const int cit = p.Nc / (32 * QN);
+  const int ntile = (Mtot / 32) * cit;
+  const int split = blockIdx.x / ntile, tile = blockIdx.x - split * ntile;
+  const int co_blk = tile / cit, ci_blk = tile - co_blk * cit;
+  const int co0 = co_blk * 32, ci0 = ci_blk * 32 * QN;
+  constexpr int OOB = 0x7fffffff;
+  const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc((void*)p.a1, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, OOB, 0x00020000);
+  const int w_begin = (int)((long long)split * nwin / p.splits);
+  const int w_end = (int)((long long)(split + 1) * nwin / p.splits);
+  const bool do_bias = p.bias_mode == 2 && ci_blk == 0 && qn == 0;
+
+  f32x4 acc[4][2][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc[t][i][0] = acc[t][i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 bacc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+  const u32x4 ones_u = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_u);
+  const int lslot = lane >> 2;
+  const int lchunk = (lane & 3) ^ (((lslot >> 3) & 1) << 1);
+  const int G = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  auto tr_addr = [&](int slot, int ch) -> int {   // swizzle keyed on slot mod 16
+    return slot * 64 + ((((ch >> 3) ^ (((slot >> 3) & 1) << 1))) << 4) + ((ch & 7) << 1);
+  };
+  auto tr8 = [&](const char* base0, const char* base1) -> bf16x8 {
+    const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base0));
+    const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base1));
+    const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+    const u32x4 v = {l2[0], l2[1], h2[0], h2[1]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  const char* Xq = Xs + qn * (BMc * 64);
+
+  for (int win = w_begin; win < w_end; ++win) {
+    const int g0 = win * R;
+    __syncthreads();
+#pragma unroll
+    for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
+      const int k = wave + 4 * qq;
+      if (k < XI) {
+        const int o = k / (BMc / 16), sb = (k - o * (BMc / 16)) * 16;   // x image o (channel block)
+        const int pix = g0 * W + sb + lslot;
+        const int off = pix < Mq ? (pix * p.Nc + ci0 + 32 * o + lchunk * 8) * 2 : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsx, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int qq = 0; qq < (YI + 3) / 4; ++qq) {
+      const int k = wave + 4 * qq;
+      if (k < YI) {
+        const int sl = 16 * k + lslot;
+        const int frr = sl / FW, s = sl - frr * FW;
+        const int col = s < W ? 2 * s : 2 * (s - W) + 1;
+        const int gf = 2 * g0 + frr;
+        const int off = gf < fine_rows_total ? ((gf * FW + col) * Mtot + co0 + lchunk * 8) * 2 : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsy, (__attribute__((address_space(3))) void*)(Ys + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int kk = ps; kk < KS; kk += PS) {
+      const int px0 = kk * 32;
+      const int rr = px0 / W, c0 = px0 - rr * W;
+      if (g0 + rr >= rows_total) break;
+      bf16x8 bf[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int s0 = px0 + 8 * G + q;
+        bf[j] = tr8(Xq + tr_addr(s0, 16 * j + 4 * pp), Xq + tr_addr(s0 + 4, 16 * j + 4 * pp));
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int th = t >> 1, tw = t & 1;
+        const int s0 = (2 * rr + th) * FW + tw * W + c0 + 8 * G + q;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bf16x8 af = tr8(Ys + tr_addr(s0, 16 * i + 4 * pp), Ys + tr_addr(s0 + 4, 16 * i + 4 * pp));
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[t][i][j] = mfma16(af, bf[j], acc[t][i][j]);
+          if (do_bias) bacc[i] = mfma16(af, ones, bacc[i]);
+        }
+      }
+    }
+  }
+
+  // reduce the PS pixel-split partials of each channel block through LDS, then write
+  // acc[t][i][j][r] = dW[t][co0 + 16i + 4(lane>>4) + r][ci0 + 32 qn + 16j + (lane&15)]
+  float* red = (float*)smem;
+  auto reduce_store = [&](const f32x4 (&v4)[2][2], const int t) {
+    __syncthreads();
+    if (PS > 1 && ps > 0) {
+      float* dst = red + (wave * 64 + lane) * 16;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) *(f32x4*)(dst + (i * 2 + j) * 4) = v4[i][j];
+    }
+    __syncthreads();
+    if (ps == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 v = v4[i][j];
+#pragma unroll
+          for (int o = 1; o < PS; ++o) v += *(const f32x4*)(red + ((qn + QN * o) * 64 + lane) * 16 + (i * 2 + j) * 4);
+          const int m = co0 + 16 * i + 4 * (lane >> 4), n = ci0 + 32 * qn + 16 * j + (lane & 15);
+          if (t < 4) {
+            float* o = p.slab + (((size_t)split * 4 + t) * Mtot + m) * p.Nc + n;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[(size_t)r * p.Nc] = v[r];
+          } else if (qn == 0 && j == 0 && (lane & 15) == 0) {   // bias: channel-block-0 waves only
+#pragma unroll
+            for (int r = 0; r < 4; ++r) p.bias_slab[(size_t)split * Mtot + m + r] = v[r];
+          }
+        }
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < 4; ++t) reduce_store(acc[t], t);
+  if (p.bias_mode == 2 && ci_blk == 0) {     // uniform over the workgroup (qn > 0 waves hold zeros)
+    const f32x4 z = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const f32x4 bv[2][2] = {{bacc[0], z}, {bacc[1], z}};
+    reduce_store(bv, 4);
+  }
+}
+
 template <int W, int QO>
 hipError_t launch_wgrad_win(const WgradParams& p, hipStream_t s) {
   const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.splits;
@@ -834,11 +997,20 @@ static bool wgrad_win_first_eligible(const WgradParams& p) {
          (p.Nc % 32) == 0 && p.bias_mode != 2;
 }
 
+// 2D transposed conv (2x2 stride 2) on coarse rows 32 / 64 wide.
+static bool wgrad_tconv_win_eligible(const WgradParams& p) {
+  return p.win >= 0 && (p.QW == 32 || p.QW == 64) && p.QD == 1 && p.KD == 1 && p.KH == 2 && p.KW == 2 &&
+         p.stride == 2 && p.pad == 0 && p.upA == 1 && p.AW == 2 * p.QW && p.AH == 2 * p.QH && p.M2 == 0 &&
+         (p.M1 % 32) == 0 && (p.Nc % 32) == 0 && p.bias_mode != 1;
+}
+
 WgradCfg wgrad_pick(const WgradParams& p) {
   const int KT = p.KD * p.KH * p.KW;
   const int M = p.M1 + p.M2;
   if (wgrad_win_eligible(p)) return {32, (p.Nc % 64 == 0) ? 64 : 32, 9, 0};   // row-window tile
   if (wgrad_win_first_eligible(p)) return {p.M1 == 4 ? 48 : 80, 32, 1, 1};      // first-layer window
+  if (wgrad_tconv_win_eligible(p))                                                 // transposed-conv window
+    return {32, p.Nc % 128 == 0 ? 128 : (p.Nc % 64 == 0 ? 64 : 32), 4, 0};
   if ((p.M1 == 4 || p.M1 == 8) && p.M2 == 0) return {64, 32, 1, 1};
   if (M <= 64 && p.Nc <= 64 && KT % 9 == 0) return {32, 32, 9, 0};
   if (M <= 64 && p.Nc <= 64 && KT % 4 == 0) return {32, 32, 4, 0};
@@ -867,6 +1039,18 @@ const char* wgrad_check(const WgradParams& p) {
 hipError_t wgrad_launch(const WgradParams& p, hipStream_t s) {
   const WgradCfg c = wgrad_pick(p);
   if (wgrad_win_first_eligible(p)) return p.M1 == 4 ? launch_wgrad_win_first<4>(p, s) : launch_wgrad_win_first<8>(p, s);
+  if (wgrad_tconv_win_eligible(p)) {
+    const int qn = p.Nc % 128 == 0 ? 4 : (p.Nc % 64 == 0 ? 2 : 1);
+    const int grid = (p.M1 / 32) * (p.Nc / (32 * qn)) * p.splits;
+#define TW_CASE(WW, QQ) hipLaunchKernelGGL((wgrad_tconv_win_kernel<WW, QQ>), dim3(grid), dim3(NTHR), 0, s, p)
+    if (p.QW == 32) {
+      if (qn == 4) TW_CASE(32, 4); else if (qn == 2) TW_CASE(32, 2); else TW_CASE(32, 1);
+    } else {
+      if (qn == 4) TW_CASE(64, 4); else if (qn == 2) TW_CASE(64, 2); else TW_CASE(64, 1);
+    }
+#undef TW_CASE
+    return hipGetLastError();
+  }
   if (wgrad_win_eligible(p)) {
     const bool q2 = c.BN == 64;
     switch (p.QW) {

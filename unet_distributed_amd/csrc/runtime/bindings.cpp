@@ -384,12 +384,20 @@ PYBIND11_MODULE(_C, m) {
         p.upA = upA;
         p.win = win;
         p.bias_mode = 1;
-        if (QW > 0 && KT == 9) {
+        if (QW > 0 && KT == 9) {          // 3x3 stride-1 'same' conv
           p.KH = p.KW = 3;
           p.QD = p.AD = 1;
           p.QW = p.QH = p.AW = p.AH = QW;
           p.stride = 1;
           p.pad = 1;
+        } else if (QW > 0 && KT == 4) {   // 2x2 stride-2 transposed conv (QW = coarse width)
+          p.KH = p.KW = 2;
+          p.QD = p.AD = 1;
+          p.QW = p.QH = QW;
+          p.AW = p.AH = 2 * QW;
+          p.stride = 2;
+          p.pad = 0;
+          p.bias_mode = 2;
         }
         WgradCfg c = wgrad_pick(p);
         return py::make_tuple(c.BM, c.BN, c.NTAP, c.smallc);

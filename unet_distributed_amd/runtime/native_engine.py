@@ -522,6 +522,7 @@ class NativeUNet:
                           KD=2 if self.dims == 3 else 1, KH=2, KW=2, stride=2, pad=0, upA=1,
                           a1=_ptr(du), b=_ptr(b[src]))
                 emit_wgrad(dict(lname=l.name, kd=kd, M1=l.cout, M2=0, Nc=l.cin, KT=KT2,
+                                QW=lo[2] if self.dims == 2 else 0,
                                 Q=self.npix(l.level + 1), kernel=l.name + "/kernel",
                                 bias=l.name + "/bias", bias_mode=2, bias_width=l.cout, real_rows=None,
                                 bias_src=(du, self.npix(l.level))))
