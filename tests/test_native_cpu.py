@@ -28,9 +28,15 @@ def test_plan_construction_dry_run(kw, img):
     names = e.plan.names()
     assert names[0] == "cast_input" and names[e.fwd_end - 1] == "fwd:Mask"
     assert names[e.fwd_end] == "bwd:Mask"
-    # every parameter gradient is produced by exactly one reduce op
-    produced = [n for n in names if n.startswith(("wred:", "bred:")) or n == "bwd:Mask"]
-    assert len([n for n in names if n.startswith("wred:")]) == len(spec.param_layers()) - 1
+    # every conv / tconv gradient is reduced by exactly one batched reduce op
+    reduced = [ln for n in names if n.startswith("reduce:") for ln in n[len("reduce:"):].split(",")]
+    assert sorted(reduced) == sorted(l.name for l in spec.param_layers() if l.kind != "mask")
+    assert len(reduced) == len(set(reduced))
+    # every wgrad is followed (later) by the reduce that covers its layer
+    for i, n in enumerate(names):
+        if n.startswith("wgrad:"):
+            ln = n.split(":", 1)[1]
+            assert any(m.startswith("reduce:") and ln in m[len("reduce:"):].split(",") for m in names[i + 1:])
     assert e.seg_ends[-1] == e.plan.size() and sorted(e.seg_ends) == e.seg_ends
     # dgrad of the first conv is never planned
     assert "dgrad:conv1a" not in names

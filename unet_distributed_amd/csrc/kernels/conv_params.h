@@ -71,6 +71,21 @@ struct WgradCfg {
   int BM, BN, NTAP, smallc;
 };
 
+// One gradient of a batched slab reduction (conv_wgrad.hip::multi_reduce*).  Built on
+// the host (runtime/native_engine.py mirrors this layout, 96 bytes).
+struct ReduceJob {
+  const float* slab;     // [splits][n4 * 4]
+  float* out;            // [n4o * 4]
+  float* stage;          // [groups][n4 * 4] (unused when direct)
+  long long n4, n4o;     // float4 elements per split / of the output
+  long long p1_begin;    // first global thread index of phase 1 (groups * n4 threads)
+  long long p2_begin;    // first global thread index of phase 2 (n4o threads)
+  int splits, groups;
+  int taps, Mtot, Mout, Nc;
+  int rg, rkeep;
+  int direct, pad_;
+};
+
 // Segment descriptor of the fused Adam + bf16 repack kernel (adam.hip).
 struct PackSeg {
   int off, n;          // element range in the flat master buffer

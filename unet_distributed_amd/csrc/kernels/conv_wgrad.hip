@@ -366,6 +366,57 @@ __global__ void __launch_bounds__(256) slab_final_kernel(const float* __restrict
   ((f32x4*)out)[i] = acc;
 }
 
+
+// Batched deterministic slab reduction: one launch per phase for a whole list of
+// weight / bias gradients (a backward segment's worth), instead of two tiny launches
+// per gradient.  Phase 1: stage[g][i] = sum of the splits of group g (groups of
+// RED_G); jobs with a single group and an identity row map write the output directly.
+// Phase 2: out[o] = sum_g stage[g][row_map(o)].  Threads find their job by a scan of
+// the (few dozen) prefix offsets.
+__global__ void __launch_bounds__(256) multi_reduce1_kernel(const ReduceJob* __restrict__ jobs, int njobs,
+                                                            long long total) {
+  const long long gi = blockIdx.x * 256LL + threadIdx.x;
+  if (gi >= total) return;
+  int j = 0;
+  while (j + 1 < njobs && jobs[j + 1].p1_begin <= gi) ++j;
+  const ReduceJob& J = jobs[j];
+  const long long local = gi - J.p1_begin;
+  const int g = (int)(local / J.n4);
+  const long long i = local - (long long)g * J.n4;
+  const int s0 = g * RED_G, s1 = min(J.splits, s0 + RED_G);
+  const f32x4* src = (const f32x4*)J.slab + i;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  int s = s0;
+  for (; s + 4 <= s1; s += 4) {
+    const f32x4 a = src[(size_t)s * J.n4], b = src[(size_t)(s + 1) * J.n4];
+    const f32x4 c = src[(size_t)(s + 2) * J.n4], d = src[(size_t)(s + 3) * J.n4];
+    acc += (a + b) + (c + d);
+  }
+  for (; s < s1; ++s) acc += src[(size_t)s * J.n4];
+  ((f32x4*)(J.direct ? J.out : J.stage))[(size_t)g * J.n4 + i] = acc;
+}
+
+__global__ void __launch_bounds__(256) multi_reduce2_kernel(const ReduceJob* __restrict__ jobs, int njobs,
+                                                            long long total) {
+  const long long gi = blockIdx.x * 256LL + threadIdx.x;
+  if (gi >= total) return;
+  int j = 0;
+  while (j + 1 < njobs && jobs[j + 1].p2_begin <= gi) ++j;
+  const ReduceJob& J = jobs[j];
+  const long long i = gi - J.p2_begin;
+  if (J.direct || i >= J.n4o) return;
+  const size_t e = i * 4;
+  const int n = e % J.Nc;
+  const size_t r = e / J.Nc;
+  const int mo = r % J.Mout;
+  const int t = r / J.Mout;
+  const int m = (mo / J.rkeep) * J.rg + (mo % J.rkeep);
+  const size_t src = (((size_t)t * J.Mtot + m) * J.Nc + n) / 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int y = 0; y < J.groups; ++y) acc += ((const f32x4*)J.stage)[(size_t)y * J.n4 + src];
+  ((f32x4*)J.out)[i] = acc;
+}
+
 // partial[b][c] = sum over rows r of block b of x[r][c]   (bf16 [rows][C], C % 8 == 0, C <= 1024)
 __global__ void __launch_bounds__(256) colsum_kernel(const bf16* __restrict__ x, int rows, int C, int rows_per_block,
                                                      float* __restrict__ partial) {
@@ -1091,6 +1142,18 @@ hipError_t wgrad_reduce_launch(const float* slab, int splits, int taps, int Mtot
   const size_t n4o = (size_t)taps * Mout * Nc / 4;
   hipLaunchKernelGGL(slab_final_kernel, dim3((unsigned)((n4o + 255) / 256)), dim3(256), 0, s, stage, groups, taps,
                      Mtot, Mout, Nc, rg, rkeep, out);
+  return hipGetLastError();
+}
+
+int reduce_groups(int splits) { return (splits + RED_G - 1) / RED_G; }
+
+hipError_t multi_reduce_launch(const void* jobs, int njobs, long long total1, long long total2, hipStream_t s) {
+  if (total1 > 0)
+    hipLaunchKernelGGL(multi_reduce1_kernel, dim3((unsigned)((total1 + 255) / 256)), dim3(256), 0, s,
+                       (const ReduceJob*)jobs, njobs, total1);
+  if (total2 > 0)
+    hipLaunchKernelGGL(multi_reduce2_kernel, dim3((unsigned)((total2 + 255) / 256)), dim3(256), 0, s,
+                       (const ReduceJob*)jobs, njobs, total2);
   return hipGetLastError();
 }
 

@@ -188,6 +188,14 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
       throw std::invalid_argument("wgrad_reduce: stage buffer required for >16 splits or row remap");
     return [=](hipStream_t s) { return wgrad_reduce_launch(slab, sp, taps, mt, mo, nc, rg, rk, sc, out, stage, s); };
   }
+  if (kind == "multi_reduce") {
+    // ptrs: job table (device, ReduceJob[njobs])   ints: njobs, total1, total2
+    need(1, 3, 0);
+    const void* jobs = vp(0);
+    int nj = (int)I[0];
+    long long t1 = I[1], t2 = I[2];
+    return [=](hipStream_t s) { return multi_reduce_launch(jobs, nj, t1, t2, s); };
+  }
   if (kind == "colsum") {
     need(2, 3, 0);
     void* x = vp(0);
@@ -405,6 +413,8 @@ PYBIND11_MODULE(_C, m) {
       py::arg("M1"), py::arg("M2"), py::arg("Nc"), py::arg("KT"), py::arg("QW") = 0, py::arg("upA") = 1,
       py::arg("win") = -1);
   m.def("packseg_bytes", []() { return (int)sizeof(PackSeg); });
+  m.def("reduce_job_bytes", []() { return (int)sizeof(ReduceJob); });
+  m.def("reduce_groups", &reduce_groups);
   m.def("crc32c", [](py::buffer b, uint32_t crc) {
     py::buffer_info info = b.request();
     const size_t n = (size_t)info.size * (size_t)info.itemsize;

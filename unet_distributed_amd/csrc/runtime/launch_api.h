@@ -17,6 +17,8 @@ hipError_t wgrad_launch(const WgradParams& p, hipStream_t s);
 hipError_t wgrad_reduce_launch(const float* slab, int splits, int taps, int Mtot, int Mout, int Nc, int rg, int rkeep,
                                float scale, float* out, float* stage, hipStream_t s);
 size_t wgrad_reduce_stage_floats(int splits, int taps, int Mtot, int Nc);
+int reduce_groups(int splits);
+hipError_t multi_reduce_launch(const void* jobs, int njobs, long long total1, long long total2, hipStream_t s);
 hipError_t colsum_launch(const void* x, int rows, int C, int blocks, float* partial, hipStream_t s);
 
 hipError_t cast_input_launch(const float* x, int P, int Cin, int Cpad, void* y, hipStream_t s);

@@ -538,71 +538,112 @@ class NativeUNet:
             elif l.kind == "up":
                 pass
 
-        # size the wgrad workspaces
-        sized = []
-        smax, bmax = 1, 1
-        for w in wg_specs:
-            splits, Mtot, taps, tg, smallc = self._wgrad_splits(w)
-            sized.append((splits, Mtot, taps, tg, smallc))
-            smax = max(smax, splits * taps * Mtot * w["Nc"])
-            bw = w["bias_width"] if w["bias_mode"] == 1 else Mtot
-            bmax = max(bmax, splits * tg * bw)
-            bmax = max(bmax, self._colsum_blocks(w["bias_src"][1], w["bias_width"]) * w["bias_width"])
-        stmax = 1
+        # size the wgrad workspaces: every wgrad gets its own slab / bias-slab / stage
+        # region (HBM is plentiful) so the split-K reductions of several layers can be
+        # batched into one launch per phase (multi_reduce), flushed every few layers
+        sized = [self._wgrad_splits(w) for w in wg_specs]
+        stot = btot = sttot = 0
+        regions = []
         for w, (splits, Mtot, taps, tg, smallc) in zip(wg_specs, sized):
-            stmax = max(stmax, self.C.wgrad_reduce_stage_floats(splits, taps, Mtot, w["Nc"]))
             bw = w["bias_width"] if w["bias_mode"] == 1 else Mtot
-            stmax = max(stmax, self.C.wgrad_reduce_stage_floats(splits * tg, 1, 1, bw))
-            stmax = max(stmax, self.C.wgrad_reduce_stage_floats(
-                self._colsum_blocks(w["bias_src"][1], w["bias_width"]), 1, 1, w["bias_width"]))
-        self.slab = torch.empty(smax, dtype=torch.float32, device=self.device)
-        self.bias_slab = torch.empty(bmax, dtype=torch.float32, device=self.device)
-        self.red_stage = torch.empty(stmax, dtype=torch.float32, device=self.device)
+            ncol = self._colsum_blocks(w["bias_src"][1], w["bias_width"])
+            nb_rows = max(splits * tg, ncol)
+            st_k = self.C.reduce_groups(splits) * taps * Mtot * w["Nc"]
+            st_b = self.C.reduce_groups(nb_rows) * max(bw, w["bias_width"])
+            regions.append((stot, btot, sttot, sttot + _r64(st_k)))
+            stot += _r64(splits * taps * Mtot * w["Nc"])
+            btot += _r64(nb_rows * max(bw, w["bias_width"]))
+            sttot += _r64(st_k) + _r64(st_b)
+        self.slab = torch.empty(max(stot, 64), dtype=torch.float32, device=self.device)
+        self.bias_slab = torch.empty(max(btot, 64), dtype=torch.float32, device=self.device)
+        self.red_stage = torch.empty(max(sttot, 64), dtype=torch.float32, device=self.device)
+        self._job_tables = []
+        job_dt = np.dtype([("slab", "<i8"), ("out", "<i8"), ("stage", "<i8"), ("n4", "<i8"), ("n4o", "<i8"),
+                           ("p1", "<i8"), ("p2", "<i8"), ("splits", "<i4"), ("groups", "<i4"), ("taps", "<i4"),
+                           ("Mtot", "<i4"), ("Mout", "<i4"), ("Nc", "<i4"), ("rg", "<i4"), ("rkeep", "<i4"),
+                           ("direct", "<i4"), ("pad", "<i4")])
+        assert job_dt.itemsize == self.C.reduce_job_bytes()
+        pending_jobs, pending_layers = [], []
+        wgrad_layers = {w["lname"] for w in wg_specs}
+        FLUSH_LAYERS = 3
 
+        def job(slab, out, stage, splits, taps, Mtot, Mout, Nc, rg=0, rkeep=0):
+            rg = rg if rg > 0 else Mout
+            rkeep = rkeep if rkeep > 0 else rg
+            groups = self.C.reduce_groups(splits)
+            direct = int(groups == 1 and Mout == Mtot and rg == rkeep)
+            assert (taps * Mtot * Nc) % 4 == 0 and (taps * Mout * Nc) % 4 == 0
+            return dict(slab=slab, out=out, stage=stage, n4=taps * Mtot * Nc // 4, n4o=taps * Mout * Nc // 4,
+                        splits=splits, groups=groups, taps=taps, Mtot=Mtot, Mout=Mout, Nc=Nc, rg=rg, rkeep=rkeep,
+                        direct=direct)
+
+        def flush():
+            if not pending_jobs:
+                return
+            arr = np.zeros(len(pending_jobs), dtype=job_dt)
+            t1 = t2 = 0
+            for k, j in enumerate(pending_jobs):
+                for f in ("slab", "out", "stage", "n4", "n4o", "splits", "groups", "taps", "Mtot", "Mout", "Nc",
+                          "rg", "rkeep", "direct"):
+                    arr[k][f] = j[f]
+                arr[k]["p1"], arr[k]["p2"] = t1, t2
+                t1 += j["groups"] * j["n4"]
+                t2 += 0 if j["direct"] else j["n4o"]
+            table = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
+            self._job_tables.append(table)
+            plan.add_generic("multi_reduce", [_ptr(table)], [len(pending_jobs), t1, t2], [],
+                             "reduce:" + ",".join(pending_layers))
+            for ln in pending_layers:
+                self._layer_done_at[ln] = plan.size()
+            pending_jobs.clear()
+            pending_layers.clear()
+
+        slab0, bslab0, stage0 = _ptr(self.slab), _ptr(self.bias_slab), _ptr(self.red_stage)
         for op in ops:
             if callable(op):
                 op(plan)
             elif op[0] == "done":
-                self._layer_done_at[op[1]] = plan.size()
+                if op[1] in wgrad_layers:
+                    pending_layers.append(op[1])
+                    if len(pending_layers) >= FLUSH_LAYERS:
+                        flush()
+                else:
+                    self._layer_done_at[op[1]] = plan.size()
             else:
                 w = wg_specs[op[1]]
                 splits, Mtot, taps, tg, smallc = sized[op[1]]
+                so, bo, sto_k, sto_b = regions[op[1]]
+                slab, bslab = slab0 + 4 * so, bslab0 + 4 * bo
+                stage_k, stage_b = stage0 + 4 * sto_k, stage0 + 4 * sto_b
                 d = dict(w["kd"])
                 BM = self._wgrad_pick(w)[0]
                 # the 128x128 tile has no register room for the fused ones-MFMA bias sums:
                 # those (level >= 3, small dY) use a separate column-sum pass instead
                 fused_bias = BM < 128
                 d.update(name="wgrad:" + w["lname"], M1=w["M1"], M2=w["M2"], Nc=w["Nc"], splits=splits,
-                         win=self.wgrad_win,
-                         slab=_ptr(self.slab), bias_mode=w["bias_mode"] if fused_bias else 0,
-                         bias_slab=_ptr(self.bias_slab))
+                         win=self.wgrad_win, slab=slab, bias_mode=w["bias_mode"] if fused_bias else 0,
+                         bias_slab=bslab)
                 plan.add_wgrad(d)
-                rr = w["real_rows"]
                 KT = w["KT"]
                 if smallc:
-                    cpad, creal = rr
-                    plan.add_generic("wgrad_reduce", [_ptr(self.slab), self.grad_ptr(w["kernel"]), _ptr(self.red_stage)],
-                                     [splits, 1, Mtot, KT * creal, w["Nc"], cpad, creal], [1.0],
-                                     "wred:" + w["lname"])
+                    cpad, creal = w["real_rows"]
+                    pending_jobs.append(job(slab, self.grad_ptr(w["kernel"]), stage_k, splits, 1, Mtot, KT * creal,
+                                            w["Nc"], cpad, creal))
                 else:
-                    plan.add_generic("wgrad_reduce", [_ptr(self.slab), self.grad_ptr(w["kernel"]), _ptr(self.red_stage)],
-                                     [splits, taps, Mtot, Mtot, w["Nc"]], [1.0], "wred:" + w["lname"])
+                    pending_jobs.append(job(slab, self.grad_ptr(w["kernel"]), stage_k, splits, taps, Mtot, Mtot,
+                                            w["Nc"]))
                 bw = w["bias_width"]
                 if not fused_bias:
                     src, rows = w["bias_src"]
                     nb = self._colsum_blocks(rows, bw)
-                    plan.add_generic("colsum", [_ptr(src), _ptr(self.bias_slab)], [rows, bw, nb], [],
-                                     "bsum:" + w["lname"])
-                    plan.add_generic("wgrad_reduce", [_ptr(self.bias_slab), self.grad_ptr(w["bias"]),
-                                                      _ptr(self.red_stage)],
-                                     [nb, 1, 1, 1, bw], [1.0], "bred:" + w["lname"])
+                    plan.add_generic("colsum", [_ptr(src), bslab], [rows, bw, nb], [], "bsum:" + w["lname"])
+                    pending_jobs.append(job(bslab, self.grad_ptr(w["bias"]), stage_b, nb, 1, 1, 1, bw))
                 elif w["bias_mode"] == 1:
-                    plan.add_generic("wgrad_reduce", [_ptr(self.bias_slab), self.grad_ptr(w["bias"]), _ptr(self.red_stage)],
-                                     [splits, 1, 1, 1, bw], [1.0], "bred:" + w["lname"])
+                    pending_jobs.append(job(bslab, self.grad_ptr(w["bias"]), stage_b, splits, 1, 1, 1, bw))
                 else:
                     # [splits*tg][Mtot] rows -> bias (Mtot == cout for tconv)
-                    plan.add_generic("wgrad_reduce", [_ptr(self.bias_slab), self.grad_ptr(w["bias"]), _ptr(self.red_stage)],
-                                     [splits * tg, 1, 1, 1, bw], [1.0], "bred:" + w["lname"])
+                    pending_jobs.append(job(bslab, self.grad_ptr(w["bias"]), stage_b, splits * tg, 1, 1, 1, bw))
+        flush()
 
     # ------------------------------------------------------------------ buckets
     def set_buckets(self, bounds: Optional[Sequence[int]]):
