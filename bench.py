@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp16"])
     p.add_argument("--bucket_mb", type=float, default=8.0)
     p.add_argument("--no_overlap", action="store_true")
+    p.add_argument("--hip_graph", type=int, default=0, help="replay the step as captured HIP graphs")
     p.add_argument("--profile_dir", default="")
     return p.parse_args()
 
@@ -67,7 +68,8 @@ def main():
     cfg = Config(batch_size=a.per_gpu_batch * N, in_channels=a.in_channels, img_size=a.img_size,
                  dims=a.dims, use_upsampling=a.use_upsampling, backend=a.backend, dtype=a.dtype,
                  norm=a.norm, groups=a.groups,
-                 synthetic=True, no_checkpoint=True, bucket_mb=a.bucket_mb, overlap_comm=not a.no_overlap)
+                 synthetic=True, no_checkpoint=True, bucket_mb=a.bucket_mb, overlap_comm=not a.no_overlap,
+                 hip_graph=bool(a.hip_graph))
     dev = ctx.device
     spec = spec_from_config(cfg)
     flat = FlatParams(spec, device=dev)

@@ -26,7 +26,13 @@ __global__ void __launch_bounds__(256) adam_pack_kernel(float* __restrict__ w, c
                                                         float* __restrict__ m, float* __restrict__ v, int n_total,
                                                         const PackSeg* __restrict__ segs, int nseg, float lr_t,
                                                         float b1, float b2, float eps, float gscale, int do_adam,
+                                                        const float* __restrict__ dev_scalars,
                                                         bf16* __restrict__ arena) {
+  // HIP-graph replay: the per-step lr_t / gradient scale come from device memory
+  if (dev_scalars) {
+    lr_t = dev_scalars[0];
+    gscale = dev_scalars[1];
+  }
   __shared__ PackSeg S[MAX_SEG];
   for (int i = threadIdx.x; i < nseg; i += blockDim.x) S[i] = segs[i];
   __syncthreads();
@@ -77,12 +83,12 @@ const char* adam_check(int nseg) {
 }
 
 hipError_t adam_pack_launch(float* w, const float* g, float* m, float* v, int n_total, const void* segs, int nseg,
-                            float lr_t, float b1, float b2, float eps, float gscale, int do_adam, void* arena,
-                            hipStream_t s) {
+                            float lr_t, float b1, float b2, float eps, float gscale, int do_adam,
+                            const float* dev_scalars, void* arena, hipStream_t s) {
   int grid = (n_total + 255) / 256;
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL(adam_pack_kernel, dim3(grid), dim3(256), 0, s, w, g, m, v, n_total, (const PackSeg*)segs, nseg,
-                     lr_t, b1, b2, eps, gscale, do_adam, (bf16*)arena);
+                     lr_t, b1, b2, eps, gscale, do_adam, dev_scalars, (bf16*)arena);
   return hipGetLastError();
 }
 

@@ -57,6 +57,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
   constexpr bool kMaskScale = EPI != EPI_FWD;
   const float inv_keep = p.drop_rate > 0.f ? 1.f / (1.f - p.drop_rate) : 1.f;
   const uint32_t drop_thr = (uint32_t)(p.drop_rate * 4294967296.0);
+  const uint32_t seed = (kDrop && p.seed_ptr) ? *p.seed_ptr : p.seed;
   const int Dtb = kShuffle ? (p.Cout >> p.shuffle) : p.Cout;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -79,7 +80,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
         float x = G ? acc[i][j][r] * p.out_scale + bsv[r] : acc[i][j][r] + bsv[r];
         if (kRelu) x = fmaxf(x, 0.f);
         if (kDrop) {
-          const uint32_t h = drop_hash((uint64_t)q * p.Cout + n + r, p.seed, p.salt);
+          const uint32_t h = drop_hash((uint64_t)q * p.Cout + n + r, seed, p.salt);
           x = (h >= drop_thr) ? x * inv_keep : 0.f;
         }
         if (kMaskScale) x *= msc[r];

@@ -24,6 +24,8 @@ struct ConvFwdParams {
   float out_scale;
   float drop_rate;            // >0: inverted dropout on the output
   uint32_t seed, salt;
+  const uint32_t* seed_ptr;   // non-null: the per-step seed is read from device memory
+                              // (HIP-graph replay, where kernel arguments are frozen)
   void* dst1;                 // channels [0, D1)
   void* dst2;                 // channels [D1, Cout)
   int D1;

@@ -191,7 +191,9 @@ __global__ void __launch_bounds__(NT) norm_apply_kernel(const bf16* __restrict__
                                                         const float* __restrict__ rstd, int cstride,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int relu, float drop_rate,
-                                                        uint32_t seed, uint32_t salt, bf16* __restrict__ y) {
+                                                        uint32_t seed0, const uint32_t* __restrict__ seed_ptr,
+                                                        uint32_t salt, bf16* __restrict__ y) {
+  const uint32_t seed = (drop_rate > 0.f && seed_ptr) ? *seed_ptr : seed0;
   const int cpr = C / 8;
   const long long total = (long long)N * P * cpr;
   const float inv_keep = drop_rate > 0.f ? 1.f / (1.f - drop_rate) : 1.f;
@@ -297,9 +299,9 @@ hipError_t gn_finalize_launch(const float* S, int N, int C, int G, int P, int mo
 
 hipError_t norm_apply_launch(const void* z, int N, int P, int C, const float* mean, const float* rstd, int cstride,
                              const float* gamma, const float* beta, int relu, float drop_rate, uint32_t seed,
-                             uint32_t salt, void* y, hipStream_t s) {
+                             const uint32_t* seed_ptr, uint32_t salt, void* y, hipStream_t s) {
   hipLaunchKernelGGL(norm_apply_kernel, dim3(ew_grid((long long)N * P * (C / 8))), dim3(NT), 0, s, (const bf16*)z, N,
-                     P, C, mean, rstd, cstride, gamma, beta, relu, drop_rate, seed, salt, (bf16*)y);
+                     P, C, mean, rstd, cstride, gamma, beta, relu, drop_rate, seed, seed_ptr, salt, (bf16*)y);
   return hipGetLastError();
 }
 

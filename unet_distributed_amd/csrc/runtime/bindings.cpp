@@ -137,9 +137,11 @@ using Launcher = std::function<hipError_t(hipStream_t)>;
 
 // generic memory-bound ops: (kind, pointer args, int args, float args)
 // seedp: the owning plan's per-step dropout seed (nullptr for immediate calls: the
-// seed is then the op's last int argument)
+// seed is then the op's last int argument); seed_devp: the plan's device seed pointer
+// (set for HIP-graph capture, where kernel arguments are frozen at capture time)
 Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, const std::vector<long long>& I,
-                      const std::vector<double>& F, const uint32_t* seedp = nullptr) {
+                      const std::vector<double>& F, const uint32_t* seedp = nullptr,
+                      const uint32_t* const* seed_devp = nullptr) {
   auto need = [&](size_t np, size_t ni, size_t nf) {
     if (P.size() < np || I.size() < ni || F.size() < nf)
       throw std::invalid_argument("generic op '" + kind + "': wrong argument count");
@@ -282,7 +284,8 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     float dr = (float)F[0];
     check_msg(norm_check(c, 0));
     return [=](hipStream_t s) {
-      return norm_apply_launch(z, n, np, c, mu, rs, cs, gm, bt, relu, dr, seedp ? *seedp : seed0, salt, y, s);
+      return norm_apply_launch(z, n, np, c, mu, rs, cs, gm, bt, relu, dr, seedp ? *seedp : seed0,
+                               seed_devp ? *seed_devp : nullptr, salt, y, s);
     };
   }
   if (kind == "norm_bwd_apply") {
@@ -311,9 +314,13 @@ class Plan {
   int add_conv_fwd(const py::dict& d) {
     ConvFwdParams p = conv_params(d);
     const bool seeded = p.drop_rate > 0.f;
-    uint32_t* seedp = &seed_;
-    ops_.push_back([p, seeded, seedp](hipStream_t s) mutable {
-      if (seeded) p.seed = *seedp;
+    const uint32_t* seedp = &seed_;
+    const uint32_t* const* seed_devp = &seed_dev_;
+    ops_.push_back([p, seeded, seedp, seed_devp](hipStream_t s) mutable {
+      if (seeded) {
+        p.seed = *seedp;
+        p.seed_ptr = *seed_devp;
+      }
       return conv_fwd_launch(p, s);
     });
     names_.push_back(get<std::string>(d, "name", "conv_fwd"));
@@ -327,11 +334,13 @@ class Plan {
   }
   int add_generic(const std::string& kind, const std::vector<uintptr_t>& P, const std::vector<long long>& I,
                   const std::vector<double>& F, const std::string& name) {
-    ops_.push_back(make_generic(kind, P, I, F, &seed_));
+    ops_.push_back(make_generic(kind, P, I, F, &seed_, &seed_dev_));
     names_.push_back(name.empty() ? kind : name);
     return (int)ops_.size() - 1;
   }
   void set_seed(uint32_t s) { seed_ = s; }
+  // device address of a uint32 seed: dropout kernels read it at run time (graph mode)
+  void set_seed_ptr(uintptr_t p) { seed_dev_ = reinterpret_cast<const uint32_t*>(p); }
   int size() const { return (int)ops_.size(); }
   std::vector<std::string> names() const { return names_; }
   void run(int begin, int end, uintptr_t stream) {
@@ -348,6 +357,7 @@ class Plan {
   std::vector<Launcher> ops_;
   std::vector<std::string> names_;
   uint32_t seed_ = 0;
+  const uint32_t* seed_dev_ = nullptr;
 };
 
 }  // namespace
@@ -368,13 +378,16 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("adam_pack", [](uintptr_t w, uintptr_t g, uintptr_t mm, uintptr_t v, int n_total, uintptr_t segs, int nseg,
                         double lr_t, double b1, double b2, double eps, double gscale, int do_adam, uintptr_t arena,
-                        uintptr_t stream) {
+                        uintptr_t stream, uintptr_t scalars) {
+    // scalars: optional device float[2] = {lr_t, gscale} read by the kernel (HIP-graph replay)
     check_msg(adam_check(nseg));
     check(adam_pack_launch((float*)w, (const float*)g, (float*)mm, (float*)v, n_total, (const void*)segs, nseg,
-                           (float)lr_t, (float)b1, (float)b2, (float)eps, (float)gscale, do_adam, (void*)arena,
-                           as_stream(stream)),
+                           (float)lr_t, (float)b1, (float)b2, (float)eps, (float)gscale, do_adam,
+                           (const float*)scalars, (void*)arena, as_stream(stream)),
           "adam_pack");
-  });
+  }, py::arg("w"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("n_total"), py::arg("segs"), py::arg("nseg"),
+     py::arg("lr_t"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("gscale"), py::arg("do_adam"),
+     py::arg("arena"), py::arg("stream"), py::arg("scalars") = 0);
   m.def("head_blocks", &head_blocks_py);
   m.def("norm_blocks_per_sample", &norm_blocks_per_sample);
   m.def("wgrad_reduce_stage_floats", &wgrad_reduce_stage_floats);
@@ -437,6 +450,7 @@ PYBIND11_MODULE(_C, m) {
       .def("add_generic", &Plan::add_generic, py::arg("kind"), py::arg("ptrs"), py::arg("ints"),
            py::arg("floats"), py::arg("name") = "")
       .def("set_seed", &Plan::set_seed)
+      .def("set_seed_ptr", &Plan::set_seed_ptr)
       .def("size", &Plan::size)
       .def("names", &Plan::names)
       .def("run", &Plan::run, py::call_guard<py::gil_scoped_release>());

@@ -49,14 +49,14 @@ hipError_t gn_finalize_launch(const float* S, int N, int C, int G, int P, int mo
                               hipStream_t s);
 hipError_t norm_apply_launch(const void* z, int N, int P, int C, const float* mean, const float* rstd, int cstride,
                              const float* gamma, const float* beta, int relu, float drop_rate, uint32_t seed,
-                             uint32_t salt, void* y, hipStream_t s);
+                             const uint32_t* seed_ptr, uint32_t salt, void* y, hipStream_t s);
 hipError_t norm_bwd_apply_launch(const void* g, const void* z, int N, int P, int C, const float* ca, const float* cb,
                                  const float* cc, int cstride, void* dz, hipStream_t s);
 
 const char* adam_check(int nseg);
 hipError_t adam_pack_launch(float* w, const float* g, float* m, float* v, int n_total, const void* segs, int nseg,
-                            float lr_t, float b1, float b2, float eps, float gscale, int do_adam, void* arena,
-                            hipStream_t s);
+                            float lr_t, float b1, float b2, float eps, float gscale, int do_adam,
+                            const float* dev_scalars, void* arena, hipStream_t s);
 
 uint32_t crc32c_extend(uint32_t crc, const uint8_t* p, size_t n);
 void gather_rows(const uint8_t* src, const int64_t* idx, int64_t n, int64_t row_bytes, uint8_t* dst, int threads);

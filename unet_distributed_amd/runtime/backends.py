@@ -102,6 +102,8 @@ class NativeBackend:
                                  bce_weight=cfg.bce_weight, bucket_bounds=bounds,
                                  eval_dropout=cfg.eval_dropout)
         self.B = per_rank_batch
+        if getattr(cfg, "hip_graph", False):
+            self.engine.enable_graphs()
         self.state = self.engine.state        # BatchNorm running statistics (checkpointed)
 
     def set_buckets(self, bounds):

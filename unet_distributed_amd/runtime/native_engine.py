@@ -29,6 +29,7 @@ The executor plays the role of the reference's TF graph + session
 
 import math
 import os
+from contextlib import nullcontext as _nullctx
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -63,6 +64,7 @@ class NativeUNet:
             raise NotImplementedError("native executor: n_cl_out must be 1")
         self.spec = spec
         self.flat = flat
+        self.graphs = None      # HIP-graph cache (enable_graphs)
         self.B = batch
         self.img = img
         self.dims = spec.dims
@@ -182,6 +184,15 @@ class NativeUNet:
                   beta1=0.9, beta2=0.999, eps=1e-8):
         f = self.flat
         lr_t = lr * math.sqrt(1.0 - beta2_power) / (1.0 - beta1_power)
+        if self.graphs is not None:
+            # the captured launch reads {lr_t, gscale} from device memory
+            self.adam_scalars[0].fill_(lr_t)
+            self.adam_scalars[1].fill_(grad_scale)
+            sc = _ptr(self.adam_scalars)
+            self._replay(("adam", beta1, beta2, eps), lambda s: self.C.adam_pack(
+                _ptr(f.master), _ptr(f.grad), _ptr(f.m), _ptr(f.v), f.numel, _ptr(self.segs), self.nseg,
+                lr_t, beta1, beta2, eps, grad_scale, 1, _ptr(self.arena), s, sc))
+            return
         self.C.adam_pack(_ptr(f.master), _ptr(f.grad), _ptr(f.m), _ptr(f.v), f.numel,
                          _ptr(self.segs), self.nseg, lr_t, beta1, beta2, eps, grad_scale, 1,
                          _ptr(self.arena), native.stream_handle(stream))
@@ -671,15 +682,53 @@ class NativeUNet:
         self.x_f32.view(-1).copy_(x.reshape(-1), non_blocking=True)
         self.target.copy_(y.reshape(-1), non_blocking=True)
 
+    # ------------------------------------------------------------------ HIP graphs
+    def enable_graphs(self):
+        """Replay the forward, every backward segment and the Adam launch as captured
+        HIP graphs (one graph launch instead of ~150 kernel launches per step).
+
+        Values that change per step live in device memory so the frozen kernel
+        arguments stay valid: the dropout seed (``Plan.set_seed_ptr``) and Adam's
+        {lr_t, grad scale}.  Segments are captured separately so the bucketed
+        allreduces still start eagerly between segment replays (overlap unchanged).
+        Graphs are captured lazily on first use and dropped when buckets change."""
+        if self.device.type != "cuda":
+            raise RuntimeError("HIP graphs need a GPU")
+        self.seed_dev = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.adam_scalars = torch.zeros(2, dtype=torch.float32, device=self.device)
+        self.plan.set_seed_ptr(_ptr(self.seed_dev))
+        self.graphs = {}
+
+    def _replay(self, key, launch):
+        g = self.graphs.get(key)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                launch(native.stream_handle(None))
+            self.graphs[key] = g
+        g.replay()
+
     def forward(self, seed: int, stream=None):
-        self.plan.set_seed(seed & 0xFFFFFFFF)
+        seed &= 0xFFFFFFFF
+        self.plan.set_seed(seed)
+        if self.graphs is not None:
+            self.seed_dev.fill_(seed - (1 << 32) if seed >= (1 << 31) else seed)
+            with torch.cuda.stream(stream) if stream is not None else _nullctx():
+                self._replay(("fwd", self.fwd_end), lambda s: self.plan.run(0, self.fwd_end, s))
+            return
         self.plan.run(0, self.fwd_end, native.stream_handle(stream))
 
     def backward(self, on_segment=None, stream=None):
         s = native.stream_handle(stream)
         begin = self.fwd_end
         for i, end in enumerate(self.seg_ends):
-            self.plan.run(begin, end, s)
+            if end == begin:
+                pass                    # bucket finished by the previous segment already
+            elif self.graphs is not None:
+                with torch.cuda.stream(stream) if stream is not None else _nullctx():
+                    self._replay(("bwd", begin, end), lambda hs, b=begin, e=end: self.plan.run(b, e, hs))
+            else:
+                self.plan.run(begin, end, s)
             begin = end
             if on_segment is not None:
                 on_segment(i)
