@@ -59,6 +59,7 @@ def main():
     from unet_distributed_amd.runtime.optim import TFAdam
     from unet_distributed_amd.runtime.params import FlatParams
     from unet_distributed_amd.runtime.trainer import _NativeOpt
+    from unet_distributed_amd.runtime.amp import LossScaler
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     ctx = D.init("auto", "auto", 600.0)
@@ -90,10 +91,14 @@ def main():
         xs.append(torch.from_numpy(x).to(dev))
         ys.append(torch.from_numpy(y).to(dev))
 
+    scaler = LossScaler(cfg.dtype, cfg.loss_scale)
+
     def step(i):
-        backend.fwd_bwd(xs[i % 2], ys[i % 2], seed=12345 + i, on_segment=sync.on_segment)
+        scale = scaler.scale
+        backend.fwd_bwd(xs[i % 2], ys[i % 2], seed=12345 + i, on_segment=sync.on_segment, grad_scale=scale)
         sync.finish()
-        opt.step()
+        if scaler.update(flat.grad):            # fp16: finiteness check + dynamic scale (no-op in bf16)
+            opt.step(grad_scale=1.0 / scale)
 
     for i in range(a.warmup):
         step(i)

@@ -24,8 +24,11 @@ def run(kind, dtype):
     torch.cuda.synchronize()
     return f
 f32, fb, fn = run("torch", "fp32"), run("torch", "bf16"), run("native", "bf16")
+fh = run("native", "fp16")
 cos = lambda a, b: (a.double() @ b.double() / (a.double().norm() * b.double().norm() + 1e-30)).item()
 for name, shape, off, n in f32.entries:
-    if name.endswith("kernel"):
-        g0 = f32.grad[off:off + n]
-        print("%-24s native %.4f  aten-bf16 %.4f" % (name, cos(fn.grad[off:off + n], g0), cos(fb.grad[off:off + n], g0)))
+    g0 = f32.grad[off:off + n]
+    if g0.norm() < 1e-6:
+        continue
+    print("%-28s native-bf16 %.4f  aten-bf16 %.4f  native-fp16 %.4f" % (
+        name, cos(fn.grad[off:off + n], g0), cos(fb.grad[off:off + n], g0), cos(fh.grad[off:off + n], g0)))

@@ -158,12 +158,17 @@ def test_native_norm_step_matches_bf16_noise_floor(cuda_dev, norm):
     for be in (nb, tb, bb):
         be.fwd_bwd(x, y, seed=77)
     torch.cuda.synchronize()
+    cns, cbs = [], []
     for name, shape, off, n in fn.entries:
         g32 = ft.grad[off:off + n]
         if g32.norm() < 1e-6:
             continue
         cn, cb = _cos(fn.grad[off:off + n], g32), _cos(fb.grad[off:off + n], g32)
-        assert cn > cb - 0.02, (name, cn, cb)
+        # single layers at the bottleneck scatter by ~+-0.02 around the floor
+        assert cn > cb - 0.04, (name, cn, cb)
+        cns.append(cn)
+        cbs.append(cb)
+    assert sum(cns) / len(cns) > sum(cbs) / len(cbs) - 0.005, (cns, cbs)
     assert _cos(fn.grad, ft.grad) > 0.98
 
 

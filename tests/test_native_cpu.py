@@ -17,14 +17,17 @@ def test_extension_builds_and_imports():
     assert C.crc32c(b"123456789") == 0xE3069283
 
 
-@pytest.mark.parametrize("kw,img", [(dict(in_channels=4), 64), (dict(in_channels=1, use_upsampling=True), 64),
-                                    (dict(in_channels=4, dims=3), 32), (dict(in_channels=8), 64)])
-def test_plan_construction_dry_run(kw, img):
+@pytest.mark.parametrize("kw,img,dtype", [(dict(in_channels=4), 64, "bf16"),
+                                          (dict(in_channels=1, use_upsampling=True), 64, "bf16"),
+                                          (dict(in_channels=4, dims=3), 32, "bf16"), (dict(in_channels=8), 64, "bf16"),
+                                          (dict(in_channels=4, norm="group"), 64, "fp16")])
+def test_plan_construction_dry_run(kw, img, dtype):
     from unet_distributed_amd.runtime.native_engine import NativeUNet
     spec = UNetSpec(**kw)
     flat = FlatParams(spec)
     b = plan_buckets(flat, 4.0)
-    e = NativeUNet(spec, flat, 2, img, "cpu", bucket_bounds=b, dry_run=True)
+    e = NativeUNet(spec, flat, 2, img, "cpu", bucket_bounds=b, dry_run=True, dtype=dtype)
+    assert e.arena.dtype == e.adt and e.target.dtype == e.adt
     names = e.plan.names()
     assert names[0] == "cast_input" and names[e.fwd_end - 1] == "fwd:Mask"
     assert names[e.fwd_end] == "bwd:Mask"

@@ -133,3 +133,19 @@ def test_flat_params_views_and_optimizer_state():
     flat.grad.normal_()
     opt.step()
     assert flat.global_step == 1 and abs(flat.beta1_power - 0.81) < 1e-12
+
+
+def test_loss_scaler_dynamic_skip_halve_grow():
+    from unet_distributed_amd.runtime.amp import LossScaler
+    off = LossScaler("bf16")
+    assert not off.enabled and off.scale == 1.0 and off.update(torch.tensor([float("inf")]))
+    s = LossScaler("fp16", growth_interval=3)
+    assert s.dynamic and s.scale == 2.0 ** 16
+    assert not s.update(torch.tensor([1.0, float("nan")]))
+    assert s.scale == 2.0 ** 15 and s.skipped == 1
+    for _ in range(3):
+        assert s.update(torch.ones(4))
+    assert s.scale == 2.0 ** 16
+    st = LossScaler("fp16", loss_scale=128.0)
+    assert not st.dynamic and st.scale == 128.0
+    assert not st.update(torch.tensor([float("inf")])) and st.scale == 128.0

@@ -27,7 +27,7 @@ __global__ void __launch_bounds__(256) adam_pack_kernel(float* __restrict__ w, c
                                                         const PackSeg* __restrict__ segs, int nseg, float lr_t,
                                                         float b1, float b2, float eps, float gscale, int do_adam,
                                                         const float* __restrict__ dev_scalars,
-                                                        bf16* __restrict__ arena) {
+                                                        h16* __restrict__ arena) {
   // HIP-graph replay: the per-step lr_t / gradient scale come from device memory
   if (dev_scalars) {
     lr_t = dev_scalars[0];
@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(256) adam_pack_kernel(float* __restrict__ w, c
     const PackSeg& sg = S[lo];
     const int e = i - sg.off;
     if (sg.kind == 0 || e >= sg.n) continue;
-    const bf16 wb = (bf16)wi;
+    const h16 wb = (h16)wi;
     if (sg.kind == 1) {
       const int co = e % sg.Co;
       const int r = e / sg.Co;
@@ -88,7 +88,7 @@ hipError_t adam_pack_launch(float* w, const float* g, float* m, float* v, int n_
   int grid = (n_total + 255) / 256;
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL(adam_pack_kernel, dim3(grid), dim3(256), 0, s, w, g, m, v, n_total, (const PackSeg*)segs, nseg,
-                     lr_t, b1, b2, eps, gscale, do_adam, dev_scalars, (bf16*)arena);
+                     lr_t, b1, b2, eps, gscale, do_adam, dev_scalars, (h16*)arena);
   return hipGetLastError();
 }
 

@@ -7,48 +7,73 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// 16-bit activation / weight-copy element type.  Every kernel TU is compiled twice
+// (native/build.py): as bf16 in namespace `unet` and, with -DUNET_FP16
+// -Dunet=unet_f16, as IEEE fp16 in namespace `unet_f16`.  The two builds share the
+// kernel source; only the element type, its conversions and the MFMA opcode
+// (v_mfma_f32_16x16x32_{bf16,f16}, identical operand layouts) differ.
 namespace unet {
 
-typedef __bf16 bf16;
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#ifdef UNET_FP16
+typedef _Float16 h16;
+#else
+typedef __bf16 h16;
+#endif
+typedef h16 h16x8 __attribute__((ext_vector_type(8)));
+typedef h16 h16x4 __attribute__((ext_vector_type(4)));
+typedef h16 h16x2 __attribute__((ext_vector_type(2)));
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
+#ifdef UNET_FP16
+constexpr uint32_t kOnes2 = 0x3C003C00u;   // two fp16 1.0
+#else
+constexpr uint32_t kOnes2 = 0x3F803F80u;   // two bf16 1.0
+#endif
+
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
-__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
-__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+__device__ __forceinline__ float h2f(h16 x) { return (float)x; }
+__device__ __forceinline__ h16 f2h(float x) { return (h16)x; }
 
 __device__ __forceinline__ float bits2f(uint16_t b) {
+#ifdef UNET_FP16
+  return (float)__builtin_bit_cast(_Float16, b);
+#else
   return __uint_as_float(((uint32_t)b) << 16);
+#endif
 }
 
-// unpack 8 bf16 held in a 16-byte vector into floats
+// unpack 8 16-bit elements held in a 16-byte vector into floats
 __device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
+#ifdef UNET_FP16
+  const f32x8 r = __builtin_convertvector(__builtin_bit_cast(h16x8, v), f32x8);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = r[i];
+#else
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     f[2 * i] = __uint_as_float(v[i] << 16);
     f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
   }
+#endif
 }
 
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// one v_cvt_pk_bf16_f32 (round-to-nearest-even) for two values
-__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+// one packed convert (round-to-nearest-even) for two values
+__device__ __forceinline__ uint32_t pack2h(float a, float b) {
   const f32x2 v = {a, b};
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, h16x2));
 }
 
 __device__ __forceinline__ u32x4 pack8(const float* f) {
   u32x4 r;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) r[i] = pack2bf(f[2 * i], f[2 * i + 1]);
+  for (int i = 0; i < 4; ++i) r[i] = pack2h(f[2 * i], f[2 * i + 1]);
   return r;
 }
 
@@ -66,8 +91,12 @@ __device__ __forceinline__ uint32_t drop_hash(uint64_t idx, uint32_t seed, uint3
   return x;
 }
 
-__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+__device__ __forceinline__ f32x4 mfma16(const h16x8& a, const h16x8& b, const f32x4& c) {
+#ifdef UNET_FP16
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+#else
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+#endif
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

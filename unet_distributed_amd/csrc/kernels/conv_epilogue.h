@@ -89,14 +89,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       if (kStats && q < M) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float xr = (float)(bf16)v[r];
+          const float xr = (float)(h16)v[r];
           s1[r] += xr;
           s2[r] += xr * xr;
         }
       }
       u32x2 pk;
-      pk[0] = pack2bf(v[0], v[1]);
-      pk[1] = pack2bf(v[2], v[3]);
+      pk[0] = pack2h(v[0], v[1]);
+      pk[1] = pack2h(v[2], v[3]);
       *(u32x2*)(E + ml * EPI_STRIDE + nl * 2) = pk;
     }
     if (kStats) {
@@ -129,8 +129,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     const bool side1 = n < p.D1;
     const int rs = side1 ? p.D1 : p.Cout - p.D1;
     const int co = side1 ? n : n - p.D1;
-    bf16* dst = (bf16*)(side1 ? p.dst1 : p.dst2);
-    const bf16* mk = (const bf16*)(side1 ? p.mask1 : p.mask2);
+    h16* dst = (h16*)(side1 ? p.dst1 : p.dst2);
+    const h16* mk = (const h16*)(side1 ? p.mask1 : p.mask2);
     u32x4 mv[NIT];
     if (mk) {
 #pragma unroll
@@ -172,11 +172,11 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
     u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
     size_t off;
-    bf16* dst;
+    h16* dst;
     const void* mk;
     if (EPI == EPI_FWD) {
       off = (size_t)q * p.Cout + n;
-      dst = (bf16*)p.dst1;
+      dst = (h16*)p.dst1;
       mk = nullptr;
     } else if (kShuffle) {
       const int tap = n / Dt, co = n - tap * Dt;
@@ -194,19 +194,19 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       const size_t pix = (((size_t)pc.n * (p.OD * dd) + pc.d * dd + td) * (2 * p.OH) + 2 * pc.h + th) *
                              (2 * p.OW) + 2 * pc.w + tw;
       off = pix * Dt + co;
-      dst = (bf16*)p.dst1;
+      dst = (h16*)p.dst1;
       mk = p.mask1;
     } else if (n < p.D1) {
       off = (size_t)q * p.D1 + n;
-      dst = (bf16*)p.dst1;
+      dst = (h16*)p.dst1;
       mk = p.mask1;
     } else {
       off = (size_t)q * (p.Cout - p.D1) + (n - p.D1);
-      dst = (bf16*)p.dst2;
+      dst = (h16*)p.dst2;
       mk = p.mask2;
     }
     if (EPI != EPI_FWD && mk) {
-      const u32x4 mv = *(const u32x4*)((const bf16*)mk + off);
+      const u32x4 mv = *(const u32x4*)((const h16*)mk + off);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         // bf16 > 0 <=> sign bit clear and not zero (-0 counts as not positive)

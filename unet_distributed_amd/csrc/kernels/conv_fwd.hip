@@ -251,11 +251,11 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int fo = h ? frag1 : frag0;
-      bf16x8 xf[TM], wf[TN];
+      h16x8 xf[TM], wf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) xf[i] = *(const bf16x8*)(As + (wm * WM + i * 16) * 128 + fo);
+      for (int i = 0; i < TM; ++i) xf[i] = *(const h16x8*)(As + (wm * WM + i * 16) * 128 + fo);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) wf[j] = *(const bf16x8*)(Bs + (wn * WN + j * 16) * 128 + fo);
+      for (int j = 0; j < TN; ++j) wf[j] = *(const h16x8*)(Bs + (wn * WN + j * 16) * 128 + fo);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -417,15 +417,15 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int dh = t / 3, dw = t % 3;
-      bf16x8 wf[TN];
+      h16x8 wf[TN];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) wf[j] = *(const bf16x8*)(Ws + (t * BN + 16 * j) * 64 + wbase);
+      for (int j = 0; j < TN; ++j) wf[j] = *(const h16x8*)(Ws + (t * BN + 16 * j) * 64 + wbase);
       const uint32_t okm = (dh == 0 ? top_ok : (dh == 2 ? bot_ok : 0xffffffffu)) & live;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         if ((okm >> i) & 1u) {
-          const bf16x8 xf =
-              *(const bf16x8*)(Xs + xbase[dw] + ((i / TPR) + dh) * ROWB + (i % TPR) * 16 * 64);
+          const h16x8 xf =
+              *(const h16x8*)(Xs + xbase[dw] + ((i / TPR) + dh) * ROWB + (i % TPR) * 16 * 64);
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[j], xf, acc[i][j]);
         }
@@ -497,14 +497,14 @@ __global__ void __launch_bounds__(NTHR) conv_win_first_kernel(const ConvFwdParam
   }
   // weight fragments (B operand: k = 32 s + 8 (lane >> 4) .. + 7, n = lane & 15), from global
   const int fsub = lane >> 4, fr = lane & 15;
-  bf16x8 wf[KS][TN];
+  h16x8 wf[KS][TN];
 #pragma unroll
   for (int s = 0; s < KS; ++s)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
           rsw, ((n0 + 16 * j + fr) * p.Kpad + 32 * s + 8 * fsub) * 2, 0, 0);
-      wf[s][j] = __builtin_bit_cast(bf16x8, v);
+      wf[s][j] = __builtin_bit_cast(h16x8, v);
     }
 
   const int rw0 = (128 * wave) / W;
@@ -551,7 +551,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_first_kernel(const ConvFwdParam
         const int slot = (rr + dh) * RS + cw + dw + 1;
         v = *(const u32x4*)(Xs + (ok ? slot * SB : 0));
       }
-      const bf16x8 xf = __builtin_bit_cast(bf16x8, v);
+      const h16x8 xf = __builtin_bit_cast(h16x8, v);
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[s][j], xf, acc[i][j]);
     }
@@ -659,12 +659,12 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
       }
     }
     __syncthreads();
-    bf16x8 wf[TN];
+    h16x8 wf[TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) wf[j] = *(const bf16x8*)(Ws + (wave * 32 + 16 * j) * 64 + fbase);
+    for (int j = 0; j < TN; ++j) wf[j] = *(const h16x8*)(Ws + (wave * 32 + 16 * j) * 64 + fbase);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const bf16x8 xf = *(const bf16x8*)(Xs + (16 * i) * 64 + fbase);
+      const h16x8 xf = *(const h16x8*)(Xs + (16 * i) * 64 + fbase);
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[j], xf, acc[i][j]);
     }
@@ -685,8 +685,8 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
       const int rr = pl / W, w = pl - rr * W;
       const int fp = (2 * rr + th) * (2 * W) + 2 * w + tw;
       u32x2 pk;
-      pk[0] = pack2bf(acc[i][j][0] + bs[0], acc[i][j][1] + bs[1]);
-      pk[1] = pack2bf(acc[i][j][2] + bs[2], acc[i][j][3] + bs[3]);
+      pk[0] = pack2h(acc[i][j][0] + bs[0], acc[i][j][1] + bs[1]);
+      pk[1] = pack2h(acc[i][j][2] + bs[2], acc[i][j][3] + bs[3]);
       *(u32x2*)(E + fp * FST + nl * 2) = pk;
     }
   }
@@ -703,7 +703,7 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
     const u32x2 lo = *(const u32x2*)(E + fp * FST + q * 16);
     const u32x2 hi = *(const u32x2*)(E + fp * FST + q * 16 + 8);
     const u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
-    *(u32x4*)((bf16*)p.dst1 + gp * cof + n0 + q * 8) = v;
+    *(u32x4*)((h16*)p.dst1 + gp * cof + n0 + q * 8) = v;
   }
 }
 
@@ -776,15 +776,15 @@ __global__ void __launch_bounds__(NTHR) tconv_dgrad_kernel(const ConvFwdParams p
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int th = t >> 1, tw = t & 1;
-      bf16x8 wf[TN];
+      h16x8 wf[TN];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) wf[j] = *(const bf16x8*)(Ws + (t * BN + 16 * j) * 64 + wbase);
+      for (int j = 0; j < TN; ++j) wf[j] = *(const h16x8*)(Ws + (t * BN + 16 * j) * 64 + wbase);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int pl = wave * (BMc / 4) + 16 * i + fr;     // this lane's coarse pixel
         const int rr = pl / W, w = pl - rr * W;
         const int slot = (2 * rr + th) * FW + tw * W + w;
-        const bf16x8 xf = *(const bf16x8*)(Ys + slot * 64 + 16 * (fsub ^ ((slot >> 1) & 3)));
+        const h16x8 xf = *(const h16x8*)(Ys + slot * 64 + 16 * (fsub ^ ((slot >> 1) & 3)));
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[j], xf, acc[i][j]);
       }

@@ -2,7 +2,10 @@
 #pragma once
 #include <stdint.h>
 
-namespace unet {
+// Shared by the bf16 (`unet`) and fp16 (`unet_f16`) builds of the kernels (see
+// common.h): the parameter blocks live outside the element-type namespaces so both
+// builds' launchers take the same host types.
+namespace unet_types {
 
 // Implicit-GEMM "NT" convolution: out[q][n] = epilogue(sum_{tap,c} X[q*s + tap - pad][c] * W[n][tap][c])
 // GEMM M = output pixels q over [N][OD][OH][OW], GEMM N = Cout, K = taps * Cin.
@@ -99,4 +102,8 @@ struct PackSeg {
   long long dg_off;    // dgrad copy, -1 = none
 };
 
+}  // namespace unet_types
+
+namespace unet {
+using namespace unet_types;
 }  // namespace unet

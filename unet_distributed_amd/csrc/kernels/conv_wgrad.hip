@@ -49,7 +49,7 @@ __device__ __forceinline__ int tr_off(int k, int c) {
 }
 
 template <int W>
-__device__ __forceinline__ bf16x8 tr_frag(const char* img, int lane, int cbase) {
+__device__ __forceinline__ h16x8 tr_frag(const char* img, int lane, int cbase) {
   // lane (g = lane>>4, i = lane&15, q = i>>2, p = i&3) supplies row 8g + 4h + q, cols cbase + 4p
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
   const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -60,7 +60,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* img, int lane, int cbase) 
   // first dword of each 64-bit transposed read survived in ROCm 7.2 hipcc)
   const u32x2 a = __builtin_bit_cast(u32x2, lo), b = __builtin_bit_cast(u32x2, hi);
   const u32x4 v = {a[0], a[1], b[0], b[1]};
-  return __builtin_bit_cast(bf16x8, v);
+  return __builtin_bit_cast(h16x8, v);
 }
 
 // BK = 64 pixels per K step; 4 threads per pixel row (tid >> 2 = row, tid & 3 = sub).
@@ -241,12 +241,12 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
   f32x4 bacc[NF];
 #pragma unroll
   for (int j = 0; j < NF; ++j) bacc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const u32x4 ones_u = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+  const u32x4 ones_u = {kOnes2, kOnes2, kOnes2, kOnes2};
   // wave-uniform scalar branches (readfirstlane) so the compiler does not predicate
   // the extra MFMAs with exec masks
   const bool do_b1 = BIAS && __builtin_amdgcn_readfirstlane((int)(bias_on && p.bias_mode == 1 && wm == 0));
   const bool do_b2 = BIAS && __builtin_amdgcn_readfirstlane((int)(bias_on && p.bias_mode == 2 && wn == 0));
-  const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_u);
+  const h16x8 ones = __builtin_bit_cast(h16x8, ones_u);
 
   if (nks > 0) {
     load(0);
@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
     const char* S = smem + buf * STAGE;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {      // two k32 halves of the 64-pixel step
-      bf16x8 bfr[TN];
+      h16x8 bfr[TN];
 #pragma unroll
       for (int j = 0; j < TN; ++j) bfr[j] = tr_frag<BN>(S + NTAP * A_IMG + h * 32 * BN * 2, lane, wn * WN + j * 16);
       if constexpr (BIAS) {
@@ -272,7 +272,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
       for (int a = 0; a < NTAP; ++a) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-          const bf16x8 af = tr_frag<BM>(S + a * A_IMG + h * 32 * BM * 2, lane, wm * WM + i * 16);
+          const h16x8 af = tr_frag<BM>(S + a * A_IMG + h * 32 * BM * 2, lane, wm * WM + i * 16);
           if constexpr (BIAS) {
             if (do_b2) bacc[i] = mfma16(ones, af, bacc[i]);
           }
@@ -418,7 +418,7 @@ __global__ void __launch_bounds__(256) multi_reduce2_kernel(const ReduceJob* __r
 }
 
 // partial[b][c] = sum over rows r of block b of x[r][c]   (bf16 [rows][C], C % 8 == 0, C <= 1024)
-__global__ void __launch_bounds__(256) colsum_kernel(const bf16* __restrict__ x, int rows, int C, int rows_per_block,
+__global__ void __launch_bounds__(256) colsum_kernel(const h16* __restrict__ x, int rows, int C, int rows_per_block,
                                                      float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float red[];
   const int cpr = C / 8;                        // chunks per row
@@ -543,8 +543,8 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   f32x4 bacc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
-  const u32x4 ones_u = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
-  const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_u);
+  const u32x4 ones_u = {kOnes2, kOnes2, kOnes2, kOnes2};
+  const h16x8 ones = __builtin_bit_cast(h16x8, ones_u);
 
   // LDS-DMA lane roles (slot 16k + lslot, physical chunk lane & 3)
   const int lslot = lane >> 2;
@@ -558,12 +558,12 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   auto tr_addr = [&](int slot, int col, int ch) -> int {   // ch: channel within the 32-ch slot
     return slot * 64 + ((((ch >> 3) ^ (((col >> 3) & 1) << 1))) << 4) + ((ch & 7) << 1);
   };
-  auto tr8 = [&](const char* base0, const char* base1) -> bf16x8 {
+  auto tr8 = [&](const char* base0, const char* base1) -> h16x8 {
     const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base0));
     const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base1));
     const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
     const u32x4 v = {l2[0], l2[1], h2[0], h2[1]};
-    return __builtin_bit_cast(bf16x8, v);
+    return __builtin_bit_cast(h16x8, v);
   };
 
   for (int win = w_begin; win < w_end; ++win) {
@@ -603,7 +603,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
       if (g >= rows_total) break;
       const int h = g % H;
       // dY fragments (B operand: k = pixels, n = output channels)
-      bf16x8 bf[2];
+      h16x8 bf[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int s0 = px0 + 8 * G + q, s1 = s0 + 4;
@@ -627,9 +627,9 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
         const int slotA = (rr + lr + dh) * HWP + colA;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          bf16x8 af = tr8(Xs + tr_addr(slotA, colA, 16 * i + 4 * pp),
+          h16x8 af = tr8(Xs + tr_addr(slotA, colA, 16 * i + 4 * pp),
                           Xs + tr_addr(slotA + 4, colA + 4, 16 * i + 4 * pp));
-          if (W < 32 && !lane_ok) af = __builtin_bit_cast(bf16x8, (u32x4){0u, 0u, 0u, 0u});
+          if (W < 32 && !lane_ok) af = __builtin_bit_cast(h16x8, (u32x4){0u, 0u, 0u, 0u});
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[t][i][j] = mfma16(af, bf[j], acc[t][i][j]);
         }
@@ -724,8 +724,8 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i][0] = acc[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
   f32x4 bacc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
-  const u32x4 ones_u = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
-  const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_u);
+  const u32x4 ones_u = {kOnes2, kOnes2, kOnes2, kOnes2};
+  const h16x8 ones = __builtin_bit_cast(h16x8, ones_u);
   const int lslot = lane >> 2;
   const int lchunk = (lane & 3) ^ (((lslot >> 3) & 1) << 1);
   const int yl = (lslot * p.Nc + co0 + lchunk * 8) * 2;
@@ -734,12 +734,12 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
   auto tr_addr = [&](int slot, int col, int ch) -> int {
     return slot * 64 + ((((ch >> 3) ^ (((col >> 3) & 1) << 1))) << 4) + ((ch & 7) << 1);
   };
-  auto tr8 = [&](const char* base0, const char* base1) -> bf16x8 {
+  auto tr8 = [&](const char* base0, const char* base1) -> h16x8 {
     const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base0));
     const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base1));
     const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
     const u32x4 v = {l2[0], l2[1], h2[0], h2[1]};
-    return __builtin_bit_cast(bf16x8, v);
+    return __builtin_bit_cast(h16x8, v);
   };
 
   for (int win = w_begin; win < w_end; ++win) {
@@ -774,7 +774,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
     for (int kk = wave; kk < KS; kk += 4) {
       const int px0 = kk * 32;
       if (g0 + px0 / W >= rows_total) break;
-      bf16x8 bf[2];
+      h16x8 bf[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int s0 = px0 + 8 * G + q, s1 = s0 + 4;
@@ -804,7 +804,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
           const bool ok = t < 9 && !(dh == 0 && hlp[hh] == 0) && !(dh == 2 && hlp[hh] == H - 1);
           a[hh] = ok ? (slotp[hh] + dh * RS + dw) * SB + chb : 0;
         }
-        const bf16x8 af = tr8(Xs + a[0], Xs + a[1]);
+        const h16x8 af = tr8(Xs + a[0], Xs + a[1]);
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[mt][j] = mfma16(af, bf[j], acc[mt][j]);
       }
@@ -906,20 +906,20 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
 #pragma unroll
     for (int i = 0; i < 2; ++i) acc[t][i][0] = acc[t][i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
   f32x4 bacc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
-  const u32x4 ones_u = {0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
-  const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_u);
+  const u32x4 ones_u = {kOnes2, kOnes2, kOnes2, kOnes2};
+  const h16x8 ones = __builtin_bit_cast(h16x8, ones_u);
   const int lslot = lane >> 2;
   const int lchunk = (lane & 3) ^ (((lslot >> 3) & 1) << 1);
   const int G = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
   auto tr_addr = [&](int slot, int ch) -> int {   // swizzle keyed on slot mod 16
     return slot * 64 + ((((ch >> 3) ^ (((slot >> 3) & 1) << 1))) << 4) + ((ch & 7) << 1);
   };
-  auto tr8 = [&](const char* base0, const char* base1) -> bf16x8 {
+  auto tr8 = [&](const char* base0, const char* base1) -> h16x8 {
     const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base0));
     const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base1));
     const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
     const u32x4 v = {l2[0], l2[1], h2[0], h2[1]};
-    return __builtin_bit_cast(bf16x8, v);
+    return __builtin_bit_cast(h16x8, v);
   };
   const char* Xq = Xs + qn * (BMc * 64);
 
@@ -956,7 +956,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
       const int px0 = kk * 32;
       const int rr = px0 / W, c0 = px0 - rr * W;
       if (g0 + rr >= rows_total) break;
-      bf16x8 bf[2];
+      h16x8 bf[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int s0 = px0 + 8 * G + q;
@@ -968,7 +968,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
         const int s0 = (2 * rr + th) * FW + tw * W + c0 + 8 * G + q;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const bf16x8 af = tr8(Ys + tr_addr(s0, 16 * i + 4 * pp), Ys + tr_addr(s0 + 4, 16 * i + 4 * pp));
+          const h16x8 af = tr8(Ys + tr_addr(s0, 16 * i + 4 * pp), Ys + tr_addr(s0 + 4, 16 * i + 4 * pp));
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[t][i][j] = mfma16(af, bf[j], acc[t][i][j]);
           if (do_bias) bacc[i] = mfma16(af, ones, bacc[i]);
@@ -1159,7 +1159,7 @@ hipError_t multi_reduce_launch(const void* jobs, int njobs, long long total1, lo
 
 hipError_t colsum_launch(const void* x, int rows, int C, int blocks, float* partial, hipStream_t s) {
   const int rpb = (rows + blocks - 1) / blocks;
-  hipLaunchKernelGGL(colsum_kernel, dim3(blocks), dim3(256), 256 * 8 * sizeof(float), s, (const bf16*)x, rows, C,
+  hipLaunchKernelGGL(colsum_kernel, dim3(blocks), dim3(256), 256 * 8 * sizeof(float), s, (const h16*)x, rows, C,
                      rpb, partial);
   return hipGetLastError();
 }

@@ -20,17 +20,17 @@ __device__ __forceinline__ uint32_t bf_pos_mask(uint32_t w) {
 }
 
 __global__ void __launch_bounds__(256) cast_input_kernel(const float* __restrict__ x, int P, int Cin, int Cpad,
-                                                         bf16* __restrict__ y) {
+                                                         h16* __restrict__ y) {
   const int total = P * Cpad;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int p = i / Cpad, c = i - p * Cpad;
-    y[i] = (bf16)(c < Cin ? x[(size_t)p * Cin + c] : 0.f);
+    y[i] = (h16)(c < Cin ? x[(size_t)p * Cin + c] : 0.f);
   }
 }
 
 // one thread = one pooled pixel x 8 channels
-__global__ void __launch_bounds__(256) maxpool2_fwd_kernel(const bf16* __restrict__ x, int N, int D, int H, int W,
-                                                           int C, int dims3, bf16* __restrict__ y) {
+__global__ void __launch_bounds__(256) maxpool2_fwd_kernel(const h16* __restrict__ x, int N, int D, int H, int W,
+                                                           int C, int dims3, h16* __restrict__ y) {
   const int OD = dims3 ? D / 2 : 1, OH = H / 2, OW = W / 2;
   const int cpp = C / 8;
   const long long total = (long long)N * OD * OH * OW * cpp;
@@ -66,9 +66,9 @@ __global__ void __launch_bounds__(256) maxpool2_fwd_kernel(const bf16* __restric
 }
 
 // dx[window] = (first argmax ? dy : 0) + skip_grad (optional)
-__global__ void __launch_bounds__(256) maxpool2_bwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
-                                                           const bf16* __restrict__ skip, int N, int D, int H, int W,
-                                                           int C, int dims3, bf16* __restrict__ dx) {
+__global__ void __launch_bounds__(256) maxpool2_bwd_kernel(const h16* __restrict__ x, const h16* __restrict__ dy,
+                                                           const h16* __restrict__ skip, int N, int D, int H, int W,
+                                                           int C, int dims3, h16* __restrict__ dx) {
   const int OD = dims3 ? D / 2 : 1, OH = H / 2, OW = W / 2;
   const int cpp = C / 8;
   const long long total = (long long)N * OD * OH * OW * cpp;
@@ -128,9 +128,9 @@ __global__ void __launch_bounds__(256) maxpool2_bwd_kernel(const bf16* __restric
 }
 
 // dlow[p] = sum_{2x2(x2) children} dup[child] * (mask[p] > 0)
-__global__ void __launch_bounds__(256) upsample2_bwd_kernel(const bf16* __restrict__ dup, const bf16* __restrict__ mask,
+__global__ void __launch_bounds__(256) upsample2_bwd_kernel(const h16* __restrict__ dup, const h16* __restrict__ mask,
                                                             int N, int D, int H, int W, int C, int dims3,
-                                                            bf16* __restrict__ dlow) {
+                                                            h16* __restrict__ dlow) {
   // D, H, W: LOW resolution dims
   const int cpp = C / 8;
   const int FD = dims3 ? 2 : 1;
@@ -176,30 +176,30 @@ inline int grid_for(long long work, int per_block = 256) {
 
 hipError_t cast_input_launch(const float* x, int P, int Cin, int Cpad, void* y, hipStream_t s) {
   hipLaunchKernelGGL(cast_input_kernel, dim3(grid_for((long long)P * Cpad)), dim3(256), 0, s, x, P, Cin, Cpad,
-                     (bf16*)y);
+                     (h16*)y);
   return hipGetLastError();
 }
 
 hipError_t maxpool2_fwd_launch(const void* x, int N, int D, int H, int W, int C, int dims3, void* y, hipStream_t s) {
   const long long work = (long long)N * (dims3 ? D / 2 : 1) * (H / 2) * (W / 2) * (C / 8);
-  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const bf16*)x, N, D, H, W, C,
-                     dims3, (bf16*)y);
+  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, N, D, H, W, C,
+                     dims3, (h16*)y);
   return hipGetLastError();
 }
 
 hipError_t maxpool2_bwd_launch(const void* x, const void* dy, const void* skip, int N, int D, int H, int W, int C,
                                int dims3, void* dx, hipStream_t s) {
   const long long work = (long long)N * (dims3 ? D / 2 : 1) * (H / 2) * (W / 2) * (C / 8);
-  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const bf16*)x, (const bf16*)dy,
-                     (const bf16*)skip, N, D, H, W, C, dims3, (bf16*)dx);
+  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, (const h16*)dy,
+                     (const h16*)skip, N, D, H, W, C, dims3, (h16*)dx);
   return hipGetLastError();
 }
 
 hipError_t upsample2_bwd_launch(const void* dup, const void* mask, int N, int D, int H, int W, int C, int dims3,
                                 void* dlow, hipStream_t s) {
   const long long work = (long long)N * D * H * W * (C / 8);
-  hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const bf16*)dup,
-                     (const bf16*)mask, N, D, H, W, C, dims3, (bf16*)dlow);
+  hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)dup,
+                     (const h16*)mask, N, D, H, W, C, dims3, (h16*)dlow);
   return hipGetLastError();
 }
 

@@ -21,8 +21,8 @@ constexpr int HT = 256;
 // Forward: one thread per pixel (the sigmoid / BCE transcendentals then run once per
 // pixel on full waves; a lane-per-chunk mapping measured 2x slower here).
 template <int C>
-__global__ void __launch_bounds__(HT) head_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
-                                                      const float* __restrict__ b, const bf16* __restrict__ t,
+__global__ void __launch_bounds__(HT) head_fwd_kernel(const h16* __restrict__ x, const float* __restrict__ w,
+                                                      const float* __restrict__ b, const h16* __restrict__ t,
                                                       int P, float* __restrict__ prob, float* __restrict__ partial) {
   __shared__ float red[4][HT / 64];
   float wr[C];
@@ -87,12 +87,13 @@ __global__ void __launch_bounds__(256) partial_reduce_kernel(const float* __rest
 }
 
 template <int C>
-__global__ void __launch_bounds__(HT) head_bwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
-                                                      const float* __restrict__ prob, const bf16* __restrict__ t,
+__global__ void __launch_bounds__(HT) head_bwd_kernel(const h16* __restrict__ x, const float* __restrict__ w,
+                                                      const float* __restrict__ prob, const h16* __restrict__ t,
                                                       const float* __restrict__ sums, int P, float inv_total,
-                                                      float bce_w, float gscale, bf16* __restrict__ dx,
-                                                      float* __restrict__ partial) {
+                                                      float bce_w, float gscale, const float* __restrict__ gscale_ptr,
+                                                      h16* __restrict__ dx, float* __restrict__ partial) {
   constexpr int CP = C / 8;
+  if (gscale_ptr) gscale = *gscale_ptr;      // loss scale kept on the device (fp16 dynamic scaling)
   __shared__ float red[HT / 64][C + 1];
   const int cc = threadIdx.x % CP;
   float wr[8];
@@ -181,15 +182,15 @@ hipError_t head_fwd_launch(const void* x, const float* w, const float* b, const 
   const int nb = head_blocks(P);
   switch (C) {
     case 16:
-      hipLaunchKernelGGL(head_fwd_kernel<16>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, b, (const bf16*)t, P,
+      hipLaunchKernelGGL(head_fwd_kernel<16>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, b, (const h16*)t, P,
                          prob, partial);
       break;
     case 32:
-      hipLaunchKernelGGL(head_fwd_kernel<32>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, b, (const bf16*)t, P,
+      hipLaunchKernelGGL(head_fwd_kernel<32>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, b, (const h16*)t, P,
                          prob, partial);
       break;
     default:
-      hipLaunchKernelGGL(head_fwd_kernel<64>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, b, (const bf16*)t, P,
+      hipLaunchKernelGGL(head_fwd_kernel<64>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, b, (const h16*)t, P,
                          prob, partial);
   }
   hipLaunchKernelGGL(partial_reduce_kernel, dim3(4), dim3(256), 0, s, partial, nb, 4, sums);
@@ -197,21 +198,21 @@ hipError_t head_fwd_launch(const void* x, const float* w, const float* b, const 
 }
 
 hipError_t head_bwd_launch(const void* x, const float* w, const float* prob, const void* t, const float* sums, int P,
-                           int C, float inv_total, float bce_w, float gscale, void* dx, float* partial, float* gw,
-                           float* gb, hipStream_t s) {
+                           int C, float inv_total, float bce_w, float gscale, const float* gscale_ptr, void* dx,
+                           float* partial, float* gw, float* gb, hipStream_t s) {
   const int nb = head_blocks(P);
   switch (C) {
     case 16:
-      hipLaunchKernelGGL(head_bwd_kernel<16>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, prob, (const bf16*)t,
-                         sums, P, inv_total, bce_w, gscale, (bf16*)dx, partial);
+      hipLaunchKernelGGL(head_bwd_kernel<16>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, prob, (const h16*)t,
+                         sums, P, inv_total, bce_w, gscale, gscale_ptr, (h16*)dx, partial);
       break;
     case 32:
-      hipLaunchKernelGGL(head_bwd_kernel<32>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, prob, (const bf16*)t,
-                         sums, P, inv_total, bce_w, gscale, (bf16*)dx, partial);
+      hipLaunchKernelGGL(head_bwd_kernel<32>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, prob, (const h16*)t,
+                         sums, P, inv_total, bce_w, gscale, gscale_ptr, (h16*)dx, partial);
       break;
     default:
-      hipLaunchKernelGGL(head_bwd_kernel<64>, dim3(nb), dim3(HT), 0, s, (const bf16*)x, w, prob, (const bf16*)t,
-                         sums, P, inv_total, bce_w, gscale, (bf16*)dx, partial);
+      hipLaunchKernelGGL(head_bwd_kernel<64>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, prob, (const h16*)t,
+                         sums, P, inv_total, bce_w, gscale, gscale_ptr, (h16*)dx, partial);
   }
   hipLaunchKernelGGL(head_grad_reduce_kernel, dim3(C + 1), dim3(256), 0, s, partial, nb, C, gw, gb);
   return hipGetLastError();

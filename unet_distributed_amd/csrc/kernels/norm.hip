@@ -25,7 +25,7 @@ namespace {
 constexpr int NT = 256;
 
 // partial[(n * nbp + blk)][2][C]: sums over this block's pixels of sample n
-__global__ void __launch_bounds__(NT) chan_moments_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+__global__ void __launch_bounds__(NT) chan_moments_kernel(const h16* __restrict__ A, const h16* __restrict__ B,
                                                           int P, int C, int nbp, float* __restrict__ partial) {
   extern __shared__ float red[];   // [NT][2][8]
   const int n = blockIdx.x / nbp, blk = blockIdx.x - n * nbp;
@@ -186,13 +186,13 @@ __global__ void __launch_bounds__(NT) gn_param_grad_kernel(const float* __restri
 
 // y = relu(gamma (z - mean) rstd + beta) with optional inverted dropout (counter hash,
 // same stream as the conv epilogue's); coefficient arrays are [C] (cstride 0) or [N][C]
-__global__ void __launch_bounds__(NT) norm_apply_kernel(const bf16* __restrict__ z, int N, int P, int C,
+__global__ void __launch_bounds__(NT) norm_apply_kernel(const h16* __restrict__ z, int N, int P, int C,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, int cstride,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int relu, float drop_rate,
                                                         uint32_t seed0, const uint32_t* __restrict__ seed_ptr,
-                                                        uint32_t salt, bf16* __restrict__ y) {
+                                                        uint32_t salt, h16* __restrict__ y) {
   const uint32_t seed = (drop_rate > 0.f && seed_ptr) ? *seed_ptr : seed0;
   const int cpr = C / 8;
   const long long total = (long long)N * P * cpr;
@@ -222,11 +222,11 @@ __global__ void __launch_bounds__(NT) norm_apply_kernel(const bf16* __restrict__
 }
 
 // dz = a g + b z + c  (coefficients [C] or [N][C])
-__global__ void __launch_bounds__(NT) norm_bwd_apply_kernel(const bf16* __restrict__ g, const bf16* __restrict__ z,
+__global__ void __launch_bounds__(NT) norm_bwd_apply_kernel(const h16* __restrict__ g, const h16* __restrict__ z,
                                                             int N, int P, int C, const float* __restrict__ ca,
                                                             const float* __restrict__ cb,
                                                             const float* __restrict__ ccf, int cstride,
-                                                            bf16* __restrict__ dz) {
+                                                            h16* __restrict__ dz) {
   const int cpr = C / 8;
   const long long total = (long long)N * P * cpr;
   for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
@@ -272,7 +272,7 @@ hipError_t norm_moments_launch(const void* A, const void* B, int N, int P, int C
                                hipStream_t s) {
   const int nbp = norm_blocks_per_sample(N, P);
   hipLaunchKernelGGL(chan_moments_kernel, dim3(N * nbp), dim3(NT), NT * 2 * 8 * sizeof(float), s,
-                     (const bf16*)A, (const bf16*)B, P, C, nbp, partial);
+                     (const h16*)A, (const h16*)B, P, C, nbp, partial);
   hipLaunchKernelGGL(moments_collect_kernel, dim3(ew_grid((long long)N * 2 * C)), dim3(NT), 0, s, partial, N, C, nbp,
                      S);
   return hipGetLastError();
@@ -300,15 +300,15 @@ hipError_t gn_finalize_launch(const float* S, int N, int C, int G, int P, int mo
 hipError_t norm_apply_launch(const void* z, int N, int P, int C, const float* mean, const float* rstd, int cstride,
                              const float* gamma, const float* beta, int relu, float drop_rate, uint32_t seed,
                              const uint32_t* seed_ptr, uint32_t salt, void* y, hipStream_t s) {
-  hipLaunchKernelGGL(norm_apply_kernel, dim3(ew_grid((long long)N * P * (C / 8))), dim3(NT), 0, s, (const bf16*)z, N,
-                     P, C, mean, rstd, cstride, gamma, beta, relu, drop_rate, seed, seed_ptr, salt, (bf16*)y);
+  hipLaunchKernelGGL(norm_apply_kernel, dim3(ew_grid((long long)N * P * (C / 8))), dim3(NT), 0, s, (const h16*)z, N,
+                     P, C, mean, rstd, cstride, gamma, beta, relu, drop_rate, seed, seed_ptr, salt, (h16*)y);
   return hipGetLastError();
 }
 
 hipError_t norm_bwd_apply_launch(const void* g, const void* z, int N, int P, int C, const float* ca, const float* cb,
                                  const float* cc, int cstride, void* dz, hipStream_t s) {
   hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(ew_grid((long long)N * P * (C / 8))), dim3(NT), 0, s,
-                     (const bf16*)g, (const bf16*)z, N, P, C, ca, cb, cc, cstride, (bf16*)dz);
+                     (const h16*)g, (const h16*)z, N, P, C, ca, cb, cc, cstride, (h16*)dz);
   return hipGetLastError();
 }
 

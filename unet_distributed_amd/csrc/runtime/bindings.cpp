@@ -133,14 +133,54 @@ WgradParams wgrad_params(const py::dict& d) {
   return p;
 }
 
+// Kernel launchers of one element-type build.  dtype 0 = bf16 (namespace unet),
+// 1 = fp16 (namespace unet_f16); host-only helpers (prepare / pick / check) are
+// element-type independent and always come from the bf16 build.
+#define UNET_KERNEL_FNS(X) \
+  X(conv_fwd_launch) \
+  X(wgrad_launch) \
+  X(wgrad_reduce_launch) \
+  X(multi_reduce_launch) \
+  X(colsum_launch) \
+  X(cast_input_launch) \
+  X(maxpool2_fwd_launch) \
+  X(maxpool2_bwd_launch) \
+  X(upsample2_bwd_launch) \
+  X(head_fwd_launch) \
+  X(head_bwd_launch) \
+  X(partial_reduce_launch) \
+  X(norm_moments_launch) \
+  X(bn_finalize_launch) \
+  X(gn_finalize_launch) \
+  X(norm_apply_launch) \
+  X(norm_bwd_apply_launch) \
+  X(adam_pack_launch)
+
+struct KernelApi {
+#define UNET_DECL(f) decltype(&unet::f) f;
+  UNET_KERNEL_FNS(UNET_DECL)
+#undef UNET_DECL
+};
+
+#define UNET_BF16(f) &unet::f,
+#define UNET_F16(f) &unet_f16::f,
+const KernelApi kApi[2] = {{UNET_KERNEL_FNS(UNET_BF16)}, {UNET_KERNEL_FNS(UNET_F16)}};
+#undef UNET_BF16
+#undef UNET_F16
+
+const KernelApi* api(int dtype) {
+  if (dtype != 0 && dtype != 1) throw std::invalid_argument("dtype must be 0 (bf16) or 1 (fp16)");
+  return &kApi[dtype];
+}
+
 using Launcher = std::function<hipError_t(hipStream_t)>;
 
 // generic memory-bound ops: (kind, pointer args, int args, float args)
 // seedp: the owning plan's per-step dropout seed (nullptr for immediate calls: the
 // seed is then the op's last int argument); seed_devp: the plan's device seed pointer
 // (set for HIP-graph capture, where kernel arguments are frozen at capture time)
-Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, const std::vector<long long>& I,
-                      const std::vector<double>& F, const uint32_t* seedp = nullptr,
+Launcher make_generic(const KernelApi* A, const std::string& kind, const std::vector<uintptr_t>& P,
+                      const std::vector<long long>& I, const std::vector<double>& F, const uint32_t* seedp = nullptr,
                       const uint32_t* const* seed_devp = nullptr) {
   auto need = [&](size_t np, size_t ni, size_t nf) {
     if (P.size() < np || I.size() < ni || F.size() < nf)
@@ -152,28 +192,28 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     const float* x = (const float*)vp(0);
     void* y = vp(1);
     int a = I[0], b = I[1], c = I[2];
-    return [=](hipStream_t s) { return cast_input_launch(x, a, b, c, y, s); };
+    return [=](hipStream_t s) { return A->cast_input_launch(x, a, b, c, y, s); };
   }
   if (kind == "pool_fwd") {
     need(2, 6, 0);
     void *x = vp(0), *y = vp(1);
     int n = I[0], d = I[1], h = I[2], w = I[3], c = I[4], d3 = I[5];
     if (c % 8) throw std::invalid_argument("pool: C % 8");
-    return [=](hipStream_t s) { return maxpool2_fwd_launch(x, n, d, h, w, c, d3, y, s); };
+    return [=](hipStream_t s) { return A->maxpool2_fwd_launch(x, n, d, h, w, c, d3, y, s); };
   }
   if (kind == "pool_bwd") {
     need(4, 6, 0);
     void *x = vp(0), *dy = vp(1), *sk = vp(2), *dx = vp(3);
     int n = I[0], d = I[1], h = I[2], w = I[3], c = I[4], d3 = I[5];
     if (c % 8) throw std::invalid_argument("pool: C % 8");
-    return [=](hipStream_t s) { return maxpool2_bwd_launch(x, dy, sk, n, d, h, w, c, d3, dx, s); };
+    return [=](hipStream_t s) { return A->maxpool2_bwd_launch(x, dy, sk, n, d, h, w, c, d3, dx, s); };
   }
   if (kind == "ups_bwd") {
     need(3, 6, 0);
     void *du = vp(0), *mk = vp(1), *dl = vp(2);
     int n = I[0], d = I[1], h = I[2], w = I[3], c = I[4], d3 = I[5];
     if (c % 8) throw std::invalid_argument("ups_bwd: C % 8");
-    return [=](hipStream_t s) { return upsample2_bwd_launch(du, mk, n, d, h, w, c, d3, dl, s); };
+    return [=](hipStream_t s) { return A->upsample2_bwd_launch(du, mk, n, d, h, w, c, d3, dl, s); };
   }
   if (kind == "wgrad_reduce") {
     // ptrs: slab, out[, stage]   ints: splits, taps, Mtot, Mout, Nc[, rg, rkeep]
@@ -188,7 +228,7 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     const bool identity = (mo == mt) && (rg == rk);
     if (!stage && !(identity && sp <= 16))
       throw std::invalid_argument("wgrad_reduce: stage buffer required for >16 splits or row remap");
-    return [=](hipStream_t s) { return wgrad_reduce_launch(slab, sp, taps, mt, mo, nc, rg, rk, sc, out, stage, s); };
+    return [=](hipStream_t s) { return A->wgrad_reduce_launch(slab, sp, taps, mt, mo, nc, rg, rk, sc, out, stage, s); };
   }
   if (kind == "multi_reduce") {
     // ptrs: job table (device, ReduceJob[njobs])   ints: njobs, total1, total2
@@ -196,7 +236,7 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     const void* jobs = vp(0);
     int nj = (int)I[0];
     long long t1 = I[1], t2 = I[2];
-    return [=](hipStream_t s) { return multi_reduce_launch(jobs, nj, t1, t2, s); };
+    return [=](hipStream_t s) { return A->multi_reduce_launch(jobs, nj, t1, t2, s); };
   }
   if (kind == "colsum") {
     need(2, 3, 0);
@@ -204,14 +244,14 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     float* part = (float*)vp(1);
     int rows = I[0], c = I[1], blocks = I[2];
     if (c % 8 || c > 2048) throw std::invalid_argument("colsum: C % 8 / C > 2048");
-    return [=](hipStream_t s) { return colsum_launch(x, rows, c, blocks, part, s); };
+    return [=](hipStream_t s) { return A->colsum_launch(x, rows, c, blocks, part, s); };
   }
   if (kind == "partial_reduce") {
     need(2, 2, 0);
     const float* part = (const float*)vp(0);
     float* out = (float*)vp(1);
     int nb = I[0], width = I[1];
-    return [=](hipStream_t s) { return partial_reduce_launch(part, nb, width, out, s); };
+    return [=](hipStream_t s) { return A->partial_reduce_launch(part, nb, width, out, s); };
   }
   if (kind == "head_fwd") {
     need(7, 2, 0);
@@ -221,7 +261,7 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     float *prob = (float*)vp(4), *part = (float*)vp(5), *sums = (float*)vp(6);
     int P_ = I[0], C = I[1];
     check_msg(head_check(C));
-    return [=](hipStream_t s) { return head_fwd_launch(x, w, b, t, P_, C, prob, part, sums, s); };
+    return [=](hipStream_t s) { return A->head_fwd_launch(x, w, b, t, P_, C, prob, part, sums, s); };
   }
   if (kind == "head_bwd") {
     need(9, 2, 3);
@@ -233,9 +273,13 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     void* dx = vp(5);
     float *part = (float*)vp(6), *gw = (float*)vp(7), *gb = (float*)vp(8);
     int P_ = I[0], C = I[1];
+    // optional 10th pointer: device float loss scale (overrides floats[2])
+    const float* gsp = P.size() > 9 ? (const float*)vp(9) : nullptr;
     float it = (float)F[0], bw = (float)F[1], gs = (float)F[2];
     check_msg(head_check(C));
-    return [=](hipStream_t s) { return head_bwd_launch(x, w, prob, t, sums, P_, C, it, bw, gs, dx, part, gw, gb, s); };
+    return [=](hipStream_t s) {
+      return A->head_bwd_launch(x, w, prob, t, sums, P_, C, it, bw, gs, gsp, dx, part, gw, gb, s);
+    };
   }
   if (kind == "norm_moments") {
     // ptrs: A, B, partial, S   ints: N, P, C    (S[n][2][C] = per-sample sums of A and A*B)
@@ -244,7 +288,7 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     float *part = (float*)vp(2), *S = (float*)vp(3);
     int n = I[0], np = I[1], c = I[2];
     check_msg(norm_check(c, 0));
-    return [=](hipStream_t s) { return norm_moments_launch(a, b, n, np, c, part, S, s); };
+    return [=](hipStream_t s) { return A->norm_moments_launch(a, b, n, np, c, part, S, s); };
   }
   if (kind == "bn_finalize") {
     // ptrs: S, gamma, run_mean, run_var, mean, rstd, ca, cb, cc, dgamma, dbeta  ints: N, C, mode
@@ -257,7 +301,7 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     int n = I[0], c = I[1], mode = I[2];
     float cnt = (float)F[0], eps = (float)F[1], mom = (float)F[2];
     return [=](hipStream_t s) {
-      return bn_finalize_launch(S, n, c, cnt, mode, gm, eps, mom, rm, rv, mu, rs, ca, cb, cc, dg, db, s);
+      return A->bn_finalize_launch(S, n, c, cnt, mode, gm, eps, mom, rm, rv, mu, rs, ca, cb, cc, dg, db, s);
     };
   }
   if (kind == "gn_finalize") {
@@ -270,7 +314,7 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     int n = I[0], c = I[1], g = I[2], np = I[3], mode = I[4];
     float eps = (float)F[0];
     check_msg(norm_check(c, g));
-    return [=](hipStream_t s) { return gn_finalize_launch(S, n, c, g, np, mode, gm, eps, mu, rs, ca, cb, cc, dg, db, s); };
+    return [=](hipStream_t s) { return A->gn_finalize_launch(S, n, c, g, np, mode, gm, eps, mu, rs, ca, cb, cc, dg, db, s); };
   }
   if (kind == "norm_apply") {
     // ptrs: z, mean, rstd, gamma, beta, y   ints: N, P, C, cstride, relu, salt[, seed]   floats: drop_rate
@@ -284,7 +328,7 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     float dr = (float)F[0];
     check_msg(norm_check(c, 0));
     return [=](hipStream_t s) {
-      return norm_apply_launch(z, n, np, c, mu, rs, cs, gm, bt, relu, dr, seedp ? *seedp : seed0,
+      return A->norm_apply_launch(z, n, np, c, mu, rs, cs, gm, bt, relu, dr, seedp ? *seedp : seed0,
                                seed_devp ? *seed_devp : nullptr, salt, y, s);
     };
   }
@@ -296,7 +340,7 @@ Launcher make_generic(const std::string& kind, const std::vector<uintptr_t>& P, 
     void* dz = vp(5);
     int n = I[0], np = I[1], c = I[2], cs = I[3];
     check_msg(norm_check(c, 0));
-    return [=](hipStream_t s) { return norm_bwd_apply_launch(g, z, n, np, c, ca, cb, cc, cs, dz, s); };
+    return [=](hipStream_t s) { return A->norm_bwd_apply_launch(g, z, n, np, c, ca, cb, cc, cs, dz, s); };
   }
   if (kind == "memset") {
     need(1, 1, 0);
@@ -311,30 +355,33 @@ int head_blocks_py(int P) { return head_blocks(P); }
 
 class Plan {
  public:
+  explicit Plan(int dtype = 0) : A_(api(dtype)) {}
   int add_conv_fwd(const py::dict& d) {
     ConvFwdParams p = conv_params(d);
     const bool seeded = p.drop_rate > 0.f;
     const uint32_t* seedp = &seed_;
     const uint32_t* const* seed_devp = &seed_dev_;
-    ops_.push_back([p, seeded, seedp, seed_devp](hipStream_t s) mutable {
+    const KernelApi* A = A_;
+    ops_.push_back([p, seeded, seedp, seed_devp, A](hipStream_t s) mutable {
       if (seeded) {
         p.seed = *seedp;
         p.seed_ptr = *seed_devp;
       }
-      return conv_fwd_launch(p, s);
+      return A->conv_fwd_launch(p, s);
     });
     names_.push_back(get<std::string>(d, "name", "conv_fwd"));
     return (int)ops_.size() - 1;
   }
   int add_wgrad(const py::dict& d) {
     WgradParams p = wgrad_params(d);
-    ops_.push_back([p](hipStream_t s) { return wgrad_launch(p, s); });
+    const KernelApi* A = A_;
+    ops_.push_back([p, A](hipStream_t s) { return A->wgrad_launch(p, s); });
     names_.push_back(get<std::string>(d, "name", "wgrad"));
     return (int)ops_.size() - 1;
   }
   int add_generic(const std::string& kind, const std::vector<uintptr_t>& P, const std::vector<long long>& I,
                   const std::vector<double>& F, const std::string& name) {
-    ops_.push_back(make_generic(kind, P, I, F, &seed_, &seed_dev_));
+    ops_.push_back(make_generic(A_, kind, P, I, F, &seed_, &seed_dev_));
     names_.push_back(name.empty() ? kind : name);
     return (int)ops_.size() - 1;
   }
@@ -354,6 +401,7 @@ class Plan {
   }
 
  private:
+  const KernelApi* A_;
   std::vector<Launcher> ops_;
   std::vector<std::string> names_;
   uint32_t seed_ = 0;
@@ -364,30 +412,31 @@ class Plan {
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X (gfx950) HIP kernels and launch-plan executor for the UNet trainer";
-  m.def("conv_fwd", [](const py::dict& d, uintptr_t stream) {
+  // dtype: 0 = bf16 activations / weight copies, 1 = fp16
+  m.def("conv_fwd", [](const py::dict& d, uintptr_t stream, int dtype) {
     ConvFwdParams p = conv_params(d);
-    check(conv_fwd_launch(p, as_stream(stream)), "conv_fwd");
-  });
-  m.def("wgrad", [](const py::dict& d, uintptr_t stream) {
+    check(api(dtype)->conv_fwd_launch(p, as_stream(stream)), "conv_fwd");
+  }, py::arg("params"), py::arg("stream"), py::arg("dtype") = 0);
+  m.def("wgrad", [](const py::dict& d, uintptr_t stream, int dtype) {
     WgradParams p = wgrad_params(d);
-    check(wgrad_launch(p, as_stream(stream)), "wgrad");
-  });
+    check(api(dtype)->wgrad_launch(p, as_stream(stream)), "wgrad");
+  }, py::arg("params"), py::arg("stream"), py::arg("dtype") = 0);
   m.def("generic", [](const std::string& kind, const std::vector<uintptr_t>& P, const std::vector<long long>& I,
-                      const std::vector<double>& F, uintptr_t stream) {
-    check(make_generic(kind, P, I, F)(as_stream(stream)), kind.c_str());
-  });
+                      const std::vector<double>& F, uintptr_t stream, int dtype) {
+    check(make_generic(api(dtype), kind, P, I, F)(as_stream(stream)), kind.c_str());
+  }, py::arg("kind"), py::arg("ptrs"), py::arg("ints"), py::arg("floats"), py::arg("stream"), py::arg("dtype") = 0);
   m.def("adam_pack", [](uintptr_t w, uintptr_t g, uintptr_t mm, uintptr_t v, int n_total, uintptr_t segs, int nseg,
                         double lr_t, double b1, double b2, double eps, double gscale, int do_adam, uintptr_t arena,
-                        uintptr_t stream, uintptr_t scalars) {
+                        uintptr_t stream, uintptr_t scalars, int dtype) {
     // scalars: optional device float[2] = {lr_t, gscale} read by the kernel (HIP-graph replay)
     check_msg(adam_check(nseg));
-    check(adam_pack_launch((float*)w, (const float*)g, (float*)mm, (float*)v, n_total, (const void*)segs, nseg,
+    check(api(dtype)->adam_pack_launch((float*)w, (const float*)g, (float*)mm, (float*)v, n_total, (const void*)segs, nseg,
                            (float)lr_t, (float)b1, (float)b2, (float)eps, (float)gscale, do_adam,
                            (const float*)scalars, (void*)arena, as_stream(stream)),
           "adam_pack");
   }, py::arg("w"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("n_total"), py::arg("segs"), py::arg("nseg"),
      py::arg("lr_t"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("gscale"), py::arg("do_adam"),
-     py::arg("arena"), py::arg("stream"), py::arg("scalars") = 0);
+     py::arg("arena"), py::arg("stream"), py::arg("scalars") = 0, py::arg("dtype") = 0);
   m.def("head_blocks", &head_blocks_py);
   m.def("norm_blocks_per_sample", &norm_blocks_per_sample);
   m.def("wgrad_reduce_stage_floats", &wgrad_reduce_stage_floats);
@@ -444,7 +493,7 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("device_sync", []() { check(hipDeviceSynchronize(), "hipDeviceSynchronize"); });
   py::class_<Plan>(m, "Plan")
-      .def(py::init<>())
+      .def(py::init<int>(), py::arg("dtype") = 0)
       .def("add_conv_fwd", &Plan::add_conv_fwd)
       .def("add_wgrad", &Plan::add_wgrad)
       .def("add_generic", &Plan::add_generic, py::arg("kind"), py::arg("ptrs"), py::arg("ints"),

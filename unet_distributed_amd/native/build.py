@@ -43,24 +43,31 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
 
 
+# every kernel TU is built once per 16-bit element type (common.h): bf16 in namespace
+# `unet`, fp16 in namespace `unet_f16`
+VARIANTS = {"bf16": [], "f16": ["-DUNET_FP16", "-Dunet=unet_f16"]}
+
+
 def _hash(path, flags):
     h = hashlib.sha256()
     h.update(" ".join(flags).encode())
-    for f in sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)):
+    for f in sorted(glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True) +
+                    glob.glob(os.path.join(CSRC, "**", "*.inc"), recursive=True)):
         h.update(open(f, "rb").read())
     h.update(open(path, "rb").read())
     return h.hexdigest()[:20]
 
 
-def _compile(src):
+def _compile(job):
+    src, variant = job
     is_hip = src.endswith(".hip")
     flags = COMMON + _includes()
     if is_hip:
-        flags = flags + ["--offload-arch=" + ARCH, "-munsafe-fp-atomics"]
+        flags = flags + ["--offload-arch=" + ARCH, "-munsafe-fp-atomics"] + VARIANTS[variant]
     else:
         flags = flags + ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
     key = _hash(src, flags)
-    obj = os.path.join(OBJDIR, os.path.basename(src) + "." + key + ".o")
+    obj = os.path.join(OBJDIR, os.path.basename(src) + "." + variant + "." + key + ".o")
     if os.path.exists(obj):
         return obj, False
     cmd = [HIPCC] + flags + ["-c", src, "-o", obj + ".tmp"]
@@ -75,9 +82,12 @@ def build(verbose=True, jobs=None):
     os.makedirs(OBJDIR, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")) +
                   glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    work = [(f, v) for f in srcs for v in (VARIANTS if f.endswith(".hip") else ["bf16"])]
+    # largest TUs first so the pool finishes together
+    work.sort(key=lambda j: -os.path.getsize(j[0]))
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        results = list(ex.map(_compile, srcs))
+        results = list(ex.map(_compile, work))
     objs = [r[0] for r in results]
     rebuilt = any(r[1] for r in results)
     out = so_path()

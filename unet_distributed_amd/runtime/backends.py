@@ -100,7 +100,7 @@ class NativeBackend:
         self.flat = flat
         self.engine = NativeUNet(spec, flat, per_rank_batch, cfg.img_size, device, loss=cfg.loss,
                                  bce_weight=cfg.bce_weight, bucket_bounds=bounds,
-                                 eval_dropout=cfg.eval_dropout)
+                                 eval_dropout=cfg.eval_dropout, dtype=cfg.dtype)
         self.B = per_rank_batch
         if getattr(cfg, "hip_graph", False):
             self.engine.enable_graphs()
@@ -111,6 +111,7 @@ class NativeBackend:
 
     def fwd_bwd(self, x, y, seed: int, on_segment=None, grad_scale: float = 1.0):
         e = self.engine
+        e.set_loss_scale(grad_scale)
         e.load_batch(x, y)
         e.forward(seed)
         e.backward(on_segment)
@@ -142,8 +143,8 @@ def native_supported(spec, cfg, device) -> Optional[str]:
     """None if the native executor supports this config, else the reason."""
     if torch.device(device).type != "cuda":
         return "not on a GPU"
-    if cfg.dtype != "bf16":
-        return "native kernels are bf16 (dtype=%s)" % cfg.dtype
+    if cfg.dtype not in ("bf16", "fp16"):
+        return "native kernels are bf16 / fp16 (dtype=%s)" % cfg.dtype
     if spec.n_cl_out != 1:
         return "n_cl_out != 1"
     if spec.base % 32:

@@ -39,7 +39,6 @@ from .. import native
 from ..models.spec import UNetSpec
 from .params import FlatParams
 
-BF16 = torch.bfloat16
 
 
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -56,7 +55,7 @@ class NativeUNet:
     def __init__(self, spec: UNetSpec, flat: FlatParams, batch: int, img: int,
                  device, loss: str = "dice", bce_weight: float = 1.0,
                  bucket_bounds: Optional[Sequence[int]] = None, eval_dropout: bool = False,
-                 dry_run: bool = False):
+                 dry_run: bool = False, dtype: str = "bf16"):
         self.C = native.require()
         if spec.norm not in ("none", "batch", "group"):
             raise NotImplementedError("native executor: norm=%s" % spec.norm)
@@ -65,6 +64,13 @@ class NativeUNet:
         self.spec = spec
         self.flat = flat
         self.graphs = None      # HIP-graph cache (enable_graphs)
+        # 16-bit element type of activations, gradients w.r.t. activations and the
+        # weight copies: selects the bf16 or fp16 build of every kernel (common.h)
+        if dtype not in ("bf16", "fp16"):
+            raise NotImplementedError("native executor: dtype=%s" % dtype)
+        self.dtype = dtype
+        self.adt = torch.bfloat16 if dtype == "bf16" else torch.float16
+        self.dt_id = 0 if dtype == "bf16" else 1
         self.B = batch
         self.img = img
         self.dims = spec.dims
@@ -86,8 +92,8 @@ class NativeUNet:
         self.wgrad_win = int(os.environ.get("UNET_WGRAD_WIN", "0"))
         self._alloc_weights()
         self._alloc_activations()
-        self.plan = self.C.Plan()
-        self.eval_plan = self.C.Plan()
+        self.plan = self.C.Plan(self.dt_id)
+        self.eval_plan = self.C.Plan(self.dt_id)
         self._build_forward(self.plan, dropout=True)
         self.fwd_end = self.plan.size()
         self.seg_ends: List[int] = []
@@ -108,7 +114,8 @@ class NativeUNet:
         d, h, w = self.sdims(level)
         return self.B * d * h * w
 
-    def _buf(self, name, level, ch, dtype=BF16):
+    def _buf(self, name, level, ch, dtype=None):
+        dtype = self.adt if dtype is None else dtype
         d, h, w = self.sdims(level)
         shape = (self.B, h, w, ch) if self.dims == 2 else (self.B, d, h, w, ch)
         t = torch.empty(shape, dtype=dtype, device=self.device)
@@ -145,7 +152,7 @@ class NativeUNet:
                 self.w_dg_off[l.name] = off
                 off += l.cin * dgrow
                 layouts[l.name] = (2, Tt, l.cin, l.cout, l.cin, row, dgrow)
-        self.arena = torch.zeros(max(off, 64), dtype=BF16, device=self.device)
+        self.arena = torch.zeros(max(off, 64), dtype=self.adt, device=self.device)
         segs = []
         for name, shape, foff, n in flat.entries:
             lname, var = name.split("/", 1)
@@ -178,7 +185,7 @@ class NativeUNet:
         f = self.flat
         self.C.adam_pack(_ptr(f.master), _ptr(f.grad), _ptr(f.m), _ptr(f.v), f.numel,
                          _ptr(self.segs), self.nseg, 0.0, 0.9, 0.999, 1e-8, 1.0, 0,
-                         _ptr(self.arena), native.stream_handle(stream))
+                         _ptr(self.arena), native.stream_handle(stream), dtype=self.dt_id)
 
     def adam_step(self, lr, beta1_power, beta2_power, grad_scale=1.0, stream=None,
                   beta1=0.9, beta2=0.999, eps=1e-8):
@@ -191,11 +198,11 @@ class NativeUNet:
             sc = _ptr(self.adam_scalars)
             self._replay(("adam", beta1, beta2, eps), lambda s: self.C.adam_pack(
                 _ptr(f.master), _ptr(f.grad), _ptr(f.m), _ptr(f.v), f.numel, _ptr(self.segs), self.nseg,
-                lr_t, beta1, beta2, eps, grad_scale, 1, _ptr(self.arena), s, sc))
+                lr_t, beta1, beta2, eps, grad_scale, 1, _ptr(self.arena), s, sc, self.dt_id))
             return
         self.C.adam_pack(_ptr(f.master), _ptr(f.grad), _ptr(f.m), _ptr(f.v), f.numel,
                          _ptr(self.segs), self.nseg, lr_t, beta1, beta2, eps, grad_scale, 1,
-                         _ptr(self.arena), native.stream_handle(stream))
+                         _ptr(self.arena), native.stream_handle(stream), dtype=self.dt_id)
 
     # ------------------------------------------------------------------ buffers
     def _alloc_activations(self):
@@ -203,7 +210,10 @@ class NativeUNet:
         self.x_f32 = torch.zeros((self.npix(1), spec.in_channels), dtype=torch.float32,
                                  device=self.device)
         self._buf("x", 1, self.cpad)
-        self.target = torch.zeros(self.npix(1), dtype=BF16, device=self.device)
+        self.target = torch.zeros(self.npix(1), dtype=self.adt, device=self.device)
+        # loss-gradient scale read by the head backward (fp16 dynamic loss scaling)
+        self.loss_scale_dev = torch.ones(1, dtype=torch.float32, device=self.device)
+        self._loss_scale = 1.0
         # tensor graph: name -> (level, channels, produced_by_relu, dropout)
         self.tinfo: Dict[str, Tuple[int, int, bool, bool]] = {"x": (1, self.cpad, False, False)}
         self.inputs: Dict[str, Tuple] = {}
@@ -258,7 +268,7 @@ class NativeUNet:
                     lvl, ch = self.tinfo[src1][0], self.tinfo[src1][1]
                     d, h, w = self.sdims(l.level)
                     shape = (self.B, h, w, ch) if self.dims == 2 else (self.B, d, h, w, ch)
-                    self.bufs["dfull:" + src1] = torch.empty(shape, dtype=BF16, device=self.device)
+                    self.bufs["dfull:" + src1] = torch.empty(shape, dtype=self.adt, device=self.device)
         self.slab = None
         self.bias_slab = None
         self._alloc_norm()
@@ -463,7 +473,7 @@ class NativeUNet:
                              lambda hc=hc: [_ptr(b[self.head_in]), self.master_ptr("Mask/kernel"), _ptr(self.prob),
                                             _ptr(self.target), _ptr(self.sums), _ptr(b["d:" + self.head_in]),
                                             _ptr(self.head_partial), self.grad_ptr("Mask/kernel"),
-                                            self.grad_ptr("Mask/bias")],
+                                            self.grad_ptr("Mask/bias"), _ptr(self.loss_scale_dev)],
                              [P1, hc], [inv_total, self.bce_weight, 1.0], "bwd:Mask")
                 done("Mask")
             elif l.kind == "conv":
@@ -707,6 +717,13 @@ class NativeUNet:
                 launch(native.stream_handle(None))
             self.graphs[key] = g
         g.replay()
+
+    def set_loss_scale(self, scale: float):
+        """Scale of the loss gradient entering the backward (all parameter gradients
+        scale with it); lives on the device so plans and graphs need no rebuild."""
+        if scale != self._loss_scale:
+            self.loss_scale_dev.fill_(scale)
+            self._loss_scale = scale
 
     def forward(self, seed: int, stream=None):
         seed &= 0xFFFFFFFF

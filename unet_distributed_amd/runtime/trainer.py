@@ -34,6 +34,7 @@ from ..parallel.async_ps import AsyncPS
 from ..parallel.grad_sync import GradSync, plan_buckets
 from ..utils import checkpoint as ckpt
 from ..utils.metrics import MetricLogger
+from .amp import LossScaler
 from .backends import make_backend
 from .optim import TFAdam, learning_rate
 from .params import FlatParams
@@ -141,6 +142,7 @@ class Trainer:
         self.sync = GradSync(self.flat, self.bounds, self.ctx, overlap=cfg.overlap_comm)
         native_opt = self.backend if hasattr(self.backend, "adam_step") else None
         self.opt = TFAdam(self.flat, cfg, native=_NativeOpt(native_opt) if native_opt else None)
+        self.scaler = LossScaler(cfg.dtype, cfg.loss_scale)
         self.log = MetricLogger(cfg, self.is_chief, self.ckpt.logdir)
         self.ranges = _Ranges(cfg.profile)
         self.tb_proc = None
@@ -221,18 +223,25 @@ class Trainer:
     # ------------------------------------------------------------------ step
     def train_step(self, x, y, seed: int) -> None:
         R = self.ranges
+        scale = self.scaler.scale
         if self.async_ps is not None:
             with R("forward_backward"):
-                self.backend.fwd_bwd(x, y, seed, on_segment=None)
+                self.backend.fwd_bwd(x, y, seed, on_segment=None, grad_scale=scale)
+            if self.scaler.enabled:
+                if not self.scaler.update(self.flat.grad):
+                    return                      # fp16 overflow: nothing is pushed
+                self.flat.grad.mul_(1.0 / scale)
             with R("ps_push_pull"):
                 self.async_ps.push_pull()
             return
         with R("forward_backward"):
-            self.backend.fwd_bwd(x, y, seed, on_segment=self.sync.on_segment)
+            self.backend.fwd_bwd(x, y, seed, on_segment=self.sync.on_segment, grad_scale=scale)
         with R("grad_sync"):
             self.sync.finish()
+        if not self.scaler.update(self.flat.grad):
+            return                              # fp16 overflow: step skipped, scale halved
         with R("optimizer"):
-            self.opt.step()
+            self.opt.step(grad_scale=1.0 / scale)
 
     def check_sync(self):
         """Cross-rank parameter checksum (detects DP divergence)."""
