@@ -401,7 +401,8 @@ def test_dropout_matches_reference_hash(cuda_dev):
 
 
 @pytest.mark.parametrize("norm,N,H,Cc,G", [("batch", 4, 16, 32, 0), ("batch", 3, 8, 64, 0), ("group", 4, 16, 64, 8),
-                                           ("group", 2, 8, 32, 4)])
+                                           ("group", 2, 8, 32, 4), ("batch", 80, 4, 32, 0), ("group", 70, 4, 48, 4),
+                                           ("batch", 2, 32, 48, 0)])
 def test_norm_fwd_bwd_kernels(cuda_dev, norm, N, H, Cc, G):
     """BN / GN forward (batch statistics, ReLU) and backward (dz, dgamma, dbeta) against
     autograd of the fp32 ATen ops on the same bf16 inputs."""
@@ -419,26 +420,29 @@ def test_norm_fwd_bwd_kernels(cuda_dev, norm, N, H, Cc, G):
     mean, rstd, ca, cb, cc = [torch.zeros(rows * Cc, device=dev) for _ in range(5)]
     rm, rv = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
     dg, db = torch.zeros(Cc, device=dev), torch.zeros(Cc, device=dev)
+    work = torch.zeros(C().sample_slices(N) * 2 * Cc, device=dev)        # finalize workspace
+    wp = ptr(work)
     y = torch.empty_like(z)
     dz = torch.empty_like(z)
     st = stream()
     C().generic("norm_moments", [ptr(z), ptr(z), ptr(part), ptr(S)], [N, P, Cc], [], st)
     if norm == "batch":
-        C().generic("bn_finalize", [ptr(S), ptr(gam), ptr(rm), ptr(rv), ptr(mean), ptr(rstd), 0, 0, 0, 0, 0],
+        C().generic("bn_finalize", [ptr(S), ptr(gam), ptr(rm), ptr(rv), ptr(mean), ptr(rstd), 0, 0, 0, 0, 0, wp],
                     [N, Cc, 0], [float(N * P), 1e-3, 0.01], st)
         cs = 0
     else:
-        C().generic("gn_finalize", [ptr(S), ptr(gam), ptr(mean), ptr(rstd), 0, 0, 0, 0, 0], [N, Cc, G, P, 0], [1e-3], st)
+        C().generic("gn_finalize", [ptr(S), ptr(gam), ptr(mean), ptr(rstd), 0, 0, 0, 0, 0, wp], [N, Cc, G, P, 0],
+                    [1e-3], st)
         cs = Cc
     C().generic("norm_apply", [ptr(z), ptr(mean), ptr(rstd), ptr(gam), ptr(bet), ptr(y)], [N, P, Cc, cs, 1, 0, 0],
                 [0.0], st)
     C().generic("norm_moments", [ptr(g), ptr(z), ptr(part), ptr(S)], [N, P, Cc], [], st)
     if norm == "batch":
         C().generic("bn_finalize", [ptr(S), ptr(gam), 0, 0, ptr(mean), ptr(rstd), ptr(ca), ptr(cb), ptr(cc), ptr(dg),
-                                    ptr(db)], [N, Cc, 1], [float(N * P), 1e-3, 0.01], st)
+                                    ptr(db), wp], [N, Cc, 1], [float(N * P), 1e-3, 0.01], st)
     else:
         C().generic("gn_finalize", [ptr(S), ptr(gam), ptr(mean), ptr(rstd), ptr(ca), ptr(cb), ptr(cc), ptr(dg),
-                                    ptr(db)], [N, Cc, G, P, 1], [1e-3], st)
+                                    ptr(db), wp], [N, Cc, G, P, 1], [1e-3], st)
     C().generic("norm_bwd_apply", [ptr(g), ptr(z), ptr(ca), ptr(cb), ptr(cc), ptr(dz)], [N, P, Cc, cs], [], st)
     torch.cuda.synchronize()
     zr = nchw(z.float()).requires_grad_(True)

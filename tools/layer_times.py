@@ -50,15 +50,18 @@ def main():
     ap.add_argument("--dims", type=int, default=2)
     ap.add_argument("--upsampling", action="store_true")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--norm", default="none", choices=["none", "batch", "group"])
+    ap.add_argument("--groups", type=int, default=8)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     cfg = Config(batch_size=a.batch, img_size=a.img, in_channels=a.in_channels, dims=a.dims,
-                 use_upsampling=a.upsampling)
+                 use_upsampling=a.upsampling, norm=a.norm, groups=a.groups, dtype=a.dtype)
     spec = spec_from_config(cfg)
     flat = FlatParams(spec, device=dev)
     flat.load_dict(reference.init_params(spec, seed=1))
-    e = NativeUNet(spec, flat, a.batch, a.img, dev)
+    e = NativeUNet(spec, flat, a.batch, a.img, dev, dtype=a.dtype)
     x, y = synthetic_brats(min(a.batch, 64), a.img, a.in_channels, a.dims, seed=0)
     reps = (a.batch + 63) // 64
     x = torch.from_numpy(x).repeat((reps,) + (1,) * (x.ndim - 1))[:a.batch].to(dev)
@@ -94,8 +97,8 @@ def main():
     en.record()
     torch.cuda.synchronize()
     step = st.elapsed_time(en) / a.reps
-    lines = ["# Per-launch times, native step, %dD UNet %dx%d in_ch=%d, batch %d (1x MI355X)" %
-             (a.dims, a.img, a.img, a.in_channels, a.batch), "",
+    lines = ["# Per-launch times, native step, %dD UNet %dx%d in_ch=%d, batch %d, norm %s, %s (1x MI355X)" %
+             (a.dims, a.img, a.img, a.in_channels, a.batch, a.norm, a.dtype), "",
              "sum of isolated launches %.3f ms; back-to-back step %.3f ms (%.0f img/s fwd+bwd only)"
              % (total, step, a.batch / step * 1e3), "",
              "| # | launch | ms | TFLOP/s |", "|---|---|---|---|"]

@@ -74,33 +74,60 @@ __global__ void __launch_bounds__(NT) moments_collect_kernel(const float* __rest
   }
 }
 
-// BatchNorm per channel (grid: C / 64 blocks of 64 channels x 4 sample slices).
+// Sample-slice sums of the per-sample moments (deterministic first level of every
+// reduction over samples; the finalize kernels then sum <= 64 slices per channel):
+//   partial[sl][0][c] = sum_{n in sl} S1[n][c]
+//   partial[sl][1][c] = sum_{n in sl} S2[n][c]                      (mean == nullptr)
+//                     = sum_{n in sl} rstd[n][c] (S2 - mean[n][c] S1)  (GroupNorm dgamma)
+// grid: (ceil(C / 64), nsl), 256 threads = 64 channels x 4 sample lanes
+__global__ void __launch_bounds__(NT) sample_slices_kernel(const float* __restrict__ S, int N, int C, int nsl,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd,
+                                                           float* __restrict__ partial) {
+  __shared__ float red[4][2][64];
+  const int cl = threadIdx.x & 63, sub = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, sl = blockIdx.y;
+  const int n0 = (int)((long long)sl * N / nsl), n1 = (int)((long long)(sl + 1) * N / nsl);
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    for (int n = n0 + sub; n < n1; n += 4) {
+      const float s1 = S[((size_t)n * 2 + 0) * C + c], s2 = S[((size_t)n * 2 + 1) * C + c];
+      a += s1;
+      b += mean ? rstd[(size_t)n * C + c] * (s2 - mean[(size_t)n * C + c] * s1) : s2;
+    }
+  }
+  red[sub][0][cl] = a;
+  red[sub][1][cl] = b;
+  __syncthreads();
+  if (sub == 0 && c < C) {
+    partial[((size_t)sl * 2 + 0) * C + c] = red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl];
+    partial[((size_t)sl * 2 + 1) * C + c] = red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl];
+  }
+}
+
+// BatchNorm per channel from the sample-slice sums (thread per channel).
 //   mode 0 (forward, training): mean/rstd[c] from the batch, running stats updated
 //   mode 1 (backward): coefficients a/b/c[c], dgamma/dbeta
 //   mode 2 (forward, inference): mean/rstd[c] from the running stats
-__global__ void __launch_bounds__(NT) bn_finalize_kernel(const float* __restrict__ S, int N, int C, float count,
+__global__ void __launch_bounds__(NT) bn_finalize_kernel(const float* __restrict__ part, int nsl, int C, float count,
                                                          int mode, const float* __restrict__ gamma, float eps,
                                                          float momentum, float* __restrict__ run_mean,
                                                          float* __restrict__ run_var, float* __restrict__ mean,
                                                          float* __restrict__ rstd, float* __restrict__ ca,
                                                          float* __restrict__ cb, float* __restrict__ cc,
                                                          float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  __shared__ float red[4][2][64];
-  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  float s1 = 0.f, s2 = 0.f;
-  if (c < C && mode != 2) {
-    for (int n = sl; n < N; n += 4) {
-      s1 += S[((size_t)n * 2 + 0) * C + c];
-      s2 += S[((size_t)n * 2 + 1) * C + c];
-    }
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  if (mode == 2) {
+    mean[c] = run_mean[c];
+    rstd[c] = rsqrtf(run_var[c] + eps);
+    return;
   }
-  red[sl][0][cl] = s1;
-  red[sl][1][cl] = s2;
-  __syncthreads();
-  if (sl != 0 || c >= C) return;
-  s1 = red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl];
-  s2 = red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl];
+  float s1 = 0.f, s2 = 0.f;
+  for (int sl = 0; sl < nsl; ++sl) {
+    s1 += part[((size_t)sl * 2 + 0) * C + c];
+    s2 += part[((size_t)sl * 2 + 1) * C + c];
+  }
   if (mode == 0) {
     const float mu = s1 / count;
     const float var = fmaxf(s2 / count - mu * mu, 0.f);
@@ -108,9 +135,6 @@ __global__ void __launch_bounds__(NT) bn_finalize_kernel(const float* __restrict
     rstd[c] = rsqrtf(var + eps);
     run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
     run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * (count / fmaxf(count - 1.f, 1.f));
-  } else if (mode == 2) {
-    mean[c] = run_mean[c];
-    rstd[c] = rsqrtf(run_var[c] + eps);
   } else {
     const float mu = mean[c], r = rstd[c], gm = gamma[c];
     const float sgx = r * (s2 - mu * s1);       // sum g x^
@@ -167,82 +191,138 @@ __global__ void __launch_bounds__(NT) gn_finalize_kernel(const float* __restrict
   }
 }
 
-// GroupNorm parameter gradients (per channel over samples), thread per channel
-__global__ void __launch_bounds__(NT) gn_param_grad_kernel(const float* __restrict__ S, int N, int C,
-                                                           const float* __restrict__ mean,
-                                                           const float* __restrict__ rstd,
+// GroupNorm parameter gradients from the sample-slice sums (thread per channel)
+__global__ void __launch_bounds__(NT) gn_param_grad_kernel(const float* __restrict__ part, int nsl, int C,
                                                            float* __restrict__ dgamma, float* __restrict__ dbeta) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= C) return;
   float db = 0.f, dg = 0.f;
-  for (int n = 0; n < N; ++n) {
-    const float s1 = S[((size_t)n * 2 + 0) * C + c], s2 = S[((size_t)n * 2 + 1) * C + c];
-    db += s1;
-    dg += rstd[(size_t)n * C + c] * (s2 - mean[(size_t)n * C + c] * s1);
+  for (int sl = 0; sl < nsl; ++sl) {
+    db += part[((size_t)sl * 2 + 0) * C + c];
+    dg += part[((size_t)sl * 2 + 1) * C + c];
   }
   dgamma[c] = dg;
   dbeta[c] = db;
 }
 
-// y = relu(gamma (z - mean) rstd + beta) with optional inverted dropout (counter hash,
-// same stream as the conv epilogue's); coefficient arrays are [C] (cstride 0) or [N][C]
-__global__ void __launch_bounds__(NT) norm_apply_kernel(const h16* __restrict__ z, int N, int P, int C,
+// Elementwise passes: grid (blocks per sample, N).  A thread keeps ONE 8-channel
+// column (cc) for the whole pass, so its per-(n, c) coefficients are loaded once and
+// the pixel loop is one 16-byte load, 8 FMAs and one 16-byte store per step (unrolled
+// 4x for memory-level parallelism).  Rows of the block: rstep = NT / cpr.
+constexpr int kUnroll = 4;
+
+// y = relu(A z + B) with A = gamma rstd, B = beta - mean A (coefficients [C] or [N][C]),
+// optional inverted dropout (counter hash, same stream as the conv epilogue's)
+__global__ void __launch_bounds__(NT) norm_apply_kernel(const h16* __restrict__ z, int P, int C,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, int cstride,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int relu, float drop_rate,
                                                         uint32_t seed0, const uint32_t* __restrict__ seed_ptr,
                                                         uint32_t salt, h16* __restrict__ y) {
-  const uint32_t seed = (drop_rate > 0.f && seed_ptr) ? *seed_ptr : seed0;
-  const int cpr = C / 8;
-  const long long total = (long long)N * P * cpr;
-  const float inv_keep = drop_rate > 0.f ? 1.f / (1.f - drop_rate) : 1.f;
-  const uint32_t thr = (uint32_t)(drop_rate * 4294967296.0);
-  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    const int cc = (int)(i % cpr);
-    const long long q = i / cpr;
-    const int n = (int)(q / P);
-    const int c0 = cc * 8;
-    float v[8];
-    unpack8(*(const u32x4*)(z + q * C + c0), v);
+  const int n = blockIdx.y, nbp = gridDim.x, blk = blockIdx.x;
+  const int cpr = C / 8, rstep = NT / cpr;
+  const int cc = threadIdx.x % cpr, rs = threadIdx.x / cpr;
+  if (rs >= rstep) return;
+  const int c0 = cc * 8;
+  float A[8], B[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = c0 + e;
-      const size_t k = (size_t)n * cstride + c;
-      float x = gamma[c] * (v[e] - mean[k]) * rstd[k] + beta[c];
-      if (relu) x = fmaxf(x, 0.f);
-      if (drop_rate > 0.f) {
-        const uint32_t h = drop_hash((uint64_t)q * C + c, seed, salt);
-        x = (h >= thr) ? x * inv_keep : 0.f;
+  for (int e = 0; e < 8; ++e) {
+    const size_t k = (size_t)n * cstride + c0 + e;
+    A[e] = gamma[c0 + e] * rstd[k];
+    B[e] = beta[c0 + e] - mean[k] * A[e];
+  }
+  const int p0 = (int)((long long)blk * P / nbp), p1 = (int)((long long)(blk + 1) * P / nbp);
+  const size_t base = (size_t)n * P * C + c0;
+  if (drop_rate > 0.f) {
+    const uint32_t seed = seed_ptr ? *seed_ptr : seed0;
+    const float inv_keep = 1.f / (1.f - drop_rate);
+    const uint32_t thr = (uint32_t)(drop_rate * 4294967296.0);
+    for (int p = p0 + rs; p < p1; p += rstep) {
+      const size_t q = (size_t)n * P + p;
+      float v[8];
+      unpack8(*(const u32x4*)(z + base + (size_t)p * C), v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = fmaf(A[e], v[e], B[e]);
+        if (relu) x = fmaxf(x, 0.f);
+        const uint32_t h = drop_hash((uint64_t)q * C + c0 + e, seed, salt);
+        v[e] = (h >= thr) ? x * inv_keep : 0.f;
       }
-      v[e] = x;
+      *(u32x4*)(y + base + (size_t)p * C) = pack8(v);
     }
-    *(u32x4*)(y + q * C + c0) = pack8(v);
+    return;
+  }
+  const float lo = relu ? 0.f : -INFINITY;
+  int p = p0 + rs;
+  for (; p + (kUnroll - 1) * rstep < p1; p += kUnroll * rstep) {
+    u32x4 raw[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) raw[u] = *(const u32x4*)(z + base + (size_t)(p + u * rstep) * C);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      float v[8];
+      unpack8(raw[u], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(A[e], v[e], B[e]), lo);
+      *(u32x4*)(y + base + (size_t)(p + u * rstep) * C) = pack8(v);
+    }
+  }
+  for (; p < p1; p += rstep) {
+    float v[8];
+    unpack8(*(const u32x4*)(z + base + (size_t)p * C), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(A[e], v[e], B[e]), lo);
+    *(u32x4*)(y + base + (size_t)p * C) = pack8(v);
   }
 }
 
 // dz = a g + b z + c  (coefficients [C] or [N][C])
 __global__ void __launch_bounds__(NT) norm_bwd_apply_kernel(const h16* __restrict__ g, const h16* __restrict__ z,
-                                                            int N, int P, int C, const float* __restrict__ ca,
+                                                            int P, int C, const float* __restrict__ ca,
                                                             const float* __restrict__ cb,
                                                             const float* __restrict__ ccf, int cstride,
                                                             h16* __restrict__ dz) {
-  const int cpr = C / 8;
-  const long long total = (long long)N * P * cpr;
-  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    const int cc = (int)(i % cpr);
-    const long long q = i / cpr;
-    const int n = (int)(q / P);
-    const int c0 = cc * 8;
-    float gv[8], zv[8];
-    unpack8(*(const u32x4*)(g + q * C + c0), gv);
-    unpack8(*(const u32x4*)(z + q * C + c0), zv);
+  const int n = blockIdx.y, nbp = gridDim.x, blk = blockIdx.x;
+  const int cpr = C / 8, rstep = NT / cpr;
+  const int cc = threadIdx.x % cpr, rs = threadIdx.x / cpr;
+  if (rs >= rstep) return;
+  const int c0 = cc * 8;
+  float a[8], b[8], c[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const size_t k = (size_t)n * cstride + c0 + e;
-      gv[e] = ca[k] * gv[e] + cb[k] * zv[e] + ccf[k];
+  for (int e = 0; e < 8; ++e) {
+    const size_t k = (size_t)n * cstride + c0 + e;
+    a[e] = ca[k];
+    b[e] = cb[k];
+    c[e] = ccf[k];
+  }
+  const int p0 = (int)((long long)blk * P / nbp), p1 = (int)((long long)(blk + 1) * P / nbp);
+  const size_t base = (size_t)n * P * C + c0;
+  int p = p0 + rs;
+  for (; p + (kUnroll - 1) * rstep < p1; p += kUnroll * rstep) {
+    u32x4 rg[kUnroll], rz[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      rg[u] = *(const u32x4*)(g + base + (size_t)(p + u * rstep) * C);
+      rz[u] = *(const u32x4*)(z + base + (size_t)(p + u * rstep) * C);
     }
-    *(u32x4*)(dz + q * C + c0) = pack8(gv);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      float gv[8], zv[8];
+      unpack8(rg[u], gv);
+      unpack8(rz[u], zv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gv[e] = fmaf(a[e], gv[e], fmaf(b[e], zv[e], c[e]));
+      *(u32x4*)(dz + base + (size_t)(p + u * rstep) * C) = pack8(gv);
+    }
+  }
+  for (; p < p1; p += rstep) {
+    float gv[8], zv[8];
+    unpack8(*(const u32x4*)(g + base + (size_t)p * C), gv);
+    unpack8(*(const u32x4*)(z + base + (size_t)p * C), zv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gv[e] = fmaf(a[e], gv[e], fmaf(b[e], zv[e], c[e]));
+    *(u32x4*)(dz + base + (size_t)p * C) = pack8(gv);
   }
 }
 
@@ -278,37 +358,47 @@ hipError_t norm_moments_launch(const void* A, const void* B, int N, int P, int C
   return hipGetLastError();
 }
 
+int sample_slices(int N) { return N < 64 ? N : 64; }
+
 hipError_t bn_finalize_launch(const float* S, int N, int C, float count, int mode, const float* gamma, float eps,
                               float momentum, float* run_mean, float* run_var, float* mean, float* rstd, float* ca,
-                              float* cb, float* cc, float* dgamma, float* dbeta, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(NT), 0, s, S, N, C, count, mode, gamma, eps,
-                     momentum, run_mean, run_var, mean, rstd, ca, cb, cc, dgamma, dbeta);
+                              float* cb, float* cc, float* dgamma, float* dbeta, float* partial, hipStream_t s) {
+  const int nsl = sample_slices(N);
+  if (mode != 2)
+    hipLaunchKernelGGL(sample_slices_kernel, dim3((C + 63) / 64, nsl), dim3(NT), 0, s, S, N, C, nsl,
+                       (const float*)nullptr, (const float*)nullptr, partial);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, partial, nsl, C, count, mode, gamma,
+                     eps, momentum, run_mean, run_var, mean, rstd, ca, cb, cc, dgamma, dbeta);
   return hipGetLastError();
 }
 
 hipError_t gn_finalize_launch(const float* S, int N, int C, int G, int P, int mode, const float* gamma, float eps,
                               float* mean, float* rstd, float* ca, float* cb, float* cc, float* dgamma, float* dbeta,
-                              hipStream_t s) {
+                              float* partial, hipStream_t s) {
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((N * G + NT - 1) / NT), dim3(NT), 0, s, S, N, C, G, (float)P, mode,
                      gamma, eps, mean, rstd, ca, cb, cc);
-  if (mode == 1)
-    hipLaunchKernelGGL(gn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, S, N, C, mean, rstd, dgamma,
-                       dbeta);
+  if (mode == 1) {
+    const int nsl = sample_slices(N);
+    hipLaunchKernelGGL(sample_slices_kernel, dim3((C + 63) / 64, nsl), dim3(NT), 0, s, S, N, C, nsl,
+                       (const float*)mean, (const float*)rstd, partial);
+    hipLaunchKernelGGL(gn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, (const float*)partial, nsl, C,
+                       dgamma, dbeta);
+  }
   return hipGetLastError();
 }
 
 hipError_t norm_apply_launch(const void* z, int N, int P, int C, const float* mean, const float* rstd, int cstride,
                              const float* gamma, const float* beta, int relu, float drop_rate, uint32_t seed,
                              const uint32_t* seed_ptr, uint32_t salt, void* y, hipStream_t s) {
-  hipLaunchKernelGGL(norm_apply_kernel, dim3(ew_grid((long long)N * P * (C / 8))), dim3(NT), 0, s, (const h16*)z, N,
-                     P, C, mean, rstd, cstride, gamma, beta, relu, drop_rate, seed, seed_ptr, salt, (h16*)y);
+  hipLaunchKernelGGL(norm_apply_kernel, dim3(norm_blocks_per_sample(N, P), N), dim3(NT), 0, s, (const h16*)z, P, C,
+                     mean, rstd, cstride, gamma, beta, relu, drop_rate, seed, seed_ptr, salt, (h16*)y);
   return hipGetLastError();
 }
 
 hipError_t norm_bwd_apply_launch(const void* g, const void* z, int N, int P, int C, const float* ca, const float* cb,
                                  const float* cc, int cstride, void* dz, hipStream_t s) {
-  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(ew_grid((long long)N * P * (C / 8))), dim3(NT), 0, s,
-                     (const h16*)g, (const h16*)z, N, P, C, ca, cb, cc, cstride, (h16*)dz);
+  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(norm_blocks_per_sample(N, P), N), dim3(NT), 0, s, (const h16*)g,
+                     (const h16*)z, P, C, ca, cb, cc, cstride, (h16*)dz);
   return hipGetLastError();
 }
 

@@ -291,30 +291,36 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     return [=](hipStream_t s) { return A->norm_moments_launch(a, b, n, np, c, part, S, s); };
   }
   if (kind == "bn_finalize") {
-    // ptrs: S, gamma, run_mean, run_var, mean, rstd, ca, cb, cc, dgamma, dbeta  ints: N, C, mode
-    // floats: count, eps, momentum
-    need(11, 3, 3);
+    // ptrs: S, gamma, run_mean, run_var, mean, rstd, ca, cb, cc, dgamma, dbeta, partial  ints: N, C, mode
+    // floats: count, eps, momentum   (partial: sample_slices(N) * 2 * C floats of workspace)
+    need(12, 3, 3);
     const float* S = (const float*)vp(0);
     const float* gm = (const float*)vp(1);
     float *rm = (float*)vp(2), *rv = (float*)vp(3), *mu = (float*)vp(4), *rs = (float*)vp(5);
     float *ca = (float*)vp(6), *cb = (float*)vp(7), *cc = (float*)vp(8), *dg = (float*)vp(9), *db = (float*)vp(10);
     int n = I[0], c = I[1], mode = I[2];
+    float* pt = (float*)vp(11);
     float cnt = (float)F[0], eps = (float)F[1], mom = (float)F[2];
+    if (mode != 2 && !pt) throw std::invalid_argument("bn_finalize: partial workspace required");
     return [=](hipStream_t s) {
-      return A->bn_finalize_launch(S, n, c, cnt, mode, gm, eps, mom, rm, rv, mu, rs, ca, cb, cc, dg, db, s);
+      return A->bn_finalize_launch(S, n, c, cnt, mode, gm, eps, mom, rm, rv, mu, rs, ca, cb, cc, dg, db, pt, s);
     };
   }
   if (kind == "gn_finalize") {
-    // ptrs: S, gamma, mean, rstd, ca, cb, cc, dgamma, dbeta   ints: N, C, G, P, mode   floats: eps
-    need(9, 5, 1);
+    // ptrs: S, gamma, mean, rstd, ca, cb, cc, dgamma, dbeta, partial   ints: N, C, G, P, mode   floats: eps
+    need(10, 5, 1);
     const float* S = (const float*)vp(0);
     const float* gm = (const float*)vp(1);
     float *mu = (float*)vp(2), *rs = (float*)vp(3), *ca = (float*)vp(4), *cb = (float*)vp(5), *cc = (float*)vp(6);
     float *dg = (float*)vp(7), *db = (float*)vp(8);
     int n = I[0], c = I[1], g = I[2], np = I[3], mode = I[4];
+    float* pt = (float*)vp(9);
     float eps = (float)F[0];
     check_msg(norm_check(c, g));
-    return [=](hipStream_t s) { return A->gn_finalize_launch(S, n, c, g, np, mode, gm, eps, mu, rs, ca, cb, cc, dg, db, s); };
+    if (mode == 1 && !pt) throw std::invalid_argument("gn_finalize: partial workspace required");
+    return [=](hipStream_t s) {
+      return A->gn_finalize_launch(S, n, c, g, np, mode, gm, eps, mu, rs, ca, cb, cc, dg, db, pt, s);
+    };
   }
   if (kind == "norm_apply") {
     // ptrs: z, mean, rstd, gamma, beta, y   ints: N, P, C, cstride, relu, salt[, seed]   floats: drop_rate
@@ -439,6 +445,7 @@ PYBIND11_MODULE(_C, m) {
      py::arg("arena"), py::arg("stream"), py::arg("scalars") = 0, py::arg("dtype") = 0);
   m.def("head_blocks", &head_blocks_py);
   m.def("norm_blocks_per_sample", &norm_blocks_per_sample);
+  m.def("sample_slices", &sample_slices);
   m.def("wgrad_reduce_stage_floats", &wgrad_reduce_stage_floats);
   // QW > 0 describes a 2D 3x3 stride-1 'same' conv on QW-wide rows (row-window candidate)
   m.def(

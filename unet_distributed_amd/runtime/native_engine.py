@@ -303,7 +303,7 @@ class NativeUNet:
             P = self.npix(l.level) // self.B
             nbp = self.C.norm_blocks_per_sample(self.B, P)
             maxS = max(maxS, self.B * 2 * l.cout)
-            maxPart = max(maxPart, self.B * nbp * 2 * l.cout)
+            maxPart = max(maxPart, self.B * nbp * 2 * l.cout, self.C.sample_slices(self.B) * 2 * l.cout)
         self.norm_S = torch.zeros(maxS, dtype=f32, device=self.device)
         self.norm_part = torch.zeros(maxPart, dtype=f32, device=self.device)
 
@@ -321,14 +321,15 @@ class NativeUNet:
                 plan.add_generic("norm_moments", [_ptr(z), _ptr(z), _ptr(self.norm_part), _ptr(self.norm_S)],
                                  [N, P, C], [], "bnstat:" + l.name)
             plan.add_generic("bn_finalize", [_ptr(self.norm_S), gamma, _ptr(rm), _ptr(rv), _ptr(mean), _ptr(rstd),
-                                             0, 0, 0, 0, 0],
+                                             0, 0, 0, 0, 0, _ptr(self.norm_part)],
                              [N, C, 0 if train else 2], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM],
                              "bnfin:" + l.name)
             cstride = 0
         else:
             plan.add_generic("norm_moments", [_ptr(z), _ptr(z), _ptr(self.norm_part), _ptr(self.norm_S)],
                              [N, P, C], [], "gnstat:" + l.name)
-            plan.add_generic("gn_finalize", [_ptr(self.norm_S), gamma, _ptr(mean), _ptr(rstd), 0, 0, 0, 0, 0],
+            plan.add_generic("gn_finalize", [_ptr(self.norm_S), gamma, _ptr(mean), _ptr(rstd), 0, 0, 0, 0, 0,
+                                             _ptr(self.norm_part)],
                              [N, C, spec.groups, P, 0], [self.NORM_EPS], "gnfin:" + l.name)
             cstride = C
         plan.add_generic("norm_apply", [_ptr(z), _ptr(mean), _ptr(rstd), gamma, beta, _ptr(b[l.name])],
@@ -348,12 +349,12 @@ class NativeUNet:
                 "nstat_bwd:" + l.name)]
         if spec.norm == "batch":
             ops.append(("bn_finalize", [_ptr(self.norm_S), gamma, 0, 0, _ptr(mean), _ptr(rstd), _ptr(ca), _ptr(cb),
-                                        _ptr(cc), dgam, dbet],
+                                        _ptr(cc), dgam, dbet, _ptr(self.norm_part)],
                         [N, C, 1], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM], "bnfin_bwd:" + l.name))
             cstride = 0
         else:
             ops.append(("gn_finalize", [_ptr(self.norm_S), gamma, _ptr(mean), _ptr(rstd), _ptr(ca), _ptr(cb),
-                                        _ptr(cc), dgam, dbet],
+                                        _ptr(cc), dgam, dbet, _ptr(self.norm_part)],
                         [N, C, spec.groups, P, 1], [self.NORM_EPS], "gnfin_bwd:" + l.name))
             cstride = C
         ops.append(("norm_bwd_apply", [_ptr(g), _ptr(z), _ptr(ca), _ptr(cb), _ptr(cc), _ptr(dz)],
