@@ -42,7 +42,8 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp16"])
     p.add_argument("--bucket_mb", type=float, default=8.0)
     p.add_argument("--no_overlap", action="store_true")
-    p.add_argument("--hip_graph", type=int, default=0, help="replay the step as captured HIP graphs")
+    p.add_argument("--hip_graph", type=int, default=1,
+                   help="replay fwd / bwd segments / Adam as captured HIP graphs (0: eager launches)")
     p.add_argument("--profile_dir", default="")
     return p.parse_args()
 
