@@ -40,7 +40,23 @@ __host__ __device__ inline int conv_epi_mode(const ConvFwdParams& p) {
   return EPI_GENERIC;
 }
 
-template <int BM, int BN, int WM, int WN, int TM, int TN, int NTHR, int EPI = EPI_GENERIC>
+// Pixel-tile maps: window-relative first pixel of accumulator tile i of wave wm.
+// LinearTiles: a wave owns WM consecutive pixels.  StripTiles: a wave owns an RW-row x
+// (16 TC)-column strip of a row window of width W (column strips cs = wave % NCS, row
+// groups wave / NCS), tile i = (row i / TC, column tile i % TC).
+template <int WM>
+struct LinearTiles {
+  __device__ static int base(int wm, int i) { return wm * WM + i * 16; }
+};
+template <int W, int RW, int TC, int NCS>
+struct StripTiles {
+  __device__ static int base(int wave, int i) {
+    return ((wave / NCS) * RW + i / TC) * W + (wave % NCS) * 16 * TC + (i % TC) * 16;
+  }
+};
+
+template <int BM, int BN, int WM, int WN, int TM, int TN, int NTHR, int EPI = EPI_GENERIC,
+          class MapM = LinearTiles<WM>>
 __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc)[TM][TN], char* smem,
                                               const int m0, const int n0, const int M, const int wm,
                                               const int wn, const int lane, const int tid) {
@@ -72,7 +88,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int ml = wm * WM + i * 16 + (lane & 15);
+      const int ml = MapM::base(wm, i) + (lane & 15);
       const int q = m0 + ml;
       float v[4];
 #pragma unroll

@@ -343,17 +343,27 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
       __builtin_amdgcn_make_buffer_rsrc((void*)(p.src2 ? p.src2 : p.src1), (short)0, OOB, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
 
-  // wave w owns window pixels [WMP w, WMP (w + 1)): rows rw0 .. rw0 + WMP/W - 1
-  const int rw0 = (WMP * wave) / W;
-  uint32_t top_ok = 0, bot_ok = 0, live = 0;
+  // Wave w owns an RW-row x 16 TC-column strip of the window (StripTiles): an A
+  // fragment read from halo row r at horizontal shift dw feeds the output rows r - dh
+  // of all three vertical taps, so per chunk a wave reads 3 (RW + 2) TC fragments
+  // instead of 9 RW TC (2-2.4x less LDS read traffic than one fragment per tap).
+  constexpr int TC = W >= 128 ? 2 : 1;            // 16-pixel column tiles per strip
+  constexpr int NCS = W / (16 * TC);              // column strips per window row
+  constexpr int RW = R / (4 / NCS);               // rows per strip
+  static_assert(NCS <= 4 && 4 % NCS == 0 && RW * TC == TM, "strip map");
+  using Map = StripTiles<W, RW, TC, NCS>;
+  const int r0 = (wave / NCS) * RW, c0 = (wave % NCS) * 16 * TC;
+  // per strip row: does its top / bottom tap row lie in the same image?  Rows past the
+  // tensor need no mask (their halo rows load zeros and the epilogue drops them).
+  uint32_t top_ok = 0, bot_ok = 0;
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int g = g0 + rw0 + (i / TPR);
-    const int h = g % H;
-    if (g < rows_total) live |= 1u << i;
+  for (int i = 0; i < RW; ++i) {
+    const int h = (g0 + r0 + i) % H;
     if (h > 0) top_ok |= 1u << i;
     if (h < H - 1) bot_ok |= 1u << i;
   }
+  constexpr uint32_t ALL = (1u << RW) - 1u;
+  const bool interior = (top_ok & bot_ok) == ALL;   // wave-uniform: no image edge in the strip
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -362,14 +372,43 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int fsub = lane >> 4, fr = lane & 15;
-  // per-lane fragment bases: horizontal tap dw -> column fr + dw (+ the wave's first row)
+  // per-lane fragment bases: horizontal tap dw -> column c0 + fr + dw of halo row r0
+  // (c0 is a multiple of 16, so the swizzle only depends on fr + dw)
   int xbase[3];
 #pragma unroll
   for (int dw = 0; dw < 3; ++dw) {
     const int hc = fr + dw;
-    xbase[dw] = rw0 * ROWB + ((WMP * wave) % W) * 64 + hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3));
+    xbase[dw] = r0 * ROWB + c0 * 64 + hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3));
   }
   const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
+  // one 32-channel chunk: per horizontal tap, the three vertical taps' weights are
+  // held in registers and every halo-row fragment feeds up to three output rows
+  const bool guard = !interior;
+  auto chunk_mfmas = [&]() {
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw) {
+      h16x8 wf[3][TN];
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) wf[dh][j] = *(const h16x8*)(Ws + ((3 * dh + dw) * BN + 16 * j) * 64 + wbase);
+#pragma unroll
+      for (int hr = 0; hr < RW + 2; ++hr) {
+#pragma unroll
+        for (int ci = 0; ci < TC; ++ci) {
+          const h16x8 xf = *(const h16x8*)(Xs + xbase[dw] + hr * ROWB + ci * 16 * 64);
+#pragma unroll
+          for (int dh = 0; dh < 3; ++dh) {
+            const int ri = hr - dh;
+            if (ri < 0 || ri >= RW) continue;
+            if (guard && dh != 1 && !(((dh == 0 ? top_ok : bot_ok) >> ri) & 1u)) continue;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[ri * TC + ci][j] = mfma16(wf[dh][j], xf, acc[ri * TC + ci][j]);
+          }
+        }
+      }
+    }
+  };
   // LDS-DMA lane roles: lane l fills physical 16-byte chunk (l & 3) of slot (l >> 2) of a
   // 16-slot run; it loads logical chunk (l & 3) ^ swizzle(slot), which depends only on l
   // because every run starts at a multiple of 16 slots.
@@ -414,26 +453,10 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
       }
     }
     __syncthreads();
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int dh = t / 3, dw = t % 3;
-      h16x8 wf[TN];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) wf[j] = *(const h16x8*)(Ws + (t * BN + 16 * j) * 64 + wbase);
-      const uint32_t okm = (dh == 0 ? top_ok : (dh == 2 ? bot_ok : 0xffffffffu)) & live;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        if ((okm >> i) & 1u) {
-          const h16x8 xf =
-              *(const h16x8*)(Xs + xbase[dw] + ((i / TPR) + dh) * ROWB + (i % TPR) * 16 * 64);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[j], xf, acc[i][j]);
-        }
-      }
-    }
+    chunk_mfmas();
   }
   __syncthreads();
-  conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI>(p, acc, smem, m0, n0, M, wave, 0, lane, tid);
+  conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map>(p, acc, smem, m0, n0, M, wave, 0, lane, tid);
 }
 
 

@@ -595,6 +595,89 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
     }
     __syncthreads();
     const char* Yq = Ys + qo * (BMW * 64);
+    // (one column unit per wave: with two, the 128-wide QO = 2 case spills)
+    if constexpr (W >= 32 && W / 32 <= PS) {
+      // Column units: 32 pixels wide x RWG rows.  The dY fragments of the unit's rows
+      // stay in registers; each halo-row A fragment (row hr, shift dw) is read once
+      // and feeds the output rows hr - dh of all three vertical taps, so a unit reads
+      // 3 (RWG + 2) A fragment pairs instead of 9 RWG.
+      constexpr int NCOL = W / 32;
+      constexpr int RG = PS > NCOL ? PS / NCOL : 1;
+      constexpr int RWG = R / RG;
+      constexpr int UNITS = NCOL * RG;
+      static_assert(R % RG == 0 && RWG >= 1, "wgrad column units");
+      const int lp = 8 * G + q;
+#pragma unroll 1
+      for (int u = ps; u < UNITS; u += PS) {
+        const int cu = u % NCOL, rr0 = (u / NCOL) * RWG;
+        const int c0 = cu * 32;
+        uint32_t top_ok = 0, bot_ok = 0;
+#pragma unroll
+        for (int y = 0; y < RWG; ++y) {
+          const int h = (g0 + rr0 + y) % H;
+          if (h > 0) top_ok |= 1u << y;
+          if (h < H - 1) bot_ok |= 1u << y;
+        }
+        constexpr uint32_t ALL = (1u << RWG) - 1u;
+        const bool interior = (top_ok & bot_ok) == ALL;
+        // Per-lane LDS byte bases (the swizzle depends only on lp + dw because c0 and
+        // the row pitches are multiples of 32 slots): halo row hr and dY row y are
+        // compile-time immediates on top of these 16 registers.
+        int ab[3][2][2], yb[2][2];
+#pragma unroll
+        for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              const int col = c0 + dw + lp + 4 * hh;
+              ab[dw][i][hh] = tr_addr(rr0 * HWP + col, col, 16 * i + 4 * pp);
+            }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int sl = rr0 * W + c0 + lp + 4 * hh;
+            yb[j][hh] = tr_addr(sl, sl, 16 * j + 4 * pp);
+          }
+        const bool guard = !interior;
+        // dY fragments of the unit's rows, loaded when first needed (halo row hr = y
+        // feeds output row y through dh = 0) and live for three halo rows; pixels past
+        // the tensor were DMA'd as zeros
+        h16x8 bf[RWG][2];
+#pragma unroll
+        for (int hr = 0; hr < RWG + 2; ++hr) {
+          if (hr < RWG) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bf[hr][j] = tr8(Yq + yb[j][0] + hr * W * 64, Yq + yb[j][1] + hr * W * 64);
+            if (do_bias) {
+#pragma unroll
+              for (int j = 0; j < 2; ++j) bacc[j] = mfma16(ones, bf[hr][j], bacc[j]);
+            }
+          }
+#pragma unroll
+          for (int dw = 0; dw < 3; ++dw) {
+            h16x8 af[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[i] = tr8(Xs + ab[dw][i][0] + hr * ROWB, Xs + ab[dw][i][1] + hr * ROWB);
+#pragma unroll
+            for (int dh = 0; dh < 3; ++dh) {
+              const int y = hr - dh;
+              if (y < 0 || y >= RWG) continue;
+              if (guard && dh != 1 && !(((dh == 0 ? top_ok : bot_ok) >> y) & 1u)) continue;
+#pragma unroll
+              for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[3 * dh + dw][i][j] = mfma16(af[i], bf[y][j], acc[3 * dh + dw][i][j]);
+            }
+          }
+          // keep the scheduler from hoisting every row's fragment reads to the top
+          // (144 accumulator registers leave room for about one row of fragments)
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      continue;
+    }
 #pragma unroll 1
     for (int kk = ps; kk < KS; kk += PS) {
       const int px0 = kk * 32;
