@@ -91,13 +91,21 @@ def build(verbose=True, jobs=None):
     objs = [r[0] for r in results]
     rebuilt = any(r[1] for r in results)
     out = so_path()
-    if rebuilt or not os.path.exists(out) or any(
+    # the link manifest names the objects the current .so was built from: a cached
+    # object set that differs (e.g. after reverting a source) must be relinked even
+    # though no object is newer than the library
+    manifest = os.path.join(OBJDIR, "link_manifest.txt")
+    want = "\n".join(sorted(os.path.basename(o) for o in objs))
+    have = open(manifest).read() if os.path.exists(manifest) else ""
+    if rebuilt or not os.path.exists(out) or want != have or any(
             os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
         cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH] + objs + ["-o", out + ".tmp"]
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed: %s\n%s" % (" ".join(cmd), r.stdout))
         os.replace(out + ".tmp", out)
+        with open(manifest, "w") as f:
+            f.write(want)
         if verbose:
             print("built", out)
     elif verbose:
