@@ -353,17 +353,11 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   static_assert(NCS <= 4 && 4 % NCS == 0 && RW * TC == TM, "strip map");
   using Map = StripTiles<W, RW, TC, NCS>;
   const int r0 = (wave / NCS) * RW, c0 = (wave % NCS) * 16 * TC;
-  // per strip row: does its top / bottom tap row lie in the same image?  Rows past the
-  // tensor need no mask (their halo rows load zeros and the epilogue drops them).
-  uint32_t top_ok = 0, bot_ok = 0;
-#pragma unroll
-  for (int i = 0; i < RW; ++i) {
-    const int h = (g0 + r0 + i) % H;
-    if (h > 0) top_ok |= 1u << i;
-    if (h < H - 1) bot_ok |= 1u << i;
-  }
-  constexpr uint32_t ALL = (1u << RW) - 1u;
-  const bool interior = (top_ok & bot_ok) == ALL;   // wave-uniform: no image edge in the strip
+  // H % R == 0 (win_eligible): a window never spans two images, so the only rows of
+  // another image are the halo rows above / below it, which the DMA fills with zeros
+  // (the 'same' padding) -- the tap loop needs no image-edge branches at all, and the
+  // whole chunk is one basic block the scheduler can pipeline LDS reads through.
+  const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -383,7 +377,6 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
   // one 32-channel chunk: per horizontal tap, the three vertical taps' weights are
   // held in registers and every halo-row fragment feeds up to three output rows
-  const bool guard = !interior;
   auto chunk_mfmas = [&]() {
 #pragma unroll
     for (int dw = 0; dw < 3; ++dw) {
@@ -401,7 +394,6 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
           for (int dh = 0; dh < 3; ++dh) {
             const int ri = hr - dh;
             if (ri < 0 || ri >= RW) continue;
-            if (guard && dh != 1 && !(((dh == 0 ? top_ok : bot_ok) >> ri) & 1u)) continue;
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[ri * TC + ci][j] = mfma16(wf[dh][j], xf, acc[ri * TC + ci][j]);
           }
@@ -433,7 +425,8 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
           const int hr = k / IPR, j = k - hr * IPR;      // wave-uniform
           const int gr = g0 - 1 + hr;
           const int col = 16 * j + lslot - 1;
-          const bool ok = (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+          const bool row_in = (hr > 0 || top_in) && (hr < R + 1 || bot_in);   // same image
+          const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
           const int off = ok ? (gr * W + 16 * j) * C * 2 + lofs : OOB;
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
                                                    16, off, 0, 0, 0);
@@ -896,7 +889,8 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
 // source at full resolution, full rows of width 16..128).
 static bool win_eligible(const ConvFwdParams& p) {
   const bool w_ok = p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128;
-  return p.KD == 1 && p.OD == 1 && p.ID == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.pad == 1 &&
+  const int R = (p.OW == 16 ? 256 : 512) / (p.OW > 0 ? p.OW : 1);     // window rows
+  return w_ok && p.OH % R == 0 && p.KD == 1 && p.OD == 1 && p.ID == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.pad == 1 &&
          p.up1 == 1 && !p.shuffle && !p.stats && w_ok && p.IW == p.OW && p.IH == p.OH &&
          (p.C1 % 32) == 0 && (p.C2 % 32) == 0 && p.C1 > 0;
 }

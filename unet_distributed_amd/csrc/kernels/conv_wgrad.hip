@@ -566,8 +566,13 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
     return __builtin_bit_cast(h16x8, v);
   };
 
+  // column-unit path (below): the window never spans two images (H % R == 0,
+  // wgrad_win_eligible), so halo rows of a neighbouring image are DMA'd as zeros and
+  // its tap loop needs no image-edge branches
+  constexpr bool UNITS_PATH = W >= 32 && W / 32 <= PS;
   for (int win = w_begin; win < w_end; ++win) {
     const int g0 = win * R;
+    const bool top_in = !UNITS_PATH || (g0 % H) != 0, bot_in = !UNITS_PATH || ((g0 + R) % H) != 0;
     __syncthreads();   // the previous window's fragment reads are done
 #pragma unroll
     for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
@@ -576,7 +581,8 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
         const int hr = k / IPR, j = k - hr * IPR;
         const int gr = g0 - 1 + hr;
         const int col = 16 * j + lslot - 1;
-        const bool ok = (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+        const bool row_in = (hr > 0 || top_in) && (hr < R + 1 || bot_in);
+        const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
         const int off = ok ? (gr * W + 16 * j) * CA * 2 + xl : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
                                                  off, 0, 0, 0);
@@ -596,7 +602,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
     __syncthreads();
     const char* Yq = Ys + qo * (BMW * 64);
     // (one column unit per wave: with two, the 128-wide QO = 2 case spills)
-    if constexpr (W >= 32 && W / 32 <= PS) {
+    if constexpr (UNITS_PATH) {
       // Column units: 32 pixels wide x RWG rows.  The dY fragments of the unit's rows
       // stay in registers; each halo-row A fragment (row hr, shift dw) is read once
       // and feeds the output rows hr - dh of all three vertical taps, so a unit reads
@@ -611,15 +617,6 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
       for (int u = ps; u < UNITS; u += PS) {
         const int cu = u % NCOL, rr0 = (u / NCOL) * RWG;
         const int c0 = cu * 32;
-        uint32_t top_ok = 0, bot_ok = 0;
-#pragma unroll
-        for (int y = 0; y < RWG; ++y) {
-          const int h = (g0 + rr0 + y) % H;
-          if (h > 0) top_ok |= 1u << y;
-          if (h < H - 1) bot_ok |= 1u << y;
-        }
-        constexpr uint32_t ALL = (1u << RWG) - 1u;
-        const bool interior = (top_ok & bot_ok) == ALL;
         // Per-lane LDS byte bases (the swizzle depends only on lp + dw because c0 and
         // the row pitches are multiples of 32 slots): halo row hr and dY row y are
         // compile-time immediates on top of these 16 registers.
@@ -640,7 +637,6 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
             const int sl = rr0 * W + c0 + lp + 4 * hh;
             yb[j][hh] = tr_addr(sl, sl, 16 * j + 4 * pp);
           }
-        const bool guard = !interior;
         // dY fragments of the unit's rows, loaded when first needed (halo row hr = y
         // feeds output row y through dh = 0) and live for three halo rows; pixels past
         // the tensor were DMA'd as zeros
@@ -664,7 +660,6 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
             for (int dh = 0; dh < 3; ++dh) {
               const int y = hr - dh;
               if (y < 0 || y >= RWG) continue;
-              if (guard && dh != 1 && !(((dh == 0 ? top_ok : bot_ok) >> y) & 1u)) continue;
 #pragma unroll
               for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1118,7 +1113,9 @@ hipError_t launch_wgrad_win(const WgradParams& p, hipStream_t s) {
 // (p.win < 0 disables it for A/B tests).
 static bool wgrad_win_eligible(const WgradParams& p) {
   const bool w_ok = p.QW == 8 || p.QW == 16 || p.QW == 32 || p.QW == 64 || p.QW == 128;
-  return p.win >= 0 && w_ok && p.QD == 1 && p.KD == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 &&
+  // the column-unit path (W >= 32) needs windows (256 / W rows) that never span two images
+  const bool rows_ok = p.QW < 32 || p.QH % (256 / p.QW) == 0;
+  return p.win >= 0 && w_ok && rows_ok && p.QD == 1 && p.KD == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 &&
          p.pad == 1 && p.upA == 1 && p.AW == p.QW && p.AH == p.QH && (p.M1 % 32) == 0 && (p.M2 % 32) == 0 &&
          p.M1 > 0 && (p.Nc % 32) == 0 && p.bias_mode != 2;
 }
