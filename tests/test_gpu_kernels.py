@@ -142,6 +142,67 @@ def test_conv_row_window(cuda_dev, N, H, C1, C2, Cout, tile):
     assert rel_err(out, ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout", [(2, 8, 256, 32, 0, 32), (1, 4, 384, 32, 32, 32),
+                                               (2, 8, 512, 64, 0, 64), (1, 4, 256, 64, 64, 64)])
+def test_conv_row_window_segmented_rows(cuda_dev, N, H, W, C1, C2, Cout):
+    """Rows wider than 128 run as 128-wide segments whose halo columns are the
+    neighbouring segments' pixels (512x512 config levels)."""
+    torch.manual_seed(N + H + W + C1 + C2)
+    a = torch.randn(N, H, W, C1, device=cuda_dev).bfloat16()
+    b2 = torch.randn(N, H, W, max(C2, 1), device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, C1 + C2, Cout, device=cuda_dev) * 0.08).bfloat16()
+    bias = torch.randn(Cout, device=cuda_dev) * 0.1
+    out = torch.empty(N, H, W, Cout, device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(N=N, OH=H, OW=W, IH=H, IW=W, KH=3, KW=3, pad=1, C1=C1, C2=C2, src1=ptr(a),
+                      src2=ptr(b2) if C2 else None, wgt=ptr(pack_fwd(w)), bias=ptr(bias), Cout=Cout, relu=1,
+                      dst1=ptr(out), tile=6), stream())
+    xin = nchw(a.float()) if not C2 else torch.cat([nchw(a.float()), nchw(b2.float())], 1)
+    ref = nhwc(F.relu(F.conv2d(xin, w.float().permute(3, 2, 0, 1), bias, padding=1)))
+    assert rel_err(out, ref) < 1e-2
+
+
+def ncdhw(x):
+    return x.permute(0, 4, 1, 2, 3)
+
+
+def ndhwc(x):
+    return x.permute(0, 2, 3, 4, 1)
+
+
+@pytest.mark.parametrize("N,D,H,C1,C2,Cout", [(1, 4, 32, 32, 0, 32), (2, 3, 64, 32, 32, 32), (1, 2, 128, 64, 0, 64),
+                                               (1, 4, 16, 64, 64, 128)])
+def test_conv3d_row_window(cuda_dev, N, D, H, C1, C2, Cout):
+    """3x3x3 conv on the row-window kernel: three depth taps, each a 9-tap window pass over
+    the rows of slice d + dz - 1 (zero outside the volume); fwd + concat dgrad."""
+    torch.manual_seed(N + D + H + C1)
+    a = torch.randn(N, D, H, H, C1, device=cuda_dev).bfloat16()
+    b2 = torch.randn(N, D, H, H, max(C2, 1), device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, 3, C1 + C2, Cout, device=cuda_dev) * 0.05).bfloat16()
+    bias = torch.randn(Cout, device=cuda_dev) * 0.1
+    out = torch.empty(N, D, H, H, Cout, device=cuda_dev, dtype=torch.bfloat16)
+    wp = pad64(w.permute(4, 0, 1, 2, 3).reshape(Cout, -1))
+    geo = dict(N=N, OD=D, OH=H, OW=H, ID=D, IH=H, IW=H, KD=3, KH=3, KW=3, pad=1)
+    C().conv_fwd(dict(geo, C1=C1, C2=C2, src1=ptr(a), src2=ptr(b2) if C2 else None, wgt=ptr(wp), bias=ptr(bias),
+                      Cout=Cout, relu=1, dst1=ptr(out), tile=6), stream())
+    xin = ncdhw(a.float()) if not C2 else torch.cat([ncdhw(a.float()), ncdhw(b2.float())], 1)
+    wt = w.float().permute(4, 3, 0, 1, 2)
+    ref = ndhwc(F.relu(F.conv3d(xin, wt, bias, padding=1)))
+    assert rel_err(out, ref) < 1e-2
+    # dgrad: flipped taps, weights [ci][tap][co], split destinations, ReLU mask on src2
+    dy = torch.randn(N, D, H, H, Cout, device=cuda_dev).bfloat16()
+    wdg = pad64(w.flip(0, 1, 2).permute(3, 0, 1, 2, 4).reshape(C1 + C2, -1))
+    d1 = torch.empty(N, D, H, H, C1, device=cuda_dev, dtype=torch.bfloat16)
+    d2 = torch.empty(N, D, H, H, max(C2, 1), device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(geo, C1=Cout, src1=ptr(dy), wgt=ptr(wdg), Cout=C1 + C2, D1=C1, dst1=ptr(d1),
+                      dst2=ptr(d2) if C2 else None, mask2=ptr(b2) if C2 else None, tile=6), stream())
+    xr = torch.zeros(N, C1 + C2, D, H, H, device=cuda_dev, requires_grad=True)
+    (g,) = torch.autograd.grad(F.conv3d(xr, wt, padding=1), xr, ncdhw(dy.float()))
+    g = ndhwc(g)
+    assert rel_err(d1, g[..., :C1]) < 1e-2
+    if C2:
+        assert rel_err(d2, g[..., C1:] * (b2.float() > 0)) < 1e-2
+
+
 def test_conv_row_window_dgrad_dual_dest_mask_dropout(cuda_dev):
     """The row-window kernel as a concat dgrad (flipped weights, two destinations,
     ReLU mask + dropout rescale) at the 128-wide level."""
@@ -266,6 +327,48 @@ def test_wgrad_row_window(cuda_dev, N, H, C1, C2, Cout, splits, win):
     bb = torch.zeros(Cout, device=cuda_dev, requires_grad=True)
     gwr, gbr = torch.autograd.grad(F.conv2d(inp, w, bb, padding=1), [w, bb], nchw(dy.float()))
     assert rel_err(gw, gwr.permute(2, 3, 1, 0).reshape(-1)) < 2e-3
+    assert rel_err(gb, gbr) < 2e-3
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout,splits", [(2, 4, 256, 32, 0, 32, 3), (1, 6, 384, 32, 32, 32, 4),
+                                                      (2, 4, 512, 64, 0, 64, 5), (1, 4, 256, 64, 64, 64, 2)])
+def test_wgrad_row_window_segmented_rows(cuda_dev, N, H, W, C1, C2, Cout, splits):
+    """Window wgrad on rows wider than 128 (128-wide segments, neighbour halo columns)."""
+    torch.manual_seed(N + H + W + C1 + C2)
+    a = F.relu(torch.randn(N, H, W, C1, device=cuda_dev)).bfloat16()
+    b2 = F.relu(torch.randn(N, H, W, max(C2, 1), device=cuda_dev)).bfloat16()
+    dy = torch.randn(N, H, W, Cout, device=cuda_dev).bfloat16()
+    Mt = C1 + C2
+    assert C().wgrad_pick(C1, C2, Cout, 9, QW=W, QH=H, win=0)[2] == 9      # window tile picked
+    d = dict(N=N, QH=H, QW=W, AH=H, AW=W, KH=3, KW=3, pad=1, M1=C1, M2=C2, a1=ptr(a),
+             a2=ptr(b2) if C2 else None, b=ptr(dy), Nc=Cout, bias_mode=1)
+    gw, gb = _wgrad(d, splits, 9, Mt, Mt, Cout, 9 * Mt * Cout, bias_w=(splits, Cout))
+    inp = nchw(a.float()) if not C2 else torch.cat([nchw(a.float()), nchw(b2.float())], 1)
+    w = torch.zeros(Cout, Mt, 3, 3, device=cuda_dev, requires_grad=True)
+    bb = torch.zeros(Cout, device=cuda_dev, requires_grad=True)
+    gwr, gbr = torch.autograd.grad(F.conv2d(inp, w, bb, padding=1), [w, bb], nchw(dy.float()))
+    assert rel_err(gw, gwr.permute(2, 3, 1, 0).reshape(-1)) < 2e-3
+    assert rel_err(gb, gbr) < 2e-3
+
+
+@pytest.mark.parametrize("N,D,H,C1,C2,Cout,splits", [(1, 4, 32, 32, 0, 32, 3), (2, 3, 64, 32, 32, 32, 5),
+                                                      (1, 2, 128, 64, 0, 64, 2), (1, 4, 32, 64, 64, 128, 7)])
+def test_wgrad3d_row_window(cuda_dev, N, D, H, C1, C2, Cout, splits):
+    """3x3x3 wgrad on the window kernel: one tap group per depth tap (27-tap slab)."""
+    torch.manual_seed(N + D + H + C1 + C2)
+    a = F.relu(torch.randn(N, D, H, H, C1, device=cuda_dev)).bfloat16()
+    b2 = F.relu(torch.randn(N, D, H, H, max(C2, 1), device=cuda_dev)).bfloat16()
+    dy = torch.randn(N, D, H, H, Cout, device=cuda_dev).bfloat16()
+    Mt = C1 + C2
+    assert C().wgrad_pick(C1, C2, Cout, 27, QW=H, QH=H, QD=D, win=0)[2] == 9
+    d = dict(N=N, QD=D, QH=H, QW=H, AD=D, AH=H, AW=H, KD=3, KH=3, KW=3, pad=1, M1=C1, M2=C2, a1=ptr(a),
+             a2=ptr(b2) if C2 else None, b=ptr(dy), Nc=Cout, bias_mode=1)
+    gw, gb = _wgrad(d, splits, 27, Mt, Mt, Cout, 27 * Mt * Cout, bias_w=(splits, Cout))
+    inp = ncdhw(a.float()) if not C2 else torch.cat([ncdhw(a.float()), ncdhw(b2.float())], 1)
+    w = torch.zeros(Cout, Mt, 3, 3, 3, device=cuda_dev, requires_grad=True)
+    bb = torch.zeros(Cout, device=cuda_dev, requires_grad=True)
+    gwr, gbr = torch.autograd.grad(F.conv3d(inp, w, bb, padding=1), [w, bb], ncdhw(dy.float()))
+    assert rel_err(gw, gwr.permute(2, 3, 4, 1, 0).reshape(-1)) < 2e-3
     assert rel_err(gb, gbr) < 2e-3
 
 

@@ -55,11 +55,20 @@ struct StripTiles {
   }
 };
 
+// SEGW > 0: the tile is a row window of SEGW-wide row segments (window kernels on rows
+// wider than one window, or any row-window kernel): tile pixel ml is at row
+// m0 + ml / SEGW (m0 = first row), column col0 + ml % SEGW of rows `pitch` pixels wide.
+// SEGW == 0: tile pixel ml is output pixel m0 + ml.
 template <int BM, int BN, int WM, int WN, int TM, int TN, int NTHR, int EPI = EPI_GENERIC,
-          class MapM = LinearTiles<WM>>
+          class MapM = LinearTiles<WM>, int SEGW = 0>
 __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc)[TM][TN], char* smem,
                                               const int m0, const int n0, const int M, const int wm,
-                                              const int wn, const int lane, const int tid) {
+                                              const int wn, const int lane, const int tid,
+                                              const int pitch = 0, const int col0 = 0) {
+  auto qof = [&](int ml) -> int {
+    if constexpr (SEGW > 0) return (m0 + ml / SEGW) * pitch + col0 + (ml % SEGW);
+    else return m0 + ml;
+  };
   constexpr int EPI_STRIDE = (BN + 4) * 2;          // bytes; 8B-aligned, conflict-free b64 writes
   // register phase: acc[i][j][r] = out[pixel = m0 + wm*WM + i*16 + (lane&15)]
   //                                   [chan  = n0 + wn*WN + j*16 + (lane>>4)*4 + r]
@@ -89,7 +98,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int ml = MapM::base(wm, i) + (lane & 15);
-      const int q = m0 + ml;
+      const int q = qof(ml);
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -151,14 +160,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     if (mk) {
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
-        const int q = m0 + ml0 + it * RPI;
+        const int q = qof(ml0 + it * RPI);
         if (q < M) mv[it] = *(const u32x4*)(mk + (size_t)q * rs + co);
       }
     }
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int ml = ml0 + it * RPI;
-      const int q = m0 + ml;
+      const int q = qof(ml);
       if (q >= M) continue;
       const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
       const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
@@ -181,7 +190,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
 #pragma unroll 2
   for (int c = tid; c < NCHUNK; c += NTHR) {
     const int ml = c / CPR, cb = c % CPR;
-    const int q = m0 + ml;
+    const int q = qof(ml);
     if (q >= M) continue;
     const int n = n0 + cb * 8;
     const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);

@@ -305,7 +305,11 @@ hipError_t launch_cfg(const ConvFwdParams& p, hipStream_t s) {
 // swizzle depends only on the column, a lane's address is one of three per-lane bases
 // (one per horizontal tap) plus a compile-time immediate (row, tile) -- no per-tap
 // address registers.  Weight rows (tap, n) use the same swizzle on the row index.
-template <int W, int BN, bool CONCAT, int EPI>
+// GEO: 0 = 2D full rows (Wf = W), 1 = 2D segmented rows (Wf = p.OW, a multiple of W),
+// 2 = 3D full rows (three depth taps).  Compile-time so the common 2D case carries no
+// segment / depth state (extra SGPR state spilled to VGPR lanes inside the chunk loop).
+enum { GEO_2D = 0, GEO_SEG = 1, GEO_3D = 2 };
+template <int W, int BN, bool CONCAT, int EPI, int GEO>
 __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   static_assert(BN == 32 || BN == 64, "row-window tile is 32 or 64 output channels wide");
   constexpr int BM = W == 16 ? 256 : 512;       // window pixels (16-wide rows: 16 rows)
@@ -327,14 +331,24 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
 
   // wave index as a scalar: every per-wave quantity below (rows, DMA slots) stays in SGPRs
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // Row space: rows g = (n, d, h) of Wf pixels.  Rows wider than 128 are cut into
+  // nseg W-wide segments (a window = R rows x one segment; its halo columns -1 / W are
+  // the neighbouring segments' pixels).  3D (KD = 3): depth tap dz reads the halo rows
+  // of slice d + dz - 1, i.e. row g + (dz - 1) H, as three more 32-channel K chunks.
+  constexpr int KD = GEO == GEO_3D ? 3 : 1;
   const int H = p.OH;
-  const int rows_total = p.N * H;
-  const int M = rows_total * W;
+  const int D = GEO == GEO_3D ? p.OD : 1;
+  const int Wf = GEO == GEO_SEG ? p.OW : W;
+  const int nseg = GEO == GEO_SEG ? p.OW / W : 1;
+  const int rows_total = p.N * D * H;
+  const int M = rows_total * Wf;
   const int tiles_n = p.Cout / BN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = bid / tiles_n, tn = bid % tiles_n;
-  const int g0 = tm * R;
-  const int m0 = g0 * W, n0 = tn * BN;
+  const int rgi = GEO == GEO_SEG ? tm / nseg : tm;
+  const int g0 = rgi * R, col0 = GEO == GEO_SEG ? (tm - rgi * nseg) * W : 0;
+  const int n0 = tn * BN;
+  const int dsl = GEO == GEO_3D ? (g0 / H) % D : 0;   // depth slice of the window
   const int Cin = p.C1 + p.C2;
   const int nchunks = Cin >> 5;
   constexpr int OOB = 0x7fffffff;
@@ -407,49 +421,110 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   const int lslot = lane >> 2;
   const int lchunk = (lane & 3) ^ ((lslot >> 1) & 3);
 
-  for (int kc = 0; kc < nchunks; ++kc) {
-    const bool from1 = !CONCAT || (kc << 5) < p.C1;
-    const int C = from1 ? p.C1 : p.C2;
-    const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
-    if (kc) __syncthreads();   // previous chunk's fragment reads are done
-    {
-      // halo image: row hr, slot hc holds pixel (g0 - 1 + hr, hc - 1); instruction
-      // (hr, j) covers slots 16j .. 16j + 15 of row hr.  Rows outside the tensor and
-      // columns outside [0, W) load zeros (out-of-range offsets).
-      const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
-      const int lofs = ((lslot - 1) * C + cb + lchunk * 8) * 2;
+  // one 32-channel chunk of depth tap kd (input rows shifted by gsh): stage, then MFMAs
+  auto run_chunk = [&](const int kc, const int kd, const int gsh) {
+      const bool from1 = !CONCAT || (kc << 5) < p.C1;
+      const int C = from1 ? p.C1 : p.C2;
+      const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
+      {
+        // halo image: row hr, slot hc holds pixel (g0 - 1 + hr + gsh, col0 + hc - 1);
+        // instruction (hr, j) covers slots 16j .. 16j + 15 of row hr.  Rows outside the
+        // tensor / image and columns outside [0, Wf) load zeros (out-of-range offsets).
+        const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
+        const int lofs = ((lslot - 1) * C + cb + lchunk * 8) * 2;
 #pragma unroll
-      for (int q = 0; q < (XI + 3) / 4; ++q) {
-        const int k = wave + 4 * q;
-        if (k < XI) {
-          const int hr = k / IPR, j = k - hr * IPR;      // wave-uniform
-          const int gr = g0 - 1 + hr;
-          const int col = 16 * j + lslot - 1;
-          const bool row_in = (hr > 0 || top_in) && (hr < R + 1 || bot_in);   // same image
-          const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
-          const int off = ok ? (gr * W + 16 * j) * C * 2 + lofs : OOB;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
-                                                   16, off, 0, 0, 0);
+        for (int q = 0; q < (XI + 3) / 4; ++q) {
+          const int k = wave + 4 * q;
+          if (k < XI) {
+            const int hr = k / IPR, j = k - hr * IPR;      // wave-uniform
+            const int gr = g0 - 1 + hr + gsh;
+            const int col = col0 + 16 * j + lslot - 1;
+            const bool row_in = (hr > 0 || top_in) && (hr < R + 1 || bot_in);   // same image
+            // (slots past W + 1 are never read: skip them, they would be real pixels of
+            // the next segment on segmented rows)
+            const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)Wf &&
+                            (GEO != GEO_SEG || 16 * j + lslot <= W + 1);
+            const int off = ok ? (gr * Wf + col0 + 16 * j) * C * 2 + lofs : OOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
+                                                     16, off, 0, 0, 0);
+          }
+        }
+        // weight image: row r = tap * 32 + n (64 bytes = this chunk's 32 input channels)
+        const int wl = (lslot * p.Kpad + (kc << 5) + lchunk * 8) * 2;
+#pragma unroll
+        for (int q = 0; q < (WI + 3) / 4; ++q) {
+          const int k = wave + 4 * q;
+          if (k < WI) {
+            const int tap = k / (BN / 16), nb = (k % (BN / 16)) * 16;     // wave-uniform
+            const int off = ((n0 + nb) * p.Kpad + (kd * 9 + tap) * Cin) * 2 + wl;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024),
+                                                     16, off, 0, 0, 0);
+          }
         }
       }
-      // weight image: row r = tap * 32 + n (64 bytes = this chunk's 32 input channels)
-      const int wl = (lslot * p.Kpad + (kc << 5) + lchunk * 8) * 2;
-#pragma unroll
-      for (int q = 0; q < (WI + 3) / 4; ++q) {
-        const int k = wave + 4 * q;
-        if (k < WI) {
-          const int tap = k / (BN / 16), nb = (k % (BN / 16)) * 16;     // wave-uniform
-          const int off = ((n0 + nb) * p.Kpad + tap * Cin) * 2 + wl;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024),
-                                                   16, off, 0, 0, 0);
-        }
+      __syncthreads();
+      chunk_mfmas();
+  };
+  if constexpr (GEO == GEO_3D) {
+    // depth taps whose input slice is padding contribute nothing: skip them
+    const int kd_lo = dsl == 0 ? 1 : 0, kd_hi = dsl == D - 1 ? 2 : 3;
+    for (int kd = kd_lo; kd < kd_hi; ++kd)
+      for (int kc = 0; kc < nchunks; ++kc) {
+        if (kc || kd != kd_lo) __syncthreads();   // previous chunk's fragment reads are done
+        run_chunk(kc, kd, (kd - 1) * H);
       }
+  } else if constexpr (GEO == GEO_SEG) {
+    for (int kc = 0; kc < nchunks; ++kc) {
+      if (kc) __syncthreads();                    // previous chunk's fragment reads are done
+      run_chunk(kc, 0, 0);
     }
-    __syncthreads();
-    chunk_mfmas();
+  } else {
+    // 2D full rows: the same staging with compile-time row pitch and no segment / depth
+    // offsets, spelled out (through run_chunk the scheduler keeps ~100 more scalar
+    // instructions per chunk and spills SGPRs to VGPR lanes: 2-4 % slower, A/B measured)
+    for (int kc = 0; kc < nchunks; ++kc) {
+      const bool from1 = !CONCAT || (kc << 5) < p.C1;
+      const int C = from1 ? p.C1 : p.C2;
+      const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
+      if (kc) __syncthreads();
+      {
+        const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
+        const int lofs = ((lslot - 1) * C + cb + lchunk * 8) * 2;
+#pragma unroll
+        for (int q = 0; q < (XI + 3) / 4; ++q) {
+          const int k = wave + 4 * q;
+          if (k < XI) {
+            const int hr = k / IPR, j = k - hr * IPR;
+            const int gr = g0 - 1 + hr;
+            const int col = 16 * j + lslot - 1;
+            const bool row_in = (hr > 0 || top_in) && (hr < R + 1 || bot_in);
+            const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+            const int off = ok ? (gr * W + 16 * j) * C * 2 + lofs : OOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
+                                                     16, off, 0, 0, 0);
+          }
+        }
+        const int wl = (lslot * p.Kpad + (kc << 5) + lchunk * 8) * 2;
+#pragma unroll
+        for (int q = 0; q < (WI + 3) / 4; ++q) {
+          const int k = wave + 4 * q;
+          if (k < WI) {
+            const int tap = k / (BN / 16), nb = (k % (BN / 16)) * 16;
+            const int off = ((n0 + nb) * p.Kpad + tap * Cin) * 2 + wl;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024),
+                                                     16, off, 0, 0, 0);
+          }
+        }
+      }
+      __syncthreads();
+      chunk_mfmas();
+    }
   }
   __syncthreads();
-  conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map>(p, acc, smem, m0, n0, M, wave, 0, lane, tid);
+  if constexpr (GEO == GEO_SEG)
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, W>(p, acc, smem, g0, n0, M, wave, 0, lane, tid, Wf, col0);
+  else
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid);
 }
 
 
@@ -849,27 +924,42 @@ hipError_t launch_tconv_dgrad(const ConvFwdParams& p, hipStream_t s) {
 
 template <int BN>
 hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
-  const int W = p.OW;
-  const int rows = p.N * p.OH;
+  const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
+  const int rows = p.N * p.OD * p.OH;
   const int R = (W == 16 ? 256 : 512) / W;
-  const int grid = ((rows + R - 1) / R) * (p.Cout / BN);
+  const int grid = ((rows + R - 1) / R) * (p.OW / W) * (p.Cout / BN);
   const bool cc = p.C2 > 0;
   const int epi = conv_epi_mode(p);
-#define WIN_EPI(WW, CC)                                                                                   \
+  const int geo = p.KD == 3 ? GEO_3D : (p.OW > W ? GEO_SEG : GEO_2D);
+#define WIN_EPI(WW, CC, GG)                                                                               \
   if (epi == EPI_FWD)                                                                                     \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p);         \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_FWD, GG>), dim3(grid), dim3(NTHR), 0, s, p);     \
   else if (epi == EPI_DGRAD)                                                                              \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_DGRAD>), dim3(grid), dim3(NTHR), 0, s, p);       \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_DGRAD, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
   else                                                                                                    \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p);
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_GENERIC, GG>), dim3(grid), dim3(NTHR), 0, s, p);
+#define WIN_GEO(WW, CC)                                                                                   \
+  if (geo == GEO_3D) {                                                                                    \
+    WIN_EPI(WW, CC, GEO_3D)                                                                               \
+  } else {                                                                                                \
+    WIN_EPI(WW, CC, GEO_2D)                                                                               \
+  }
 #define WIN_CASE(WW)                                                                                      \
   case WW:                                                                                                \
     if (cc) {                                                                                             \
-      WIN_EPI(WW, true)                                                                                   \
+      WIN_GEO(WW, true)                                                                                   \
     } else {                                                                                              \
-      WIN_EPI(WW, false)                                                                                  \
+      WIN_GEO(WW, false)                                                                                  \
     }                                                                                                     \
     break;
+  if (geo == GEO_SEG) {                 // 3D volumes wider than 128 are not window-eligible
+    if (cc) {
+      WIN_EPI(128, true, GEO_SEG)
+    } else {
+      WIN_EPI(128, false, GEO_SEG)
+    }
+    return hipGetLastError();
+  }
   switch (W) {
     WIN_CASE(16)
     WIN_CASE(32)
@@ -879,19 +969,23 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
       return hipErrorInvalidValue;
   }
 #undef WIN_CASE
+#undef WIN_GEO
 #undef WIN_EPI
   return hipGetLastError();
 }
 
 }  // namespace
 
-// True when the row-window kernel can run this conv (2D, 3x3 s1 p1, plain / concat
-// source at full resolution, full rows of width 16..128).
+// True when the row-window kernel can run this conv: 3x3 (2D) or 3x3x3 (3D) stride 1
+// 'same', plain / concat source at full resolution, rows 16..128 wide or a multiple of
+// 128 (cut into 128-wide segments).
 static bool win_eligible(const ConvFwdParams& p) {
-  const bool w_ok = p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128;
-  const int R = (p.OW == 16 ? 256 : 512) / (p.OW > 0 ? p.OW : 1);     // window rows
-  return w_ok && p.OH % R == 0 && p.KD == 1 && p.OD == 1 && p.ID == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.pad == 1 &&
-         p.up1 == 1 && !p.shuffle && !p.stats && w_ok && p.IW == p.OW && p.IH == p.OH &&
+  const bool w_ok = p.OW == 16 || p.OW == 32 || p.OW == 64 || (p.OW % 128 == 0 && p.OW > 0 && p.OW <= 8192);
+  const int W = p.OW > 128 ? 128 : (p.OW > 0 ? p.OW : 1);
+  const int R = (W == 16 ? 256 : 512) / W;     // window rows
+  const bool dims_ok = (p.KD == 1 && p.OD == 1 && p.ID == 1) || (p.KD == 3 && p.OD == p.ID && p.OD > 1 && p.OW <= 128);
+  return w_ok && p.OH % R == 0 && dims_ok && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.pad == 1 &&
+         p.up1 == 1 && !p.shuffle && !p.stats && p.IW == p.OW && p.IH == p.OH &&
          (p.C1 % 32) == 0 && (p.C2 % 32) == 0 && p.C1 > 0;
 }
 

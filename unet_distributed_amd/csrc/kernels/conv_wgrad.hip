@@ -499,7 +499,10 @@ hipError_t launch_wg(WgradParams p, hipStream_t s) {
 // Images: 64-byte pixel slots; 16-byte chunk c of the slot in column col is stored at
 // c ^ (((col >> 3) & 1) << 1), which makes the transposed fragment reads conflict free
 // (tools/lds_bank_model.py) and depends only on col mod 16 (DMA lane roles fixed).
-template <int W, int QO, bool CONCAT>
+// GEO: 0 = 2D full rows, 1 = 2D segmented rows (Wf = p.QW > W), 2 = 3D (tap group =
+// depth tap); compile-time so the 2D full-row kernel carries no segment / depth state.
+enum { WGEO_2D = 0, WGEO_SEG = 1, WGEO_3D = 2 };
+template <int W, int QO, bool CONCAT, int GEO>
 __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p) {
   constexpr int BMW = 256, R = BMW / W, HR = R + 2;
   constexpr int HWP = ((W + 2 + 15) / 16) * 16, IPR = HWP / 16, ROWB = HWP * 64;
@@ -515,14 +518,24 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int qo = wave % QO, ps = wave / QO;
+  // Row space g = (n, d, h), rows of Wf pixels cut into nseg W-wide segments (Wf > 128);
+  // a window is R rows x one segment.  3D: tap group kd (grid dimension) computes the
+  // nine (dh, dw) taps of depth tap kd from the halo rows of slice d + kd - 1.
+  constexpr int KD = GEO == WGEO_3D ? 3 : 1;
   const int H = p.QH;
-  const int rows_total = p.N * H;
-  const int Mq = rows_total * W;
-  const int nwin = (rows_total + R - 1) / R;
+  const int D = GEO == WGEO_3D ? p.QD : 1;
+  const int Wf = GEO == WGEO_SEG ? p.QW : W;
+  const int nseg = GEO == WGEO_SEG ? p.QW / W : 1;
+  const int rows_total = p.N * D * H;
+  const int Mq = rows_total * Wf;
+  const int nwin = ((rows_total + R - 1) / R) * nseg;
   const int Mtot = p.M1 + p.M2;
   const int cob = p.Nc / (32 * QO);
-  const int ntile = (Mtot / 32) * cob;
-  const int split = blockIdx.x / ntile, tile = blockIdx.x - split * ntile;
+  const int ntile = (Mtot / 32) * cob * KD;
+  const int split = blockIdx.x / ntile;
+  int tile = blockIdx.x - split * ntile;
+  const int kd = tile % KD;
+  tile /= KD;
   const int ci_blk = tile / cob, co_blk = tile - ci_blk * cob;
   const int ci0 = ci_blk * 32, co0 = co_blk * 32 * QO;
   const bool from1 = !CONCAT || ci0 < p.M1;
@@ -533,7 +546,9 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, OOB, 0x00020000);
   const int w_begin = (int)((long long)split * nwin / p.splits);
   const int w_end = (int)((long long)(split + 1) * nwin / p.splits);
-  const bool do_bias = p.bias_mode == 1 && ci_blk == 0;
+  // bias: once per output-channel block, by the centre depth tap (it sees every window)
+  const bool do_bias = p.bias_mode == 1 && ci_blk == 0 && kd == (KD >> 1);
+  const int gsh = (kd - (KD >> 1)) * H;
 
   f32x4 acc[9][2][2];
 #pragma unroll
@@ -571,7 +586,11 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   // its tap loop needs no image-edge branches
   constexpr bool UNITS_PATH = W >= 32 && W / 32 <= PS;
   for (int win = w_begin; win < w_end; ++win) {
-    const int g0 = win * R;
+    const int g0 = (GEO == WGEO_SEG ? win / nseg : win) * R;
+    const int col0 = GEO == WGEO_SEG ? (win % nseg) * W : 0;
+    // 3D: a window lies in one (n, d) slice (H % R == 0); its depth-shifted input slice
+    // is padding -> the window contributes nothing to this tap group (uniform skip)
+    if (GEO == WGEO_3D && (unsigned)((g0 / H) % D + kd - 1) >= (unsigned)D) continue;
     const bool top_in = !UNITS_PATH || (g0 % H) != 0, bot_in = !UNITS_PATH || ((g0 + R) % H) != 0;
     __syncthreads();   // the previous window's fragment reads are done
 #pragma unroll
@@ -579,11 +598,12 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
       const int k = wave + 4 * qq;
       if (k < XI) {
         const int hr = k / IPR, j = k - hr * IPR;
-        const int gr = g0 - 1 + hr;
-        const int col = 16 * j + lslot - 1;
+        const int gr = g0 - 1 + hr + gsh;
+        const int col = col0 + 16 * j + lslot - 1;
         const bool row_in = (hr > 0 || top_in) && (hr < R + 1 || bot_in);
-        const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
-        const int off = ok ? (gr * W + 16 * j) * CA * 2 + xl : OOB;
+        const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)Wf &&
+                        (GEO != WGEO_SEG || 16 * j + lslot <= W + 1);
+        const int off = ok ? (gr * Wf + col0 + 16 * j) * CA * 2 + xl : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
                                                  off, 0, 0, 0);
       }
@@ -593,7 +613,9 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
       const int k = wave + 4 * qq;
       if (k < YI) {
         const int o = k / (BMW / 16), sb = (k - o * (BMW / 16)) * 16;   // image o, first slot
-        const int pix = g0 * W + sb;
+        // window slot sb -> row g0 + sb / W, column col0 + sb % W (W = 8: one segment,
+        // the 16-slot run covers two consecutive rows contiguous in memory)
+        const int pix = GEO == WGEO_SEG ? (g0 + sb / W) * Wf + col0 + sb % W : g0 * W + sb;
         const int off = (pix + lslot < Mq) ? (pix * p.Nc + 32 * o) * 2 + yl : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (__attribute__((address_space(3))) void*)(Ys + k * 1024), 16,
                                                  off, 0, 0, 0);
@@ -739,7 +761,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
 #pragma unroll
           for (int o = 1; o < PS; ++o) v += *(const f32x4*)(red + ((qo + QO * o) * 64 + lane) * 16 + (i * 2 + j) * 4);
           if (t < 9) {
-            float* dst = p.slab + (((size_t)split * 9 + t) * Mtot + m_base + 16 * i) * p.Nc + n_base + 16 * j;
+            float* dst = p.slab + (((size_t)split * 9 * KD + 9 * kd + t) * Mtot + m_base + 16 * i) * p.Nc + n_base + 16 * j;
 #pragma unroll
             for (int r = 0; r < 4; ++r) dst[(size_t)r * p.Nc] = v[r];
           } else if (i == 0 && lane < 16) {
@@ -1097,25 +1119,44 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
   }
 }
 
+template <int W, int QO, int GEO>
+hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
+  const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.KD * p.splits;
+  if (p.M2 > 0)
+    hipLaunchKernelGGL((wgrad_win_kernel<W, QO, true, GEO>), dim3(grid), dim3(NTHR), 0, s, p);
+  else
+    hipLaunchKernelGGL((wgrad_win_kernel<W, QO, false, GEO>), dim3(grid), dim3(NTHR), 0, s, p);
+  return hipGetLastError();
+}
+
 template <int W, int QO>
 hipError_t launch_wgrad_win(const WgradParams& p, hipStream_t s) {
-  const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.splits;
-  if (p.M2 > 0)
-    hipLaunchKernelGGL((wgrad_win_kernel<W, QO, true>), dim3(grid), dim3(NTHR), 0, s, p);
-  else
-    hipLaunchKernelGGL((wgrad_win_kernel<W, QO, false>), dim3(grid), dim3(NTHR), 0, s, p);
-  return hipGetLastError();
+  if (p.KD == 3) {
+    if constexpr (W >= 32) return launch_wgrad_win_g<W, QO, WGEO_3D>(p, s);
+    return hipErrorInvalidValue;          // (not eligible: 3D needs the column-unit rows)
+  }
+  if (p.QW > W) {
+    if constexpr (W == 128) return launch_wgrad_win_g<W, QO, WGEO_SEG>(p, s);
+    return hipErrorInvalidValue;
+  }
+  return launch_wgrad_win_g<W, QO, WGEO_2D>(p, s);
 }
 
 }  // namespace
 
 // Row-window wgrad applies to 2D 3x3 stride-1 'same' convs on full rows 8..128 wide
 // (p.win < 0 disables it for A/B tests).
+// Rows wider than 128 (a multiple of 128) are cut into 128-wide segments; 3D 3x3x3 runs
+// one tap group per depth tap on rows >= 32 wide (column-unit path: windows never span
+// two (n, d) slices, so the depth padding is a per-window skip).
 static bool wgrad_win_eligible(const WgradParams& p) {
-  const bool w_ok = p.QW == 8 || p.QW == 16 || p.QW == 32 || p.QW == 64 || p.QW == 128;
+  const bool w_ok = p.QW == 8 || p.QW == 16 || p.QW == 32 || p.QW == 64 ||
+                    (p.QW % 128 == 0 && p.QW > 0 && p.QW <= 8192);
+  const int W = p.QW > 128 ? 128 : (p.QW > 0 ? p.QW : 1);
   // the column-unit path (W >= 32) needs windows (256 / W rows) that never span two images
-  const bool rows_ok = p.QW < 32 || p.QH % (256 / p.QW) == 0;
-  return p.win >= 0 && w_ok && rows_ok && p.QD == 1 && p.KD == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 &&
+  const bool rows_ok = W < 32 || p.QH % (256 / W) == 0;
+  const bool dims_ok = (p.QD == 1 && p.KD == 1) || (p.KD == 3 && p.QD == p.AD && p.QD > 1 && W >= 32);
+  return p.win >= 0 && w_ok && rows_ok && dims_ok && p.KH == 3 && p.KW == 3 && p.stride == 1 &&
          p.pad == 1 && p.upA == 1 && p.AW == p.QW && p.AH == p.QH && (p.M1 % 32) == 0 && (p.M2 % 32) == 0 &&
          p.M1 > 0 && (p.Nc % 32) == 0 && p.bias_mode != 2;
 }

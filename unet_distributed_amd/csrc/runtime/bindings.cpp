@@ -447,10 +447,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("norm_blocks_per_sample", &norm_blocks_per_sample);
   m.def("sample_slices", &sample_slices);
   m.def("wgrad_reduce_stage_floats", &wgrad_reduce_stage_floats);
-  // QW > 0 describes a 2D 3x3 stride-1 'same' conv on QW-wide rows (row-window candidate)
+  // QW > 0 describes a 3x3 (KT 9) or 3x3x3 (KT 27) stride-1 'same' conv on a QD x QH x QW
+  // grid (QH, QD default to QW: square / cubic levels), a row-window candidate
   m.def(
       "wgrad_pick",
-      [](int M1, int M2, int Nc, int KT, int QW, int upA, int win) {
+      [](int M1, int M2, int Nc, int KT, int QW, int upA, int win, int QH, int QD) {
         WgradParams p{};
         p.M1 = M1;
         p.M2 = M2;
@@ -461,10 +462,13 @@ PYBIND11_MODULE(_C, m) {
         p.upA = upA;
         p.win = win;
         p.bias_mode = 1;
-        if (QW > 0 && KT == 9) {          // 3x3 stride-1 'same' conv
+        if (QH <= 0) QH = QW;
+        if (QW > 0 && (KT == 9 || KT == 27)) {   // 3x3 (x3) stride-1 'same' conv
           p.KH = p.KW = 3;
-          p.QD = p.AD = 1;
-          p.QW = p.QH = p.AW = p.AH = QW;
+          p.KD = KT == 27 ? 3 : 1;
+          p.QD = p.AD = KT == 27 ? (QD > 0 ? QD : QW) : 1;
+          p.QW = p.AW = QW;
+          p.QH = p.AH = QH;
           p.stride = 1;
           p.pad = 1;
         } else if (QW > 0 && KT == 4) {   // 2x2 stride-2 transposed conv (QW = coarse width)
@@ -480,7 +484,7 @@ PYBIND11_MODULE(_C, m) {
         return py::make_tuple(c.BM, c.BN, c.NTAP, c.smallc);
       },
       py::arg("M1"), py::arg("M2"), py::arg("Nc"), py::arg("KT"), py::arg("QW") = 0, py::arg("upA") = 1,
-      py::arg("win") = -1);
+      py::arg("win") = -1, py::arg("QH") = 0, py::arg("QD") = 0);
   m.def("packseg_bytes", []() { return (int)sizeof(PackSeg); });
   m.def("reduce_job_bytes", []() { return (int)sizeof(ReduceJob); });
   m.def("reduce_groups", &reduce_groups);

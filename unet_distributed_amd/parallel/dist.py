@@ -56,6 +56,10 @@ def init(device_pref: str = "auto", backend: str = "auto", timeout_s: float = 30
         ctx.device = torch.device("cpu")
     ctx.rank, ctx.world_size, ctx.local_rank = rank, world, local
     if world > 1 and not dist.is_initialized():
+        # UNET_DIST_BACKEND=gloo forces gloo for GPU tensors too: lets several
+        # ranks share ONE card (RCCL refuses duplicate devices) to rehearse the
+        # multi-rank GPU path on a 1-GPU box.
+        backend = os.environ.get("UNET_DIST_BACKEND", backend)
         if backend == "auto":
             backend = "nccl" if use_cuda else "gloo"
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")

@@ -423,7 +423,7 @@ class NativeUNet:
     def _wgrad_pick(self, w):
         """Tile config of a wgrad spec; QW marks 2D 3x3 convs (row-window candidates)."""
         return self.C.wgrad_pick(w["M1"], w["M2"], w["Nc"], w["KT"], QW=w.get("QW", 0), upA=w.get("upA", 1),
-                                 win=self.wgrad_win)
+                                 win=self.wgrad_win, QH=w.get("QH", 0), QD=w.get("QD", 0))
 
     def _wgrad_splits(self, w):
         M1, M2, Nc, KT, Q = w["M1"], w["M2"], w["Nc"], w["KT"], w["Q"]
@@ -495,7 +495,8 @@ class NativeUNet:
                           pad=1, upA=up1, a1=_ptr(b[src1]), a2=_ptr(b[skip]) if skip else None,
                           b=_ptr(dy))
                 emit_wgrad(dict(lname=l.name, kd=kd, M1=c1, M2=c2, Nc=l.cout, KT=KT3, Q=Q,
-                                QW=self.sdims(l.level)[2] if self.dims == 2 else 0, upA=up1,
+                                QD=self.sdims(l.level)[0], QH=self.sdims(l.level)[1],
+                                QW=self.sdims(l.level)[2], upA=up1,
                                 kernel=l.name + "/kernel", bias=l.name + "/bias", bias_mode=1,
                                 bias_width=l.cout, bias_src=(dy, Q),
                                 real_rows=(self.cpad, spec.in_channels) if first else None))
