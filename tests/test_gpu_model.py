@@ -218,3 +218,48 @@ def test_hip_graph_replay_equals_eager(cuda_dev, norm):
     assert torch.equal(s0, s1)
     assert torch.equal(m0, m1)
     assert torch.equal(w0, w1)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(batch_size=8, img_size=64, in_channels=4),
+    dict(batch_size=4, img_size=64, in_channels=1, use_upsampling=True),
+])
+def test_chunked_forward_equals_whole_batch(cuda_dev, monkeypatch, kw):
+    """UNET_FWD_CHUNK runs the full-resolution forward layer runs chunk by chunk
+    (Infinity-Cache residency); every activation and gradient is unchanged."""
+    outs = []
+    for n in ("1", "4"):
+        monkeypatch.setenv("UNET_FWD_CHUNK", n)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
+        if n != "1":
+            names = nb.engine.plan.names()[:nb.engine.fwd_end]
+            assert names.count("fwd:conv1a") == 4
+        nb.fwd_bwd(x, y, seed=77)
+        torch.cuda.synchronize()
+        outs.append((nb.sums().cpu(), fn.grad.clone(), nb.engine.bufs["conv9b"].clone()))
+    (s0, g0, a0), (s1, g1, a1) = outs
+    assert torch.equal(a0, a1)
+    assert torch.allclose(s0, s1, rtol=1e-5, atol=1e-3), (s0, s1)
+    assert _cos(g0, g1) > 0.99999
+
+
+@pytest.mark.parametrize("kw", [
+    dict(batch_size=4, img_size=64, in_channels=4, loss="dice_bce"),
+    dict(batch_size=2, img_size=32, in_channels=4, dims=3),
+])
+def test_fused_head_matches_separate_head(cuda_dev, monkeypatch, kw):
+    """The head fused into the head-input conv's epilogue (UNET_HEAD_FUSE=1) gives the
+    separate head kernel's probabilities, loss sums and gradients up to fp32
+    summation order."""
+    outs = []
+    for f in ("0", "1"):
+        monkeypatch.setenv("UNET_HEAD_FUSE", f)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
+        assert bool(nb.engine._head_fused_blocks) == (f == "1")
+        nb.fwd_bwd(x, y, seed=77)
+        torch.cuda.synchronize()
+        outs.append((nb.sums().cpu(), nb.engine.prob.clone(), fn.grad.clone()))
+    (s0, p0, g0), (s1, p1, g1) = outs
+    assert torch.allclose(s0, s1, rtol=1e-4, atol=1e-2), (s0, s1)
+    assert (p0 - p1).abs().max().item() < 1e-5
+    assert _cos(g0, g1) > 0.99999

@@ -68,3 +68,39 @@ def test_bucket_plan_is_layer_aligned_and_covers_buffer():
         assert x in starts                          # cut at a variable boundary
     # the exposed tail bucket (encoder grads, ready last) stays small
     assert (flat.numel - b[-2]) * 4 / 2 ** 20 <= 8.0
+
+
+def test_forward_chunk_plan_dry_run(monkeypatch):
+    """UNET_FWD_CHUNK=4: full-resolution forward runs are emitted chunk by chunk with
+    per-chunk pointer offsets; the coarse levels and the head stay whole-batch."""
+    from unet_distributed_amd.runtime.native_engine import NativeUNet
+    monkeypatch.setenv("UNET_FWD_CHUNK", "4")
+    spec = UNetSpec(in_channels=4)
+    flat = FlatParams(spec)
+    e = NativeUNet(spec, flat, 8, 64, "cpu", bucket_bounds=plan_buckets(flat, 4.0), dry_run=True)
+    names = e.plan.names()[:e.fwd_end]
+    assert names[1:4] == ["fwd:conv1a", "fwd:conv1b", "fwd:pool1"]
+    assert names.count("fwd:conv1a") == 4 and names.count("fwd:conv9b") == 4
+    assert names.count("fwd:conv5a") == 1 and names.count("fwd:Mask") == 1
+    assert e._toff("conv1b", 1, 2) == 2 * 64 * 64 * 32 * 2
+    assert e._toff("pool1", 1, 2) == 2 * 32 * 32 * 32 * 2
+    monkeypatch.setenv("UNET_FWD_CHUNK", "3")       # batch 8 not divisible: whole batch
+    e = NativeUNet(spec, flat, 8, 64, "cpu", bucket_bounds=plan_buckets(flat, 4.0), dry_run=True)
+    assert e.plan.names()[:e.fwd_end].count("fwd:conv1a") == 1
+
+
+def test_fused_head_plan(monkeypatch):
+    """The Mask head rides on the 32-channel row-window forward of its input conv
+    (fwd:Mask is then only the partial reduction); norm layers or UNET_HEAD_FUSE=0
+    keep the separate head launch."""
+    from unet_distributed_amd.runtime.native_engine import NativeUNet
+    for kw, img, fused in [(dict(in_channels=4), 64, True), (dict(in_channels=4, dims=3), 32, True),
+                           (dict(in_channels=4, norm="batch"), 64, False)]:
+        spec = UNetSpec(**kw)
+        e = NativeUNet(spec, FlatParams(spec), 2, img, "cpu", dry_run=True)
+        assert bool(e._head_fused_blocks) == fused, kw
+        assert e.plan.names()[e.fwd_end - 1] == "fwd:Mask"
+    monkeypatch.setenv("UNET_HEAD_FUSE", "0")
+    spec = UNetSpec(in_channels=4)
+    e = NativeUNet(spec, FlatParams(spec), 2, 64, "cpu", dry_run=True)
+    assert e._head_fused_blocks == 0

@@ -187,8 +187,36 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     return;
   }
   const int Dt = kShuffle ? (p.Cout >> p.shuffle) : 0;
-#pragma unroll 2
-  for (int c = tid; c < NCHUNK; c += NTHR) {
+  // Fused segmentation head (forward of conv9b, BN == Cout == 32): the CPR = 4
+  // consecutive threads holding one pixel's four 8-channel chunks dot them with the
+  // 1x1 head weights, combine by two lane swaps, and the chunk-0 lane applies the
+  // sigmoid and accumulates the Dice / BCE sums (head.hip::head_fwd_kernel semantics
+  // on the same bf16-rounded activations) -- the 268 MB re-read of a separate head
+  // launch is gone.
+  constexpr bool kHeadable = EPI == EPI_FWD && BN == 32 && NTHR % CPR == 0;
+  const bool kHead = kHeadable && p.head_w != nullptr;
+  float hw[8], hb = 0.f, hs[4] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int HIT = kHeadable ? NCHUNK / NTHR : 1;     // chunk iterations per thread
+  static_assert(!kHeadable || (NCHUNK % NTHR == 0 && HIT % CPR == 0), "fused head tiling");
+  float hz[HIT];
+  int hq[HIT];
+#pragma unroll
+  for (int k = 0; k < HIT; ++k) {
+    hz[k] = 0.f;
+    hq[k] = M;                                          // skipped (q >= M) unless set below
+  }
+  if (kHeadable && kHead) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) hw[e] = p.head_w[(tid % CPR) * 8 + e];
+    hb = p.head_b[0];
+  }
+  // (fully unrolled with the fused head, whose per-iteration logits live in registers)
+  constexpr int NITER = (NCHUNK + NTHR - 1) / NTHR;
+  constexpr int UNR = kHeadable ? NITER : 2;
+#pragma unroll UNR
+  for (int it = 0; it < NITER; ++it) {
+    const int c = tid + it * NTHR;
+    if (NCHUNK % NTHR && c >= NCHUNK) break;
     const int ml = c / CPR, cb = c % CPR;
     const int q = qof(ml);
     if (q >= M) continue;
@@ -243,6 +271,67 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       }
     }
     *(u32x4*)(dst + off) = v;
+    if constexpr (kHeadable) {
+      if (kHead) {
+        float f[8];
+        unpack8(v, f);
+        float z = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) z += f[e] * hw[e];
+        z += __shfl_xor(z, 1, 64);     // the pixel's 4 chunk lanes (all active or all not)
+        z += __shfl_xor(z, 2, 64);
+        hz[it] = z + hb;
+        hq[it] = q;
+      }
+    }
+  }
+  if constexpr (kHeadable) {
+    if (kHead) {
+      // the 4 lanes of a pixel group hold the same HIT logits: lane cb finishes
+      // iterations cb, cb + 4, ... (all lanes busy on the transcendental part)
+      const int cb = tid % CPR;
+#pragma unroll
+      for (int k = 0; k < HIT / CPR; ++k) {
+        float z = hz[CPR * k];
+        int q = hq[CPR * k];
+#pragma unroll
+        for (int r = 1; r < CPR; ++r) {
+          z = cb == r ? hz[CPR * k + r] : z;
+          q = cb == r ? hq[CPR * k + r] : q;
+        }
+        if (q < M) {
+          const float pr = 1.f / (1.f + __expf(-z));
+          p.head_prob[q] = pr;
+          if (p.head_t) {
+            const float tv = h2f(((const h16*)p.head_t)[q]);
+            hs[0] += tv * pr;
+            hs[1] += tv;
+            hs[2] += pr;
+            hs[3] += fmaxf(z, 0.f) - z * tv + log1pf(__expf(-fabsf(z)));
+          } else {
+            hs[2] += pr;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (kHeadable) {
+    if (kHead) {
+      __shared__ float hred[4][NTHR / 64];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hs[j] = wave_sum(hs[j]);
+      if ((tid & 63) == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hred[j][tid >> 6] = hs[j];
+      }
+      __syncthreads();
+      if (tid < 4) {
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < NTHR / 64; ++k) sum += hred[tid][k];
+        p.head_part[(size_t)blockIdx.x * 4 + tid] = sum;
+      }
+    }
   }
 }
 

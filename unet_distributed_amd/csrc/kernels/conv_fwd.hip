@@ -923,11 +923,17 @@ hipError_t launch_tconv_dgrad(const ConvFwdParams& p, hipStream_t s) {
 }
 
 template <int BN>
-hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
+int win_grid(const ConvFwdParams& p) {
   const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
   const int rows = p.N * p.OD * p.OH;
   const int R = (W == 16 ? 256 : 512) / W;
-  const int grid = ((rows + R - 1) / R) * (p.OW / W) * (p.Cout / BN);
+  return ((rows + R - 1) / R) * (p.OW / W) * (p.Cout / BN);
+}
+
+template <int BN>
+hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
+  const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
+  const int grid = win_grid<BN>(p);
   const bool cc = p.C2 > 0;
   const int epi = conv_epi_mode(p);
   const int geo = p.KD == 3 ? GEO_3D : (p.OW > W ? GEO_SEG : GEO_2D);
@@ -1014,6 +1020,8 @@ static bool tconv_dgrad_eligible(const ConvFwdParams& p) {
          (p.C1 % 32) == 0 && (p.Cout % 64) == 0 && !p.stats && p.drop_rate == 0.f;
 }
 
+int conv_fwd_pick(const ConvFwdParams& p);
+
 // Fills the tap tables and Kpad; returns nullptr on success or a message describing
 // why the shape is unsupported.
 const char* conv_fwd_prepare(ConvFwdParams& p) {
@@ -1052,6 +1060,12 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     if (t == 7) return "conv_fwd: tile 7 (row-window 512x64: 268 registers, 92 KB LDS, 1 wave/SIMD) is not built";
     if (t == 6 && !win_eligible(p)) return "conv_fwd: row-window tile not applicable";
   }
+  if (p.head_w) {
+    if (!p.head_b || !p.head_prob || !p.head_part) return "conv_fwd: fused head needs head_b / head_prob / head_part";
+    if (p.Cout != 32 || p.drop_rate > 0.f || !p.relu || p.D1 != p.Cout || p.mask1 || p.out_scale != 1.f ||
+        conv_epi_mode(p) != EPI_FWD || conv_fwd_pick(p) != 6)
+      return "conv_fwd: fused head needs a 32-channel ReLU row-window forward";
+  }
   if ((long long)p.N * p.ID * p.IH * p.IW >= (1LL << 31) || (long long)p.N * p.OD * p.OH * p.OW >= (1LL << 31))
     return "conv_fwd: too many pixels";
   // buffer loads use 32-bit byte offsets: every source tensor must stay below 2 GiB
@@ -1088,6 +1102,8 @@ int conv_fwd_pick(const ConvFwdParams& p) {
   if (p.Cout % 64 == 0) return 2;
   return 4;
 }
+
+int conv_fwd_grid(const ConvFwdParams& p) { return conv_fwd_pick(p) == 6 ? win_grid<32>(p) : 0; }
 
 hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
   switch (conv_fwd_pick(p)) {

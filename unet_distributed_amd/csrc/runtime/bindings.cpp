@@ -95,6 +95,11 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.shuffle = get<int>(d, "shuffle", 0);
   p.stats = (float*)getp(d, "stats");
   p.tile = get<int>(d, "tile", 0);
+  p.head_w = (const float*)getp(d, "head_w");
+  p.head_b = (const float*)getp(d, "head_b");
+  p.head_t = getp(d, "head_t");
+  p.head_prob = (float*)const_cast<void*>(getp(d, "head_prob"));
+  p.head_part = (float*)const_cast<void*>(getp(d, "head_part"));
   if (!p.src1 || !p.wgt || !p.dst1) throw std::invalid_argument("conv_fwd: src1/wgt/dst1 required");
   check_msg(conv_fwd_prepare(p));
   return p;
@@ -423,6 +428,9 @@ PYBIND11_MODULE(_C, m) {
     ConvFwdParams p = conv_params(d);
     check(api(dtype)->conv_fwd_launch(p, as_stream(stream)), "conv_fwd");
   }, py::arg("params"), py::arg("stream"), py::arg("dtype") = 0);
+  // workgroups of a row-window conv launch (0 for other kernels): sizes per-block
+  // partial buffers of fused epilogues (the fused head); raises if the dict is invalid
+  m.def("conv_fwd_grid", [](const py::dict& d) { return unet::conv_fwd_grid(conv_params(d)); }, py::arg("params"));
   m.def("wgrad", [](const py::dict& d, uintptr_t stream, int dtype) {
     WgradParams p = wgrad_params(d);
     check(api(dtype)->wgrad_launch(p, as_stream(stream)), "wgrad");

@@ -267,6 +267,7 @@ class NativeUNet:
         hc = self.tinfo[self.head_in][1]
         self.head_partial = torch.zeros(nb * (hc + 1) + nb * 4, dtype=torch.float32, device=self.device)
         self.sums = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self.head_fused_partial = None      # per-workgroup partials of the fused head (_head_grid)
         # gradient buffers: d:<tensor>, dskip:<tensor>, dfull:<tensor> (upsample fold)
         for name, (lvl, ch, _, _) in list(self.tinfo.items()):
             if name == "x":
@@ -385,48 +386,122 @@ class NativeUNet:
     def _salt(self, lname):
         return [l.name for l in self.spec.layers].index(lname)
 
+    def _fwd_chunks(self):
+        """Batch chunks for the full-resolution forward layers.  A level-1 tensor of
+        the b256 step is 268 MB, more than the 256 MiB Infinity Cache, so conv1a ->
+        conv1b -> pool1 (and transConv9 -> conv9a -> conv9b) stream every
+        intermediate through HBM.  Run those layer runs chunk by chunk instead: a
+        chunk's output is re-read by the next layer while it is still resident
+        (UNET_FWD_CHUNK = number of chunks, 1 = off).  Batch statistics (BN) need
+        the whole batch, so only the plain and GN-free model is chunked."""
+        n = int(os.environ.get("UNET_FWD_CHUNK", "1"))
+        if n <= 1 or self.spec.norm != "none" or self.B % n:
+            return 1
+        return n
+
+    def _toff(self, tname, c, nb):
+        """Byte offset of image c*nb of activation tensor `tname`."""
+        lvl, ch = self.tinfo[tname][0], self.tinfo[tname][1]
+        d, h, w = self.sdims(lvl)
+        return c * nb * d * h * w * ch * self.bufs[tname].element_size()
+
     def _build_forward(self, plan, dropout, train=True):
         spec = self.spec
-        b = self.bufs
         P1 = self.npix(1)
-        plan.add_generic("cast_input", [_ptr(self.x_f32), _ptr(b["x"])],
+        plan.add_generic("cast_input", [_ptr(self.x_f32), _ptr(self.bufs["x"])],
                          [P1, spec.in_channels, self.cpad], [], "cast_input")
-        for l in spec.layers:
-            if l.kind == "conv":
-                src1, up1, skip = self.inputs[l.name]
-                c1 = self.tinfo[src1][1]
-                d = self._conv_common(l.level, 3, 1, 1)
-                normed = spec.norm != "none"
-                d.update(name="fwd:" + l.name, C1=c1, C2=self.tinfo[skip][1] if skip else 0, up1=up1,
-                         src1=_ptr(b[src1]), src2=_ptr(b[skip]) if skip else None,
-                         wgt=self.wptr(l.name), bias=self.master_ptr(l.name + "/bias"),
-                         Cout=l.cout, relu=0 if normed else 1,
-                         dst1=_ptr(b["z:" + l.name] if normed else b[l.name]),
-                         drop_rate=spec.dropout if (l.dropout and dropout and not normed) else 0.0,
-                         salt=self._salt(l.name))
-                plan.add_conv_fwd(d)
-                if normed:
-                    self._norm_fwd(plan, l, dropout, train)
-            elif l.kind == "pool":
-                src = self.inputs[l.name][0]
-                dd, hh, ww = self.sdims(l.level)
-                plan.add_generic("pool_fwd", [_ptr(b[src]), _ptr(b[l.name])],
-                                 [self.B, dd, hh, ww, l.cout, int(self.dims == 3)], [], "fwd:" + l.name)
-            elif l.kind == "tconv":
-                src = self.inputs[l.name][0]
-                d = self._conv_common(l.level + 1, 1, 1, 0)
-                d.update(name="fwd:" + l.name, C1=l.cin, src1=_ptr(b[src]), wgt=self.wptr(l.name),
-                         bias=self.master_ptr(l.name + "/bias"), Cout=(2 ** self.dims) * l.cout,
-                         relu=0, shuffle=self.dims, dst1=_ptr(b[l.name]))
-                plan.add_conv_fwd(d)
-            elif l.kind == "mask":
-                hc = self.tinfo[self.head_in][1]
-                nb = self.head_nb
-                part = self.head_partial
-                plan.add_generic("head_fwd", [_ptr(b[self.head_in]), self.master_ptr("Mask/kernel"),
-                                              self.master_ptr("Mask/bias"), _ptr(self.target),
-                                              _ptr(self.prob), _ptr(part), _ptr(self.sums)],
-                                 [P1, hc], [], "fwd:Mask")
+        nch = self._fwd_chunks()
+        # fused head: the Mask 1x1 conv + sigmoid + loss partials run in the epilogue of
+        # the head's input conv (whole batch only; UNET_HEAD_FUSE=0 keeps the separate
+        # head launch)
+        self._head_fused_blocks = 0
+        self._fuse_head = nch == 1 and os.environ.get("UNET_HEAD_FUSE", "1") != "0"
+        layers = [l for l in spec.layers if l.kind != "up"]
+        i = 0
+        while i < len(layers):
+            l = layers[i]
+            if nch > 1 and l.kind != "mask" and l.level == 1:
+                j = i
+                while j < len(layers) and layers[j].kind != "mask" and layers[j].level == 1:
+                    j += 1
+                nb = self.B // nch
+                for c in range(nch):
+                    for ll in layers[i:j]:
+                        self._fwd_layer(plan, ll, dropout, train, c, nb)
+                i = j
+            else:
+                self._fwd_layer(plan, l, dropout, train, 0, self.B)
+                i += 1
+
+    def _fwd_layer(self, plan, l, dropout, train, c, nb):
+        """Forward launches of layer `l` for images [c*nb, (c+1)*nb)."""
+        spec = self.spec
+        b = self.bufs
+
+        def P(t):
+            return None if t is None else _ptr(b[t]) + self._toff(t, c, nb)
+
+        if l.kind == "conv":
+            src1, up1, skip = self.inputs[l.name]
+            c1 = self.tinfo[src1][1]
+            d = self._conv_common(l.level, 3, 1, 1)
+            d["N"] = nb
+            normed = spec.norm != "none"
+            d.update(name="fwd:" + l.name, C1=c1, C2=self.tinfo[skip][1] if skip else 0, up1=up1,
+                     src1=P(src1), src2=P(skip) if skip else None,
+                     wgt=self.wptr(l.name), bias=self.master_ptr(l.name + "/bias"),
+                     Cout=l.cout, relu=0 if normed else 1,
+                     dst1=_ptr(b["z:" + l.name]) if normed else P(l.name),
+                     drop_rate=spec.dropout if (l.dropout and dropout and not normed) else 0.0,
+                     salt=self._salt(l.name))
+            if l.name == self.head_in and self._fuse_head and not normed and not d["drop_rate"]:
+                nbk = self._head_grid(d)
+                if nbk:
+                    d.update(head_w=self.master_ptr("Mask/kernel"), head_b=self.master_ptr("Mask/bias"),
+                             head_t=_ptr(self.target), head_prob=_ptr(self.prob),
+                             head_part=_ptr(self.head_fused_partial))
+                    self._head_fused_blocks = nbk
+            plan.add_conv_fwd(d)
+            if normed:
+                self._norm_fwd(plan, l, dropout, train)
+        elif l.kind == "pool":
+            src = self.inputs[l.name][0]
+            dd, hh, ww = self.sdims(l.level)
+            plan.add_generic("pool_fwd", [P(src), P(l.name)],
+                             [nb, dd, hh, ww, l.cout, int(self.dims == 3)], [], "fwd:" + l.name)
+        elif l.kind == "tconv":
+            src = self.inputs[l.name][0]
+            d = self._conv_common(l.level + 1, 1, 1, 0)
+            d["N"] = nb
+            d.update(name="fwd:" + l.name, C1=l.cin, src1=P(src), wgt=self.wptr(l.name),
+                     bias=self.master_ptr(l.name + "/bias"), Cout=(2 ** self.dims) * l.cout,
+                     relu=0, shuffle=self.dims, dst1=P(l.name))
+            plan.add_conv_fwd(d)
+        elif l.kind == "mask" and self._head_fused_blocks:
+            plan.add_generic("partial_reduce", [_ptr(self.head_fused_partial), _ptr(self.sums)],
+                             [self._head_fused_blocks, 4], [], "fwd:Mask")
+        elif l.kind == "mask":
+            P1 = self.npix(1)
+            hc = self.tinfo[self.head_in][1]
+            part = self.head_partial
+            plan.add_generic("head_fwd", [_ptr(b[self.head_in]), self.master_ptr("Mask/kernel"),
+                                          self.master_ptr("Mask/bias"), _ptr(self.target),
+                                          _ptr(self.prob), _ptr(part), _ptr(self.sums)],
+                             [P1, hc], [], "fwd:Mask")
+
+    def _head_grid(self, d):
+        """Workgroups of the head-input conv when its forward can carry the fused
+        head (32-channel ReLU row-window launch), else 0; sizes the partial buffer."""
+        if self.tinfo[self.head_in][1] != 32:
+            return 0
+        probe = dict(d, head_w=1, head_b=1, head_prob=1, head_part=1)
+        try:
+            nbk = int(self.C.conv_fwd_grid(probe))
+        except ValueError:
+            return 0
+        if nbk and (self.head_fused_partial is None or self.head_fused_partial.numel() < 4 * nbk):
+            self.head_fused_partial = torch.zeros(4 * nbk, dtype=torch.float32, device=self.device)
+        return nbk
 
     @staticmethod
     def _colsum_blocks(rows, C):
