@@ -585,13 +585,23 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   // wgrad_win_eligible), so halo rows of a neighbouring image are DMA'd as zeros and
   // its tap loop needs no image-edge branches
   constexpr bool UNITS_PATH = W >= 32 && W / 32 <= PS;
+  // 16-wide rows (row-pair path): a 32-pixel K step is a pair of rows, and each wave
+  // owns R / PS consecutive output rows.  The A fragment of halo rows (hr, hr + 1) at
+  // shift dw feeds every output pair y = hr - dh with y even: rows of even hr serve
+  // dh = 0 and 2, odd hr dh = 1, so per window a wave reads (2 NP + 1) x 6 A
+  // fragments instead of NP x 18 (25 % fewer LDS reads; this kernel is LDS-read
+  // bound at W = 16).  Needs windows inside one image (halo rows of the neighbour
+  // image are then DMA'd as zeros, as on the column-unit path).
+  constexpr bool PAIR_PATH = W == 16 && GEO == WGEO_2D;
+  constexpr bool pair_ok = PAIR_PATH;   // wgrad_win_eligible: QH % 16 == 0 for 16-wide rows
   for (int win = w_begin; win < w_end; ++win) {
     const int g0 = (GEO == WGEO_SEG ? win / nseg : win) * R;
     const int col0 = GEO == WGEO_SEG ? (win % nseg) * W : 0;
     // 3D: a window lies in one (n, d) slice (H % R == 0); its depth-shifted input slice
     // is padding -> the window contributes nothing to this tap group (uniform skip)
     if (GEO == WGEO_3D && (unsigned)((g0 / H) % D + kd - 1) >= (unsigned)D) continue;
-    const bool top_in = !UNITS_PATH || (g0 % H) != 0, bot_in = !UNITS_PATH || ((g0 + R) % H) != 0;
+    const bool zero_halo = UNITS_PATH || pair_ok;
+    const bool top_in = !zero_halo || (g0 % H) != 0, bot_in = !zero_halo || ((g0 + R) % H) != 0;
     __syncthreads();   // the previous window's fragment reads are done
 #pragma unroll
     for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
@@ -694,6 +704,59 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
         }
       }
       continue;
+    }
+    if constexpr (PAIR_PATH) {
+      {
+        constexpr int NP = R / 2 / PS;             // output row pairs per wave
+        const int y0 = ps * 2 * NP;                // first output row (window-relative)
+        const int lp = 8 * G + q;                  // lane pixel of a 32-pixel step
+        const int lr = lp >> 4, lc = lp & 15;      // its row in the pair, its column
+        // halo row of output row y, tap dh is y + dh (halo row 0 = window row -1)
+        int ab[3][2][2];
+#pragma unroll
+        for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              const int col = lc + dw + 4 * hh;
+              ab[dw][i][hh] = tr_addr((y0 + lr) * HWP + col, col, 16 * i + 4 * pp);
+            }
+        // dY fragments of output pair k: loaded at hr = 2k (first use, dh = 0), last
+        // used at hr = 2k + 2 (dh = 2) -- at most two pairs live
+        h16x8 bf[NP][2];
+#pragma unroll
+        for (int hr = 0; hr <= 2 * NP; ++hr) {
+          if (!(hr & 1) && hr < 2 * NP) {
+            const int s0 = (y0 + hr) * W + lp, s1 = s0 + 4;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              bf[hr >> 1][j] = tr8(Yq + tr_addr(s0, s0, 16 * j + 4 * pp), Yq + tr_addr(s1, s1, 16 * j + 4 * pp));
+            if (do_bias) {
+#pragma unroll
+              for (int j = 0; j < 2; ++j) bacc[j] = mfma16(ones, bf[hr >> 1][j], bacc[j]);
+            }
+          }
+#pragma unroll
+          for (int dw = 0; dw < 3; ++dw) {
+            h16x8 af[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[i] = tr8(Xs + ab[dw][i][0] + hr * ROWB, Xs + ab[dw][i][1] + hr * ROWB);
+#pragma unroll
+            for (int dh = 0; dh < 3; ++dh) {
+              const int y = hr - dh;
+              if (y < 0 || y >= 2 * NP || (y & 1)) continue;
+#pragma unroll
+              for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                  acc[3 * dh + dw][i][j] = mfma16(af[i], bf[y >> 1][j], acc[3 * dh + dw][i][j]);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        continue;
+      }
     }
 #pragma unroll 1
     for (int kk = ps; kk < KS; kk += PS) {
@@ -1153,8 +1216,9 @@ static bool wgrad_win_eligible(const WgradParams& p) {
   const bool w_ok = p.QW == 8 || p.QW == 16 || p.QW == 32 || p.QW == 64 ||
                     (p.QW % 128 == 0 && p.QW > 0 && p.QW <= 8192);
   const int W = p.QW > 128 ? 128 : (p.QW > 0 ? p.QW : 1);
-  // the column-unit path (W >= 32) needs windows (256 / W rows) that never span two images
-  const bool rows_ok = W < 32 || p.QH % (256 / W) == 0;
+  // the column-unit (W >= 32) and row-pair (W = 16) paths need windows (256 / W rows)
+  // that never span two images
+  const bool rows_ok = W < 16 || p.QH % (256 / W) == 0;
   const bool dims_ok = (p.QD == 1 && p.KD == 1) || (p.KD == 3 && p.QD == p.AD && p.QD > 1 && W >= 32);
   return p.win >= 0 && w_ok && rows_ok && dims_ok && p.KH == 3 && p.KW == 3 && p.stride == 1 &&
          p.pad == 1 && p.upA == 1 && p.AW == p.QW && p.AH == p.QH && (p.M1 % 32) == 0 && (p.M2 % 32) == 0 &&
