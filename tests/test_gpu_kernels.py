@@ -564,3 +564,29 @@ def test_norm_fwd_bwd_kernels(cuda_dev, norm, N, H, Cc, G):
     assert rel_err(dg, dgr) < 1e-3 and rel_err(db, dbr) < 1e-3
     if norm == "batch":
         assert torch.allclose(rm, rmr, atol=1e-5) and torch.allclose(rv, rvr, atol=1e-4)
+
+
+@pytest.mark.parametrize("dims3", [0, 1])
+def test_maxpool_argmax_codes_match_recomputed_argmax(cuda_dev, dims3):
+    """pool_fwd's first-argmax codes drive the same backward as recomputing the argmax
+    from the input (ReLU zeros make ties: the FIRST maximum wins in both)."""
+    torch.manual_seed(19)
+    N, D, H, Cc = 2, (4 if dims3 else 1), 16, 32
+    shape = (N, D, H, H, Cc) if dims3 else (N, H, H, Cc)
+    x = F.relu(torch.randn(*shape, device=cuda_dev)).bfloat16()
+    oshape = (N, D // 2, H // 2, H // 2, Cc) if dims3 else (N, H // 2, H // 2, Cc)
+    y = torch.empty(*oshape, device=cuda_dev, dtype=torch.bfloat16)
+    code = torch.full((y.numel() // 8,), -1, device=cuda_dev, dtype=torch.int32)
+    C().generic("pool_fwd", [ptr(x), ptr(y), ptr(code)], [N, D, H, H, Cc, dims3], [], stream())
+    if dims3:
+        ref = F.max_pool3d(x.float().permute(0, 4, 1, 2, 3), 2).permute(0, 2, 3, 4, 1)
+    else:
+        ref = nhwc(F.max_pool2d(nchw(x.float()), 2))
+    assert (y.float() - ref).abs().max().item() == 0
+    dy = torch.randn_like(y.float()).bfloat16()
+    skip = torch.randn_like(x.float()).bfloat16()
+    dx_x, dx_c = torch.empty_like(x), torch.empty_like(x)
+    C().generic("pool_bwd", [ptr(x), ptr(dy), ptr(skip), ptr(dx_x)], [N, D, H, H, Cc, dims3], [], stream())
+    C().generic("pool_bwd", [0, ptr(dy), ptr(skip), ptr(dx_c), ptr(code)], [N, D, H, H, Cc, dims3], [], stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx_x, dx_c)

@@ -189,13 +189,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
   const int Dt = kShuffle ? (p.Cout >> p.shuffle) : 0;
   // Fused segmentation head (forward of conv9b, BN == Cout == 32): the CPR = 4
   // consecutive threads holding one pixel's four 8-channel chunks dot them with the
-  // 1x1 head weights, combine by two lane swaps, and the chunk-0 lane applies the
-  // sigmoid and accumulates the Dice / BCE sums (head.hip::head_fwd_kernel semantics
-  // on the same bf16-rounded activations) -- the 268 MB re-read of a separate head
-  // launch is gone.
+  // 1x1 head weights (the same bf16-rounded activations head.hip::head_fwd_kernel
+  // reads) and combine by two lane swaps; the fp32 logit is stored per pixel -- the
+  // 268 MB re-read of a separate head launch becomes a 17 MB one.
   constexpr bool kHeadable = EPI == EPI_FWD && BN == 32 && NTHR % CPR == 0;
   const bool kHead = kHeadable && p.head_w != nullptr;
-  float hw[8], hb = 0.f, hs[4] = {0.f, 0.f, 0.f, 0.f};
+  float hw[8], hb = 0.f;
   constexpr int HIT = kHeadable ? NCHUNK / NTHR : 1;     // chunk iterations per thread
   static_assert(!kHeadable || (NCHUNK % NTHR == 0 && HIT % CPR == 0), "fused head tiling");
   float hz[HIT];
@@ -287,8 +286,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
   }
   if constexpr (kHeadable) {
     if (kHead) {
-      // the 4 lanes of a pixel group hold the same HIT logits: lane cb finishes
-      // iterations cb, cb + 4, ... (all lanes busy on the transcendental part)
+      // the 4 lanes of a pixel group hold the same HIT logits: lane cb stores
+      // iterations cb, cb + 4, ...; head.hip::head_finish turns them into
+      // probabilities and loss partials
       const int cb = tid % CPR;
 #pragma unroll
       for (int k = 0; k < HIT / CPR; ++k) {
@@ -299,37 +299,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
           z = cb == r ? hz[CPR * k + r] : z;
           q = cb == r ? hq[CPR * k + r] : q;
         }
-        if (q < M) {
-          const float pr = 1.f / (1.f + __expf(-z));
-          p.head_prob[q] = pr;
-          if (p.head_t) {
-            const float tv = h2f(((const h16*)p.head_t)[q]);
-            hs[0] += tv * pr;
-            hs[1] += tv;
-            hs[2] += pr;
-            hs[3] += fmaxf(z, 0.f) - z * tv + log1pf(__expf(-fabsf(z)));
-          } else {
-            hs[2] += pr;
-          }
-        }
-      }
-    }
-  }
-  if constexpr (kHeadable) {
-    if (kHead) {
-      __shared__ float hred[4][NTHR / 64];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) hs[j] = wave_sum(hs[j]);
-      if ((tid & 63) == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) hred[j][tid >> 6] = hs[j];
-      }
-      __syncthreads();
-      if (tid < 4) {
-        float sum = 0.f;
-#pragma unroll
-        for (int k = 0; k < NTHR / 64; ++k) sum += hred[tid][k];
-        p.head_part[(size_t)blockIdx.x * 4 + tid] = sum;
+        if (q < M) p.head_logit[q] = z;
       }
     }
   }

@@ -1061,7 +1061,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     if (t == 6 && !win_eligible(p)) return "conv_fwd: row-window tile not applicable";
   }
   if (p.head_w) {
-    if (!p.head_b || !p.head_prob || !p.head_part) return "conv_fwd: fused head needs head_b / head_prob / head_part";
+    if (!p.head_b || !p.head_logit) return "conv_fwd: fused head needs head_b / head_logit";
     if (p.Cout != 32 || p.drop_rate > 0.f || !p.relu || p.D1 != p.Cout || p.mask1 || p.out_scale != 1.f ||
         conv_epi_mode(p) != EPI_FWD || conv_fwd_pick(p) != 6)
       return "conv_fwd: fused head needs a 32-channel ReLU row-window forward";

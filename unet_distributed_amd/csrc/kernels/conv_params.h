@@ -39,13 +39,10 @@ struct ConvFwdParams {
   float* stats;               // nullptr or [2][Cout] per-channel sum / sum of squares (BN)
   int tile;                   // 0 = auto, else forced tile config id (tuning / A-B tests)
   // Fused segmentation head (row-window forward, Cout == 32, EPI_FWD only): per pixel
-  // z = sum_c out[c] head_w[c] + head_b, prob = sigmoid(z) -> head_prob, and per-block
-  // {I, St, Sp, BCE} partials -> head_part[block][4] (head_t: targets or nullptr)
+  // z = sum_c out[c] head_w[c] + head_b -> head_logit (fp32) for head_finish
   const float* head_w;
   const float* head_b;
-  const void* head_t;
-  float* head_prob;
-  float* head_part;
+  float* head_logit;
   // filled by conv_fwd_prepare (host): K padded to 64, per-tap pixel deltas / offsets
   int Kpad;
   int tap_delta[27];

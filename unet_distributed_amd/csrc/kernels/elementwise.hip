@@ -5,7 +5,8 @@
 //  * maxpool2_fwd / maxpool2_bwd: 2x2(x2) max-pool (`model.py:53-69`); the backward
 //    routes to the FIRST maximum of each window (TF MaxPoolGrad tie rule) and
 //    fuses the add of the skip-connection gradient coming from the decoder
-//    (the concat's dgrad), so the encoder output gradient is written once.
+//    (the concat's dgrad), so the encoder output gradient is written once.  The
+//    forward can record the argmax per channel (2-3 bit codes) for the backward.
 //  * upsample2_bwd: 2x2(x2) sum of the full-res gradient of the folded nearest
 //    upsample (`model.py:76-109` upsampling variant), masked by the source's ReLU.
 #include "common.h"
@@ -28,61 +29,82 @@ __global__ void __launch_bounds__(256) cast_input_kernel(const float* __restrict
   }
 }
 
-// one thread = one pooled pixel x 8 channels
+// Pooling thread map: one thread = one pooled pixel x 8 channels, 32-bit index math
+// (the 64-bit divisions of a long-long decomposition dominated these memory-bound
+// kernels).  Window corner k = (dz, dy, dx) -> input pixel base + k-offset.
+struct PoolIdx {
+  int cc;        // 8-channel chunk
+  int base;      // input pixel of window corner (0, 0, 0)
+};
+__device__ __forceinline__ PoolIdx pool_idx(int i, int cpp, int OW, int OH, int H, int W, int dims3) {
+  PoolIdx r;
+  r.cc = i % cpp;
+  const int t = i / cpp;
+  const int ow = t % OW, rr = t / OW;
+  const int ndo = rr / OH, oh = rr - ndo * OH;
+  const int dbase = dims3 ? 2 * ndo : ndo;           // n * D + 2 od  (3D: D = 2 OD)
+  r.base = (dbase * H + 2 * oh) * W + 2 * ow;
+  return r;
+}
+
+// y = max over the window; code (optional): per channel the index of the FIRST
+// maximum (2 bits in 2D, 3 bits in 3D) packed into one 32-bit word per thread, so
+// the backward routes the gradient without re-reading the 4-8x larger input
 __global__ void __launch_bounds__(256) maxpool2_fwd_kernel(const h16* __restrict__ x, int N, int D, int H, int W,
-                                                           int C, int dims3, h16* __restrict__ y) {
+                                                           int C, int dims3, h16* __restrict__ y,
+                                                           uint32_t* __restrict__ code) {
   const int OD = dims3 ? D / 2 : 1, OH = H / 2, OW = W / 2;
   const int cpp = C / 8;
-  const long long total = (long long)N * OD * OH * OW * cpp;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int cc = i % cpp;
-    long long r = i / cpp;
-    const int ow = r % OW;
-    r /= OW;
-    const int oh = r % OH;
-    r /= OH;
-    const int od = r % OD;
-    const int n = r / OD;
+  const int total = N * OD * OH * OW * cpp;
+  const int nz = dims3 ? 2 : 1;
+  const int bits = dims3 ? 3 : 2;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const PoolIdx pi = pool_idx(i, cpp, OW, OH, H, W, dims3);
     float m[8];
+    int arg[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
-    const int nz = dims3 ? 2 : 1;
+    for (int e = 0; e < 8; ++e) {
+      m[e] = -INFINITY;
+      arg[e] = 0;
+    }
     for (int dz = 0; dz < nz; ++dz)
 #pragma unroll
       for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
         for (int dx = 0; dx < 2; ++dx) {
-          const int id = dims3 ? 2 * od + dz : 0;
-          const size_t pix = (((size_t)n * D + id) * H + 2 * oh + dy) * W + 2 * ow + dx;
-          const u32x4 v = *(const u32x4*)(x + pix * C + cc * 8);
+          const int k = dz * 4 + dy * 2 + dx;
+          const int pix = pi.base + (dz * H + dy) * W + dx;
+          const u32x4 v = *(const u32x4*)(x + (size_t)pix * C + pi.cc * 8);
           float f[8];
           unpack8(v, f);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
+          for (int e = 0; e < 8; ++e)
+            if (f[e] > m[e]) {
+              m[e] = f[e];
+              arg[e] = k;
+            }
         }
     *(u32x4*)(y + (size_t)i * 8) = pack8(m);
+    if (code) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) w |= (uint32_t)arg[e] << (bits * e);
+      code[i] = w;
+    }
   }
 }
 
-// dx[window] = (first argmax ? dy : 0) + skip_grad (optional)
+// dx[window] = (first argmax ? dy : 0) + skip_grad (optional); argmax recomputed
+// from the forward input x
 __global__ void __launch_bounds__(256) maxpool2_bwd_kernel(const h16* __restrict__ x, const h16* __restrict__ dy,
                                                            const h16* __restrict__ skip, int N, int D, int H, int W,
                                                            int C, int dims3, h16* __restrict__ dx) {
   const int OD = dims3 ? D / 2 : 1, OH = H / 2, OW = W / 2;
   const int cpp = C / 8;
-  const long long total = (long long)N * OD * OH * OW * cpp;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int cc = i % cpp;
-    long long r = i / cpp;
-    const int ow = r % OW;
-    r /= OW;
-    const int oh = r % OH;
-    r /= OH;
-    const int od = r % OD;
-    const int n = r / OD;
-    const int nz = dims3 ? 2 : 1;
+  const int total = N * OD * OH * OW * cpp;
+  const int nz = dims3 ? 2 : 1;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const PoolIdx pi = pool_idx(i, cpp, OW, OH, H, W, dims3);
     float g[8];
     unpack8(*(const u32x4*)(dy + (size_t)i * 8), g);
     float best[8];
@@ -92,38 +114,80 @@ __global__ void __launch_bounds__(256) maxpool2_bwd_kernel(const h16* __restrict
       best[e] = -INFINITY;
       arg[e] = 0;
     }
-    size_t pix[8];
-    int k = 0;
     for (int dz = 0; dz < nz; ++dz)
 #pragma unroll
       for (int dyy = 0; dyy < 2; ++dyy)
 #pragma unroll
         for (int dxx = 0; dxx < 2; ++dxx) {
-          const int id = dims3 ? 2 * od + dz : 0;
-          pix[k] = (((size_t)n * D + id) * H + 2 * oh + dyy) * W + 2 * ow + dxx;
+          const int k = dz * 4 + dyy * 2 + dxx;
+          const int pix = pi.base + (dz * H + dyy) * W + dxx;
           float f[8];
-          unpack8(*(const u32x4*)(x + pix[k] * C + cc * 8), f);
+          unpack8(*(const u32x4*)(x + (size_t)pix * C + pi.cc * 8), f);
 #pragma unroll
           for (int e = 0; e < 8; ++e)
             if (f[e] > best[e]) {
               best[e] = f[e];
               arg[e] = k;
             }
-          ++k;
         }
-    for (int kk = 0; kk < k; ++kk) {
-      float o[8];
-      if (skip) {
-        unpack8(*(const u32x4*)(skip + pix[kk] * C + cc * 8), o);
-      } else {
+    for (int dz = 0; dz < nz; ++dz)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = 0.f;
-      }
+      for (int dyy = 0; dyy < 2; ++dyy)
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (arg[e] == kk) o[e] += g[e];
-      *(u32x4*)(dx + pix[kk] * C + cc * 8) = pack8(o);
-    }
+        for (int dxx = 0; dxx < 2; ++dxx) {
+          const int k = dz * 4 + dyy * 2 + dxx;
+          const size_t off = (size_t)(pi.base + (dz * H + dyy) * W + dxx) * C + pi.cc * 8;
+          float o[8];
+          if (skip) {
+            unpack8(*(const u32x4*)(skip + off), o);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (arg[e] == k) o[e] += g[e];
+          *(u32x4*)(dx + off) = pack8(o);
+        }
+  }
+}
+
+// the same from the forward's argmax codes: reads 4 bytes per 8 pooled channels
+// instead of the 4 (8 in 3D) input pixels
+__global__ void __launch_bounds__(256) maxpool2_bwd_code_kernel(const uint32_t* __restrict__ code,
+                                                                const h16* __restrict__ dy,
+                                                                const h16* __restrict__ skip, int N, int D, int H,
+                                                                int W, int C, int dims3, h16* __restrict__ dx) {
+  const int OD = dims3 ? D / 2 : 1, OH = H / 2, OW = W / 2;
+  const int cpp = C / 8;
+  const int total = N * OD * OH * OW * cpp;
+  const int nz = dims3 ? 2 : 1;
+  const int bits = dims3 ? 3 : 2;
+  const uint32_t kmask = dims3 ? 7u : 3u;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const PoolIdx pi = pool_idx(i, cpp, OW, OH, H, W, dims3);
+    float g[8];
+    unpack8(*(const u32x4*)(dy + (size_t)i * 8), g);
+    const uint32_t w = code[i];
+    for (int dz = 0; dz < nz; ++dz)
+#pragma unroll
+      for (int dyy = 0; dyy < 2; ++dyy)
+#pragma unroll
+        for (int dxx = 0; dxx < 2; ++dxx) {
+          const uint32_t k = dz * 4 + dyy * 2 + dxx;
+          const size_t off = (size_t)(pi.base + (dz * H + dyy) * W + dxx) * C + pi.cc * 8;
+          float o[8];
+          if (skip) {
+            unpack8(*(const u32x4*)(skip + off), o);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (((w >> (bits * e)) & kmask) == k) o[e] += g[e];
+          *(u32x4*)(dx + off) = pack8(o);
+        }
   }
 }
 
@@ -180,18 +244,23 @@ hipError_t cast_input_launch(const float* x, int P, int Cin, int Cpad, void* y, 
   return hipGetLastError();
 }
 
-hipError_t maxpool2_fwd_launch(const void* x, int N, int D, int H, int W, int C, int dims3, void* y, hipStream_t s) {
+hipError_t maxpool2_fwd_launch(const void* x, int N, int D, int H, int W, int C, int dims3, void* y, void* code,
+                               hipStream_t s) {
   const long long work = (long long)N * (dims3 ? D / 2 : 1) * (H / 2) * (W / 2) * (C / 8);
   hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, N, D, H, W, C,
-                     dims3, (h16*)y);
+                     dims3, (h16*)y, (uint32_t*)code);
   return hipGetLastError();
 }
 
-hipError_t maxpool2_bwd_launch(const void* x, const void* dy, const void* skip, int N, int D, int H, int W, int C,
-                               int dims3, void* dx, hipStream_t s) {
+hipError_t maxpool2_bwd_launch(const void* x, const void* code, const void* dy, const void* skip, int N, int D, int H,
+                               int W, int C, int dims3, void* dx, hipStream_t s) {
   const long long work = (long long)N * (dims3 ? D / 2 : 1) * (H / 2) * (W / 2) * (C / 8);
-  hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, (const h16*)dy,
-                     (const h16*)skip, N, D, H, W, C, dims3, (h16*)dx);
+  if (code)
+    hipLaunchKernelGGL(maxpool2_bwd_code_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const uint32_t*)code,
+                       (const h16*)dy, (const h16*)skip, N, D, H, W, C, dims3, (h16*)dx);
+  else
+    hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, (const h16*)dy,
+                       (const h16*)skip, N, D, H, W, C, dims3, (h16*)dx);
   return hipGetLastError();
 }
 

@@ -70,6 +70,60 @@ __global__ void __launch_bounds__(HT) head_fwd_kernel(const h16* __restrict__ x,
   }
 }
 
+// Finish of the fused head: prob holds the fp32 logits written by the head-input
+// conv's epilogue (conv_epilogue.h); sigmoid in place and the same per-block
+// {I, St, Sp, BCE} partials as head_fwd_kernel.
+__global__ void __launch_bounds__(HT) head_finish_kernel(float* __restrict__ prob, const h16* __restrict__ t, int P,
+                                                         float* __restrict__ partial) {
+  __shared__ float red[4][HT / 64];
+  float sI = 0.f, sT = 0.f, sP = 0.f, sB = 0.f;
+  auto one = [&](float z, float tv, bool has_t) -> float {
+    const float pr = 1.f / (1.f + __expf(-z));
+    if (has_t) {
+      sI += tv * pr;
+      sT += tv;
+      sP += pr;
+      sB += fmaxf(z, 0.f) - z * tv + log1pf(__expf(-fabsf(z)));
+    } else {
+      sP += pr;
+    }
+    return pr;
+  };
+  // 4 pixels per thread (16-byte logit / 8-byte target accesses), scalar tail
+  const int P4 = P >> 2;
+  for (int i = blockIdx.x * HT + threadIdx.x; i < P4; i += gridDim.x * HT) {
+    f32x4 z = ((const f32x4*)prob)[i];
+    float tv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (t) {
+      const u32x2 tw = ((const u32x2*)t)[i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tv[e] = bits2f((uint16_t)(tw[e >> 1] >> (16 * (e & 1))));
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) z[e] = one(z[e], tv[e], t != nullptr);
+    ((f32x4*)prob)[i] = z;
+  }
+  for (int p = 4 * P4 + blockIdx.x * HT + threadIdx.x; p < P; p += gridDim.x * HT)
+    prob[p] = one(prob[p], t ? (float)t[p] : 0.f, t != nullptr);
+  sI = wave_sum(sI);
+  sT = wave_sum(sT);
+  sP = wave_sum(sP);
+  sB = wave_sum(sB);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][wv] = sI;
+    red[1][wv] = sT;
+    red[2][wv] = sP;
+    red[3][wv] = sB;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    float s = 0.f;
+    for (int k = 0; k < HT / 64; ++k) s += red[threadIdx.x][k];
+    partial[blockIdx.x * 4 + threadIdx.x] = s;
+  }
+}
+
 // out[j] = sum_b partial[b][j]: one block per column j, fixed order
 __global__ void __launch_bounds__(256) partial_reduce_kernel(const float* __restrict__ partial, int nb, int width,
                                                              float* __restrict__ out) {
@@ -220,6 +274,18 @@ hipError_t head_bwd_launch(const void* x, const float* w, const float* prob, con
 
 hipError_t partial_reduce_launch(const float* partial, int nb, int width, float* out, hipStream_t s) {
   hipLaunchKernelGGL(partial_reduce_kernel, dim3(width), dim3(256), 0, s, partial, nb, width, out);
+  return hipGetLastError();
+}
+
+hipError_t head_finish_launch(float* prob, const void* t, int P, float* partial, float* sums, hipStream_t s) {
+  // one float4 of logits per thread (latency-bound otherwise); 4 nb floats of
+  // partials must fit the head's workspace of head_blocks(P) x (C + 5) >= 21
+  // head_blocks(P) floats (C >= 16, head_check)
+  int nb = (P / 4 + HT - 1) / HT;
+  nb = nb > 4096 ? 4096 : (nb < 1 ? 1 : nb);
+  if (nb > 5 * head_blocks(P)) nb = 5 * head_blocks(P);
+  hipLaunchKernelGGL(head_finish_kernel, dim3(nb), dim3(HT), 0, s, prob, (const h16*)t, P, partial);
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3(4), dim3(256), 0, s, partial, nb, 4, sums);
   return hipGetLastError();
 }
 

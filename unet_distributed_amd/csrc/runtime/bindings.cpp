@@ -97,9 +97,7 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.tile = get<int>(d, "tile", 0);
   p.head_w = (const float*)getp(d, "head_w");
   p.head_b = (const float*)getp(d, "head_b");
-  p.head_t = getp(d, "head_t");
-  p.head_prob = (float*)const_cast<void*>(getp(d, "head_prob"));
-  p.head_part = (float*)const_cast<void*>(getp(d, "head_part"));
+  p.head_logit = (float*)const_cast<void*>(getp(d, "head_logit"));
   if (!p.src1 || !p.wgt || !p.dst1) throw std::invalid_argument("conv_fwd: src1/wgt/dst1 required");
   check_msg(conv_fwd_prepare(p));
   return p;
@@ -154,6 +152,7 @@ WgradParams wgrad_params(const py::dict& d) {
   X(head_fwd_launch) \
   X(head_bwd_launch) \
   X(partial_reduce_launch) \
+  X(head_finish_launch) \
   X(norm_moments_launch) \
   X(bn_finalize_launch) \
   X(gn_finalize_launch) \
@@ -200,18 +199,22 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     return [=](hipStream_t s) { return A->cast_input_launch(x, a, b, c, y, s); };
   }
   if (kind == "pool_fwd") {
+    // ptrs: x, y[, code]
     need(2, 6, 0);
-    void *x = vp(0), *y = vp(1);
+    void *x = vp(0), *y = vp(1), *code = P.size() > 2 ? vp(2) : nullptr;
     int n = I[0], d = I[1], h = I[2], w = I[3], c = I[4], d3 = I[5];
     if (c % 8) throw std::invalid_argument("pool: C % 8");
-    return [=](hipStream_t s) { return A->maxpool2_fwd_launch(x, n, d, h, w, c, d3, y, s); };
+    if ((long long)n * d * h * w * c >= (1LL << 31)) throw std::invalid_argument("pool: too many elements");
+    return [=](hipStream_t s) { return A->maxpool2_fwd_launch(x, n, d, h, w, c, d3, y, code, s); };
   }
   if (kind == "pool_bwd") {
+    // ptrs: x, dy, skip, dx[, code]  (code non-null: argmax codes of pool_fwd, x unused)
     need(4, 6, 0);
-    void *x = vp(0), *dy = vp(1), *sk = vp(2), *dx = vp(3);
+    void *x = vp(0), *dy = vp(1), *sk = vp(2), *dx = vp(3), *code = P.size() > 4 ? vp(4) : nullptr;
     int n = I[0], d = I[1], h = I[2], w = I[3], c = I[4], d3 = I[5];
     if (c % 8) throw std::invalid_argument("pool: C % 8");
-    return [=](hipStream_t s) { return A->maxpool2_bwd_launch(x, dy, sk, n, d, h, w, c, d3, dx, s); };
+    if ((long long)n * d * h * w * c >= (1LL << 31)) throw std::invalid_argument("pool: too many elements");
+    return [=](hipStream_t s) { return A->maxpool2_bwd_launch(x, code, dy, sk, n, d, h, w, c, d3, dx, s); };
   }
   if (kind == "ups_bwd") {
     need(3, 6, 0);
@@ -250,6 +253,14 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     int rows = I[0], c = I[1], blocks = I[2];
     if (c % 8 || c > 2048) throw std::invalid_argument("colsum: C % 8 / C > 2048");
     return [=](hipStream_t s) { return A->colsum_launch(x, rows, c, blocks, part, s); };
+  }
+  if (kind == "head_finish") {
+    need(4, 1, 0);
+    float* prob = (float*)vp(0);
+    const void* t = vp(1);
+    float *part = (float*)vp(2), *sums = (float*)vp(3);
+    int P_ = I[0];
+    return [=](hipStream_t s) { return A->head_finish_launch(prob, t, P_, part, sums, s); };
   }
   if (kind == "partial_reduce") {
     need(2, 2, 0);

@@ -229,6 +229,7 @@ class NativeUNet:
         # tensor graph: name -> (level, channels, produced_by_relu, dropout)
         self.tinfo: Dict[str, Tuple[int, int, bool, bool]] = {"x": (1, self.cpad, False, False)}
         self.inputs: Dict[str, Tuple] = {}
+        self.pool_codes: Dict[str, torch.Tensor] = {}
         cur = "x"
         pending_up = None
         for l in spec.layers:
@@ -248,6 +249,10 @@ class NativeUNet:
             elif l.kind == "pool":
                 self.inputs[l.name] = (cur, 1, None)
                 self._buf(l.name, l.level + 1, l.cout)
+                # first-argmax codes of the forward (one uint32 per pooled pixel x 8
+                # channels): the backward reads these instead of the 4-8x larger input
+                self.pool_codes[l.name] = torch.zeros(self.npix(l.level + 1) * l.cout // 8, dtype=torch.int32,
+                                                      device=self.device)
                 self.tinfo[l.name] = (l.level + 1, l.cout, True, False)
                 cur = l.name
             elif l.kind == "tconv":
@@ -267,7 +272,6 @@ class NativeUNet:
         hc = self.tinfo[self.head_in][1]
         self.head_partial = torch.zeros(nb * (hc + 1) + nb * 4, dtype=torch.float32, device=self.device)
         self.sums = torch.zeros(4, dtype=torch.float32, device=self.device)
-        self.head_fused_partial = None      # per-workgroup partials of the fused head (_head_grid)
         # gradient buffers: d:<tensor>, dskip:<tensor>, dfull:<tensor> (upsample fold)
         for name, (lvl, ch, _, _) in list(self.tinfo.items()):
             if name == "x":
@@ -458,8 +462,7 @@ class NativeUNet:
                 nbk = self._head_grid(d)
                 if nbk:
                     d.update(head_w=self.master_ptr("Mask/kernel"), head_b=self.master_ptr("Mask/bias"),
-                             head_t=_ptr(self.target), head_prob=_ptr(self.prob),
-                             head_part=_ptr(self.head_fused_partial))
+                             head_logit=_ptr(self.prob))
                     self._head_fused_blocks = nbk
             plan.add_conv_fwd(d)
             if normed:
@@ -467,7 +470,9 @@ class NativeUNet:
         elif l.kind == "pool":
             src = self.inputs[l.name][0]
             dd, hh, ww = self.sdims(l.level)
-            plan.add_generic("pool_fwd", [P(src), P(l.name)],
+            pd, ph, pw = self.sdims(l.level + 1)
+            code = _ptr(self.pool_codes[l.name]) + c * nb * pd * ph * pw * (l.cout // 8) * 4
+            plan.add_generic("pool_fwd", [P(src), P(l.name), code],
                              [nb, dd, hh, ww, l.cout, int(self.dims == 3)], [], "fwd:" + l.name)
         elif l.kind == "tconv":
             src = self.inputs[l.name][0]
@@ -478,8 +483,8 @@ class NativeUNet:
                      relu=0, shuffle=self.dims, dst1=P(l.name))
             plan.add_conv_fwd(d)
         elif l.kind == "mask" and self._head_fused_blocks:
-            plan.add_generic("partial_reduce", [_ptr(self.head_fused_partial), _ptr(self.sums)],
-                             [self._head_fused_blocks, 4], [], "fwd:Mask")
+            plan.add_generic("head_finish", [_ptr(self.prob), _ptr(self.target), _ptr(self.head_partial),
+                                             _ptr(self.sums)], [self.npix(1)], [], "fwd:Mask")
         elif l.kind == "mask":
             P1 = self.npix(1)
             hc = self.tinfo[self.head_in][1]
@@ -491,17 +496,13 @@ class NativeUNet:
 
     def _head_grid(self, d):
         """Workgroups of the head-input conv when its forward can carry the fused
-        head (32-channel ReLU row-window launch), else 0; sizes the partial buffer."""
+        head (32-channel ReLU row-window launch), else 0."""
         if self.tinfo[self.head_in][1] != 32:
             return 0
-        probe = dict(d, head_w=1, head_b=1, head_prob=1, head_part=1)
         try:
-            nbk = int(self.C.conv_fwd_grid(probe))
+            return int(self.C.conv_fwd_grid(dict(d, head_w=1, head_b=1, head_logit=1)))
         except ValueError:
             return 0
-        if nbk and (self.head_fused_partial is None or self.head_fused_partial.numel() < 4 * nbk):
-            self.head_fused_partial = torch.zeros(4 * nbk, dtype=torch.float32, device=self.device)
-        return nbk
 
     @staticmethod
     def _colsum_blocks(rows, C):
@@ -621,7 +622,7 @@ class NativeUNet:
                 emit_generic("pool_bwd",
                              lambda src=src, l=l: [_ptr(b[src]), _ptr(b["d:" + l.name]),
                                                    _ptr(b["dskip:" + src]) if ("dskip:" + src) in b else 0,
-                                                   _ptr(b["d:" + src])],
+                                                   _ptr(b["d:" + src]), _ptr(self.pool_codes[l.name])],
                              [self.B, dd, hh, ww, l.cout, int(self.dims == 3)], [], "bwd:" + l.name)
             elif l.kind == "tconv":
                 src = self.inputs[l.name][0]
