@@ -29,7 +29,7 @@ def test_plan_construction_dry_run(kw, img, dtype):
     e = NativeUNet(spec, flat, 2, img, "cpu", bucket_bounds=b, dry_run=True, dtype=dtype)
     assert e.arena.dtype == e.adt and e.target.dtype == e.adt
     names = e.plan.names()
-    assert names[0] == "cast_input" and names[e.fwd_end - 1] == "fwd:Mask"
+    assert names[0] == "fwd:conv1a" and names[e.fwd_end - 1] == "fwd:Mask"
     assert names[e.fwd_end] == "bwd:Mask"
     # every conv / tconv gradient is reduced by exactly one batched reduce op
     reduced = [ln for n in names if n.startswith("reduce:") for ln in n[len("reduce:"):].split(",")]
@@ -79,7 +79,7 @@ def test_forward_chunk_plan_dry_run(monkeypatch):
     flat = FlatParams(spec)
     e = NativeUNet(spec, flat, 8, 64, "cpu", bucket_bounds=plan_buckets(flat, 4.0), dry_run=True)
     names = e.plan.names()[:e.fwd_end]
-    assert names[1:4] == ["fwd:conv1a", "fwd:conv1b", "fwd:pool1"]
+    assert names[0:3] == ["fwd:conv1a", "fwd:conv1b", "fwd:pool1"]
     assert names.count("fwd:conv1a") == 4 and names.count("fwd:conv9b") == 4
     assert names.count("fwd:conv5a") == 1 and names.count("fwd:Mask") == 1
     assert e._toff("conv1b", 1, 2) == 2 * 64 * 64 * 32 * 2

@@ -219,9 +219,9 @@ class NativeUNet:
     # ------------------------------------------------------------------ buffers
     def _alloc_activations(self):
         spec = self.spec
-        self.x_f32 = torch.zeros((self.npix(1), spec.in_channels), dtype=torch.float32,
-                                 device=self.device)
-        self._buf("x", 1, self.cpad)
+        # channel-padded 16-bit input; load_batch casts the fp32 batch straight into it
+        # (the pad channels stay zero)
+        self._buf("x", 1, self.cpad).zero_()
         self.target = torch.zeros(self.npix(1), dtype=self.adt, device=self.device)
         # loss-gradient scale read by the head backward (fp16 dynamic loss scaling)
         self.loss_scale_dev = torch.ones(1, dtype=torch.float32, device=self.device)
@@ -411,9 +411,6 @@ class NativeUNet:
 
     def _build_forward(self, plan, dropout, train=True):
         spec = self.spec
-        P1 = self.npix(1)
-        plan.add_generic("cast_input", [_ptr(self.x_f32), _ptr(self.bufs["x"])],
-                         [P1, spec.in_channels, self.cpad], [], "cast_input")
         nch = self._fwd_chunks()
         # fused head: the Mask 1x1 conv + sigmoid + loss partials run in the epilogue of
         # the head's input conv (whole batch only; UNET_HEAD_FUSE=0 keeps the separate
@@ -779,7 +776,9 @@ class NativeUNet:
     # ------------------------------------------------------------------ running
     def load_batch(self, x: torch.Tensor, y: torch.Tensor, stream=None):
         """x: [B, (D,) H, W, Cin] float, y: [B, (D,) H, W, 1] float/bool."""
-        self.x_f32.view(-1).copy_(x.reshape(-1), non_blocking=True)
+        cin = self.spec.in_channels
+        xb = self.bufs["x"].view(-1, self.cpad)
+        (xb if cin == self.cpad else xb[:, :cin]).copy_(x.reshape(-1, cin), non_blocking=True)
         self.target.copy_(y.reshape(-1), non_blocking=True)
 
     # ------------------------------------------------------------------ HIP graphs
