@@ -78,6 +78,13 @@ def test_native_adam_matches_reference(cuda_dev):
     torch.cuda.synchronize()
     assert torch.allclose(fn.master, w, rtol=1e-5, atol=1e-7)
     assert torch.allclose(fn.m, m) and torch.allclose(fn.v, v)
+    # the 16-bit compute copies written by the Adam launch equal a plain repack of the
+    # updated master (every kernel layout, both copies, padding untouched)
+    a1 = nb.engine.arena.clone()
+    nb.engine.repack()
+    torch.cuda.synchronize()
+    assert torch.equal(a1, nb.engine.arena)
+    assert (a1 != 0).sum().item() >= spec.num_params() - 1000
 
 
 def test_native_training_reduces_loss(cuda_dev):

@@ -43,6 +43,10 @@ def test_plan_construction_dry_run(kw, img, dtype):
     assert e.seg_ends[-1] == e.plan.size() and sorted(e.seg_ends) == e.seg_ends
     # dgrad of the first conv is never planned
     assert "dgrad:conv1a" not in names
+    # the Adam / repack segments tile the flat buffer exactly (gaps included)
+    st = e.seg_table
+    assert st["off"][0] == 0 and (st["off"][1:] == st["off"][:-1] + st["n"][:-1]).all()
+    assert st["off"][-1] + st["n"][-1] == flat.numel
 
 
 def test_host_side_shape_validation_rejects_bad_shapes():

@@ -165,20 +165,26 @@ class NativeUNet:
                 off += l.cin * dgrow
                 layouts[l.name] = (2, Tt, l.cin, l.cout, l.cin, row, dgrow)
         self.arena = torch.zeros(max(off, 64), dtype=self.adt, device=self.device)
+        # the segments tile the whole flat buffer (Adam updates alignment gaps too):
+        # a kind-0 segment absorbs the gap after it, a kernel segment gets its own
         segs = []
-        for name, shape, foff, n in flat.entries:
+        ends = [e[2] for e in flat.entries[1:]] + [flat.numel]
+        for (name, shape, foff, n), end in zip(flat.entries, ends):
             lname, var = name.split("/", 1)
             if var == "kernel" and lname in layouts:
                 kind, t, ci, co, ci_pad, row, dgrow = layouts[lname]
                 segs.append((foff, n, kind, t, ci, co, ci_pad, row, dgrow, 0,
                              self.w_fwd_off[lname], self.w_dg_off.get(lname, -1)))
+                if end > foff + n:
+                    segs.append((foff + n, end - foff - n, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1))
             else:
-                segs.append((foff, n, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1))
+                segs.append((foff, end - foff, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1))
         dt = np.dtype([("off", "<i4"), ("n", "<i4"), ("kind", "<i4"), ("T", "<i4"), ("Ci", "<i4"),
                        ("Co", "<i4"), ("Ci_pad", "<i4"), ("rowstride", "<i4"), ("dg_rowstride", "<i4"),
                        ("pad_", "<i4"), ("fwd_off", "<i8"), ("dg_off", "<i8")])
         assert dt.itemsize == self.C.packseg_bytes()
         arr = np.array(segs, dtype=dt)
+        self.seg_table = arr
         self.nseg = len(segs)
         self.segs = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
 
