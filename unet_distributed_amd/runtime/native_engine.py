@@ -72,6 +72,7 @@ class NativeUNet:
         # backward is launched eagerly even in HIP-graph mode.
         self.dual_stream = os.environ.get("UNET_DUAL_STREAM", "1") != "0"
         self._side = None
+        self._chain = None
         self._groups: Dict[tuple, list] = {}
         # 16-bit element type of activations, gradients w.r.t. activations and the
         # weight copies: selects the bf16 or fp16 build of every kernel (common.h)
@@ -853,29 +854,45 @@ class NativeUNet:
 
     def _backward_dual(self, on_segment, stream):
         """Eager backward with the weight gradients on a side stream.  Every side run
-        first waits for all main-stream work enqueued so far (its dY and any earlier
+        first waits for all dgrad-chain work enqueued so far (its dY and any earlier
         gradient producers); bucket allreduces are issued from the side stream after
-        it has also caught up with the main stream, so the dgrad chain never waits
-        for them; the main stream joins the side stream once at the end (the next
-        forward overwrites activations the side launches read)."""
+        it has also caught up with the chain, so the dgrad chain never waits for them;
+        the caller's stream joins both at the end (the next forward overwrites
+        activations the side launches read).
+
+        UNET_BWD_PRIO: "dgrad" runs the dgrad chain on a high-priority stream (the
+        critical path wins the dispatcher; the weight gradients fill in), "wgrad" the
+        reverse, anything else leaves both at the default priority."""
         main = stream if stream is not None else torch.cuda.current_stream()
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
+            lo, hi = torch.cuda.Stream.priority_range()      # (lowest, highest) priority values
+            mode = os.environ.get("UNET_BWD_PRIO", "none")
+            ps = {"dgrad": (hi, lo), "wgrad": (lo, hi)}.get(mode)
+            if ps is None:
+                self._chain, self._side = None, torch.cuda.Stream(device=self.device)
+            else:
+                self._chain = torch.cuda.Stream(device=self.device, priority=ps[0])
+                self._side = torch.cuda.Stream(device=self.device, priority=ps[1])
+        chain = self._chain if self._chain is not None else main
         side = self._side
-        hm, hs = main.cuda_stream, side.cuda_stream
+        if chain is not main:
+            chain.wait_stream(main)
+        hm, hs = chain.cuda_stream, side.cuda_stream
         begin = self.fwd_end
         for k, end in enumerate(self.seg_ends):
             for on_side, i, j in self._side_groups(begin, end):
                 if on_side:
-                    side.wait_stream(main)
+                    side.wait_stream(chain)
                     self.plan.run(i, j, hs)
                 else:
                     self.plan.run(i, j, hm)
             begin = end
             if on_segment is not None:
-                side.wait_stream(main)
+                side.wait_stream(chain)
                 with torch.cuda.stream(side):
                     on_segment(k)
+        if chain is not main:
+            main.wait_stream(chain)
         main.wait_stream(side)
 
     def backward(self, on_segment=None, stream=None):
