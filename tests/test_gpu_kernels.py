@@ -590,3 +590,19 @@ def test_maxpool_argmax_codes_match_recomputed_argmax(cuda_dev, dims3):
     C().generic("pool_bwd", [0, ptr(dy), ptr(skip), ptr(dx_c), ptr(code)], [N, D, H, H, Cc, dims3], [], stream())
     torch.cuda.synchronize()
     assert torch.equal(dx_x, dx_c)
+
+
+@pytest.mark.parametrize("dims3", [0, 1])
+def test_upsample2_fwd_materialised(cuda_dev, dims3):
+    """Nearest x2 upsample (the upsampling decoder's materialised source) is exact."""
+    torch.manual_seed(23)
+    N, D, H, Cc = 2, (3 if dims3 else 1), 8, 64
+    shape = (N, D, H, H, Cc) if dims3 else (N, H, H, Cc)
+    x = torch.randn(*shape, device=cuda_dev).bfloat16()
+    ref = x.repeat_interleave(2, -2).repeat_interleave(2, -3)
+    if dims3:
+        ref = ref.repeat_interleave(2, 1)
+    y = torch.empty_like(ref)
+    C().generic("ups_fwd", [ptr(x), ptr(y)], [N, D, H, H, Cc, dims3], [], stream())
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)

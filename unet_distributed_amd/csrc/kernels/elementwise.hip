@@ -191,6 +191,34 @@ __global__ void __launch_bounds__(256) maxpool2_bwd_code_kernel(const uint32_t* 
   }
 }
 
+// Nearest 2x(2x2) upsample, materialised: y[child] = x[p] for the 4 (8 in 3D) children of
+// each low-resolution pixel; one thread = one low pixel x 8 channels (16-byte accesses).
+// The decoder convs of the upsampling variant then read a full-resolution source and
+// run on the row-window kernels (the folded-upsample implicit GEMM was 3-10x slower).
+__global__ void __launch_bounds__(256) upsample2_fwd_kernel(const h16* __restrict__ x, int N, int D, int H, int W,
+                                                            int C, int dims3, h16* __restrict__ y) {
+  // D, H, W: LOW resolution dims
+  const int cpp = C / 8;
+  const int FD = dims3 ? 2 : 1;
+  const int total = N * D * H * W * cpp;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cc = i % cpp;
+    int r = i / cpp;
+    const int w = r % W;
+    r /= W;
+    const int h = r % H;
+    const int nd = r / H;                 // n * D + d
+    const u32x4 v = *(const u32x4*)(x + (size_t)i * 8);
+    for (int dz = 0; dz < FD; ++dz)
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy) {
+        const size_t row = ((size_t)(nd * FD + dz) * (2 * H) + 2 * h + dy) * (2 * W) + 2 * w;
+        *(u32x4*)(y + row * C + cc * 8) = v;
+        *(u32x4*)(y + (row + 1) * C + cc * 8) = v;
+      }
+  }
+}
+
 // dlow[p] = sum_{2x2(x2) children} dup[child] * (mask[p] > 0)
 __global__ void __launch_bounds__(256) upsample2_bwd_kernel(const h16* __restrict__ dup, const h16* __restrict__ mask,
                                                             int N, int D, int H, int W, int C, int dims3,
@@ -261,6 +289,13 @@ hipError_t maxpool2_bwd_launch(const void* x, const void* code, const void* dy, 
   else
     hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, (const h16*)dy,
                        (const h16*)skip, N, D, H, W, C, dims3, (h16*)dx);
+  return hipGetLastError();
+}
+
+hipError_t upsample2_fwd_launch(const void* x, int N, int D, int H, int W, int C, int dims3, void* y, hipStream_t s) {
+  const long long work = (long long)N * D * H * W * (C / 8);
+  hipLaunchKernelGGL(upsample2_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, N, D, H, W, C, dims3,
+                     (h16*)y);
   return hipGetLastError();
 }
 

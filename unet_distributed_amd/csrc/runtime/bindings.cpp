@@ -149,6 +149,7 @@ WgradParams wgrad_params(const py::dict& d) {
   X(maxpool2_fwd_launch) \
   X(maxpool2_bwd_launch) \
   X(upsample2_bwd_launch) \
+  X(upsample2_fwd_launch) \
   X(head_fwd_launch) \
   X(head_bwd_launch) \
   X(partial_reduce_launch) \
@@ -215,6 +216,15 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     if (c % 8) throw std::invalid_argument("pool: C % 8");
     if ((long long)n * d * h * w * c >= (1LL << 31)) throw std::invalid_argument("pool: too many elements");
     return [=](hipStream_t s) { return A->maxpool2_bwd_launch(x, code, dy, sk, n, d, h, w, c, d3, dx, s); };
+  }
+  if (kind == "ups_fwd") {
+    // ptrs: low-res x, full-res y; ints: N, D, H, W (low resolution), C, dims3
+    need(2, 6, 0);
+    void *x = vp(0), *y = vp(1);
+    int n = I[0], d = I[1], h = I[2], w = I[3], c = I[4], d3 = I[5];
+    if (c % 8) throw std::invalid_argument("ups_fwd: C % 8");
+    if ((long long)n * d * h * w * c * (d3 ? 8 : 4) >= (1LL << 31)) throw std::invalid_argument("ups_fwd: too large");
+    return [=](hipStream_t s) { return A->upsample2_fwd_launch(x, n, d, h, w, c, d3, y, s); };
   }
   if (kind == "ups_bwd") {
     need(3, 6, 0);

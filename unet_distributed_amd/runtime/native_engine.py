@@ -236,6 +236,10 @@ class NativeUNet:
         # tensor graph: name -> (level, channels, produced_by_relu, dropout)
         self.tinfo: Dict[str, Tuple[int, int, bool, bool]] = {"x": (1, self.cpad, False, False)}
         self.inputs: Dict[str, Tuple] = {}
+        # upsampling decoder: materialise the nearest upsample (UNET_UPS_MATERIALIZE=1) so
+        # the decoder convs and their weight gradients run on the row-window kernels;
+        # 0 folds it into the implicit-GEMM address generation instead
+        self.ups_materialize = os.environ.get("UNET_UPS_MATERIALIZE", "1") != "0"
         self.pool_codes: Dict[str, torch.Tensor] = {}
         cur = "x"
         pending_up = None
@@ -293,6 +297,9 @@ class NativeUNet:
                     d, h, w = self.sdims(l.level)
                     shape = (self.B, h, w, ch) if self.dims == 2 else (self.B, d, h, w, ch)
                     self.bufs["dfull:" + src1] = torch.empty(shape, dtype=self.adt, device=self.device)
+                    if self.ups_materialize:
+                        # nearest-upsampled copy read by the forward and the weight gradient
+                        self.bufs["up:" + src1] = torch.empty(shape, dtype=self.adt, device=self.device)
         self.slab = None
         self.bias_slab = None
         self._alloc_norm()
@@ -452,11 +459,20 @@ class NativeUNet:
         if l.kind == "conv":
             src1, up1, skip = self.inputs[l.name]
             c1 = self.tinfo[src1][1]
+            s1 = P(src1)
+            if up1 == 2 and self.ups_materialize:
+                lvl = self.tinfo[src1][0]
+                dd, hh, ww = self.sdims(lvl)
+                fd, fh, fw = self.sdims(l.level)
+                s1 = _ptr(b["up:" + src1]) + c * nb * fd * fh * fw * c1 * b["up:" + src1].element_size()
+                plan.add_generic("ups_fwd", [P(src1), s1], [nb, dd, hh, ww, c1, int(self.dims == 3)], [],
+                                 "fwd:up:" + src1)
+                up1 = 1
             d = self._conv_common(l.level, 3, 1, 1)
             d["N"] = nb
             normed = spec.norm != "none"
             d.update(name="fwd:" + l.name, C1=c1, C2=self.tinfo[skip][1] if skip else 0, up1=up1,
-                     src1=P(src1), src2=P(skip) if skip else None,
+                     src1=s1, src2=P(skip) if skip else None,
                      wgt=self.wptr(l.name), bias=self.master_ptr(l.name + "/bias"),
                      Cout=l.cout, relu=0 if normed else 1,
                      dst1=_ptr(b["z:" + l.name]) if normed else P(l.name),
@@ -580,15 +596,19 @@ class NativeUNet:
                         ops.append(lambda pl, kind=kind, P_=P_, I_=I_, F_=F_, nm=nm: pl.add_generic(kind, P_, I_, F_, nm))
                     dy = b["dz:" + l.name]
                 Q = self.npix(l.level)
-                # --- weight + bias gradient (fused column sums)
+                # --- weight + bias gradient (fused column sums); the upsampling decoder's
+                # A operand is the materialised upsample when there is one
+                a1, upA = b[src1], up1
+                if up1 == 2 and self.ups_materialize:
+                    a1, upA = b["up:" + src1], 1
                 kd = dict(N=self.B, QD=self.sdims(l.level)[0], QH=self.sdims(l.level)[1],
                           QW=self.sdims(l.level)[2], AD=self.sdims(l.level)[0], AH=self.sdims(l.level)[1],
                           AW=self.sdims(l.level)[2], KD=3 if self.dims == 3 else 1, KH=3, KW=3, stride=1,
-                          pad=1, upA=up1, a1=_ptr(b[src1]), a2=_ptr(b[skip]) if skip else None,
+                          pad=1, upA=upA, a1=_ptr(a1), a2=_ptr(b[skip]) if skip else None,
                           b=_ptr(dy))
                 emit_wgrad(dict(lname=l.name, kd=kd, M1=c1, M2=c2, Nc=l.cout, KT=KT3, Q=Q,
                                 QD=self.sdims(l.level)[0], QH=self.sdims(l.level)[1],
-                                QW=self.sdims(l.level)[2], upA=up1,
+                                QW=self.sdims(l.level)[2], upA=upA,
                                 kernel=l.name + "/kernel", bias=l.name + "/bias", bias_mode=1,
                                 bias_width=l.cout, bias_src=(dy, Q),
                                 real_rows=(self.cpad, spec.in_channels) if first else None))
