@@ -151,6 +151,21 @@ def test_async_ps_mode_two_ranks(tmp_path):
     assert [x["step"] for x in recs if x["kind"] == "test_final"] == [6]   # PS global_step at the end
 
 
+@pytest.mark.slow
+def test_async_ps_fp16_overflow_on_one_rank_keeps_ranks_in_lockstep(tmp_path):
+    """An fp16 overflow on rank 1 at its very first step (the most likely overflow,
+    at the 2^16 initial scale) must not desynchronise the per-epoch evaluations: a
+    skipped iteration that did not count would leave that rank at local step 0, a
+    multiple of the epoch length, and send it into evaluate()'s allreduce alone."""
+    r = _run_train(tmp_path, ["--is_sync", "0", "--epochs", "2", "--dtype", "fp16", "--no_checkpoint",
+                              "--fault_inject_overflow_step", "0", "--fault_inject_rank", "1",
+                              "--dist_timeout_s", "60"], timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:]
+    recs = [json.loads(l) for l in open(tmp_path / "m.jsonl")]
+    assert len([x for x in recs if x["kind"] == "test"]) >= 1
+    assert len([x for x in recs if x["kind"] == "test_final"]) == 1
+
+
 def _run_launcher(tmp_path, extra, timeout=600):
     port = _free_port()
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")

@@ -270,3 +270,39 @@ def test_fused_head_matches_separate_head(cuda_dev, monkeypatch, kw):
     assert torch.allclose(s0, s1, rtol=1e-4, atol=1e-2), (s0, s1)
     assert (p0 - p1).abs().max().item() < 1e-5
     assert _cos(g0, g1) > 0.99999
+
+
+@pytest.mark.parametrize("norm", ["batch", "group"])
+def test_native_inference_export_roundtrip_norm(cuda_dev, tmp_path, norm):
+    """A --norm batch|group export served by the native eval plan: the BatchNorm
+    moving statistics written with the export are the ones the native plan
+    normalises with (non-trivial stats, so mean 0 / var 1 would fail)."""
+    import numpy as np
+    from unet_distributed_amd.config import Config
+    from unet_distributed_amd.data.datasets import synthetic_brats
+    from unet_distributed_amd.inference import load_saved_model
+    from unet_distributed_amd.models import reference
+    from unet_distributed_amd.models.spec import spec_from_config
+    from unet_distributed_amd.runtime.params import FlatParams
+    from unet_distributed_amd.utils.checkpoint import export_model
+    cfg = Config(img_size=64, in_channels=4, checkpoint_dir=str(tmp_path), norm=norm)
+    spec = spec_from_config(cfg)
+    flat = FlatParams(spec)
+    flat.load_dict(reference.init_params(spec, seed=3))
+    g = torch.Generator().manual_seed(0)
+    state = {}
+    if norm == "batch":
+        for l in spec.param_layers():
+            if l.kind == "conv":
+                state[l.name + "/norm/moving_mean"] = 0.2 * torch.randn(l.cout, generator=g)
+                state[l.name + "/norm/moving_variance"] = 0.5 + torch.rand(l.cout, generator=g)
+    d = export_model(cfg, spec, flat, extra_state=state)
+    model = load_saved_model(d, device=cuda_dev, batch=4)
+    assert model.name == "native"
+    x, _ = synthetic_brats(4, 64, 4, seed=2)
+    p = model.predict(x)
+    with torch.no_grad():
+        ref = reference.forward(spec, {k: v.to(cuda_dev) for k, v in flat.params().items()},
+                                torch.from_numpy(x).to(cuda_dev), train=False, dropout=False,
+                                state={k: v.to(cuda_dev) for k, v in state.items()}).cpu().numpy()
+    assert np.abs(p - ref).max() < 0.05, np.abs(p - ref).max()

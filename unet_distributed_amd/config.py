@@ -92,6 +92,7 @@ class Config:
     export: bool = True
     fault_inject_step: int = -1
     fault_inject_rank: int = -1
+    fault_inject_overflow_step: int = -1   # fp16 test hook: poison this step's gradient
     check_sync_every: int = 0        # cross-rank parameter checksum every K steps
     deterministic: bool = False      # torch path: deterministic algorithms (native path always is)
     serialize_kernels: bool = False  # debug: AMD_SERIALIZE_KERNEL=3 + HIP_LAUNCH_BLOCKING=1

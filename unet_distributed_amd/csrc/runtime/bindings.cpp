@@ -5,8 +5,8 @@
 // so this module has no dependency on the PyTorch C++ ABI.
 //
 // Two ways to launch:
-//  * immediate functions (conv_fwd, wgrad, ...) used by the per-op autograd
-//    wrappers in unet_distributed_amd/ops and by the kernel tests;
+//  * immediate functions (conv_fwd, wgrad, ...) used by the kernel tests
+//    (tests/test_gpu_kernels.py) and the tuning scripts;
 //  * `Plan`: the UNet executor records every launch of a training step ONCE
 //    (all shapes, pointers and epilogue flags resolved at plan time) and then
 //    replays ranges of it from C++ with no per-kernel Python overhead.  Ranges

@@ -55,9 +55,11 @@ class Predictor:
             self.backend.engine.repack()
         else:
             self.backend = TorchBackend(spec, flat, cfg, self.device, batch)
-            for k, v in (state or {}).items():
-                if k in self.backend.state:
-                    self.backend.state[k].copy_(torch.as_tensor(v))
+        # BatchNorm moving statistics (both backends keep them under the same names;
+        # the native inference plan normalises with them)
+        for k, v in (state or {}).items():
+            if k in self.backend.state:
+                self.backend.state[k].copy_(torch.as_tensor(np.asarray(v, np.float32)))
         self.name = self.backend.name
 
     @torch.no_grad()

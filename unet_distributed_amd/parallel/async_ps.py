@@ -108,6 +108,12 @@ class AsyncPS:
         if self.repack is not None:
             self.repack()
 
+    def skip_step(self):
+        """A local iteration that pushed nothing (fp16 overflow): it still counts, so
+        every rank's epoch boundaries -- and the collectives evaluate() issues there --
+        stay in lockstep."""
+        self.local_steps += 1
+
     def snapshot_into_flat(self):
         """Copy the PS state (weights, Adam slots, step, beta powers) into ``flat``
         on rank 0 -- used before a checkpoint save so the bundle is the PS's."""

@@ -147,8 +147,10 @@ def native_supported(spec, cfg, device) -> Optional[str]:
         return "native kernels are bf16 / fp16 (dtype=%s)" % cfg.dtype
     if spec.n_cl_out != 1:
         return "n_cl_out != 1"
-    if spec.base % 32:
-        return "base filters must be a multiple of 32"
+    if spec.base not in (32, 64):
+        # the fused head / head kernels take 16, 32 or 64 head-input channels and the
+        # row-window kernels 32-channel chunks
+        return "base filters must be 32 or 64 (got %d)" % spec.base
     cin = spec.in_channels
     if not (cin <= 8 or cin % 32 == 0):
         return "in_channels=%d" % cin

@@ -168,8 +168,28 @@ class Trainer:
         f.beta1_power = float(meta[1].item())
         f.beta2_power = float(meta[2].item())
         self.restored = bool(meta[3].item())
+        self._broadcast_extra()
         if hasattr(self.backend, "engine"):
             self.backend.engine.repack()
+
+    def _extra_state(self):
+        return getattr(self.backend, "state", None) or {}
+
+    def _broadcast_extra(self):
+        """Non-trainable state (BatchNorm moving statistics) from rank 0: after a
+        resume only rank 0 restored it, and every rank must evaluate with it."""
+        for k in sorted(self._extra_state()):
+            D.broadcast_(self._extra_state()[k], 0)
+
+    def _average_extra(self):
+        """Replica-average the BatchNorm moving statistics (each rank tracks them over
+        its own shard; the reference's PS-hosted variables are shared by all workers)."""
+        st = self._extra_state()
+        if self.world == 1 or not st:
+            return
+        for k in sorted(st):
+            D.allreduce_sum_(st[k])
+            st[k].mul_(1.0 / self.world)
 
     def _load_data(self):
         cfg = self.cfg
@@ -221,21 +241,31 @@ class Trainer:
                 "batches": int(acc[4].item())}
 
     # ------------------------------------------------------------------ step
-    def train_step(self, x, y, seed: int) -> None:
+    def _poison(self, step: int) -> None:
+        """--fault_inject_overflow_step: make this rank's gradient non-finite (fp16
+        overflow drill) on the given local step."""
+        c = self.cfg
+        if c.fault_inject_overflow_step == step and c.fault_inject_rank in (-1, self.rank):
+            self.flat.grad[0] = float("inf")
+
+    def train_step(self, x, y, seed: int, step: int = -2) -> None:
         R = self.ranges
         scale = self.scaler.scale
         if self.async_ps is not None:
             with R("forward_backward"):
                 self.backend.fwd_bwd(x, y, seed, on_segment=None, grad_scale=scale)
+            self._poison(step)
             if self.scaler.enabled:
                 if not self.scaler.update(self.flat.grad):
-                    return                      # fp16 overflow: nothing is pushed
+                    self.async_ps.skip_step()   # fp16 overflow: nothing is pushed, the
+                    return                      # iteration still counts (lockstep evals)
                 self.flat.grad.mul_(1.0 / scale)
             with R("ps_push_pull"):
                 self.async_ps.push_pull()
             return
         with R("forward_backward"):
             self.backend.fwd_bwd(x, y, seed, on_segment=self.sync.on_segment, grad_scale=scale)
+        self._poison(step)
         with R("grad_sync"):
             self.sync.finish()
         if not self.scaler.update(self.flat.grad):
@@ -288,8 +318,10 @@ class Trainer:
             if cfg.fault_inject_step >= 0 and step == cfg.fault_inject_step and \
                     (cfg.fault_inject_rank < 0 or cfg.fault_inject_rank == self.rank):
                 raise FaultInjected("fault injected at step %d on rank %d" % (step, self.rank))
-            self.train_step(x, y, seed=cfg.seed * 1000003 + step * self.world + self.rank
-                            if self.async_ps is not None else cfg.seed * 1000003 + step)
+            # dropout stream per (step, rank): every replica draws its own masks, as the
+            # reference's independent TF workers do (the hash depends only on the element
+            # index, the seed and the layer)
+            self.train_step(x, y, seed=cfg.seed * 1000003 + step * self.world + self.rank, step=step)
             if prof is not None:
                 prof.step()
             step = self.async_ps.local_steps if self.async_ps is not None else self.flat.global_step
@@ -309,6 +341,7 @@ class Trainer:
                 t_last, imgs_since = time.time(), 0
             if step % self.num_batches == 0:
                 # end of an epoch: evaluate, report, keep last_good_model (test_dist.py:407-446)
+                self._average_extra()
                 tm = self.evaluate()
                 self.log.test(step, tm, step // self.num_batches, cfg.epochs)
                 if self.is_chief:
@@ -323,6 +356,7 @@ class Trainer:
             if hasattr(self.backend, "engine"):
                 self.backend.engine.repack()
             step = self.flat.global_step
+        self._average_extra()
         final = self.evaluate()
         self.log.test(step, final, step // max(self.num_batches, 1), cfg.epochs, final=True)
         if self.is_chief:

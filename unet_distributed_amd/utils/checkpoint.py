@@ -123,6 +123,8 @@ class CheckpointManager:
     def save_last_good(self) -> Optional[str]:
         if self.cfg.no_checkpoint or not self.is_chief:
             return None
+        if self.pre_save is not None:
+            self.pre_save()                 # async PS: the bundle must hold the server's state
         prefix = os.path.join(self.cfg.checkpoint_dir, "last_good_model.cpkt")
         tf_bundle.write_bundle(prefix, flat_to_tensors(self.flat, extra_state=self.extra_state))
         tf_bundle.write_checkpoint_state(self.cfg.checkpoint_dir, "last_good_model.cpkt",
