@@ -1,0 +1,163 @@
+"""Fused Conv + BatchNorm/GroupNorm epilogues (conv_epilogue.h EPI_STATS /
+EPI_DGRAD_NORM) against fp32 PyTorch references.
+
+* forward: the conv writes the pre-norm z and per-tile {sum z, sum z^2} rows; the
+  rows of every tile sum to the reference moments (per sample when the tiles are
+  per-sample, which GroupNorm needs);
+* data gradient: the ReLU / dropout mask of y = dropout(relu(a z + c)) is
+  recomputed from z, and the tile rows sum to {sum g, sum g z}.
+
+The row-window, first-layer, implicit-GEMM and transposed-conv kernels are all
+covered (shapes pick each kernel).
+"""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from test_gpu_kernels import C, nchw, nhwc, pack_dgrad, pack_fwd, ptr, rel_err, stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _moments(z):            # z: [N, H, W, C] -> per-sample [N, 2, C]
+    zf = z.float().reshape(z.shape[0], -1, z.shape[-1])
+    return torch.stack([zf.sum(1), (zf * zf).sum(1)], 1)
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,C2", [
+    (2, 128, 32, 32, 0),      # row window, 128-wide rows
+    (4, 16, 64, 64, 0),       # row window, 16-wide rows
+    (2, 32, 32, 64, 32),      # row window, concat source
+    (8, 8, 128, 256, 0),      # implicit GEMM (8-wide rows), tiles span samples
+    (2, 64, 4, 32, 0),        # first-layer window kernel
+    (2, 256, 32, 32, 0),      # segmented 128-wide windows
+])
+def test_conv_fwd_stats_epilogue(cuda_dev, N, H, Cin, Cout, C2):
+    torch.manual_seed(0)
+    x = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
+    x2 = torch.randn(N, H, H, max(C2, 1), device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, Cin + C2, Cout, device=cuda_dev) * 0.1).bfloat16()
+    b = torch.randn(Cout, device=cuda_dev)
+    z = torch.empty(N, H, H, Cout, device=cuda_dev, dtype=torch.bfloat16)
+    wp = pack_fwd(w)            # kept alive: the kernel reads it after later allocations
+    d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, C2=C2, src1=ptr(x),
+             src2=ptr(x2) if C2 else None, wgt=ptr(wp), bias=ptr(b), Cout=Cout, relu=0, dst1=ptr(z))
+    rows, px = C().conv_stat_tiles(dict(d, stats=1))
+    assert rows > 0
+    st = torch.full((rows, 2, Cout), float("nan"), device=cuda_dev)
+    C().conv_fwd(dict(d, stats=ptr(st)), stream())
+    torch.cuda.synchronize()
+    xin = torch.cat([nchw(x.float()), nchw(x2.float())], 1) if C2 else nchw(x.float())
+    ref = nhwc(F.conv2d(xin, w.float().permute(3, 2, 0, 1), b, padding=1))
+    assert rel_err(z, ref) < 1e-2
+    assert torch.isfinite(st).all()
+    mom = _moments(z)
+    tot = st.sum(0)
+    assert torch.allclose(tot, mom.sum(0), rtol=1e-4, atol=1e-2 * H), (tot - mom.sum(0)).abs().max()
+    if (H * H) % px == 0 and rows % N == 0:
+        per = st.view(N, rows // N, 2, Cout).sum(1)
+        assert torch.allclose(per, mom, rtol=1e-4, atol=1e-2 * H)
+
+
+def _keep(q_idx, C, seed, salt, rate):
+    from unet_distributed_amd.models.reference import _hash_u32
+    h = _hash_u32(q_idx, seed, salt)
+    return h >= int(rate * 4294967296.0)
+
+
+@pytest.mark.parametrize("N,H,Cg,Cy,gn,drop", [
+    (2, 64, 64, 32, False, 0.0),     # row window dgrad (d: 64 -> 32 channels), BatchNorm coefficients
+    (2, 32, 64, 64, True, 0.2),      # GroupNorm coefficients + dropout keep recomputed
+    (8, 8, 256, 128, False, 0.2),    # implicit GEMM dgrad (8-wide)
+    (4, 16, 128, 64, True, 0.0),     # 16-wide window, GroupNorm
+])
+def test_conv_dgrad_norm_epilogue(cuda_dev, N, H, Cg, Cy, gn, drop):
+    """dgrad of a conv whose input y = dropout(relu(a z + c)): g = dgrad * mask, stats."""
+    torch.manual_seed(1)
+    dz = torch.randn(N, H, H, Cg, device=cuda_dev).bfloat16()       # gradient at the conv's output
+    w = (torch.randn(3, 3, Cy, Cg, device=cuda_dev) * 0.1).bfloat16()
+    z = torch.randn(N, H, H, Cy, device=cuda_dev).bfloat16()         # pre-norm input of the conv
+    rows_c = N if gn else 1
+    a = (0.5 + torch.rand(rows_c, Cy, device=cuda_dev))
+    c = 0.3 * torch.randn(rows_c, Cy, device=cuda_dev)
+    g = torch.empty(N, H, H, Cy, device=cuda_dev, dtype=torch.bfloat16)
+    seed, salt = 1234, 7
+    wp = pack_dgrad(w)
+    d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cg, src1=ptr(dz), wgt=ptr(wp),
+             Cout=Cy, relu=0, dst1=ptr(g), nz=ptr(z), na=ptr(a), nc=ptr(c), ncs=Cy if gn else 0,
+             npix=H * H, nd_rate=drop, nd_salt=salt, seed=seed)
+    rows, px = C().conv_stat_tiles(dict(d, stats=1))
+    assert rows > 0
+    st = torch.full((rows, 2, Cy), float("nan"), device=cuda_dev)
+    C().conv_fwd(dict(d, stats=ptr(st)), stream())
+    torch.cuda.synchronize()
+    xr = torch.zeros(N, Cy, H, H, device=cuda_dev, requires_grad=True)
+    (gref,) = torch.autograd.grad(F.conv2d(xr, w.float().permute(3, 2, 0, 1), padding=1), xr, nchw(dz.float()))
+    gref = nhwc(gref)
+    ai = a.view(rows_c, 1, 1, Cy) if gn else a.view(1, 1, 1, Cy)
+    ci = c.view(rows_c, 1, 1, Cy) if gn else c.view(1, 1, 1, Cy)
+    mask = (ai * z.float() + ci) > 0
+    scale = 1.0
+    if drop > 0:
+        q = torch.arange(N * H * H * Cy, device=cuda_dev, dtype=torch.int64).view(N, H, H, Cy)
+        mask = mask & _keep(q, Cy, seed, salt, drop)
+        scale = 1.0 / (1.0 - drop)
+    gref = gref * mask * scale
+    assert rel_err(g, gref) < 1e-2
+    gf, zf = g.float().reshape(N, -1, Cy), z.float().reshape(N, -1, Cy)
+    mom = torch.stack([gf.sum(1), (gf * zf).sum(1)], 1)
+    tot = st.sum(0)
+    assert torch.allclose(tot, mom.sum(0), rtol=1e-3, atol=1e-2 * H)
+    if (H * H) % px == 0 and rows % N == 0:
+        per = st.view(N, rows // N, 2, Cy).sum(1)
+        assert torch.allclose(per, mom, rtol=1e-3, atol=1e-2 * H)
+
+
+def test_tconv_dgrad_norm_epilogue(cuda_dev):
+    """2x2 stride-2 transposed-conv data gradient (window kernel, 32-wide coarse rows)
+    writing the gradient of a BatchNorm'd activation."""
+    torch.manual_seed(2)
+    N, Hc, Ci, Co = 2, 32, 64, 32        # coarse Hc x Hc x Ci -> fine 2Hc x 2Hc x Co
+    dout = torch.randn(N, 2 * Hc, 2 * Hc, Co, device=cuda_dev).bfloat16()
+    wk = (torch.randn(2, 2, Co, Ci, device=cuda_dev) * 0.1).bfloat16()      # (kh, kw, Cout, Cin)
+    z = torch.randn(N, Hc, Hc, Ci, device=cuda_dev).bfloat16()
+    a = 0.5 + torch.rand(Ci, device=cuda_dev)
+    c = 0.3 * torch.randn(Ci, device=cuda_dev)
+    g = torch.empty(N, Hc, Hc, Ci, device=cuda_dev, dtype=torch.bfloat16)
+    # dgrad weights: [Ci][tap (kh, kw)][Co]
+    wdg = torch.zeros(Ci, 64 * ((4 * Co + 63) // 64), device=cuda_dev, dtype=torch.bfloat16)
+    wdg[:, :4 * Co] = wk.permute(3, 0, 1, 2).reshape(Ci, 4 * Co)
+    d = dict(N=N, OH=Hc, OW=Hc, IH=2 * Hc, IW=2 * Hc, KH=2, KW=2, stride=2, pad=0, C1=Co, src1=ptr(dout),
+             wgt=ptr(wdg), Cout=Ci, relu=0, dst1=ptr(g), nz=ptr(z), na=ptr(a), nc=ptr(c), ncs=0, npix=Hc * Hc)
+    rows, px = C().conv_stat_tiles(dict(d, stats=1))
+    assert rows > 0 and px == 256
+    st = torch.zeros(rows, 2, Ci, device=cuda_dev)
+    C().conv_fwd(dict(d, stats=ptr(st)), stream())
+    torch.cuda.synchronize()
+    xr = torch.zeros(N, Ci, Hc, Hc, device=cuda_dev, requires_grad=True)
+    (gref,) = torch.autograd.grad(F.conv_transpose2d(xr, wk.float().permute(3, 2, 0, 1), stride=2), xr,
+                                  nchw(dout.float()))
+    gref = nhwc(gref) * ((a * z.float() + c) > 0)
+    assert rel_err(g, gref) < 1e-2
+    gf, zf = g.float().reshape(-1, Ci), z.float().reshape(-1, Ci)
+    assert torch.allclose(st.sum(0), torch.stack([gf.sum(0), (gf * zf).sum(0)]), rtol=1e-3, atol=0.5)
+
+
+def test_maxpool_all_zero_window_routes_nothing(cuda_dev):
+    """A 2x2 window of clipped (zero) ReLU outputs passes no gradient (relu'(0) = 0);
+    the argmax-code and recompute paths agree."""
+    N, H, Cc = 1, 4, 8
+    x = torch.zeros(N, H, H, Cc, device=cuda_dev, dtype=torch.bfloat16)
+    x[0, 0, 0, :] = 1.0                  # window (0, 0) has a positive max, the others are all zero
+    y = torch.empty(N, H // 2, H // 2, Cc, device=cuda_dev, dtype=torch.bfloat16)
+    code = torch.zeros(y.numel() // 8, device=cuda_dev, dtype=torch.int32)
+    C().generic("pool_fwd", [ptr(x), ptr(y), ptr(code)], [N, 1, H, H, Cc, 0], [], stream())
+    dy = torch.ones_like(y)
+    dx1, dx2 = torch.empty_like(x), torch.empty_like(x)
+    C().generic("pool_bwd", [ptr(x), ptr(dy), 0, ptr(dx1)], [N, 1, H, H, Cc, 0], [], stream())
+    C().generic("pool_bwd", [0, ptr(dy), 0, ptr(dx2), ptr(code)], [N, 1, H, H, Cc, 0], [], stream())
+    torch.cuda.synchronize()
+    ref = torch.zeros_like(x)
+    ref[0, 0, 0, :] = 1.0
+    assert torch.equal(dx1, ref) and torch.equal(dx2, ref)

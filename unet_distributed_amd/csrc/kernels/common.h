@@ -64,6 +64,15 @@ __device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
 #endif
 }
 
+// the two 16-bit elements of a 32-bit word as floats
+__device__ __forceinline__ f32x2 unpack2(uint32_t w) {
+#ifdef UNET_FP16
+  return __builtin_convertvector(__builtin_bit_cast(h16x2, w), f32x2);
+#else
+  return (f32x2){__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+#endif
+}
+
 // one packed convert (round-to-nearest-even) for two values
 __device__ __forceinline__ uint32_t pack2h(float a, float b) {
   const f32x2 v = {a, b};

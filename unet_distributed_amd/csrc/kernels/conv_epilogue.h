@@ -30,11 +30,37 @@ __device__ __forceinline__ PixCoord decompose(int q, int OD, int OH, int OW) {
 
 // EPI selects a specialised epilogue (launch-time choice, conv_epi_mode below):
 //   0 generic (every feature read from p at run time), 1 forward (bias + ReLU only),
-//   2 data gradient (mask scales, consumer ReLU masks, optional channel split).
-enum { EPI_GENERIC = 0, EPI_FWD = 1, EPI_DGRAD = 2 };
+//   2 data gradient (mask scales, consumer ReLU masks, optional channel split),
+//   3 pre-normalisation forward (bias, no activation) + per-tile {sum z, sum z^2},
+//   4 data gradient of a normalised activation: ReLU / dropout mask recomputed from the
+//     pre-norm tensor and the norm coefficients + per-tile {sum g, sum g z}.
+// Modes 3 / 4 are the fused Conv+BatchNorm/GroupNorm blocks: the statistics leave the
+// kernel as fixed-order per-tile partials (no atomics, bit-reproducible).
+enum { EPI_GENERIC = 0, EPI_FWD = 1, EPI_DGRAD = 2, EPI_STATS = 3, EPI_DGRAD_NORM = 4 };
+
+// LDS of the epilogue: the BM x BN staging tile plus [4 waves][2][BN] fp32 of
+// statistics partials (modes 3 / 4)
+template <int BM, int BN>
+constexpr int epi_lds_bytes() {
+  return BM * (BN + 4) * 2 + 4 * 2 * BN * 4;
+}
+
+// nullptr when the normalisation fields of p form a supported epilogue
+__host__ __device__ inline const char* conv_norm_epi_check(const ConvFwdParams& p) {
+  if (!p.stats && !p.nz) return nullptr;
+  if (!p.stats) return "conv_fwd: nz (dgrad-norm epilogue) needs a stats buffer";
+  if (p.relu || p.shuffle || p.drop_rate > 0.f || p.out_scale != 1.f || p.D1 != p.Cout || p.mask1 || p.mask2 ||
+      p.head_w)
+    return "conv_fwd: statistics epilogue takes no ReLU / dropout / shuffle / scale / split / mask / head";
+  if (p.nz && (p.bias || !p.na || !p.nc || p.npix <= 0 || p.mask_scale1 != 1.f || (p.ncs != 0 && p.ncs != p.Cout)))
+    return "conv_fwd: dgrad-norm epilogue needs na / nc / npix, no bias";
+  return nullptr;
+}
 
 __host__ __device__ inline int conv_epi_mode(const ConvFwdParams& p) {
-  if (p.stats || p.shuffle || p.drop_rate > 0.f || p.out_scale != 1.f) return EPI_GENERIC;
+  if (p.nz) return EPI_DGRAD_NORM;
+  if (p.stats) return EPI_STATS;
+  if (p.shuffle || p.drop_rate > 0.f || p.out_scale != 1.f) return EPI_GENERIC;
   if (p.relu && p.D1 == p.Cout && !p.mask1 && !p.mask2 && p.mask_scale1 == 1.f) return EPI_FWD;
   if (!p.relu && !p.bias) return EPI_DGRAD;
   return EPI_GENERIC;
@@ -59,12 +85,13 @@ struct StripTiles {
 // wider than one window, or any row-window kernel): tile pixel ml is at row
 // m0 + ml / SEGW (m0 = first row), column col0 + ml % SEGW of rows `pitch` pixels wide.
 // SEGW == 0: tile pixel ml is output pixel m0 + ml.
+// stat_row: this tile's row of p.stats (modes 3 / 4).
 template <int BM, int BN, int WM, int WN, int TM, int TN, int NTHR, int EPI = EPI_GENERIC,
           class MapM = LinearTiles<WM>, int SEGW = 0>
 __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc)[TM][TN], char* smem,
                                               const int m0, const int n0, const int M, const int wm,
                                               const int wn, const int lane, const int tid,
-                                              const int pitch = 0, const int col0 = 0) {
+                                              const int pitch = 0, const int col0 = 0, const int stat_row = 0) {
   auto qof = [&](int ml) -> int {
     if constexpr (SEGW > 0) return (m0 + ml / SEGW) * pitch + col0 + (ml % SEGW);
     else return m0 + ml;
@@ -73,13 +100,15 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
   // register phase: acc[i][j][r] = out[pixel = m0 + wm*WM + i*16 + (lane&15)]
   //                                   [chan  = n0 + wn*WN + j*16 + (lane>>4)*4 + r]
   char* E = smem;
+  float* SP = (float*)(smem + BM * EPI_STRIDE);       // [4][2][BN] statistics partials
   constexpr bool G = EPI == EPI_GENERIC;
+  constexpr bool kNormG = EPI == EPI_DGRAD_NORM;
   const bool kRelu = G ? (p.relu != 0) : (EPI == EPI_FWD);
-  const bool kBias = EPI != EPI_DGRAD && p.bias;
+  const bool kBias = EPI != EPI_DGRAD && !kNormG && p.bias;
   const bool kDrop = G && p.drop_rate > 0.f;
-  const bool kStats = G && p.stats;
+  constexpr bool kStats = EPI == EPI_STATS;
   const bool kShuffle = G && p.shuffle;
-  constexpr bool kMaskScale = EPI != EPI_FWD;
+  constexpr bool kMaskScale = EPI == EPI_GENERIC || EPI == EPI_DGRAD;
   const float inv_keep = p.drop_rate > 0.f ? 1.f / (1.f - p.drop_rate) : 1.f;
   const uint32_t drop_thr = (uint32_t)(p.drop_rate * 4294967296.0);
   const uint32_t seed = (kDrop && p.seed_ptr) ? *p.seed_ptr : p.seed;
@@ -94,7 +123,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       bsv[r] = kBias ? p.bias[kShuffle ? (n + r) % Dtb : n + r] : 0.f;
       msc[r] = kMaskScale ? ((n + r < p.D1) ? p.mask_scale1 : p.mask_scale2) : 1.f;
     }
-    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int ml = MapM::base(wm, i) + (lane & 15);
@@ -111,33 +139,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
         if (kMaskScale) x *= msc[r];
         v[r] = x;
       }
-      if (kStats && q < M) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float xr = (float)(h16)v[r];
-          s1[r] += xr;
-          s2[r] += xr * xr;
-        }
-      }
       u32x2 pk;
       pk[0] = pack2h(v[0], v[1]);
       pk[1] = pack2h(v[2], v[3]);
       *(u32x2*)(E + ml * EPI_STRIDE + nl * 2) = pk;
-    }
-    if (kStats) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float a = s1[r], b = s2[r];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          a += __shfl_xor(a, o, 64);
-          b += __shfl_xor(b, o, 64);
-        }
-        if ((lane & 15) == 0) {
-          atomicAdd(p.stats + n + r, a);
-          atomicAdd(p.stats + p.Cout + n + r, b);
-        }
-      }
     }
   }
   __syncthreads();
@@ -145,6 +150,123 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
   // coalesced phase: 16-byte chunks, consecutive threads -> consecutive channels
   constexpr int CPR = BN / 8;
   constexpr int NCHUNK = BM * CPR;
+  // statistics rows (modes 3 / 4): thread (chunk column cb) holds s1[8], s2[8] of its
+  // rows; lanes congruent mod CPR are summed by xor shuffles, then the NTHR / 64 waves
+  // in fixed order through LDS -> p.stats[stat_row][mom][n0 + c]
+  auto stats_out = [&](float (&s1)[8], float (&s2)[8], int cb) {
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    const int wv = tid >> 6;
+    if ((tid & 63) < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        SP[(wv * 2 + 0) * BN + cb * 8 + e] = s1[e];
+        SP[(wv * 2 + 1) * BN + cb * 8 + e] = s2[e];
+      }
+    }
+    __syncthreads();
+    for (int t = tid; t < 2 * BN; t += NTHR) {
+      const int mom = t / BN, c = t - mom * BN;
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < NTHR / 64; ++w) a += SP[(w * 2 + mom) * BN + c];
+      p.stats[((size_t)stat_row * 2 + mom) * p.Cout + n0 + c] = a;
+    }
+  };
+  if constexpr (kStats) {
+    // pre-normalisation output z: store, and accumulate {sum z, sum z^2} of the stored
+    // (bf16-rounded) values the consumers will read
+    static_assert(NCHUNK % NTHR == 0 && NTHR % CPR == 0 && CPR <= 64, "statistics tiling");
+    constexpr int NIT = NCHUNK / NTHR, RPI = NTHR / CPR;
+    const int cb = tid % CPR, ml0 = tid / CPR;
+    const int n = n0 + cb * 8;
+    h16* dst = (h16*)p.dst1;
+    float s1[8], s2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int ml = ml0 + it * RPI;
+      const int q = qof(ml);
+      if (q >= M) continue;
+      const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
+      const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
+      const u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
+      *(u32x4*)(dst + (size_t)q * p.Cout + n) = v;
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += f[e];
+        s2[e] = fmaf(f[e], f[e], s2[e]);
+      }
+    }
+    stats_out(s1, s2, cb);
+    return;
+  }
+  if constexpr (kNormG) {
+    // gradient of y = dropout(relu(na z + nc)): mask recomputed from the pre-norm z the
+    // forward stored (the normalised y is never needed), plus the tile's {sum g, sum g z}
+    static_assert(NCHUNK % NTHR == 0 && NTHR % CPR == 0 && CPR <= 64, "dgrad-norm tiling");
+    constexpr int NIT = NCHUNK / NTHR, RPI = NTHR / CPR;
+    const int cb = tid % CPR, ml0 = tid / CPR;
+    const int n = n0 + cb * 8;
+    h16* dst = (h16*)p.dst1;
+    const h16* zt = (const h16*)p.nz;
+    // a tile never spans two samples when the coefficients are per sample (host check)
+    const size_t crow = p.ncs ? (size_t)(qof(0) / p.npix) * p.ncs : 0;
+    float ca[8], cc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      ca[e] = p.na[crow + n + e];
+      cc[e] = p.nc[crow + n + e];
+    }
+    u32x4 zv[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int q = qof(ml0 + it * RPI);
+      if (q < M) zv[it] = *(const u32x4*)(zt + (size_t)q * p.Cout + n);
+    }
+    const bool drop = p.nd_rate > 0.f;
+    const float dscale = drop ? 1.f / (1.f - p.nd_rate) : 1.f;
+    const uint32_t dthr = (uint32_t)(p.nd_rate * 4294967296.0);
+    const uint32_t dseed = p.seed_ptr ? *p.seed_ptr : p.seed;
+    float s1[8], s2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int ml = ml0 + it * RPI;
+      const int q = qof(ml);
+      if (q >= M) continue;
+      const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
+      const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
+      float g[8], z[8];
+      unpack8((u32x4){lo[0], lo[1], hi[0], hi[1]}, g);
+      unpack8(zv[it], z);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        bool keep = fmaf(ca[e], z[e], cc[e]) > 0.f;
+        if (drop) keep = keep && drop_hash((uint64_t)q * p.Cout + n + e, dseed, p.nd_salt) >= dthr;
+        g[e] = keep ? g[e] * dscale : 0.f;
+      }
+      const u32x4 gv = pack8(g);
+      *(u32x4*)(dst + (size_t)q * p.Cout + n) = gv;
+      unpack8(gv, g);                                   // the stored (rounded) gradient
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += g[e];
+        s2[e] = fmaf(g[e], z[e], s2[e]);
+      }
+    }
+    stats_out(s1, s2, cb);
+    return;
+  }
   if constexpr (EPI == EPI_DGRAD && NCHUNK % NTHR == 0 && NTHR % CPR == 0) {
     // a thread's channel chunk (hence destination tensor, row stride and mask) is the
     // same for all its rows: issue every ReLU-mask load first, then mask and store
@@ -226,7 +348,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     size_t off;
     h16* dst;
     const void* mk;
-    if (EPI == EPI_FWD) {
+    if (EPI == EPI_FWD || EPI == EPI_STATS) {
       off = (size_t)q * p.Cout + n;
       dst = (h16*)p.dst1;
       mk = nullptr;
@@ -257,7 +379,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       dst = (h16*)p.dst2;
       mk = p.mask2;
     }
-    if (EPI != EPI_FWD && mk) {
+    if (EPI != EPI_FWD && EPI != EPI_STATS && mk) {
       const u32x4 mv = *(const u32x4*)((const h16*)mk + off);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {

@@ -42,7 +42,7 @@ __device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
 
 // MODE 0: plain; MODE 1: src1 nearest-upsampled x2; MODE 2: first layer (Cin 4/8).
 // CONCAT: a second source supplies channels [C1, C1 + C2) (decoder skip concat).
-template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, bool CONCAT>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, bool CONCAT, int EPI = EPI_GENERIC>
 __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
   constexpr int BR = (BN + 31) / 32;                // B rows per thread
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int EPI_BYTES = BM * (BN + 4) * 2;
+  constexpr int EPI_BYTES = (EPI == EPI_STATS || EPI == EPI_DGRAD_NORM) ? epi_lds_bytes<BM, BN>() : BM * (BN + 4) * 2;
   constexpr int LDS_BYTES = (2 * STAGE > EPI_BYTES) ? 2 * STAGE : EPI_BYTES;
   static_assert(WAVES_M * WAVES_N == 4, "4 waves");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
     __syncthreads();
   }
 
-  conv_epilogue<BM, BN, WM, WN, TM, TN, NTHR>(p, acc, smem, m0, n0, M, wm, wn, lane, tid);
+  conv_epilogue<BM, BN, WM, WN, TM, TN, NTHR, EPI>(p, acc, smem, m0, n0, M, wm, wn, lane, tid, 0, 0, tm);
 }
 
 template <int BM, int BN, int WAVES_M, int WAVES_N>
@@ -273,6 +273,26 @@ hipError_t launch_cfg(const ConvFwdParams& p, hipStream_t s) {
   const int M = p.N * p.OD * p.OH * p.OW;
   const int grid = ((M + BM - 1) / BM) * (p.Cout / BN);
   const bool smallc = (p.C1 == 4 || p.C1 == 8) && p.C2 == 0;
+  const int epi = conv_epi_mode(p);
+  if (epi == EPI_STATS || epi == EPI_DGRAD_NORM) {
+    // fused-normalisation epilogues: plain (MODE 0) or first-layer (MODE 2) sources
+    if (p.up1 != 1) return hipErrorInvalidValue;
+    if (epi == EPI_DGRAD_NORM && !smallc && p.C2 == 0)
+      hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, false, EPI_DGRAD_NORM>), dim3(grid), dim3(NTHR),
+                         0, s, p);
+    else if (epi == EPI_STATS && smallc)
+      hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 2, false, EPI_STATS>), dim3(grid), dim3(NTHR), 0,
+                         s, p);
+    else if (epi == EPI_STATS && p.C2 > 0)
+      hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, true, EPI_STATS>), dim3(grid), dim3(NTHR), 0, s,
+                         p);
+    else if (epi == EPI_STATS)
+      hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, false, EPI_STATS>), dim3(grid), dim3(NTHR), 0,
+                         s, p);
+    else
+      return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if (smallc)
     hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 2, false>), dim3(grid), dim3(NTHR), 0, s, p);
   else if (p.up1 == 2)
@@ -319,7 +339,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   constexpr int ROWB = HWP * 64;
   constexpr int XI = HR * IPR, WI = 9 * BN / 16;
   constexpr int XB = XI * 1024, WB = WI * 1024;
-  constexpr int EPIB = BM * (BN + 4) * 2;
+  constexpr int EPIB = (EPI == EPI_STATS || EPI == EPI_DGRAD_NORM) ? epi_lds_bytes<BM, BN>() : BM * (BN + 4) * 2;
   constexpr int LDS_BYTES = (XB + WB > EPIB) ? XB + WB : EPIB;
   constexpr int WMP = BM / 4;                   // pixels per wave
   constexpr int TM = WMP / 16, TN = BN / 16;
@@ -522,9 +542,10 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   }
   __syncthreads();
   if constexpr (GEO == GEO_SEG)
-    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, W>(p, acc, smem, g0, n0, M, wave, 0, lane, tid, Wf, col0);
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, W>(p, acc, smem, g0, n0, M, wave, 0, lane, tid, Wf, col0,
+                                                              tm);
   else
-    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid);
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0, 0, tm);
 }
 
 
@@ -550,7 +571,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_first_kernel(const ConvFwdParam
   constexpr int XB = XI * 1024;
   constexpr int BN = 32, TM = 8, TN = 2;
   constexpr int KS = (9 * CIN + 31) / 32;                      // MFMA K-steps
-  constexpr int EPIB = BM * (BN + 4) * 2;
+  constexpr int EPIB = (EPI == EPI_STATS) ? epi_lds_bytes<BM, BN>() : BM * (BN + 4) * 2;
   constexpr int LDS_BYTES = XB > EPIB ? XB : EPIB;
   constexpr int TPR = W / 16;
   static_assert((CIN == 4 || CIN == 8) && W >= 16 && W <= 128 && BM % W == 0, "first-layer window");
@@ -648,7 +669,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_first_kernel(const ConvFwdParam
     }
   }
   __syncthreads();
-  conv_epilogue<BM, BN, 128, BN, TM, TN, NTHR, EPI>(p, acc, smem, m0, n0, M, wave, 0, lane, tid);
+  conv_epilogue<BM, BN, 128, BN, TM, TN, NTHR, EPI>(p, acc, smem, m0, n0, M, wave, 0, lane, tid, 0, 0, tm);
 }
 
 template <int CIN>
@@ -656,11 +677,14 @@ hipError_t launch_win_first(const ConvFwdParams& p, hipStream_t s) {
   const int W = p.OW;
   const int R = 512 / W;
   const int grid = ((p.N * p.OH + R - 1) / R) * (p.Cout / 32);
-  const bool fwd = conv_epi_mode(p) == EPI_FWD;
+  const int epi = conv_epi_mode(p);
+  const bool fwd = epi == EPI_FWD;
 #define WF_CASE(WW)                                                                                        \
   case WW:                                                                                                 \
     if (fwd)                                                                                               \
       hipLaunchKernelGGL((conv_win_first_kernel<WW, CIN, EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p);     \
+    else if (epi == EPI_STATS)                                                                             \
+      hipLaunchKernelGGL((conv_win_first_kernel<WW, CIN, EPI_STATS>), dim3(grid), dim3(NTHR), 0, s, p);   \
     else                                                                                                   \
       hipLaunchKernelGGL((conv_win_first_kernel<WW, CIN, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p); \
     break;
@@ -804,7 +828,7 @@ __global__ void __launch_bounds__(NTHR) tconv_dgrad_kernel(const ConvFwdParams p
   constexpr int YI = (2 * R * FW) / 16;                 // dy image DMA instructions per chunk
   constexpr int WI = 4 * BN / 16;
   constexpr int YB = YI * 1024, WB = WI * 1024;
-  constexpr int EPIB = BMc * (BN + 4) * 2;
+  constexpr int EPIB = (EPI == EPI_DGRAD_NORM) ? epi_lds_bytes<BMc, BN>() : BMc * (BN + 4) * 2;
   constexpr int LDS_BYTES = (YB + WB > EPIB) ? YB + WB : EPIB;
   constexpr int TM = BMc / 4 / 16, TN = BN / 16;
   static_assert(BMc % W == 0 && W >= 8 && W <= 128, "tconv window");
@@ -882,7 +906,7 @@ __global__ void __launch_bounds__(NTHR) tconv_dgrad_kernel(const ConvFwdParams p
     }
   }
   __syncthreads();
-  conv_epilogue<BMc, BN, BMc / 4, BN, TM, TN, NTHR, EPI>(p, acc, smem, m0, n0, Mc, wave, 0, lane, tid);
+  conv_epilogue<BMc, BN, BMc / 4, BN, TM, TN, NTHR, EPI>(p, acc, smem, m0, n0, Mc, wave, 0, lane, tid, 0, 0, tm);
 }
 
 hipError_t launch_tconv_fwd(const ConvFwdParams& p, hipStream_t s) {
@@ -904,11 +928,14 @@ hipError_t launch_tconv_dgrad(const ConvFwdParams& p, hipStream_t s) {
   const int W = p.OW;
   const int R = 256 / W;
   const int grid = ((p.N * p.OH + R - 1) / R) * (p.Cout / 64);
-  const bool dg = conv_epi_mode(p) == EPI_DGRAD;
+  const int epi = conv_epi_mode(p);
+  const bool dg = epi == EPI_DGRAD;
 #define TD_CASE(WW)                                                                                          \
   case WW:                                                                                                   \
     if (dg)                                                                                                  \
       hipLaunchKernelGGL((tconv_dgrad_kernel<WW, 64, EPI_DGRAD>), dim3(grid), dim3(NTHR), 0, s, p);       \
+    else if (epi == EPI_DGRAD_NORM)                                                                          \
+      hipLaunchKernelGGL((tconv_dgrad_kernel<WW, 64, EPI_DGRAD_NORM>), dim3(grid), dim3(NTHR), 0, s, p);  \
     else                                                                                                     \
       hipLaunchKernelGGL((tconv_dgrad_kernel<WW, 64, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p);     \
     break;
@@ -942,6 +969,12 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
     hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_FWD, GG>), dim3(grid), dim3(NTHR), 0, s, p);     \
   else if (epi == EPI_DGRAD)                                                                              \
     hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_DGRAD, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
+  else if (epi == EPI_STATS)                                                                              \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_STATS, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
+  else if (epi == EPI_DGRAD_NORM && !CC)                                                                  \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, false, EPI_DGRAD_NORM, GG>), dim3(grid), dim3(NTHR), 0, s, p); \
+  else if (epi == EPI_DGRAD_NORM)                                                                         \
+    return hipErrorInvalidValue;                                                                          \
   else                                                                                                    \
     hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_GENERIC, GG>), dim3(grid), dim3(NTHR), 0, s, p);
 #define WIN_GEO(WW, CC)                                                                                   \
@@ -991,7 +1024,7 @@ static bool win_eligible(const ConvFwdParams& p) {
   const int R = (W == 16 ? 256 : 512) / W;     // window rows
   const bool dims_ok = (p.KD == 1 && p.OD == 1 && p.ID == 1) || (p.KD == 3 && p.OD == p.ID && p.OD > 1 && p.OW <= 128);
   return w_ok && p.OH % R == 0 && dims_ok && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.pad == 1 &&
-         p.up1 == 1 && !p.shuffle && !p.stats && p.IW == p.OW && p.IH == p.OH &&
+         p.up1 == 1 && !p.shuffle && p.IW == p.OW && p.IH == p.OH &&
          (p.C1 % 32) == 0 && (p.C2 % 32) == 0 && p.C1 > 0;
 }
 
@@ -999,7 +1032,7 @@ static bool win_eligible(const ConvFwdParams& p) {
 static bool win_first_eligible(const ConvFwdParams& p) {
   const bool w_ok = p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128;
   return p.KD == 1 && p.OD == 1 && p.ID == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.pad == 1 &&
-         p.up1 == 1 && !p.shuffle && !p.stats && w_ok && p.IW == p.OW && p.IH == p.OH && p.C2 == 0 &&
+         p.up1 == 1 && !p.shuffle && !p.nz && w_ok && p.IW == p.OW && p.IH == p.OH && p.C2 == 0 &&
          (p.C1 == 4 || p.C1 == 8) && p.Cout % 32 == 0 && p.D1 == p.Cout;
 }
 
@@ -1017,7 +1050,7 @@ static bool tconv_dgrad_eligible(const ConvFwdParams& p) {
   const bool w_ok = p.OW == 32 || p.OW == 64;
   return !p.shuffle && p.KD == 1 && p.KH == 2 && p.KW == 2 && p.stride == 2 && p.pad == 0 && p.OD == 1 &&
          p.ID == 1 && w_ok && p.IW == 2 * p.OW && p.IH == 2 * p.OH && p.up1 == 1 && p.C2 == 0 &&
-         (p.C1 % 32) == 0 && (p.Cout % 64) == 0 && !p.stats && p.drop_rate == 0.f;
+         (p.C1 % 32) == 0 && (p.Cout % 64) == 0 && (!p.stats || p.nz) && p.drop_rate == 0.f;
 }
 
 int conv_fwd_pick(const ConvFwdParams& p);
@@ -1048,7 +1081,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.shuffle && (p.Cout % (1 << p.shuffle))) return "conv_fwd: shuffle needs Cout % taps == 0";
   if (p.shuffle && ((p.Cout >> p.shuffle) % 8)) return "conv_fwd: shuffle channels must be multiples of 8";
   if (p.shuffle && p.D1 != p.Cout) return "conv_fwd: shuffle with channel split unsupported";
-  if (p.stats && p.shuffle) return "conv_fwd: stats with shuffle unsupported";
+  if (const char* m = conv_norm_epi_check(p)) return m;
   if (p.tile < 0 || p.tile > 11) return "conv_fwd: bad tile id";
   if (p.tile == 10 && !tconv_fwd_eligible(p)) return "conv_fwd: transposed-conv window tile not applicable";
   if (p.tile == 11 && !tconv_dgrad_eligible(p)) return "conv_fwd: transposed-conv dgrad tile not applicable";
@@ -1104,6 +1137,46 @@ int conv_fwd_pick(const ConvFwdParams& p) {
 }
 
 int conv_fwd_grid(const ConvFwdParams& p) { return conv_fwd_pick(p) == 6 ? win_grid<32>(p) : 0; }
+
+void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
+  *rows = *tile_px = 0;
+  const int M = p.N * p.OD * p.OH * p.OW;
+  const int t = conv_fwd_pick(p);
+  const bool smallc = (p.C1 == 4 || p.C1 == 8) && p.C2 == 0;
+  switch (t) {
+    case 6: {        // row window: R rows x (segment) width, tiles in (row group, segment) order
+      const int W = p.OW > 128 ? 128 : p.OW;
+      const int R = (W == 16 ? 256 : 512) / W;
+      if (p.nz && p.C2) return;
+      *rows = ((p.N * p.OD * p.OH + R - 1) / R) * (p.OW / W);
+      *tile_px = R * W;
+      return;
+    }
+    case 9: {
+      const int R = 512 / p.OW;
+      if (p.nz) return;
+      *rows = (p.N * p.OH + R - 1) / R;
+      *tile_px = 512;
+      return;
+    }
+    case 11: {
+      const int R = 256 / p.OW;
+      if (!p.nz) return;
+      *rows = (p.N * p.OH + R - 1) / R;
+      *tile_px = 256;
+      return;
+    }
+    case 10:
+      return;
+    default: {
+      if (p.up1 != 1 || (p.nz && (smallc || p.C2))) return;
+      const int BM = (t == 3 || t == 5) ? 256 : 128;
+      *rows = (M + BM - 1) / BM;
+      *tile_px = BM;
+      return;
+    }
+  }
+}
 
 hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
   switch (conv_fwd_pick(p)) {

@@ -36,7 +36,22 @@ struct ConvFwdParams {
   const void* mask2;
   float mask_scale1, mask_scale2;
   int shuffle;                // 0, or number of upsampled dims (2/3): tconv pixel shuffle
-  float* stats;               // nullptr or [2][Cout] per-channel sum / sum of squares (BN)
+  // Fused normalisation statistics (deterministic: per-tile partial sums, no atomics).
+  // stats: nullptr or [rows][2][Cout] -- one row per M tile of the launch
+  // (conv_stat_tiles).  Forward (EPI_STATS): row = {sum z, sum z^2} of the tile's
+  // bf16-rounded outputs.  Data gradient (EPI_DGRAD_NORM): {sum g, sum g * nz}.
+  float* stats;
+  // EPI_DGRAD_NORM: the destination is the gradient of a normalised activation
+  // y = dropout(relu(u)), u = na * nz + nc; the gradient is masked by u > 0 and the
+  // forward's dropout keep (recomputed from nd_rate / seed / nd_salt, scaled by
+  // 1 / (1 - nd_rate)).  na / nc: [Cout] (BatchNorm, ncs = 0) or [N][Cout]
+  // (GroupNorm, ncs = Cout; pixel q's sample is q / npix).
+  const void* nz;
+  const float* na;
+  const float* nc;
+  int ncs, npix;
+  float nd_rate;
+  uint32_t nd_salt;
   int tile;                   // 0 = auto, else forced tile config id (tuning / A-B tests)
   // Fused segmentation head (row-window forward, Cout == 32, EPI_FWD only): per pixel
   // z = sum_c out[c] head_w[c] + head_b -> head_logit (fp32) for head_finish

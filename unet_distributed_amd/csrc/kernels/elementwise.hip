@@ -7,6 +7,9 @@
 //    fuses the add of the skip-connection gradient coming from the decoder
 //    (the concat's dgrad), so the encoder output gradient is written once.  The
 //    forward can record the argmax per channel (2-3 bit codes) for the backward.
+//    The pooled tensor is always a ReLU output (convNb), and the backward applies
+//    that ReLU's derivative too: a window whose maximum is 0 (every input clipped)
+//    routes nothing (TF: relu'(0) = 0), so the encoder gradient needs no extra mask.
 //  * upsample2_bwd: 2x2(x2) sum of the full-res gradient of the folded nearest
 //    upsample (`model.py:76-109` upsampling variant), masked by the source's ReLU.
 #include "common.h"
@@ -86,9 +89,10 @@ __global__ void __launch_bounds__(256) maxpool2_fwd_kernel(const h16* __restrict
         }
     *(u32x4*)(y + (size_t)i * 8) = pack8(m);
     if (code) {
+      // bits [bits*e ..): argmax of channel e; bit 24 + e: its maximum is positive
       uint32_t w = 0;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) w |= (uint32_t)arg[e] << (bits * e);
+      for (int e = 0; e < 8; ++e) w |= ((uint32_t)arg[e] << (bits * e)) | ((m[e] > 0.f ? 1u : 0u) << (24 + e));
       code[i] = w;
     }
   }
@@ -146,7 +150,7 @@ __global__ void __launch_bounds__(256) maxpool2_bwd_kernel(const h16* __restrict
           }
 #pragma unroll
           for (int e = 0; e < 8; ++e)
-            if (arg[e] == k) o[e] += g[e];
+            if (arg[e] == k && best[e] > 0.f) o[e] += g[e];
           *(u32x4*)(dx + off) = pack8(o);
         }
   }
@@ -185,7 +189,7 @@ __global__ void __launch_bounds__(256) maxpool2_bwd_code_kernel(const uint32_t* 
           }
 #pragma unroll
           for (int e = 0; e < 8; ++e)
-            if (((w >> (bits * e)) & kmask) == k) o[e] += g[e];
+            if (((w >> (bits * e)) & kmask) == k && ((w >> (24 + e)) & 1u)) o[e] += g[e];
           *(u32x4*)(dx + off) = pack8(o);
         }
   }

@@ -115,12 +115,19 @@ __global__ void __launch_bounds__(NT) bn_finalize_kernel(const float* __restrict
                                                          float* __restrict__ run_var, float* __restrict__ mean,
                                                          float* __restrict__ rstd, float* __restrict__ ca,
                                                          float* __restrict__ cb, float* __restrict__ cc,
-                                                         float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                                         float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                         const float* __restrict__ beta, float* __restrict__ fa,
+                                                         float* __restrict__ fc) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= C) return;
   if (mode == 2) {
-    mean[c] = run_mean[c];
-    rstd[c] = rsqrtf(run_var[c] + eps);
+    const float mu = run_mean[c], r = rsqrtf(run_var[c] + eps);
+    mean[c] = mu;
+    rstd[c] = r;
+    if (fa) {
+      fa[c] = gamma[c] * r;
+      fc[c] = beta[c] - mu * gamma[c] * r;
+    }
     return;
   }
   float s1 = 0.f, s2 = 0.f;
@@ -131,8 +138,13 @@ __global__ void __launch_bounds__(NT) bn_finalize_kernel(const float* __restrict
   if (mode == 0) {
     const float mu = s1 / count;
     const float var = fmaxf(s2 / count - mu * mu, 0.f);
+    const float r = rsqrtf(var + eps);
     mean[c] = mu;
-    rstd[c] = rsqrtf(var + eps);
+    rstd[c] = r;
+    if (fa) {            // relu-input coefficients u = fa z + fc (fused consumers)
+      fa[c] = gamma[c] * r;
+      fc[c] = beta[c] - mu * gamma[c] * r;
+    }
     run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
     run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * (count / fmaxf(count - 1.f, 1.f));
   } else {
@@ -154,7 +166,8 @@ __global__ void __launch_bounds__(NT) gn_finalize_kernel(const float* __restrict
                                                          int mode, const float* __restrict__ gamma, float eps,
                                                          float* __restrict__ mean, float* __restrict__ rstd,
                                                          float* __restrict__ ca, float* __restrict__ cb,
-                                                         float* __restrict__ cc) {
+                                                         float* __restrict__ cc, const float* __restrict__ beta,
+                                                         float* __restrict__ fa, float* __restrict__ fc) {
   const int i = blockIdx.x * NT + threadIdx.x;
   if (i >= N * G) return;
   const int n = i / G, g = i - n * G;
@@ -173,6 +186,10 @@ __global__ void __launch_bounds__(NT) gn_finalize_kernel(const float* __restrict
     for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
       mean[(size_t)n * C + c] = mu;
       rstd[(size_t)n * C + c] = r;
+      if (fa) {
+        fa[(size_t)n * C + c] = gamma[c] * r;
+        fc[(size_t)n * C + c] = beta[c] - mu * gamma[c] * r;
+      }
     }
   } else {
     const float mu = mean[(size_t)n * C + g * Cg], r = rstd[(size_t)n * C + g * Cg];
@@ -358,25 +375,34 @@ hipError_t norm_moments_launch(const void* A, const void* B, int N, int P, int C
   return hipGetLastError();
 }
 
+// S[n][2][C] = sum of the nbp consecutive partial rows of sample n (rows written by
+// a conv epilogue's per-tile statistics, conv_epilogue.h EPI_STATS / EPI_DGRAD_NORM)
+hipError_t moments_collect_launch(const float* partial, int N, int C, int nbp, float* S, hipStream_t s) {
+  hipLaunchKernelGGL(moments_collect_kernel, dim3(ew_grid((long long)N * 2 * C)), dim3(NT), 0, s, partial, N, C, nbp,
+                     S);
+  return hipGetLastError();
+}
+
 int sample_slices(int N) { return N < 64 ? N : 64; }
 
 hipError_t bn_finalize_launch(const float* S, int N, int C, float count, int mode, const float* gamma, float eps,
                               float momentum, float* run_mean, float* run_var, float* mean, float* rstd, float* ca,
-                              float* cb, float* cc, float* dgamma, float* dbeta, float* partial, hipStream_t s) {
+                              float* cb, float* cc, float* dgamma, float* dbeta, float* partial, const float* beta,
+                              float* fa, float* fc, hipStream_t s) {
   const int nsl = sample_slices(N);
   if (mode != 2)
     hipLaunchKernelGGL(sample_slices_kernel, dim3((C + 63) / 64, nsl), dim3(NT), 0, s, S, N, C, nsl,
                        (const float*)nullptr, (const float*)nullptr, partial);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, partial, nsl, C, count, mode, gamma,
-                     eps, momentum, run_mean, run_var, mean, rstd, ca, cb, cc, dgamma, dbeta);
+                     eps, momentum, run_mean, run_var, mean, rstd, ca, cb, cc, dgamma, dbeta, beta, fa, fc);
   return hipGetLastError();
 }
 
 hipError_t gn_finalize_launch(const float* S, int N, int C, int G, int P, int mode, const float* gamma, float eps,
                               float* mean, float* rstd, float* ca, float* cb, float* cc, float* dgamma, float* dbeta,
-                              float* partial, hipStream_t s) {
+                              float* partial, const float* beta, float* fa, float* fc, hipStream_t s) {
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((N * G + NT - 1) / NT), dim3(NT), 0, s, S, N, C, G, (float)P, mode,
-                     gamma, eps, mean, rstd, ca, cb, cc);
+                     gamma, eps, mean, rstd, ca, cb, cc, beta, fa, fc);
   if (mode == 1) {
     const int nsl = sample_slices(N);
     hipLaunchKernelGGL(sample_slices_kernel, dim3((C + 63) / 64, nsl), dim3(NT), 0, s, S, N, C, nsl,

@@ -94,6 +94,13 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.mask_scale2 = get<float>(d, "mask_scale2", 1.f);
   p.shuffle = get<int>(d, "shuffle", 0);
   p.stats = (float*)getp(d, "stats");
+  p.nz = getp(d, "nz");
+  p.na = (const float*)getp(d, "na");
+  p.nc = (const float*)getp(d, "nc");
+  p.ncs = get<int>(d, "ncs", 0);
+  p.npix = get<int>(d, "npix", 0);
+  p.nd_rate = get<float>(d, "nd_rate", 0.f);
+  p.nd_salt = get<uint32_t>(d, "nd_salt", 0u);
   p.tile = get<int>(d, "tile", 0);
   p.head_w = (const float*)getp(d, "head_w");
   p.head_b = (const float*)getp(d, "head_b");
@@ -155,6 +162,7 @@ WgradParams wgrad_params(const py::dict& d) {
   X(partial_reduce_launch) \
   X(head_finish_launch) \
   X(norm_moments_launch) \
+  X(moments_collect_launch) \
   X(bn_finalize_launch) \
   X(gn_finalize_launch) \
   X(norm_apply_launch) \
@@ -317,9 +325,13 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     return [=](hipStream_t s) { return A->norm_moments_launch(a, b, n, np, c, part, S, s); };
   }
   if (kind == "bn_finalize") {
-    // ptrs: S, gamma, run_mean, run_var, mean, rstd, ca, cb, cc, dgamma, dbeta, partial  ints: N, C, mode
-    // floats: count, eps, momentum   (partial: sample_slices(N) * 2 * C floats of workspace)
+    // ptrs: S, gamma, run_mean, run_var, mean, rstd, ca, cb, cc, dgamma, dbeta, partial[, beta, fa, fc]
+    // ints: N, C, mode   floats: count, eps, momentum   (partial: sample_slices(N) * 2 * C floats of
+    // workspace; fa / fc: forward modes also write the relu-input coefficients gamma r, beta - mu gamma r)
     need(12, 3, 3);
+    const float* bt = P.size() > 14 ? (const float*)vp(12) : nullptr;
+    float* fa = P.size() > 14 ? (float*)vp(13) : nullptr;
+    float* fc = P.size() > 14 ? (float*)vp(14) : nullptr;
     const float* S = (const float*)vp(0);
     const float* gm = (const float*)vp(1);
     float *rm = (float*)vp(2), *rv = (float*)vp(3), *mu = (float*)vp(4), *rs = (float*)vp(5);
@@ -329,12 +341,17 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     float cnt = (float)F[0], eps = (float)F[1], mom = (float)F[2];
     if (mode != 2 && !pt) throw std::invalid_argument("bn_finalize: partial workspace required");
     return [=](hipStream_t s) {
-      return A->bn_finalize_launch(S, n, c, cnt, mode, gm, eps, mom, rm, rv, mu, rs, ca, cb, cc, dg, db, pt, s);
+      return A->bn_finalize_launch(S, n, c, cnt, mode, gm, eps, mom, rm, rv, mu, rs, ca, cb, cc, dg, db, pt, bt, fa, fc,
+                                   s);
     };
   }
   if (kind == "gn_finalize") {
-    // ptrs: S, gamma, mean, rstd, ca, cb, cc, dgamma, dbeta, partial   ints: N, C, G, P, mode   floats: eps
+    // ptrs: S, gamma, mean, rstd, ca, cb, cc, dgamma, dbeta, partial[, beta, fa, fc]
+    // ints: N, C, G, P, mode   floats: eps
     need(10, 5, 1);
+    const float* bt = P.size() > 12 ? (const float*)vp(10) : nullptr;
+    float* fa = P.size() > 12 ? (float*)vp(11) : nullptr;
+    float* fc = P.size() > 12 ? (float*)vp(12) : nullptr;
     const float* S = (const float*)vp(0);
     const float* gm = (const float*)vp(1);
     float *mu = (float*)vp(2), *rs = (float*)vp(3), *ca = (float*)vp(4), *cb = (float*)vp(5), *cc = (float*)vp(6);
@@ -345,8 +362,16 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     check_msg(norm_check(c, g));
     if (mode == 1 && !pt) throw std::invalid_argument("gn_finalize: partial workspace required");
     return [=](hipStream_t s) {
-      return A->gn_finalize_launch(S, n, c, g, np, mode, gm, eps, mu, rs, ca, cb, cc, dg, db, pt, s);
+      return A->gn_finalize_launch(S, n, c, g, np, mode, gm, eps, mu, rs, ca, cb, cc, dg, db, pt, bt, fa, fc, s);
     };
+  }
+  if (kind == "stat_collect") {
+    // ptrs: partial rows, S   ints: N, C, nbp   (S[n][2][C] = sum of rows n*nbp .. n*nbp + nbp - 1)
+    need(2, 3, 0);
+    const float* part = (const float*)vp(0);
+    float* S = (float*)vp(1);
+    int n = I[0], c = I[1], nbp = I[2];
+    return [=](hipStream_t s) { return A->moments_collect_launch(part, n, c, nbp, S, s); };
   }
   if (kind == "norm_apply") {
     // ptrs: z, mean, rstd, gamma, beta, y   ints: N, P, C, cstride, relu, salt[, seed]   floats: drop_rate
@@ -390,7 +415,7 @@ class Plan {
   explicit Plan(int dtype = 0) : A_(api(dtype)) {}
   int add_conv_fwd(const py::dict& d) {
     ConvFwdParams p = conv_params(d);
-    const bool seeded = p.drop_rate > 0.f;
+    const bool seeded = p.drop_rate > 0.f || p.nd_rate > 0.f;
     const uint32_t* seedp = &seed_;
     const uint32_t* const* seed_devp = &seed_dev_;
     const KernelApi* A = A_;
@@ -452,6 +477,13 @@ PYBIND11_MODULE(_C, m) {
   // workgroups of a row-window conv launch (0 for other kernels): sizes per-block
   // partial buffers of fused epilogues (the fused head); raises if the dict is invalid
   m.def("conv_fwd_grid", [](const py::dict& d) { return unet::conv_fwd_grid(conv_params(d)); }, py::arg("params"));
+  // (rows, pixels per tile) of the per-tile statistics the conv's epilogue writes
+  // (rows 0: no statistics epilogue for this shape -> separate moments pass)
+  m.def("conv_stat_tiles", [](const py::dict& d) {
+    int rows = 0, px = 0;
+    unet::conv_stat_tiles(conv_params(d), &rows, &px);
+    return py::make_tuple(rows, px);
+  }, py::arg("params"));
   m.def("wgrad", [](const py::dict& d, uintptr_t stream, int dtype) {
     WgradParams p = wgrad_params(d);
     check(api(dtype)->wgrad_launch(p, as_stream(stream)), "wgrad");

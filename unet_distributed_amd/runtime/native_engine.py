@@ -315,6 +315,10 @@ class NativeUNet:
         same names as the ATen backend so checkpoints are interchangeable)."""
         self.state: Dict[str, torch.Tensor] = {}
         self.norm_layers = []
+        # fused statistics (conv epilogues write per-tile partial sums): name -> buffer
+        self._stat_bufs: Dict[str, torch.Tensor] = {}
+        self._bwd_fused: Dict[str, Tuple[int, bool]] = {}
+        self.fuse_norm_stats = os.environ.get("UNET_NORM_FUSE", "1") != "0"
         if self.spec.norm == "none":
             return
         f32 = torch.float32
@@ -326,7 +330,9 @@ class NativeUNet:
             self.bufs["z:" + l.name] = torch.empty_like(self.bufs[l.name])
             self.bufs["dz:" + l.name] = torch.empty_like(self.bufs[l.name])
             rows = 1 if self.spec.norm == "batch" else self.B
-            for k in ("mean", "rstd", "ca", "cb", "cc"):
+            # mean / rstd; relu-input coefficients fa / fc (u = fa z + fc, read by fused
+            # consumers); backward coefficients ca / cb / cc
+            for k in ("mean", "rstd", "fa", "fc", "ca", "cb", "cc"):
                 self.bufs["%s:%s" % (k, l.name)] = torch.zeros(rows * l.cout, dtype=f32, device=self.device)
             if self.spec.norm == "batch":
                 self.state[l.name + "/norm/moving_mean"] = torch.zeros(l.cout, dtype=f32, device=self.device)
@@ -338,29 +344,66 @@ class NativeUNet:
         self.norm_S = torch.zeros(maxS, dtype=f32, device=self.device)
         self.norm_part = torch.zeros(maxPart, dtype=f32, device=self.device)
 
-    def _norm_fwd(self, plan, l, dropout, train):
-        """z:<L> -> activation <L> = relu(norm(z)) (+ dropout)."""
+    def _stat_buf(self, key, floats):
+        t = self._stat_bufs.get(key)
+        if t is None or t.numel() < floats:
+            t = torch.zeros(max(floats, 64), dtype=torch.float32, device=self.device)
+            self._stat_bufs[key] = t
+        return t
+
+    def _fuse_stats(self, d, key, C, level):
+        """Let conv dict `d` write per-tile normalisation statistics from its epilogue
+        (conv_epilogue.h EPI_STATS / EPI_DGRAD_NORM) if its kernel can.  Returns
+        (rows, per_sample) or None; per_sample: every sample owns rows / B
+        consecutive rows (required by GroupNorm's per-sample statistics)."""
+        if not self.fuse_norm_stats:
+            return None
+        try:
+            rows, px = self.C.conv_stat_tiles(dict(d, stats=1))
+        except ValueError:
+            return None
+        if rows == 0:
+            return None
+        P = self.npix(level) // self.B
+        per_sample = px > 0 and P % px == 0 and rows % self.B == 0
+        if self.spec.norm == "group" and not per_sample:
+            return None
+        d["stats"] = _ptr(self._stat_buf(key, rows * 2 * C))
+        return rows, per_sample
+
+    def _norm_fwd(self, plan, l, dropout, train, fused=None):
+        """z:<L> -> activation <L> = relu(norm(z)) (+ dropout).  fused: (rows, per_sample)
+        when conv L's epilogue wrote the statistics (no separate moments pass)."""
         b, spec = self.bufs, self.spec
         C, P, N = l.cout, self.npix(l.level) // self.B, self.B
         z = b["z:" + l.name]
         mean, rstd = b["mean:" + l.name], b["rstd:" + l.name]
+        fa, fc = b["fa:" + l.name], b["fc:" + l.name]
         gamma, beta = self.master_ptr(l.name + "/norm/gamma"), self.master_ptr(l.name + "/norm/beta")
+        st = self._stat_bufs.get("st:" + l.name) if fused else None
         if spec.norm == "batch":
             rm = self.state[l.name + "/norm/moving_mean"]
             rv = self.state[l.name + "/norm/moving_variance"]
-            if train:
+            S, nS = self.norm_S, N
+            if train and fused:
+                S, nS = st, fused[0]           # fixed-order reduction straight over the tile rows
+            elif train:
                 plan.add_generic("norm_moments", [_ptr(z), _ptr(z), _ptr(self.norm_part), _ptr(self.norm_S)],
                                  [N, P, C], [], "bnstat:" + l.name)
-            plan.add_generic("bn_finalize", [_ptr(self.norm_S), gamma, _ptr(rm), _ptr(rv), _ptr(mean), _ptr(rstd),
-                                             0, 0, 0, 0, 0, _ptr(self.norm_part)],
-                             [N, C, 0 if train else 2], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM],
+            plan.add_generic("bn_finalize", [_ptr(S), gamma, _ptr(rm), _ptr(rv), _ptr(mean), _ptr(rstd),
+                                             0, 0, 0, 0, 0, _ptr(self.norm_part), beta, _ptr(fa), _ptr(fc)],
+                             [nS, C, 0 if train else 2], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM],
                              "bnfin:" + l.name)
             cstride = 0
         else:
-            plan.add_generic("norm_moments", [_ptr(z), _ptr(z), _ptr(self.norm_part), _ptr(self.norm_S)],
-                             [N, P, C], [], "gnstat:" + l.name)
+            if fused:
+                plan.add_generic("stat_collect", [_ptr(st), _ptr(self.norm_S)], [N, C, fused[0] // N], [],
+                                 "gncol:" + l.name)
+            else:
+                plan.add_generic("norm_moments", [_ptr(z), _ptr(z), _ptr(self.norm_part), _ptr(self.norm_S)],
+                                 [N, P, C], [], "gnstat:" + l.name)
             plan.add_generic("gn_finalize", [_ptr(self.norm_S), gamma, _ptr(mean), _ptr(rstd), 0, 0, 0, 0, 0,
-                                             _ptr(self.norm_part)],
+                                             _ptr(self.norm_part), beta, _ptr(fa), _ptr(fc)],
                              [N, C, spec.groups, P, 0], [self.NORM_EPS], "gnfin:" + l.name)
             cstride = C
         plan.add_generic("norm_apply", [_ptr(z), _ptr(mean), _ptr(rstd), gamma, beta, _ptr(b[l.name])],
@@ -376,12 +419,21 @@ class NativeUNet:
         ca, cb, cc = b["ca:" + l.name], b["cb:" + l.name], b["cc:" + l.name]
         gamma = self.master_ptr(l.name + "/norm/gamma")
         dgam, dbet = self.grad_ptr(l.name + "/norm/gamma"), self.grad_ptr(l.name + "/norm/beta")
-        ops = [("norm_moments", [_ptr(g), _ptr(z), _ptr(self.norm_part), _ptr(self.norm_S)], [N, P, C], [],
-                "nstat_bwd:" + l.name)]
+        fused = self._bwd_fused.get(l.name)
+        S, nS = self.norm_S, N
+        if fused is None:
+            ops = [("norm_moments", [_ptr(g), _ptr(z), _ptr(self.norm_part), _ptr(self.norm_S)], [N, P, C], [],
+                    "nstat_bwd:" + l.name)]
+        elif spec.norm == "batch":
+            # the producer's dgrad epilogue wrote {sum g, sum g z} per tile
+            ops, S, nS = [], self._stat_bufs["bst:" + l.name], fused[0]
+        else:
+            ops = [("stat_collect", [_ptr(self._stat_bufs["bst:" + l.name]), _ptr(self.norm_S)],
+                    [N, C, fused[0] // N], [], "gncol_bwd:" + l.name)]
         if spec.norm == "batch":
-            ops.append(("bn_finalize", [_ptr(self.norm_S), gamma, 0, 0, _ptr(mean), _ptr(rstd), _ptr(ca), _ptr(cb),
+            ops.append(("bn_finalize", [_ptr(S), gamma, 0, 0, _ptr(mean), _ptr(rstd), _ptr(ca), _ptr(cb),
                                         _ptr(cc), dgam, dbet, _ptr(self.norm_part)],
-                        [N, C, 1], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM], "bnfin_bwd:" + l.name))
+                        [nS, C, 1], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM], "bnfin_bwd:" + l.name))
             cstride = 0
         else:
             ops.append(("gn_finalize", [_ptr(self.norm_S), gamma, _ptr(mean), _ptr(rstd), _ptr(ca), _ptr(cb),
@@ -391,6 +443,25 @@ class NativeUNet:
         ops.append(("norm_bwd_apply", [_ptr(g), _ptr(z), _ptr(ca), _ptr(cb), _ptr(cc), _ptr(dz)],
                     [N, P, C, cstride], [], "norm_bwd:" + l.name))
         return ops
+
+    def _fuse_dgrad_norm(self, d, tname):
+        """dgrad dict `d` writes the gradient of tensor `tname`: when that is a
+        normalised conv output, let its epilogue recompute the ReLU / dropout mask
+        from the pre-norm z and emit the backward statistics (no nstat_bwd pass)."""
+        if tname not in self.norm_layers:
+            return
+        l = next(x for x in self.spec.layers if x.name == tname)
+        C = l.cout
+        d2 = dict(d, mask1=None, mask_scale1=1.0, nz=_ptr(self.bufs["z:" + tname]),
+                  na=_ptr(self.bufs["fa:" + tname]), nc=_ptr(self.bufs["fc:" + tname]),
+                  ncs=0 if self.spec.norm == "batch" else C, npix=self.npix(l.level) // self.B,
+                  nd_rate=self.spec.dropout if self.tinfo[tname][3] else 0.0, nd_salt=self._salt(tname))
+        fused = self._fuse_stats(d2, "bst:" + tname, C, l.level)
+        if fused is None:
+            return
+        d.clear()
+        d.update(d2)
+        self._bwd_fused[tname] = fused
 
     # ------------------------------------------------------------------ plans
     def _conv_common(self, level, K, stride, pad, out_level=None, in_level=None):
@@ -484,9 +555,12 @@ class NativeUNet:
                     d.update(head_w=self.master_ptr("Mask/kernel"), head_b=self.master_ptr("Mask/bias"),
                              head_logit=_ptr(self.prob))
                     self._head_fused_blocks = nbk
+            fused = None
+            if normed and (train or spec.norm == "group"):
+                fused = self._fuse_stats(d, "st:" + l.name, l.cout, l.level)
             plan.add_conv_fwd(d)
             if normed:
-                self._norm_fwd(plan, l, dropout, train)
+                self._norm_fwd(plan, l, dropout, train, fused)
         elif l.kind == "pool":
             src = self.inputs[l.name][0]
             dd, hh, ww = self.sdims(l.level)
@@ -623,6 +697,7 @@ class NativeUNet:
                             d.update(dst1=_ptr(b["d:" + src1]), D1=l.cin,
                                      mask1=_ptr(b[src1]) if relu_src else None,
                                      mask_scale1=(1.0 / (1.0 - spec.dropout)) if drop else 1.0)
+                            self._fuse_dgrad_norm(d, src1)
                         else:
                             if up1 == 2:
                                 dst1 = b["dfull:" + src1]          # full-res grad of the folded upsample
@@ -631,7 +706,8 @@ class NativeUNet:
                             d.update(dst1=_ptr(dst1), D1=c1, dst2=_ptr(b["dskip:" + skip]),
                                      mask2=_ptr(b[skip]))
                         return d
-                    emit_conv(mk)
+                    dd_ = mk()                 # built now: it decides the fused norm backward
+                    emit_conv(lambda dd_=dd_: dd_)
                     if up1 == 2:
                         lvl = self.tinfo[src1][0]
                         dd, hh, ww = self.sdims(lvl)
@@ -667,8 +743,10 @@ class NativeUNet:
                     d.update(name="dgrad:" + l.name, C1=l.cout, src1=_ptr(du),
                              wgt=self.wptr(l.name, "dg"), Cout=l.cin, relu=0,
                              dst1=_ptr(b["d:" + src]), mask1=_ptr(b[src]))
+                    self._fuse_dgrad_norm(d, src)
                     return d
-                emit_conv(mk)
+                dd_ = mk()
+                emit_conv(lambda dd_=dd_: dd_)
                 done(l.name)
             elif l.kind == "up":
                 pass
