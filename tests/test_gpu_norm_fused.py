@@ -161,3 +161,32 @@ def test_maxpool_all_zero_window_routes_nothing(cuda_dev):
     ref = torch.zeros_like(x)
     ref[0, 0, 0, :] = 1.0
     assert torch.equal(dx1, ref) and torch.equal(dx2, ref)
+
+
+@pytest.mark.parametrize("N,H,Cc,dims3", [(4, 32, 32, 0), (2, 16, 64, 0), (2, 8, 32, 1)])
+def test_pool_bwd_norm_rows(cuda_dev, N, H, Cc, dims3):
+    """pool_bwd_norm writes the same gradient as the code-driven pool backward and
+    per-sample rows summing to {sum g, sum g z}."""
+    torch.manual_seed(4)
+    D = 4 if dims3 else 1
+    shape = (N, D, H, H, Cc) if dims3 else (N, H, H, Cc)
+    x = F.relu(torch.randn(*shape, device=cuda_dev)).bfloat16()
+    z = torch.randn(*shape, device=cuda_dev).bfloat16()
+    oshape = (N, D // 2, H // 2, H // 2, Cc) if dims3 else (N, H // 2, H // 2, Cc)
+    y = torch.empty(*oshape, device=cuda_dev, dtype=torch.bfloat16)
+    code = torch.zeros(y.numel() // 8, device=cuda_dev, dtype=torch.int32)
+    C().generic("pool_fwd", [ptr(x), ptr(y), ptr(code)], [N, D, H, H, Cc, dims3], [], stream())
+    dy = torch.randn_like(y.float()).bfloat16()
+    skip = torch.randn_like(x.float()).bfloat16()
+    dx_ref, dx = torch.empty_like(x), torch.empty_like(x)
+    C().generic("pool_bwd", [0, ptr(dy), ptr(skip), ptr(dx_ref), ptr(code)], [N, D, H, H, Cc, dims3], [], stream())
+    nbp = 3
+    rows = torch.full((N * nbp, 2, Cc), float("nan"), device=cuda_dev)
+    C().generic("pool_bwd_norm", [ptr(code), ptr(dy), ptr(skip), ptr(z), ptr(dx), ptr(rows)],
+                [N, D, H, H, Cc, dims3, nbp], [], stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx_ref)
+    gf, zf = dx.float().reshape(N, -1, Cc), z.float().reshape(N, -1, Cc)
+    mom = torch.stack([gf.sum(1), (gf * zf).sum(1)], 1)
+    per = rows.view(N, nbp, 2, Cc).sum(1)
+    assert torch.allclose(per, mom, rtol=1e-4, atol=1e-2)

@@ -195,6 +195,80 @@ __global__ void __launch_bounds__(256) maxpool2_bwd_code_kernel(const uint32_t* 
   }
 }
 
+// Pool backward of a normalised convNb output: as maxpool2_bwd_code_kernel (argmax
+// codes + the decoder's skip gradient), plus the backward statistics of the norm
+// {sum g, sum g z} over the sample's full-resolution pixels (z = the pre-norm tensor):
+// one row per block, rows[(n * nbp + blk)][2][C] (GroupNorm / BatchNorm finalize read
+// them like the conv epilogues' tile rows).  Grid (nbp, N); a thread keeps one 8-channel
+// column for the whole block (fixed-order reduction over the block's threads).
+__global__ void __launch_bounds__(256) maxpool2_bwd_norm_kernel(const uint32_t* __restrict__ code,
+                                                                const h16* __restrict__ dy,
+                                                                const h16* __restrict__ skip,
+                                                                const h16* __restrict__ z, int D, int H, int W, int C,
+                                                                int dims3, h16* __restrict__ dx,
+                                                                float* __restrict__ rows) {
+  __shared__ float red[256 * 2 * 8];     // [thread][moment][8 channels]
+  const int OD = dims3 ? D / 2 : 1, OH = H / 2, OW = W / 2;
+  const int cpp = C / 8, rstep = 256 / cpp;
+  const int n = blockIdx.y, nbp = gridDim.x, blk = blockIdx.x;
+  const int OP = OD * OH * OW;
+  const int cc = threadIdx.x % cpp, rs = threadIdx.x / cpp;
+  const int nz = dims3 ? 2 : 1;
+  const int bits = dims3 ? 3 : 2;
+  const uint32_t kmask = dims3 ? 7u : 3u;
+  const int p0 = (int)((long long)blk * OP / nbp), p1 = (int)((long long)(blk + 1) * OP / nbp);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+  for (int pp = p0 + rs; pp < p1; pp += rstep) {
+    const int i = (n * OP + pp) * cpp + cc;
+    const PoolIdx pi = pool_idx(i, cpp, OW, OH, H, W, dims3);
+    float g[8];
+    unpack8(*(const u32x4*)(dy + (size_t)i * 8), g);
+    const uint32_t w = code[i];
+    for (int dz = 0; dz < nz; ++dz)
+#pragma unroll
+      for (int dyy = 0; dyy < 2; ++dyy)
+#pragma unroll
+        for (int dxx = 0; dxx < 2; ++dxx) {
+          const uint32_t k = dz * 4 + dyy * 2 + dxx;
+          const size_t off = (size_t)(pi.base + (dz * H + dyy) * W + dxx) * C + pi.cc * 8;
+          float o[8], zf[8];
+          if (skip) {
+            unpack8(*(const u32x4*)(skip + off), o);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = 0.f;
+          }
+          unpack8(*(const u32x4*)(z + off), zf);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (((w >> (bits * e)) & kmask) == k && ((w >> (24 + e)) & 1u)) o[e] += g[e];
+          const u32x4 ov = pack8(o);
+          *(u32x4*)(dx + off) = ov;
+          unpack8(ov, o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            s1[e] += o[e];
+            s2[e] = fmaf(o[e], zf[e], s2[e]);
+          }
+        }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[(threadIdx.x * 2 + 0) * 8 + e] = s1[e];
+    red[(threadIdx.x * 2 + 1) * 8 + e] = s2[e];
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * C; t += 256) {
+    const int mom = t / C, c = t - mom * C;
+    const int col = c / 8, e = c & 7;
+    float a = 0.f;
+    for (int r = 0; r < rstep; ++r) a += red[((r * cpp + col) * 2 + mom) * 8 + e];
+    rows[((size_t)(n * nbp + blk) * 2 + mom) * C + c] = a;
+  }
+}
+
 // Nearest 2x(2x2) upsample, materialised: y[child] = x[p] for the 4 (8 in 3D) children of
 // each low-resolution pixel; one thread = one low pixel x 8 channels (16-byte accesses).
 // The decoder convs of the upsampling variant then read a full-resolution source and
@@ -293,6 +367,13 @@ hipError_t maxpool2_bwd_launch(const void* x, const void* code, const void* dy, 
   else
     hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, (const h16*)dy,
                        (const h16*)skip, N, D, H, W, C, dims3, (h16*)dx);
+  return hipGetLastError();
+}
+
+hipError_t maxpool2_bwd_norm_launch(const void* code, const void* dy, const void* skip, const void* z, int N, int D,
+                                    int H, int W, int C, int dims3, int nbp, void* dx, float* rows, hipStream_t s) {
+  hipLaunchKernelGGL(maxpool2_bwd_norm_kernel, dim3(nbp, N), dim3(256), 0, s, (const uint32_t*)code, (const h16*)dy,
+                     (const h16*)skip, (const h16*)z, D, H, W, C, dims3, (h16*)dx, rows);
   return hipGetLastError();
 }
 

@@ -343,6 +343,179 @@ __global__ void __launch_bounds__(NT) norm_bwd_apply_kernel(const h16* __restric
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Statistics reductions over partial rows (one row per conv tile / moments block):
+// rows[R][2][C] -> per-channel (BatchNorm) or per-sample (GroupNorm) coefficients.
+// Two fixed-order levels, no atomics; every level keeps >= 4 independent loads in
+// flight per thread (the previous single-thread-per-channel finalize was a serial
+// latency chain: ~19 us per launch at 64 slices).
+
+constexpr int SL_ROWS = 32;          // rows per slice of the first level
+
+// slices[sl][col] = sum of rows sl*SL_ROWS .. +SL_ROWS-1 (col < W = 2C);
+// grid (nsl, ceil(W / 64)), 256 threads = 64 columns x 4 row lanes
+__global__ void __launch_bounds__(NT) row_slices_kernel(const float* __restrict__ rows, int R, int W,
+                                                        float* __restrict__ slices) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int col = blockIdx.y * 64 + cl, sl = blockIdx.x;
+  const int r0 = sl * SL_ROWS, r1 = min(R, r0 + SL_ROWS);
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (col < W) {
+#pragma unroll
+    for (int u = 0; u < SL_ROWS / 16; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = r0 + rl + 4 * (4 * u + k);
+        if (r < r1) a[k] += rows[(size_t)r * W + col];
+      }
+  }
+  red[rl][cl] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (rl == 0 && col < W) slices[(size_t)sl * W + col] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+}
+
+// sum over nsl slices of column col (fixed order: 4 lanes x unrolled accumulators)
+__device__ __forceinline__ float slice_sum(const float* __restrict__ sl, int nsl, int W, int col, int rl) {
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  int s = rl;
+  for (; s + 12 < nsl; s += 16)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] += sl[(size_t)(s + 4 * k) * W + col];
+  for (; s < nsl; s += 4) a[0] += sl[(size_t)s * W + col];
+  return (a[0] + a[1]) + (a[2] + a[3]);
+}
+
+// BatchNorm coefficients from the slices; grid ceil(C / 32), 256 threads = 32 channels x
+// 2 moments x 4 slice lanes.  mode 0: forward (batch stats, running stats, fa / fc);
+// 1: backward (ca / cb / cc, dgamma / dbeta); 2: forward inference (running stats; no
+// slices read); 3: plain column sums -> dbeta = S1, dgamma = S2 (GroupNorm parameter grads).
+__global__ void __launch_bounds__(NT) bn_final_kernel(const float* __restrict__ slices, int nsl, int C, float count,
+                                                      int mode, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, float eps, float momentum,
+                                                      float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                      float* __restrict__ mean, float* __restrict__ rstd,
+                                                      float* __restrict__ fa, float* __restrict__ fc,
+                                                      float* __restrict__ ca, float* __restrict__ cb,
+                                                      float* __restrict__ cc, float* __restrict__ dgamma,
+                                                      float* __restrict__ dbeta) {
+  __shared__ float red[4][64];
+  const int t = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 32 + (t & 31), mom = t >> 5;
+  if (mode != 2) {
+    red[rl][t] = c < C ? slice_sum(slices, nsl, 2 * C, mom * C + c, rl) : 0.f;
+    __syncthreads();
+  }
+  if (threadIdx.x >= 32 || c >= C) return;
+  const int i = t;      // channel lane (mom 0)
+  if (mode == 2) {
+    const float mu = run_mean[c], r = rsqrtf(run_var[c] + eps);
+    mean[c] = mu;
+    rstd[c] = r;
+    fa[c] = gamma[c] * r;
+    fc[c] = beta[c] - mu * gamma[c] * r;
+    return;
+  }
+  const float s1 = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  const float s2 = red[0][i + 32] + red[1][i + 32] + red[2][i + 32] + red[3][i + 32];
+  if (mode == 3) {
+    dbeta[c] = s1;
+    dgamma[c] = s2;
+    return;
+  }
+  if (mode == 0) {
+    const float mu = s1 / count;
+    const float var = fmaxf(s2 / count - mu * mu, 0.f);
+    const float r = rsqrtf(var + eps);
+    mean[c] = mu;
+    rstd[c] = r;
+    fa[c] = gamma[c] * r;
+    fc[c] = beta[c] - mu * gamma[c] * r;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * var * (count / fmaxf(count - 1.f, 1.f));
+  } else {
+    const float mu = mean[c], r = rstd[c], gm = gamma[c];
+    const float sgx = r * (s2 - mu * s1);
+    dbeta[c] = s1;
+    dgamma[c] = sgx;
+    const float m1 = s1 / count, m2 = sgx / count;
+    ca[c] = gm * r;
+    cb[c] = -gm * r * r * m2;
+    cc[c] = -gm * r * m1 + gm * r * r * mu * m2;
+  }
+}
+
+// GroupNorm per sample: block n sums its rps rows (sample n) into S[2][C] in LDS, then
+// one thread per group finalises.  mode 0: mean / rstd / fa / fc;  mode 1: ca / cb / cc
+// and contrib[n][2][C] = {sum g, r (sum g z - mu sum g)} (summed over samples for
+// dbeta / dgamma by row_slices + bn_final mode 3).
+__global__ void __launch_bounds__(NT) gn_sample_kernel(const float* __restrict__ rows, int rps, int C, int G, float P,
+                                                       int mode, const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float eps,
+                                                       float* __restrict__ mean, float* __restrict__ rstd,
+                                                       float* __restrict__ fa, float* __restrict__ fc,
+                                                       float* __restrict__ ca, float* __restrict__ cb,
+                                                       float* __restrict__ cc, float* __restrict__ contrib) {
+  extern __shared__ float S[];   // [2C] + [4][64] scratch
+  float* red = S + 2 * C;
+  const int n = blockIdx.x, W = 2 * C;
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const float* base = rows + (size_t)n * rps * W;
+  for (int c0 = 0; c0 < W; c0 += 64) {
+    const int col = c0 + cl;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (col < W) {
+      int r = rl;
+      for (; r + 12 < rps; r += 16)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] += base[(size_t)(r + 4 * k) * W + col];
+      for (; r < rps; r += 4) a[0] += base[(size_t)r * W + col];
+    }
+    red[rl * 64 + cl] = (a[0] + a[1]) + (a[2] + a[3]);
+    __syncthreads();
+    if (rl == 0 && col < W) S[col] = red[cl] + red[64 + cl] + red[128 + cl] + red[192 + cl];
+    __syncthreads();
+  }
+  const int Cg = C / G;
+  const float count = P * Cg;
+  for (int g = threadIdx.x; g < G; g += NT) {
+    if (mode == 0) {
+      float s1 = 0.f, s2 = 0.f;
+      for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+        s1 += S[c];
+        s2 += S[C + c];
+      }
+      const float mu = s1 / count;
+      const float r = rsqrtf(fmaxf(s2 / count - mu * mu, 0.f) + eps);
+      for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+        const size_t k = (size_t)n * C + c;
+        mean[k] = mu;
+        rstd[k] = r;
+        fa[k] = gamma[c] * r;
+        fc[k] = beta[c] - mu * gamma[c] * r;
+      }
+    } else {
+      const float mu = mean[(size_t)n * C + g * Cg], r = rstd[(size_t)n * C + g * Cg];
+      float M1 = 0.f, M2 = 0.f;
+      for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+        const float sgx = r * (S[C + c] - mu * S[c]);
+        M1 += gamma[c] * S[c];
+        M2 += gamma[c] * sgx;
+        contrib[((size_t)n * 2 + 0) * C + c] = S[c];
+        contrib[((size_t)n * 2 + 1) * C + c] = sgx;
+      }
+      M1 /= count;
+      M2 /= count;
+      for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+        const size_t k = (size_t)n * C + c;
+        ca[k] = gamma[c] * r;
+        cb[k] = -r * r * M2;
+        cc[k] = -r * M1 + r * r * mu * M2;
+      }
+    }
+  }
+}
+
 int ew_grid(long long work) {
   long long b = (work + NT - 1) / NT;
   return (int)(b < 8192 ? (b < 1 ? 1 : b) : 8192);
@@ -410,6 +583,51 @@ hipError_t gn_finalize_launch(const float* S, int N, int C, int G, int P, int mo
     hipLaunchKernelGGL(gn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, (const float*)partial, nsl, C,
                        dgamma, dbeta);
   }
+  return hipGetLastError();
+}
+
+int row_slices(int R) { return (R + SL_ROWS - 1) / SL_ROWS; }
+
+// BatchNorm from partial rows [R][2][C]: row_slices -> bn_final (mode 2 reads no rows)
+hipError_t bn_stats_launch(const float* rows, int R, int C, float count, int mode, const float* gamma,
+                           const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* mean,
+                           float* rstd, float* fa, float* fc, float* ca, float* cb, float* cc, float* dgamma,
+                           float* dbeta, float* slices, hipStream_t s) {
+  const int nsl = row_slices(R);
+  if (mode != 2)
+    hipLaunchKernelGGL(row_slices_kernel, dim3(nsl, (2 * C + 63) / 64), dim3(NT), 0, s, rows, R, 2 * C, slices);
+  hipLaunchKernelGGL(bn_final_kernel, dim3((C + 31) / 32), dim3(NT), 0, s, slices, nsl, C, count, mode, gamma, beta,
+                     eps, momentum, run_mean, run_var, mean, rstd, fa, fc, ca, cb, cc, dgamma, dbeta);
+  return hipGetLastError();
+}
+
+// GroupNorm from partial rows [N * rps][2][C] (rows of sample n consecutive).  mode 1 also
+// reduces the per-sample parameter-gradient contributions (work: N * 2 * C floats of
+// contrib + row_slices(N) * 2 * C floats of slices) into dgamma / dbeta.
+hipError_t gn_stats_launch(const float* rows, int N, int rps, int C, int G, int P, int mode, const float* gamma,
+                           const float* beta, float eps, float* mean, float* rstd, float* fa, float* fc, float* ca,
+                           float* cb, float* cc, float* dgamma, float* dbeta, float* work, hipStream_t s) {
+  const size_t lds = (2 * C + 4 * 64) * sizeof(float);
+  hipLaunchKernelGGL(gn_sample_kernel, dim3(N), dim3(NT), lds, s, rows, rps, C, G, (float)P, mode, gamma, beta, eps,
+                     mean, rstd, fa, fc, ca, cb, cc, work);
+  if (mode == 1) {
+    float* slices = work + (size_t)N * 2 * C;
+    const int nsl = row_slices(N);
+    hipLaunchKernelGGL(row_slices_kernel, dim3(nsl, (2 * C + 63) / 64), dim3(NT), 0, s, (const float*)work, N, 2 * C,
+                       slices);
+    hipLaunchKernelGGL(bn_final_kernel, dim3((C + 31) / 32), dim3(NT), 0, s, (const float*)slices, nsl, C, 1.f, 3,
+                       gamma, beta, eps, 0.f, (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr,
+                       (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr, dgamma,
+                       dbeta);
+  }
+  return hipGetLastError();
+}
+
+// chan_moments only (no collect): partial rows [N * nbp][2][C] for bn/gn_stats
+hipError_t norm_rows_launch(const void* A, const void* B, int N, int P, int C, float* rows, hipStream_t s) {
+  const int nbp = norm_blocks_per_sample(N, P);
+  hipLaunchKernelGGL(chan_moments_kernel, dim3(N * nbp), dim3(NT), NT * 2 * 8 * sizeof(float), s, (const h16*)A,
+                     (const h16*)B, P, C, nbp, rows);
   return hipGetLastError();
 }
 

@@ -155,6 +155,7 @@ WgradParams wgrad_params(const py::dict& d) {
   X(cast_input_launch) \
   X(maxpool2_fwd_launch) \
   X(maxpool2_bwd_launch) \
+  X(maxpool2_bwd_norm_launch) \
   X(upsample2_bwd_launch) \
   X(upsample2_fwd_launch) \
   X(head_fwd_launch) \
@@ -163,6 +164,9 @@ WgradParams wgrad_params(const py::dict& d) {
   X(head_finish_launch) \
   X(norm_moments_launch) \
   X(moments_collect_launch) \
+  X(bn_stats_launch) \
+  X(gn_stats_launch) \
+  X(norm_rows_launch) \
   X(bn_finalize_launch) \
   X(gn_finalize_launch) \
   X(norm_apply_launch) \
@@ -224,6 +228,16 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     if (c % 8) throw std::invalid_argument("pool: C % 8");
     if ((long long)n * d * h * w * c >= (1LL << 31)) throw std::invalid_argument("pool: too many elements");
     return [=](hipStream_t s) { return A->maxpool2_bwd_launch(x, code, dy, sk, n, d, h, w, c, d3, dx, s); };
+  }
+  if (kind == "pool_bwd_norm") {
+    // ptrs: code, dy, skip, z, dx, rows   ints: N, D, H, W, C, dims3, nbp
+    need(6, 7, 0);
+    void *code = vp(0), *dy = vp(1), *sk = vp(2), *z = vp(3), *dx = vp(4);
+    float* rows = (float*)vp(5);
+    int n = I[0], d = I[1], h = I[2], w = I[3], c = I[4], d3 = I[5], nbp = I[6];
+    if (c % 8 || 256 % (c / 8)) throw std::invalid_argument("pool_bwd_norm: C % 8, 256 % (C / 8)");
+    if ((long long)n * d * h * w * c >= (1LL << 31)) throw std::invalid_argument("pool: too many elements");
+    return [=](hipStream_t s) { return A->maxpool2_bwd_norm_launch(code, dy, sk, z, n, d, h, w, c, d3, nbp, dx, rows, s); };
   }
   if (kind == "ups_fwd") {
     // ptrs: low-res x, full-res y; ints: N, D, H, W (low resolution), C, dims3
@@ -364,6 +378,43 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     return [=](hipStream_t s) {
       return A->gn_finalize_launch(S, n, c, g, np, mode, gm, eps, mu, rs, ca, cb, cc, dg, db, pt, bt, fa, fc, s);
     };
+  }
+  if (kind == "bn_stats") {
+    // ptrs: rows, gamma, beta, run_mean, run_var, mean, rstd, fa, fc, ca, cb, cc, dgamma, dbeta, slices
+    // ints: R, C, mode   floats: count, eps, momentum
+    need(15, 3, 3);
+    std::vector<float*> q(15);
+    for (int i = 0; i < 15; ++i) q[i] = (float*)vp(i);
+    int R = I[0], c = I[1], mode = I[2];
+    float cnt = (float)F[0], eps = (float)F[1], mom = (float)F[2];
+    if (c % 8) throw std::invalid_argument("bn_stats: C % 8");
+    return [=](hipStream_t s) {
+      return A->bn_stats_launch(q[0], R, c, cnt, mode, q[1], q[2], eps, mom, q[3], q[4], q[5], q[6], q[7], q[8], q[9],
+                                q[10], q[11], q[12], q[13], q[14], s);
+    };
+  }
+  if (kind == "gn_stats") {
+    // ptrs: rows, gamma, beta, mean, rstd, fa, fc, ca, cb, cc, dgamma, dbeta, work
+    // ints: N, rps, C, G, P, mode   floats: eps
+    need(13, 6, 1);
+    std::vector<float*> q(13);
+    for (int i = 0; i < 13; ++i) q[i] = (float*)vp(i);
+    int n = I[0], rps = I[1], c = I[2], g = I[3], np = I[4], mode = I[5];
+    float eps = (float)F[0];
+    check_msg(norm_check(c, g));
+    return [=](hipStream_t s) {
+      return A->gn_stats_launch(q[0], n, rps, c, g, np, mode, q[1], q[2], eps, q[3], q[4], q[5], q[6], q[7], q[8], q[9],
+                                q[10], q[11], q[12], s);
+    };
+  }
+  if (kind == "norm_rows") {
+    // ptrs: A, B, rows   ints: N, P, C   (rows[N * norm_blocks_per_sample][2][C])
+    need(3, 3, 0);
+    void *a = vp(0), *b = vp(1);
+    float* rows = (float*)vp(2);
+    int n = I[0], np = I[1], c = I[2];
+    check_msg(norm_check(c, 0));
+    return [=](hipStream_t s) { return A->norm_rows_launch(a, b, n, np, c, rows, s); };
   }
   if (kind == "stat_collect") {
     // ptrs: partial rows, S   ints: N, C, nbp   (S[n][2][C] = sum of rows n*nbp .. n*nbp + nbp - 1)
@@ -507,6 +558,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_blocks", &head_blocks_py);
   m.def("norm_blocks_per_sample", &norm_blocks_per_sample);
   m.def("sample_slices", &sample_slices);
+  m.def("row_slices", &row_slices);
   m.def("wgrad_reduce_stage_floats", &wgrad_reduce_stage_floats);
   // QW > 0 describes a 3x3 (KT 9) or 3x3x3 (KT 27) stride-1 'same' conv on a QD x QH x QW
   // grid (QH, QD default to QW: square / cubic levels), a row-window candidate

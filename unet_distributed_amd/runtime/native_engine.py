@@ -322,7 +322,6 @@ class NativeUNet:
         if self.spec.norm == "none":
             return
         f32 = torch.float32
-        maxS = maxPart = 1
         for l in self.spec.layers:
             if l.kind != "conv":
                 continue
@@ -337,12 +336,6 @@ class NativeUNet:
             if self.spec.norm == "batch":
                 self.state[l.name + "/norm/moving_mean"] = torch.zeros(l.cout, dtype=f32, device=self.device)
                 self.state[l.name + "/norm/moving_variance"] = torch.ones(l.cout, dtype=f32, device=self.device)
-            P = self.npix(l.level) // self.B
-            nbp = self.C.norm_blocks_per_sample(self.B, P)
-            maxS = max(maxS, self.B * 2 * l.cout)
-            maxPart = max(maxPart, self.B * nbp * 2 * l.cout, self.C.sample_slices(self.B) * 2 * l.cout)
-        self.norm_S = torch.zeros(maxS, dtype=f32, device=self.device)
-        self.norm_part = torch.zeros(maxPart, dtype=f32, device=self.device)
 
     def _stat_buf(self, key, floats):
         t = self._stat_bufs.get(key)
@@ -371,6 +364,23 @@ class NativeUNet:
         d["stats"] = _ptr(self._stat_buf(key, rows * 2 * C))
         return rows, per_sample
 
+    def _stat_rows(self, key, A, B, l, fused, plan, name):
+        """(rows buffer, row count) of the per-tile / per-block partial sums of layer l:
+        the producer's epilogue rows when `fused`, else a moments pass over (A, A*B)."""
+        C, P, N = l.cout, self.npix(l.level) // self.B, self.B
+        if fused:
+            return self._stat_bufs[key], fused[0]
+        R = N * self.C.norm_blocks_per_sample(N, P)
+        rows = self._stat_buf("m" + key, R * 2 * C)
+        plan.add_generic("norm_rows", [_ptr(A), _ptr(B), _ptr(rows)], [N, P, C], [], name)
+        return rows, R
+
+    def _stat_work(self, key, R, C):
+        """Workspace of bn_stats / gn_stats (slices of R rows, or GroupNorm's per-sample
+        parameter-gradient rows + their slices)."""
+        n = max(self.C.row_slices(R), 1) * 2 * C + self.B * 2 * C + self.C.row_slices(self.B) * 2 * C
+        return self._stat_buf("w" + key, n)
+
     def _norm_fwd(self, plan, l, dropout, train, fused=None):
         """z:<L> -> activation <L> = relu(norm(z)) (+ dropout).  fused: (rows, per_sample)
         when conv L's epilogue wrote the statistics (no separate moments pass)."""
@@ -380,68 +390,59 @@ class NativeUNet:
         mean, rstd = b["mean:" + l.name], b["rstd:" + l.name]
         fa, fc = b["fa:" + l.name], b["fc:" + l.name]
         gamma, beta = self.master_ptr(l.name + "/norm/gamma"), self.master_ptr(l.name + "/norm/beta")
-        st = self._stat_bufs.get("st:" + l.name) if fused else None
         if spec.norm == "batch":
             rm = self.state[l.name + "/norm/moving_mean"]
             rv = self.state[l.name + "/norm/moving_variance"]
-            S, nS = self.norm_S, N
-            if train and fused:
-                S, nS = st, fused[0]           # fixed-order reduction straight over the tile rows
-            elif train:
-                plan.add_generic("norm_moments", [_ptr(z), _ptr(z), _ptr(self.norm_part), _ptr(self.norm_S)],
-                                 [N, P, C], [], "bnstat:" + l.name)
-            plan.add_generic("bn_finalize", [_ptr(S), gamma, _ptr(rm), _ptr(rv), _ptr(mean), _ptr(rstd),
-                                             0, 0, 0, 0, 0, _ptr(self.norm_part), beta, _ptr(fa), _ptr(fc)],
-                             [nS, C, 0 if train else 2], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM],
+            if train:
+                rows, R = self._stat_rows("st:" + l.name, z, z, l, fused, plan, "bnstat:" + l.name)
+            else:
+                rows, R = self._stat_buf("st:" + l.name, 64), 1        # inference: running statistics
+            ws = self._stat_work("st:" + l.name, R, C)
+            plan.add_generic("bn_stats", [_ptr(rows), gamma, beta, _ptr(rm), _ptr(rv), _ptr(mean), _ptr(rstd),
+                                          _ptr(fa), _ptr(fc), 0, 0, 0, 0, 0, _ptr(ws)],
+                             [R, C, 0 if train else 2], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM],
                              "bnfin:" + l.name)
             cstride = 0
         else:
-            if fused:
-                plan.add_generic("stat_collect", [_ptr(st), _ptr(self.norm_S)], [N, C, fused[0] // N], [],
-                                 "gncol:" + l.name)
-            else:
-                plan.add_generic("norm_moments", [_ptr(z), _ptr(z), _ptr(self.norm_part), _ptr(self.norm_S)],
-                                 [N, P, C], [], "gnstat:" + l.name)
-            plan.add_generic("gn_finalize", [_ptr(self.norm_S), gamma, _ptr(mean), _ptr(rstd), 0, 0, 0, 0, 0,
-                                             _ptr(self.norm_part), beta, _ptr(fa), _ptr(fc)],
-                             [N, C, spec.groups, P, 0], [self.NORM_EPS], "gnfin:" + l.name)
+            rows, R = self._stat_rows("st:" + l.name, z, z, l, fused, plan, "gnstat:" + l.name)
+            ws = self._stat_work("st:" + l.name, R, C)
+            plan.add_generic("gn_stats", [_ptr(rows), gamma, beta, _ptr(mean), _ptr(rstd), _ptr(fa), _ptr(fc),
+                                          0, 0, 0, 0, 0, _ptr(ws)],
+                             [N, R // N, C, spec.groups, P, 0], [self.NORM_EPS], "gnfin:" + l.name)
             cstride = C
         plan.add_generic("norm_apply", [_ptr(z), _ptr(mean), _ptr(rstd), gamma, beta, _ptr(b[l.name])],
                          [N, P, C, cstride, 1, self._salt(l.name)],
                          [spec.dropout if (l.dropout and dropout) else 0.0], "norm:" + l.name)
 
     def _norm_bwd_ops(self, l):
-        """(kind, ptrs, ints, floats, name) of d:<L> -> dz:<L> plus gamma/beta grads."""
+        """Plan ops (callables) of d:<L> -> dz:<L> plus gamma/beta grads."""
         b, spec = self.bufs, self.spec
         C, P, N = l.cout, self.npix(l.level) // self.B, self.B
         g, z, dz = b["d:" + l.name], b["z:" + l.name], b["dz:" + l.name]
         mean, rstd = b["mean:" + l.name], b["rstd:" + l.name]
         ca, cb, cc = b["ca:" + l.name], b["cb:" + l.name], b["cc:" + l.name]
         gamma = self.master_ptr(l.name + "/norm/gamma")
+        beta = self.master_ptr(l.name + "/norm/beta")
         dgam, dbet = self.grad_ptr(l.name + "/norm/gamma"), self.grad_ptr(l.name + "/norm/beta")
         fused = self._bwd_fused.get(l.name)
-        S, nS = self.norm_S, N
-        if fused is None:
-            ops = [("norm_moments", [_ptr(g), _ptr(z), _ptr(self.norm_part), _ptr(self.norm_S)], [N, P, C], [],
-                    "nstat_bwd:" + l.name)]
-        elif spec.norm == "batch":
-            # the producer's dgrad epilogue wrote {sum g, sum g z} per tile
-            ops, S, nS = [], self._stat_bufs["bst:" + l.name], fused[0]
-        else:
-            ops = [("stat_collect", [_ptr(self._stat_bufs["bst:" + l.name]), _ptr(self.norm_S)],
-                    [N, C, fused[0] // N], [], "gncol_bwd:" + l.name)]
-        if spec.norm == "batch":
-            ops.append(("bn_finalize", [_ptr(S), gamma, 0, 0, _ptr(mean), _ptr(rstd), _ptr(ca), _ptr(cb),
-                                        _ptr(cc), dgam, dbet, _ptr(self.norm_part)],
-                        [nS, C, 1], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM], "bnfin_bwd:" + l.name))
-            cstride = 0
-        else:
-            ops.append(("gn_finalize", [_ptr(self.norm_S), gamma, _ptr(mean), _ptr(rstd), _ptr(ca), _ptr(cb),
-                                        _ptr(cc), dgam, dbet, _ptr(self.norm_part)],
-                        [N, C, spec.groups, P, 1], [self.NORM_EPS], "gnfin_bwd:" + l.name))
-            cstride = C
-        ops.append(("norm_bwd_apply", [_ptr(g), _ptr(z), _ptr(ca), _ptr(cb), _ptr(cc), _ptr(dz)],
-                    [N, P, C, cstride], [], "norm_bwd:" + l.name))
+        ops = []
+
+        def emit(pl):
+            rows, R = self._stat_rows("bst:" + l.name, g, z, l, fused, pl, "nstat_bwd:" + l.name)
+            ws = self._stat_work("bst:" + l.name, R, C)
+            if spec.norm == "batch":
+                pl.add_generic("bn_stats", [_ptr(rows), gamma, beta, 0, 0, _ptr(mean), _ptr(rstd), 0, 0,
+                                            _ptr(ca), _ptr(cb), _ptr(cc), dgam, dbet, _ptr(ws)],
+                               [R, C, 1], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM], "bnfin_bwd:" + l.name)
+                cstride = 0
+            else:
+                pl.add_generic("gn_stats", [_ptr(rows), gamma, beta, _ptr(mean), _ptr(rstd), 0, 0, _ptr(ca),
+                                            _ptr(cb), _ptr(cc), dgam, dbet, _ptr(ws)],
+                               [N, R // N, C, spec.groups, P, 1], [self.NORM_EPS], "gnfin_bwd:" + l.name)
+                cstride = C
+            pl.add_generic("norm_bwd_apply", [_ptr(g), _ptr(z), _ptr(ca), _ptr(cb), _ptr(cc), _ptr(dz)],
+                           [N, P, C, cstride], [], "norm_bwd:" + l.name)
+        ops.append(emit)
         return ops
 
     def _fuse_dgrad_norm(self, d, tname):
@@ -647,6 +648,9 @@ class NativeUNet:
         def done(lname):
             ops.append(("done", lname))
 
+        def src_normed(t):
+            return t in self.norm_layers and self.fuse_norm_stats
+
         for li in range(len(layers) - 1, -1, -1):
             l = layers[li]
             if l.kind == "mask":
@@ -666,8 +670,7 @@ class NativeUNet:
                 c2 = self.tinfo[skip][1] if skip else 0
                 dy = b["d:" + l.name]
                 if spec.norm != "none":
-                    for kind, P_, I_, F_, nm in self._norm_bwd_ops(l):
-                        ops.append(lambda pl, kind=kind, P_=P_, I_=I_, F_=F_, nm=nm: pl.add_generic(kind, P_, I_, F_, nm))
+                    ops.extend(self._norm_bwd_ops(l))
                     dy = b["dz:" + l.name]
                 Q = self.npix(l.level)
                 # --- weight + bias gradient (fused column sums); the upsampling decoder's
@@ -716,6 +719,21 @@ class NativeUNet:
                                                         _ptr(b["d:" + src1])],
                                      [self.B, dd, hh, ww, c1, int(self.dims == 3)], [], "bwd:up:" + src1)
                 done(l.name)
+            elif l.kind == "pool" and src_normed(self.inputs[l.name][0]):
+                # gradient of a normalised convNb output: the pool backward also emits
+                # the norm's backward statistics (no separate nstat_bwd pass)
+                src = self.inputs[l.name][0]
+                dd, hh, ww = self.sdims(l.level)
+                P_ = self.npix(l.level + 1) // self.B
+                nbp = self.C.norm_blocks_per_sample(self.B, P_)
+                rows = self._stat_buf("bst:" + src, self.B * nbp * 2 * l.cout)
+                self._bwd_fused[src] = (self.B * nbp, True)
+                emit_generic("pool_bwd_norm",
+                             lambda src=src, l=l, rows=rows: [
+                                 _ptr(self.pool_codes[l.name]), _ptr(b["d:" + l.name]),
+                                 _ptr(b["dskip:" + src]) if ("dskip:" + src) in b else 0,
+                                 _ptr(b["z:" + src]), _ptr(b["d:" + src]), _ptr(rows)],
+                             [self.B, dd, hh, ww, l.cout, int(self.dims == 3), nbp], [], "bwd:" + l.name)
             elif l.kind == "pool":
                 src = self.inputs[l.name][0]
                 dd, hh, ww = self.sdims(l.level)
