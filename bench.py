@@ -54,7 +54,81 @@ def parse():
     p.add_argument("--hip_graph", type=int, default=1,
                    help="replay fwd / bwd segments / Adam as captured HIP graphs (0: eager launches)")
     p.add_argument("--profile_dir", default="")
+    p.add_argument("--comm_diag", type=int, default=1,
+                   help="N > 1: after the timed steps, measure per-bucket allreduce time and the exposed "
+                        "communication (A/B against compute-only and non-overlapped steps)")
     return p.parse_args()
+
+
+class _NoComm:
+    """Compute-only stand-in for GradSync (comm diagnostics A/B)."""
+
+    def on_segment(self, i):
+        pass
+
+    def finish(self):
+        pass
+
+
+def comm_diagnostics(a, ctx, flat, bounds, sync_overlap, step_fn, dev):
+    """Outside the timed region: per-bucket allreduce time (isolated, median of 5,
+    events on the issuing stream) and the step time with overlapped / serial / no
+    communication, so a multi-GPU number comes with its comm breakdown."""
+    import statistics
+    import torch.distributed as dist
+    from unet_distributed_amd.parallel import dist as D
+    from unet_distributed_amd.parallel.grad_sync import GradSync
+    out = {"backend": ctx.backend or "none", "world_size": ctx.world_size,
+           "buckets_mb": [round(4.0 * (b - (bounds[i - 1] if i else 0)) / 2 ** 20, 3) for i, b in enumerate(bounds)]}
+    if ctx.world_size == 1 or not a.comm_diag:
+        return out
+    per = []
+    for i in range(len(bounds)):
+        t = sync_overlap._slice(i)
+        samples = []
+        cuda = dev.type == "cuda"
+        for _ in range(5):
+            D.barrier()
+            if cuda:
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            t0 = time.perf_counter()
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            if cuda:
+                e1.record()
+                torch.cuda.synchronize()
+                samples.append(e0.elapsed_time(e1))
+            else:
+                samples.append((time.perf_counter() - t0) * 1000.0)
+        per.append(round(D.allreduce_max_scalar(statistics.median(samples), dev), 4))
+    out["allreduce_ms_per_bucket"] = per
+    out["allreduce_ms_total"] = round(sum(per), 4)
+
+    def sync_dev():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
+    def timed(sync, k=5):
+        step_fn(0, sync)
+        sync_dev()
+        D.barrier()
+        sync_dev()
+        t0 = time.perf_counter()
+        for i in range(k):
+            step_fn(1 + i, sync)
+        sync_dev()
+        D.barrier()
+        sync_dev()
+        return D.allreduce_max_scalar((time.perf_counter() - t0) * 1000.0 / k, dev)
+
+    t_none = timed(_NoComm())
+    t_ovl = timed(sync_overlap)
+    t_ser = timed(GradSync(flat, bounds, ctx, overlap=False))
+    out.update(step_ms_compute_only=round(t_none, 3), step_ms_overlapped=round(t_ovl, 3),
+               step_ms_serial_comm=round(t_ser, 3), exposed_comm_ms=round(t_ovl - t_none, 3),
+               serial_comm_ms=round(t_ser - t_none, 3))
+    return out
 
 
 def main():
@@ -103,7 +177,7 @@ def main():
 
     scaler = LossScaler(cfg.dtype, cfg.loss_scale)
 
-    def step(i):
+    def step(i, sync=sync):
         scale = scaler.scale
         backend.fwd_bwd(xs[i % 2], ys[i % 2], seed=12345 + i, on_segment=sync.on_segment, grad_scale=scale)
         sync.finish()
@@ -140,6 +214,7 @@ def main():
     s = backend.sums()
     i_, st, sp = [float(v) for v in s[:3].tolist()]
     dice = (2 * i_ + 1) / (st + sp + 1)
+    comm = comm_diagnostics(a, ctx, flat, bounds, sync, step, dev)
     if ctx.rank == 0:
         rec = {
             "metric": (_baseline_metric()
@@ -165,6 +240,7 @@ def main():
                        "img_size": a.img_size, "in_channels": a.in_channels,
                        "parallelism": "dp%d" % N, "backend": backend.name},
             "train_dice_last_batch": round(dice, 5),
+            "comm": comm,
         }
         print(json.dumps(rec), flush=True)
     D.destroy()

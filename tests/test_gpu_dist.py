@@ -1,0 +1,89 @@
+"""Multi-rank data parallelism on the NATIVE backend, rehearsed on one card.
+
+Two ranks share cuda:0 and talk over gloo (RCCL refuses two ranks on one device;
+the 8-GPU node runs the same code with the nccl backend).  Each rank runs the HIP
+executor's forward + backward on its own shard; the bucketed allreduce issued
+between backward segments (parallel/grad_sync.py, overlapped on the side stream)
+must leave every rank with the MEAN of the per-rank shard gradients -- the
+reference's SyncReplicasOptimizer semantics (`test_dist.py:249-262`, SURVEY.md
+§2.5).  A second check runs the same step through the non-overlapped path.
+"""
+
+import json
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, out, overlap, hip_graph):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", UNET_DIST_BACKEND="gloo")
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from unet_distributed_amd.config import Config
+    from unet_distributed_amd.data.datasets import synthetic_brats
+    from unet_distributed_amd.models import reference
+    from unet_distributed_amd.models.spec import spec_from_config
+    from unet_distributed_amd.parallel import dist as D
+    from unet_distributed_amd.parallel.grad_sync import GradSync, plan_buckets
+    from unet_distributed_amd.runtime.backends import NativeBackend
+    from unet_distributed_amd.runtime.params import FlatParams
+    ctx = D.init("cuda", "auto", 120)
+    dev = ctx.device
+    cfg = Config(batch_size=4 * world, img_size=64, in_channels=4, hip_graph=hip_graph)
+    spec = spec_from_config(cfg)
+    flat = FlatParams(spec, device=dev)
+    flat.load_dict(reference.init_params(spec, seed=7 + rank))       # different inits ...
+    D.broadcast_(flat.master, 0)                                       # ... made identical
+    bounds = plan_buckets(flat, 0.25)                                  # several buckets
+    be = NativeBackend(spec, flat, cfg, dev, 4, bounds)
+    be.engine.repack()
+    x, y = synthetic_brats(4, 64, 4, seed=100 + rank)                  # this rank's shard
+    x, y = torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev)
+    # local (un-synchronised) gradient of the shard
+    be.fwd_bwd(x, y, seed=5 + rank)
+    torch.cuda.synchronize()
+    local = flat.grad.detach().cpu().clone()
+    gathered = [torch.zeros_like(local) for _ in range(world)]
+    dist.all_gather(gathered, local)
+    mean = torch.stack(gathered).mean(0)
+    # the same step with the bucketed allreduce between backward segments
+    sync = GradSync(flat, bounds, ctx, overlap=overlap)
+    be.fwd_bwd(x, y, seed=5 + rank, on_segment=sync.on_segment)
+    sync.finish()
+    torch.cuda.synchronize()
+    g = flat.grad.detach().cpu()
+    rec = dict(rank=rank, buckets=len(bounds), max_err=(g - mean).abs().max().item(),
+               scale=mean.abs().max().item(), local_diff=(local - mean).abs().max().item())
+    with open(os.path.join(out, "r%d.json" % rank), "w") as f:
+        json.dump(rec, f)
+    D.destroy()
+
+
+@pytest.mark.parametrize("overlap,hip_graph", [(True, True), (False, False)])
+def test_native_two_ranks_bucket_average_equals_mean_of_shard_grads(tmp_path, overlap, hip_graph):
+    world = 2
+    mp.spawn(_rank, args=(world, _free_port(), str(tmp_path), overlap, hip_graph), nprocs=world, join=True)
+    recs = [json.load(open(tmp_path / ("r%d.json" % r))) for r in range(world)]
+    for r in recs:
+        assert r["buckets"] >= 3
+        # the shards differ, so the local gradients differ from the mean ...
+        assert r["local_diff"] > 1e-3 * r["scale"]
+        # ... and after the bucketed allreduce every rank holds exactly the mean
+        assert r["max_err"] <= 1e-6 * r["scale"] + 1e-9, r

@@ -66,6 +66,31 @@ def test_native_step_matches_reference(cuda_dev, kw):
     assert _cos(fn.grad, ft.grad) > 0.99
 
 
+def test_native_step_matches_reference_at_shipped_shape(cuda_dev):
+    """The benchmarked configuration itself: 128x128x4, bf16, per-GPU batch 64 with the
+    production split-K sizing (wg_target), dual-stream backward, HIP-graph forward and
+    the fused segmentation head; gradients vs the fp32 ATen step."""
+    spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, batch_size=64, img_size=128, in_channels=4,
+                                              hip_graph=True)
+    e = nb.engine
+    assert e.dual_stream and e._head_fused_blocks > 0 and e.graphs is not None
+    for rep in range(2):                       # second pass replays the captured graphs
+        nb.fwd_bwd(x, y, seed=77)
+    tb.fwd_bwd(x, y, seed=77)
+    torch.cuda.synchronize()
+    sn, st = nb.sums().cpu(), tb.sums().cpu()
+    assert torch.allclose(sn[:3], st[:3], rtol=2e-2, atol=1.0), (sn, st)
+    worst = 1.0
+    for name, shape, off, n in fn.entries:
+        gn, gt = fn.grad[off:off + n], ft.grad[off:off + n]
+        c = _cos(gn, gt)
+        worst = min(worst, c)
+        assert c > (0.95 if name.endswith("/bias") else 0.98), (name, c)
+        r = (gn.norm() / (gt.norm() + 1e-30)).item()
+        assert 0.9 < r < 1.1, (name, r)
+    assert _cos(fn.grad, ft.grad) > 0.99, worst
+
+
 def test_native_adam_matches_reference(cuda_dev):
     from unet_distributed_amd.runtime.optim import adam_reference_
     spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, batch_size=2, img_size=32, in_channels=4)

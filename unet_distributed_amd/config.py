@@ -97,7 +97,7 @@ class Config:
     deterministic: bool = False      # torch path: deterministic algorithms (native path always is)
     serialize_kernels: bool = False  # debug: AMD_SERIALIZE_KERNEL=3 + HIP_LAUNCH_BLOCKING=1
     launch_tensorboard: bool = False # start `tensorboard --logdir` on the chief if installed
-    hip_graph: bool = False          # native: replay fwd / bwd segments / Adam as HIP graphs
+    hip_graph: bool = True           # native: replay the forward / Adam as HIP graphs (the bench default)
     progress: bool = True
     loss_scale: float = 0.0          # fp16 static loss scale (0 = dynamic)
 

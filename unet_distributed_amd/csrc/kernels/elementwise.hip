@@ -32,6 +32,34 @@ __global__ void __launch_bounds__(256) cast_input_kernel(const float* __restrict
   }
 }
 
+// Batch load from the HBM-resident training set (trainer hot path): sample idx[b] of
+// x_all [Nall][P][Cin] and y_all [Nall][P] (fp32) -> the channel-padded 16-bit input
+// [B][P][Cpad] (pad channels written as zeros) and the 16-bit target [B][P].  One
+// launch replaces index_select + cast copies; one thread per pixel.
+__global__ void __launch_bounds__(256) gather_batch_kernel(const float* __restrict__ x_all,
+                                                           const float* __restrict__ y_all,
+                                                           const long long* __restrict__ idx, int B, int P, int Cin,
+                                                           int Cpad, h16* __restrict__ xb, h16* __restrict__ tb) {
+  const long long total = (long long)B * P;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / P), p = (int)(i - (long long)b * P);
+    const size_t s = (size_t)idx[b] * P + p;
+    const float* src = x_all + s * Cin;
+    h16* dst = xb + (size_t)i * Cpad;
+    if (Cin == 4 && Cpad == 4) {
+      const float4 v = *(const float4*)src;
+      u32x2 o;
+      o[0] = pack2h(v.x, v.y);
+      o[1] = pack2h(v.z, v.w);
+      *(u32x2*)dst = o;
+    } else {
+      for (int c = 0; c < Cpad; ++c) dst[c] = (h16)(c < Cin ? src[c] : 0.f);
+    }
+    tb[i] = (h16)y_all[s];
+  }
+}
+
 // Pooling thread map: one thread = one pooled pixel x 8 channels, 32-bit index math
 // (the 64-bit divisions of a long-long decomposition dominated these memory-bound
 // kernels).  Window corner k = (dz, dy, dx) -> input pixel base + k-offset.
@@ -347,6 +375,13 @@ inline int grid_for(long long work, int per_block = 256) {
 hipError_t cast_input_launch(const float* x, int P, int Cin, int Cpad, void* y, hipStream_t s) {
   hipLaunchKernelGGL(cast_input_kernel, dim3(grid_for((long long)P * Cpad)), dim3(256), 0, s, x, P, Cin, Cpad,
                      (h16*)y);
+  return hipGetLastError();
+}
+
+hipError_t gather_batch_launch(const float* x_all, const float* y_all, const long long* idx, int B, int P, int Cin,
+                               int Cpad, void* xb, void* tb, hipStream_t s) {
+  hipLaunchKernelGGL(gather_batch_kernel, dim3(grid_for((long long)B * P)), dim3(256), 0, s, x_all, y_all, idx, B, P,
+                     Cin, Cpad, (h16*)xb, (h16*)tb);
   return hipGetLastError();
 }
 

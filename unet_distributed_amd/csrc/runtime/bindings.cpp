@@ -153,6 +153,7 @@ WgradParams wgrad_params(const py::dict& d) {
   X(multi_reduce_launch) \
   X(colsum_launch) \
   X(cast_input_launch) \
+  X(gather_batch_launch) \
   X(maxpool2_fwd_launch) \
   X(maxpool2_bwd_launch) \
   X(maxpool2_bwd_norm_launch) \
@@ -210,6 +211,16 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     void* y = vp(1);
     int a = I[0], b = I[1], c = I[2];
     return [=](hipStream_t s) { return A->cast_input_launch(x, a, b, c, y, s); };
+  }
+  if (kind == "gather_batch") {
+    // ptrs: x_all, y_all, idx (int64, device), xb, tb   ints: B, P, Cin, Cpad
+    need(5, 4, 0);
+    const float *xa = (const float*)vp(0), *ya = (const float*)vp(1);
+    const long long* ix = (const long long*)vp(2);
+    void *xb = vp(3), *tb = vp(4);
+    int B = I[0], P_ = I[1], cin = I[2], cpad = I[3];
+    if (cin > cpad || cpad > 64) throw std::invalid_argument("gather_batch: Cin <= Cpad <= 64");
+    return [=](hipStream_t s) { return A->gather_batch_launch(xa, ya, ix, B, P_, cin, cpad, xb, tb, s); };
   }
   if (kind == "pool_fwd") {
     // ptrs: x, y[, code]

@@ -43,6 +43,22 @@ class BatchLoader:
         return self.bx, self.by
 
 
+class ResidentBatch:
+    """A batch of the HBM-resident dataset named by sample index: the native backend
+    gathers and casts it into its input buffers in one kernel; anything else asks
+    for the tensors."""
+
+    def __init__(self, x_all: torch.Tensor, y_all: torch.Tensor, idx: torch.Tensor):
+        self.x_all, self.y_all, self.idx = x_all, y_all, idx
+
+    def tensors(self):
+        return self.x_all.index_select(0, self.idx), self.y_all.index_select(0, self.idx)
+
+    @property
+    def npix(self) -> int:
+        return int(self.idx.numel()) * int(self.y_all[0].numel())
+
+
 class DeviceFeeder:
     """Per-step batches on the training device.
 
@@ -78,9 +94,13 @@ class DeviceFeeder:
         self.events = [None] * len(self.loaders)
         self.k = 0
 
-    def get(self, idx: np.ndarray):
+    def get(self, idx: np.ndarray, lazy: bool = False):
+        """(x, y) of the samples `idx`; lazy (resident data only): a ResidentBatch
+        for a backend that gathers it itself."""
         if self.resident:
             ii = torch.from_numpy(np.sort(np.asarray(idx, dtype=np.int64))).to(self.device, non_blocking=True)
+            if lazy:
+                return ResidentBatch(self.x, self.y, ii), None
             return self.x.index_select(0, ii), self.y.index_select(0, ii)
         k = self.k
         self.k = (self.k + 1) % len(self.loaders)

@@ -50,6 +50,8 @@ class TorchBackend:
 
     def fwd_bwd(self, x, y, seed: int, on_segment: Optional[Callable[[int], None]] = None,
                 grad_scale: float = 1.0):
+        if hasattr(x, "x_all"):
+            x, y = x.tensors()
         names = [e[0] for e in self.flat.entries]
         leaves = {n: self.flat.view(self.flat.master, n).detach().requires_grad_(True) for n in names}
         logits = self._forward_logits(leaves, x, True, seed, True).float()
@@ -110,9 +112,13 @@ class NativeBackend:
         self.engine.set_buckets(bounds)
 
     def fwd_bwd(self, x, y, seed: int, on_segment=None, grad_scale: float = 1.0):
+        """x, y: batch tensors, or x = a data.loader.ResidentBatch (y unused)."""
         e = self.engine
         e.set_loss_scale(grad_scale)
-        e.load_batch(x, y)
+        if hasattr(x, "x_all"):
+            e.load_indexed(x.x_all, x.y_all, x.idx)
+        else:
+            e.load_batch(x, y)
         e.forward(seed)
         e.backward(on_segment)
 

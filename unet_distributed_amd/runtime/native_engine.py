@@ -904,6 +904,16 @@ class NativeUNet:
         (xb if cin == self.cpad else xb[:, :cin]).copy_(x.reshape(-1, cin), non_blocking=True)
         self.target.copy_(y.reshape(-1), non_blocking=True)
 
+    def load_indexed(self, x_all: torch.Tensor, y_all: torch.Tensor, idx: torch.Tensor, stream=None):
+        """Batch = samples `idx` (device int64) of the HBM-resident dataset, gathered
+        and cast straight into the padded 16-bit input and target (one launch)."""
+        cin = self.spec.in_channels
+        P = x_all[0].numel() // cin
+        assert idx.dtype == torch.int64 and idx.numel() == self.B and x_all.dtype == torch.float32
+        assert y_all[0].numel() == P and x_all.is_contiguous() and y_all.is_contiguous()
+        self.C.generic("gather_batch", [_ptr(x_all), _ptr(y_all), _ptr(idx), _ptr(self.bufs["x"]), _ptr(self.target)],
+                       [self.B, P, cin, self.cpad], [], native.stream_handle(stream), self.dt_id)
+
     # ------------------------------------------------------------------ HIP graphs
     def enable_graphs(self):
         """Replay the forward, every backward segment and the Adam launch as captured

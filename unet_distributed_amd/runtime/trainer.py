@@ -218,7 +218,9 @@ class Trainer:
                                          else "streamed from host (pinned, double-buffered)"))
 
     def _batch(self, idx: np.ndarray):
-        return self.feeder.get(idx)
+        # native backend + resident data: the backend gathers the batch itself (one
+        # gather+cast kernel into its input buffers, no fp32 batch copy)
+        return self.feeder.get(idx, lazy=self.backend.name == "native")
 
     # ------------------------------------------------------------------ eval
     def evaluate(self) -> dict:
@@ -332,7 +334,7 @@ class Trainer:
                 if self.device.type == "cuda":
                     torch.cuda.synchronize()
                 dt = time.time() - t_last
-                m = metrics_from_sums(self.backend.sums(), y.numel(), cfg)
+                m = metrics_from_sums(self.backend.sums(), x.npix if y is None else y.numel(), cfg)
                 m["images_per_sec"] = imgs_since / max(dt, 1e-9)
                 m["lr"] = learning_rate(cfg, step)
                 m["percent_complete"] = 100.0 * step / total
