@@ -8,7 +8,7 @@ import torch
 
 from unet_distributed_amd.utils import tf_bundle, events
 from unet_distributed_amd.utils.checkpoint import CheckpointManager, flat_to_tensors, tensors_to_flat, export_model
-from unet_distributed_amd.models.spec import UNetSpec
+from unet_distributed_amd.models.spec import UNetSpec, spec_from_config
 from unet_distributed_amd.models import reference
 from unet_distributed_amd.runtime.params import FlatParams
 from unet_distributed_amd.config import Config
@@ -134,3 +134,94 @@ def test_event_file_roundtrip(tmp_path):
 def test_png_encoder_produces_valid_signature():
     png = events.png_gray(np.arange(64, dtype=np.uint8).reshape(8, 8))
     assert png[:8] == b"\x89PNG\r\n\x1a\n" and b"IEND" in png
+
+
+def _graph_nodes(graph_def: bytes):
+    """name -> (op, inputs, attr keys) from a GraphDef (wire-format reader)."""
+    out = {}
+    for nd in tf_bundle._parse(graph_def).get(1, []):
+        f = tf_bundle._parse(nd)
+        attrs = [tf_bundle._parse(a)[1][0].decode() for a in f.get(5, [])]
+        out[f[1][0].decode()] = (f[2][0].decode(), [i.decode() for i in f.get(3, [])], attrs)
+    return out
+
+
+def _map(entries):
+    return {tf_bundle._parse(e)[1][0].decode(): tf_bundle._parse(e).get(2, [b""])[0] for e in entries}
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(norm="batch"), dict(use_upsampling=True, in_channels=1),
+                                dict(dims=3, in_channels=4)])
+def test_saved_model_pb_structure(tmp_path, kw):
+    """export_model writes saved_model.pb: SavedModel {schema 1, MetaGraphDef tagged
+    serve, signature intel_unet_brats_model image -> prediction (Placeholder:0 ->
+    Mask/Sigmoid:0), a GraphDef connecting them, a V2 SaverDef}.  Parsed with the
+    wire-format reader; TF-loader parity is unpinned (TF not installed)."""
+    cfg = Config(checkpoint_dir=str(tmp_path), img_size=32 if kw.get("dims") == 3 else 64, **kw)
+    spec = spec_from_config(cfg)
+    d = export_model(cfg, spec, FlatParams(spec))
+    sm = tf_bundle._parse(open(os.path.join(d, "saved_model.pb"), "rb").read())
+    assert sm[1] == [1] and len(sm[2]) == 1
+    mg = tf_bundle._parse(sm[2][0])
+    info = tf_bundle._parse(mg[1][0])
+    assert [t.decode() for t in info[4]] == ["serve"]
+    sigs = _map(mg[5])
+    sig = tf_bundle._parse(sigs["intel_unet_brats_model"])
+    ins, outs = _map(sig[1]), _map(sig[2])
+    assert tf_bundle._parse(ins["image"])[1][0] == b"Placeholder:0"
+    assert tf_bundle._parse(outs["prediction"])[1][0] == b"Mask/Sigmoid:0"
+    assert sig[3][0] == b"tensorflow/serving/predict"
+    nodes = _graph_nodes(mg[2][0])
+    assert nodes["Placeholder"][0] == "Placeholder" and nodes["Mask/Sigmoid"][0] == "Sigmoid"
+    # every trainable variable is a VariableV2 restored by the saver
+    for name, shape in spec.variables():
+        assert nodes[name][0] == "VariableV2", name
+    saver = tf_bundle._parse(mg[3][0])
+    assert saver[3][0] == b"save/restore_all" and saver[7] == [2]
+    assert nodes["save/restore_all"][0] == "NoOp"
+    # the graph is connected: walk back from the output to the placeholder
+    seen, stack = set(), ["Mask/Sigmoid"]
+    while stack:
+        n = stack.pop()
+        if n in seen:
+            continue
+        seen.add(n)
+        stack.extend(i.lstrip("^").split(":")[0] for i in nodes[n][1])
+    assert "Placeholder" in seen and "conv1a/kernel" in seen
+    if kw.get("norm") == "batch":
+        assert nodes["conv1a/norm/FusedBatchNorm"][0] == "FusedBatchNorm"
+
+
+def test_checkpoint_writes_saver_meta(tmp_path):
+    cfg = Config(checkpoint_dir=str(tmp_path), img_size=64, save_model_secs=0)
+    spec = spec_from_config(cfg)
+    flat = FlatParams(spec)
+    mgr = CheckpointManager(cfg, flat, True)
+    prefix = mgr.save()
+    meta = tf_bundle._parse(open(prefix + ".meta", "rb").read())
+    nodes = _graph_nodes(meta[2][0])
+    bundle = tf_bundle.read_bundle(prefix)
+    for name in bundle:                       # weights, Adam slots, beta powers, global_step
+        assert name in nodes and nodes[name][0] == "VariableV2", name
+    restore = nodes["save/RestoreV2/tensor_names"]
+    assert restore[0] == "Const"
+    colls = _map(meta[4])
+    assert "trainable_variables" in colls and "variables" in colls
+    lg = mgr.save_last_good()
+    assert os.path.exists(lg + ".meta")
+
+
+def test_metric_logger_writes_histograms_and_images(tmp_path):
+    from unet_distributed_amd.utils.metrics import MetricLogger
+    cfg = Config(checkpoint_dir=str(tmp_path), log_jsonl="")
+    log = MetricLogger(cfg, True, str(tmp_path / "logs"))
+    m = dict(loss=0.5, dice=0.6, sensitivity=0.7, specificity=0.8, percent_complete=10.0, images_per_sec=1.0,
+             lr=1e-3)
+    imgs = {k: np.random.rand(3, 16, 16).astype(np.float32) for k in ("predictions", "ground_truth", "images")}
+    log.train(1, m, 10, images=imgs)
+    log.close()
+    recs = events.read_events(log.events.path)
+    tags = set(t for _, v in recs for t in v)
+    for t in ("loss", "loss_1", "dice_1", "sensitivity_1", "specificity_1", "predictions/image/0",
+              "ground_truth/image/2", "images/image/1"):
+        assert t in tags, (t, tags)

@@ -68,12 +68,18 @@ class TorchBackend:
             i, st, sp = losses.dice_sums(t, p)
             bce = torch.nn.functional.binary_cross_entropy_with_logits(logits, t, reduction="sum")
             self._sums = torch.stack([i, st, sp, bce]).detach()
+        self._last = (x, t, p.detach())
         if on_segment is not None:
             for k in range(len(self.bounds)):
                 on_segment(k)
 
     def sums(self) -> torch.Tensor:
         return self._sums
+
+    def summary_images(self, n: int) -> dict:
+        """First n samples of the last training batch (channel 0; 3D: middle slice)."""
+        x, t, p = self._last
+        return _summary_arrays(x, t, p, n)
 
     @torch.no_grad()
     def eval_sums(self, x, y) -> torch.Tensor:
@@ -125,6 +131,15 @@ class NativeBackend:
     def sums(self) -> torch.Tensor:
         return self.engine.sums
 
+    def summary_images(self, n: int) -> dict:
+        """From the buffers the step already holds (no extra forward, Q8): the padded
+        16-bit input, the target and the head's probabilities."""
+        e = self.engine
+        d, h, w = e.sdims(1)
+        shape = (e.B, h, w) if e.dims == 2 else (e.B, d, h, w)
+        x = e.bufs["x"][..., 0]
+        return _summary_arrays(x, e.target.view(shape), e.prob.view(shape), n)
+
     @torch.no_grad()
     def eval_sums(self, x, y) -> torch.Tensor:
         e = self.engine
@@ -143,6 +158,23 @@ class NativeBackend:
 
     def adam_step(self, lr, b1p, b2p, grad_scale=1.0):
         self.engine.adam_step(lr, b1p, b2p, grad_scale)
+
+
+def _summary_arrays(x, t, p, n) -> dict:
+    def prep(a):
+        a = a[:n].detach().float()
+        if a.dim() == 5:                     # [n, D, H, W, 1]
+            a = a[..., 0]
+        if a.dim() == 4 and a.shape[-1] == 1:
+            a = a[..., 0]
+        if a.dim() == 4:                     # 3D volume [n, D, H, W]: middle slice
+            a = a[:, a.shape[1] // 2]
+        return a.cpu().numpy()
+    if x.dim() == 4 and x.shape[-1] > 1 and t.dim() == 4 and t.shape[-1] == 1:
+        x = x[..., 0]                        # NHWC input: first channel
+    elif x.dim() == 5 and x.shape[-1] > 1:
+        x = x[..., 0]
+    return {"predictions": prep(p), "ground_truth": prep(t), "images": prep(x)}
 
 
 def native_supported(spec, cfg, device) -> Optional[str]:

@@ -338,7 +338,10 @@ class Trainer:
                 m["images_per_sec"] = imgs_since / max(dt, 1e-9)
                 m["lr"] = learning_rate(cfg, step)
                 m["percent_complete"] = 100.0 * step / total
-                self.log.train(self.flat.global_step, m, total)
+                imgs = None
+                if self.is_chief and self.log.events is not None and hasattr(self.backend, "summary_images"):
+                    imgs = self.backend.summary_images(self.log.max_images)
+                self.log.train(self.flat.global_step, m, total, images=imgs)
                 last_metrics = m
                 t_last, imgs_since = time.time(), 0
             if step % self.num_batches == 0:

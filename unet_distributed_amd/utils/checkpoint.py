@@ -12,11 +12,15 @@ Layout:
   ``<layer>/bias``, Adam slots ``<var>/Adam`` and ``<var>/Adam_1``,
   ``beta1_power``, ``beta2_power`` and ``global_step`` (int64) -- everything
   the Supervisor restores (`test_dist.py:361-362`);
+* every bundle gets the Saver's ``<prefix>.meta`` MetaGraphDef (graph + SaverDef +
+  variable collections, hand-encoded: utils/tf_graph.py);
 * export (C19, `test_dist.py:511-532`): ``CHECKPOINT_DIRECTORY/saved_model/``
-  with ``variables/variables.{index,data-00000-of-00001}`` (TF bundle) and a
-  ``saved_model.json`` describing the graph and the ``intel_unet_brats_model``
-  signature {image -> prediction}.  A TF SavedModel protobuf graph cannot be
-  produced without TensorFlow; ``sanity_check.py`` consumes this export.
+  with ``saved_model.pb`` (SavedModel protobuf: tag ``serve``, signature
+  ``intel_unet_brats_model`` {image: Placeholder:0 -> prediction: Mask/Sigmoid:0}),
+  ``variables/variables.{index,data-00000-of-00001}`` (TF bundle) and a
+  ``saved_model.json`` side-car that ``inference.py`` / ``sanity_check.py`` read.
+  Format parity with TensorFlow is unpinned (TF is not installed): the files are
+  verified structurally against the proto field layout, not by a TF loader.
 
 Only rank 0 writes; writes are atomic (tmp + rename).  Restores happen on rank 0
 and are broadcast to every rank (replaces ``prepare_or_wait_for_session``).
@@ -30,7 +34,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from . import tf_bundle
+from . import tf_bundle, tf_graph
 
 
 def logdir_name(cfg) -> str:
@@ -77,6 +81,17 @@ def tensors_to_flat(flat, tensors, strict=True, extra_state=None):
             t.copy_(torch.from_numpy(np.asarray(tensors[k], np.float32)).to(t.device))
 
 
+def _var_shapes(tensors) -> list:
+    return [(k, tuple(np.asarray(v).shape)) for k, v in tensors.items()]
+
+
+def write_with_meta(prefix: str, tensors, spec, img_size: int) -> None:
+    """TF V2 bundle + the Saver's .meta MetaGraphDef over the same variables."""
+    tf_bundle.write_bundle(prefix, tensors)
+    if spec is not None:
+        tf_graph.write_meta(prefix, spec, img_size, _var_shapes(tensors))
+
+
 class CheckpointManager:
     def __init__(self, cfg, flat, is_chief: bool, extra_state=None, max_to_keep: int = 5):
         self.cfg = cfg
@@ -105,12 +120,13 @@ class CheckpointManager:
             self.pre_save()                 # e.g. async PS: pull server state into flat
         step = self.flat.global_step
         prefix = os.path.join(self.logdir, "model.ckpt-%d" % step)
-        tf_bundle.write_bundle(prefix, flat_to_tensors(self.flat, extra_state=self.extra_state))
+        write_with_meta(prefix, flat_to_tensors(self.flat, extra_state=self.extra_state),
+                        getattr(self.flat, "spec", None), self.cfg.img_size)
         _, paths = tf_bundle.read_checkpoint_state(self.logdir)
         name = os.path.basename(prefix)
         paths = [p for p in paths if p != name] + [name]
         for old in paths[:-self.max_to_keep]:
-            for suf in (".index", ".data-00000-of-00001"):
+            for suf in (".index", ".data-00000-of-00001", ".meta"):
                 try:
                     os.remove(os.path.join(self.logdir, old + suf))
                 except FileNotFoundError:
@@ -126,7 +142,8 @@ class CheckpointManager:
         if self.pre_save is not None:
             self.pre_save()                 # async PS: the bundle must hold the server's state
         prefix = os.path.join(self.cfg.checkpoint_dir, "last_good_model.cpkt")
-        tf_bundle.write_bundle(prefix, flat_to_tensors(self.flat, extra_state=self.extra_state))
+        write_with_meta(prefix, flat_to_tensors(self.flat, extra_state=self.extra_state),
+                        getattr(self.flat, "spec", None), self.cfg.img_size)
         tf_bundle.write_checkpoint_state(self.cfg.checkpoint_dir, "last_good_model.cpkt",
                                          ["last_good_model.cpkt"])
         return prefix
@@ -169,4 +186,5 @@ def export_model(cfg, spec, flat, directory: Optional[str] = None, extra_state=N
     }
     with open(os.path.join(d, "saved_model.json"), "w") as f:
         json.dump(meta, f, indent=2)
+    tf_graph.write_saved_model(d, spec, cfg.img_size)
     return d

@@ -32,13 +32,22 @@ class MetricLogger:
             except OSError:
                 self.events = None
         self.t0 = time.time()
+        from .. import settings
+        self.max_images = int(getattr(settings, "TENSORBOARD_IMAGES", 3))
 
     def _emit(self, rec):
         if self.jsonl:
             self.jsonl.write(json.dumps(rec) + "\n")
             self.jsonl.flush()
 
-    def train(self, step, m, total):
+    # TF 1.x uniquifies the second summary op of a name: the histograms the reference
+    # adds next to the scalars (`test_dist.py:275-282`) carry the tags "<name>_1"
+    HIST_TAGS = {"loss": "loss_1", "dice": "dice_1", "sensitivity": "sensitivity_1",
+                 "specificity": "specificity_1"}
+
+    def train(self, step, m, total, images=None):
+        """images: optional {"predictions", "ground_truth", "images"} -> [n, H, W] arrays
+        (first TENSORBOARD_IMAGES samples of the step's batch, `test_dist.py:285-287`)."""
         if not self.on:
             return
         if self.cfg.progress:
@@ -48,6 +57,10 @@ class MetricLogger:
         if self.events:
             self.events.scalars(step, {k: m[k] for k in ("loss", "dice", "sensitivity", "specificity",
                                                            "percent_complete", "images_per_sec")})
+            for k, tag in self.HIST_TAGS.items():
+                self.events.histogram(step, tag, [m[k]])
+            for tag, arr in (images or {}).items():
+                self.events.images(step, tag, arr, max_outputs=self.max_images)
             self.events.flush()
 
     def test(self, step, m, epoch, epochs, final=False):

@@ -3,9 +3,8 @@
 The reference saves with ``tf.train.Saver`` (`test_dist.py:269-271,446,490`)
 through ``tf.train.Supervisor(save_model_secs=60)`` (`test_dist.py:347-355`):
 ``<prefix>.index`` + ``<prefix>.data-00000-of-00001`` plus a ``checkpoint``
-text file naming the latest prefix.  We produce the same on-disk format so
-existing TF tooling (``tf.train.NewCheckpointReader``) can read our
-checkpoints and we can resume from TF-written ones:
+text file naming the latest prefix.  We write that on-disk layout (the V2
+bundle format TF tooling such as ``tf.train.NewCheckpointReader`` reads):
 
 * ``.data-00000-of-00001``: the raw little-endian tensor bytes, back to back;
 * ``.index``: a LevelDB-format SSTable (no compression) whose empty key maps to
@@ -13,6 +12,11 @@ checkpoints and we can resume from TF-written ones:
   (dtype, shape, shard 0, offset, size, masked CRC32C of the bytes);
 * block trailers carry masked CRC32C of block contents + type byte; the footer
   ends with the table magic ``0xdb4775248b80fb57``.
+
+Format parity is UNPINNED: TensorFlow is not installed here and the reference
+ships no TF-written checkpoint, so the files are verified against the format's
+structure (SSTable footer / block CRCs / BundleEntryProto fields) and by
+round-trip, not by a TF reader.
 
 Protobufs are hand-encoded (wire format) since TF's .proto files are absent.
 CRC32C runs in the native runtime (SSE4.2), with a pure-Python fallback.
