@@ -8,10 +8,11 @@ synthetic slices (BASELINE.json metric), one process per GPU.
 Each timed step is a complete training step of the flagship configuration:
 device-side batch load, UNet forward (bf16 HIP kernels), Dice loss, backward,
 bucketed RCCL allreduce (overlapped with backward), fused TF-Adam update.
-Weak scaling: the per-GPU micro-batch is fixed (default 256 = the reference's
-per-worker shard of its 1024 global batch, `settings_dist.py:17`,
-`test_dist.py:390`), so the global batch is 256*N.  Random-init weights
-(he_uniform / glorot as the reference), synthetic data.
+Weak scaling: the per-GPU micro-batch is fixed (default 1024, sized from the batch sweep
+in profiles/r2_batch_sweep.md: throughput saturates from 512 on; the reference's
+per-worker shard is 256 = its 1024 global batch over 4 workers, `settings_dist.py:17`,
+`test_dist.py:390`, and ``--per_gpu_batch 256`` reproduces it), so the global batch is
+1024*N.  Random-init weights (he_uniform / glorot as the reference), synthetic data.
 
 Rank 0 prints ONE JSON line; ``value`` is whole-job images/sec computed from the
 MAX over ranks of the timed wall time.
@@ -40,7 +41,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--per_gpu_batch", type=int, default=256)
+    p.add_argument("--per_gpu_batch", type=int, default=1024,
+                   help="images per GPU (profiles/r2_batch_sweep.md: throughput saturates from 512)")
     p.add_argument("--img_size", type=int, default=128)
     p.add_argument("--in_channels", type=int, default=4)
     p.add_argument("--dims", type=int, default=2)
