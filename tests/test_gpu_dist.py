@@ -87,3 +87,70 @@ def test_native_two_ranks_bucket_average_equals_mean_of_shard_grads(tmp_path, ov
         assert r["local_diff"] > 1e-3 * r["scale"]
         # ... and after the bucketed allreduce every rank holds exactly the mean
         assert r["max_err"] <= 1e-6 * r["scale"] + 1e-9, r
+
+
+def _ps_rank(rank, world, port, out, steps, batch):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", UNET_DIST_BACKEND="gloo")
+    sys.path.insert(0, ROOT)
+    import time
+    import statistics
+    from unet_distributed_amd.config import Config
+    from unet_distributed_amd.data.datasets import synthetic_brats
+    from unet_distributed_amd.models import reference
+    from unet_distributed_amd.models.spec import spec_from_config
+    from unet_distributed_amd.parallel import dist as D
+    from unet_distributed_amd.parallel.async_ps import AsyncPS, DeviceParameterServer
+    from unet_distributed_amd.runtime.backends import NativeBackend
+    from unet_distributed_amd.runtime.params import FlatParams
+    ctx = D.init("cuda", "auto", 120)
+    dev = ctx.device
+    cfg = Config(batch_size=batch * world, img_size=128, in_channels=4, is_sync=0)
+    spec = spec_from_config(cfg)
+    flat = FlatParams(spec, device=dev)
+    flat.load_dict(reference.init_params(spec, seed=7))
+    be = NativeBackend(spec, flat, cfg, dev, batch)
+    be.engine.repack()
+    ps = AsyncPS(flat, cfg, ctx, repack=be.engine.repack)
+    x, y = synthetic_brats(batch, 128, 4, seed=100 + rank)
+    x, y = torch.from_numpy(x).to(dev), torch.from_numpy(y).to(dev)
+    t_comp, t_ps = [], []
+    for i in range(steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        be.fwd_bwd(x, y, seed=i * world + rank)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        ps.push_pull()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        t_comp.append(t1 - t0)
+        t_ps.append(t2 - t1)
+    ps.finish()
+    D.barrier()
+    D.broadcast_(flat.master, 0)
+    torch.cuda.synchronize()
+    rec = dict(rank=rank, comp_ms=1e3 * statistics.median(t_comp[2:]), ps_ms=1e3 * statistics.median(t_ps[2:]),
+               device_server=isinstance(ps.server, DeviceParameterServer) if rank == 0 else None,
+               step=flat.global_step, finite=bool(torch.isfinite(flat.master).all().item()))
+    with open(os.path.join(out, "ps%d.json" % rank), "w") as f:
+        json.dump(rec, f)
+    D.destroy()
+
+
+def test_async_ps_device_server_two_ranks_one_card(tmp_path):
+    """--is_sync=0 with the GPU-resident parameter server: rank 0's server thread runs
+    TF-Adam as one native launch per push on its own stream; 2 ranks x 8 steps all
+    land (PS global_step 16); the push/pull round trip (gloo data plane staged through
+    host buffers on one card) is recorded against the compute step."""
+    world, steps = 2, 8
+    mp.spawn(_ps_rank, args=(world, _free_port(), str(tmp_path), steps, 256), nprocs=world, join=True)
+    recs = [json.load(open(tmp_path / ("ps%d.json" % r))) for r in range(world)]
+    assert recs[0]["device_server"] is True
+    assert all(r["finite"] for r in recs)
+    assert recs[0]["step"] == world * steps
+    print("async PS: compute %.2f ms, push/pull %.2f ms (rank 0, in-process) / %.2f ms (rank 1, gloo)"
+          % (recs[0]["comp_ms"], recs[0]["ps_ms"], recs[1]["ps_ms"]))
+    if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
+        with open(os.path.join(ROOT, "gpurun_out", "async_ps_timing.json"), "w") as f:
+            json.dump(recs, f)

@@ -608,3 +608,27 @@ def test_upsample2_fwd_materialised(cuda_dev, dims3):
     C().generic("ups_fwd", [ptr(x), ptr(y)], [N, D, H, H, Cc, dims3], [], stream())
     torch.cuda.synchronize()
     assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout", [(2, 128, 32, 32), (2, 64, 32, 64), (4, 32, 64, 128), (4, 16, 128, 256),
+                                          (1, 256, 32, 32)])
+def test_conv_fwd_fused_maxpool_matches_pool_kernel(cuda_dev, N, H, Cin, Cout):
+    """convNb forward with the fused 2x2 max-pool epilogue: the conv output, the pooled
+    tensor and the argmax codes equal the plain conv + the separate pool kernel."""
+    torch.manual_seed(31)
+    x = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, Cin, Cout, device=cuda_dev) * 0.1).bfloat16()
+    b = torch.randn(Cout, device=cuda_dev) * 0.1
+    wp = pack_fwd(w)
+    y0, y1 = [torch.empty(N, H, H, Cout, device=cuda_dev, dtype=torch.bfloat16) for _ in range(2)]
+    p0, p1 = [torch.empty(N, H // 2, H // 2, Cout, device=cuda_dev, dtype=torch.bfloat16) for _ in range(2)]
+    c0, c1 = [torch.full((N * (H // 2) ** 2 * Cout // 8,), -1, device=cuda_dev, dtype=torch.int32) for _ in range(2)]
+    d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(x), wgt=ptr(wp), bias=ptr(b),
+             Cout=Cout, relu=1)
+    C().conv_fwd(dict(d, dst1=ptr(y0)), stream())
+    C().generic("pool_fwd", [ptr(y0), ptr(p0), ptr(c0)], [N, 1, H, H, Cout, 0], [], stream())
+    C().conv_fwd(dict(d, dst1=ptr(y1), pool_dst=ptr(p1), pool_code=ptr(c1)), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    assert torch.equal(p0, p1)
+    assert torch.equal(c0, c1)

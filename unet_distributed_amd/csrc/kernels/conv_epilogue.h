@@ -85,9 +85,10 @@ struct StripTiles {
 // wider than one window, or any row-window kernel): tile pixel ml is at row
 // m0 + ml / SEGW (m0 = first row), column col0 + ml % SEGW of rows `pitch` pixels wide.
 // SEGW == 0: tile pixel ml is output pixel m0 + ml.
-// stat_row: this tile's row of p.stats (modes 3 / 4).
+// stat_row: this tile's row of p.stats (modes 3 / 4).  TROW > 0: the tile is BM / TROW
+// whole rows of TROW pixels (row-window kernels; enables the fused max-pool).
 template <int BM, int BN, int WM, int WN, int TM, int TN, int NTHR, int EPI = EPI_GENERIC,
-          class MapM = LinearTiles<WM>, int SEGW = 0>
+          class MapM = LinearTiles<WM>, int SEGW = 0, int TROW = 0>
 __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc)[TM][TN], char* smem,
                                               const int m0, const int n0, const int M, const int wm,
                                               const int wn, const int lane, const int tid,
@@ -422,6 +423,51 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
           q = cb == r ? hq[CPR * k + r] : q;
         }
         if (q < M) p.head_logit[q] = z;
+      }
+    }
+  }
+  if constexpr (EPI == EPI_FWD && TROW > 0 && (BM / TROW) % 2 == 0 && TROW % 2 == 0) {
+    if (p.pool_dst) {
+      // 2x2 max-pool of the tile's complete row pairs (a window starts on an even row
+      // and holds an even number of rows): max + first-argmax code per channel, the
+      // "max > 0" flag in bit 24 + e (elementwise.hip::maxpool2_fwd_kernel layout)
+      constexpr int PC = TROW / 2, NP = (BM / TROW / 2) * PC * CPR;
+      const int Wp = p.OW >> 1, cpp = p.Cout >> 3;
+      h16* pdst = (h16*)p.pool_dst;
+      for (int k = tid; k < NP; k += NTHR) {
+        const int cb = k % CPR, pp = k / CPR;
+        const int pr = pp / PC, pc = pp - pr * PC;
+        const int ml00 = 2 * pr * TROW + 2 * pc;
+        const int q00 = qof(ml00);
+        if (q00 >= M) continue;
+        float m[8];
+        uint32_t a[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          m[e] = -INFINITY;
+          a[e] = 0u;
+        }
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int ml = ml00 + (kk >> 1) * TROW + (kk & 1);
+          const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
+          const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
+          float f[8];
+          unpack8((u32x4){lo[0], lo[1], hi[0], hi[1]}, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const bool gt = f[e] > m[e];            // first maximum wins ties
+            m[e] = gt ? f[e] : m[e];
+            a[e] = gt ? (uint32_t)kk : a[e];
+          }
+        }
+        uint32_t w = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) w |= (a[e] << (2 * e)) | ((m[e] > 0.f ? 1u : 0u) << (24 + e));
+        const int grow = q00 / p.OW, gcol = q00 - grow * p.OW;
+        const size_t pq = (size_t)(grow >> 1) * Wp + (gcol >> 1);
+        *(u32x4*)(pdst + pq * p.Cout + n0 + cb * 8) = pack8(m);
+        p.pool_code[pq * cpp + (n0 >> 3) + cb] = w;
       }
     }
   }

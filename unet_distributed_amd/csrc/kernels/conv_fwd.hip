@@ -542,8 +542,11 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   }
   __syncthreads();
   if constexpr (GEO == GEO_SEG)
-    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, W>(p, acc, smem, g0, n0, M, wave, 0, lane, tid, Wf, col0,
-                                                              tm);
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, W, W>(p, acc, smem, g0, n0, M, wave, 0, lane, tid, Wf,
+                                                                 col0, tm);
+  else if constexpr (GEO == GEO_2D)
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0,
+                                                                 0, tm);
   else
     conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0, 0, tm);
 }
@@ -1082,6 +1085,13 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.shuffle && ((p.Cout >> p.shuffle) % 8)) return "conv_fwd: shuffle channels must be multiples of 8";
   if (p.shuffle && p.D1 != p.Cout) return "conv_fwd: shuffle with channel split unsupported";
   if (const char* m = conv_norm_epi_check(p)) return m;
+  if (p.pool_dst) {
+    const int W = p.OW > 128 ? 128 : p.OW;
+    const int R = (W == 16 ? 256 : 512) / W;
+    if (!p.pool_code || conv_epi_mode(p) != EPI_FWD || !win_eligible(p) || p.KD != 1 || p.OD != 1 || R % 2 ||
+        p.OH % 2 || p.OW % 2 || p.Cout % 8 || p.head_w)
+      return "conv_fwd: fused max-pool needs a 2D row-window ReLU forward (even rows, codes buffer)";
+  }
   if (p.tile < 0 || p.tile > 11) return "conv_fwd: bad tile id";
   if (p.tile == 10 && !tconv_fwd_eligible(p)) return "conv_fwd: transposed-conv window tile not applicable";
   if (p.tile == 11 && !tconv_dgrad_eligible(p)) return "conv_fwd: transposed-conv dgrad tile not applicable";

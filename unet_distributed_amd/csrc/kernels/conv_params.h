@@ -52,6 +52,12 @@ struct ConvFwdParams {
   int ncs, npix;
   float nd_rate;
   uint32_t nd_salt;
+  // Fused 2x2 max-pool (row-window forward of a convNb, EPI_FWD): the epilogue also
+  // writes the pooled tensor [N][H/2][W/2][Cout] and the first-argmax codes of
+  // elementwise.hip::maxpool2_fwd (one uint32 per pooled pixel x 8 channels), so the
+  // separate pool launch and its full re-read of the conv output disappear.
+  void* pool_dst;
+  uint32_t* pool_code;
   int tile;                   // 0 = auto, else forced tile config id (tuning / A-B tests)
   // Fused segmentation head (row-window forward, Cout == 32, EPI_FWD only): per pixel
   // z = sum_c out[c] head_w[c] + head_b -> head_logit (fp32) for head_finish

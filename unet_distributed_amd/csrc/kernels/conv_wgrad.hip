@@ -565,13 +565,19 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   const int lslot = lane >> 2;
   const int lchunk = (lane & 3) ^ (((lslot >> 3) & 1) << 1);
   const int xl = ((lslot - 1) * CA + ca0 + lchunk * 8) * 2;
+  // 8-wide rows: a 32-pixel step spans 4 halo rows whose slots sit 1 KB apart (same
+  // banks), so odd halo rows additionally flip chunk bit 1 -- the transposed A reads of
+  // lanes in rows r and r + 1 then hit disjoint banks (was 2-way, 49 % conflict cycles)
+  constexpr bool ROWSWZ = W == 8;
+  const int xl_odd = ((lslot - 1) * CA + ca0 + (lchunk ^ 2) * 8) * 2;
   const int yl = (lslot * p.Nc + co0 + lchunk * 8) * 2;
   // transposed-read lane roles: group G = lane >> 4 covers pixels 8G .. 8G + 7 of a
   // 32-pixel step; lane 4q + pp addresses pixel 8G + 4hh + q, channels 4pp .. 4pp + 3
   const int G = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
 
-  auto tr_addr = [&](int slot, int col, int ch) -> int {   // ch: channel within the 32-ch slot
-    return slot * 64 + ((((ch >> 3) ^ (((col >> 3) & 1) << 1))) << 4) + ((ch & 7) << 1);
+  auto tr_addr = [&](int slot, int col, int ch, int row = 0) -> int {   // ch: channel within the 32-ch slot
+    const int swz = (((col >> 3) & 1) ^ (ROWSWZ ? (row & 1) : 0)) << 1;
+    return slot * 64 + (((ch >> 3) ^ swz) << 4) + ((ch & 7) << 1);
   };
   auto tr8 = [&](const char* base0, const char* base1) -> h16x8 {
     const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base0));
@@ -613,7 +619,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
         const bool row_in = (hr > 0 || top_in) && (hr < R + 1 || bot_in);
         const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)Wf &&
                         (GEO != WGEO_SEG || 16 * j + lslot <= W + 1);
-        const int off = ok ? (gr * Wf + col0 + 16 * j) * CA * 2 + xl : OOB;
+        const int off = ok ? (gr * Wf + col0 + 16 * j) * CA * 2 + ((ROWSWZ && (hr & 1)) ? xl_odd : xl) : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
                                                  off, 0, 0, 0);
       }
@@ -790,8 +796,9 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
         const int slotA = (rr + lr + dh) * HWP + colA;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          h16x8 af = tr8(Xs + tr_addr(slotA, colA, 16 * i + 4 * pp),
-                          Xs + tr_addr(slotA + 4, colA + 4, 16 * i + 4 * pp));
+          const int rowA = rr + lr + dh;            // halo row (row swizzle of 8-wide rows)
+          h16x8 af = tr8(Xs + tr_addr(slotA, colA, 16 * i + 4 * pp, rowA),
+                          Xs + tr_addr(slotA + 4, colA + 4, 16 * i + 4 * pp, rowA));
           if (W < 32 && !lane_ok) af = __builtin_bit_cast(h16x8, (u32x4){0u, 0u, 0u, 0u});
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[t][i][j] = mfma16(af, bf[j], acc[t][i][j]);

@@ -503,6 +503,11 @@ class NativeUNet:
         # head launch)
         self._head_fused_blocks = 0
         self._fuse_head = nch == 1 and os.environ.get("UNET_HEAD_FUSE", "1") != "0"
+        # convNb -> pool fusion (UNET_POOL_FUSE=0 keeps the separate pool launch)
+        self._pool_of = {}
+        self._pool_fused = set()
+        if os.environ.get("UNET_POOL_FUSE", "1") != "0":
+            self._pool_of = {self.inputs[x.name][0]: x.name for x in spec.layers if x.kind == "pool"}
         layers = [l for l in spec.layers if l.kind != "up"]
         i = 0
         while i < len(layers):
@@ -524,6 +529,7 @@ class NativeUNet:
         """Forward launches of layer `l` for images [c*nb, (c+1)*nb)."""
         spec = self.spec
         b = self.bufs
+        nch = self.B // nb
 
         def P(t):
             return None if t is None else _ptr(b[t]) + self._toff(t, c, nb)
@@ -550,6 +556,16 @@ class NativeUNet:
                      dst1=_ptr(b["z:" + l.name]) if normed else P(l.name),
                      drop_rate=spec.dropout if (l.dropout and dropout and not normed) else 0.0,
                      salt=self._salt(l.name))
+            pool = self._pool_of.get(l.name)
+            if pool is not None and not normed and nch == 1:
+                # fused 2x2 max-pool: the epilogue writes the pooled tensor + argmax codes
+                dp = dict(d, pool_dst=P(pool), pool_code=_ptr(self.pool_codes[pool]))
+                try:
+                    self.C.conv_fwd_grid(dp)
+                    d = dp
+                    self._pool_fused.add(pool)
+                except ValueError:
+                    pass
             if l.name == self.head_in and self._fuse_head and not normed and not d["drop_rate"]:
                 nbk = self._head_grid(d)
                 if nbk:
@@ -562,6 +578,8 @@ class NativeUNet:
             plan.add_conv_fwd(d)
             if normed:
                 self._norm_fwd(plan, l, dropout, train, fused)
+        elif l.kind == "pool" and l.name in self._pool_fused:
+            pass                                 # written by its source conv's epilogue
         elif l.kind == "pool":
             src = self.inputs[l.name][0]
             dd, hh, ww = self.sdims(l.level)
