@@ -124,7 +124,9 @@ def test_conv_dgrad_dual_dest_mask(cuda_dev):
 @pytest.mark.parametrize("N,H,C1,C2,Cout,tile", [
     (2, 128, 32, 0, 32, 6), (3, 128, 32, 32, 32, 6), (2, 64, 64, 0, 64, 6), (3, 64, 64, 64, 64, 6),
     (2, 64, 32, 0, 64, 6), (3, 16, 32, 0, 32, 6), (5, 16, 64, 0, 64, 6), (3, 32, 128, 0, 32, 6),
-    (1, 128, 32, 0, 64, 0), (2, 64, 64, 64, 64, 0), (2, 32, 64, 0, 128, 8)])
+    (1, 128, 32, 0, 64, 0), (2, 64, 64, 64, 64, 0), (2, 32, 64, 0, 128, 8),
+    (2, 128, 32, 0, 64, 12), (3, 128, 32, 32, 64, 12), (3, 64, 64, 64, 64, 12), (5, 16, 64, 0, 128, 12),
+    (3, 32, 128, 0, 64, 12), (2, 16, 256, 256, 256, 12)])
 def test_conv_row_window(cuda_dev, N, H, C1, C2, Cout, tile):
     """Row-window kernel (tile 6, auto for 16 <= W <= 128): image boundaries inside a window,
     row tails (N*H not a multiple of the window), concat sources, bias + ReLU + dropout."""
@@ -142,9 +144,10 @@ def test_conv_row_window(cuda_dev, N, H, C1, C2, Cout, tile):
     assert rel_err(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("N,H,W,C1,C2,Cout", [(2, 8, 256, 32, 0, 32), (1, 4, 384, 32, 32, 32),
-                                               (2, 8, 512, 64, 0, 64), (1, 4, 256, 64, 64, 64)])
-def test_conv_row_window_segmented_rows(cuda_dev, N, H, W, C1, C2, Cout):
+@pytest.mark.parametrize("N,H,W,C1,C2,Cout,tile", [(2, 8, 256, 32, 0, 32, 6), (1, 4, 384, 32, 32, 32, 6),
+                                                    (2, 8, 512, 64, 0, 64, 6), (1, 4, 256, 64, 64, 64, 6),
+                                                    (2, 8, 512, 64, 0, 64, 12), (1, 4, 256, 64, 64, 128, 12)])
+def test_conv_row_window_segmented_rows(cuda_dev, N, H, W, C1, C2, Cout, tile):
     """Rows wider than 128 run as 128-wide segments whose halo columns are the
     neighbouring segments' pixels (512x512 config levels)."""
     torch.manual_seed(N + H + W + C1 + C2)
@@ -155,7 +158,7 @@ def test_conv_row_window_segmented_rows(cuda_dev, N, H, W, C1, C2, Cout):
     out = torch.empty(N, H, W, Cout, device=cuda_dev, dtype=torch.bfloat16)
     C().conv_fwd(dict(N=N, OH=H, OW=W, IH=H, IW=W, KH=3, KW=3, pad=1, C1=C1, C2=C2, src1=ptr(a),
                       src2=ptr(b2) if C2 else None, wgt=ptr(pack_fwd(w)), bias=ptr(bias), Cout=Cout, relu=1,
-                      dst1=ptr(out), tile=6), stream())
+                      dst1=ptr(out), tile=tile), stream())
     xin = nchw(a.float()) if not C2 else torch.cat([nchw(a.float()), nchw(b2.float())], 1)
     ref = nhwc(F.relu(F.conv2d(xin, w.float().permute(3, 2, 0, 1), bias, padding=1)))
     assert rel_err(out, ref) < 1e-2
@@ -214,7 +217,7 @@ def test_conv_row_window_dgrad_dual_dest_mask_dropout(cuda_dev):
     dy = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
     d1 = torch.empty(N, H, H, C1, device=cuda_dev, dtype=torch.bfloat16)
     d2 = torch.empty(N, H, H, C2, device=cuda_dev, dtype=torch.bfloat16)
-    for tile in (6, 8):
+    for tile in (6, 8, 12):
         C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Co, src1=ptr(dy),
                           wgt=ptr(pack_dgrad(w)), Cout=C1 + C2, D1=C1, dst1=ptr(d1), dst2=ptr(d2),
                           mask1=ptr(m1), mask2=ptr(skip), mask_scale2=1.25, tile=tile), stream())
@@ -610,9 +613,10 @@ def test_upsample2_fwd_materialised(cuda_dev, dims3):
     assert torch.equal(y, ref)
 
 
-@pytest.mark.parametrize("N,H,Cin,Cout", [(2, 128, 32, 32), (2, 64, 32, 64), (4, 32, 64, 128), (4, 16, 128, 256),
-                                          (1, 256, 32, 32)])
-def test_conv_fwd_fused_maxpool_matches_pool_kernel(cuda_dev, N, H, Cin, Cout):
+@pytest.mark.parametrize("N,H,Cin,Cout,tile", [(2, 128, 32, 32, 0), (2, 64, 32, 64, 0), (4, 32, 64, 128, 0),
+                                               (4, 16, 128, 256, 0), (1, 256, 32, 32, 0), (2, 128, 32, 64, 12),
+                                               (2, 64, 32, 64, 12), (4, 32, 64, 128, 12), (4, 16, 128, 256, 12)])
+def test_conv_fwd_fused_maxpool_matches_pool_kernel(cuda_dev, N, H, Cin, Cout, tile):
     """convNb forward with the fused 2x2 max-pool epilogue: the conv output, the pooled
     tensor and the argmax codes equal the plain conv + the separate pool kernel."""
     torch.manual_seed(31)
@@ -624,7 +628,7 @@ def test_conv_fwd_fused_maxpool_matches_pool_kernel(cuda_dev, N, H, Cin, Cout):
     p0, p1 = [torch.empty(N, H // 2, H // 2, Cout, device=cuda_dev, dtype=torch.bfloat16) for _ in range(2)]
     c0, c1 = [torch.full((N * (H // 2) ** 2 * Cout // 8,), -1, device=cuda_dev, dtype=torch.int32) for _ in range(2)]
     d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(x), wgt=ptr(wp), bias=ptr(b),
-             Cout=Cout, relu=1)
+             Cout=Cout, relu=1, tile=tile)
     C().conv_fwd(dict(d, dst1=ptr(y0)), stream())
     C().generic("pool_fwd", [ptr(y0), ptr(p0), ptr(c0)], [N, 1, H, H, Cout, 0], [], stream())
     C().conv_fwd(dict(d, dst1=ptr(y1), pool_dst=ptr(p1), pool_code=ptr(c1)), stream())
@@ -632,3 +636,80 @@ def test_conv_fwd_fused_maxpool_matches_pool_kernel(cuda_dev, N, H, Cin, Cout):
     assert torch.equal(y0, y1)
     assert torch.equal(p0, p1)
     assert torch.equal(c0, c1)
+
+
+def _pack_bits(y):
+    """[..., C] activation -> [..., C / 8] uint8, bit e of byte b = channel 8b + e > 0."""
+    pos = (y.float() > 0).to(torch.int32).reshape(*y.shape[:-1], y.shape[-1] // 8, 8)
+    return (pos << torch.arange(8, device=y.device, dtype=torch.int32)).sum(-1).to(torch.uint8)
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,tile,drop", [(2, 128, 32, 32, 0, 0.0), (2, 64, 32, 64, 0, 0.0),
+                                                    (4, 16, 128, 256, 0, 0.0), (2, 32, 64, 64, 8, 0.0),
+                                                    (2, 128, 4, 32, 9, 0.0), (2, 16, 64, 128, 0, 0.3)])
+def test_conv_fwd_relu_bits(cuda_dev, N, H, Cin, Cout, tile, drop):
+    """A ReLU forward (row-window, implicit-GEMM, first-layer, dropout / generic
+    epilogue) also writes the 1-bit-per-element mask of its stored output, and the
+    output itself is unchanged."""
+    torch.manual_seed(41)
+    x = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, Cin, Cout, device=cuda_dev) * 0.1).bfloat16()
+    b = torch.randn(Cout, device=cuda_dev) * 0.1
+    wp = pack_fwd(w)
+    y0, y1 = [torch.empty(N, H, H, Cout, device=cuda_dev, dtype=torch.bfloat16) for _ in range(2)]
+    bits = torch.full((N, H, H, Cout // 8), 0xA5, device=cuda_dev, dtype=torch.uint8)
+    d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(x), wgt=ptr(wp), bias=ptr(b),
+             Cout=Cout, relu=1, drop_rate=drop, seed=5, salt=3, tile=tile)
+    C().conv_fwd(dict(d, dst1=ptr(y0)), stream())
+    C().conv_fwd(dict(d, dst1=ptr(y1), relu_bits=ptr(bits)), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    assert torch.equal(bits, _pack_bits(y1))
+
+
+@pytest.mark.parametrize("tile", [6, 8, 12])
+def test_conv_dgrad_bit_masks_match_activation_masks(cuda_dev, tile):
+    """Data gradient with two destinations whose ReLU masks come from bit tensors
+    (mask_bits) equals the same launch masked by the 16-bit activations."""
+    torch.manual_seed(42)
+    N, H, C1, C2, Co = 2, 64, 32, 32, 32
+    skip = F.relu(torch.randn(N, H, H, C2, device=cuda_dev)).bfloat16()
+    m1 = torch.randn(N, H, H, C1, device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, C1 + C2, Co, device=cuda_dev) * 0.1).bfloat16()
+    dy = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
+    outs = []
+    for bits in (False, True):
+        d1 = torch.empty(N, H, H, C1, device=cuda_dev, dtype=torch.bfloat16)
+        d2 = torch.empty(N, H, H, C2, device=cuda_dev, dtype=torch.bfloat16)
+        mk1 = _pack_bits(m1) if bits else m1
+        mk2 = _pack_bits(skip) if bits else skip
+        C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Co, src1=ptr(dy),
+                          wgt=ptr(pack_dgrad(w)), Cout=C1 + C2, D1=C1, dst1=ptr(d1), dst2=ptr(d2),
+                          mask1=ptr(mk1), mask2=ptr(mk2), mask_bits=3 if bits else 0, mask_scale2=1.25,
+                          tile=tile), stream())
+        torch.cuda.synchronize()
+        outs.append((d1, d2))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("H,Ci,Co,tile", [(32, 64, 32, 0), (8, 512, 256, 0), (32, 64, 32, 8)])
+def test_tconv_dgrad_bit_mask(cuda_dev, H, Ci, Co, tile):
+    """Transposed-conv data gradient (window and implicit-GEMM kernels) with its ReLU
+    mask read from a bit tensor."""
+    torch.manual_seed(43)
+    N = 2
+    x = torch.randn(N, H, H, Ci, device=cuda_dev).bfloat16()
+    k = (torch.randn(2, 2, Co, Ci, device=cuda_dev) * 0.1).bfloat16()
+    dout = torch.randn(N, 2 * H, 2 * H, Co, device=cuda_dev).bfloat16()
+    wdg = pad64(k.permute(3, 0, 1, 2).reshape(Ci, 4 * Co))
+    res = []
+    for bits in (False, True):
+        dx = torch.empty(N, H, H, Ci, device=cuda_dev, dtype=torch.bfloat16)
+        mk = _pack_bits(x) if bits else x
+        C().conv_fwd(dict(N=N, OH=H, OW=H, IH=2 * H, IW=2 * H, KH=2, KW=2, stride=2, pad=0, C1=Co,
+                          src1=ptr(dout), wgt=ptr(wdg), Cout=Ci, dst1=ptr(dx), mask1=ptr(mk),
+                          mask_bits=int(bits), tile=tile), stream())
+        torch.cuda.synchronize()
+        res.append(dx)
+    assert torch.equal(res[0], res[1])

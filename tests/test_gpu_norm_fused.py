@@ -25,15 +25,18 @@ def _moments(z):            # z: [N, H, W, C] -> per-sample [N, 2, C]
     return torch.stack([zf.sum(1), (zf * zf).sum(1)], 1)
 
 
-@pytest.mark.parametrize("N,H,Cin,Cout,C2", [
-    (2, 128, 32, 32, 0),      # row window, 128-wide rows
-    (4, 16, 64, 64, 0),       # row window, 16-wide rows
-    (2, 32, 32, 64, 32),      # row window, concat source
-    (8, 8, 128, 256, 0),      # implicit GEMM (8-wide rows), tiles span samples
-    (2, 64, 4, 32, 0),        # first-layer window kernel
-    (2, 256, 32, 32, 0),      # segmented 128-wide windows
+@pytest.mark.parametrize("N,H,Cin,Cout,C2,tile", [
+    (2, 128, 32, 32, 0, 0),      # row window, 128-wide rows
+    (4, 16, 64, 64, 0, 0),       # row window, 16-wide rows
+    (2, 32, 32, 64, 32, 0),      # row window, concat source
+    (8, 8, 128, 256, 0, 0),      # implicit GEMM (8-wide rows), tiles span samples
+    (2, 64, 4, 32, 0, 0),        # first-layer window kernel
+    (2, 256, 32, 32, 0, 0),      # segmented 128-wide windows
+    (2, 128, 32, 64, 0, 12),     # 64-channel row window (256-pixel windows)
+    (4, 16, 64, 128, 0, 12),
+    (2, 32, 32, 64, 32, 12),
 ])
-def test_conv_fwd_stats_epilogue(cuda_dev, N, H, Cin, Cout, C2):
+def test_conv_fwd_stats_epilogue(cuda_dev, N, H, Cin, Cout, C2, tile):
     torch.manual_seed(0)
     x = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
     x2 = torch.randn(N, H, H, max(C2, 1), device=cuda_dev).bfloat16()
@@ -42,7 +45,7 @@ def test_conv_fwd_stats_epilogue(cuda_dev, N, H, Cin, Cout, C2):
     z = torch.empty(N, H, H, Cout, device=cuda_dev, dtype=torch.bfloat16)
     wp = pack_fwd(w)            # kept alive: the kernel reads it after later allocations
     d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, C2=C2, src1=ptr(x),
-             src2=ptr(x2) if C2 else None, wgt=ptr(wp), bias=ptr(b), Cout=Cout, relu=0, dst1=ptr(z))
+             src2=ptr(x2) if C2 else None, wgt=ptr(wp), bias=ptr(b), Cout=Cout, relu=0, dst1=ptr(z), tile=tile)
     rows, px = C().conv_stat_tiles(dict(d, stats=1))
     assert rows > 0
     st = torch.full((rows, 2, Cout), float("nan"), device=cuda_dev)
@@ -66,13 +69,15 @@ def _keep(q_idx, C, seed, salt, rate):
     return h >= int(rate * 4294967296.0)
 
 
-@pytest.mark.parametrize("N,H,Cg,Cy,gn,drop", [
-    (2, 64, 64, 32, False, 0.0),     # row window dgrad (d: 64 -> 32 channels), BatchNorm coefficients
-    (2, 32, 64, 64, True, 0.2),      # GroupNorm coefficients + dropout keep recomputed
-    (8, 8, 256, 128, False, 0.2),    # implicit GEMM dgrad (8-wide)
-    (4, 16, 128, 64, True, 0.0),     # 16-wide window, GroupNorm
+@pytest.mark.parametrize("N,H,Cg,Cy,gn,drop,tile", [
+    (2, 64, 64, 32, False, 0.0, 0),     # row window dgrad (d: 64 -> 32 channels), BatchNorm coefficients
+    (2, 32, 64, 64, True, 0.2, 0),      # GroupNorm coefficients + dropout keep recomputed
+    (8, 8, 256, 128, False, 0.2, 0),    # implicit GEMM dgrad (8-wide)
+    (4, 16, 128, 64, True, 0.0, 0),     # 16-wide window, GroupNorm
+    (2, 32, 64, 64, True, 0.2, 12),     # 64-channel row window
+    (2, 128, 32, 64, False, 0.0, 12),
 ])
-def test_conv_dgrad_norm_epilogue(cuda_dev, N, H, Cg, Cy, gn, drop):
+def test_conv_dgrad_norm_epilogue(cuda_dev, N, H, Cg, Cy, gn, drop, tile):
     """dgrad of a conv whose input y = dropout(relu(a z + c)): g = dgrad * mask, stats."""
     torch.manual_seed(1)
     dz = torch.randn(N, H, H, Cg, device=cuda_dev).bfloat16()       # gradient at the conv's output
@@ -86,7 +91,7 @@ def test_conv_dgrad_norm_epilogue(cuda_dev, N, H, Cg, Cy, gn, drop):
     wp = pack_dgrad(w)
     d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cg, src1=ptr(dz), wgt=ptr(wp),
              Cout=Cy, relu=0, dst1=ptr(g), nz=ptr(z), na=ptr(a), nc=ptr(c), ncs=Cy if gn else 0,
-             npix=H * H, nd_rate=drop, nd_salt=salt, seed=seed)
+             npix=H * H, nd_rate=drop, nd_salt=salt, seed=seed, tile=tile)
     rows, px = C().conv_stat_tiles(dict(d, stats=1))
     assert rows > 0
     st = torch.full((rows, 2, Cy), float("nan"), device=cuda_dev)

@@ -86,6 +86,40 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return r;
 }
 
+// ReLU masks of 8 packed 16-bit values (bf16 / fp16 alike: > 0 <=> sign bit clear and
+// not zero; -0 counts as not positive).  pos_bits: bit e = element e > 0.
+__device__ __forceinline__ uint32_t pos_bits(const u32x4& v) {
+  // a 16-bit value moved to the top of a word is > 0 as int32 iff its sign bit is clear
+  // and it is not zero: one shift / mask and one signed compare per element
+  uint32_t b = 0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    b |= ((int32_t)(v[e] << 16) > 0 ? 1u : 0u) << (2 * e);
+    b |= ((int32_t)(v[e] & 0xffff0000u) > 0 ? 1u : 0u) << (2 * e + 1);
+  }
+  return b;
+}
+// v with element e zeroed unless bit e of `bits` is set
+__device__ __forceinline__ u32x4 keep_bits(u32x4 v, uint32_t bits) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t lo = ((bits >> (2 * e)) & 1u) ? 0xffffu : 0u;
+    const uint32_t hi = ((bits >> (2 * e + 1)) & 1u) ? 0xffff0000u : 0u;
+    v[e] &= (lo | hi);
+  }
+  return v;
+}
+// v with element e zeroed unless element e of the activation m is > 0
+__device__ __forceinline__ u32x4 keep_pos(u32x4 v, const u32x4& m) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t keep_lo = (int32_t)(m[e] << 16) > 0 ? 0xffffu : 0u;
+    const uint32_t keep_hi = (int32_t)(m[e] & 0xffff0000u) > 0 ? 0xffff0000u : 0u;
+    v[e] &= (keep_lo | keep_hi);
+  }
+  return v;
+}
+
 // Counter-based dropout hash (murmur3 fmix32 of (index, seed, salt)).  The
 // PyTorch reference reproduces it bit-for-bit
 // (models/reference.py::_hash_u32) so both paths draw the same keep-mask.

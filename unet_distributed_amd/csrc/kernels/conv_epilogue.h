@@ -50,7 +50,7 @@ __host__ __device__ inline const char* conv_norm_epi_check(const ConvFwdParams& 
   if (!p.stats && !p.nz) return nullptr;
   if (!p.stats) return "conv_fwd: nz (dgrad-norm epilogue) needs a stats buffer";
   if (p.relu || p.shuffle || p.drop_rate > 0.f || p.out_scale != 1.f || p.D1 != p.Cout || p.mask1 || p.mask2 ||
-      p.head_w)
+      p.head_w || p.relu_bits || p.mask_bits)
     return "conv_fwd: statistics epilogue takes no ReLU / dropout / shuffle / scale / split / mask / head";
   if (p.nz && (p.bias || !p.na || !p.nc || p.npix <= 0 || p.mask_scale1 != 1.f || (p.ncs != 0 && p.ncs != p.Cout)))
     return "conv_fwd: dgrad-norm epilogue needs na / nc / npix, no bias";
@@ -279,12 +279,19 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     const int co = side1 ? n : n - p.D1;
     h16* dst = (h16*)(side1 ? p.dst1 : p.dst2);
     const h16* mk = (const h16*)(side1 ? p.mask1 : p.mask2);
+    const bool mbit = (p.mask_bits >> (side1 ? 0 : 1)) & 1;
     u32x4 mv[NIT];
+    uint32_t mb[NIT];
     if (mk) {
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
         const int q = qof(ml0 + it * RPI);
-        if (q < M) mv[it] = *(const u32x4*)(mk + (size_t)q * rs + co);
+        if (q < M) {
+          if (mbit)
+            mb[it] = ((const uint8_t*)mk)[((size_t)q * rs + co) >> 3];
+          else
+            mv[it] = *(const u32x4*)(mk + (size_t)q * rs + co);
+        }
       }
     }
 #pragma unroll
@@ -295,16 +302,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
       const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
       u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
-      if (mk) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t w = mv[it][e];
-          const uint32_t lo16 = w & 0xffffu, hi16 = w >> 16;
-          const uint32_t keep_lo = (lo16 != 0u && !(lo16 & 0x8000u)) ? 0xffffu : 0u;
-          const uint32_t keep_hi = (hi16 != 0u && !(hi16 & 0x8000u)) ? 0xffff0000u : 0u;
-          v[e] &= (keep_lo | keep_hi);
-        }
-      }
+      if (mk) v = mbit ? keep_bits(v, mb[it]) : keep_pos(v, mv[it]);
       *(u32x4*)(dst + (size_t)q * rs + co) = v;
     }
     return;
@@ -349,6 +347,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     size_t off;
     h16* dst;
     const void* mk;
+    bool mbit = false;
     if (EPI == EPI_FWD || EPI == EPI_STATS) {
       off = (size_t)q * p.Cout + n;
       dst = (h16*)p.dst1;
@@ -371,28 +370,24 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       off = pix * Dt + co;
       dst = (h16*)p.dst1;
       mk = p.mask1;
+      mbit = p.mask_bits & 1;
     } else if (n < p.D1) {
       off = (size_t)q * p.D1 + n;
       dst = (h16*)p.dst1;
       mk = p.mask1;
+      mbit = p.mask_bits & 1;
     } else {
       off = (size_t)q * (p.Cout - p.D1) + (n - p.D1);
       dst = (h16*)p.dst2;
       mk = p.mask2;
+      mbit = (p.mask_bits >> 1) & 1;
     }
     if (EPI != EPI_FWD && EPI != EPI_STATS && mk) {
-      const u32x4 mv = *(const u32x4*)((const h16*)mk + off);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        // bf16 > 0 <=> sign bit clear and not zero (-0 counts as not positive)
-        const uint32_t w = mv[e];
-        const uint32_t lo16 = w & 0xffffu, hi16 = w >> 16;
-        const uint32_t keep_lo = (lo16 != 0u && !(lo16 & 0x8000u)) ? 0xffffu : 0u;
-        const uint32_t keep_hi = (hi16 != 0u && !(hi16 & 0x8000u)) ? 0xffff0000u : 0u;
-        v[e] &= (keep_lo | keep_hi);
-      }
+      // (off is a multiple of 8: the bit tensor's byte of these 8 channels is off / 8)
+      v = mbit ? keep_bits(v, ((const uint8_t*)mk)[off >> 3]) : keep_pos(v, *(const u32x4*)((const h16*)mk + off));
     }
     *(u32x4*)(dst + off) = v;
+    if ((EPI == EPI_FWD || G) && p.relu_bits) p.relu_bits[off >> 3] = (uint8_t)pos_bits(v);
     if constexpr (kHeadable) {
       if (kHead) {
         float f[8];

@@ -329,10 +329,38 @@ hipError_t launch_cfg(const ConvFwdParams& p, hipStream_t s) {
 // 2 = 3D full rows (three depth taps).  Compile-time so the common 2D case carries no
 // segment / depth state (extra SGPR state spilled to VGPR lanes inside the chunk loop).
 enum { GEO_2D = 0, GEO_SEG = 1, GEO_3D = 2 };
+
+// Window pixels of a BN-wide tile: 512 (256 for 16-wide rows); the 64-channel tile
+// halves the window so its accumulators (4 x 4 fragments per wave) and LDS
+// (halo + 36 KB of weights per chunk) still fit two workgroups per CU.
+__host__ __device__ constexpr int win_bm(int W, int BN) { return (W == 16 || BN == 64) ? 256 : 512; }
+
+// Output-channel tile of the row-window conv: 64 where Cout allows it and the row
+// width is enabled in UNET_WIN_BN64 (bit mask over W = 16 / 32 / 64 / 128 -> bits
+// 0..3; read once per process), else 32.  Default 7 (W = 16..64), from a same-box
+// sweep of the headline step: +2.8 % (16), +0.5 % (32), +0.4 % (64), -0.3 % (128).
+// 64 halves the halo image's LDS-DMA and fragment reads per MFMA and doubles the MFMA
+// work per synchronisation.
+static int win_bn(const ConvFwdParams& p) {
+  static const int mask = [] {
+    const char* e = getenv("UNET_WIN_BN64");
+    return e ? atoi(e) : 7;
+  }();
+  if (p.tile == 12) return 64;                       // forced (tests / A-B)
+  if (p.tile == 6) return 32;
+  const int W = p.OW > 128 ? 128 : p.OW;
+  const int bit = W == 16 ? 1 : W == 32 ? 2 : W == 64 ? 4 : 8;
+  return (p.Cout % 64 == 0 && (mask & bit) && !p.head_w) ? 64 : 32;
+}
+static int win_rows(const ConvFwdParams& p) {
+  const int W = p.OW > 128 ? 128 : p.OW;
+  return win_bm(W, win_bn(p)) / W;
+}
+
 template <int W, int BN, bool CONCAT, int EPI, int GEO>
 __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   static_assert(BN == 32 || BN == 64, "row-window tile is 32 or 64 output channels wide");
-  constexpr int BM = W == 16 ? 256 : 512;       // window pixels (16-wide rows: 16 rows)
+  constexpr int BM = win_bm(W, BN);             // window pixels
   constexpr int R = BM / W, HR = R + 2;
   constexpr int HWP = ((W + 2 + 15) / 16) * 16; // halo row pitch in 64-byte pixel slots
   constexpr int IPR = HWP / 16;                 // LDS-DMA wave-instructions per halo row
@@ -952,18 +980,17 @@ hipError_t launch_tconv_dgrad(const ConvFwdParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int BN>
 int win_grid(const ConvFwdParams& p) {
   const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
   const int rows = p.N * p.OD * p.OH;
-  const int R = (W == 16 ? 256 : 512) / W;
-  return ((rows + R - 1) / R) * (p.OW / W) * (p.Cout / BN);
+  const int R = win_rows(p);
+  return ((rows + R - 1) / R) * (p.OW / W) * (p.Cout / win_bn(p));
 }
 
 template <int BN>
 hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
   const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
-  const int grid = win_grid<BN>(p);
+  const int grid = win_grid(p);
   const bool cc = p.C2 > 0;
   const int epi = conv_epi_mode(p);
   const int geo = p.KD == 3 ? GEO_3D : (p.OW > W ? GEO_SEG : GEO_2D);
@@ -1085,20 +1112,26 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.shuffle && ((p.Cout >> p.shuffle) % 8)) return "conv_fwd: shuffle channels must be multiples of 8";
   if (p.shuffle && p.D1 != p.Cout) return "conv_fwd: shuffle with channel split unsupported";
   if (const char* m = conv_norm_epi_check(p)) return m;
+  if (p.relu_bits && (!p.relu || p.shuffle || p.D1 != p.Cout || p.mask1 || p.mask2))
+    return "conv_fwd: relu_bits needs an unsplit ReLU forward";
+  if ((p.mask_bits & ~3) || ((p.mask_bits & 1) && !p.mask1) || ((p.mask_bits & 2) && !p.mask2))
+    return "conv_fwd: mask_bits marks a missing mask";
   if (p.pool_dst) {
     const int W = p.OW > 128 ? 128 : p.OW;
-    const int R = (W == 16 ? 256 : 512) / W;
+    const int R = win_rows(p);
     if (!p.pool_code || conv_epi_mode(p) != EPI_FWD || !win_eligible(p) || p.KD != 1 || p.OD != 1 || R % 2 ||
         p.OH % 2 || p.OW % 2 || p.Cout % 8 || p.head_w)
       return "conv_fwd: fused max-pool needs a 2D row-window ReLU forward (even rows, codes buffer)";
   }
-  if (p.tile < 0 || p.tile > 11) return "conv_fwd: bad tile id";
+  if (p.tile < 0 || p.tile > 12) return "conv_fwd: bad tile id";
+  if (p.tile == 12 && (!win_eligible(p) || p.Cout % 64 || p.head_w))
+    return "conv_fwd: 64-wide row-window tile not applicable";
   if (p.tile == 10 && !tconv_fwd_eligible(p)) return "conv_fwd: transposed-conv window tile not applicable";
   if (p.tile == 11 && !tconv_dgrad_eligible(p)) return "conv_fwd: transposed-conv dgrad tile not applicable";
   if (p.tile == 9 && !win_first_eligible(p)) return "conv_fwd: first-layer window tile not applicable";
   {
     const int t = p.tile ? p.tile : 0;
-    const int bn = t == 1 ? 128 : (t == 2 || t == 5 || t == 7) ? 64 : 32;
+    const int bn = t == 1 ? 128 : (t == 2 || t == 5 || t == 7 || t == 12) ? 64 : 32;
     if (t && p.Cout % bn) return "conv_fwd: forced tile does not divide Cout";
     if (t == 7) return "conv_fwd: tile 7 (row-window 512x64: 268 registers, 92 KB LDS, 1 wave/SIMD) is not built";
     if (t == 6 && !win_eligible(p)) return "conv_fwd: row-window tile not applicable";
@@ -1146,7 +1179,10 @@ int conv_fwd_pick(const ConvFwdParams& p) {
   return 4;
 }
 
-int conv_fwd_grid(const ConvFwdParams& p) { return conv_fwd_pick(p) == 6 ? win_grid<32>(p) : 0; }
+int conv_fwd_grid(const ConvFwdParams& p) {
+  const int t = conv_fwd_pick(p);
+  return (t == 6 || t == 12) ? win_grid(p) : 0;
+}
 
 void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
   *rows = *tile_px = 0;
@@ -1154,9 +1190,10 @@ void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
   const int t = conv_fwd_pick(p);
   const bool smallc = (p.C1 == 4 || p.C1 == 8) && p.C2 == 0;
   switch (t) {
-    case 6: {        // row window: R rows x (segment) width, tiles in (row group, segment) order
+    case 6:
+    case 12: {       // row window: R rows x (segment) width, tiles in (row group, segment) order
       const int W = p.OW > 128 ? 128 : p.OW;
-      const int R = (W == 16 ? 256 : 512) / W;
+      const int R = win_rows(p);
       if (p.nz && p.C2) return;
       *rows = ((p.N * p.OD * p.OH + R - 1) / R) * (p.OW / W);
       *tile_px = R * W;
@@ -1194,7 +1231,8 @@ hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
     case 2: return launch_cfg<128, 64, 2, 2>(p, s);
     case 3: return launch_cfg<256, 32, 4, 1>(p, s);
     case 5: return launch_cfg<256, 64, 4, 1>(p, s);
-    case 6: return launch_win<32>(p, s);
+    case 6:
+    case 12: return win_bn(p) == 64 ? launch_win<64>(p, s) : launch_win<32>(p, s);
     case 9: return p.C1 == 4 ? launch_win_first<4>(p, s) : launch_win_first<8>(p, s);
     case 10: return launch_tconv_fwd(p, s);
     case 11: return launch_tconv_dgrad(p, s);

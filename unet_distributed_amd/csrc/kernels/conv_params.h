@@ -58,7 +58,14 @@ struct ConvFwdParams {
   // separate pool launch and its full re-read of the conv output disappear.
   void* pool_dst;
   uint32_t* pool_code;
-  int tile;                   // 0 = auto, else forced tile config id (tuning / A-B tests)
+  // ReLU bit masks, 1 bit per element: [pixels][C / 8] bytes, bit e of byte b set when
+  // channel 8b + e of the stored 16-bit activation is > 0.  relu_bits: written by a ReLU
+  // forward (generic / EPI_FWD epilogue).  mask_bits bit 0 / 1: mask1 / mask2 point to
+  // such bit tensors instead of activations -- the data gradient's ReLU mask then costs
+  // 1/16 of the bytes of re-reading the activation.
+  uint8_t* relu_bits;
+  int mask_bits;
+  int tile;                  // 0 = auto, else forced tile config id (tuning / A-B tests)
   // Fused segmentation head (row-window forward, Cout == 32, EPI_FWD only): per pixel
   // z = sum_c out[c] head_w[c] + head_b -> head_logit (fp32) for head_finish
   const float* head_w;

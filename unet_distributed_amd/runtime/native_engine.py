@@ -276,6 +276,22 @@ class NativeUNet:
             elif l.kind == "mask":
                 self.inputs[l.name] = (cur, 1, None)
                 self.head_in = cur
+        # ReLU bit masks (conv_params.h relu_bits): the forward of every ReLU conv whose
+        # output masks a data gradient also writes 1 bit per element, and those data
+        # gradients read the bits instead of the 16-bit activation -- at b1024 ~8 GB
+        # less backward traffic (UNET_RELU_BITS=0 keeps the activation masks).  Pool
+        # outputs need no mask at all: the pool backward routes a gradient only where
+        # the window maximum is positive (code flag bits).  UNET_RELU_BITS = 1 (all
+        # levels), 0 (none) or a comma list of levels.
+        self.relu_bits: Dict[str, torch.Tensor] = {}
+        self.pool_outs = {l.name for l in spec.layers if l.kind == "pool"}
+        rb = os.environ.get("UNET_RELU_BITS", "1")
+        rb_levels = None if rb == "1" else {int(v) for v in rb.split(",") if v.strip() and v != "0"}
+        if spec.norm == "none":
+            for l in spec.layers:
+                if l.kind == "conv" and l.name != self.head_in and (rb_levels is None or l.level in rb_levels):
+                    self.relu_bits[l.name] = torch.zeros(self.npix(l.level) * l.cout // 8, dtype=torch.uint8,
+                                                         device=self.device)
         P = self.npix(1)
         self.prob = torch.zeros(P, dtype=torch.float32, device=self.device)
         nb = self.C.head_blocks(P)
@@ -445,6 +461,17 @@ class NativeUNet:
         ops.append(emit)
         return ops
 
+    def _relu_mask(self, tname):
+        """(mask pointer, is-bits) of the ReLU mask a data gradient into tensor `tname`
+        applies: its bit tensor when the forward writes one, none for a pool output
+        (norm-free model: the pool backward routes only to positive maxima), else the
+        16-bit activation itself."""
+        if tname in self.relu_bits:
+            return _ptr(self.relu_bits[tname]), 1
+        if tname in self.pool_outs and self.spec.norm == "none":
+            return None, 0
+        return _ptr(self.bufs[tname]), 0
+
     def _fuse_dgrad_norm(self, d, tname):
         """dgrad dict `d` writes the gradient of tensor `tname`: when that is a
         normalised conv output, let its epilogue recompute the ReLU / dropout mask
@@ -453,7 +480,7 @@ class NativeUNet:
             return
         l = next(x for x in self.spec.layers if x.name == tname)
         C = l.cout
-        d2 = dict(d, mask1=None, mask_scale1=1.0, nz=_ptr(self.bufs["z:" + tname]),
+        d2 = dict(d, mask1=None, mask_bits=0, mask_scale1=1.0, nz=_ptr(self.bufs["z:" + tname]),
                   na=_ptr(self.bufs["fa:" + tname]), nc=_ptr(self.bufs["fc:" + tname]),
                   ncs=0 if self.spec.norm == "batch" else C, npix=self.npix(l.level) // self.B,
                   nd_rate=self.spec.dropout if self.tinfo[tname][3] else 0.0, nd_salt=self._salt(tname))
@@ -556,6 +583,9 @@ class NativeUNet:
                      dst1=_ptr(b["z:" + l.name]) if normed else P(l.name),
                      drop_rate=spec.dropout if (l.dropout and dropout and not normed) else 0.0,
                      salt=self._salt(l.name))
+            bits = self.relu_bits.get(l.name)
+            if bits is not None and not normed:
+                d["relu_bits"] = _ptr(bits) + c * nb * (self.npix(l.level) // self.B) * l.cout // 8
             pool = self._pool_of.get(l.name)
             if pool is not None and not normed and nch == 1:
                 # fused 2x2 max-pool: the epilogue writes the pooled tensor + argmax codes
@@ -715,8 +745,8 @@ class NativeUNet:
                                  wgt=self.wptr(l.name, "dg"), Cout=l.cin, relu=0)
                         if skip is None:
                             lvl, ch, relu_src, drop = self.tinfo[src1]
-                            d.update(dst1=_ptr(b["d:" + src1]), D1=l.cin,
-                                     mask1=_ptr(b[src1]) if relu_src else None,
+                            m1, mb = self._relu_mask(src1) if relu_src else (None, 0)
+                            d.update(dst1=_ptr(b["d:" + src1]), D1=l.cin, mask1=m1, mask_bits=mb,
                                      mask_scale1=(1.0 / (1.0 - spec.dropout)) if drop else 1.0)
                             self._fuse_dgrad_norm(d, src1)
                         else:
@@ -724,8 +754,9 @@ class NativeUNet:
                                 dst1 = b["dfull:" + src1]          # full-res grad of the folded upsample
                             else:
                                 dst1 = b["d:" + src1]              # tconv output: linear, no mask
+                            m2, mb = self._relu_mask(skip)
                             d.update(dst1=_ptr(dst1), D1=c1, dst2=_ptr(b["dskip:" + skip]),
-                                     mask2=_ptr(b[skip]))
+                                     mask2=m2, mask_bits=2 * mb)
                         return d
                     dd_ = mk()                 # built now: it decides the fused norm backward
                     emit_conv(lambda dd_=dd_: dd_)
@@ -776,9 +807,10 @@ class NativeUNet:
 
                 def mk(l=l, src=src, du=du):
                     d = self._conv_common(l.level + 1, 2, 2, 0, out_level=l.level + 1, in_level=l.level)
+                    m1, mb = self._relu_mask(src)
                     d.update(name="dgrad:" + l.name, C1=l.cout, src1=_ptr(du),
                              wgt=self.wptr(l.name, "dg"), Cout=l.cin, relu=0,
-                             dst1=_ptr(b["d:" + src]), mask1=_ptr(b[src]))
+                             dst1=_ptr(b["d:" + src]), mask1=m1, mask_bits=mb)
                     self._fuse_dgrad_norm(d, src)
                     return d
                 dd_ = mk()
