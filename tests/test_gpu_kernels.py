@@ -713,3 +713,40 @@ def test_tconv_dgrad_bit_mask(cuda_dev, H, Ci, Co, tile):
         torch.cuda.synchronize()
         res.append(dx)
     assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.parametrize("N,H,C1,C2,Co", [(2, 128, 32, 32, 32), (2, 64, 64, 64, 64), (4, 32, 128, 128, 128),
+                                          (4, 16, 256, 256, 256)])
+def test_dgrad_skip_half_with_fused_pool_backward(cuda_dev, N, H, C1, C2, Co):
+    """Decoder conv data gradient split in two: the upsampled half alone, and the skip
+    half later with the max-pool backward in its epilogue (route_gy) -- equal, bit for
+    bit, to the dual-destination dgrad + the separate argmax-code pool backward."""
+    torch.manual_seed(44)
+    y = F.relu(torch.randn(N, H, H, C2, device=cuda_dev)).bfloat16()        # convNb output (skip source)
+    pooled = torch.empty(N, H // 2, H // 2, C2, device=cuda_dev, dtype=torch.bfloat16)
+    codes = torch.zeros(N * (H // 2) ** 2 * C2 // 8, device=cuda_dev, dtype=torch.int32)
+    C().generic("pool_fwd", [ptr(y), ptr(pooled), ptr(codes)], [N, 1, H, H, C2, 0], [], stream())
+    dpool = torch.randn(N, H // 2, H // 2, C2, device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, C1 + C2, Co, device=cuda_dev) * 0.1).bfloat16()
+    wdg = pack_dgrad(w)                                  # [C1 + C2][9 Co pad 64]
+    dy = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
+    bits = _pack_bits(y)
+    geo = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Co, src1=ptr(dy))
+    # reference path: both halves in one dgrad, then the pool backward
+    d_up0 = torch.empty(N, H, H, C1, device=cuda_dev, dtype=torch.bfloat16)
+    dskip = torch.empty(N, H, H, C2, device=cuda_dev, dtype=torch.bfloat16)
+    dy0 = torch.empty(N, H, H, C2, device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(geo, wgt=ptr(wdg), Cout=C1 + C2, D1=C1, dst1=ptr(d_up0), dst2=ptr(dskip), mask2=ptr(bits),
+                      mask_bits=2), stream())
+    C().generic("pool_bwd", [ptr(y), ptr(dpool), ptr(dskip), ptr(dy0), ptr(codes)], [N, 1, H, H, C2, 0], [],
+                stream())
+    # split path
+    d_up1 = torch.empty_like(d_up0)
+    dy1 = torch.empty_like(dy0)
+    C().conv_fwd(dict(geo, wgt=ptr(wdg), Cout=C1, dst1=ptr(d_up1)), stream())
+    C().conv_fwd(dict(geo, wgt=ptr(wdg) + 2 * C1 * wdg.shape[1], Cout=C2, dst1=ptr(dy1), mask1=ptr(bits),
+                      mask_bits=1, route_gy=ptr(dpool), pool_code=ptr(codes)), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(d_up0, d_up1)
+    assert torch.equal(dy0, dy1)
+    assert dy1.float().abs().sum() > 0

@@ -50,7 +50,7 @@ __host__ __device__ inline const char* conv_norm_epi_check(const ConvFwdParams& 
   if (!p.stats && !p.nz) return nullptr;
   if (!p.stats) return "conv_fwd: nz (dgrad-norm epilogue) needs a stats buffer";
   if (p.relu || p.shuffle || p.drop_rate > 0.f || p.out_scale != 1.f || p.D1 != p.Cout || p.mask1 || p.mask2 ||
-      p.head_w || p.relu_bits || p.mask_bits)
+      p.head_w || p.relu_bits || p.mask_bits || p.route_gy)
     return "conv_fwd: statistics epilogue takes no ReLU / dropout / shuffle / scale / split / mask / head";
   if (p.nz && (p.bias || !p.na || !p.nc || p.npix <= 0 || p.mask_scale1 != 1.f || (p.ncs != 0 && p.ncs != p.Cout)))
     return "conv_fwd: dgrad-norm epilogue needs na / nc / npix, no bias";
@@ -294,6 +294,25 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
         }
       }
     }
+    // fused pool backward (route_gy, 2D, one destination): pixel q = (row g, column w)
+    // is window position k = 2 (g & 1) + (w & 1) of pooled pixel (g / 2, w / 2)
+    const bool route = p.route_gy != nullptr;
+    u32x4 rg[NIT];
+    uint32_t rc[NIT], rk[NIT];
+    if (route) {
+      const int OW = p.OW, cpp = p.Cout >> 3;
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int q = qof(ml0 + it * RPI);
+        if (q < M) {
+          const int g = q / OW, w = q - g * OW;
+          const size_t pq = (size_t)(g >> 1) * (OW >> 1) + (w >> 1);
+          rc[it] = p.pool_code[pq * cpp + (n >> 3)];
+          rg[it] = *(const u32x4*)((const h16*)p.route_gy + pq * p.Cout + n);
+          rk[it] = ((uint32_t)(g & 1) << 1) | (uint32_t)(w & 1);
+        }
+      }
+    }
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int ml = ml0 + it * RPI;
@@ -303,6 +322,18 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
       u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
       if (mk) v = mbit ? keep_bits(v, mb[it]) : keep_pos(v, mv[it]);
+      if (route) {
+        // the (masked, 16-bit rounded) skip gradient plus the routed pool gradient,
+        // in the order and precision of elementwise.hip::maxpool2_bwd_code_kernel
+        float o[8], gg[8];
+        unpack8(v, o);
+        unpack8(rg[it], gg);
+        const uint32_t cw = rc[it];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (((cw >> (2 * e)) & 3u) == rk[it] && ((cw >> (24 + e)) & 1u)) o[e] += gg[e];
+        v = pack8(o);
+      }
       *(u32x4*)(dst + (size_t)q * rs + co) = v;
     }
     return;

@@ -1116,6 +1116,10 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     return "conv_fwd: relu_bits needs an unsplit ReLU forward";
   if ((p.mask_bits & ~3) || ((p.mask_bits & 1) && !p.mask1) || ((p.mask_bits & 2) && !p.mask2))
     return "conv_fwd: mask_bits marks a missing mask";
+  if (p.route_gy && (!p.pool_code || conv_epi_mode(p) != EPI_DGRAD || !win_eligible(p) || p.KD != 1 || p.OD != 1 ||
+                     p.OH % 2 || p.OW % 2 || p.D1 != p.Cout || p.pool_dst || p.mask_scale1 != 1.f ||
+                     (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12)))
+    return "conv_fwd: fused pool backward needs a 2D row-window data gradient (even dims, one destination, codes)";
   if (p.pool_dst) {
     const int W = p.OW > 128 ? 128 : p.OW;
     const int R = win_rows(p);

@@ -65,6 +65,12 @@ struct ConvFwdParams {
   // 1/16 of the bytes of re-reading the activation.
   uint8_t* relu_bits;
   int mask_bits;
+  // Fused 2x2 max-pool backward in a data gradient (2D row-window EPI_DGRAD, the skip
+  // half of a decoder conv's dgrad, deferred until the pool's output gradient exists):
+  // the epilogue adds route_gy[pooled pixel][c] where this pixel is the first argmax of
+  // its window and the maximum is positive (pool_code, maxpool2_fwd layout) -- the
+  // gradient of the convNb output in one pass, no separate skip-gradient tensor.
+  const void* route_gy;
   int tile;                  // 0 = auto, else forced tile config id (tuning / A-B tests)
   // Fused segmentation head (row-window forward, Cout == 32, EPI_FWD only): per pixel
   // z = sum_c out[c] head_w[c] + head_b -> head_logit (fp32) for head_finish

@@ -105,6 +105,7 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.pool_code = (uint32_t*)const_cast<void*>(getp(d, "pool_code"));
   p.relu_bits = (uint8_t*)const_cast<void*>(getp(d, "relu_bits"));
   p.mask_bits = get<int>(d, "mask_bits", 0);
+  p.route_gy = getp(d, "route_gy");
   p.tile = get<int>(d, "tile", 0);
   p.head_w = (const float*)getp(d, "head_w");
   p.head_b = (const float*)getp(d, "head_b");

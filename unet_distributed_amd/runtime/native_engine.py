@@ -461,6 +461,31 @@ class NativeUNet:
         ops.append(emit)
         return ops
 
+    def _skip_route(self, l, skip, c1, c2, dy):
+        """(pool name, dgrad dict) of the deferred skip half of decoder conv l's data
+        gradient when it can carry the pool backward of its skip source (2D row-window
+        data gradient, norm-free model; UNET_SKIP_ROUTE=0 keeps the dual-destination
+        dgrad + separate pool backward), else None.  Saves the skip-gradient tensor's
+        write and re-read: the pool backward's read of it becomes a second read of dy."""
+        if self.spec.norm != "none" or self.dims != 2 or os.environ.get("UNET_SKIP_ROUTE", "1") == "0":
+            return None
+        pool = next((x.name for x in self.spec.layers if x.kind == "pool" and self.inputs[x.name][0] == skip), None)
+        if pool is None:
+            return None
+        b = self.bufs
+        m, mb = self._relu_mask(skip)
+        dgrow = _r64((3 ** self.dims) * l.cout)
+        d = self._conv_common(l.level, 3, 1, 1)
+        d.update(name="dgrad_skip:" + l.name, C1=l.cout, src1=_ptr(dy),
+                 wgt=self.wptr(l.name, "dg") + 2 * c1 * dgrow, Cout=c2, relu=0,
+                 dst1=_ptr(b["d:" + skip]), D1=c2, mask1=m, mask_bits=mb, route_gy=_ptr(b["d:" + pool]),
+                 pool_code=_ptr(self.pool_codes[pool]))
+        try:
+            self.C.conv_fwd_grid(d)
+        except ValueError:
+            return None
+        return pool, d
+
     def _relu_mask(self, tname):
         """(mask pointer, is-bits) of the ReLU mask a data gradient into tensor `tname`
         applies: its bit tensor when the forward writes one, none for a pool output
@@ -699,6 +724,7 @@ class NativeUNet:
         def src_normed(t):
             return t in self.norm_layers and self.fuse_norm_stats
 
+        self._deferred_skip = {}
         for li in range(len(layers) - 1, -1, -1):
             l = layers[li]
             if l.kind == "mask":
@@ -754,9 +780,15 @@ class NativeUNet:
                                 dst1 = b["dfull:" + src1]          # full-res grad of the folded upsample
                             else:
                                 dst1 = b["d:" + src1]              # tconv output: linear, no mask
-                            m2, mb = self._relu_mask(skip)
-                            d.update(dst1=_ptr(dst1), D1=c1, dst2=_ptr(b["dskip:" + skip]),
-                                     mask2=m2, mask_bits=2 * mb)
+                            dsk = self._skip_route(l, skip, c1, c2, dy)
+                            if dsk is not None:
+                                # the skip half runs later, fused with the pool backward
+                                d.update(Cout=c1, dst1=_ptr(dst1), D1=c1)
+                                self._deferred_skip[dsk[0]] = dsk[1]
+                            else:
+                                m2, mb = self._relu_mask(skip)
+                                d.update(dst1=_ptr(dst1), D1=c1, dst2=_ptr(b["dskip:" + skip]),
+                                         mask2=m2, mask_bits=2 * mb)
                         return d
                     dd_ = mk()                 # built now: it decides the fused norm backward
                     emit_conv(lambda dd_=dd_: dd_)
@@ -768,6 +800,10 @@ class NativeUNet:
                                                         _ptr(b["d:" + src1])],
                                      [self.B, dd, hh, ww, c1, int(self.dims == 3)], [], "bwd:up:" + src1)
                 done(l.name)
+            elif l.kind == "pool" and l.name in self._deferred_skip:
+                # the decoder conv's skip-half data gradient with this pool's backward
+                # in its epilogue: writes d:<convNb> in one pass
+                emit_conv(lambda dsk=self._deferred_skip[l.name]: dsk)
             elif l.kind == "pool" and src_normed(self.inputs[l.name][0]):
                 # gradient of a normalised convNb output: the pool backward also emits
                 # the norm's backward statistics (no separate nstat_bwd pass)
