@@ -750,3 +750,40 @@ def test_dgrad_skip_half_with_fused_pool_backward(cuda_dev, N, H, C1, C2, Co):
     assert torch.equal(d_up0, d_up1)
     assert torch.equal(dy0, dy1)
     assert dy1.float().abs().sum() > 0
+
+
+@pytest.mark.parametrize("kind", ["first", "win", "tconv"])
+def test_wgrad_split_ranges_compose(cuda_dev, kind):
+    """A weight gradient issued in parts (split_lo / split_n, e.g. the first layer's
+    wgrad halves overlapping the last dgrad) writes exactly the slab rows of one
+    launch over all splits."""
+    torch.manual_seed(45)
+    N, H = 4, 32
+    if kind == "first":
+        a = torch.randn(N, H, H, 4, device=cuda_dev).bfloat16()
+        bt = torch.randn(N, H, H, 32, device=cuda_dev).bfloat16()
+        d = dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=4, a1=ptr(a), b=ptr(bt), Nc=32, bias_mode=1)
+        BM = C().wgrad_pick(4, 0, 32, 9, QW=H, win=0)[0]
+        rows = (9 * 4 + BM - 1) // BM * BM * 32
+    elif kind == "win":
+        a = torch.randn(N, H, H, 64, device=cuda_dev).bfloat16()
+        bt = torch.randn(N, H, H, 64, device=cuda_dev).bfloat16()
+        d = dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=64, a1=ptr(a), b=ptr(bt), Nc=64, bias_mode=1)
+        rows = 9 * 64 * 64
+    else:
+        a = torch.randn(N, 2 * H, 2 * H, 32, device=cuda_dev).bfloat16()     # dOut (fine)
+        bt = torch.randn(N, H, H, 64, device=cuda_dev).bfloat16()            # layer input (coarse)
+        d = dict(N=N, QH=H, QW=H, AH=2 * H, AW=2 * H, KH=2, KW=2, stride=2, pad=0, M1=32, a1=ptr(a), b=ptr(bt),
+                 Nc=64, bias_mode=2)
+        rows = 4 * 32 * 64
+    splits = 6
+    outs = []
+    for parts in ([(0, 0)], [(0, 3), (3, 3)], [(0, 2), (2, 1), (3, 0)]):
+        slab = torch.full((splits * rows,), float("nan"), device=cuda_dev)
+        bslab = torch.full((splits * 8 * 64,), float("nan"), device=cuda_dev)
+        for lo, n in parts:
+            C().wgrad(dict(d, splits=splits, split_lo=lo, split_n=n, slab=ptr(slab), bias_slab=ptr(bslab)), stream())
+        torch.cuda.synchronize()
+        outs.append(slab)
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])

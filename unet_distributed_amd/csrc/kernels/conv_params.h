@@ -98,6 +98,8 @@ struct WgradParams {
   const void* b;              // [Q][Nc]
   int Nc;
   int splits;                 // K splits (grid dim)
+  int split_lo, split_n;      // this launch runs splits [split_lo, split_lo + split_n) (split_n 0 = to the
+                              // end): a weight gradient issued in parts as its dY is produced
   int tap_groups;             // taps handled per WG = (KD*KH*KW)/tap_groups
   float* slab;                // [splits][taps][M][Nc] fp32
   // fused bias gradient: 0 = off, 1 = column sums of B (conv: dY -> n),

@@ -28,6 +28,9 @@
 
 namespace unet {
 
+// splits handled by one launch: [split_lo, split_lo + split_n) of p.splits (0 = all)
+static inline int launch_splits(const WgradParams& p) { return p.split_n > 0 ? p.split_n : p.splits - p.split_lo; }
+
 namespace {
 
 constexpr int NTHR = 256;
@@ -88,8 +91,9 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
   const int tiles_m = Mtot / BM, tiles_n = p.Nc / BN;
   const int ntile = tiles_m * tiles_n * p.tap_groups;
   // blockIdx.x = split * ntile + tile   (splits of one tile spread over XCDs)
-  const int split = blockIdx.x / ntile;
-  int t = blockIdx.x - split * ntile;
+  const int lsplit = blockIdx.x / ntile;
+  const int split = p.split_lo + lsplit;
+  int t = blockIdx.x - lsplit * ntile;
   const int tg = t % p.tap_groups;
   t /= p.tap_groups;
   const int tn = t % tiles_n, tmi = t / tiles_n;
@@ -460,7 +464,7 @@ hipError_t launch_wg(WgradParams p, hipStream_t s) {
   const int Mtot = SMALLC ? (((KT * p.M1 + BM - 1) / BM) * BM) : (p.M1 + p.M2);
   p.tap_groups = SMALLC ? 1 : KT / NTAP;
   const int ntile = (Mtot / BM) * (p.Nc / BN) * p.tap_groups;
-  const int grid = ntile * p.splits;
+  const int grid = ntile * launch_splits(p);
   auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
   auto lg = [](int v) { int l = 0; while ((1 << l) < v) ++l; return l; };
   const bool p2 = pow2(p.QW) && pow2(p.QH) && pow2(p.QD);
@@ -532,8 +536,9 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   const int Mtot = p.M1 + p.M2;
   const int cob = p.Nc / (32 * QO);
   const int ntile = (Mtot / 32) * cob * KD;
-  const int split = blockIdx.x / ntile;
-  int tile = blockIdx.x - split * ntile;
+  const int lsplit = blockIdx.x / ntile;
+  const int split = p.split_lo + lsplit;
+  int tile = blockIdx.x - lsplit * ntile;
   const int kd = tile % KD;
   tile /= KD;
   const int ci_blk = tile / cob, co_blk = tile - ci_blk * cob;
@@ -881,7 +886,8 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
   const int nwin = (rows_total + R - 1) / R;
   const int Mtot = MT * 16;
   const int cot = p.Nc / 32;
-  const int split = blockIdx.x / cot, co_blk = blockIdx.x - split * cot;
+  const int lsplit = blockIdx.x / cot, co_blk = blockIdx.x - lsplit * cot;
+  const int split = p.split_lo + lsplit;
   const int co0 = co_blk * 32;
   constexpr int OOB = 0x7fffffff;
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.a1, (short)0, OOB, 0x00020000);
@@ -1016,7 +1022,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
 
 template <int CIN>
 hipError_t launch_wgrad_win_first(const WgradParams& p, hipStream_t s) {
-  const int grid = (p.Nc / 32) * p.splits;
+  const int grid = (p.Nc / 32) * launch_splits(p);
   switch (p.QW) {
     case 16: hipLaunchKernelGGL((wgrad_win_first_kernel<16, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
     case 32: hipLaunchKernelGGL((wgrad_win_first_kernel<32, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
@@ -1060,7 +1066,8 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
   const int Mtot = p.M1;                    // output channels of the transposed conv
   const int cit = p.Nc / (32 * QN);
   const int ntile = (Mtot / 32) * cit;
-  const int split = blockIdx.x / ntile, tile = blockIdx.x - split * ntile;
+  const int lsplit = blockIdx.x / ntile, tile = blockIdx.x - lsplit * ntile;
+  const int split = p.split_lo + lsplit;
   const int co_blk = tile / cit, ci_blk = tile - co_blk * cit;
   const int co0 = co_blk * 32, ci0 = ci_blk * 32 * QN;
   constexpr int OOB = 0x7fffffff;
@@ -1191,7 +1198,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
 
 template <int W, int QO, int GEO>
 hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
-  const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.KD * p.splits;
+  const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.KD * launch_splits(p);
   if (p.M2 > 0)
     hipLaunchKernelGGL((wgrad_win_kernel<W, QO, true, GEO>), dim3(grid), dim3(NTHR), 0, s, p);
   else
@@ -1276,6 +1283,8 @@ const char* wgrad_check(const WgradParams& p) {
   }
   if (p.upA != 1 && p.upA != 2) return "wgrad: upA must be 1 or 2";
   if (p.splits < 1) return "wgrad: splits must be >= 1";
+  if (p.split_lo < 0 || p.split_n < 0 || p.split_lo + launch_splits(p) > p.splits)
+    return "wgrad: split range [split_lo, split_lo + split_n) outside [0, splits)";
   return nullptr;
 }
 
@@ -1284,7 +1293,7 @@ hipError_t wgrad_launch(const WgradParams& p, hipStream_t s) {
   if (wgrad_win_first_eligible(p)) return p.M1 == 4 ? launch_wgrad_win_first<4>(p, s) : launch_wgrad_win_first<8>(p, s);
   if (wgrad_tconv_win_eligible(p)) {
     const int qn = p.Nc % 128 == 0 ? 4 : (p.Nc % 64 == 0 ? 2 : 1);
-    const int grid = (p.M1 / 32) * (p.Nc / (32 * qn)) * p.splits;
+    const int grid = (p.M1 / 32) * (p.Nc / (32 * qn)) * launch_splits(p);
 #define TW_CASE(WW, QQ) hipLaunchKernelGGL((wgrad_tconv_win_kernel<WW, QQ>), dim3(grid), dim3(NTHR), 0, s, p)
     if (p.QW == 32) {
       if (qn == 4) TW_CASE(32, 4); else if (qn == 2) TW_CASE(32, 2); else TW_CASE(32, 1);

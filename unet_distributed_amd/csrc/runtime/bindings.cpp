@@ -137,6 +137,8 @@ WgradParams wgrad_params(const py::dict& d) {
   p.b = getp(d, "b");
   p.Nc = get<int>(d, "Nc", 0);
   p.splits = get<int>(d, "splits", 1);
+  p.split_lo = get<int>(d, "split_lo", 0);
+  p.split_n = get<int>(d, "split_n", 0);
   p.tap_groups = 1;
   p.slab = (float*)getp(d, "slab");
   p.bias_mode = get<int>(d, "bias_mode", 0);

@@ -461,6 +461,32 @@ class NativeUNet:
         ops.append(emit)
         return ops
 
+    def _tail_halves(self, d, l, src1, skip, dy):
+        """Two half-batch copies of dgrad dict `d` when its destination is the first
+        layer's output (the last dgrad of the backward) and the halves line up with
+        the first layer's weight-gradient splits (norm-free 2D model, even batch;
+        UNET_TAIL_SPLIT=0 off), else None."""
+        if (skip is not None or self.inputs.get(src1, ("",))[0] != "x" or self.spec.norm != "none"
+                or self.dims != 2 or self.B % 2 or os.environ.get("UNET_TAIL_SPLIT", "1") == "0"
+                or self.img not in (16, 32, 64, 128) or self.cpad not in (4, 8) or self.wgrad_win < 0):
+            return None      # (the first-layer row-window wgrad, whose split halves are image halves)
+        b = self.bufs
+
+        def half(t):
+            return t.numel() * t.element_size() // 2
+
+        mk = self.relu_bits.get(src1, b[src1]) if d.get("mask1") else None
+        h1 = dict(d, N=self.B // 2)
+        h2 = dict(h1, src1=d["src1"] + half(dy), dst1=d["dst1"] + half(b["d:" + src1]))
+        if mk is not None:
+            h2["mask1"] = d["mask1"] + half(mk)
+        try:
+            for h in (h1, h2):
+                self.C.conv_fwd_grid(h)
+        except ValueError:
+            return None
+        return h1, h2
+
     def _skip_route(self, l, skip, c1, c2, dy):
         """(pool name, dgrad dict) of the deferred skip half of decoder conv l's data
         gradient when it can carry the pool backward of its skip source (2D row-window
@@ -725,6 +751,7 @@ class NativeUNet:
             return t in self.norm_layers and self.fuse_norm_stats
 
         self._deferred_skip = {}
+        tail_parts = {}
         for li in range(len(layers) - 1, -1, -1):
             l = layers[li]
             if l.kind == "mask":
@@ -757,12 +784,22 @@ class NativeUNet:
                           AW=self.sdims(l.level)[2], KD=3 if self.dims == 3 else 1, KH=3, KW=3, stride=1,
                           pad=1, upA=upA, a1=_ptr(a1), a2=_ptr(b[skip]) if skip else None,
                           b=_ptr(dy))
-                emit_wgrad(dict(lname=l.name, kd=kd, M1=c1, M2=c2, Nc=l.cout, KT=KT3, Q=Q,
-                                QD=self.sdims(l.level)[0], QH=self.sdims(l.level)[1],
-                                QW=self.sdims(l.level)[2], upA=upA,
-                                kernel=l.name + "/kernel", bias=l.name + "/bias", bias_mode=1,
-                                bias_width=l.cout, bias_src=(dy, Q),
-                                real_rows=(self.cpad, spec.in_channels) if first else None))
+                wspec = dict(lname=l.name, kd=kd, M1=c1, M2=c2, Nc=l.cout, KT=KT3, Q=Q,
+                             QD=self.sdims(l.level)[0], QH=self.sdims(l.level)[1],
+                             QW=self.sdims(l.level)[2], upA=upA,
+                             kernel=l.name + "/kernel", bias=l.name + "/bias", bias_mode=1,
+                             bias_width=l.cout, bias_src=(dy, Q),
+                             real_rows=(self.cpad, spec.in_channels) if first else None)
+                part_at = tail_parts.pop(l.name, None)
+                if part_at is not None:
+                    # first half of this weight gradient at the placeholder between the two
+                    # halves of the consumer's dgrad, second half here
+                    wspec["parts"] = 2
+                    wg_specs.append(wspec)
+                    ops[part_at] = ("wgrad", len(wg_specs) - 1, 0)
+                    ops.append(("wgrad", len(wg_specs) - 1, 1))
+                else:
+                    emit_wgrad(wspec)
                 # --- data gradient
                 if not first:
                     def mk(l=l, src1=src1, up1=up1, skip=skip, c1=c1, c2=c2, dy=dy):
@@ -791,7 +828,17 @@ class NativeUNet:
                                          mask2=m2, mask_bits=2 * mb)
                         return d
                     dd_ = mk()                 # built now: it decides the fused norm backward
-                    emit_conv(lambda dd_=dd_: dd_)
+                    halves = self._tail_halves(dd_, l, src1, skip, dy)
+                    if halves is None:
+                        emit_conv(lambda dd_=dd_: dd_)
+                    else:
+                        # the last dgrad of the chain in two batch halves: the first layer's
+                        # weight gradient (the backward's tail, alone on the GPU otherwise)
+                        # starts on the side stream as soon as the first half is written
+                        emit_conv(lambda h=halves[0]: h)
+                        tail_parts[src1] = len(ops)
+                        ops.append(("placeholder",))
+                        emit_conv(lambda h=halves[1]: h)
                     if up1 == 2:
                         lvl = self.tinfo[src1][0]
                         dd, hh, ww = self.sdims(lvl)
@@ -859,6 +906,10 @@ class NativeUNet:
         # region (HBM is plentiful) so the split-K reductions of several layers can be
         # batched into one launch per phase (multi_reduce), flushed every few layers
         sized = [self._wgrad_splits(w) for w in wg_specs]
+        for k, w in enumerate(wg_specs):
+            if w.get("parts"):                     # each half keeps the full grid
+                sp = sized[k]
+                sized[k] = (2 * sp[0],) + tuple(sp[1:])
         stot = btot = sttot = 0
         regions = []
         for w, (splits, Mtot, taps, tg, smallc) in zip(wg_specs, sized):
@@ -926,8 +977,9 @@ class NativeUNet:
                         flush()
                 else:
                     self._layer_done_at[op[1]] = plan.size()
-            else:
+            elif op[0] == "wgrad":
                 w = wg_specs[op[1]]
+                part = op[2] if len(op) > 2 else None
                 splits, Mtot, taps, tg, smallc = sized[op[1]]
                 so, bo, sto_k, sto_b = regions[op[1]]
                 slab, bslab = slab0 + 4 * so, bslab0 + 4 * bo
@@ -940,7 +992,11 @@ class NativeUNet:
                 d.update(name="wgrad:" + w["lname"], M1=w["M1"], M2=w["M2"], Nc=w["Nc"], splits=splits,
                          win=self.wgrad_win, slab=slab, bias_mode=w["bias_mode"] if fused_bias else 0,
                          bias_slab=bslab)
+                if part is not None:
+                    d.update(split_lo=part * splits // 2, split_n=splits // 2)
                 plan.add_wgrad(d)
+                if part == 0:
+                    continue                       # the reductions follow the last part
                 KT = w["KT"]
                 if smallc:
                     cpad, creal = w["real_rows"]
