@@ -126,7 +126,8 @@ def test_conv_dgrad_dual_dest_mask(cuda_dev):
     (2, 64, 32, 0, 64, 6), (3, 16, 32, 0, 32, 6), (5, 16, 64, 0, 64, 6), (3, 32, 128, 0, 32, 6),
     (1, 128, 32, 0, 64, 0), (2, 64, 64, 64, 64, 0), (2, 32, 64, 0, 128, 8),
     (2, 128, 32, 0, 64, 12), (3, 128, 32, 32, 64, 12), (3, 64, 64, 64, 64, 12), (5, 16, 64, 0, 128, 12),
-    (3, 32, 128, 0, 64, 12), (2, 16, 256, 256, 256, 12)])
+    (3, 32, 128, 0, 64, 12), (2, 16, 256, 256, 256, 12),
+    (2, 128, 32, 0, 32, 13), (3, 128, 32, 32, 32, 13), (3, 64, 64, 64, 64, 13), (3, 32, 128, 0, 32, 13)])
 def test_conv_row_window(cuda_dev, N, H, C1, C2, Cout, tile):
     """Row-window kernel (tile 6, auto for 16 <= W <= 128): image boundaries inside a window,
     row tails (N*H not a multiple of the window), concat sources, bias + ReLU + dropout."""
@@ -146,7 +147,8 @@ def test_conv_row_window(cuda_dev, N, H, C1, C2, Cout, tile):
 
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout,tile", [(2, 8, 256, 32, 0, 32, 6), (1, 4, 384, 32, 32, 32, 6),
                                                     (2, 8, 512, 64, 0, 64, 6), (1, 4, 256, 64, 64, 64, 6),
-                                                    (2, 8, 512, 64, 0, 64, 12), (1, 4, 256, 64, 64, 128, 12)])
+                                                    (2, 8, 512, 64, 0, 64, 12), (1, 4, 256, 64, 64, 128, 12),
+                                                    (2, 8, 256, 32, 0, 32, 13), (1, 4, 384, 32, 32, 32, 13)])
 def test_conv_row_window_segmented_rows(cuda_dev, N, H, W, C1, C2, Cout, tile):
     """Rows wider than 128 run as 128-wide segments whose halo columns are the
     neighbouring segments' pixels (512x512 config levels)."""
@@ -217,7 +219,7 @@ def test_conv_row_window_dgrad_dual_dest_mask_dropout(cuda_dev):
     dy = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
     d1 = torch.empty(N, H, H, C1, device=cuda_dev, dtype=torch.bfloat16)
     d2 = torch.empty(N, H, H, C2, device=cuda_dev, dtype=torch.bfloat16)
-    for tile in (6, 8, 12):
+    for tile in (6, 8, 12, 13):
         C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Co, src1=ptr(dy),
                           wgt=ptr(pack_dgrad(w)), Cout=C1 + C2, D1=C1, dst1=ptr(d1), dst2=ptr(d2),
                           mask1=ptr(m1), mask2=ptr(skip), mask_scale2=1.25, tile=tile), stream())
@@ -615,7 +617,8 @@ def test_upsample2_fwd_materialised(cuda_dev, dims3):
 
 @pytest.mark.parametrize("N,H,Cin,Cout,tile", [(2, 128, 32, 32, 0), (2, 64, 32, 64, 0), (4, 32, 64, 128, 0),
                                                (4, 16, 128, 256, 0), (1, 256, 32, 32, 0), (2, 128, 32, 64, 12),
-                                               (2, 64, 32, 64, 12), (4, 32, 64, 128, 12), (4, 16, 128, 256, 12)])
+                                               (2, 64, 32, 64, 12), (4, 32, 64, 128, 12), (4, 16, 128, 256, 12),
+                                               (2, 128, 32, 32, 13), (2, 64, 32, 64, 13), (1, 256, 32, 32, 13)])
 def test_conv_fwd_fused_maxpool_matches_pool_kernel(cuda_dev, N, H, Cin, Cout, tile):
     """convNb forward with the fused 2x2 max-pool epilogue: the conv output, the pooled
     tensor and the argmax codes equal the plain conv + the separate pool kernel."""
@@ -667,7 +670,7 @@ def test_conv_fwd_relu_bits(cuda_dev, N, H, Cin, Cout, tile, drop):
     assert torch.equal(bits, _pack_bits(y1))
 
 
-@pytest.mark.parametrize("tile", [6, 8, 12])
+@pytest.mark.parametrize("tile", [6, 8, 12, 13])
 def test_conv_dgrad_bit_masks_match_activation_masks(cuda_dev, tile):
     """Data gradient with two destinations whose ReLU masks come from bit tensors
     (mask_bits) equals the same launch masked by the 16-bit activations."""

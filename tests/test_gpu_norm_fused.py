@@ -35,6 +35,8 @@ def _moments(z):            # z: [N, H, W, C] -> per-sample [N, 2, C]
     (2, 128, 32, 64, 0, 12),     # 64-channel row window (256-pixel windows)
     (4, 16, 64, 128, 0, 12),
     (2, 32, 32, 64, 32, 12),
+    (2, 128, 32, 32, 0, 13),     # 256-pixel windows, 32-channel tile
+    (2, 256, 32, 32, 0, 13),
 ])
 def test_conv_fwd_stats_epilogue(cuda_dev, N, H, Cin, Cout, C2, tile):
     torch.manual_seed(0)
@@ -76,6 +78,7 @@ def _keep(q_idx, C, seed, salt, rate):
     (4, 16, 128, 64, True, 0.0, 0),     # 16-wide window, GroupNorm
     (2, 32, 64, 64, True, 0.2, 12),     # 64-channel row window
     (2, 128, 32, 64, False, 0.0, 12),
+    (2, 64, 64, 32, False, 0.0, 13),
 ])
 def test_conv_dgrad_norm_epilogue(cuda_dev, N, H, Cg, Cy, gn, drop, tile):
     """dgrad of a conv whose input y = dropout(relu(a z + c)): g = dgrad * mask, stats."""

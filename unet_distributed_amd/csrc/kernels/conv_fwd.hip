@@ -330,11 +330,6 @@ hipError_t launch_cfg(const ConvFwdParams& p, hipStream_t s) {
 // segment / depth state (extra SGPR state spilled to VGPR lanes inside the chunk loop).
 enum { GEO_2D = 0, GEO_SEG = 1, GEO_3D = 2 };
 
-// Window pixels of a BN-wide tile: 512 (256 for 16-wide rows); the 64-channel tile
-// halves the window so its accumulators (4 x 4 fragments per wave) and LDS
-// (halo + 36 KB of weights per chunk) still fit two workgroups per CU.
-__host__ __device__ constexpr int win_bm(int W, int BN) { return (W == 16 || BN == 64) ? 256 : 512; }
-
 // Output-channel tile of the row-window conv: 64 where Cout allows it and the row
 // width is enabled in UNET_WIN_BN64 (bit mask over W = 16 / 32 / 64 / 128 -> bits
 // 0..3; read once per process), else 32.  Default 7 (W = 16..64), from a same-box
@@ -347,25 +342,42 @@ static int win_bn(const ConvFwdParams& p) {
     return e ? atoi(e) : 7;
   }();
   if (p.tile == 12) return 64;                       // forced (tests / A-B)
-  if (p.tile == 6) return 32;
+  if (p.tile == 6 || p.tile == 13) return 32;
   const int W = p.OW > 128 ? 128 : p.OW;
   const int bit = W == 16 ? 1 : W == 32 ? 2 : W == 64 ? 4 : 8;
   return (p.Cout % 64 == 0 && (mask & bit) && !p.head_w) ? 64 : 32;
 }
+// Window pixels: 256 for 16-wide rows and for the 64-channel tile (its accumulators,
+// 4 x 4 fragments per wave, and LDS then still fit two workgroups per CU); for the
+// 32-channel tile 512, or 256 where the row width is enabled in UNET_WIN_BM256 (bit
+// mask as UNET_WIN_BN64): the smaller window's LDS (tight halo pitch + 18 KB of
+// weights) fits three workgroups per CU.
+static int win_bm(const ConvFwdParams& p) {
+  static const int mask = [] {
+    const char* e = getenv("UNET_WIN_BM256");
+    return e ? atoi(e) : 0;
+  }();
+  const int W = p.OW > 128 ? 128 : p.OW;
+  if (W == 16 || win_bn(p) == 64 || p.tile == 13) return 256;
+  if (p.tile == 6) return 512;
+  const int bit = W == 32 ? 2 : W == 64 ? 4 : 8;
+  return (mask & bit) ? 256 : 512;
+}
 static int win_rows(const ConvFwdParams& p) {
   const int W = p.OW > 128 ? 128 : p.OW;
-  return win_bm(W, win_bn(p)) / W;
+  return win_bm(p) / W;
 }
 
-template <int W, int BN, bool CONCAT, int EPI, int GEO>
+template <int W, int BN, int BM, bool CONCAT, int EPI, int GEO>
 __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   static_assert(BN == 32 || BN == 64, "row-window tile is 32 or 64 output channels wide");
-  constexpr int BM = win_bm(W, BN);             // window pixels
   constexpr int R = BM / W, HR = R + 2;
-  constexpr int HWP = ((W + 2 + 15) / 16) * 16; // halo row pitch in 64-byte pixel slots
-  constexpr int IPR = HWP / 16;                 // LDS-DMA wave-instructions per halo row
+  // halo row pitch in 64-byte pixel slots: W + 2 columns rounded up to a multiple of 4
+  // (every row starts on a 256-byte bank row); the DMA fills the image as one linear
+  // run of slots, so rows need not align to the 16-slot DMA instructions
+  constexpr int HWP = W + 4;
   constexpr int ROWB = HWP * 64;
-  constexpr int XI = HR * IPR, WI = 9 * BN / 16;
+  constexpr int XI = (HR * HWP + 15) / 16, WI = 9 * BN / 16;
   constexpr int XB = XI * 1024, WB = WI * 1024;
   constexpr int EPIB = (EPI == EPI_STATS || EPI == EPI_DGRAD_NORM) ? epi_lds_bytes<BM, BN>() : BM * (BN + 4) * 2;
   constexpr int LDS_BYTES = (XB + WB > EPIB) ? XB + WB : EPIB;
@@ -479,20 +491,21 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
         // instruction (hr, j) covers slots 16j .. 16j + 15 of row hr.  Rows outside the
         // tensor / image and columns outside [0, Wf) load zeros (out-of-range offsets).
         const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
-        const int lofs = ((lslot - 1) * C + cb + lchunk * 8) * 2;
 #pragma unroll
         for (int q = 0; q < (XI + 3) / 4; ++q) {
           const int k = wave + 4 * q;
           if (k < XI) {
-            const int hr = k / IPR, j = k - hr * IPR;      // wave-uniform
+            const int sl = 16 * k + lslot;                  // this lane's halo slot
+            const int hr = sl / HWP, hc = sl - hr * HWP;    // its row / column
             const int gr = g0 - 1 + hr + gsh;
-            const int col = col0 + 16 * j + lslot - 1;
-            const bool row_in = (hr > 0 || top_in) && (hr < R + 1 || bot_in);   // same image
+            const int col = col0 + hc - 1;
+            const bool row_in = hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in);   // same image
             // (slots past W + 1 are never read: skip them, they would be real pixels of
             // the next segment on segmented rows)
             const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)Wf &&
-                            (GEO != GEO_SEG || 16 * j + lslot <= W + 1);
-            const int off = ok ? (gr * Wf + col0 + 16 * j) * C * 2 + lofs : OOB;
+                            (GEO != GEO_SEG || hc <= W + 1);
+            const int lch = (lane & 3) ^ ((hc >> 1) & 3);
+            const int off = ok ? ((gr * Wf + col) * C + cb + lch * 8) * 2 : OOB;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
                                                      16, off, 0, 0, 0);
           }
@@ -537,17 +550,18 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
       if (kc) __syncthreads();
       {
         const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
-        const int lofs = ((lslot - 1) * C + cb + lchunk * 8) * 2;
 #pragma unroll
         for (int q = 0; q < (XI + 3) / 4; ++q) {
           const int k = wave + 4 * q;
           if (k < XI) {
-            const int hr = k / IPR, j = k - hr * IPR;
+            const int sl = 16 * k + lslot;
+            const int hr = sl / HWP, hc = sl - hr * HWP;
             const int gr = g0 - 1 + hr;
-            const int col = 16 * j + lslot - 1;
-            const bool row_in = (hr > 0 || top_in) && (hr < R + 1 || bot_in);
+            const int col = hc - 1;
+            const bool row_in = hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in);
             const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
-            const int off = ok ? (gr * W + 16 * j) * C * 2 + lofs : OOB;
+            const int lch = (lane & 3) ^ ((hc >> 1) & 3);
+            const int off = ok ? ((gr * W + col) * C + cb + lch * 8) * 2 : OOB;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
                                                      16, off, 0, 0, 0);
           }
@@ -987,7 +1001,7 @@ int win_grid(const ConvFwdParams& p) {
   return ((rows + R - 1) / R) * (p.OW / W) * (p.Cout / win_bn(p));
 }
 
-template <int BN>
+template <int BN, int BM>
 hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
   const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
   const int grid = win_grid(p);
@@ -996,17 +1010,17 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
   const int geo = p.KD == 3 ? GEO_3D : (p.OW > W ? GEO_SEG : GEO_2D);
 #define WIN_EPI(WW, CC, GG)                                                                               \
   if (epi == EPI_FWD)                                                                                     \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_FWD, GG>), dim3(grid), dim3(NTHR), 0, s, p);     \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_FWD, GG>), dim3(grid), dim3(NTHR), 0, s, p);     \
   else if (epi == EPI_DGRAD)                                                                              \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_DGRAD, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_DGRAD, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
   else if (epi == EPI_STATS)                                                                              \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_STATS, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_STATS, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
   else if (epi == EPI_DGRAD_NORM && !CC)                                                                  \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, false, EPI_DGRAD_NORM, GG>), dim3(grid), dim3(NTHR), 0, s, p); \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD_NORM, GG>), dim3(grid), dim3(NTHR), 0, s, p); \
   else if (epi == EPI_DGRAD_NORM)                                                                         \
     return hipErrorInvalidValue;                                                                          \
   else                                                                                                    \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, CC, EPI_GENERIC, GG>), dim3(grid), dim3(NTHR), 0, s, p);
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_GENERIC, GG>), dim3(grid), dim3(NTHR), 0, s, p);
 #define WIN_GEO(WW, CC)                                                                                   \
   if (geo == GEO_3D) {                                                                                    \
     WIN_EPI(WW, CC, GEO_3D)                                                                               \
@@ -1015,10 +1029,14 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
   }
 #define WIN_CASE(WW)                                                                                      \
   case WW:                                                                                                \
-    if (cc) {                                                                                             \
-      WIN_GEO(WW, true)                                                                                   \
+    if constexpr (BM == 256 || WW != 16) {                                                                \
+      if (cc) {                                                                                           \
+        WIN_GEO(WW, true)                                                                                 \
+      } else {                                                                                            \
+        WIN_GEO(WW, false)                                                                                \
+      }                                                                                                   \
     } else {                                                                                              \
-      WIN_GEO(WW, false)                                                                                  \
+      return hipErrorInvalidValue;                                                                        \
     }                                                                                                     \
     break;
   if (geo == GEO_SEG) {                 // 3D volumes wider than 128 are not window-eligible
@@ -1118,7 +1136,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     return "conv_fwd: mask_bits marks a missing mask";
   if (p.route_gy && (!p.pool_code || conv_epi_mode(p) != EPI_DGRAD || !win_eligible(p) || p.KD != 1 || p.OD != 1 ||
                      p.OH % 2 || p.OW % 2 || p.D1 != p.Cout || p.pool_dst || p.mask_scale1 != 1.f ||
-                     (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12)))
+                     (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12 && conv_fwd_pick(p) != 13)))
     return "conv_fwd: fused pool backward needs a 2D row-window data gradient (even dims, one destination, codes)";
   if (p.pool_dst) {
     const int W = p.OW > 128 ? 128 : p.OW;
@@ -1127,7 +1145,8 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
         p.OH % 2 || p.OW % 2 || p.Cout % 8 || p.head_w)
       return "conv_fwd: fused max-pool needs a 2D row-window ReLU forward (even rows, codes buffer)";
   }
-  if (p.tile < 0 || p.tile > 12) return "conv_fwd: bad tile id";
+  if (p.tile < 0 || p.tile > 13) return "conv_fwd: bad tile id";
+  if (p.tile == 13 && !win_eligible(p)) return "conv_fwd: 256-pixel row-window tile not applicable";
   if (p.tile == 12 && (!win_eligible(p) || p.Cout % 64 || p.head_w))
     return "conv_fwd: 64-wide row-window tile not applicable";
   if (p.tile == 10 && !tconv_fwd_eligible(p)) return "conv_fwd: transposed-conv window tile not applicable";
@@ -1143,7 +1162,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.head_w) {
     if (!p.head_b || !p.head_logit) return "conv_fwd: fused head needs head_b / head_logit";
     if (p.Cout != 32 || p.drop_rate > 0.f || !p.relu || p.D1 != p.Cout || p.mask1 || p.out_scale != 1.f ||
-        conv_epi_mode(p) != EPI_FWD || conv_fwd_pick(p) != 6)
+        conv_epi_mode(p) != EPI_FWD || (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 13))
       return "conv_fwd: fused head needs a 32-channel ReLU row-window forward";
   }
   if ((long long)p.N * p.ID * p.IH * p.IW >= (1LL << 31) || (long long)p.N * p.OD * p.OH * p.OW >= (1LL << 31))
@@ -1185,7 +1204,7 @@ int conv_fwd_pick(const ConvFwdParams& p) {
 
 int conv_fwd_grid(const ConvFwdParams& p) {
   const int t = conv_fwd_pick(p);
-  return (t == 6 || t == 12) ? win_grid(p) : 0;
+  return (t == 6 || t == 12 || t == 13) ? win_grid(p) : 0;
 }
 
 void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
@@ -1195,7 +1214,8 @@ void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
   const bool smallc = (p.C1 == 4 || p.C1 == 8) && p.C2 == 0;
   switch (t) {
     case 6:
-    case 12: {       // row window: R rows x (segment) width, tiles in (row group, segment) order
+    case 12:
+    case 13: {       // row window: R rows x (segment) width, tiles in (row group, segment) order
       const int W = p.OW > 128 ? 128 : p.OW;
       const int R = win_rows(p);
       if (p.nz && p.C2) return;
@@ -1236,7 +1256,10 @@ hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
     case 3: return launch_cfg<256, 32, 4, 1>(p, s);
     case 5: return launch_cfg<256, 64, 4, 1>(p, s);
     case 6:
-    case 12: return win_bn(p) == 64 ? launch_win<64>(p, s) : launch_win<32>(p, s);
+    case 12:
+    case 13:
+      if (win_bn(p) == 64) return launch_win<64, 256>(p, s);
+      return win_bm(p) == 256 ? launch_win<32, 256>(p, s) : launch_win<32, 512>(p, s);
     case 9: return p.C1 == 4 ? launch_win_first<4>(p, s) : launch_win_first<8>(p, s);
     case 10: return launch_tconv_fwd(p, s);
     case 11: return launch_tconv_dgrad(p, s);
