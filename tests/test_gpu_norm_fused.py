@@ -198,3 +198,99 @@ def test_pool_bwd_norm_rows(cuda_dev, N, H, Cc, dims3):
     mom = torch.stack([gf.sum(1), (gf * zf).sum(1)], 1)
     per = rows.view(N, nbp, 2, Cc).sum(1)
     assert torch.allclose(per, mom, rtol=1e-4, atol=1e-2)
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,gn,tile,stats", [
+    (2, 128, 32, 32, False, 6, True),       # 512-pixel windows, BatchNorm coefficients, stats epilogue
+    (2, 64, 64, 64, True, 0, True),         # 64-channel tile, GroupNorm (per-sample) coefficients
+    (4, 16, 128, 128, False, 0, True),      # 16-wide rows, 4 K chunks
+    (2, 128, 32, 32, True, 13, False),      # 256-pixel windows, eval-style generic epilogue
+])
+def test_conv_fwd_operand_norm_on_load(cuda_dev, N, H, Cin, Cout, gn, tile, stats):
+    """xform 1: the conv reads the PRE-norm z of its input and normalises it in LDS
+    (relu(a z + b)); equals the conv of the materialised activation, and xout holds
+    that activation (written once per pixel)."""
+    torch.manual_seed(50)
+    z = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
+    rows = N if gn else 1
+    a = 0.5 + torch.rand(rows, Cin, device=cuda_dev)
+    b = 0.3 * torch.randn(rows, Cin, device=cuda_dev)
+    ai = a.view(rows, 1, 1, Cin)
+    bi = b.view(rows, 1, 1, Cin)
+    y_ref = _bf(torch.clamp(ai.double() * z.double() + bi.double(), min=0).float())
+    w = (torch.randn(3, 3, Cin, Cout, device=cuda_dev) * 0.1).bfloat16()
+    bias = torch.randn(Cout, device=cuda_dev) * 0.1
+    wp = pack_fwd(w)
+    out = torch.empty(N, H, H, Cout, device=cuda_dev, dtype=torch.bfloat16)
+    yo = torch.full_like(z, float("nan"))
+    d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(z), wgt=ptr(wp), bias=ptr(bias),
+             Cout=Cout, relu=0, dst1=ptr(out), tile=tile, xform=1, xa=ptr(a), xb=ptr(b), xcs=Cin if gn else 0,
+             xout=ptr(yo))
+    st = None
+    if stats:
+        nr, _ = C().conv_stat_tiles(dict(d, stats=1))
+        st = torch.zeros(nr, 2, Cout, device=cuda_dev)
+        d["stats"] = ptr(st)
+    C().conv_fwd(d, stream())
+    torch.cuda.synchronize()
+    ref = nhwc(F.conv2d(nchw(y_ref.float()), w.float().permute(3, 2, 0, 1), bias, padding=1))
+    assert rel_err(out, ref) < 1e-2
+    assert torch.isfinite(yo.float()).all()
+    assert (yo.float() - y_ref.float()).abs().max() <= 1e-2 * y_ref.float().abs().max()
+    if stats:
+        tot = st.sum(0)
+        zf = out.float().reshape(-1, Cout)
+        assert torch.allclose(tot[0], zf.sum(0), rtol=1e-3, atol=1e-2 * H)
+
+
+@pytest.mark.parametrize("N,H,Cg,Cy,gn,tile,norm_epi", [
+    (2, 128, 32, 32, False, 6, False),      # dgrad into a ReLU'd input (bit mask), BatchNorm dz
+    (2, 64, 64, 32, True, 0, True),         # dgrad into a normalised input (EPI_DGRAD_NORM), GroupNorm dz
+    (4, 16, 128, 128, False, 0, False),
+    (2, 128, 32, 64, True, 13, True),
+])
+def test_conv_dgrad_operand_dz_on_load(cuda_dev, N, H, Cg, Cy, gn, tile, norm_epi):
+    """xform 2: the data gradient reads g (the gradient of the norm's output) and the
+    pre-norm z, forms dz = a g + b z + c in LDS and convolves it; equals the dgrad of
+    the materialised dz, and xout holds dz."""
+    torch.manual_seed(51)
+    g = torch.randn(N, H, H, Cg, device=cuda_dev).bfloat16()
+    z = torch.randn(N, H, H, Cg, device=cuda_dev).bfloat16()
+    rows = N if gn else 1
+    ca = 0.5 + torch.rand(rows, Cg, device=cuda_dev)
+    cb = 0.2 * torch.randn(rows, Cg, device=cuda_dev)
+    cc = 0.1 * torch.randn(rows, Cg, device=cuda_dev)
+    v = lambda t: t.view(rows, 1, 1, Cg).double()
+    dz_ref = _bf((v(ca) * g.double() + (v(cb) * z.double() + v(cc))).float())
+    w = (torch.randn(3, 3, Cy, Cg, device=cuda_dev) * 0.1).bfloat16()
+    wp = pack_dgrad(w)
+    dx = torch.empty(N, H, H, Cy, device=cuda_dev, dtype=torch.bfloat16)
+    dzo = torch.full_like(g, float("nan"))
+    d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cg, src1=ptr(g), wgt=ptr(wp), Cout=Cy, relu=0,
+             dst1=ptr(dx), tile=tile, xform=2, xa=ptr(ca), xb=ptr(cb), xc=ptr(cc), xz=ptr(z),
+             xcs=Cg if gn else 0, xout=ptr(dzo))
+    zy = torch.randn(N, H, H, Cy, device=cuda_dev).bfloat16()         # pre-norm input of the conv
+    if norm_epi:
+        na = 0.5 + torch.rand(Cy, device=cuda_dev)
+        nc = 0.3 * torch.randn(Cy, device=cuda_dev)
+        d.update(nz=ptr(zy), na=ptr(na), nc=ptr(nc), ncs=0, npix=H * H)
+        nr, _ = C().conv_stat_tiles(dict(d, stats=1))
+        st = torch.zeros(nr, 2, Cy, device=cuda_dev)
+        d["stats"] = ptr(st)
+        mask = (na.view(1, 1, 1, Cy) * zy.float() + nc.view(1, 1, 1, Cy)) > 0
+    else:
+        d.update(mask1=ptr(zy))
+        mask = zy.float() > 0
+    C().conv_fwd(d, stream())
+    torch.cuda.synchronize()
+    xr = torch.zeros(N, Cy, H, H, device=cuda_dev, requires_grad=True)
+    (gref,) = torch.autograd.grad(F.conv2d(xr, w.float().permute(3, 2, 0, 1), padding=1), xr,
+                                  nchw(dz_ref.float()))
+    gref = nhwc(gref) * mask
+    assert rel_err(dx, gref) < 1e-2
+    assert torch.isfinite(dzo.float()).all()
+    assert (dzo.float() - dz_ref.float()).abs().max() <= 1e-2 * dz_ref.float().abs().max()

@@ -368,9 +368,13 @@ static int win_rows(const ConvFwdParams& p) {
   return win_bm(p) / W;
 }
 
-template <int W, int BN, int BM, bool CONCAT, int EPI, int GEO>
+// XF (2D, single source): operand transform of the src1 halo image in LDS before the
+// MFMAs, conv_params.h xform -- 1: y = relu(xa z + xb), 2: dz = xa g + xb z + xc (z
+// from xz); the window's own rows of the transformed operand go to xout.
+template <int W, int BN, int BM, bool CONCAT, int EPI, int GEO, int XF = 0>
 __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   static_assert(BN == 32 || BN == 64, "row-window tile is 32 or 64 output channels wide");
+  static_assert(XF == 0 || (GEO == GEO_2D && !CONCAT), "operand transform: 2D single-source windows");
   constexpr int R = BM / W, HR = R + 2;
   // halo row pitch in 64-byte pixel slots: W + 2 columns rounded up to a multiple of 4
   // (every row starts on a 256-byte bank row); the DMA fills the image as one linear
@@ -543,11 +547,37 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
     // 2D full rows: the same staging with compile-time row pitch and no segment / depth
     // offsets, spelled out (through run_chunk the scheduler keeps ~100 more scalar
     // instructions per chunk and spills SGPRs to VGPR lanes: 2-4 % slower, A/B measured)
+    // operand transform: thread t owns logical 16-byte chunk xlc = t & 3 (channels
+    // cb + 8 xlc ..) of slots (t >> 2) + 64 j, so its 8 channels' coefficients are fixed
+    // per chunk; the slot's physical chunk is xlc ^ swizzle(column), as the DMA wrote it
+    constexpr int XNJ = XF ? (XI * 64 + NTHR - 1) / NTHR : 1;
+    const int xlc = tid & 3, xs0 = tid >> 2;
+    auto xslot = [&](const int j, int& hr, int& hc, int& gr, bool& ok) {
+      const int sl = xs0 + (NTHR / 4) * j;
+      hr = sl / HWP;
+      hc = sl - hr * HWP;
+      gr = g0 - 1 + hr;
+      ok = hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)gr < (unsigned)rows_total &&
+           (unsigned)(hc - 1) < (unsigned)W;
+      return sl;
+    };
+    const size_t xsample = XF ? (size_t)(g0 / H) * p.xcs : 0;   // the window's sample (GroupNorm rows)
     for (int kc = 0; kc < nchunks; ++kc) {
       const bool from1 = !CONCAT || (kc << 5) < p.C1;
       const int C = from1 ? p.C1 : p.C2;
       const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
       if (kc) __syncthreads();
+      u32x4 xz[XNJ];
+      if constexpr (XF == 2) {
+        // the pre-norm z of this thread's transform chunks, loaded beside the DMA
+#pragma unroll
+        for (int j = 0; j < XNJ; ++j) {
+          int hr, hc, gr;
+          bool ok;
+          xslot(j, hr, hc, gr, ok);
+          if (ok) xz[j] = *(const u32x4*)((const h16*)p.xz + (size_t)(gr * W + hc - 1) * C + cb + xlc * 8);
+        }
+      }
       {
         const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
 #pragma unroll
@@ -579,6 +609,41 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
         }
       }
       __syncthreads();
+      if constexpr (XF != 0) {
+        float xa[8], xb[8], xc[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const size_t ci = xsample + cb + xlc * 8 + e;
+          xa[e] = p.xa[ci];
+          xb[e] = p.xb[ci];
+          xc[e] = XF == 2 ? p.xc[ci] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < XNJ; ++j) {
+          int hr, hc, gr;
+          bool ok;
+          const int sl = xslot(j, hr, hc, gr, ok);
+          if (!ok) continue;                              // padding stays the DMA's zeros
+          char* a = Xs + sl * 64 + 16 * (xlc ^ ((hc >> 1) & 3));
+          float v[8];
+          unpack8(*(const u32x4*)a, v);
+          if constexpr (XF == 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(xa[e], v[e], xb[e]), 0.f);
+          } else {
+            float zf[8];
+            unpack8(xz[j], zf);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaf(xa[e], v[e], fmaf(xb[e], zf[e], xc[e]));
+          }
+          const u32x4 o = pack8(v);
+          *(u32x4*)a = o;
+          // the window's own rows (once: output-channel tile 0) -> xout
+          if (p.xout && tn == 0 && hr >= 1 && hr <= R)
+            *(u32x4*)((h16*)p.xout + (size_t)(gr * W + hc - 1) * C + cb + xlc * 8) = o;
+        }
+        __syncthreads();
+      }
       chunk_mfmas();
     }
   }
@@ -1039,6 +1104,42 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
       return hipErrorInvalidValue;                                                                        \
     }                                                                                                     \
     break;
+#define XF_EPI(WW, XFV)                                                                                       \
+  if (XFV == 1 && epi == EPI_STATS)                                                                           \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_STATS, GEO_2D, XFV>), dim3(grid), dim3(NTHR), 0, s, p); \
+  else if (XFV == 1 && epi == EPI_GENERIC)                                                                    \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_GENERIC, GEO_2D, XFV>), dim3(grid), dim3(NTHR), 0, s, p); \
+  else if (XFV == 2 && epi == EPI_DGRAD)                                                                      \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_2D, XFV>), dim3(grid), dim3(NTHR), 0, s, p); \
+  else if (XFV == 2 && epi == EPI_DGRAD_NORM)                                                                 \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD_NORM, GEO_2D, XFV>), dim3(grid), dim3(NTHR), 0, s, p); \
+  else                                                                                                        \
+    return hipErrorInvalidValue;
+#define XF_CASE(WW)                                                                                           \
+  case WW:                                                                                                    \
+    if constexpr (BM == 256 || WW != 16) {                                                                    \
+      if (p.xform == 1) {                                                                                     \
+        XF_EPI(WW, 1)                                                                                         \
+      } else {                                                                                                \
+        XF_EPI(WW, 2)                                                                                         \
+      }                                                                                                       \
+    } else {                                                                                                  \
+      return hipErrorInvalidValue;                                                                            \
+    }                                                                                                         \
+    break;
+  if (p.xform) {                        // operand transform: 2D single source (conv_fwd_prepare)
+    switch (W) {
+      XF_CASE(16)
+      XF_CASE(32)
+      XF_CASE(64)
+      XF_CASE(128)
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+#undef XF_CASE
+#undef XF_EPI
   if (geo == GEO_SEG) {                 // 3D volumes wider than 128 are not window-eligible
     if (cc) {
       WIN_EPI(128, true, GEO_SEG)
@@ -1134,6 +1235,15 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     return "conv_fwd: relu_bits needs an unsplit ReLU forward";
   if ((p.mask_bits & ~3) || ((p.mask_bits & 1) && !p.mask1) || ((p.mask_bits & 2) && !p.mask2))
     return "conv_fwd: mask_bits marks a missing mask";
+  if (p.xform) {
+    const int ep = conv_epi_mode(p), t = conv_fwd_pick(p);
+    if (p.xform < 0 || p.xform > 2 || p.C2 || p.up1 != 1 || !p.xa || !p.xb || (p.xform == 2 && (!p.xc || !p.xz)) ||
+        p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) || (t != 6 && t != 12 && t != 13) ||
+        (p.xcs != 0 && p.xcs != p.C1) || p.head_w ||
+        (p.xform == 1 ? (ep != EPI_STATS && ep != EPI_GENERIC) : (ep != EPI_DGRAD && ep != EPI_DGRAD_NORM)))
+      return "conv_fwd: operand transform needs a 2D single-source row-window conv (norm-input forward / "
+             "norm-output data gradient)";
+  }
   if (p.route_gy && (!p.pool_code || conv_epi_mode(p) != EPI_DGRAD || !win_eligible(p) || p.KD != 1 || p.OD != 1 ||
                      p.OH % 2 || p.OW % 2 || p.D1 != p.Cout || p.pool_dst || p.mask_scale1 != 1.f ||
                      (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12 && conv_fwd_pick(p) != 13)))

@@ -71,6 +71,21 @@ struct ConvFwdParams {
   // its window and the maximum is positive (pool_code, maxpool2_fwd layout) -- the
   // gradient of the convNb output in one pass, no separate skip-gradient tensor.
   const void* route_gy;
+  // Operand transform on load (2D row-window conv, src1 only): the halo image is
+  // rewritten in LDS before the MFMAs, so a normalisation pass never runs on its own --
+  //   xform 1: src1 = pre-norm z, operand y = relu(xa z + xb)   (forward of a normalised
+  //            activation's consumer; eval / train alike)
+  //   xform 2: src1 = g (gradient of the norm's output), operand dz = xa g + xb z + xc
+  //            with z = xz (the norm backward's dz)
+  // coefficients [C] (xcs = 0, BatchNorm) or [N][C] (xcs = C, GroupNorm; a window lies
+  // in one sample).  xout (optional): the transformed operand's own-window rows are also
+  // stored there (the weight gradient reads them), by output-channel tile 0.
+  int xform, xcs;
+  const float* xa;
+  const float* xb;
+  const float* xc;
+  const void* xz;
+  void* xout;
   int tile;                  // 0 = auto, else forced tile config id (tuning / A-B tests)
   // Fused segmentation head (row-window forward, Cout == 32, EPI_FWD only): per pixel
   // z = sum_c out[c] head_w[c] + head_b -> head_logit (fp32) for head_finish

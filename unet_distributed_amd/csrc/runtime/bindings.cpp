@@ -106,6 +106,13 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.relu_bits = (uint8_t*)const_cast<void*>(getp(d, "relu_bits"));
   p.mask_bits = get<int>(d, "mask_bits", 0);
   p.route_gy = getp(d, "route_gy");
+  p.xform = get<int>(d, "xform", 0);
+  p.xcs = get<int>(d, "xcs", 0);
+  p.xa = (const float*)getp(d, "xa");
+  p.xb = (const float*)getp(d, "xb");
+  p.xc = (const float*)getp(d, "xc");
+  p.xz = getp(d, "xz");
+  p.xout = const_cast<void*>(getp(d, "xout"));
   p.tile = get<int>(d, "tile", 0);
   p.head_w = (const float*)getp(d, "head_w");
   p.head_b = (const float*)getp(d, "head_b");

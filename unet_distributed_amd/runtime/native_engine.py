@@ -107,6 +107,7 @@ class NativeUNet:
         self._alloc_activations()
         self.plan = self.C.Plan(self.dt_id)
         self.eval_plan = self.C.Plan(self.dt_id)
+        self._plan_xforms()
         self._build_forward(self.plan, dropout=True)
         self.fwd_end = self.plan.size()
         self.seg_ends: List[int] = []
@@ -426,12 +427,15 @@ class NativeUNet:
                                           0, 0, 0, 0, 0, _ptr(ws)],
                              [N, R // N, C, spec.groups, P, 0], [self.NORM_EPS], "gnfin:" + l.name)
             cstride = C
+        if l.name in self._xf_fwd:
+            return          # the consumer conv normalises z on load and writes the activation
         plan.add_generic("norm_apply", [_ptr(z), _ptr(mean), _ptr(rstd), gamma, beta, _ptr(b[l.name])],
                          [N, P, C, cstride, 1, self._salt(l.name)],
                          [spec.dropout if (l.dropout and dropout) else 0.0], "norm:" + l.name)
 
-    def _norm_bwd_ops(self, l):
-        """Plan ops (callables) of d:<L> -> dz:<L> plus gamma/beta grads."""
+    def _norm_bwd_ops(self, l, apply=True):
+        """Plan ops (callables) of d:<L> -> dz:<L> plus gamma/beta grads (apply=False:
+        statistics and coefficients only -- conv L's data gradient forms dz on load)."""
         b, spec = self.bufs, self.spec
         C, P, N = l.cout, self.npix(l.level) // self.B, self.B
         g, z, dz = b["d:" + l.name], b["z:" + l.name], b["dz:" + l.name]
@@ -456,6 +460,8 @@ class NativeUNet:
                                             _ptr(cb), _ptr(cc), dgam, dbet, _ptr(ws)],
                                [N, R // N, C, spec.groups, P, 1], [self.NORM_EPS], "gnfin_bwd:" + l.name)
                 cstride = C
+            if not apply:
+                return
             pl.add_generic("norm_bwd_apply", [_ptr(g), _ptr(z), _ptr(ca), _ptr(cb), _ptr(cc), _ptr(dz)],
                            [N, P, C, cstride], [], "norm_bwd:" + l.name)
         ops.append(emit)
@@ -573,6 +579,70 @@ class NativeUNet:
         d, h, w = self.sdims(lvl)
         return c * nb * d * h * w * ch * self.bufs[tname].element_size()
 
+    def _xf_bwd_fields(self, l):
+        """Operand-transform fields (conv_params.h xform 2) that let conv l's data
+        gradient form dz = ca g + cb z + cc on load and store it for the weight gradient
+        (no norm_bwd_apply pass), or None.  UNET_NORM_XFORM = fwd (default) | bwd | 1
+        (both) | 0: the backward transform measured -1.1 % on the BN b1024 step (the
+        fine-level dgrads are VALU-bound already; the separate pass streams at 5.3 TB/s),
+        the forward one +0.4 % (scripts/gpu_sweep_env.sh, same box)."""
+        if self.spec.norm == "none" or self.dims != 2 or os.environ.get("UNET_NORM_XFORM", "fwd") not in ("1", "bwd"):
+            return None
+        b = self.bufs
+        f = dict(xform=2, xa=_ptr(b["ca:" + l.name]), xb=_ptr(b["cb:" + l.name]), xc=_ptr(b["cc:" + l.name]),
+                 xz=_ptr(b["z:" + l.name]), xcs=0 if self.spec.norm == "batch" else l.cout,
+                 xout=_ptr(b["dz:" + l.name]))
+        d = self._conv_common(l.level, 3, 1, 1)
+        d.update(C1=l.cout, src1=_ptr(b["d:" + l.name]), wgt=self.wptr(l.name, "dg"), Cout=l.cin, relu=0,
+                 dst1=_ptr(b["dz:" + l.name]), **f)
+        try:
+            self.C.conv_fwd_grid(d)
+        except ValueError:
+            return None
+        return f
+
+    def _xf_fwd_fields(self, src):
+        """Operand-transform fields of a conv reading normalised activation `src` as the
+        pre-norm z (conv_params.h xform 1); the conv also writes the activation."""
+        b = self.bufs
+        return dict(xform=1, xa=_ptr(b["fa:" + src]), xb=_ptr(b["fc:" + src]),
+                    xcs=0 if self.spec.norm == "batch" else self.tinfo[src][1], xout=_ptr(b[src]))
+
+    def _plan_xforms(self):
+        """Normalised activations whose only consumer is the next conv's first source
+        (the 'a' convs of each block, no dropout): that conv normalises z on load
+        (UNET_NORM_XFORM=0 or bwd keeps the separate norm_apply pass).  Decided once, for
+        the training and the evaluation plans alike."""
+        self._xf_fwd = set()
+        if self.spec.norm == "none" or self.dims != 2 or os.environ.get("UNET_NORM_XFORM", "fwd") not in ("1", "fwd"):
+            return
+        users: Dict[str, list] = {}
+        for name, inp in self.inputs.items():
+            for k, t in enumerate(inp[:1] + inp[2:3]):
+                if t:
+                    users.setdefault(t, []).append((name, k))
+        users.setdefault(self.head_in, []).append(("Mask", 0))
+        kinds = {l.name: l.kind for l in self.spec.layers}
+        for l in self.spec.layers:
+            if l.kind != "conv" or l.name not in self.norm_layers or self.tinfo[l.name][3]:
+                continue
+            u = users.get(l.name, [])
+            if len(u) != 1 or u[0][1] != 0 or kinds.get(u[0][0]) != "conv":
+                continue
+            l2 = next(x for x in self.spec.layers if x.name == u[0][0])
+            src1, up1, skip = self.inputs[l2.name]
+            if skip or up1 != 1:
+                continue
+            d = self._conv_common(l2.level, 3, 1, 1)
+            d.update(C1=l.cout, src1=_ptr(self.bufs["z:" + l.name]), wgt=self.wptr(l2.name), Cout=l2.cout,
+                     relu=0, dst1=_ptr(self.bufs["z:" + l2.name]), bias=self.master_ptr(l2.name + "/bias"))
+            d.update(self._xf_fwd_fields(l.name))
+            try:
+                self.C.conv_fwd_grid(d)
+            except ValueError:
+                continue
+            self._xf_fwd.add(l.name)
+
     def _build_forward(self, plan, dropout, train=True):
         spec = self.spec
         nch = self._fwd_chunks()
@@ -627,6 +697,9 @@ class NativeUNet:
             d = self._conv_common(l.level, 3, 1, 1)
             d["N"] = nb
             normed = spec.norm != "none"
+            if src1 in self._xf_fwd:
+                d.update(self._xf_fwd_fields(src1))
+                s1 = _ptr(b["z:" + src1])
             d.update(name="fwd:" + l.name, C1=c1, C2=self.tinfo[skip][1] if skip else 0, up1=up1,
                      src1=s1, src2=P(skip) if skip else None,
                      wgt=self.wptr(l.name), bias=self.master_ptr(l.name + "/bias"),
@@ -770,9 +843,12 @@ class NativeUNet:
                 c1 = self.tinfo[src1][1]
                 c2 = self.tinfo[skip][1] if skip else 0
                 dy = b["d:" + l.name]
+                xf_bwd = None
                 if spec.norm != "none":
-                    ops.extend(self._norm_bwd_ops(l))
+                    xf_bwd = self._xf_bwd_fields(l) if not first else None
+                    ops.extend(self._norm_bwd_ops(l, apply=xf_bwd is None))
                     dy = b["dz:" + l.name]
+                wg_at = len(ops)
                 Q = self.npix(l.level)
                 # --- weight + bias gradient (fused column sums); the upsampling decoder's
                 # A operand is the materialised upsample when there is one
@@ -828,6 +904,13 @@ class NativeUNet:
                                          mask2=m2, mask_bits=2 * mb)
                         return d
                     dd_ = mk()                 # built now: it decides the fused norm backward
+                    if xf_bwd is not None:
+                        # dz formed on load by this dgrad (which also stores it): the weight
+                        # gradient reading dz moves behind it
+                        dd_.update(xf_bwd, src1=_ptr(b["d:" + l.name]))
+                        self.C.conv_fwd_grid(dd_)          # validated in _xf_bwd_fields
+                        wg_ops = ops[wg_at:]
+                        del ops[wg_at:]
                     halves = self._tail_halves(dd_, l, src1, skip, dy)
                     if halves is None:
                         emit_conv(lambda dd_=dd_: dd_)
@@ -839,6 +922,8 @@ class NativeUNet:
                         tail_parts[src1] = len(ops)
                         ops.append(("placeholder",))
                         emit_conv(lambda h=halves[1]: h)
+                    if xf_bwd is not None:
+                        ops.extend(wg_ops)
                     if up1 == 2:
                         lvl = self.tinfo[src1][0]
                         dd, hh, ww = self.sdims(lvl)
