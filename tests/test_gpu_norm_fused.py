@@ -294,3 +294,34 @@ def test_conv_dgrad_operand_dz_on_load(cuda_dev, N, H, Cg, Cy, gn, tile, norm_ep
     assert rel_err(dx, gref) < 1e-2
     assert torch.isfinite(dzo.float()).all()
     assert (dzo.float() - dz_ref.float()).abs().max() <= 1e-2 * dz_ref.float().abs().max()
+
+
+@pytest.mark.parametrize("N,H,Ch,gn,dims3", [(2, 64, 32, False, 0), (3, 32, 64, True, 0), (2, 16, 32, True, 1)])
+def test_norm_pool_matches_apply_then_pool(cuda_dev, N, H, Ch, gn, dims3):
+    """norm_pool (normalise a convNb output and max-pool it in one pass) writes the
+    activation, the pooled tensor and the argmax codes of norm_apply + pool_fwd."""
+    torch.manual_seed(52)
+    D = H if dims3 else 1
+    shape = (N, D, H, H, Ch) if dims3 else (N, H, H, Ch)
+    z = torch.randn(*shape, device=cuda_dev).bfloat16()
+    rows = N if gn else 1
+    fa = 0.5 + torch.rand(rows, Ch, device=cuda_dev)
+    fc = 0.3 * torch.randn(rows, Ch, device=cuda_dev)
+    view = (rows,) + (1,) * (len(shape) - 2) + (Ch,)
+    y_ref = torch.clamp(fa.view(view).double() * z.double() + fc.view(view).double(), min=0).float().bfloat16()
+    y = torch.empty_like(z)
+    pshape = (N, D // 2, H // 2, H // 2, Ch) if dims3 else (N, H // 2, H // 2, Ch)
+    py, py_ref = torch.empty(pshape, device=cuda_dev, dtype=torch.bfloat16), torch.empty(pshape, device=cuda_dev,
+                                                                                         dtype=torch.bfloat16)
+    n_codes = py.numel() // 8
+    code, code_ref = [torch.zeros(n_codes, device=cuda_dev, dtype=torch.int32) for _ in range(2)]
+    C().generic("norm_pool", [ptr(z), ptr(fa), ptr(fc), ptr(y), ptr(py), ptr(code)],
+                [N, D, H, H, Ch, dims3, Ch if gn else 0], [], stream())
+    C().generic("pool_fwd", [ptr(y_ref), ptr(py_ref), ptr(code_ref)], [N, D, H, H, Ch, dims3], [], stream())
+    torch.cuda.synchronize()
+    assert (y.float() - y_ref.float()).abs().max() <= 1e-2 * y_ref.float().abs().max()
+    same = torch.equal(y, y_ref)
+    if same:        # identical activations -> identical pool outputs and codes
+        assert torch.equal(py, py_ref) and torch.equal(code, code_ref)
+    else:
+        assert (py.float() - py_ref.float()).abs().max() <= 1e-2 * py_ref.float().abs().max()

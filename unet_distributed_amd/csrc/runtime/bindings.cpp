@@ -169,6 +169,7 @@ WgradParams wgrad_params(const py::dict& d) {
   X(cast_input_launch) \
   X(gather_batch_launch) \
   X(maxpool2_fwd_launch) \
+  X(norm_pool_launch) \
   X(maxpool2_bwd_launch) \
   X(maxpool2_bwd_norm_launch) \
   X(upsample2_bwd_launch) \
@@ -244,6 +245,17 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     if (c % 8) throw std::invalid_argument("pool: C % 8");
     if ((long long)n * d * h * w * c >= (1LL << 31)) throw std::invalid_argument("pool: too many elements");
     return [=](hipStream_t s) { return A->maxpool2_fwd_launch(x, n, d, h, w, c, d3, y, code, s); };
+  }
+  if (kind == "norm_pool") {
+    // ptrs: z, fa, fc, y, pooled y, code   ints: N, D, H, W, C, dims3, cstride
+    need(6, 7, 0);
+    const void* z = vp(0);
+    const float *fa = (const float*)vp(1), *fc = (const float*)vp(2);
+    void *y = vp(3), *py = vp(4), *code = vp(5);
+    int n = I[0], d = I[1], h = I[2], w = I[3], c = I[4], d3 = I[5], cs = I[6];
+    if (c % 8 || (cs != 0 && cs != c)) throw std::invalid_argument("norm_pool: C % 8, cstride 0 or C");
+    if ((long long)n * d * h * w * c >= (1LL << 31)) throw std::invalid_argument("norm_pool: too many elements");
+    return [=](hipStream_t s) { return A->norm_pool_launch(z, fa, fc, cs, n, d, h, w, c, d3, y, py, code, s); };
   }
   if (kind == "pool_bwd") {
     // ptrs: x, dy, skip, dx[, code]  (code non-null: argmax codes of pool_fwd, x unused)

@@ -429,6 +429,15 @@ class NativeUNet:
             cstride = C
         if l.name in self._xf_fwd:
             return          # the consumer conv normalises z on load and writes the activation
+        pool = self._pool_of.get(l.name)
+        if pool is not None and not (l.dropout and dropout) and os.environ.get("UNET_NORM_POOL", "1") != "0":
+            # convNb: normalisation and the 2x2 max-pool of its output in one pass
+            dd, hh, ww = self.sdims(l.level)
+            plan.add_generic("norm_pool", [_ptr(z), _ptr(fa), _ptr(fc), _ptr(b[l.name]), _ptr(b[pool]),
+                                           _ptr(self.pool_codes[pool])],
+                             [N, dd, hh, ww, C, int(self.dims == 3), cstride], [], "norm:" + l.name)
+            self._pool_fused.add(pool)
+            return
         plan.add_generic("norm_apply", [_ptr(z), _ptr(mean), _ptr(rstd), gamma, beta, _ptr(b[l.name])],
                          [N, P, C, cstride, 1, self._salt(l.name)],
                          [spec.dropout if (l.dropout and dropout) else 0.0], "norm:" + l.name)
