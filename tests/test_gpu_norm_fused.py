@@ -325,3 +325,26 @@ def test_norm_pool_matches_apply_then_pool(cuda_dev, N, H, Ch, gn, dims3):
         assert torch.equal(py, py_ref) and torch.equal(code, code_ref)
     else:
         assert (py.float() - py_ref.float()).abs().max() <= 1e-2 * py_ref.float().abs().max()
+
+
+@pytest.mark.parametrize("N,H,Ch,gn", [(2, 64, 32, False), (3, 32, 32, True), (2, 32, 64, True), (2, 16, 16, False)])
+def test_norm_head_logits(cuda_dev, N, H, Ch, gn):
+    """norm_head: the head input's activation y = relu(fa z + fc) and the 1x1 head
+    logits sum_c y w + b in one pass."""
+    torch.manual_seed(53)
+    z = torch.randn(N, H, H, Ch, device=cuda_dev).bfloat16()
+    rows = N if gn else 1
+    fa = 0.5 + torch.rand(rows, Ch, device=cuda_dev)
+    fc = 0.3 * torch.randn(rows, Ch, device=cuda_dev)
+    w = 0.2 * torch.randn(Ch, device=cuda_dev)
+    b = 0.1 * torch.randn(1, device=cuda_dev)
+    y_ref = torch.clamp(fa.view(rows, 1, 1, Ch).double() * z.double() + fc.view(rows, 1, 1, Ch).double(),
+                        min=0).float().bfloat16()
+    y = torch.empty_like(z)
+    logit = torch.zeros(N * H * H, device=cuda_dev)
+    C().generic("norm_head", [ptr(z), ptr(fa), ptr(fc), ptr(w), ptr(b), ptr(y), ptr(logit)],
+                [N * H * H, Ch, Ch if gn else 0, H * H], [], stream())
+    torch.cuda.synchronize()
+    assert (y.float() - y_ref.float()).abs().max() <= 1e-2 * y_ref.float().abs().max()
+    ref = (y.float().reshape(-1, Ch) * w).sum(1) + b
+    assert torch.allclose(logit, ref, rtol=1e-4, atol=1e-4)

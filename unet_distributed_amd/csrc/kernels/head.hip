@@ -277,6 +277,61 @@ hipError_t partial_reduce_launch(const float* partial, int nb, int width, float*
   return hipGetLastError();
 }
 
+// Normalised head input in one pass (norm mode): y = relu(fa z + fc) of the head's
+// input conv is stored (the head backward reads it) and the 1x1 head's logit
+// sum_c y[c] w[c] + b is written to `logit` (head_finish turns it into probabilities
+// and loss partials) -- head_fwd's full re-read of y disappears.  The CP = C / 8 lanes
+// of a pixel are adjacent; their partial dots are combined by xor shuffles.
+template <int C>
+__global__ void __launch_bounds__(HT) norm_head_kernel(const h16* __restrict__ z, const float* __restrict__ fa,
+                                                       const float* __restrict__ fc, int cstride, int npix,
+                                                       const float* __restrict__ w, const float* __restrict__ b,
+                                                       int P, h16* __restrict__ y, float* __restrict__ logit) {
+  constexpr int CP = C / 8;
+  const int cc = threadIdx.x % CP;
+  float wr[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) wr[e] = w[cc * 8 + e];
+  const float bias = b[0];
+  const long long total = (long long)P * CP;
+  for (long long i = blockIdx.x * (long long)HT + threadIdx.x; i < total; i += (long long)gridDim.x * HT) {
+    const int p = (int)(i / CP);
+    const size_t cb = (size_t)(p / npix) * cstride + cc * 8;
+    float f[8];
+    unpack8(*(const u32x4*)(z + i * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(fa[cb + e], f[e], fc[cb + e]), 0.f);
+    const u32x4 v = pack8(f);
+    *(u32x4*)(y + i * 8) = v;
+    unpack8(v, f);
+    float d = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d += f[e] * wr[e];
+#pragma unroll
+    for (int o = 1; o < CP; o <<= 1) d += __shfl_xor(d, o, 64);
+    if (cc == 0) logit[p] = d + bias;
+  }
+}
+
+hipError_t norm_head_launch(const void* z, const float* fa, const float* fc, int cstride, int npix, const float* w,
+                            const float* b, int P, int C, void* y, float* logit, hipStream_t s) {
+  const int nb = head_blocks(P * (C / 8) / 4 + 1);
+  switch (C) {
+    case 16:
+      hipLaunchKernelGGL(norm_head_kernel<16>, dim3(nb), dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
+                         P, (h16*)y, logit);
+      break;
+    case 32:
+      hipLaunchKernelGGL(norm_head_kernel<32>, dim3(nb), dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
+                         P, (h16*)y, logit);
+      break;
+    default:
+      hipLaunchKernelGGL(norm_head_kernel<64>, dim3(nb), dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
+                         P, (h16*)y, logit);
+  }
+  return hipGetLastError();
+}
+
 hipError_t head_finish_launch(float* prob, const void* t, int P, float* partial, float* sums, hipStream_t s) {
   // one float4 of logits per thread (latency-bound otherwise); 4 nb floats of
   // partials must fit the head's workspace of head_blocks(P) x (C + 5) >= 21

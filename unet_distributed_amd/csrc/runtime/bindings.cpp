@@ -178,6 +178,7 @@ WgradParams wgrad_params(const py::dict& d) {
   X(head_bwd_launch) \
   X(partial_reduce_launch) \
   X(head_finish_launch) \
+  X(norm_head_launch) \
   X(norm_moments_launch) \
   X(moments_collect_launch) \
   X(bn_stats_launch) \
@@ -330,6 +331,19 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     float *part = (float*)vp(2), *sums = (float*)vp(3);
     int P_ = I[0];
     return [=](hipStream_t s) { return A->head_finish_launch(prob, t, P_, part, sums, s); };
+  }
+  if (kind == "norm_head") {
+    // ptrs: z, fa, fc, w, b, y, logit   ints: P, C, cstride, npix
+    need(7, 4, 0);
+    const void* z = vp(0);
+    const float *fa = (const float*)vp(1), *fc = (const float*)vp(2), *w = (const float*)vp(3),
+                *bb = (const float*)vp(4);
+    void* y = vp(5);
+    float* lg = (float*)vp(6);
+    int P_ = I[0], C = I[1], cs = I[2], np_ = I[3];
+    check_msg(head_check(C));
+    if ((cs != 0 && cs != C) || np_ <= 0) throw std::invalid_argument("norm_head: cstride 0 or C, npix > 0");
+    return [=](hipStream_t s) { return A->norm_head_launch(z, fa, fc, cs, np_, w, bb, P_, C, y, lg, s); };
   }
   if (kind == "partial_reduce") {
     need(2, 2, 0);

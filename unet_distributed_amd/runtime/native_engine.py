@@ -429,6 +429,14 @@ class NativeUNet:
             cstride = C
         if l.name in self._xf_fwd:
             return          # the consumer conv normalises z on load and writes the activation
+        if (l.name == self.head_in and not (l.dropout and dropout) and self.tinfo[l.name][1] in (16, 32, 64)
+                and os.environ.get("UNET_NORM_HEAD", "1") != "0"):
+            # head input: normalisation + the 1x1 head's logits in one pass (head_finish follows)
+            plan.add_generic("norm_head", [_ptr(z), _ptr(fa), _ptr(fc), self.master_ptr("Mask/kernel"),
+                                           self.master_ptr("Mask/bias"), _ptr(b[l.name]), _ptr(self.prob)],
+                             [self.npix(l.level), C, cstride, P], [], "norm:" + l.name)
+            self._norm_head = True
+            return
         pool = self._pool_of.get(l.name)
         if pool is not None and not (l.dropout and dropout) and os.environ.get("UNET_NORM_POOL", "1") != "0":
             # convNb: normalisation and the 2x2 max-pool of its output in one pass
@@ -659,6 +667,7 @@ class NativeUNet:
         # the head's input conv (whole batch only; UNET_HEAD_FUSE=0 keeps the separate
         # head launch)
         self._head_fused_blocks = 0
+        self._norm_head = False
         self._fuse_head = nch == 1 and os.environ.get("UNET_HEAD_FUSE", "1") != "0"
         # convNb -> pool fusion (UNET_POOL_FUSE=0 keeps the separate pool launch)
         self._pool_of = {}
@@ -758,7 +767,7 @@ class NativeUNet:
                      bias=self.master_ptr(l.name + "/bias"), Cout=(2 ** self.dims) * l.cout,
                      relu=0, shuffle=self.dims, dst1=P(l.name))
             plan.add_conv_fwd(d)
-        elif l.kind == "mask" and self._head_fused_blocks:
+        elif l.kind == "mask" and (self._head_fused_blocks or self._norm_head):
             plan.add_generic("head_finish", [_ptr(self.prob), _ptr(self.target), _ptr(self.head_partial),
                                              _ptr(self.sums)], [self.npix(1)], [], "fwd:Mask")
         elif l.kind == "mask":
