@@ -97,10 +97,10 @@ class NativeUNet:
         else:
             raise NotImplementedError("native executor: in_channels=%d" % cin)
         self.bufs: Dict[str, torch.Tensor] = {}
-        # wgrad split-K grid target (workgroups per weight gradient): ~2 per CU when the
-        # wgrads run alone; ~1 per CU when they share the GPU with the dgrad chain (dual
-        # stream: 256 > 320 > 512 > 192 >> 128, bench sweep on MI355X)
-        self.wg_target = int(os.environ.get("UNET_WGRAD_WG_TARGET", "256" if self.dual_stream else "512"))
+        # wgrad split-K grid target (workgroups per weight gradient): ~2 per CU.  Dual
+        # stream at the default per-GPU batch 1024: 512 > 768 > 384 > 256 > 1024 >> 128
+        # (same-box sweep, +1.7 % over 256; at batch 256 the earlier sweep preferred 256)
+        self.wg_target = int(os.environ.get("UNET_WGRAD_WG_TARGET", "512"))
         # UNET_WGRAD_WIN=-1: never use the row-window wgrad kernel (A/B measurements)
         self.wgrad_win = int(os.environ.get("UNET_WGRAD_WIN", "0"))
         self._alloc_weights()
