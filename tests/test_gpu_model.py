@@ -276,6 +276,40 @@ def test_chunked_forward_equals_whole_batch(cuda_dev, monkeypatch, kw):
 
 
 @pytest.mark.parametrize("kw", [
+    dict(batch_size=8, img_size=64, in_channels=4, dropout=0.0),
+    dict(batch_size=4, img_size=64, in_channels=1, use_upsampling=True, hip_graph=True, dropout=0.0),
+    dict(batch_size=4, img_size=64, in_channels=4),
+])
+def test_two_stream_forward_equals_one_stream(cuda_dev, monkeypatch, kw):
+    """UNET_FWD_STREAMS=2 runs the training forward as two half-batch chunks on two
+    streams (fused pools / head logits written at the chunk's offset): without
+    dropout, activations, loss sums and gradients are bit-identical to the one-stream
+    forward; with dropout the second chunk draws its mask under its own salt, so only
+    the first chunk's bottleneck activation is compared."""
+    outs = []
+    for n in ("1", "2"):
+        monkeypatch.setenv("UNET_FWD_STREAMS", n)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
+        assert (getattr(nb.engine, "_fwd2", None) is not None) == (n == "2")
+        for seed in (77, 0x9E3779B9):
+            nb.fwd_bwd(x, y, seed=seed)
+        torch.cuda.synchronize()
+        outs.append((nb.sums().cpu(), nb.engine.prob.clone(), fn.grad.clone(),
+                     nb.engine.bufs["conv5b"].clone()))
+    (s0, p0, g0, a0), (s1, p1, g1, a1) = outs
+    if kw.get("dropout", 0.2):
+        h = a0.numel() // 2
+        assert torch.equal(a0.reshape(-1)[:h], a1.reshape(-1)[:h])
+        assert not torch.equal(a0, a1)
+        assert torch.isfinite(s1).all()
+        return
+    assert torch.equal(a0, a1)
+    assert torch.equal(p0, p1)
+    assert torch.equal(s0, s1)
+    assert torch.equal(g0, g1)
+
+
+@pytest.mark.parametrize("kw", [
     dict(batch_size=4, img_size=64, in_channels=4, loss="dice_bce"),
     dict(batch_size=2, img_size=32, in_channels=4, dims=3),
 ])

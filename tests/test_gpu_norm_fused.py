@@ -122,6 +122,56 @@ def test_conv_dgrad_norm_epilogue(cuda_dev, N, H, Cg, Cy, gn, drop, tile):
         assert torch.allclose(per, mom, rtol=1e-3, atol=1e-2 * H)
 
 
+@pytest.mark.parametrize("N,H,Cg,Cy,gn,tile", [
+    (2, 128, 32, 32, False, 0),     # level-1 shape (128-wide rows), BatchNorm coefficients
+    (2, 64, 64, 64, True, 0),       # GroupNorm coefficients
+    (4, 16, 256, 256, False, 0),    # 16-wide rows
+    (2, 32, 128, 128, True, 12),    # 64-channel row window
+])
+def test_dgrad_norm_skip_half_with_fused_pool_backward(cuda_dev, N, H, Cg, Cy, gn, tile):
+    """Skip half of a decoder data gradient into a normalised convNb output y =
+    relu(a z + c) that was also max-pooled: the epilogue adds the pooled gradient at
+    each window's argmax (route_gy), masks by the recomputed ReLU and writes the
+    {sum g, sum g z} rows -- the dskip tensor + pool_bwd_norm pass it replaces."""
+    torch.manual_seed(11)
+    dz = torch.randn(N, H, H, Cg, device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, Cy, Cg, device=cuda_dev) * 0.1).bfloat16()
+    z = torch.randn(N, H, H, Cy, device=cuda_dev).bfloat16()
+    rows_c = N if gn else 1
+    a = 0.5 + torch.rand(rows_c, Cy, device=cuda_dev)
+    c = 0.3 * torch.randn(rows_c, Cy, device=cuda_dev)
+    ai = a.view(rows_c, 1, 1, Cy) if gn else a.view(1, 1, 1, Cy)
+    ci = c.view(rows_c, 1, 1, Cy) if gn else c.view(1, 1, 1, Cy)
+    y = torch.relu(ai * z.float() + ci).bfloat16()
+    pooled = torch.empty(N, H // 2, H // 2, Cy, device=cuda_dev, dtype=torch.bfloat16)
+    codes = torch.zeros(N * (H // 2) ** 2 * Cy // 8, device=cuda_dev, dtype=torch.int32)
+    C().generic("pool_fwd", [ptr(y), ptr(pooled), ptr(codes)], [N, 1, H, H, Cy, 0], [], stream())
+    dpool = torch.randn(N, H // 2, H // 2, Cy, device=cuda_dev).bfloat16()
+    routed = torch.empty_like(y)
+    C().generic("pool_bwd", [0, ptr(dpool), 0, ptr(routed), ptr(codes)], [N, 1, H, H, Cy, 0], [], stream())
+    g = torch.empty_like(y)
+    wp = pack_dgrad(w)
+    d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cg, src1=ptr(dz), wgt=ptr(wp),
+             Cout=Cy, relu=0, dst1=ptr(g), nz=ptr(z), na=ptr(a), nc=ptr(c), ncs=Cy if gn else 0,
+             npix=H * H, route_gy=ptr(dpool), pool_code=ptr(codes), tile=tile)
+    rows, px = C().conv_stat_tiles(dict(d, stats=1))
+    assert rows > 0
+    st = torch.full((rows, 2, Cy), float("nan"), device=cuda_dev)
+    C().conv_fwd(dict(d, stats=ptr(st)), stream())
+    torch.cuda.synchronize()
+    xr = torch.zeros(N, Cy, H, H, device=cuda_dev, requires_grad=True)
+    (gref,) = torch.autograd.grad(F.conv2d(xr, w.float().permute(3, 2, 0, 1), padding=1), xr, nchw(dz.float()))
+    gref = (nhwc(gref) + routed.float()) * ((ai * z.float() + ci) > 0)
+    assert routed.float().abs().sum() > 0
+    assert rel_err(g, gref) < 1e-2
+    gf, zf = g.float().reshape(N, -1, Cy), z.float().reshape(N, -1, Cy)
+    mom = torch.stack([gf.sum(1), (gf * zf).sum(1)], 1)
+    assert torch.allclose(st.sum(0), mom.sum(0), rtol=1e-3, atol=1e-2 * H)
+    if (H * H) % px == 0 and rows % N == 0:
+        per = st.view(N, rows // N, 2, Cy).sum(1)
+        assert torch.allclose(per, mom, rtol=1e-3, atol=1e-2 * H)
+
+
 def test_tconv_dgrad_norm_epilogue(cuda_dev):
     """2x2 stride-2 transposed-conv data gradient (window kernel, 32-wide coarse rows)
     writing the gradient of a BatchNorm'd activation."""

@@ -79,6 +79,14 @@ __device__ __forceinline__ uint32_t pack2h(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, h16x2));
 }
 
+// ReLU of two packed 16-bit floats: the sign bit makes every negative value (and -0)
+// a negative int16, so one packed signed max with 0 clamps both
+__device__ __forceinline__ uint32_t relu2h(uint32_t w) {
+  typedef short s16x2 __attribute__((ext_vector_type(2)));
+  const s16x2 v = __builtin_elementwise_max(__builtin_bit_cast(s16x2, w), (s16x2){0, 0});
+  return __builtin_bit_cast(uint32_t, v);
+}
+
 __device__ __forceinline__ u32x4 pack8(const float* f) {
   u32x4 r;
 #pragma unroll

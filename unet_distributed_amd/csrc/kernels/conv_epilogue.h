@@ -50,7 +50,7 @@ __host__ __device__ inline const char* conv_norm_epi_check(const ConvFwdParams& 
   if (!p.stats && !p.nz) return nullptr;
   if (!p.stats) return "conv_fwd: nz (dgrad-norm epilogue) needs a stats buffer";
   if (p.relu || p.shuffle || p.drop_rate > 0.f || p.out_scale != 1.f || p.D1 != p.Cout || p.mask1 || p.mask2 ||
-      p.head_w || p.relu_bits || p.mask_bits || p.route_gy)
+      p.head_w || p.relu_bits || p.mask_bits || (p.route_gy && !p.nz))
     return "conv_fwd: statistics epilogue takes no ReLU / dropout / shuffle / scale / split / mask / head";
   if (p.nz && (p.bias || !p.na || !p.nc || p.npix <= 0 || p.mask_scale1 != 1.f || (p.ncs != 0 && p.ncs != p.Cout)))
     return "conv_fwd: dgrad-norm epilogue needs na / nc / npix, no bias";
@@ -123,6 +123,22 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     for (int r = 0; r < 4; ++r) {
       bsv[r] = kBias ? p.bias[kShuffle ? (n + r) % Dtb : n + r] : 0.f;
       msc[r] = kMaskScale ? ((n + r < p.D1) ? p.mask_scale1 : p.mask_scale2) : 1.f;
+    }
+    if constexpr (EPI == EPI_FWD) {
+      // bias + ReLU: packed fp32 adds, the ReLU on the packed 16-bit pair (relu2h; the
+      // same bits as clamping before the rounding)
+      const f32x2 b01 = {bsv[0], bsv[1]}, b23 = {bsv[2], bsv[3]};
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int ml = MapM::base(wm, i) + (lane & 15);
+        const f32x2 a01 = (f32x2){acc[i][j][0], acc[i][j][1]} + b01;
+        const f32x2 a23 = (f32x2){acc[i][j][2], acc[i][j][3]} + b23;
+        u32x2 pk;
+        pk[0] = relu2h(pack2h(a01[0], a01[1]));
+        pk[1] = relu2h(pack2h(a23[0], a23[1]));
+        *(u32x2*)(E + ml * EPI_STRIDE + nl * 2) = pk;
+      }
+      continue;
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -233,6 +249,25 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       const int q = qof(ml0 + it * RPI);
       if (q < M) zv[it] = *(const u32x4*)(zt + (size_t)q * p.Cout + n);
     }
+    // fused max-pool backward (route_gy; the skip half of a decoder data gradient): the
+    // pooled gradient is added at each window's recorded argmax before the mask
+    const bool route = p.route_gy != nullptr;
+    u32x4 rg[NIT];
+    uint32_t rc[NIT], rk[NIT];
+    if (route) {
+      const int OW = p.OW, cpp = p.Cout >> 3;
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int q = qof(ml0 + it * RPI);
+        if (q < M) {
+          const int gr = q / OW, w = q - gr * OW;
+          const size_t pq = (size_t)(gr >> 1) * (OW >> 1) + (w >> 1);
+          rc[it] = p.pool_code[pq * cpp + (n >> 3)];
+          rg[it] = *(const u32x4*)((const h16*)p.route_gy + pq * p.Cout + n);
+          rk[it] = ((uint32_t)(gr & 1) << 1) | (uint32_t)(w & 1);
+        }
+      }
+    }
     const bool drop = p.nd_rate > 0.f;
     const float dscale = drop ? 1.f / (1.f - p.nd_rate) : 1.f;
     const uint32_t dthr = (uint32_t)(p.nd_rate * 4294967296.0);
@@ -250,6 +285,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       float g[8], z[8];
       unpack8((u32x4){lo[0], lo[1], hi[0], hi[1]}, g);
       unpack8(zv[it], z);
+      if (route) {
+        float gg[8];
+        unpack8(rg[it], gg);
+        const uint32_t cw = rc[it];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (((cw >> (2 * e)) & 3u) == rk[it] && ((cw >> (24 + e)) & 1u)) g[e] += gg[e];
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         bool keep = fmaf(ca[e], z[e], cc[e]) > 0.f;
@@ -466,33 +509,35 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
         const int ml00 = 2 * pr * TROW + 2 * pc;
         const int q00 = qof(ml00);
         if (q00 >= M) continue;
-        float m[8];
-        uint32_t a[8];
+        // the staged values are ReLU outputs (>= 0, never -0): their 16-bit patterns
+        // order like the values, so key = bits << 16 | (3 - kk) as int32 gives max and
+        // first argmax (ties: larger 3 - kk wins) in one integer max per element
+        int32_t key[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          m[e] = -INFINITY;
-          a[e] = 0u;
-        }
+        for (int e = 0; e < 8; ++e) key[e] = INT32_MIN;
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           const int ml = ml00 + (kk >> 1) * TROW + (kk & 1);
           const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
           const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
-          float f[8];
-          unpack8((u32x4){lo[0], lo[1], hi[0], hi[1]}, f);
+          const u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const bool gt = f[e] > m[e];            // first maximum wins ties
-            m[e] = gt ? f[e] : m[e];
-            a[e] = gt ? (uint32_t)kk : a[e];
+          for (int e = 0; e < 4; ++e) {
+            key[2 * e] = max(key[2 * e], (int32_t)((v[e] << 16) | (3u - kk)));
+            key[2 * e + 1] = max(key[2 * e + 1], (int32_t)((v[e] & 0xffff0000u) | (3u - kk)));
           }
         }
         uint32_t w = 0;
+        u32x4 mv;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) w |= (a[e] << (2 * e)) | ((m[e] > 0.f ? 1u : 0u) << (24 + e));
+        for (int e = 0; e < 8; ++e)
+          w |= ((3u - ((uint32_t)key[e] & 3u)) << (2 * e)) | ((key[e] > 3 ? 1u : 0u) << (24 + e));
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          mv[e] = ((uint32_t)key[2 * e] >> 16) | ((uint32_t)key[2 * e + 1] & 0xffff0000u);
         const int grow = q00 / p.OW, gcol = q00 - grow * p.OW;
         const size_t pq = (size_t)(grow >> 1) * Wp + (gcol >> 1);
-        *(u32x4*)(pdst + pq * p.Cout + n0 + cb * 8) = pack8(m);
+        *(u32x4*)(pdst + pq * p.Cout + n0 + cb * 8) = mv;
         p.pool_code[pq * cpp + (n0 >> 3) + cb] = w;
       }
     }

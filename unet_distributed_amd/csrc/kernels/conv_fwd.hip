@@ -1244,7 +1244,8 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
       return "conv_fwd: operand transform needs a 2D single-source row-window conv (norm-input forward / "
              "norm-output data gradient)";
   }
-  if (p.route_gy && (!p.pool_code || conv_epi_mode(p) != EPI_DGRAD || !win_eligible(p) || p.KD != 1 || p.OD != 1 ||
+  if (p.route_gy && (!p.pool_code || (conv_epi_mode(p) != EPI_DGRAD && conv_epi_mode(p) != EPI_DGRAD_NORM) ||
+                     !win_eligible(p) || p.KD != 1 || p.OD != 1 ||
                      p.OH % 2 || p.OW % 2 || p.D1 != p.Cout || p.pool_dst || p.mask_scale1 != 1.f ||
                      (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12 && conv_fwd_pick(p) != 13)))
     return "conv_fwd: fused pool backward needs a 2D row-window data gradient (even dims, one destination, codes)";

@@ -516,7 +516,9 @@ class NativeUNet:
         data gradient, norm-free model; UNET_SKIP_ROUTE=0 keeps the dual-destination
         dgrad + separate pool backward), else None.  Saves the skip-gradient tensor's
         write and re-read: the pool backward's read of it becomes a second read of dy."""
-        if self.spec.norm != "none" or self.dims != 2 or os.environ.get("UNET_SKIP_ROUTE", "1") == "0":
+        if self.dims != 2 or os.environ.get("UNET_SKIP_ROUTE", "1") == "0":
+            return None
+        if self.spec.norm != "none" and not (skip in self.norm_layers and self.fuse_norm_stats):
             return None
         pool = next((x.name for x in self.spec.layers if x.kind == "pool" and self.inputs[x.name][0] == skip), None)
         if pool is None:
@@ -529,9 +531,19 @@ class NativeUNet:
                  wgt=self.wptr(l.name, "dg") + 2 * c1 * dgrow, Cout=c2, relu=0,
                  dst1=_ptr(b["d:" + skip]), D1=c2, mask1=m, mask_bits=mb, route_gy=_ptr(b["d:" + pool]),
                  pool_code=_ptr(self.pool_codes[pool]))
+        if self.spec.norm != "none":
+            # normalised skip source: the epilogue also recomputes the ReLU mask from the
+            # pre-norm z and writes the norm backward's {sum g, sum g z} rows (the
+            # pool_bwd_norm pass and the skip-gradient tensor are gone)
+            saved = dict(self._bwd_fused)
+            self._fuse_dgrad_norm(d, skip)
+            if not d.get("nz"):
+                self._bwd_fused = saved
+                return None
         try:
             self.C.conv_fwd_grid(d)
         except ValueError:
+            self._bwd_fused.pop(skip, None)
             return None
         return pool, d
 
@@ -660,8 +672,22 @@ class NativeUNet:
                 continue
             self._xf_fwd.add(l.name)
 
+    def _fwd_streams(self, train):
+        """2: the training forward runs as two half-batch chunks on two HIP streams, the
+        second chunk started once the first has finished the first `UNET_FWD_OFFSET`
+        layers, so kernels of different levels (bandwidth-bound full-resolution ones,
+        MFMA-bound coarse ones) share the GPU.  Norm-free 2D model with an even batch
+        (BatchNorm needs whole-batch statistics); UNET_FWD_STREAMS=1 keeps one stream."""
+        n = int(os.environ.get("UNET_FWD_STREAMS", "1"))
+        if n != 2 or not train or self.spec.norm != "none" or self.B % 2 or self.device.type != "cuda":
+            return 1
+        return 2
+
     def _build_forward(self, plan, dropout, train=True):
         spec = self.spec
+        nst = self._fwd_streams(train) if plan is self.plan else 1
+        if nst == 2:
+            return self._build_forward_2s(plan, dropout, train)
         nch = self._fwd_chunks()
         # fused head: the Mask 1x1 conv + sigmoid + loss partials run in the epilogue of
         # the head's input conv (whole batch only; UNET_HEAD_FUSE=0 keeps the separate
@@ -690,6 +716,34 @@ class NativeUNet:
             else:
                 self._fwd_layer(plan, l, dropout, train, 0, self.B)
                 i += 1
+
+    def _build_forward_2s(self, plan, dropout, train):
+        """Plan order: chunk 0's layers, chunk 1's layers, then the head finish on the
+        whole batch (its loss partials need every pixel); forward() launches the two
+        chunks on two streams."""
+        spec = self.spec
+        self._head_fused_blocks = 0
+        self._norm_head = False
+        self._fuse_head = os.environ.get("UNET_HEAD_FUSE", "1") != "0"
+        self._pool_of = {}
+        self._pool_fused = set()
+        if os.environ.get("UNET_POOL_FUSE", "1") != "0":
+            self._pool_of = {self.inputs[x.name][0]: x.name for x in spec.layers if x.kind == "pool"}
+        layers = [l for l in spec.layers if l.kind not in ("up", "mask")]
+        nb = self.B // 2
+        off = int(os.environ.get("UNET_FWD_OFFSET", "6"))
+        self._fwd2 = []                      # (first op, op after the offset layers, end) per chunk
+        for c in range(2):
+            start = plan.size()
+            mark = start
+            for k, l in enumerate(layers):
+                self._fwd_layer(plan, l, dropout, train, c, nb)
+                if k + 1 == off:
+                    mark = plan.size()
+            self._fwd2.append((start, mark, plan.size()))
+        for l in spec.layers:
+            if l.kind == "mask":
+                self._fwd_layer(plan, l, dropout, train, 0, self.B)
 
     def _fwd_layer(self, plan, l, dropout, train, c, nb):
         """Forward launches of layer `l` for images [c*nb, (c+1)*nb)."""
@@ -724,14 +778,15 @@ class NativeUNet:
                      Cout=l.cout, relu=0 if normed else 1,
                      dst1=_ptr(b["z:" + l.name]) if normed else P(l.name),
                      drop_rate=spec.dropout if (l.dropout and dropout and not normed) else 0.0,
-                     salt=self._salt(l.name))
+                     salt=(self._salt(l.name) + c * 0x9E3779B9) & 0xFFFFFFFF)
             bits = self.relu_bits.get(l.name)
             if bits is not None and not normed:
                 d["relu_bits"] = _ptr(bits) + c * nb * (self.npix(l.level) // self.B) * l.cout // 8
             pool = self._pool_of.get(l.name)
-            if pool is not None and not normed and nch == 1:
+            if pool is not None and not normed and (nch == 1 or self._fwd2_active(plan)):
                 # fused 2x2 max-pool: the epilogue writes the pooled tensor + argmax codes
-                dp = dict(d, pool_dst=P(pool), pool_code=_ptr(self.pool_codes[pool]))
+                pcode = _ptr(self.pool_codes[pool]) + c * nb * (self.npix(l.level + 1) // self.B) * (l.cout // 8) * 4
+                dp = dict(d, pool_dst=P(pool), pool_code=pcode)
                 try:
                     self.C.conv_fwd_grid(dp)
                     d = dp
@@ -742,7 +797,7 @@ class NativeUNet:
                 nbk = self._head_grid(d)
                 if nbk:
                     d.update(head_w=self.master_ptr("Mask/kernel"), head_b=self.master_ptr("Mask/bias"),
-                             head_logit=_ptr(self.prob))
+                             head_logit=_ptr(self.prob) + 4 * c * nb * (self.npix(1) // self.B))
                     self._head_fused_blocks = nbk
             fused = None
             if normed and (train or spec.norm == "group"):
@@ -778,6 +833,9 @@ class NativeUNet:
                                           self.master_ptr("Mask/bias"), _ptr(self.target),
                                           _ptr(self.prob), _ptr(part), _ptr(self.sums)],
                              [P1, hc], [], "fwd:Mask")
+
+    def _fwd2_active(self, plan):
+        return plan is self.plan and getattr(self, "_fwd2", None) is not None and self._fwd_streams(True) == 2
 
     def _head_grid(self, d):
         """Workgroups of the head-input conv when its forward can carry the fused
@@ -1192,9 +1250,32 @@ class NativeUNet:
             self.loss_scale_dev.fill_(scale)
             self._loss_scale = scale
 
+    def _forward_2s(self, stream):
+        """Chunk 0 on the caller's stream; chunk 1 on a side stream once chunk 0 has
+        finished its first layers; the head finish after both."""
+        main = stream if stream is not None else torch.cuda.current_stream()
+        if getattr(self, "_fside", None) is None:
+            self._fside = torch.cuda.Stream(device=self.device)
+            self._fev = torch.cuda.Event()
+        side = self._fside
+        (a0, m0, e0), (a1, m1, e1) = self._fwd2
+        hm, hs = main.cuda_stream, side.cuda_stream
+        side.wait_stream(main)                      # inputs loaded, previous step done
+        self.plan.run(a0, m0, hm)
+        self._fev.record(main)
+        self.plan.run(m0, e0, hm)
+        side.wait_event(self._fev)
+        self.plan.run(a1, e1, hs)
+        main.wait_stream(side)
+        self.plan.run(e1, self.fwd_end, hm)
+
     def forward(self, seed: int, stream=None):
         seed &= 0xFFFFFFFF
         self.plan.set_seed(seed)
+        if getattr(self, "_fwd2", None) is not None and self._fwd_streams(True) == 2:
+            if self.graphs is not None:
+                self.seed_dev.fill_(seed - (1 << 32) if seed >= (1 << 31) else seed)
+            return self._forward_2s(stream)
         if self.graphs is not None:
             self.seed_dev.fill_(seed - (1 << 32) if seed >= (1 << 31) else seed)
             with torch.cuda.stream(stream) if stream is not None else _nullctx():
