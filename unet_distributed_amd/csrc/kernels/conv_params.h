@@ -116,6 +116,8 @@ struct WgradParams {
   int split_lo, split_n;      // this launch runs splits [split_lo, split_lo + split_n) (split_n 0 = to the
                               // end): a weight gradient issued in parts as its dY is produced
   int tap_groups;             // taps handled per WG = (KD*KH*KW)/tap_groups
+  int xcd;                    // set by wgrad_launch: bit 0 = window kernels, bit 1 = tiled kernel map
+                              // logical workgroups to XCDs in contiguous runs (common.h xcd_remap)
   float* slab;                // [splits][taps][M][Nc] fp32
   // fused bias gradient: 0 = off, 1 = column sums of B (conv: dY -> n),
   // 2 = column sums of A over the WG's taps (tconv: dOut -> m)

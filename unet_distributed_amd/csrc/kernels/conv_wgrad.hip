@@ -91,9 +91,10 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
   const int tiles_m = Mtot / BM, tiles_n = p.Nc / BN;
   const int ntile = tiles_m * tiles_n * p.tap_groups;
   // blockIdx.x = split * ntile + tile   (splits of one tile spread over XCDs)
-  const int lsplit = blockIdx.x / ntile;
+  const int bid = (p.xcd & 2) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int lsplit = bid / ntile;
   const int split = p.split_lo + lsplit;
-  int t = blockIdx.x - lsplit * ntile;
+  int t = bid - lsplit * ntile;
   const int tg = t % p.tap_groups;
   t /= p.tap_groups;
   const int tn = t % tiles_n, tmi = t / tiles_n;
@@ -536,9 +537,12 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   const int Mtot = p.M1 + p.M2;
   const int cob = p.Nc / (32 * QO);
   const int ntile = (Mtot / 32) * cob * KD;
-  const int lsplit = blockIdx.x / ntile;
+  // (p.xcd bit 0: the tiles of one split -- which read the same dY / input windows --
+  // run on one XCD and share its L2)
+  const int bid = (p.xcd & 1) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int lsplit = bid / ntile;
   const int split = p.split_lo + lsplit;
-  int tile = blockIdx.x - lsplit * ntile;
+  int tile = bid - lsplit * ntile;
   const int kd = tile % KD;
   tile /= KD;
   const int ci_blk = tile / cob, co_blk = tile - ci_blk * cob;
@@ -886,7 +890,8 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
   const int nwin = (rows_total + R - 1) / R;
   const int Mtot = MT * 16;
   const int cot = p.Nc / 32;
-  const int lsplit = blockIdx.x / cot, co_blk = blockIdx.x - lsplit * cot;
+  const int bid = (p.xcd & 1) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int lsplit = bid / cot, co_blk = bid - lsplit * cot;
   const int split = p.split_lo + lsplit;
   const int co0 = co_blk * 32;
   constexpr int OOB = 0x7fffffff;
@@ -1066,7 +1071,8 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
   const int Mtot = p.M1;                    // output channels of the transposed conv
   const int cit = p.Nc / (32 * QN);
   const int ntile = (Mtot / 32) * cit;
-  const int lsplit = blockIdx.x / ntile, tile = blockIdx.x - lsplit * ntile;
+  const int bid = (p.xcd & 1) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int lsplit = bid / ntile, tile = bid - lsplit * ntile;
   const int split = p.split_lo + lsplit;
   const int co_blk = tile / cit, ci_blk = tile - co_blk * cit;
   const int co0 = co_blk * 32, ci0 = ci_blk * 32 * QN;
@@ -1288,7 +1294,17 @@ const char* wgrad_check(const WgradParams& p) {
   return nullptr;
 }
 
-hipError_t wgrad_launch(const WgradParams& p, hipStream_t s) {
+hipError_t wgrad_launch(const WgradParams& p0, hipStream_t s) {
+  // UNET_WGRAD_XCD: workgroup -> XCD map of the weight-gradient kernels (bit 0 window
+  // kernels, bit 1 tiled kernel; read once per process).  Default 1: same-box sweep of
+  // the headline step 43.4k -> 44.1k img/s (the 64 tiles of a split share one L2 instead
+  // of fetching each dY / input window into several); the tiled kernel's map is neutral.
+  static const int xcd = [] {
+    const char* e = getenv("UNET_WGRAD_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  WgradParams p = p0;
+  p.xcd = xcd;
   const WgradCfg c = wgrad_pick(p);
   if (wgrad_win_first_eligible(p)) return p.M1 == 4 ? launch_wgrad_win_first<4>(p, s) : launch_wgrad_win_first<8>(p, s);
   if (wgrad_tconv_win_eligible(p)) {
