@@ -790,3 +790,34 @@ def test_wgrad_split_ranges_compose(cuda_dev, kind):
         outs.append(slab)
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,tile", [(2, 128, 32, 32, 0), (4, 32, 64, 128, 0), (4, 16, 128, 256, 0),
+                                               (2, 256, 32, 32, 0), (2, 64, 64, 64, 13)])
+def test_window_conv_reverse_order_same_result(cuda_dev, N, H, Cin, Cout, tile):
+    """rev = 1 (windows walked last to first: the consumer starts on its producer's
+    most recent output) writes exactly the rev = 0 tensors, fused pool and ReLU bits
+    included."""
+    torch.manual_seed(46)
+    x = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, Cin, Cout, device=cuda_dev) * 0.1).bfloat16()
+    b = torch.randn(Cout, device=cuda_dev)
+    wp = pack_fwd(w)
+    outs = []
+    for rev in (0, 1):
+        y = torch.empty(N, H, H, Cout, device=cuda_dev, dtype=torch.bfloat16)
+        bits = torch.zeros(N * H * H * Cout // 8, device=cuda_dev, dtype=torch.uint8)
+        pooled = torch.empty(N, H // 2, H // 2, Cout, device=cuda_dev, dtype=torch.bfloat16)
+        codes = torch.zeros(N * (H // 2) ** 2 * Cout // 8, device=cuda_dev, dtype=torch.int32)
+        d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(x), wgt=ptr(wp), bias=ptr(b),
+                 Cout=Cout, relu=1, dst1=ptr(y), relu_bits=ptr(bits), tile=tile, rev=rev)
+        if H <= 128:
+            d.update(pool_dst=ptr(pooled), pool_code=ptr(codes))
+        assert C().conv_fwd_grid(d) > 0
+        C().conv_fwd(d, stream())
+        torch.cuda.synchronize()
+        outs.append((y, bits, pooled, codes))
+    for a, bb in zip(*outs):
+        assert torch.equal(a, bb)
+    ref = nhwc(F.relu(F.conv2d(nchw(x.float()), w.float().permute(3, 2, 0, 1), b, padding=1)))
+    assert rel_err(outs[1][0], ref) < 1e-2

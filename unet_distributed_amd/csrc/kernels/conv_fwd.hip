@@ -408,7 +408,8 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   const int M = rows_total * Wf;
   const int tiles_n = p.Cout / BN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int tm0 = bid / tiles_n, tn = bid % tiles_n;
+  const int tm = p.rev ? (int)(gridDim.x / tiles_n) - 1 - tm0 : tm0;
   const int rgi = GEO == GEO_SEG ? tm / nseg : tm;
   const int g0 = rgi * R, col0 = GEO == GEO_SEG ? (tm - rgi * nseg) * W : 0;
   const int n0 = tn * BN;

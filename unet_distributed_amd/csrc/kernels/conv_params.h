@@ -92,6 +92,8 @@ struct ConvFwdParams {
   const float* head_w;
   const float* head_b;
   float* head_logit;
+  int rev;                    // row-window kernels: windows in reverse order (the consumer starts
+                              // where its producer ended, on the tail still in the Infinity Cache)
   // filled by conv_fwd_prepare (host): K padded to 64, per-tap pixel deltas / offsets
   int Kpad;
   int tap_delta[27];

@@ -85,6 +85,7 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.drop_rate = get<float>(d, "drop_rate", 0.f);
   p.seed = get<uint32_t>(d, "seed", 0u);
   p.salt = get<uint32_t>(d, "salt", 0u);
+  p.rev = get<int>(d, "rev", 0);
   p.dst1 = const_cast<void*>(getp(d, "dst1"));
   p.dst2 = const_cast<void*>(getp(d, "dst2"));
   p.D1 = get<int>(d, "D1", p.Cout);
