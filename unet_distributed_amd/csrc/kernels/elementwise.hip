@@ -41,12 +41,10 @@ __global__ void __launch_bounds__(256) gather_batch_kernel(const float* __restri
                                                            const long long* __restrict__ idx, int B, int P, int Cin,
                                                            int Cpad, h16* __restrict__ xb, h16* __restrict__ tb) {
   const long long total = (long long)B * P;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int b = (int)(i / P), p = (int)(i - (long long)b * P);
+  auto one = [&](const size_t i, const int b, const int p) {
     const size_t s = (size_t)idx[b] * P + p;
     const float* src = x_all + s * Cin;
-    h16* dst = xb + (size_t)i * Cpad;
+    h16* dst = xb + i * Cpad;
     if (Cin == 4 && Cpad == 4) {
       const float4 v = *(const float4*)src;
       u32x2 o;
@@ -57,6 +55,20 @@ __global__ void __launch_bounds__(256) gather_batch_kernel(const float* __restri
       for (int c = 0; c < Cpad; ++c) dst[c] = (h16)(c < Cin ? src[c] : 0.f);
     }
     tb[i] = (h16)y_all[s];
+  };
+  if (total <= 0x7fffffffLL) {
+    // 32-bit index math (a 64-bit division per pixel dominated this streaming pass)
+    const int n = (int)total;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+      const int b = i / P;
+      one((size_t)i, b, i - b * P);
+    }
+    return;
+  }
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / P);
+    one((size_t)i, b, (int)(i - (long long)b * P));
   }
 }
 
