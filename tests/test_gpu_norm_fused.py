@@ -398,3 +398,64 @@ def test_norm_head_logits(cuda_dev, N, H, Ch, gn):
     assert (y.float() - y_ref.float()).abs().max() <= 1e-2 * y_ref.float().abs().max()
     ref = (y.float().reshape(-1, Ch) * w).sum(1) + b
     assert torch.allclose(logit, ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("N,H,Ch,gn", [(2, 64, 32, False), (3, 32, 32, True), (2, 32, 64, True), (4, 16, 16, False)])
+def test_norm_head_loss_and_backward(cuda_dev, N, H, Ch, gn):
+    """norm_head_loss -> head_norm_coef -> head_norm_bwd (the norm-mode training head,
+    head.hip) against an fp32 autograd-free reference: probabilities and loss sums, the
+    1x1 head's weight / bias gradient, the head input's norm-backward rows {sum g, sum g z}
+    of g = dlogit w [fa z + fc > 0] (per sample), and dz = ca g + cb z + cc."""
+    torch.manual_seed(54)
+    P = H * H
+    z = torch.randn(N, H, H, Ch, device=cuda_dev).bfloat16()
+    rows_c = N if gn else 1
+    fa = 0.5 + torch.rand(rows_c, Ch, device=cuda_dev)
+    fc = 0.3 * torch.randn(rows_c, Ch, device=cuda_dev)
+    w = 0.2 * torch.randn(Ch, device=cuda_dev)
+    b = 0.1 * torch.randn(1, device=cuda_dev)
+    t = (torch.rand(N, H, H, device=cuda_dev) > 0.7).to(torch.bfloat16)
+    nparts = C().hn_partial_floats(N, P, Ch)
+    part = torch.full((nparts,), float("nan"), device=cuda_dev)
+    prob = torch.zeros(N * P, device=cuda_dev)
+    sums = torch.zeros(4, device=cuda_dev)
+    cs = Ch if gn else 0
+    C().generic("norm_head_loss", [ptr(z), ptr(fa), ptr(fc), ptr(w), ptr(b), ptr(t), 0, ptr(prob), ptr(part),
+                                   ptr(sums)], [N, P, Ch, cs], [], stream())
+    torch.cuda.synchronize()
+    v = fa.view(rows_c, 1, Ch) * z.float().view(N, P, Ch) + fc.view(rows_c, 1, Ch)
+    y = torch.clamp(v, min=0).bfloat16().float()
+    logit = (y * w).sum(-1) + b                                  # [N, P]
+    pr = torch.sigmoid(logit)
+    tf = t.float().view(N, P)
+    assert torch.allclose(prob.view(N, P), pr, rtol=1e-4, atol=1e-5)
+    bce = torch.clamp(logit, min=0) - logit * tf + torch.log1p(torch.exp(-logit.abs()))
+    ref_sums = torch.stack([(tf * pr).sum(), tf.sum(), pr.sum(), bce.sum()])
+    assert torch.allclose(sums, ref_sums, rtol=1e-4, atol=1e-2)
+    # backward from the forward's sums
+    inv_total, bce_w, gs = 1.0 / (N * P), 0.3, 2.0
+    nbp = C().hn_blocks_per_sample(N, P)
+    rows = torch.full((N * nbp, 2, Ch), float("nan"), device=cuda_dev)
+    gw, gb = torch.zeros(Ch, device=cuda_dev), torch.zeros(1, device=cuda_dev)
+    C().generic("head_norm_coef", [ptr(part), ptr(sums), ptr(w), ptr(rows), ptr(gw), ptr(gb)], [N, P, Ch],
+                [inv_total, bce_w, gs], stream())
+    ca = 0.5 + torch.rand(rows_c, Ch, device=cuda_dev)
+    cb = 0.2 * torch.randn(rows_c, Ch, device=cuda_dev)
+    cc = 0.1 * torch.randn(rows_c, Ch, device=cuda_dev)
+    dz = torch.full_like(z, float("nan"))
+    C().generic("head_norm_bwd", [ptr(z), ptr(prob), ptr(t), ptr(sums), ptr(w), ptr(fa), ptr(fc), ptr(ca), ptr(cb),
+                                  ptr(cc), ptr(dz)], [N, P, Ch, cs], [inv_total, bce_w, gs], stream())
+    torch.cuda.synchronize()
+    I, St, Sp = ref_sums[0], ref_sums[1], ref_sums[2]
+    dl = gs * ((-2.0 / (2 * I + 1) * tf + 1.0 / (St + Sp + 1)) * pr * (1 - pr) + bce_w * (pr - tf) * inv_total)
+    g = dl.unsqueeze(-1) * w * (v > 0).float()                   # [N, P, C]
+    zf = z.float().view(N, P, Ch)
+    ref_rows = torch.stack([g.sum(1), (g * zf).sum(1)], 1)       # per sample [N, 2, C]
+    got = rows.view(N, nbp, 2, Ch).sum(1)
+    scale = ref_rows.abs().max()
+    assert (got - ref_rows).abs().max() <= 1e-3 * scale, (got - ref_rows).abs().max()
+    ref_gw = (dl.unsqueeze(-1) * y).sum((0, 1))
+    assert (gw - ref_gw).abs().max() <= 1e-3 * ref_gw.abs().max()
+    assert abs(gb.item() - dl.sum().item()) <= 1e-3 * dl.abs().sum().item()
+    ref_dz = ca.view(rows_c, 1, Ch) * g + cb.view(rows_c, 1, Ch) * zf + cc.view(rows_c, 1, Ch)
+    assert (dz.float().view(N, P, Ch) - ref_dz).abs().max() <= 1e-2 * ref_dz.abs().max()

@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(HT) head_finish_kernel(float* __restrict__ pro
   }
 }
 
-// out[j] = sum_b partial[b][j]: one block per column j, fixed order
+// out[j] = sum_b partial[b][j]: one block per column j (row stride `width`), fixed order
 __global__ void __launch_bounds__(256) partial_reduce_kernel(const float* __restrict__ partial, int nb, int width,
                                                              float* __restrict__ out) {
   __shared__ float red[256];
@@ -329,6 +329,306 @@ hipError_t norm_head_launch(const void* z, const float* fa, const float* fc, int
       hipLaunchKernelGGL(norm_head_kernel<64>, dim3(nb), dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
                          P, (h16*)y, logit);
   }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// Norm-mode training head: the loss and every pixel sum the head's backward needs are
+// formed in the forward pass, so the backward reads the head input's z once.
+//
+// The logit gradient is linear in three per-pixel terms with batch-scalar weights,
+//   dlogit_p = al u_p + be v_p + ga w_p,   u = t p (1 - p), v = p (1 - p), w = p - t,
+//   al = -2 gs / (2 I + 1), be = gs / (St + Sp + 1), ga = gs bce_w / P_total
+// (gs: loss scale), and the scalars are only known once the loss sums are.  So the
+// sums the backward needs over pixels -- the 1x1 head's weight gradient sum_p dlogit y_c
+// and the head input's norm-backward statistics {sum_p g_c, sum_p g_c z_c} of
+// g_c = dlogit w_c m_c (m_c = [fa z + fc > 0], as the dgrad-norm epilogue recomputes it)
+// -- are al/be/ga combinations of nine per-channel sums {u, v, w} x {m, m z, y} that the
+// forward accumulates beside the logits.  The backward is then
+//   head_norm_coef:  rows [R][2][C] + head weight/bias gradient from the block partials
+//   bn/gn_stats:     dz coefficients a, b, c (unchanged)
+//   head_norm_bwd:   dz = a w dlogit m + b z + c  (dlogit from prob and t per pixel)
+// replacing head_bwd (y read, dx written), the moments pass over (dx, z) and
+// norm_bwd_apply (dx, z read).  The activation y itself need not be stored.
+//
+// Block partial row (HN_W(C) floats): [k][C] for k = 0..8 = U_m V_m W_m U_mz V_mz W_mz
+// U_y V_y W_y, then Su Sv Sw I St Sp BCE and one pad float.
+// Grid (blocks per sample, N): the rows of sample n are consecutive (GroupNorm).
+__host__ __device__ constexpr int hn_width(int C) { return 9 * C + 8; }
+
+namespace {
+
+__device__ __forceinline__ void hn_scalars(const float* __restrict__ sums, float inv_total, float bce_w, float gs,
+                                           float& al, float& be, float& ga) {
+  al = -2.f * gs / (2.f * sums[0] + 1.f);
+  be = gs / (sums[1] + sums[2] + 1.f);
+  ga = gs * bce_w * inv_total;
+}
+
+template <int C>
+__global__ void __launch_bounds__(HT) norm_head_loss_kernel(const h16* __restrict__ z, const float* __restrict__ fa,
+                                                            const float* __restrict__ fc, int cstride, int npix,
+                                                            const float* __restrict__ w, const float* __restrict__ b,
+                                                            const h16* __restrict__ t, h16* __restrict__ y,
+                                                            float* __restrict__ prob, float* __restrict__ partial) {
+  constexpr int CP = C / 8, PPB = HT / CP, WD = hn_width(C);
+  __shared__ float red[HT / 64][WD];
+  const int n = blockIdx.y, nbp = gridDim.x, blk = blockIdx.x;
+  const int cc = threadIdx.x % CP, pr0 = threadIdx.x / CP, c0 = cc * 8;
+  float wr[8], A[8], B[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    wr[e] = w[c0 + e];
+    A[e] = fa[(size_t)n * cstride + c0 + e];
+    B[e] = fc[(size_t)n * cstride + c0 + e];
+  }
+  const float bias = b[0];
+  float acc[9][8];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
+  float su = 0.f, sv = 0.f, sw = 0.f, sI = 0.f, sT = 0.f, sP = 0.f, sB = 0.f;
+  const int p0 = (int)((long long)blk * npix / nbp), p1 = (int)((long long)(blk + 1) * npix / nbp);
+  const size_t sb = (size_t)n * npix;
+  // the CP lanes of one pixel are adjacent and always take the same trip count
+#pragma unroll 2
+  for (int p = p0 + pr0; p < p1; p += PPB) {
+    const size_t q = sb + p;
+    float zf[8], v[8], yv[8];
+    unpack8(*(const u32x4*)(z + q * C + c0), zf);
+    const float tv = (float)t[q];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = fmaf(A[e], zf[e], B[e]);
+      yv[e] = fmaxf(v[e], 0.f);
+    }
+    const u32x4 yp = pack8(yv);
+    if (y) *(u32x4*)(y + q * C + c0) = yp;
+    unpack8(yp, yv);                                 // the logit of the stored 16-bit y
+    float d = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d += yv[e] * wr[e];
+#pragma unroll
+    for (int o = 1; o < CP; o <<= 1) d += __shfl_xor(d, o, 64);
+    const float zl = d + bias;
+    const float pr = 1.f / (1.f + __expf(-zl));
+    const float vv = pr * (1.f - pr), uu = tv * vv, ww = pr - tv;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float m = v[e] > 0.f ? 1.f : 0.f;
+      const float mz = m * zf[e];
+      acc[0][e] = fmaf(m, uu, acc[0][e]);
+      acc[1][e] = fmaf(m, vv, acc[1][e]);
+      acc[2][e] = fmaf(m, ww, acc[2][e]);
+      acc[3][e] = fmaf(mz, uu, acc[3][e]);
+      acc[4][e] = fmaf(mz, vv, acc[4][e]);
+      acc[5][e] = fmaf(mz, ww, acc[5][e]);
+      acc[6][e] = fmaf(yv[e], uu, acc[6][e]);
+      acc[7][e] = fmaf(yv[e], vv, acc[7][e]);
+      acc[8][e] = fmaf(yv[e], ww, acc[8][e]);
+    }
+    if (cc == 0) {
+      prob[q] = pr;
+      su += uu;
+      sv += vv;
+      sw += ww;
+      sI += tv * pr;
+      sT += tv;
+      sP += pr;
+      sB += fmaxf(zl, 0.f) - zl * tv + log1pf(__expf(-fabsf(zl)));
+    }
+  }
+  // lanes l, l + CP, l + 2 CP, ... of a wave hold the same channels
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = CP; o < 64; o <<= 1) acc[k][e] += __shfl_xor(acc[k][e], o, 64);
+  su = wave_sum(su);
+  sv = wave_sum(sv);
+  sw = wave_sum(sw);
+  sI = wave_sum(sI);
+  sT = wave_sum(sT);
+  sP = wave_sum(sP);
+  sB = wave_sum(sB);
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  if (ln < CP) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wv][k * C + ln * 8 + e] = acc[k][e];
+  }
+  if (ln == 0) {
+    float* r = &red[wv][9 * C];
+    r[0] = su;
+    r[1] = sv;
+    r[2] = sw;
+    r[3] = sI;
+    r[4] = sT;
+    r[5] = sP;
+    r[6] = sB;
+    r[7] = 0.f;
+  }
+  __syncthreads();
+  float* out = partial + ((size_t)n * nbp + blk) * WD;
+  for (int j = threadIdx.x; j < WD; j += HT) {
+    float s = red[0][j];
+#pragma unroll
+    for (int k = 1; k < HT / 64; ++k) s += red[k][j];
+    out[j] = s;
+  }
+}
+
+// Blocks 0 .. C: head weight (j < C) / bias (j == C) gradient, column sums over the nb
+// partial rows in a fixed order.  Blocks past C: norm-backward rows
+//   rows[r][0][c] = w_c (al U_m + be V_m + ga W_m)[r][c],  rows[r][1][c] = w_c (... m z ...)
+__global__ void __launch_bounds__(256) head_norm_coef_kernel(const float* __restrict__ partial, int nb, int C,
+                                                             const float* __restrict__ sums,
+                                                             const float* __restrict__ w, float inv_total,
+                                                             float bce_w, float gscale,
+                                                             const float* __restrict__ gscale_ptr,
+                                                             float* __restrict__ rows, float* __restrict__ gw,
+                                                             float* __restrict__ gb) {
+  __shared__ float red[256];
+  const float gs = gscale_ptr ? *gscale_ptr : gscale;
+  float al, be, ga;
+  hn_scalars(sums, inv_total, bce_w, gs, al, be, ga);
+  const int WD = hn_width(C);
+  if ((int)blockIdx.x <= C) {
+    const int j = blockIdx.x;
+    const int o = j < C ? 6 * C + j : 9 * C;
+    const int st = j < C ? C : 1;
+    float s = 0.f;
+    for (int k = threadIdx.x; k < nb; k += 256) {
+      const float* r = partial + (size_t)k * WD + o;
+      s += al * r[0] + be * r[st] + ga * r[2 * st];
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+      if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      if (j < C)
+        gw[j] = red[0];
+      else
+        gb[0] = red[0];
+    }
+    return;
+  }
+  const long long total = (long long)nb * C;
+  for (long long i = (long long)(blockIdx.x - C - 1) * 256 + threadIdx.x; i < total;
+       i += (long long)(gridDim.x - C - 1) * 256) {
+    const int r = (int)(i / C), c = (int)(i - (long long)r * C);
+    const float* pr = partial + (size_t)r * WD + c;
+    rows[((size_t)r * 2 + 0) * C + c] = w[c] * (al * pr[0] + be * pr[C] + ga * pr[2 * C]);
+    rows[((size_t)r * 2 + 1) * C + c] = w[c] * (al * pr[3 * C] + be * pr[4 * C] + ga * pr[5 * C]);
+  }
+}
+
+// dz = a (w dlogit m) + b z + c for the head input (coefficients [C] or [N][C]); grid
+// (blocks per sample, N), one 8-channel column per thread as norm_bwd_apply
+__global__ void __launch_bounds__(256) head_norm_bwd_kernel(
+    const h16* __restrict__ z, const float* __restrict__ prob, const h16* __restrict__ t,
+    const float* __restrict__ sums, const float* __restrict__ w, const float* __restrict__ fa,
+    const float* __restrict__ fc, const float* __restrict__ ca, const float* __restrict__ cb,
+    const float* __restrict__ ccf, int cstride, int P, int C, float inv_total, float bce_w, float gscale,
+    const float* __restrict__ gscale_ptr, h16* __restrict__ dz) {
+  const int n = blockIdx.y, nbp = gridDim.x, blk = blockIdx.x;
+  const int cpr = C / 8, rstep = 256 / cpr;
+  const int cc = threadIdx.x % cpr, rs = threadIdx.x / cpr;
+  if (rs >= rstep) return;
+  const float gs = gscale_ptr ? *gscale_ptr : gscale;
+  float al, be, ga;
+  hn_scalars(sums, inv_total, bce_w, gs, al, be, ga);
+  const int c0 = cc * 8;
+  float aw[8], bz[8], c1[8], A[8], B[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const size_t k = (size_t)n * cstride + c0 + e;
+    aw[e] = ca[k] * w[c0 + e];
+    bz[e] = cb[k];
+    c1[e] = ccf[k];
+    A[e] = fa[k];
+    B[e] = fc[k];
+  }
+  const int p0 = (int)((long long)blk * P / nbp), p1 = (int)((long long)(blk + 1) * P / nbp);
+  const size_t sb = (size_t)n * P;
+#pragma unroll 4
+  for (int p = p0 + rs; p < p1; p += rstep) {
+    const size_t q = sb + p;
+    float zf[8];
+    unpack8(*(const u32x4*)(z + q * C + c0), zf);
+    const float pr = prob[q], tv = (float)t[q];
+    const float vv = pr * (1.f - pr);
+    const float dl = al * tv * vv + be * vv + ga * (pr - tv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float g = fmaf(A[e], zf[e], B[e]) > 0.f ? aw[e] * dl : 0.f;
+      zf[e] = g + fmaf(bz[e], zf[e], c1[e]);
+    }
+    *(u32x4*)(dz + q * C + c0) = pack8(zf);
+  }
+}
+
+}  // namespace
+
+int hn_blocks_per_sample(int N, int P) {
+  int nbp = (2048 + N - 1) / N;
+  const int maxb = (P + 255) / 256;
+  if (nbp > maxb) nbp = maxb;
+  return nbp < 1 ? 1 : nbp;
+}
+
+int hn_partial_floats(int N, int P, int C) { return N * hn_blocks_per_sample(N, P) * hn_width(C); }
+
+hipError_t norm_head_loss_launch(const void* z, const float* fa, const float* fc, int cstride, int N, int npix,
+                                 const float* w, const float* b, const void* t, void* y, int C, float* prob,
+                                 float* partial, float* sums, hipStream_t s) {
+  const int nbp = hn_blocks_per_sample(N, npix);
+  const dim3 grid(nbp, N);
+  switch (C) {
+    case 16:
+      hipLaunchKernelGGL(norm_head_loss_kernel<16>, grid, dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
+                         (const h16*)t, (h16*)y, prob, partial);
+      break;
+    case 32:
+      hipLaunchKernelGGL(norm_head_loss_kernel<32>, grid, dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
+                         (const h16*)t, (h16*)y, prob, partial);
+      break;
+    default:
+      hipLaunchKernelGGL(norm_head_loss_kernel<64>, grid, dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
+                         (const h16*)t, (h16*)y, prob, partial);
+  }
+  // loss sums {I, St, Sp, BCE}: columns 9C + 3 .. 9C + 6 of the block rows
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3(4), dim3(256), 0, s, partial + 9 * C + 3, N * nbp, hn_width(C),
+                     sums);
+  return hipGetLastError();
+}
+
+hipError_t head_norm_coef_launch(const float* partial, int N, int npix, int C, const float* sums, const float* w,
+                                 float inv_total, float bce_w, float gscale, const float* gscale_ptr, float* rows,
+                                 float* gw, float* gb, hipStream_t s) {
+  const int nb = N * hn_blocks_per_sample(N, npix);
+  long long eb = ((long long)nb * C + 255) / 256;
+  if (eb > 2048) eb = 2048;
+  hipLaunchKernelGGL(head_norm_coef_kernel, dim3(C + 1 + (int)eb), dim3(256), 0, s, partial, nb, C, sums, w,
+                     inv_total, bce_w, gscale, gscale_ptr, rows, gw, gb);
+  return hipGetLastError();
+}
+
+hipError_t head_norm_bwd_launch(const void* z, const float* prob, const void* t, const float* sums, const float* w,
+                                const float* fa, const float* fc, const float* ca, const float* cb, const float* cc,
+                                int cstride, int N, int P, int C, float inv_total, float bce_w, float gscale,
+                                const float* gscale_ptr, void* dz, hipStream_t s) {
+  int nbp = (1024 + N - 1) / N;
+  const int maxb = (P + 255) / 256;
+  nbp = nbp > maxb ? maxb : (nbp < 1 ? 1 : nbp);
+  hipLaunchKernelGGL(head_norm_bwd_kernel, dim3(nbp, N), dim3(256), 0, s, (const h16*)z, prob, (const h16*)t, sums, w,
+                     fa, fc, ca, cb, cc, cstride, P, C, inv_total, bce_w, gscale, gscale_ptr, (h16*)dz);
   return hipGetLastError();
 }
 

@@ -180,6 +180,9 @@ WgradParams wgrad_params(const py::dict& d) {
   X(partial_reduce_launch) \
   X(head_finish_launch) \
   X(norm_head_launch) \
+  X(norm_head_loss_launch) \
+  X(head_norm_coef_launch) \
+  X(head_norm_bwd_launch) \
   X(norm_moments_launch) \
   X(moments_collect_launch) \
   X(bn_stats_launch) \
@@ -345,6 +348,54 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     check_msg(head_check(C));
     if ((cs != 0 && cs != C) || np_ <= 0) throw std::invalid_argument("norm_head: cstride 0 or C, npix > 0");
     return [=](hipStream_t s) { return A->norm_head_launch(z, fa, fc, cs, np_, w, bb, P_, C, y, lg, s); };
+  }
+  if (kind == "norm_head_loss") {
+    // ptrs: z, fa, fc, w, b, t, y (0: not stored), prob, partial, sums
+    // ints: N, npix, C, cstride   (partial: hn_partial_floats(N, npix, C) floats)
+    need(10, 4, 0);
+    const void *z = vp(0), *t = vp(5);
+    const float *fa = (const float*)vp(1), *fc = (const float*)vp(2), *w = (const float*)vp(3),
+                *bb = (const float*)vp(4);
+    void* y = vp(6);
+    float *prob = (float*)vp(7), *part = (float*)vp(8), *sums = (float*)vp(9);
+    int n = I[0], np_ = I[1], C = I[2], cs = I[3];
+    check_msg(head_check(C));
+    if ((cs != 0 && cs != C) || np_ <= 0 || n <= 0) throw std::invalid_argument("norm_head_loss: cstride 0 or C");
+    return [=](hipStream_t s) {
+      return A->norm_head_loss_launch(z, fa, fc, cs, n, np_, w, bb, t, y, C, prob, part, sums, s);
+    };
+  }
+  if (kind == "head_norm_coef") {
+    // ptrs: partial, sums, w, rows, gw, gb [, gscale_ptr]   ints: N, npix, C
+    // floats: inv_total, bce_w, gscale    (rows: N * hn_blocks_per_sample x 2 x C)
+    need(6, 3, 3);
+    const float *part = (const float*)vp(0), *sums = (const float*)vp(1), *w = (const float*)vp(2);
+    float *rows = (float*)vp(3), *gw = (float*)vp(4), *gb = (float*)vp(5);
+    const float* gsp = P.size() > 6 ? (const float*)vp(6) : nullptr;
+    int n = I[0], np_ = I[1], C = I[2];
+    check_msg(head_check(C));
+    float it = (float)F[0], bw = (float)F[1], gs = (float)F[2];
+    return [=](hipStream_t s) {
+      return A->head_norm_coef_launch(part, n, np_, C, sums, w, it, bw, gs, gsp, rows, gw, gb, s);
+    };
+  }
+  if (kind == "head_norm_bwd") {
+    // ptrs: z, prob, t, sums, w, fa, fc, ca, cb, cc, dz [, gscale_ptr]   ints: N, P, C, cstride
+    // floats: inv_total, bce_w, gscale
+    need(11, 4, 3);
+    const void *z = vp(0), *t = vp(2);
+    const float *prob = (const float*)vp(1), *sums = (const float*)vp(3), *w = (const float*)vp(4),
+                *fa = (const float*)vp(5), *fc = (const float*)vp(6), *ca = (const float*)vp(7),
+                *cb = (const float*)vp(8), *cc = (const float*)vp(9);
+    void* dz = vp(10);
+    const float* gsp = P.size() > 11 ? (const float*)vp(11) : nullptr;
+    int n = I[0], np_ = I[1], C = I[2], cs = I[3];
+    check_msg(norm_check(C, 0));
+    if (cs != 0 && cs != C) throw std::invalid_argument("head_norm_bwd: cstride 0 or C");
+    float it = (float)F[0], bw = (float)F[1], gs = (float)F[2];
+    return [=](hipStream_t s) {
+      return A->head_norm_bwd_launch(z, prob, t, sums, w, fa, fc, ca, cb, cc, cs, n, np_, C, it, bw, gs, gsp, dz, s);
+    };
   }
   if (kind == "partial_reduce") {
     need(2, 2, 0);
@@ -611,6 +662,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("norm_blocks_per_sample", &norm_blocks_per_sample);
   m.def("sample_slices", &sample_slices);
   m.def("row_slices", &row_slices);
+  m.def("hn_blocks_per_sample", &hn_blocks_per_sample);
+  m.def("hn_partial_floats", &hn_partial_floats);
   m.def("wgrad_reduce_stage_floats", &wgrad_reduce_stage_floats);
   // QW > 0 describes a 3x3 (KT 9) or 3x3x3 (KT 27) stride-1 'same' conv on a QD x QH x QW
   // grid (QH, QD default to QW: square / cubic levels), a row-window candidate

@@ -109,6 +109,7 @@ class NativeUNet:
         self.plan = self.C.Plan(self.dt_id)
         self.eval_plan = self.C.Plan(self.dt_id)
         self._plan_xforms()
+        self._norm_head_loss = False
         self._build_forward(self.plan, dropout=True)
         self.fwd_end = self.plan.size()
         self.seg_ends: List[int] = []
@@ -432,6 +433,17 @@ class NativeUNet:
             return          # the consumer conv normalises z on load and writes the activation
         if (l.name == self.head_in and not (l.dropout and dropout) and self.tinfo[l.name][1] in (16, 32, 64)
                 and os.environ.get("UNET_NORM_HEAD", "1") != "0"):
+            if train and os.environ.get("UNET_NORM_HEAD_LOSS", "1") != "0":
+                # training: normalisation, logits, sigmoid, loss sums and the nine per-channel
+                # pixel sums of the head's backward in one pass (head.hip norm_head_loss);
+                # the activation is not stored -- nothing downstream reads it
+                hp = self._stat_buf("hn:part", self.C.hn_partial_floats(N, P, C))
+                plan.add_generic("norm_head_loss", [_ptr(z), _ptr(fa), _ptr(fc), self.master_ptr("Mask/kernel"),
+                                                    self.master_ptr("Mask/bias"), _ptr(self.target), 0,
+                                                    _ptr(self.prob), _ptr(hp), _ptr(self.sums)],
+                                 [N, P, C, cstride], [], "fwd:Mask")
+                self._norm_head_loss = True
+                return
             # head input: normalisation + the 1x1 head's logits in one pass (head_finish follows)
             plan.add_generic("norm_head", [_ptr(z), _ptr(fa), _ptr(fc), self.master_ptr("Mask/kernel"),
                                            self.master_ptr("Mask/bias"), _ptr(b[l.name]), _ptr(self.prob)],
@@ -465,8 +477,13 @@ class NativeUNet:
         fused = self._bwd_fused.get(l.name)
         ops = []
 
+        hn = self._norm_head_loss and l.name == self.head_in
+
         def emit(pl):
-            rows, R = self._stat_rows("bst:" + l.name, g, z, l, fused, pl, "nstat_bwd:" + l.name)
+            if hn:      # rows from the forward's head sums (head_norm_coef)
+                rows, R = self._hn_rows, N * self.C.hn_blocks_per_sample(N, P)
+            else:
+                rows, R = self._stat_rows("bst:" + l.name, g, z, l, fused, pl, "nstat_bwd:" + l.name)
             ws = self._stat_work("bst:" + l.name, R, C)
             if spec.norm == "batch":
                 pl.add_generic("bn_stats", [_ptr(rows), gamma, beta, 0, 0, _ptr(mean), _ptr(rstd), 0, 0,
@@ -479,6 +496,14 @@ class NativeUNet:
                                [N, R // N, C, spec.groups, P, 1], [self.NORM_EPS], "gnfin_bwd:" + l.name)
                 cstride = C
             if not apply:
+                return
+            if hn:      # dz = a w dlogit m + b z + c: g formed per pixel from prob and t
+                fa, fc = b["fa:" + l.name], b["fc:" + l.name]
+                pl.add_generic("head_norm_bwd", [_ptr(z), _ptr(self.prob), _ptr(self.target), _ptr(self.sums),
+                                                 self.master_ptr("Mask/kernel"), _ptr(fa), _ptr(fc), _ptr(ca),
+                                                 _ptr(cb), _ptr(cc), _ptr(dz), _ptr(self.loss_scale_dev)],
+                               [N, P, C, cstride], [1.0 / float(N * P), self.bce_weight, 1.0],
+                               "norm_bwd:" + l.name)
                 return
             pl.add_generic("norm_bwd_apply", [_ptr(g), _ptr(z), _ptr(ca), _ptr(cb), _ptr(cc), _ptr(dz)],
                            [N, P, C, cstride], [], "norm_bwd:" + l.name)
@@ -697,6 +722,8 @@ class NativeUNet:
         # head launch)
         self._head_fused_blocks = 0
         self._norm_head = False
+        if train:
+            self._norm_head_loss = False
         self._fuse_head = nch == 1 and os.environ.get("UNET_HEAD_FUSE", "1") != "0"
         # convNb -> pool fusion (UNET_POOL_FUSE=0 keeps the separate pool launch)
         self._pool_of = {}
@@ -826,6 +853,8 @@ class NativeUNet:
                      bias=self.master_ptr(l.name + "/bias"), Cout=(2 ** self.dims) * l.cout,
                      relu=0, shuffle=self.dims, dst1=P(l.name))
             plan.add_conv_fwd(d)
+        elif l.kind == "mask" and train and self._norm_head_loss:
+            pass                                 # loss sums written by norm_head_loss
         elif l.kind == "mask" and (self._head_fused_blocks or self._norm_head):
             plan.add_generic("head_finish", [_ptr(self.prob), _ptr(self.target), _ptr(self.head_partial),
                                              _ptr(self.sums)], [self.npix(1)], [], "fwd:Mask")
@@ -931,7 +960,20 @@ class NativeUNet:
         tail_parts = {}
         for li in range(len(layers) - 1, -1, -1):
             l = layers[li]
-            if l.kind == "mask":
+            if l.kind == "mask" and self._norm_head_loss:
+                # head weight / bias gradients and the head input's norm-backward rows from
+                # the forward's per-channel sums (no pass over the activation)
+                hc = self.tinfo[self.head_in][1]
+                Nb, Pb = self.B, self.npix(1) // self.B
+                self._hn_rows = self._stat_buf("hn:rows", Nb * self.C.hn_blocks_per_sample(Nb, Pb) * 2 * hc)
+                emit_generic("head_norm_coef",
+                             lambda hc=hc: [_ptr(self._stat_bufs["hn:part"]), _ptr(self.sums),
+                                            self.master_ptr("Mask/kernel"), _ptr(self._hn_rows),
+                                            self.grad_ptr("Mask/kernel"), self.grad_ptr("Mask/bias"),
+                                            _ptr(self.loss_scale_dev)],
+                             [Nb, Pb, hc], [inv_total, self.bce_weight, 1.0], "bwd:Mask")
+                done("Mask")
+            elif l.kind == "mask":
                 hc = self.tinfo[self.head_in][1]
                 nb = self.head_nb
                 emit_generic("head_bwd",
@@ -949,7 +991,8 @@ class NativeUNet:
                 dy = b["d:" + l.name]
                 xf_bwd = None
                 if spec.norm != "none":
-                    xf_bwd = self._xf_bwd_fields(l) if not first else None
+                    hn = self._norm_head_loss and l.name == self.head_in
+                    xf_bwd = self._xf_bwd_fields(l) if not (first or hn) else None
                     ops.extend(self._norm_bwd_ops(l, apply=xf_bwd is None))
                     dy = b["dz:" + l.name]
                 wg_at = len(ops)
