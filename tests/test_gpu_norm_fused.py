@@ -404,7 +404,8 @@ def test_norm_head_logits(cuda_dev, N, H, Ch, gn):
 def test_norm_head_loss_and_backward(cuda_dev, N, H, Ch, gn):
     """norm_head_loss -> head_norm_coef -> head_norm_bwd (the norm-mode training head,
     head.hip) against an fp32 autograd-free reference: probabilities and loss sums, the
-    1x1 head's weight / bias gradient, the head input's norm-backward rows {sum g, sum g z}
+    1x1 head's weight / bias gradient (of the unrounded activation relu(fa z + fc),
+    formed from the masked z sums), the head input's norm-backward rows {sum g, sum g z}
     of g = dlogit w [fa z + fc > 0] (per sample), and dz = ca g + cb z + cc."""
     torch.manual_seed(54)
     P = H * H
@@ -438,8 +439,8 @@ def test_norm_head_loss_and_backward(cuda_dev, N, H, Ch, gn):
     nbp = C().hn_blocks_per_sample(N, P)
     rows = torch.full((N * nbp, 2, Ch), float("nan"), device=cuda_dev)
     gw, gb = torch.zeros(Ch, device=cuda_dev), torch.zeros(1, device=cuda_dev)
-    C().generic("head_norm_coef", [ptr(part), ptr(sums), ptr(w), ptr(rows), ptr(gw), ptr(gb)], [N, P, Ch],
-                [inv_total, bce_w, gs], stream())
+    C().generic("head_norm_coef", [ptr(part), ptr(sums), ptr(w), ptr(fa), ptr(fc), ptr(rows), ptr(gw), ptr(gb)],
+                [N, P, Ch, cs], [inv_total, bce_w, gs], stream())
     ca = 0.5 + torch.rand(rows_c, Ch, device=cuda_dev)
     cb = 0.2 * torch.randn(rows_c, Ch, device=cuda_dev)
     cc = 0.1 * torch.randn(rows_c, Ch, device=cuda_dev)
@@ -455,7 +456,7 @@ def test_norm_head_loss_and_backward(cuda_dev, N, H, Ch, gn):
     got = rows.view(N, nbp, 2, Ch).sum(1)
     scale = ref_rows.abs().max()
     assert (got - ref_rows).abs().max() <= 1e-3 * scale, (got - ref_rows).abs().max()
-    ref_gw = (dl.unsqueeze(-1) * y).sum((0, 1))
+    ref_gw = (dl.unsqueeze(-1) * torch.clamp(v, min=0)).sum((0, 1))      # of the unrounded y
     assert (gw - ref_gw).abs().max() <= 1e-3 * ref_gw.abs().max()
     assert abs(gb.item() - dl.sum().item()) <= 1e-3 * dl.abs().sum().item()
     ref_dz = ca.view(rows_c, 1, Ch) * g + cb.view(rows_c, 1, Ch) * zf + cc.view(rows_c, 1, Ch)

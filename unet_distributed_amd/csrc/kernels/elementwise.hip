@@ -143,58 +143,74 @@ __global__ void __launch_bounds__(256) maxpool2_fwd_kernel(const h16* __restrict
 // the argmax codes of maxpool2_fwd_kernel are formed from the same registers -- the
 // pool's re-read of y disappears.  fa / fc: [C] (BatchNorm, cstride 0) or [N][C]
 // (GroupNorm, cstride C); sample of pooled item i is i / (OD OH OW cpp).
+template <bool D3>
 __global__ void __launch_bounds__(256) norm_pool_kernel(const h16* __restrict__ z, const float* __restrict__ fa,
                                                         const float* __restrict__ fc, int cstride, int N, int D,
-                                                        int H, int W, int C, int dims3, h16* __restrict__ y,
+                                                        int H, int W, int C, h16* __restrict__ y,
                                                         h16* __restrict__ py, uint32_t* __restrict__ code) {
-  const int OD = dims3 ? D / 2 : 1, OH = H / 2, OW = W / 2;
+  constexpr int NK = D3 ? 8 : 4, BITS = D3 ? 3 : 2;
+  const int OD = D3 ? D / 2 : 1, OH = H / 2, OW = W / 2;
   const int cpp = C / 8;
   const int per_n = OD * OH * OW * cpp;
   const int total = N * per_n;
-  const int nz = dims3 ? 2 : 1;
-  const int bits = dims3 ? 3 : 2;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const PoolIdx pi = pool_idx(i, cpp, OW, OH, H, W, dims3);
+  const int step = gridDim.x * blockDim.x;
+  // the window's NK input vectors of two grid-stride items are loaded before either is
+  // used (the per-item chain load -> normalise -> store is otherwise exposed)
+  auto load = [&](const int i, u32x4 (&raw)[NK]) {
+    const PoolIdx pi = pool_idx(i, cpp, OW, OH, H, W, D3);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int dz = k >> 2, dy = (k >> 1) & 1, dx = k & 1;
+      raw[k] = *(const u32x4*)(z + (size_t)(pi.base + (dz * H + dy) * W + dx) * C + pi.cc * 8);
+    }
+  };
+  auto finish = [&](const int i, const u32x4 (&raw)[NK]) {
+    const PoolIdx pi = pool_idx(i, cpp, OW, OH, H, W, D3);
     const size_t cb = (size_t)(i / per_n) * cstride + pi.cc * 8;
-    float A[8], B[8];
+    float A[8], B[8], m[8];
+    uint32_t arg[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       A[e] = fa[cb + e];
       B[e] = fc[cb + e];
-    }
-    float m[8];
-    uint32_t arg[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
       m[e] = -INFINITY;
       arg[e] = 0u;
     }
-    for (int dz = 0; dz < nz; ++dz)
 #pragma unroll
-      for (int dy = 0; dy < 2; ++dy)
+    for (int k = 0; k < NK; ++k) {
+      const int dz = k >> 2, dy = (k >> 1) & 1, dx = k & 1;
+      float f[8];
+      unpack8(raw[k], f);
 #pragma unroll
-        for (int dx = 0; dx < 2; ++dx) {
-          const uint32_t k = dz * 4 + dy * 2 + dx;
-          const size_t off = (size_t)(pi.base + (dz * H + dy) * W + dx) * C + pi.cc * 8;
-          float f[8];
-          unpack8(*(const u32x4*)(z + off), f);
+      for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(A[e], f[e], B[e]), 0.f);
+      const u32x4 v = pack8(f);
+      *(u32x4*)(y + (size_t)(pi.base + (dz * H + dy) * W + dx) * C + pi.cc * 8) = v;
+      unpack8(v, f);                                 // the stored (rounded) activation
 #pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(A[e], f[e], B[e]), 0.f);
-          const u32x4 v = pack8(f);
-          *(u32x4*)(y + off) = v;
-          unpack8(v, f);                                 // the stored (rounded) activation
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const bool gt = f[e] > m[e];                 // first maximum wins ties
-            m[e] = gt ? f[e] : m[e];
-            arg[e] = gt ? k : arg[e];
-          }
-        }
+      for (int e = 0; e < 8; ++e) {
+        const bool gt = f[e] > m[e];                 // first maximum wins ties
+        m[e] = gt ? f[e] : m[e];
+        arg[e] = gt ? (uint32_t)k : arg[e];
+      }
+    }
     *(u32x4*)(py + (size_t)i * 8) = pack8(m);
     uint32_t w = 0;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) w |= (arg[e] << (bits * e)) | ((m[e] > 0.f ? 1u : 0u) << (24 + e));
+    for (int e = 0; e < 8; ++e) w |= (arg[e] << (BITS * e)) | ((m[e] > 0.f ? 1u : 0u) << (24 + e));
     code[i] = w;
+  };
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + step < total; i += 2 * step) {
+    u32x4 r0[NK], r1[NK];
+    load(i, r0);
+    load(i + step, r1);
+    finish(i, r0);
+    finish(i + step, r1);
+  }
+  if (i < total) {
+    u32x4 r0[NK];
+    load(i, r0);
+    finish(i, r0);
   }
 }
 
@@ -468,8 +484,12 @@ hipError_t maxpool2_fwd_launch(const void* x, int N, int D, int H, int W, int C,
 hipError_t norm_pool_launch(const void* z, const float* fa, const float* fc, int cstride, int N, int D, int H, int W,
                             int C, int dims3, void* y, void* py, void* code, hipStream_t s) {
   const long long work = (long long)N * (dims3 ? D / 2 : 1) * (H / 2) * (W / 2) * (C / 8);
-  hipLaunchKernelGGL(norm_pool_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)z, fa, fc, cstride, N, D, H,
-                     W, C, dims3, (h16*)y, (h16*)py, (uint32_t*)code);
+  if (dims3)
+    hipLaunchKernelGGL(norm_pool_kernel<true>, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)z, fa, fc, cstride,
+                       N, D, H, W, C, (h16*)y, (h16*)py, (uint32_t*)code);
+  else
+    hipLaunchKernelGGL(norm_pool_kernel<false>, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)z, fa, fc,
+                       cstride, N, D, H, W, C, (h16*)y, (h16*)py, (uint32_t*)code);
   return hipGetLastError();
 }
 

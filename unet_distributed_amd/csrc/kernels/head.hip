@@ -343,18 +343,20 @@ hipError_t norm_head_launch(const void* z, const float* fa, const float* fc, int
 // sums the backward needs over pixels -- the 1x1 head's weight gradient sum_p dlogit y_c
 // and the head input's norm-backward statistics {sum_p g_c, sum_p g_c z_c} of
 // g_c = dlogit w_c m_c (m_c = [fa z + fc > 0], as the dgrad-norm epilogue recomputes it)
-// -- are al/be/ga combinations of nine per-channel sums {u, v, w} x {m, m z, y} that the
-// forward accumulates beside the logits.  The backward is then
+// -- are al/be/ga combinations of six per-channel sums {u, v, w} x {m, m z} that the
+// forward accumulates beside the logits (y = m (fa z + fc), so sum dlogit y_c =
+// fa_c sum dlogit m z + fc_c sum dlogit m: the weight gradient of the unrounded y).
+// The backward is then
 //   head_norm_coef:  rows [R][2][C] + head weight/bias gradient from the block partials
 //   bn/gn_stats:     dz coefficients a, b, c (unchanged)
 //   head_norm_bwd:   dz = a w dlogit m + b z + c  (dlogit from prob and t per pixel)
 // replacing head_bwd (y read, dx written), the moments pass over (dx, z) and
 // norm_bwd_apply (dx, z read).  The activation y itself need not be stored.
 //
-// Block partial row (HN_W(C) floats): [k][C] for k = 0..8 = U_m V_m W_m U_mz V_mz W_mz
-// U_y V_y W_y, then Su Sv Sw I St Sp BCE and one pad float.
+// Block partial row (hn_width(C) floats): [k][C] for k = 0..5 = U_m V_m W_m U_mz V_mz
+// W_mz, then Su Sv Sw I St Sp BCE and one pad float.
 // Grid (blocks per sample, N): the rows of sample n are consecutive (GroupNorm).
-__host__ __device__ constexpr int hn_width(int C) { return 9 * C + 8; }
+__host__ __device__ constexpr int hn_width(int C) { return 6 * C + 8; }
 
 namespace {
 
@@ -366,7 +368,7 @@ __device__ __forceinline__ void hn_scalars(const float* __restrict__ sums, float
 }
 
 template <int C>
-__global__ void __launch_bounds__(HT) norm_head_loss_kernel(const h16* __restrict__ z, const float* __restrict__ fa,
+__global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(3))) norm_head_loss_kernel(const h16* __restrict__ z, const float* __restrict__ fa,
                                                             const float* __restrict__ fc, int cstride, int npix,
                                                             const float* __restrict__ w, const float* __restrict__ b,
                                                             const h16* __restrict__ t, h16* __restrict__ y,
@@ -383,21 +385,17 @@ __global__ void __launch_bounds__(HT) norm_head_loss_kernel(const h16* __restric
     B[e] = fc[(size_t)n * cstride + c0 + e];
   }
   const float bias = b[0];
-  float acc[9][8];
+  float acc[6][8];
 #pragma unroll
-  for (int k = 0; k < 9; ++k)
+  for (int k = 0; k < 6; ++k)
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
   float su = 0.f, sv = 0.f, sw = 0.f, sI = 0.f, sT = 0.f, sP = 0.f, sB = 0.f;
   const int p0 = (int)((long long)blk * npix / nbp), p1 = (int)((long long)(blk + 1) * npix / nbp);
   const size_t sb = (size_t)n * npix;
-  // the CP lanes of one pixel are adjacent and always take the same trip count
-#pragma unroll 2
-  for (int p = p0 + pr0; p < p1; p += PPB) {
-    const size_t q = sb + p;
+  auto pixel = [&](const u32x4 raw, const float tv, const size_t q) {
     float zf[8], v[8], yv[8];
-    unpack8(*(const u32x4*)(z + q * C + c0), zf);
-    const float tv = (float)t[q];
+    unpack8(raw, zf);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       v[e] = fmaf(A[e], zf[e], B[e]);
@@ -424,9 +422,6 @@ __global__ void __launch_bounds__(HT) norm_head_loss_kernel(const h16* __restric
       acc[3][e] = fmaf(mz, uu, acc[3][e]);
       acc[4][e] = fmaf(mz, vv, acc[4][e]);
       acc[5][e] = fmaf(mz, ww, acc[5][e]);
-      acc[6][e] = fmaf(yv[e], uu, acc[6][e]);
-      acc[7][e] = fmaf(yv[e], vv, acc[7][e]);
-      acc[8][e] = fmaf(yv[e], ww, acc[8][e]);
     }
     if (cc == 0) {
       prob[q] = pr;
@@ -438,10 +433,31 @@ __global__ void __launch_bounds__(HT) norm_head_loss_kernel(const h16* __restric
       sP += pr;
       sB += fmaxf(zl, 0.f) - zl * tv + log1pf(__expf(-fabsf(zl)));
     }
+  };
+  // the CP lanes of one pixel are adjacent and always take the same path; KU pixel
+  // steps' loads are issued before any of them is used (memory-level parallelism: the
+  // per-pixel chain load -> dot -> shuffles -> sigmoid is long)
+  constexpr int KU = 2;
+  int p = p0 + pr0;
+  for (; p + (KU - 1) * PPB < p1; p += KU * PPB) {
+    u32x4 raw[KU];
+    float tv[KU];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const size_t q = sb + p + u * PPB;
+      raw[u] = *(const u32x4*)(z + q * C + c0);
+      tv[u] = (float)t[q];
+    }
+#pragma unroll
+    for (int u = 0; u < KU; ++u) pixel(raw[u], tv[u], sb + p + u * PPB);
+  }
+  for (; p < p1; p += PPB) {
+    const size_t q = sb + p;
+    pixel(*(const u32x4*)(z + q * C + c0), (float)t[q], q);
   }
   // lanes l, l + CP, l + 2 CP, ... of a wave hold the same channels
 #pragma unroll
-  for (int k = 0; k < 9; ++k)
+  for (int k = 0; k < 6; ++k)
 #pragma unroll
     for (int e = 0; e < 8; ++e)
 #pragma unroll
@@ -456,12 +472,12 @@ __global__ void __launch_bounds__(HT) norm_head_loss_kernel(const h16* __restric
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
   if (ln < CP) {
 #pragma unroll
-    for (int k = 0; k < 9; ++k)
+    for (int k = 0; k < 6; ++k)
 #pragma unroll
       for (int e = 0; e < 8; ++e) red[wv][k * C + ln * 8 + e] = acc[k][e];
   }
   if (ln == 0) {
-    float* r = &red[wv][9 * C];
+    float* r = &red[wv][6 * C];
     r[0] = su;
     r[1] = sv;
     r[2] = sw;
@@ -482,12 +498,15 @@ __global__ void __launch_bounds__(HT) norm_head_loss_kernel(const h16* __restric
 }
 
 // Blocks 0 .. C: head weight (j < C) / bias (j == C) gradient, column sums over the nb
-// partial rows in a fixed order.  Blocks past C: norm-backward rows
+// partial rows in a fixed order (row r belongs to sample r / nbp: fa / fc [C] or [N][C]).
+// Blocks past C: norm-backward rows
 //   rows[r][0][c] = w_c (al U_m + be V_m + ga W_m)[r][c],  rows[r][1][c] = w_c (... m z ...)
-__global__ void __launch_bounds__(256) head_norm_coef_kernel(const float* __restrict__ partial, int nb, int C,
-                                                             const float* __restrict__ sums,
-                                                             const float* __restrict__ w, float inv_total,
-                                                             float bce_w, float gscale,
+__global__ void __launch_bounds__(256) head_norm_coef_kernel(const float* __restrict__ partial, int nb, int nbp,
+                                                             int C, const float* __restrict__ sums,
+                                                             const float* __restrict__ w,
+                                                             const float* __restrict__ fa,
+                                                             const float* __restrict__ fc, int cstride,
+                                                             float inv_total, float bce_w, float gscale,
                                                              const float* __restrict__ gscale_ptr,
                                                              float* __restrict__ rows, float* __restrict__ gw,
                                                              float* __restrict__ gb) {
@@ -498,12 +517,16 @@ __global__ void __launch_bounds__(256) head_norm_coef_kernel(const float* __rest
   const int WD = hn_width(C);
   if ((int)blockIdx.x <= C) {
     const int j = blockIdx.x;
-    const int o = j < C ? 6 * C + j : 9 * C;
-    const int st = j < C ? C : 1;
     float s = 0.f;
     for (int k = threadIdx.x; k < nb; k += 256) {
-      const float* r = partial + (size_t)k * WD + o;
-      s += al * r[0] + be * r[st] + ga * r[2 * st];
+      const float* r = partial + (size_t)k * WD;
+      if (j < C) {
+        const size_t ci = (size_t)(k / nbp) * cstride + j;
+        s += fa[ci] * (al * r[3 * C + j] + be * r[4 * C + j] + ga * r[5 * C + j]) +
+             fc[ci] * (al * r[j] + be * r[C + j] + ga * r[2 * C + j]);
+      } else {
+        s += al * r[6 * C] + be * r[6 * C + 1] + ga * r[6 * C + 2];
+      }
     }
     red[threadIdx.x] = s;
     __syncthreads();
@@ -577,7 +600,7 @@ __global__ void __launch_bounds__(256) head_norm_bwd_kernel(
 }  // namespace
 
 int hn_blocks_per_sample(int N, int P) {
-  int nbp = (2048 + N - 1) / N;
+  int nbp = (4096 + N - 1) / N;
   const int maxb = (P + 255) / 256;
   if (nbp > maxb) nbp = maxb;
   return nbp < 1 ? 1 : nbp;
@@ -603,20 +626,21 @@ hipError_t norm_head_loss_launch(const void* z, const float* fa, const float* fc
       hipLaunchKernelGGL(norm_head_loss_kernel<64>, grid, dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
                          (const h16*)t, (h16*)y, prob, partial);
   }
-  // loss sums {I, St, Sp, BCE}: columns 9C + 3 .. 9C + 6 of the block rows
-  hipLaunchKernelGGL(partial_reduce_kernel, dim3(4), dim3(256), 0, s, partial + 9 * C + 3, N * nbp, hn_width(C),
+  // loss sums {I, St, Sp, BCE}: columns 6C + 3 .. 6C + 6 of the block rows
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3(4), dim3(256), 0, s, partial + 6 * C + 3, N * nbp, hn_width(C),
                      sums);
   return hipGetLastError();
 }
 
 hipError_t head_norm_coef_launch(const float* partial, int N, int npix, int C, const float* sums, const float* w,
-                                 float inv_total, float bce_w, float gscale, const float* gscale_ptr, float* rows,
-                                 float* gw, float* gb, hipStream_t s) {
-  const int nb = N * hn_blocks_per_sample(N, npix);
+                                 const float* fa, const float* fc, int cstride, float inv_total, float bce_w,
+                                 float gscale, const float* gscale_ptr, float* rows, float* gw, float* gb,
+                                 hipStream_t s) {
+  const int nbp = hn_blocks_per_sample(N, npix), nb = N * nbp;
   long long eb = ((long long)nb * C + 255) / 256;
   if (eb > 2048) eb = 2048;
-  hipLaunchKernelGGL(head_norm_coef_kernel, dim3(C + 1 + (int)eb), dim3(256), 0, s, partial, nb, C, sums, w,
-                     inv_total, bce_w, gscale, gscale_ptr, rows, gw, gb);
+  hipLaunchKernelGGL(head_norm_coef_kernel, dim3(C + 1 + (int)eb), dim3(256), 0, s, partial, nb, nbp, C, sums, w, fa,
+                     fc, cstride, inv_total, bce_w, gscale, gscale_ptr, rows, gw, gb);
   return hipGetLastError();
 }
 

@@ -366,17 +366,19 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     };
   }
   if (kind == "head_norm_coef") {
-    // ptrs: partial, sums, w, rows, gw, gb [, gscale_ptr]   ints: N, npix, C
+    // ptrs: partial, sums, w, fa, fc, rows, gw, gb [, gscale_ptr]   ints: N, npix, C, cstride
     // floats: inv_total, bce_w, gscale    (rows: N * hn_blocks_per_sample x 2 x C)
-    need(6, 3, 3);
-    const float *part = (const float*)vp(0), *sums = (const float*)vp(1), *w = (const float*)vp(2);
-    float *rows = (float*)vp(3), *gw = (float*)vp(4), *gb = (float*)vp(5);
-    const float* gsp = P.size() > 6 ? (const float*)vp(6) : nullptr;
-    int n = I[0], np_ = I[1], C = I[2];
+    need(8, 4, 3);
+    const float *part = (const float*)vp(0), *sums = (const float*)vp(1), *w = (const float*)vp(2),
+                *fa = (const float*)vp(3), *fc = (const float*)vp(4);
+    float *rows = (float*)vp(5), *gw = (float*)vp(6), *gb = (float*)vp(7);
+    const float* gsp = P.size() > 8 ? (const float*)vp(8) : nullptr;
+    int n = I[0], np_ = I[1], C = I[2], cs = I[3];
     check_msg(head_check(C));
+    if (cs != 0 && cs != C) throw std::invalid_argument("head_norm_coef: cstride 0 or C");
     float it = (float)F[0], bw = (float)F[1], gs = (float)F[2];
     return [=](hipStream_t s) {
-      return A->head_norm_coef_launch(part, n, np_, C, sums, w, it, bw, gs, gsp, rows, gw, gb, s);
+      return A->head_norm_coef_launch(part, n, np_, C, sums, w, fa, fc, cs, it, bw, gs, gsp, rows, gw, gb, s);
     };
   }
   if (kind == "head_norm_bwd") {

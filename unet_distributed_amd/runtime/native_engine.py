@@ -968,10 +968,12 @@ class NativeUNet:
                 self._hn_rows = self._stat_buf("hn:rows", Nb * self.C.hn_blocks_per_sample(Nb, Pb) * 2 * hc)
                 emit_generic("head_norm_coef",
                              lambda hc=hc: [_ptr(self._stat_bufs["hn:part"]), _ptr(self.sums),
-                                            self.master_ptr("Mask/kernel"), _ptr(self._hn_rows),
+                                            self.master_ptr("Mask/kernel"), _ptr(b["fa:" + self.head_in]),
+                                            _ptr(b["fc:" + self.head_in]), _ptr(self._hn_rows),
                                             self.grad_ptr("Mask/kernel"), self.grad_ptr("Mask/bias"),
                                             _ptr(self.loss_scale_dev)],
-                             [Nb, Pb, hc], [inv_total, self.bce_weight, 1.0], "bwd:Mask")
+                             [Nb, Pb, hc, 0 if spec.norm == "batch" else hc], [inv_total, self.bce_weight, 1.0],
+                             "bwd:Mask")
                 done("Mask")
             elif l.kind == "mask":
                 hc = self.tinfo[self.head_in][1]
