@@ -456,28 +456,51 @@ __global__ void __launch_bounds__(NT) gn_sample_kernel(const float* __restrict__
                                                        float* __restrict__ fa, float* __restrict__ fc,
                                                        float* __restrict__ ca, float* __restrict__ cb,
                                                        float* __restrict__ cc, float* __restrict__ contrib) {
-  extern __shared__ float S[];   // [2C] + [4][64] scratch
+  extern __shared__ float S[];   // [2C] + max([4][64], [4][G]) scratch + [2C] (mode 1)
   float* red = S + 2 * C;
   const int n = blockIdx.x, W = 2 * C;
-  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  // column sums over the sample's rps rows: passes of CH columns x RL row lanes (wide
+  // rows -- the coarse levels, few rows -- use all 256 threads on columns)
+  const int CH = W >= NT ? NT : 64, RL = NT / CH;
+  const int cl = threadIdx.x % CH, rl = threadIdx.x / CH;
   const float* base = rows + (size_t)n * rps * W;
-  for (int c0 = 0; c0 < W; c0 += 64) {
+  for (int c0 = 0; c0 < W; c0 += CH) {
     const int col = c0 + cl;
     float a[4] = {0.f, 0.f, 0.f, 0.f};
     if (col < W) {
       int r = rl;
-      for (; r + 12 < rps; r += 16)
+      for (; r + 3 * RL < rps; r += 4 * RL)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) a[k] += base[(size_t)(r + 4 * k) * W + col];
-      for (; r < rps; r += 4) a[0] += base[(size_t)r * W + col];
+        for (int k = 0; k < 4; ++k) a[k] += base[(size_t)(r + k * RL) * W + col];
+      for (; r < rps; r += RL) a[0] += base[(size_t)r * W + col];
     }
-    red[rl * 64 + cl] = (a[0] + a[1]) + (a[2] + a[3]);
+    red[rl * CH + cl] = (a[0] + a[1]) + (a[2] + a[3]);
     __syncthreads();
-    if (rl == 0 && col < W) S[col] = red[cl] + red[64 + cl] + red[128 + cl] + red[192 + cl];
+    if (rl == 0 && col < W) {
+      float sm = red[cl];
+      for (int k = 1; k < RL; ++k) sm += red[k * CH + cl];
+      S[col] = sm;
+    }
     __syncthreads();
   }
+  // per group (thread g): mean / rstd (mode 0) or the backward's M1 / M2 (mode 1) into
+  // LDS, then every channel's outputs in parallel (coalesced stores; a serial per-group
+  // loop over C / G channels with global loads made the level-5 finalize ~20x slower).
+  // Mode 1 first forms the per-channel terms gamma S1, gamma r (S2 - mu S1) in parallel.
   const int Cg = C / G;
   const float count = P * Cg;
+  float* gs = red;                                   // [G][2] (the row scratch is free now)
+  float* gs2 = red + 2 * G;                          // mode 1: [G][2] = mu, r
+  float* T = S + 2 * C + (4 * G > 4 * 64 ? 4 * G : 4 * 64);   // mode 1: [2][C]
+  if (mode == 1) {
+    for (int c = threadIdx.x; c < C; c += NT) {
+      const size_t k0 = (size_t)n * C + (c / Cg) * Cg;
+      const float mu = mean[k0], r = rstd[k0];
+      T[c] = gamma[c] * S[c];
+      T[C + c] = gamma[c] * (r * (S[C + c] - mu * S[c]));
+    }
+    __syncthreads();
+  }
   for (int g = threadIdx.x; g < G; g += NT) {
     if (mode == 0) {
       float s1 = 0.f, s2 = 0.f;
@@ -486,32 +509,37 @@ __global__ void __launch_bounds__(NT) gn_sample_kernel(const float* __restrict__
         s2 += S[C + c];
       }
       const float mu = s1 / count;
-      const float r = rsqrtf(fmaxf(s2 / count - mu * mu, 0.f) + eps);
-      for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
-        const size_t k = (size_t)n * C + c;
-        mean[k] = mu;
-        rstd[k] = r;
-        fa[k] = gamma[c] * r;
-        fc[k] = beta[c] - mu * gamma[c] * r;
-      }
+      gs[2 * g] = mu;
+      gs[2 * g + 1] = rsqrtf(fmaxf(s2 / count - mu * mu, 0.f) + eps);
     } else {
-      const float mu = mean[(size_t)n * C + g * Cg], r = rstd[(size_t)n * C + g * Cg];
       float M1 = 0.f, M2 = 0.f;
       for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
-        const float sgx = r * (S[C + c] - mu * S[c]);
-        M1 += gamma[c] * S[c];
-        M2 += gamma[c] * sgx;
-        contrib[((size_t)n * 2 + 0) * C + c] = S[c];
-        contrib[((size_t)n * 2 + 1) * C + c] = sgx;
+        M1 += T[c];
+        M2 += T[C + c];
       }
-      M1 /= count;
-      M2 /= count;
-      for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
-        const size_t k = (size_t)n * C + c;
-        ca[k] = gamma[c] * r;
-        cb[k] = -r * r * M2;
-        cc[k] = -r * M1 + r * r * mu * M2;
-      }
+      gs[2 * g] = M1 / count;
+      gs[2 * g + 1] = M2 / count;
+      gs2[2 * g] = mean[(size_t)n * C + g * Cg];
+      gs2[2 * g + 1] = rstd[(size_t)n * C + g * Cg];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += NT) {
+    const int g = c / Cg;
+    const size_t k = (size_t)n * C + c;
+    if (mode == 0) {
+      const float mu = gs[2 * g], r = gs[2 * g + 1];
+      mean[k] = mu;
+      rstd[k] = r;
+      fa[k] = gamma[c] * r;
+      fc[k] = beta[c] - mu * gamma[c] * r;
+    } else {
+      const float M1 = gs[2 * g], M2 = gs[2 * g + 1], mu = gs2[2 * g], r = gs2[2 * g + 1];
+      contrib[((size_t)n * 2 + 0) * C + c] = S[c];
+      contrib[((size_t)n * 2 + 1) * C + c] = r * (S[C + c] - mu * S[c]);
+      ca[k] = gamma[c] * r;
+      cb[k] = -r * r * M2;
+      cc[k] = -r * M1 + r * r * mu * M2;
     }
   }
 }
@@ -607,7 +635,7 @@ hipError_t bn_stats_launch(const float* rows, int R, int C, float count, int mod
 hipError_t gn_stats_launch(const float* rows, int N, int rps, int C, int G, int P, int mode, const float* gamma,
                            const float* beta, float eps, float* mean, float* rstd, float* fa, float* fc, float* ca,
                            float* cb, float* cc, float* dgamma, float* dbeta, float* work, hipStream_t s) {
-  const size_t lds = (2 * C + 4 * 64) * sizeof(float);
+  const size_t lds = (4 * C + (4 * G > 4 * 64 ? 4 * G : 4 * 64)) * sizeof(float);
   hipLaunchKernelGGL(gn_sample_kernel, dim3(N), dim3(NT), lds, s, rows, rps, C, G, (float)P, mode, gamma, beta, eps,
                      mean, rstd, fa, fc, ca, cb, cc, work);
   if (mode == 1) {
