@@ -204,6 +204,24 @@ def test_native_norm_step_matches_bf16_noise_floor(cuda_dev, norm):
     assert _cos(fn.grad, ft.grad) > 0.98
 
 
+@pytest.mark.parametrize("norm", ["batch", "group"])
+def test_norm_wgrad_operand_transform_matches_stored_activation(cuda_dev, monkeypatch, norm):
+    """UNET_NORM_XFORM_WG=1 (opt-in): the 'a' conv activations are never stored and the
+    consumer's weight gradient normalises the pre-norm z on load -- same loss sums and
+    gradients as the default (stored activation) up to the rounding of the coefficients."""
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("UNET_NORM_XFORM_WG", v)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, batch_size=4, img_size=64, in_channels=4, norm=norm)
+        assert bool(nb.engine._xf_wg) == (v == "1")
+        nb.fwd_bwd(x, y, seed=77)
+        torch.cuda.synchronize()
+        outs.append((nb.sums().cpu(), fn.grad.clone()))
+    (s0, g0), (s1, g1) = outs
+    assert torch.allclose(s0, s1, rtol=1e-4, atol=1e-2), (s0, s1)
+    assert _cos(g0, g1) > 0.9999
+
+
 @pytest.mark.parametrize("norm", ["none", "batch"])
 def test_hip_graph_replay_equals_eager(cuda_dev, norm):
     """Graph mode (captured fwd, per-bucket bwd segments, Adam reading its scalars from

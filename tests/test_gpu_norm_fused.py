@@ -461,3 +461,28 @@ def test_norm_head_loss_and_backward(cuda_dev, N, H, Ch, gn):
     assert abs(gb.item() - dl.sum().item()) <= 1e-3 * dl.abs().sum().item()
     ref_dz = ca.view(rows_c, 1, Ch) * g + cb.view(rows_c, 1, Ch) * zf + cc.view(rows_c, 1, Ch)
     assert (dz.float().view(N, P, Ch) - ref_dz).abs().max() <= 1e-2 * ref_dz.abs().max()
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,gn,splits", [(3, 128, 32, 32, False, 5), (2, 64, 64, 64, True, 3),
+                                                     (4, 32, 128, 128, False, 4), (2, 64, 64, 128, True, 7)])
+def test_wgrad_operand_normalised_on_load(cuda_dev, N, H, Cin, Cout, gn, splits):
+    """Window wgrad with the A-operand transform (WgradParams xform; opt-in in the engine,
+    UNET_NORM_XFORM_WG=1): a1 = pre-norm z and
+    y = relu(xa z + xb) formed in LDS gives the weight gradient of the materialised 16-bit
+    y (same operand values up to the reference's rounding of xa z + xb, same order)."""
+    from test_gpu_kernels import _wgrad
+    torch.manual_seed(55)
+    z = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
+    rows = N if gn else 1
+    fa = 0.5 + torch.rand(rows, Cin, device=cuda_dev)
+    fc = 0.3 * torch.randn(rows, Cin, device=cuda_dev)
+    view = (rows, 1, 1, Cin)
+    y = torch.clamp(fa.view(view).double() * z.double() + fc.view(view).double(), min=0).float().bfloat16()
+    dy = torch.randn(N, H, H, Cout, device=cuda_dev).bfloat16()
+    base = dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=Cin, b=ptr(dy), Nc=Cout, bias_mode=1)
+    g0, b0 = _wgrad(dict(base, a1=ptr(y)), splits, 9, Cin, Cin, Cout, 9 * Cin * Cout, bias_w=(splits, Cout))
+    g1, b1 = _wgrad(dict(base, a1=ptr(z), xform=1, xa=ptr(fa), xb=ptr(fc), xcs=Cin if gn else 0), splits, 9, Cin,
+                    Cin, Cout, 9 * Cin * Cout, bias_w=(splits, Cout))
+    torch.cuda.synchronize()
+    assert rel_err(g1, g0) < 1e-4, rel_err(g1, g0)
+    assert torch.equal(b0, b1)                      # bias: column sums of dy, untouched

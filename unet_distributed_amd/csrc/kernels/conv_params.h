@@ -126,6 +126,13 @@ struct WgradParams {
   int bias_mode;
   float* bias_slab;           // [splits][tap_groups][M or Nc] fp32
   int win;                    // 0 = row-window kernel when eligible, -1 = never (A/B tests)
+  // A-operand transform on load (2D row-window kernel, single source, rows 32..128 wide):
+  // a1 = pre-norm z, operand y = relu(xa z + xb) formed in LDS -- the normalised
+  // activation of an 'a' conv is then never stored (its consumer conv normalises on load
+  // too, conv_params.h xform 1).  xa / xb: [M1] (xcs = 0) or [N][M1] (xcs = M1).
+  int xform, xcs;
+  const float* xa;
+  const float* xb;
   // filled by the launcher
   int lqw, lqh, lqd;          // log2 of the pixel grid (power-of-two fast path)
   signed char tap_d[27], tap_h[27], tap_w[27];

@@ -507,7 +507,7 @@ hipError_t launch_wg(WgradParams p, hipStream_t s) {
 // GEO: 0 = 2D full rows, 1 = 2D segmented rows (Wf = p.QW > W), 2 = 3D (tap group =
 // depth tap); compile-time so the 2D full-row kernel carries no segment / depth state.
 enum { WGEO_2D = 0, WGEO_SEG = 1, WGEO_3D = 2 };
-template <int W, int QO, bool CONCAT, int GEO>
+template <int W, int QO, bool CONCAT, int GEO, bool XF = false>
 __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p) {
   constexpr int BMW = 256, R = BMW / W, HR = R + 2;
   constexpr int HWP = ((W + 2 + 15) / 16) * 16, IPR = HWP / 16, ROWB = HWP * 64;
@@ -647,6 +647,41 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
       }
     }
     __syncthreads();
+    if constexpr (XF) {
+      // A operand normalised on load: y = relu(xa z + xb) of the halo image in place.  A
+      // thread keeps the DMA lane role of its lane (slot lane >> 2, physical chunk lane & 3,
+      // logical chunk = physical ^ swizzle), so its 8 channels are fixed; padding slots
+      // keep the DMA's zeros (the activation's zero padding).
+      static_assert(GEO == WGEO_2D && !CONCAT && !ROWSWZ, "A transform: 2D single-source rows >= 16");
+      const int xsl = lane >> 2, xpc = lane & 3;
+      const int xlc = xpc ^ (((xsl >> 3) & 1) << 1);
+      const size_t crow = p.xcs ? (size_t)(g0 / H) * p.xcs : 0;
+      float xa[8], xb[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        xa[e] = p.xa[crow + ca0 + xlc * 8 + e];
+        xb[e] = p.xb[crow + ca0 + xlc * 8 + e];
+      }
+#pragma unroll
+      for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
+        const int k = wave + 4 * qq;
+        if (k < XI) {
+          const int hr = k / IPR, j = k - hr * IPR;
+          const int gr = g0 - 1 + hr;
+          const int col = 16 * j + xsl - 1;
+          const bool row_in = (hr > 0 || top_in) && (hr < R + 1 || bot_in);
+          if (row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W) {
+            char* a = Xs + k * 1024 + xsl * 64 + xpc * 16;
+            float v[8];
+            unpack8(*(const u32x4*)a, v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(xa[e], v[e], xb[e]), 0.f);
+            *(u32x4*)a = pack8(v);
+          }
+        }
+      }
+      __syncthreads();
+    }
     const char* Yq = Ys + qo * (BMW * 64);
     // (one column unit per wave: with two, the 128-wide QO = 2 case spills)
     if constexpr (UNITS_PATH) {
@@ -1205,6 +1240,12 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
 template <int W, int QO, int GEO>
 hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
   const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.KD * launch_splits(p);
+  if constexpr (GEO == WGEO_2D && W >= 32) {
+    if (p.xform) {
+      hipLaunchKernelGGL((wgrad_win_kernel<W, QO, false, GEO, true>), dim3(grid), dim3(NTHR), 0, s, p);
+      return hipGetLastError();
+    }
+  }
   if (p.M2 > 0)
     hipLaunchKernelGGL((wgrad_win_kernel<W, QO, true, GEO>), dim3(grid), dim3(NTHR), 0, s, p);
   else
@@ -1287,6 +1328,9 @@ const char* wgrad_check(const WgradParams& p) {
     if (p.M1 % 8 || p.M2 % 8) return "wgrad: channel split must be a multiple of 8";
     if (KT % c.NTAP) return "wgrad: taps not divisible by the tap group";
   }
+  if (p.xform && (!wgrad_win_eligible(p) || p.M2 != 0 || p.KD != 1 || p.QD != 1 ||
+                  (p.QW != 32 && p.QW != 64 && p.QW != 128) || !p.xa || !p.xb || (p.xcs != 0 && p.xcs != p.M1)))
+    return "wgrad: A transform needs a 2D single-source row-window wgrad, rows 32 / 64 / 128 wide";
   if (p.upA != 1 && p.upA != 2) return "wgrad: upA must be 1 or 2";
   if (p.splits < 1) return "wgrad: splits must be >= 1";
   if (p.split_lo < 0 || p.split_n < 0 || p.split_lo + launch_splits(p) > p.splits)

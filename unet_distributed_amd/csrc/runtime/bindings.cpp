@@ -152,6 +152,10 @@ WgradParams wgrad_params(const py::dict& d) {
   p.bias_mode = get<int>(d, "bias_mode", 0);
   p.bias_slab = (float*)getp(d, "bias_slab");
   p.win = get<int>(d, "win", 0);
+  p.xform = get<int>(d, "xform", 0);
+  p.xcs = get<int>(d, "xcs", 0);
+  p.xa = (const float*)getp(d, "xa");
+  p.xb = (const float*)getp(d, "xb");
   if (p.bias_mode && !p.bias_slab) throw std::invalid_argument("wgrad: bias_slab required");
   if (!p.a1 || !p.b || !p.slab) throw std::invalid_argument("wgrad: a1/b/slab required");
   check_msg(wgrad_check(p));

@@ -600,6 +600,9 @@ class NativeUNet:
                   nd_rate=self.spec.dropout if self.tinfo[tname][3] else 0.0, nd_salt=self._salt(tname))
         fused = self._fuse_stats(d2, "bst:" + tname, C, l.level)
         if fused is None:
+            if tname in self._xf_wg:     # the fallback masks with the (never stored) activation
+                raise RuntimeError("native engine: %s is normalised on load but its data gradient "
+                                   "cannot recompute the mask (unset UNET_NORM_XFORM_WG)" % tname)
             return
         d.clear()
         d.update(d2)
@@ -663,7 +666,8 @@ class NativeUNet:
         pre-norm z (conv_params.h xform 1); the conv also writes the activation."""
         b = self.bufs
         return dict(xform=1, xa=_ptr(b["fa:" + src]), xb=_ptr(b["fc:" + src]),
-                    xcs=0 if self.spec.norm == "batch" else self.tinfo[src][1], xout=_ptr(b[src]))
+                    xcs=0 if self.spec.norm == "batch" else self.tinfo[src][1],
+                    xout=None if src in self._xf_wg else _ptr(b[src]))
 
     def _plan_xforms(self):
         """Normalised activations whose only consumer is the next conv's first source
@@ -671,6 +675,12 @@ class NativeUNet:
         (UNET_NORM_XFORM=0 or bwd keeps the separate norm_apply pass).  Decided once, for
         the training and the evaluation plans alike."""
         self._xf_fwd = set()
+        # ... and, opt-in (UNET_NORM_XFORM_WG=1), whose consumer's weight gradient
+        # normalises its A operand on load too (2D row-window wgrad, rows 32..128 wide), so
+        # the activation is never stored: measured -1.3 % BN / -1.5 % GN b1024 (the
+        # per-window transform pass and its barrier cost the side-stream weight gradients
+        # more than the skipped activation stores save)
+        self._xf_wg = set()
         if self.spec.norm == "none" or self.dims != 2 or os.environ.get("UNET_NORM_XFORM", "fwd") not in ("1", "fwd"):
             return
         users: Dict[str, list] = {}
@@ -699,6 +709,9 @@ class NativeUNet:
             except ValueError:
                 continue
             self._xf_fwd.add(l.name)
+            if (self.sdims(l2.level)[2] in (32, 64, 128) and self.wgrad_win >= 0
+                    and os.environ.get("UNET_NORM_XFORM_WG", "0") == "1"):
+                self._xf_wg.add(l.name)
 
     def _fwd_streams(self, train):
         """2: the training forward runs as two half-batch chunks on two HIP streams, the
@@ -1009,6 +1022,10 @@ class NativeUNet:
                           AW=self.sdims(l.level)[2], KD=3 if self.dims == 3 else 1, KH=3, KW=3, stride=1,
                           pad=1, upA=upA, a1=_ptr(a1), a2=_ptr(b[skip]) if skip else None,
                           b=_ptr(dy))
+                if src1 in self._xf_wg:
+                    # the activation was never stored: normalise its pre-norm z on load
+                    kd.update(a1=_ptr(b["z:" + src1]), xform=1, xa=_ptr(b["fa:" + src1]),
+                              xb=_ptr(b["fc:" + src1]), xcs=0 if spec.norm == "batch" else c1)
                 wspec = dict(lname=l.name, kd=kd, M1=c1, M2=c2, Nc=l.cout, KT=KT3, Q=Q,
                              QD=self.sdims(l.level)[0], QH=self.sdims(l.level)[1],
                              QW=self.sdims(l.level)[2], upA=upA,
