@@ -46,14 +46,15 @@ def main():
         ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
                    r.get(qk, "0") if qk else "0"))
     ks.sort()
-    ends = [i for i, k in enumerate(ks) if k[2].startswith("adam_pack")]
+    ends = [i for i, k in enumerate(ks) if "adam_pack" in k[2]]
     if len(ends) < 2:
         print("need two adam_pack launches in the trace")
         return
     step = ks[ends[-2] + 1: ends[-1] + 1]
     t0 = step[0][0]
     t1 = max(k[1] for k in step)
-    fwd_end = next((k[1] for k in step if k[2].startswith(("head_finish", "head_fwd"))), None)
+    fwd_end = next((k[1] for k in step if k[2].startswith(("head_finish", "head_fwd")) or "norm_head_loss" in k[2]),
+                   None)
     span = (t1 - t0) / 1e6
     busy, gaps = union([(k[0], k[1]) for k in step])
     ksum = sum(k[1] - k[0] for k in step) / 1e6
