@@ -486,3 +486,32 @@ def test_wgrad_operand_normalised_on_load(cuda_dev, N, H, Cin, Cout, gn, splits)
     torch.cuda.synchronize()
     assert rel_err(g1, g0) < 1e-4, rel_err(g1, g0)
     assert torch.equal(b0, b1)                      # bias: column sums of dy, untouched
+
+
+@pytest.mark.parametrize("N,H,Cpad,gn,splits", [(2, 128, 4, False, 3), (3, 64, 8, True, 5), (4, 32, 4, True, 2)])
+def test_first_layer_wgrad_dz_on_load(cuda_dev, N, H, Cpad, gn, splits):
+    """First-layer window wgrad with the B transform (WgradParams xform 2): b = g and
+    dz = xa g + xb z + xc formed in LDS gives the weight / bias gradient of the
+    materialised dz (the norm backward's dz of the first layer is never stored)."""
+    from test_gpu_kernels import _wgrad
+    torch.manual_seed(56)
+    Co = 32
+    x = torch.randn(N, H, H, Cpad, device=cuda_dev).bfloat16()
+    g = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
+    z = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
+    rows = N if gn else 1
+    ca = 0.5 + torch.rand(rows, Co, device=cuda_dev)
+    cb = 0.2 * torch.randn(rows, Co, device=cuda_dev)
+    cc = 0.1 * torch.randn(rows, Co, device=cuda_dev)
+    v = lambda t: t.view(rows, 1, 1, Co).double()
+    dz = (v(ca) * g.double() + (v(cb) * z.double() + v(cc))).float().bfloat16()
+    BM = C().wgrad_pick(Cpad, 0, Co, 9, QW=H, win=0)[0]
+    Mtot = (9 * Cpad + BM - 1) // BM * BM
+    base = dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=Cpad, a1=ptr(x), Nc=Co, bias_mode=1, win=0)
+    kw = dict(bias_w=(splits, Co), rows=(Cpad, Cpad))
+    g0, b0 = _wgrad(dict(base, b=ptr(dz)), splits, 1, Mtot, 9 * Cpad, Co, 9 * Cpad * Co, **kw)
+    g1, b1 = _wgrad(dict(base, b=ptr(g), xform=2, xa=ptr(ca), xb=ptr(cb), xc=ptr(cc), xz=ptr(z),
+                         xcs=Co if gn else 0), splits, 1, Mtot, 9 * Cpad, Co, 9 * Cpad * Co, **kw)
+    torch.cuda.synchronize()
+    assert rel_err(g1, g0) < 1e-2, rel_err(g1, g0)
+    assert rel_err(b1, b0) < 1e-2, rel_err(b1, b0)

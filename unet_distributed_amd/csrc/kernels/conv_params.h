@@ -130,9 +130,15 @@ struct WgradParams {
   // a1 = pre-norm z, operand y = relu(xa z + xb) formed in LDS -- the normalised
   // activation of an 'a' conv is then never stored (its consumer conv normalises on load
   // too, conv_params.h xform 1).  xa / xb: [M1] (xcs = 0) or [N][M1] (xcs = M1).
+  // xform 2 (first-layer window wgrad): b = g (gradient of the normalised output) and the
+  // B operand dz = xa g + xb z + xc (z = xz, the pre-norm output) is formed in LDS -- the
+  // norm backward's dz of the first layer, read by nothing else, is never materialised
+  // (coefficients [Nc] or [N][Nc], xcs = Nc).
   int xform, xcs;
   const float* xa;
   const float* xb;
+  const float* xc;
+  const void* xz;
   // filled by the launcher
   int lqw, lqh, lqd;          // log2 of the pixel grid (power-of-two fast path)
   signed char tap_d[27], tap_h[27], tap_w[27];

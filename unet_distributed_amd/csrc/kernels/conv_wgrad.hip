@@ -903,7 +903,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
 // supplies pixel q's slot for tap 4mt + pp (CIN 4) or tap 2mt + pp/2 and channel half
 // pp & 1 (CIN 8), so the transpose hands lane i the (tap, channel) row 16 mt + i; taps
 // past the ninth and taps whose input row leaves the pixel's image address slot 0.
-template <int W, int CIN>
+template <int W, int CIN, bool XF = false>
 __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams p) {
   constexpr int BMW = 256, R = BMW / W, HR = R + 2, RS = W + 4, SB = 2 * CIN, ROWB = RS * SB;
   constexpr int CPR = ROWB / 16;
@@ -958,9 +958,29 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
     return __builtin_bit_cast(h16x8, v);
   };
 
+  // XF: this lane's B-transform coefficients (its logical chunk lchunk is fixed)
+  float xa[8], xb[8], xc[8];
   for (int win = w_begin; win < w_end; ++win) {
     const int g0 = win * R;
     __syncthreads();
+    u32x4 xzv[(YI + 3) / 4];
+    if constexpr (XF) {
+      // the pre-norm z of this lane's dY chunks, loaded beside the DMA
+      const size_t crow = p.xcs ? (size_t)(g0 / H) * p.xcs : 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        xa[e] = p.xa[crow + co0 + lchunk * 8 + e];
+        xb[e] = p.xb[crow + co0 + lchunk * 8 + e];
+        xc[e] = p.xc[crow + co0 + lchunk * 8 + e];
+      }
+#pragma unroll
+      for (int qq = 0; qq < (YI + 3) / 4; ++qq) {
+        const int k = wave + 4 * qq;
+        const int pix = g0 * W + 16 * k + lslot;
+        if (k < YI && pix < Mq)
+          xzv[qq] = *(const u32x4*)((const h16*)p.xz + (size_t)pix * p.Nc + co0 + lchunk * 8);
+      }
+    }
 #pragma unroll
     for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
       const int k = wave + 4 * qq;
@@ -986,6 +1006,24 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
       }
     }
     __syncthreads();
+    if constexpr (XF) {
+      // B operand dz = xa g + xb z + xc formed in place (each lane rewrites the chunk its
+      // own DMA lane role wrote); pixels past the tensor keep the DMA's zeros
+#pragma unroll
+      for (int qq = 0; qq < (YI + 3) / 4; ++qq) {
+        const int k = wave + 4 * qq;
+        if (k < YI && g0 * W + 16 * k + lslot < Mq) {
+          char* a = Ys + k * 1024 + lslot * 64 + (lane & 3) * 16;
+          float gv[8], zv[8];
+          unpack8(*(const u32x4*)a, gv);
+          unpack8(xzv[qq], zv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) gv[e] = fmaf(xa[e], gv[e], fmaf(xb[e], zv[e], xc[e]));
+          *(u32x4*)a = pack8(gv);
+        }
+      }
+      __syncthreads();
+    }
 #pragma unroll 1
     for (int kk = wave; kk < KS; kk += 4) {
       const int px0 = kk * 32;
@@ -1063,6 +1101,15 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
 template <int CIN>
 hipError_t launch_wgrad_win_first(const WgradParams& p, hipStream_t s) {
   const int grid = (p.Nc / 32) * launch_splits(p);
+  if (p.xform == 2) {         // dz formed on load (norm backward of the first layer)
+    switch (p.QW) {
+      case 16: hipLaunchKernelGGL((wgrad_win_first_kernel<16, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      case 32: hipLaunchKernelGGL((wgrad_win_first_kernel<32, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      case 64: hipLaunchKernelGGL((wgrad_win_first_kernel<64, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      default: hipLaunchKernelGGL((wgrad_win_first_kernel<128, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    }
+    return hipGetLastError();
+  }
   switch (p.QW) {
     case 16: hipLaunchKernelGGL((wgrad_win_first_kernel<16, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
     case 32: hipLaunchKernelGGL((wgrad_win_first_kernel<32, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
@@ -1241,7 +1288,7 @@ template <int W, int QO, int GEO>
 hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
   const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.KD * launch_splits(p);
   if constexpr (GEO == WGEO_2D && W >= 32) {
-    if (p.xform) {
+    if (p.xform == 1) {
       hipLaunchKernelGGL((wgrad_win_kernel<W, QO, false, GEO, true>), dim3(grid), dim3(NTHR), 0, s, p);
       return hipGetLastError();
     }
@@ -1328,7 +1375,10 @@ const char* wgrad_check(const WgradParams& p) {
     if (p.M1 % 8 || p.M2 % 8) return "wgrad: channel split must be a multiple of 8";
     if (KT % c.NTAP) return "wgrad: taps not divisible by the tap group";
   }
-  if (p.xform && (!wgrad_win_eligible(p) || p.M2 != 0 || p.KD != 1 || p.QD != 1 ||
+  if (p.xform == 2 && (!wgrad_win_first_eligible(p) || !p.xa || !p.xb || !p.xc || !p.xz ||
+                       (p.xcs != 0 && p.xcs != p.Nc) || (p.xcs && p.QH % (256 / p.QW))))
+    return "wgrad: B transform (dz on load) needs the first-layer window wgrad";
+  if (p.xform == 1 && (!wgrad_win_eligible(p) || p.M2 != 0 || p.KD != 1 || p.QD != 1 ||
                   (p.QW != 32 && p.QW != 64 && p.QW != 128) || !p.xa || !p.xb || (p.xcs != 0 && p.xcs != p.M1)))
     return "wgrad: A transform needs a 2D single-source row-window wgrad, rows 32 / 64 / 128 wide";
   if (p.upA != 1 && p.upA != 2) return "wgrad: upA must be 1 or 2";

@@ -156,6 +156,8 @@ WgradParams wgrad_params(const py::dict& d) {
   p.xcs = get<int>(d, "xcs", 0);
   p.xa = (const float*)getp(d, "xa");
   p.xb = (const float*)getp(d, "xb");
+  p.xc = (const float*)getp(d, "xc");
+  p.xz = getp(d, "xz");
   if (p.bias_mode && !p.bias_slab) throw std::invalid_argument("wgrad: bias_slab required");
   if (!p.a1 || !p.b || !p.slab) throw std::invalid_argument("wgrad: a1/b/slab required");
   check_msg(wgrad_check(p));

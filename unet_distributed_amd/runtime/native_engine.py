@@ -1005,11 +1005,19 @@ class NativeUNet:
                 c2 = self.tinfo[skip][1] if skip else 0
                 dy = b["d:" + l.name]
                 xf_bwd = None
+                first_xf = None
                 if spec.norm != "none":
                     hn = self._norm_head_loss and l.name == self.head_in
                     xf_bwd = self._xf_bwd_fields(l) if not (first or hn) else None
-                    ops.extend(self._norm_bwd_ops(l, apply=xf_bwd is None))
-                    dy = b["dz:" + l.name]
+                    if (first and self.dims == 2 and self.img in (16, 32, 64, 128) and self.cpad in (4, 8)
+                            and self.wgrad_win >= 0 and os.environ.get("UNET_NORM_FIRST_XF", "1") != "0"):
+                        # the first layer's dz is read only by its weight gradient: that kernel
+                        # forms dz = ca g + cb z + cc on load (no norm_bwd_apply pass)
+                        first_xf = dict(xform=2, xa=_ptr(b["ca:" + l.name]), xb=_ptr(b["cb:" + l.name]),
+                                        xc=_ptr(b["cc:" + l.name]), xz=_ptr(b["z:" + l.name]),
+                                        xcs=0 if spec.norm == "batch" else l.cout)
+                    ops.extend(self._norm_bwd_ops(l, apply=xf_bwd is None and first_xf is None))
+                    dy = b["dz:" + l.name] if first_xf is None else b["d:" + l.name]
                 wg_at = len(ops)
                 Q = self.npix(l.level)
                 # --- weight + bias gradient (fused column sums); the upsampling decoder's
@@ -1022,6 +1030,8 @@ class NativeUNet:
                           AW=self.sdims(l.level)[2], KD=3 if self.dims == 3 else 1, KH=3, KW=3, stride=1,
                           pad=1, upA=upA, a1=_ptr(a1), a2=_ptr(b[skip]) if skip else None,
                           b=_ptr(dy))
+                if first_xf is not None:
+                    kd.update(first_xf)
                 if src1 in self._xf_wg:
                     # the activation was never stored: normalise its pre-norm z on load
                     kd.update(a1=_ptr(b["z:" + src1]), xform=1, xa=_ptr(b["fa:" + src1]),
