@@ -204,16 +204,22 @@ def test_native_norm_step_matches_bf16_noise_floor(cuda_dev, norm):
     assert _cos(fn.grad, ft.grad) > 0.98
 
 
-@pytest.mark.parametrize("norm", ["batch", "group"])
-def test_norm_wgrad_operand_transform_matches_stored_activation(cuda_dev, monkeypatch, norm):
-    """UNET_NORM_XFORM_WG=1 (opt-in): the 'a' conv activations are never stored and the
-    consumer's weight gradient normalises the pre-norm z on load -- same loss sums and
-    gradients as the default (stored activation) up to the rounding of the coefficients."""
+@pytest.mark.parametrize("norm,knob,img", [("batch", "UNET_NORM_XFORM_WG", 64), ("group", "UNET_NORM_XFORM_WG", 64),
+                                            ("batch", "UNET_NORM_L1_XF", 128), ("group", "UNET_NORM_L1_XF", 128)])
+def test_norm_wgrad_operand_transform_matches_stored_activation(cuda_dev, monkeypatch, norm, knob, img):
+    """Opt-in operand transforms of the norm backward / forward, against the default path
+    (same loss sums and gradients up to the rounding of the coefficients):
+    UNET_NORM_XFORM_WG=1 -- the 'a' conv activations are never stored and the consumer's
+    weight gradient normalises the pre-norm z on load; UNET_NORM_L1_XF=1 -- level-1 data
+    and weight gradients (incl. the deferred skip half) form dz = ca g + cb z + cc on load."""
     outs = []
     for v in ("0", "1"):
-        monkeypatch.setenv("UNET_NORM_XFORM_WG", v)
-        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, batch_size=4, img_size=64, in_channels=4, norm=norm)
-        assert bool(nb.engine._xf_wg) == (v == "1")
+        monkeypatch.setenv(knob, v)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, batch_size=2, img_size=img, in_channels=4, norm=norm)
+        if knob == "UNET_NORM_XFORM_WG":
+            assert bool(nb.engine._xf_wg) == (v == "1")
+        else:
+            assert ("norm_bwd:conv1b" in nb.engine.plan.names()) == (v == "0")
         nb.fwd_bwd(x, y, seed=77)
         torch.cuda.synchronize()
         outs.append((nb.sums().cpu(), fn.grad.clone()))

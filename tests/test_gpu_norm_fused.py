@@ -515,3 +515,33 @@ def test_first_layer_wgrad_dz_on_load(cuda_dev, N, H, Cpad, gn, splits):
     torch.cuda.synchronize()
     assert rel_err(g1, g0) < 1e-2, rel_err(g1, g0)
     assert rel_err(b1, b0) < 1e-2, rel_err(b1, b0)
+
+
+@pytest.mark.parametrize("N,C1,C2,gn,splits", [(2, 32, 0, False, 3), (2, 32, 32, True, 5)])
+def test_window_wgrad_dz_on_load(cuda_dev, N, C1, C2, gn, splits):
+    """128-wide 32-channel window wgrad with the B transform (WgradParams xform 2, the
+    level-1 path of UNET_NORM_L1_XF=1): b = g and dz = xa g + xb z + xc formed in LDS gives
+    the weight / bias gradient of the materialised dz (concat A sources included)."""
+    from test_gpu_kernels import _wgrad
+    torch.manual_seed(57)
+    H, Co = 128, 32
+    a = torch.relu(torch.randn(N, H, H, C1, device=cuda_dev)).bfloat16()
+    a2 = torch.relu(torch.randn(N, H, H, max(C2, 1), device=cuda_dev)).bfloat16()
+    g = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
+    z = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
+    rows = N if gn else 1
+    ca = 0.5 + torch.rand(rows, Co, device=cuda_dev)
+    cb = 0.2 * torch.randn(rows, Co, device=cuda_dev)
+    cc = 0.1 * torch.randn(rows, Co, device=cuda_dev)
+    v = lambda t: t.view(rows, 1, 1, Co).double()
+    dz = (v(ca) * g.double() + (v(cb) * z.double() + v(cc))).float().bfloat16()
+    Mt = C1 + C2
+    base = dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=C1, M2=C2, a1=ptr(a),
+                a2=ptr(a2) if C2 else None, Nc=Co, bias_mode=1, win=0)
+    kw = dict(bias_w=(splits, Co))
+    g0, b0 = _wgrad(dict(base, b=ptr(dz)), splits, 9, Mt, Mt, Co, 9 * Mt * Co, **kw)
+    g1, b1 = _wgrad(dict(base, b=ptr(g), xform=2, xa=ptr(ca), xb=ptr(cb), xc=ptr(cc), xz=ptr(z),
+                         xcs=Co if gn else 0), splits, 9, Mt, Mt, Co, 9 * Mt * Co, **kw)
+    torch.cuda.synchronize()
+    assert rel_err(g1, g0) < 1e-2, rel_err(g1, g0)
+    assert rel_err(b1, b0) < 1e-2, rel_err(b1, b0)

@@ -507,7 +507,7 @@ hipError_t launch_wg(WgradParams p, hipStream_t s) {
 // GEO: 0 = 2D full rows, 1 = 2D segmented rows (Wf = p.QW > W), 2 = 3D (tap group =
 // depth tap); compile-time so the 2D full-row kernel carries no segment / depth state.
 enum { WGEO_2D = 0, WGEO_SEG = 1, WGEO_3D = 2 };
-template <int W, int QO, bool CONCAT, int GEO, bool XF = false>
+template <int W, int QO, bool CONCAT, int GEO, int XF = 0>
 __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p) {
   constexpr int BMW = 256, R = BMW / W, HR = R + 2;
   constexpr int HWP = ((W + 2 + 15) / 16) * 16, IPR = HWP / 16, ROWB = HWP * 64;
@@ -633,6 +633,27 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
                                                  off, 0, 0, 0);
       }
     }
+    // XF 2 (B transform, QO = 1, 2D full rows): the pre-norm z of this lane's dY chunks,
+    // loaded beside the DMA; dz = xa g + xb z + xc is formed in LDS below
+    u32x4 xzv[XF == 2 ? (YI + 3) / 4 : 1];
+    float bxa[8], bxb[8], bxc[8];
+    if constexpr (XF == 2) {
+      static_assert(QO == 1 && GEO == WGEO_2D, "B transform: one 32-channel dY image, 2D full rows");
+      const size_t crow = p.xcs ? (size_t)(g0 / H) * p.xcs : 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        bxa[e] = p.xa[crow + co0 + lchunk * 8 + e];
+        bxb[e] = p.xb[crow + co0 + lchunk * 8 + e];
+        bxc[e] = p.xc[crow + co0 + lchunk * 8 + e];
+      }
+#pragma unroll
+      for (int qq = 0; qq < (YI + 3) / 4; ++qq) {
+        const int k = wave + 4 * qq;
+        const int pix = g0 * W + k * 16 + lslot;
+        if (k < YI && pix < Mq)
+          xzv[qq] = *(const u32x4*)((const h16*)p.xz + (size_t)pix * p.Nc + co0 + lchunk * 8);
+      }
+    }
 #pragma unroll
     for (int qq = 0; qq < (YI + 3) / 4; ++qq) {
       const int k = wave + 4 * qq;
@@ -647,7 +668,23 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
       }
     }
     __syncthreads();
-    if constexpr (XF) {
+    if constexpr (XF == 2) {
+#pragma unroll
+      for (int qq = 0; qq < (YI + 3) / 4; ++qq) {
+        const int k = wave + 4 * qq;
+        if (k < YI && g0 * W + k * 16 + lslot < Mq) {
+          char* a = Ys + k * 1024 + lslot * 64 + (lane & 3) * 16;
+          float gv[8], zv[8];
+          unpack8(*(const u32x4*)a, gv);
+          unpack8(xzv[qq], zv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) gv[e] = fmaf(bxa[e], gv[e], fmaf(bxb[e], zv[e], bxc[e]));
+          *(u32x4*)a = pack8(gv);
+        }
+      }
+      __syncthreads();
+    }
+    if constexpr (XF == 1) {
       // A operand normalised on load: y = relu(xa z + xb) of the halo image in place.  A
       // thread keeps the DMA lane role of its lane (slot lane >> 2, physical chunk lane & 3,
       // logical chunk = physical ^ swizzle), so its 8 channels are fixed; padding slots
@@ -1289,7 +1326,16 @@ hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
   const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.KD * launch_splits(p);
   if constexpr (GEO == WGEO_2D && W >= 32) {
     if (p.xform == 1) {
-      hipLaunchKernelGGL((wgrad_win_kernel<W, QO, false, GEO, true>), dim3(grid), dim3(NTHR), 0, s, p);
+      hipLaunchKernelGGL((wgrad_win_kernel<W, QO, false, GEO, 1>), dim3(grid), dim3(NTHR), 0, s, p);
+      return hipGetLastError();
+    }
+  }
+  if constexpr (GEO == WGEO_2D && W == 128 && QO == 1) {
+    if (p.xform == 2) {
+      if (p.M2 > 0)
+        hipLaunchKernelGGL((wgrad_win_kernel<W, QO, true, GEO, 2>), dim3(grid), dim3(NTHR), 0, s, p);
+      else
+        hipLaunchKernelGGL((wgrad_win_kernel<W, QO, false, GEO, 2>), dim3(grid), dim3(NTHR), 0, s, p);
       return hipGetLastError();
     }
   }
@@ -1375,9 +1421,11 @@ const char* wgrad_check(const WgradParams& p) {
     if (p.M1 % 8 || p.M2 % 8) return "wgrad: channel split must be a multiple of 8";
     if (KT % c.NTAP) return "wgrad: taps not divisible by the tap group";
   }
-  if (p.xform == 2 && (!wgrad_win_first_eligible(p) || !p.xa || !p.xb || !p.xc || !p.xz ||
-                       (p.xcs != 0 && p.xcs != p.Nc) || (p.xcs && p.QH % (256 / p.QW))))
-    return "wgrad: B transform (dz on load) needs the first-layer window wgrad";
+  if (p.xform == 2 && ((!wgrad_win_first_eligible(p) && !(wgrad_win_eligible(p) && p.QW == 128 && p.QD == 1 &&
+                                                          p.KD == 1 && p.Nc % 64 != 0)) ||
+                       !p.xa || !p.xb || !p.xc || !p.xz || (p.xcs != 0 && p.xcs != p.Nc) ||
+                       (p.xcs && p.QH % (256 / p.QW))))
+    return "wgrad: B transform (dz on load) needs the first-layer or a 128-wide 32-channel window wgrad";
   if (p.xform == 1 && (!wgrad_win_eligible(p) || p.M2 != 0 || p.KD != 1 || p.QD != 1 ||
                   (p.QW != 32 && p.QW != 64 && p.QW != 128) || !p.xa || !p.xb || (p.xcs != 0 && p.xcs != p.M1)))
     return "wgrad: A transform needs a 2D single-source row-window wgrad, rows 32 / 64 / 128 wide";

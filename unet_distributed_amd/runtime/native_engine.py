@@ -661,6 +661,34 @@ class NativeUNet:
             return None
         return f
 
+    def _l1_xf_fields(self, l, first, hn):
+        """Level-1 norm layers (32 channels, 128-wide rows; not the first layer or the head
+        input, which have their own paths): the data gradient AND the window weight
+        gradient both form dz = ca g + cb z + cc on load, so dz is never stored and the
+        norm_bwd_apply pass is gone (UNET_NORM_L1_XF=1, opt-in: measured -1.2 % BN / -0.7 %
+        GN at b1024 -- the level-1 dgrads are VALU-bound and pay for the second operand),
+        or None."""
+        if (first or hn or self.spec.norm == "none" or self.dims != 2 or self.sdims(l.level)[2] != 128
+                or l.cout != 32 or self.wgrad_win < 0 or os.environ.get("UNET_NORM_L1_XF", "0") != "1"):
+            return None
+        f = self._xf_bwd_fields_any(l)
+        if f is None:
+            return None
+        return dict(f, xout=None)
+
+    def _xf_bwd_fields_any(self, l):
+        b = self.bufs
+        f = dict(xform=2, xa=_ptr(b["ca:" + l.name]), xb=_ptr(b["cb:" + l.name]), xc=_ptr(b["cc:" + l.name]),
+                 xz=_ptr(b["z:" + l.name]), xcs=0 if self.spec.norm == "batch" else l.cout)
+        d = self._conv_common(l.level, 3, 1, 1)
+        d.update(C1=l.cout, src1=_ptr(b["d:" + l.name]), wgt=self.wptr(l.name, "dg"), Cout=l.cin, relu=0,
+                 dst1=_ptr(b["dz:" + l.name]), **f)
+        try:
+            self.C.conv_fwd_grid(d)
+        except ValueError:
+            return None
+        return f
+
     def _xf_fwd_fields(self, src):
         """Operand-transform fields of a conv reading normalised activation `src` as the
         pre-norm z (conv_params.h xform 1); the conv also writes the activation."""
@@ -1005,10 +1033,11 @@ class NativeUNet:
                 c2 = self.tinfo[skip][1] if skip else 0
                 dy = b["d:" + l.name]
                 xf_bwd = None
-                first_xf = None
+                first_xf = l1_xf = None
                 if spec.norm != "none":
                     hn = self._norm_head_loss and l.name == self.head_in
-                    xf_bwd = self._xf_bwd_fields(l) if not (first or hn) else None
+                    l1_xf = self._l1_xf_fields(l, first, hn)
+                    xf_bwd = self._xf_bwd_fields(l) if not (first or hn or l1_xf) else None
                     if (first and self.dims == 2 and self.img in (16, 32, 64, 128) and self.cpad in (4, 8)
                             and self.wgrad_win >= 0 and os.environ.get("UNET_NORM_FIRST_XF", "1") != "0"):
                         # the first layer's dz is read only by its weight gradient: that kernel
@@ -1016,8 +1045,8 @@ class NativeUNet:
                         first_xf = dict(xform=2, xa=_ptr(b["ca:" + l.name]), xb=_ptr(b["cb:" + l.name]),
                                         xc=_ptr(b["cc:" + l.name]), xz=_ptr(b["z:" + l.name]),
                                         xcs=0 if spec.norm == "batch" else l.cout)
-                    ops.extend(self._norm_bwd_ops(l, apply=xf_bwd is None and first_xf is None))
-                    dy = b["dz:" + l.name] if first_xf is None else b["d:" + l.name]
+                    ops.extend(self._norm_bwd_ops(l, apply=xf_bwd is None and first_xf is None and l1_xf is None))
+                    dy = b["dz:" + l.name] if (first_xf is None and l1_xf is None) else b["d:" + l.name]
                 wg_at = len(ops)
                 Q = self.npix(l.level)
                 # --- weight + bias gradient (fused column sums); the upsampling decoder's
@@ -1032,6 +1061,8 @@ class NativeUNet:
                           b=_ptr(dy))
                 if first_xf is not None:
                     kd.update(first_xf)
+                if l1_xf is not None:
+                    kd.update({k: v for k, v in l1_xf.items() if k != "xout"})
                 if src1 in self._xf_wg:
                     # the activation was never stored: normalise its pre-norm z on load
                     kd.update(a1=_ptr(b["z:" + src1]), xform=1, xa=_ptr(b["fa:" + src1]),
@@ -1054,7 +1085,7 @@ class NativeUNet:
                     emit_wgrad(wspec)
                 # --- data gradient
                 if not first:
-                    def mk(l=l, src1=src1, up1=up1, skip=skip, c1=c1, c2=c2, dy=dy):
+                    def mk(l=l, src1=src1, up1=up1, skip=skip, c1=c1, c2=c2, dy=dy, l1_xf=l1_xf):
                         d = self._conv_common(l.level, 3, 1, 1)
                         d.update(name="dgrad:" + l.name, C1=l.cout, src1=_ptr(dy),
                                  wgt=self.wptr(l.name, "dg"), Cout=l.cin, relu=0)
@@ -1073,7 +1104,13 @@ class NativeUNet:
                             if dsk is not None:
                                 # the skip half runs later, fused with the pool backward
                                 d.update(Cout=c1, dst1=_ptr(dst1), D1=c1)
+                                if l1_xf is not None:      # it reads g too: dz formed on load
+                                    dsk[1].update(l1_xf, src1=_ptr(dy))
+                                    self.C.conv_fwd_grid(dsk[1])
                                 self._deferred_skip[dsk[0]] = dsk[1]
+                            elif l1_xf is not None:
+                                raise RuntimeError("UNET_NORM_L1_XF: %s's skip-half data gradient is not deferred"
+                                                   % l.name)
                             else:
                                 m2, mb = self._relu_mask(skip)
                                 d.update(dst1=_ptr(dst1), D1=c1, dst2=_ptr(b["dskip:" + skip]),
@@ -1082,6 +1119,10 @@ class NativeUNet:
                             self._rev_order(d, "g:" + l.name, "g:" + src1)
                         return d
                     dd_ = mk()                 # built now: it decides the fused norm backward
+                    if l1_xf is not None:
+                        # dz formed on load here and (independently) by the weight gradient
+                        dd_.update(l1_xf, src1=_ptr(b["d:" + l.name]))
+                        self.C.conv_fwd_grid(dd_)
                     if xf_bwd is not None:
                         # dz formed on load by this dgrad (which also stores it): the weight
                         # gradient reading dz moves behind it
