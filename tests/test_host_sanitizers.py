@@ -52,8 +52,11 @@ def test_host_runtime_tsan():
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not available")
 def test_conv_shape_validation_asan_ubsan():
-    """~1 minute on the first run (hipcc also compiles the gfx950 device code); cached."""
+    """~1.5 minutes on the first run (hipcc also compiles the gfx950 device code, which this
+    host-side check never launches: unoptimised and without debug info -- at -O1 -g it took
+    ~8 minutes); cached."""
     _build_and_run("shapes", ["/opt/rocm/bin/hipcc", "-std=c++17", "-O1", "-g", "--offload-arch=gfx950",
+                              "-Xarch_device", "-g0", "-Xarch_device", "-O0",
                               "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
                               "-DUNET_WITH_SHAPE_CHECKS", "-msse4.2", "-pthread",
                               "-I" + os.path.join(CSRC, "runtime"), "-I" + os.path.join(CSRC, "kernels")],
