@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--hip_graph", type=int, default=1,
                    help="replay fwd / bwd segments / Adam as captured HIP graphs (0: eager launches)")
     p.add_argument("--profile_dir", default="")
+    p.add_argument("--dist_force", type=int, default=0,
+                   help="1: create the process group and issue the bucket collectives even at one rank "
+                        "(exercises the RCCL path on a 1-GPU box; the timed step then includes them)")
     p.add_argument("--comm_diag", type=int, default=1,
                    help="N > 1: after the timed steps, measure per-bucket allreduce time and the exposed "
                         "communication (A/B against compute-only and non-overlapped steps)")
@@ -82,7 +85,7 @@ def comm_diagnostics(a, ctx, flat, bounds, sync_overlap, step_fn, dev):
     from unet_distributed_amd.parallel.grad_sync import GradSync
     out = {"backend": ctx.backend or "none", "world_size": ctx.world_size,
            "buckets_mb": [round(4.0 * (b - (bounds[i - 1] if i else 0)) / 2 ** 20, 3) for i, b in enumerate(bounds)]}
-    if ctx.world_size == 1 or not a.comm_diag:
+    if (ctx.world_size == 1 and not a.dist_force) or not ctx.initialized or not a.comm_diag:
         return out
     per = []
     for i in range(len(bounds)):
@@ -126,7 +129,7 @@ def comm_diagnostics(a, ctx, flat, bounds, sync_overlap, step_fn, dev):
 
     t_none = timed(_NoComm())
     t_ovl = timed(sync_overlap)
-    t_ser = timed(GradSync(flat, bounds, ctx, overlap=False))
+    t_ser = timed(GradSync(flat, bounds, ctx, overlap=False, force=bool(a.dist_force)))
     out.update(step_ms_compute_only=round(t_none, 3), step_ms_overlapped=round(t_ovl, 3),
                step_ms_serial_comm=round(t_ser, 3), exposed_comm_ms=round(t_ovl - t_none, 3),
                serial_comm_ms=round(t_ser - t_none, 3))
@@ -148,7 +151,7 @@ def main():
     from unet_distributed_amd.runtime.amp import LossScaler
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    ctx = D.init("auto", "auto", 600.0)
+    ctx = D.init("auto", "auto", 600.0, force=bool(a.dist_force))
     N = ctx.world_size
     if world_env != a.gpus and ctx.rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d" % (a.gpus, world_env), file=sys.stderr)
@@ -166,7 +169,7 @@ def main():
     backend = make_backend(spec, flat, cfg, dev, a.per_gpu_batch, bounds)
     if hasattr(backend, "engine"):
         backend.engine.repack()
-    sync = GradSync(flat, bounds, ctx, overlap=cfg.overlap_comm)
+    sync = GradSync(flat, bounds, ctx, overlap=cfg.overlap_comm, force=bool(a.dist_force))
     opt = TFAdam(flat, cfg, native=_NativeOpt(backend) if hasattr(backend, "adam_step") else None)
 
     # two distinct synthetic batches resident on the device (per-rank shards)

@@ -166,6 +166,23 @@ def test_async_ps_fp16_overflow_on_one_rank_keeps_ranks_in_lockstep(tmp_path):
     assert len([x for x in recs if x["kind"] == "test_final"]) == 1
 
 
+@pytest.mark.slow
+def test_sync_fp16_overflow_on_one_rank_skips_the_step_on_every_rank(tmp_path):
+    """Sync mode (the default): rank 1's gradient overflows at step 0.  The poison is
+    written before the allreduce of the bucket that holds it, so BOTH ranks see the
+    non-finite average and skip that step together; it fires once (the retried step
+    carries the same number), the replicas stay identical (checked every step) and
+    training reaches its final step."""
+    r = _run_train(tmp_path, ["--epochs", "2", "--dtype", "fp16", "--no_checkpoint",
+                              "--fault_inject_overflow_step", "0", "--fault_inject_rank", "1",
+                              "--check_sync_every", "1", "--dist_timeout_s", "60"], timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:]
+    recs = [json.loads(l) for l in open(tmp_path / "m.jsonl")]
+    train = [x for x in recs if x["kind"] == "train"]
+    assert train and train[-1]["step"] == 4                 # 2 epochs x 2 global batches
+    assert [x["step"] for x in recs if x["kind"] == "test_final"] == [4]
+
+
 def _run_launcher(tmp_path, extra, timeout=600):
     port = _free_port()
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")

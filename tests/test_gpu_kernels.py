@@ -71,17 +71,18 @@ def test_conv3x3_fwd_bias_relu(cuda_dev, N, H, Cin, Cout):
     assert rel_err(out, ref) < 1e-2
 
 
-def test_conv3x3_concat_dual_source_and_upsample(cuda_dev):
+def test_conv3x3_concat_dual_source(cuda_dev):
+    """Implicit-GEMM conv (tile 8: row-window off) reading a 64 + 64 channel concat from
+    two sources."""
     torch.manual_seed(1)
     N, H, C1, C2, Co = 2, 16, 64, 64, 64
-    lo = torch.randn(N, H // 2, H // 2, C1, device=cuda_dev).bfloat16()   # upsampled source
+    a = torch.randn(N, H, H, C1, device=cuda_dev).bfloat16()
     skip = torch.randn(N, H, H, C2, device=cuda_dev).bfloat16()
     w = (torch.randn(3, 3, C1 + C2, Co, device=cuda_dev) * 0.05).bfloat16()
     out = torch.empty(N, H, H, Co, device=cuda_dev, dtype=torch.bfloat16)
-    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=C1, C2=C2, up1=2, src1=ptr(lo),
-                      src2=ptr(skip), wgt=ptr(pack_fwd(w)), Cout=Co, relu=0, dst1=ptr(out)), stream())
-    up = F.interpolate(nchw(lo.float()), scale_factor=2, mode="nearest")
-    ref = nhwc(F.conv2d(torch.cat([up, nchw(skip.float())], 1), w.float().permute(3, 2, 0, 1), padding=1))
+    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=C1, C2=C2, src1=ptr(a),
+                      src2=ptr(skip), wgt=ptr(pack_fwd(w)), Cout=Co, relu=0, dst1=ptr(out), tile=8), stream())
+    ref = nhwc(F.conv2d(torch.cat([nchw(a.float()), nchw(skip.float())], 1), w.float().permute(3, 2, 0, 1), padding=1))
     assert rel_err(out, ref) < 1e-2
 
 
@@ -126,8 +127,7 @@ def test_conv_dgrad_dual_dest_mask(cuda_dev):
     (2, 64, 32, 0, 64, 6), (3, 16, 32, 0, 32, 6), (5, 16, 64, 0, 64, 6), (3, 32, 128, 0, 32, 6),
     (1, 128, 32, 0, 64, 0), (2, 64, 64, 64, 64, 0), (2, 32, 64, 0, 128, 8),
     (2, 128, 32, 0, 64, 12), (3, 128, 32, 32, 64, 12), (3, 64, 64, 64, 64, 12), (5, 16, 64, 0, 128, 12),
-    (3, 32, 128, 0, 64, 12), (2, 16, 256, 256, 256, 12),
-    (2, 128, 32, 0, 32, 13), (3, 128, 32, 32, 32, 13), (3, 64, 64, 64, 64, 13), (3, 32, 128, 0, 32, 13)])
+    (3, 32, 128, 0, 64, 12), (2, 16, 256, 256, 256, 12)])
 def test_conv_row_window(cuda_dev, N, H, C1, C2, Cout, tile):
     """Row-window kernel (tile 6, auto for 16 <= W <= 128): image boundaries inside a window,
     row tails (N*H not a multiple of the window), concat sources, bias + ReLU + dropout."""
@@ -147,8 +147,7 @@ def test_conv_row_window(cuda_dev, N, H, C1, C2, Cout, tile):
 
 @pytest.mark.parametrize("N,H,W,C1,C2,Cout,tile", [(2, 8, 256, 32, 0, 32, 6), (1, 4, 384, 32, 32, 32, 6),
                                                     (2, 8, 512, 64, 0, 64, 6), (1, 4, 256, 64, 64, 64, 6),
-                                                    (2, 8, 512, 64, 0, 64, 12), (1, 4, 256, 64, 64, 128, 12),
-                                                    (2, 8, 256, 32, 0, 32, 13), (1, 4, 384, 32, 32, 32, 13)])
+                                                    (2, 8, 512, 64, 0, 64, 12), (1, 4, 256, 64, 64, 128, 12)])
 def test_conv_row_window_segmented_rows(cuda_dev, N, H, W, C1, C2, Cout, tile):
     """Rows wider than 128 run as 128-wide segments whose halo columns are the
     neighbouring segments' pixels (512x512 config levels)."""
@@ -219,7 +218,7 @@ def test_conv_row_window_dgrad_dual_dest_mask_dropout(cuda_dev):
     dy = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
     d1 = torch.empty(N, H, H, C1, device=cuda_dev, dtype=torch.bfloat16)
     d2 = torch.empty(N, H, H, C2, device=cuda_dev, dtype=torch.bfloat16)
-    for tile in (6, 8, 12, 13):
+    for tile in (6, 8, 12):
         C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Co, src1=ptr(dy),
                           wgt=ptr(pack_dgrad(w)), Cout=C1 + C2, D1=C1, dst1=ptr(d1), dst2=ptr(d2),
                           mask1=ptr(m1), mask2=ptr(skip), mask_scale2=1.25, tile=tile), stream())
@@ -375,21 +374,6 @@ def test_wgrad3d_row_window(cuda_dev, N, D, H, C1, C2, Cout, splits):
     gwr, gbr = torch.autograd.grad(F.conv3d(inp, w, bb, padding=1), [w, bb], ncdhw(dy.float()))
     assert rel_err(gw, gwr.permute(2, 3, 4, 1, 0).reshape(-1)) < 2e-3
     assert rel_err(gb, gbr) < 2e-3
-
-
-def test_wgrad_concat_upsample(cuda_dev):
-    torch.manual_seed(6)
-    N, H, C1, C2, Co = 2, 16, 32, 32, 32
-    lo = F.relu(torch.randn(N, H // 2, H // 2, C1, device=cuda_dev)).bfloat16()
-    skip = F.relu(torch.randn(N, H, H, C2, device=cuda_dev)).bfloat16()
-    dy = torch.randn(N, H, H, Co, device=cuda_dev).bfloat16()
-    d = dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=C1, M2=C2, upA=2, a1=ptr(lo),
-             a2=ptr(skip), b=ptr(dy), Nc=Co)
-    gw, _ = _wgrad(d, 2, 9, C1 + C2, C1 + C2, Co, 9 * (C1 + C2) * Co)
-    inp = torch.cat([F.interpolate(nchw(lo.float()), scale_factor=2, mode="nearest"), nchw(skip.float())], 1)
-    w = torch.zeros(Co, C1 + C2, 3, 3, device=cuda_dev, requires_grad=True)
-    (gwr,) = torch.autograd.grad(F.conv2d(inp, w, padding=1), [w], nchw(dy.float()))
-    assert rel_err(gw, gwr.permute(2, 3, 1, 0).reshape(-1)) < 2e-3
 
 
 @pytest.mark.parametrize("N,H,Creal,Cpad,Co,splits,win", [(2, 32, 1, 4, 32, 3, -1), (2, 32, 1, 4, 32, 3, 0),
@@ -617,8 +601,7 @@ def test_upsample2_fwd_materialised(cuda_dev, dims3):
 
 @pytest.mark.parametrize("N,H,Cin,Cout,tile", [(2, 128, 32, 32, 0), (2, 64, 32, 64, 0), (4, 32, 64, 128, 0),
                                                (4, 16, 128, 256, 0), (1, 256, 32, 32, 0), (2, 128, 32, 64, 12),
-                                               (2, 64, 32, 64, 12), (4, 32, 64, 128, 12), (4, 16, 128, 256, 12),
-                                               (2, 128, 32, 32, 13), (2, 64, 32, 64, 13), (1, 256, 32, 32, 13)])
+                                               (2, 64, 32, 64, 12), (4, 32, 64, 128, 12), (4, 16, 128, 256, 12)])
 def test_conv_fwd_fused_maxpool_matches_pool_kernel(cuda_dev, N, H, Cin, Cout, tile):
     """convNb forward with the fused 2x2 max-pool epilogue: the conv output, the pooled
     tensor and the argmax codes equal the plain conv + the separate pool kernel."""
@@ -793,7 +776,7 @@ def test_wgrad_split_ranges_compose(cuda_dev, kind):
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout,tile", [(2, 128, 32, 32, 0), (4, 32, 64, 128, 0), (4, 16, 128, 256, 0),
-                                               (2, 256, 32, 32, 0), (2, 64, 64, 64, 13)])
+                                               (2, 256, 32, 32, 0)])
 def test_window_conv_reverse_order_same_result(cuda_dev, N, H, Cin, Cout, tile):
     """rev = 1 (windows walked last to first: the consumer starts on its producer's
     most recent output) writes exactly the rev = 0 tensors, fused pool and ReLU bits
@@ -821,3 +804,78 @@ def test_window_conv_reverse_order_same_result(cuda_dev, N, H, Cin, Cout, tile):
         assert torch.equal(a, bb)
     ref = nhwc(F.relu(F.conv2d(nchw(x.float()), w.float().permute(3, 2, 0, 1), b, padding=1)))
     assert rel_err(outs[1][0], ref) < 1e-2
+
+
+def _relu_bits(x):
+    """[P, C] 16-bit activation -> [P, C / 8] uint8, bit e of byte b = x[p, 8b + e] > 0."""
+    P, Cc = x.shape[0], x.shape[-1]
+    pos = (x.reshape(P, Cc // 8, 8).float() > 0).to(torch.int32)
+    sh = torch.arange(8, device=x.device, dtype=torch.int32)
+    return (pos << sh).sum(-1).to(torch.uint8).contiguous()
+
+
+@pytest.mark.parametrize("N,H,Cy,bce,gs,splits", [(2, 128, 64, 0.0, 1.0, 5), (3, 64, 32, 0.5, 8.0, 3),
+                                                  (4, 32, 64, 0.0, 1.0, 2), (5, 16, 32, 1.0, 2.0, 7),
+                                                  (5, 16, 64, 0.0, 1.0, 3), (2, 16, 32, 0.0, 1.0, 3)])
+def test_head_onload_matches_materialised_head_gradient(cuda_dev, N, H, Cy, bce, gs, splits):
+    """Head-on-load (head_grad.h): the head input's data gradient and weight gradient
+    forming dY = dlogit * w * (x > 0) from the probability, target and ReLU bits equal
+    the same kernels reading the dY head_bwd materialises (same formula, same rounding:
+    bit-identical), and head_bwd with dx = nullptr still reduces the Mask gradients."""
+    torch.manual_seed(71)
+    Cc = 32
+    P = N * H * H
+    x = F.relu(torch.randn(N, H, H, Cc, device=cuda_dev)).bfloat16()
+    w = torch.randn(Cc, device=cuda_dev) * 0.3
+    prob = torch.rand(P, device=cuda_dev) * 0.98 + 0.01
+    t = (torch.rand(P, device=cuda_dev) > 0.6).bfloat16()
+    sums = torch.stack([(t.float() * prob).sum(), t.float().sum(), prob.sum(), torch.zeros((), device=cuda_dev)])
+    gsc = torch.full((1,), gs, device=cuda_dev)
+    nb = C().head_blocks(P)
+    part = torch.zeros(nb * (Cc + 1), device=cuda_dev)
+    dy = torch.empty_like(x)
+    ow0, ob0, ow1, ob1 = [torch.zeros(n, device=cuda_dev) for n in (Cc, 1, Cc, 1)]
+    hb = lambda dx, ow, ob: C().generic("head_bwd", [ptr(x), ptr(w), ptr(prob), ptr(t), ptr(sums), dx, ptr(part),
+                                                     ptr(ow), ptr(ob), ptr(gsc)], [P, Cc], [1.0 / P, bce, 1.0],
+                                        stream())
+    hb(ptr(dy), ow0, ob0)
+    hb(0, ow1, ob1)
+    bits = _relu_bits(x.reshape(P, Cc))
+    hg = dict(hg_prob=ptr(prob), hg_t=ptr(t), hg_sums=ptr(sums), hg_w=ptr(w), hg_bits=ptr(bits), hg_gscale=ptr(gsc),
+              hg_inv_total=1.0 / P, hg_bce_w=bce)
+    # data gradient into a ReLU'd input (bit mask), as dgrad:conv9b
+    a9 = torch.randn(N, H, H, Cy, device=cuda_dev).bfloat16()
+    a9b = _relu_bits(a9.reshape(P, Cy))
+    wt = (torch.randn(3, 3, Cy, Cc, device=cuda_dev) * 0.1).bfloat16()
+    wp = pack_dgrad(wt)                          # kept alive: later allocations must not reuse it
+    d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cc, src1=ptr(dy), wgt=ptr(wp), Cout=Cy,
+             mask1=ptr(a9b), mask_bits=1)
+    dx0, dx1 = torch.empty_like(a9), torch.full_like(a9, float("nan"))
+    C().conv_fwd(dict(d, dst1=ptr(dx0)), stream())
+    C().conv_fwd(dict(d, dst1=ptr(dx1), src1=ptr(x), **hg), stream())     # src1 unused: dY formed on load
+    # weight + bias gradient (B = dY)
+    a = F.relu(a9.float()).bfloat16()
+    base = dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=Cy, a1=ptr(a), Nc=Cc, bias_mode=1)
+    g0, b0 = _wgrad(dict(base, b=ptr(dy)), splits, 9, Cy, Cy, Cc, 9 * Cy * Cc, bias_w=(splits, Cc))
+    g1, b1 = _wgrad(dict(base, b=ptr(x), **hg), splits, 9, Cy, Cy, Cc, 9 * Cy * Cc, bias_w=(splits, Cc))
+    torch.cuda.synchronize()
+    # the materialised path itself against autograd (fp32 head, ReLU mask)
+    pr = prob.clone().requires_grad_(True)
+    tf = t.float()
+    z = torch.log(pr / (1 - pr))
+    zz = z.detach().requires_grad_(True)
+    pz = torch.sigmoid(zz)
+    loss = (-torch.log(2 * (tf * pz).sum() + 1) + torch.log(tf.sum() + pz.sum() + 1)
+            + bce * F.binary_cross_entropy_with_logits(zz, tf, reduction="sum") / P) * gs
+    (dlog,) = torch.autograd.grad(loss, [zz])
+    ref_dy = dlog[:, None] * w[None, :] * (x.reshape(P, Cc).float() > 0)
+    assert rel_err(dy.reshape(P, Cc), ref_dy) < 1e-2
+    xr = torch.zeros(N, Cy, H, H, device=cuda_dev, requires_grad=True)
+    yr = F.conv2d(xr, wt.float().permute(3, 2, 0, 1), padding=1)
+    (gx,) = torch.autograd.grad(yr, xr, nchw(dy.float()))
+    ref_dx = nhwc(gx) * (a9.float() > 0)
+    e0, e1 = rel_err(dx0, ref_dx), rel_err(dx1, ref_dx)
+    assert e0 < 1e-2 and e1 < 1e-2, (e0, e1)
+    assert torch.equal(dx0, dx1)
+    assert torch.equal(g0, g1) and torch.equal(b0, b1)
+    assert torch.equal(ow0, ow1) and torch.equal(ob0, ob1)

@@ -60,4 +60,5 @@ def test_conv_shape_validation_asan_ubsan():
                               "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
                               "-DUNET_WITH_SHAPE_CHECKS", "-msse4.2", "-pthread",
                               "-I" + os.path.join(CSRC, "runtime"), "-I" + os.path.join(CSRC, "kernels")],
-                   extra_src=[os.path.join(CSRC, "kernels", "conv_fwd.hip")])
+                   extra_src=[os.path.join(CSRC, "kernels", "conv_fwd.hip"),
+                              os.path.join(CSRC, "tests", "win_stubs.cpp")])

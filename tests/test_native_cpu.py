@@ -30,14 +30,15 @@ def test_plan_construction_dry_run(kw, img, dtype):
     assert e.arena.dtype == e.adt and e.target.dtype == e.adt
     names = e.plan.names()
     assert names[0] == "fwd:conv1a" and names[e.fwd_end - 1] == "fwd:Mask"
-    assert names[e.fwd_end] == "bwd:Mask"
+    # (head-on-load: the head backward only reduces the Mask gradients, on the side stream)
+    assert names[e.fwd_end] == ("wgrad:Mask" if e.head_onload else "bwd:Mask")
     # every conv / tconv gradient is reduced by exactly one batched reduce op
     reduced = [ln for n in names if n.startswith("reduce:") for ln in n[len("reduce:"):].split(",")]
     assert sorted(reduced) == sorted(l.name for l in spec.param_layers() if l.kind != "mask")
     assert len(reduced) == len(set(reduced))
     # every wgrad is followed (later) by the reduce that covers its layer
     for i, n in enumerate(names):
-        if n.startswith("wgrad:"):
+        if n.startswith("wgrad:") and n != "wgrad:Mask":
             ln = n.split(":", 1)[1]
             assert any(m.startswith("reduce:") and ln in m[len("reduce:"):].split(",") for m in names[i + 1:])
     assert e.seg_ends[-1] == e.plan.size() and sorted(e.seg_ends) == e.seg_ends
@@ -74,23 +75,15 @@ def test_bucket_plan_is_layer_aligned_and_covers_buffer():
     assert (flat.numel - b[-2]) * 4 / 2 ** 20 <= 8.0
 
 
-def test_forward_chunk_plan_dry_run(monkeypatch):
-    """UNET_FWD_CHUNK=4: full-resolution forward runs are emitted chunk by chunk with
-    per-chunk pointer offsets; the coarse levels and the head stay whole-batch."""
-    from unet_distributed_amd.runtime.native_engine import NativeUNet
-    monkeypatch.setenv("UNET_FWD_CHUNK", "4")
-    spec = UNetSpec(in_channels=4)
-    flat = FlatParams(spec)
-    e = NativeUNet(spec, flat, 8, 64, "cpu", bucket_bounds=plan_buckets(flat, 4.0), dry_run=True)
-    names = e.plan.names()[:e.fwd_end]
-    assert names[0:3] == ["fwd:conv1a", "fwd:conv1b", "fwd:pool1"]
-    assert names.count("fwd:conv1a") == 4 and names.count("fwd:conv9b") == 4
-    assert names.count("fwd:conv5a") == 1 and names.count("fwd:Mask") == 1
-    assert e._toff("conv1b", 1, 2) == 2 * 64 * 64 * 32 * 2
-    assert e._toff("pool1", 1, 2) == 2 * 32 * 32 * 32 * 2
-    monkeypatch.setenv("UNET_FWD_CHUNK", "3")       # batch 8 not divisible: whole batch
-    e = NativeUNet(spec, flat, 8, 64, "cpu", bucket_bounds=plan_buckets(flat, 4.0), dry_run=True)
-    assert e.plan.names()[:e.fwd_end].count("fwd:conv1a") == 1
+def test_engine_env_knobs_are_few():
+    """The executor's behaviour is fixed by its measured defaults: only the A/B knobs
+    the GPU tests flip remain environment-driven (round-2 review: <= 12)."""
+    import re
+    from unet_distributed_amd.runtime import native_engine
+    src = open(native_engine.__file__).read()
+    knobs = set(re.findall(r'os\.environ\.get\("(UNET_[A-Z0-9_]+)"', src))
+    assert knobs <= {"UNET_DUAL_STREAM", "UNET_CONV_TILE", "UNET_FWD_STREAMS", "UNET_HEAD_FUSE",
+                     "UNET_HEAD_ONLOAD"}, knobs
 
 
 def test_fused_head_plan(monkeypatch):

@@ -21,8 +21,8 @@
 // * Fused epilogue: scale, bias, ReLU, inverted dropout (counter hash), per-channel
 //   BN statistics, consumer-side ReLU mask (out *= mask > 0), channel split into
 //   two destinations (dgrad of a concat input), transposed-conv pixel shuffle.
-// * Skip concat (two sources) and nearest-upsample (src1 at half resolution) are
-//   folded into the A address generation: neither is ever materialised.
+// * The skip concat (two sources) is folded into the A address generation: it is
+//   never materialised.
 //
 // Reference semantics: Conv2D 3x3 'same' + ReLU (`model.py:47-117`),
 // Conv2DTranspose 2x2/2 (`model.py:79-113`), concatenate (`model.py:76-113`),
@@ -30,6 +30,7 @@
 #include "common.h"
 #include "conv_params.h"
 #include "conv_epilogue.h"
+#include "conv_win.h"
 
 namespace unet {
 
@@ -40,7 +41,7 @@ constexpr int BK = 64;
 
 __device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
 
-// MODE 0: plain; MODE 1: src1 nearest-upsampled x2; MODE 2: first layer (Cin 4/8).
+// MODE 0: plain; MODE 2: first layer (Cin 4/8).
 // CONCAT: a second source supplies channels [C1, C1 + C2) (decoder skip concat).
 template <int BM, int BN, int WAVES_M, int WAVES_N, int MODE, bool CONCAT, int EPI = EPI_GENERIC>
 __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
@@ -68,14 +69,10 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
   const int nk = Kpad / BK;
   const int cc = tid & 7;                            // this thread's 16-byte chunk column
   const int padd = p.KD > 1 ? p.pad : 0;
-  const int upd = p.ID > 1 ? p.up1 : 1;
-  const int ID1 = p.ID / upd, IH1 = p.IH / p.up1, IW1 = p.IW / p.up1;
 
   // ---- per-row precomputation (hoisted out of the K loop)
   int a_pix[AR];      // full-res pixel index of the window origin (may be negative at the halo)
   int a_pb1[AR], a_pb2[AR];   // the same as byte offsets into src1 / src2
-  int a_lo[AR];       // MODE 1: low-res pixel index of the centre; parity bits in a_par
-  int a_par[AR];
   uint32_t a_mask[AR];
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
@@ -100,10 +97,6 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
           if (in) m |= 1u << ((kd * p.KH + kh) * p.KW + kw);
         }
     a_mask[i] = ok ? m : 0u;
-    if (MODE == 1) {
-      a_lo[i] = ((c.n * ID1 + c.d / upd) * IH1 + c.h / 2) * IW1 + c.w / 2;
-      a_par[i] = ((c.d & 1) << 2) | ((c.h & 1) << 1) | (c.w & 1);
-    }
   }
   u32x4 ra[AR], rb[BR];
 
@@ -164,30 +157,12 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
       const int tdel_b = __builtin_amdgcn_readfirstlane(p.tap_delta[t_b]);
       const int tdel = hi_c ? tdel_b : tdel_a;
       const bool from1 = !CONCAT || kk < p.C1;
-      int dh = 0, dw = 0, dd = 0;
-      if (MODE == 1) {
-        const int ha = __builtin_amdgcn_readfirstlane(p.tap_h[t_a]), hb = __builtin_amdgcn_readfirstlane(p.tap_h[t_b]);
-        const int wa = __builtin_amdgcn_readfirstlane(p.tap_w[t_a]), wb = __builtin_amdgcn_readfirstlane(p.tap_w[t_b]);
-        const int da = __builtin_amdgcn_readfirstlane(p.tap_d[t_a]), db = __builtin_amdgcn_readfirstlane(p.tap_d[t_b]);
-        dh = hi_c ? hb : ha;
-        dw = hi_c ? wb : wa;
-        dd = hi_c ? db : da;
-      }
       const int td1 = (tdel * p.C1 + kk) * 2;
       const int td2 = (tdel * p.C2 + kk - p.C1) * 2;
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
         const bool ok = live && ((a_mask[i] >> tap) & 1u);
-        int o1;
-        if (MODE == 1) {
-          const int par = a_par[i];
-          const int lh = (dh + ((par >> 1) & 1) - 1) >> 1;
-          const int lw = (dw + (par & 1) - 1) >> 1;
-          const int ld = p.ID > 1 ? ((dd + ((par >> 2) & 1) - 1) >> 1) : 0;
-          o1 = ((a_lo[i] + (ld * IH1 + lh) * IW1 + lw) * p.C1 + kk) * 2;
-        } else {
-          o1 = a_pb1[i] + td1;
-        }
+        const int o1 = a_pb1[i] + td1;
         if constexpr (CONCAT) {
           const int o = from1 ? o1 : a_pb2[i] + td2;
           ra[i] = __builtin_amdgcn_raw_buffer_load_b128(from1 ? rs1 : rs2, ok ? o : OOB, 0, 0);
@@ -276,7 +251,6 @@ hipError_t launch_cfg(const ConvFwdParams& p, hipStream_t s) {
   const int epi = conv_epi_mode(p);
   if (epi == EPI_STATS || epi == EPI_DGRAD_NORM) {
     // fused-normalisation epilogues: plain (MODE 0) or first-layer (MODE 2) sources
-    if (p.up1 != 1) return hipErrorInvalidValue;
     if (epi == EPI_DGRAD_NORM && !smallc && p.C2 == 0)
       hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, false, EPI_DGRAD_NORM>), dim3(grid), dim3(NTHR),
                          0, s, p);
@@ -295,368 +269,11 @@ hipError_t launch_cfg(const ConvFwdParams& p, hipStream_t s) {
   }
   if (smallc)
     hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 2, false>), dim3(grid), dim3(NTHR), 0, s, p);
-  else if (p.up1 == 2)
-    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 1, true>), dim3(grid), dim3(NTHR), 0, s, p);
   else if (p.C2 > 0)
     hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, true>), dim3(grid), dim3(NTHR), 0, s, p);
   else
     hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, false>), dim3(grid), dim3(NTHR), 0, s, p);
   return hipGetLastError();
-}
-
-
-// ---------------------------------------------------------------------------------
-// Row-window conv (fine UNet levels): 2D, 3x3, stride 1, 'same' padding, full-width rows.
-//
-// The implicit GEMM above re-gathers the input once per tap: at the 128^2 / 64^2
-// levels (Cin, Cout <= 64) that 9x L2->LDS traffic, not the MFMA, bounds it.  Here a
-// workgroup owns BM = 512 output pixels = R = 512/W whole rows of the flattened
-// (n, h) row space and BN output channels.  Per 32-channel input chunk it stages the
-// (R+2) x (W+2) halo image of those rows ONCE in LDS (zero columns at the left/right
-// border come free from out-of-range buffer loads), plus the chunk's 9 x BN weight
-// rows, and then runs all nine taps as MFMAs on shifted LDS addresses.  Rows that
-// cross an image boundary inside the window are handled by skipping the (wave-uniform)
-// MFMAs of taps whose input row falls outside the output row's image.
-//
-// LDS images: 64-byte pixel slots (32 bf16); the halo image has rows of HWP = W + 4
-// slots (a multiple of 4: every row starts on a 256-byte bank row) and stores 16-byte
-// chunk c of the pixel in column hc at c ^ ((hc >> 1) & 3).  Fragment reads are 16
-// consecutive columns from any start (any tap shift): conflict free, and because the
-// swizzle depends only on the column, a lane's address is one of three per-lane bases
-// (one per horizontal tap) plus a compile-time immediate (row, tile) -- no per-tap
-// address registers.  Weight rows (tap, n) use the same swizzle on the row index.
-// GEO: 0 = 2D full rows (Wf = W), 1 = 2D segmented rows (Wf = p.OW, a multiple of W),
-// 2 = 3D full rows (three depth taps).  Compile-time so the common 2D case carries no
-// segment / depth state (extra SGPR state spilled to VGPR lanes inside the chunk loop).
-enum { GEO_2D = 0, GEO_SEG = 1, GEO_3D = 2 };
-
-// Output-channel tile of the row-window conv: 64 where Cout allows it and the row
-// width is enabled in UNET_WIN_BN64 (bit mask over W = 16 / 32 / 64 / 128 -> bits
-// 0..3; read once per process), else 32.  Default 7 (W = 16..64), from a same-box
-// sweep of the headline step: +2.8 % (16), +0.5 % (32), +0.4 % (64), -0.3 % (128).
-// 64 halves the halo image's LDS-DMA and fragment reads per MFMA and doubles the MFMA
-// work per synchronisation.
-static int win_bn(const ConvFwdParams& p) {
-  static const int mask = [] {
-    const char* e = getenv("UNET_WIN_BN64");
-    return e ? atoi(e) : 7;
-  }();
-  if (p.tile == 12) return 64;                       // forced (tests / A-B)
-  if (p.tile == 6 || p.tile == 13) return 32;
-  const int W = p.OW > 128 ? 128 : p.OW;
-  const int bit = W == 16 ? 1 : W == 32 ? 2 : W == 64 ? 4 : 8;
-  return (p.Cout % 64 == 0 && (mask & bit) && !p.head_w) ? 64 : 32;
-}
-// Window pixels: 256 for 16-wide rows and for the 64-channel tile (its accumulators,
-// 4 x 4 fragments per wave, and LDS then still fit two workgroups per CU); for the
-// 32-channel tile 512, or 256 where the row width is enabled in UNET_WIN_BM256 (bit
-// mask as UNET_WIN_BN64): the smaller window's LDS (tight halo pitch + 18 KB of
-// weights) fits three workgroups per CU.
-static int win_bm(const ConvFwdParams& p) {
-  static const int mask = [] {
-    const char* e = getenv("UNET_WIN_BM256");
-    return e ? atoi(e) : 0;
-  }();
-  const int W = p.OW > 128 ? 128 : p.OW;
-  if (W == 16 || win_bn(p) == 64 || p.tile == 13) return 256;
-  if (p.tile == 6) return 512;
-  const int bit = W == 32 ? 2 : W == 64 ? 4 : 8;
-  return (mask & bit) ? 256 : 512;
-}
-static int win_rows(const ConvFwdParams& p) {
-  const int W = p.OW > 128 ? 128 : p.OW;
-  return win_bm(p) / W;
-}
-
-// XF (2D, single source): operand transform of the src1 halo image in LDS before the
-// MFMAs, conv_params.h xform -- 1: y = relu(xa z + xb), 2: dz = xa g + xb z + xc (z
-// from xz); the window's own rows of the transformed operand go to xout.
-template <int W, int BN, int BM, bool CONCAT, int EPI, int GEO, int XF = 0>
-__global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
-  static_assert(BN == 32 || BN == 64, "row-window tile is 32 or 64 output channels wide");
-  static_assert(XF == 0 || (GEO == GEO_2D && !CONCAT), "operand transform: 2D single-source windows");
-  constexpr int R = BM / W, HR = R + 2;
-  // halo row pitch in 64-byte pixel slots: W + 2 columns rounded up to a multiple of 4
-  // (every row starts on a 256-byte bank row); the DMA fills the image as one linear
-  // run of slots, so rows need not align to the 16-slot DMA instructions
-  constexpr int HWP = W + 4;
-  constexpr int ROWB = HWP * 64;
-  constexpr int XI = (HR * HWP + 15) / 16, WI = 9 * BN / 16;
-  constexpr int XB = XI * 1024, WB = WI * 1024;
-  constexpr int EPIB = (EPI == EPI_STATS || EPI == EPI_DGRAD_NORM) ? epi_lds_bytes<BM, BN>() : BM * (BN + 4) * 2;
-  constexpr int LDS_BYTES = (XB + WB > EPIB) ? XB + WB : EPIB;
-  constexpr int WMP = BM / 4;                   // pixels per wave
-  constexpr int TM = WMP / 16, TN = BN / 16;
-  constexpr int TPR = W / 16;                   // 16-pixel tiles per row
-  static_assert(W >= 16 && W <= 128 && BM % W == 0 && WMP % 16 == 0, "row width");
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
-  char* Xs = smem;
-  char* Ws = smem + XB;
-
-  // wave index as a scalar: every per-wave quantity below (rows, DMA slots) stays in SGPRs
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // Row space: rows g = (n, d, h) of Wf pixels.  Rows wider than 128 are cut into
-  // nseg W-wide segments (a window = R rows x one segment; its halo columns -1 / W are
-  // the neighbouring segments' pixels).  3D (KD = 3): depth tap dz reads the halo rows
-  // of slice d + dz - 1, i.e. row g + (dz - 1) H, as three more 32-channel K chunks.
-  constexpr int KD = GEO == GEO_3D ? 3 : 1;
-  const int H = p.OH;
-  const int D = GEO == GEO_3D ? p.OD : 1;
-  const int Wf = GEO == GEO_SEG ? p.OW : W;
-  const int nseg = GEO == GEO_SEG ? p.OW / W : 1;
-  const int rows_total = p.N * D * H;
-  const int M = rows_total * Wf;
-  const int tiles_n = p.Cout / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm0 = bid / tiles_n, tn = bid % tiles_n;
-  const int tm = p.rev ? (int)(gridDim.x / tiles_n) - 1 - tm0 : tm0;
-  const int rgi = GEO == GEO_SEG ? tm / nseg : tm;
-  const int g0 = rgi * R, col0 = GEO == GEO_SEG ? (tm - rgi * nseg) * W : 0;
-  const int n0 = tn * BN;
-  const int dsl = GEO == GEO_3D ? (g0 / H) % D : 0;   // depth slice of the window
-  const int Cin = p.C1 + p.C2;
-  const int nchunks = Cin >> 5;
-  constexpr int OOB = 0x7fffffff;
-  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)p.src1, (short)0, OOB, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs2 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.src2 ? p.src2 : p.src1), (short)0, OOB, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
-
-  // Wave w owns an RW-row x 16 TC-column strip of the window (StripTiles): an A
-  // fragment read from halo row r at horizontal shift dw feeds the output rows r - dh
-  // of all three vertical taps, so per chunk a wave reads 3 (RW + 2) TC fragments
-  // instead of 9 RW TC (2-2.4x less LDS read traffic than one fragment per tap).
-  constexpr int TC = W >= 128 ? 2 : 1;            // 16-pixel column tiles per strip
-  constexpr int NCS = W / (16 * TC);              // column strips per window row
-  constexpr int RW = R / (4 / NCS);               // rows per strip
-  static_assert(NCS <= 4 && 4 % NCS == 0 && RW * TC == TM, "strip map");
-  using Map = StripTiles<W, RW, TC, NCS>;
-  const int r0 = (wave / NCS) * RW, c0 = (wave % NCS) * 16 * TC;
-  // H % R == 0 (win_eligible): a window never spans two images, so the only rows of
-  // another image are the halo rows above / below it, which the DMA fills with zeros
-  // (the 'same' padding) -- the tap loop needs no image-edge branches at all, and the
-  // whole chunk is one basic block the scheduler can pipeline LDS reads through.
-  const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int fsub = lane >> 4, fr = lane & 15;
-  // per-lane fragment bases: horizontal tap dw -> column c0 + fr + dw of halo row r0
-  // (c0 is a multiple of 16, so the swizzle only depends on fr + dw)
-  int xbase[3];
-#pragma unroll
-  for (int dw = 0; dw < 3; ++dw) {
-    const int hc = fr + dw;
-    xbase[dw] = r0 * ROWB + c0 * 64 + hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3));
-  }
-  const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
-  // one 32-channel chunk: per horizontal tap, the three vertical taps' weights are
-  // held in registers and every halo-row fragment feeds up to three output rows
-  auto chunk_mfmas = [&]() {
-#pragma unroll
-    for (int dw = 0; dw < 3; ++dw) {
-      h16x8 wf[3][TN];
-#pragma unroll
-      for (int dh = 0; dh < 3; ++dh)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) wf[dh][j] = *(const h16x8*)(Ws + ((3 * dh + dw) * BN + 16 * j) * 64 + wbase);
-#pragma unroll
-      for (int hr = 0; hr < RW + 2; ++hr) {
-#pragma unroll
-        for (int ci = 0; ci < TC; ++ci) {
-          const h16x8 xf = *(const h16x8*)(Xs + xbase[dw] + hr * ROWB + ci * 16 * 64);
-#pragma unroll
-          for (int dh = 0; dh < 3; ++dh) {
-            const int ri = hr - dh;
-            if (ri < 0 || ri >= RW) continue;
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[ri * TC + ci][j] = mfma16(wf[dh][j], xf, acc[ri * TC + ci][j]);
-          }
-        }
-      }
-    }
-  };
-  // LDS-DMA lane roles: lane l fills physical 16-byte chunk (l & 3) of slot (l >> 2) of a
-  // 16-slot run; it loads logical chunk (l & 3) ^ swizzle(slot), which depends only on l
-  // because every run starts at a multiple of 16 slots.
-  const int lslot = lane >> 2;
-  const int lchunk = (lane & 3) ^ ((lslot >> 1) & 3);
-
-  // one 32-channel chunk of depth tap kd (input rows shifted by gsh): stage, then MFMAs
-  auto run_chunk = [&](const int kc, const int kd, const int gsh) {
-      const bool from1 = !CONCAT || (kc << 5) < p.C1;
-      const int C = from1 ? p.C1 : p.C2;
-      const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
-      {
-        // halo image: row hr, slot hc holds pixel (g0 - 1 + hr + gsh, col0 + hc - 1);
-        // instruction (hr, j) covers slots 16j .. 16j + 15 of row hr.  Rows outside the
-        // tensor / image and columns outside [0, Wf) load zeros (out-of-range offsets).
-        const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
-#pragma unroll
-        for (int q = 0; q < (XI + 3) / 4; ++q) {
-          const int k = wave + 4 * q;
-          if (k < XI) {
-            const int sl = 16 * k + lslot;                  // this lane's halo slot
-            const int hr = sl / HWP, hc = sl - hr * HWP;    // its row / column
-            const int gr = g0 - 1 + hr + gsh;
-            const int col = col0 + hc - 1;
-            const bool row_in = hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in);   // same image
-            // (slots past W + 1 are never read: skip them, they would be real pixels of
-            // the next segment on segmented rows)
-            const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)Wf &&
-                            (GEO != GEO_SEG || hc <= W + 1);
-            const int lch = (lane & 3) ^ ((hc >> 1) & 3);
-            const int off = ok ? ((gr * Wf + col) * C + cb + lch * 8) * 2 : OOB;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
-                                                     16, off, 0, 0, 0);
-          }
-        }
-        // weight image: row r = tap * 32 + n (64 bytes = this chunk's 32 input channels)
-        const int wl = (lslot * p.Kpad + (kc << 5) + lchunk * 8) * 2;
-#pragma unroll
-        for (int q = 0; q < (WI + 3) / 4; ++q) {
-          const int k = wave + 4 * q;
-          if (k < WI) {
-            const int tap = k / (BN / 16), nb = (k % (BN / 16)) * 16;     // wave-uniform
-            const int off = ((n0 + nb) * p.Kpad + (kd * 9 + tap) * Cin) * 2 + wl;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024),
-                                                     16, off, 0, 0, 0);
-          }
-        }
-      }
-      __syncthreads();
-      chunk_mfmas();
-  };
-  if constexpr (GEO == GEO_3D) {
-    // depth taps whose input slice is padding contribute nothing: skip them
-    const int kd_lo = dsl == 0 ? 1 : 0, kd_hi = dsl == D - 1 ? 2 : 3;
-    for (int kd = kd_lo; kd < kd_hi; ++kd)
-      for (int kc = 0; kc < nchunks; ++kc) {
-        if (kc || kd != kd_lo) __syncthreads();   // previous chunk's fragment reads are done
-        run_chunk(kc, kd, (kd - 1) * H);
-      }
-  } else if constexpr (GEO == GEO_SEG) {
-    for (int kc = 0; kc < nchunks; ++kc) {
-      if (kc) __syncthreads();                    // previous chunk's fragment reads are done
-      run_chunk(kc, 0, 0);
-    }
-  } else {
-    // 2D full rows: the same staging with compile-time row pitch and no segment / depth
-    // offsets, spelled out (through run_chunk the scheduler keeps ~100 more scalar
-    // instructions per chunk and spills SGPRs to VGPR lanes: 2-4 % slower, A/B measured)
-    // operand transform: thread t owns logical 16-byte chunk xlc = t & 3 (channels
-    // cb + 8 xlc ..) of slots (t >> 2) + 64 j, so its 8 channels' coefficients are fixed
-    // per chunk; the slot's physical chunk is xlc ^ swizzle(column), as the DMA wrote it
-    constexpr int XNJ = XF ? (XI * 64 + NTHR - 1) / NTHR : 1;
-    const int xlc = tid & 3, xs0 = tid >> 2;
-    auto xslot = [&](const int j, int& hr, int& hc, int& gr, bool& ok) {
-      const int sl = xs0 + (NTHR / 4) * j;
-      hr = sl / HWP;
-      hc = sl - hr * HWP;
-      gr = g0 - 1 + hr;
-      ok = hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)gr < (unsigned)rows_total &&
-           (unsigned)(hc - 1) < (unsigned)W;
-      return sl;
-    };
-    const size_t xsample = XF ? (size_t)(g0 / H) * p.xcs : 0;   // the window's sample (GroupNorm rows)
-    for (int kc = 0; kc < nchunks; ++kc) {
-      const bool from1 = !CONCAT || (kc << 5) < p.C1;
-      const int C = from1 ? p.C1 : p.C2;
-      const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
-      if (kc) __syncthreads();
-      u32x4 xz[XNJ];
-      if constexpr (XF == 2) {
-        // the pre-norm z of this thread's transform chunks, loaded beside the DMA
-#pragma unroll
-        for (int j = 0; j < XNJ; ++j) {
-          int hr, hc, gr;
-          bool ok;
-          xslot(j, hr, hc, gr, ok);
-          if (ok) xz[j] = *(const u32x4*)((const h16*)p.xz + (size_t)(gr * W + hc - 1) * C + cb + xlc * 8);
-        }
-      }
-      {
-        const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
-#pragma unroll
-        for (int q = 0; q < (XI + 3) / 4; ++q) {
-          const int k = wave + 4 * q;
-          if (k < XI) {
-            const int sl = 16 * k + lslot;
-            const int hr = sl / HWP, hc = sl - hr * HWP;
-            const int gr = g0 - 1 + hr;
-            const int col = hc - 1;
-            const bool row_in = hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in);
-            const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
-            const int lch = (lane & 3) ^ ((hc >> 1) & 3);
-            const int off = ok ? ((gr * W + col) * C + cb + lch * 8) * 2 : OOB;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
-                                                     16, off, 0, 0, 0);
-          }
-        }
-        const int wl = (lslot * p.Kpad + (kc << 5) + lchunk * 8) * 2;
-#pragma unroll
-        for (int q = 0; q < (WI + 3) / 4; ++q) {
-          const int k = wave + 4 * q;
-          if (k < WI) {
-            const int tap = k / (BN / 16), nb = (k % (BN / 16)) * 16;
-            const int off = ((n0 + nb) * p.Kpad + tap * Cin) * 2 + wl;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024),
-                                                     16, off, 0, 0, 0);
-          }
-        }
-      }
-      __syncthreads();
-      if constexpr (XF != 0) {
-        float xa[8], xb[8], xc[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const size_t ci = xsample + cb + xlc * 8 + e;
-          xa[e] = p.xa[ci];
-          xb[e] = p.xb[ci];
-          xc[e] = XF == 2 ? p.xc[ci] : 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < XNJ; ++j) {
-          int hr, hc, gr;
-          bool ok;
-          const int sl = xslot(j, hr, hc, gr, ok);
-          if (!ok) continue;                              // padding stays the DMA's zeros
-          char* a = Xs + sl * 64 + 16 * (xlc ^ ((hc >> 1) & 3));
-          float v[8];
-          unpack8(*(const u32x4*)a, v);
-          if constexpr (XF == 1) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(xa[e], v[e], xb[e]), 0.f);
-          } else {
-            float zf[8];
-            unpack8(xz[j], zf);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = fmaf(xa[e], v[e], fmaf(xb[e], zf[e], xc[e]));
-          }
-          const u32x4 o = pack8(v);
-          *(u32x4*)a = o;
-          // the window's own rows (once: output-channel tile 0) -> xout
-          if (p.xout && tn == 0 && hr >= 1 && hr <= R)
-            *(u32x4*)((h16*)p.xout + (size_t)(gr * W + hc - 1) * C + cb + xlc * 8) = o;
-        }
-        __syncthreads();
-      }
-      chunk_mfmas();
-    }
-  }
-  __syncthreads();
-  if constexpr (GEO == GEO_SEG)
-    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, W, W>(p, acc, smem, g0, n0, M, wave, 0, lane, tid, Wf,
-                                                                 col0, tm);
-  else if constexpr (GEO == GEO_2D)
-    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0,
-                                                                 0, tm);
-  else
-    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0, 0, tm);
 }
 
 
@@ -1060,109 +677,6 @@ hipError_t launch_tconv_dgrad(const ConvFwdParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-int win_grid(const ConvFwdParams& p) {
-  const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
-  const int rows = p.N * p.OD * p.OH;
-  const int R = win_rows(p);
-  return ((rows + R - 1) / R) * (p.OW / W) * (p.Cout / win_bn(p));
-}
-
-template <int BN, int BM>
-hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
-  const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
-  const int grid = win_grid(p);
-  const bool cc = p.C2 > 0;
-  const int epi = conv_epi_mode(p);
-  const int geo = p.KD == 3 ? GEO_3D : (p.OW > W ? GEO_SEG : GEO_2D);
-#define WIN_EPI(WW, CC, GG)                                                                               \
-  if (epi == EPI_FWD)                                                                                     \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_FWD, GG>), dim3(grid), dim3(NTHR), 0, s, p);     \
-  else if (epi == EPI_DGRAD)                                                                              \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_DGRAD, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
-  else if (epi == EPI_STATS)                                                                              \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_STATS, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
-  else if (epi == EPI_DGRAD_NORM && !CC)                                                                  \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD_NORM, GG>), dim3(grid), dim3(NTHR), 0, s, p); \
-  else if (epi == EPI_DGRAD_NORM)                                                                         \
-    return hipErrorInvalidValue;                                                                          \
-  else                                                                                                    \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_GENERIC, GG>), dim3(grid), dim3(NTHR), 0, s, p);
-#define WIN_GEO(WW, CC)                                                                                   \
-  if (geo == GEO_3D) {                                                                                    \
-    WIN_EPI(WW, CC, GEO_3D)                                                                               \
-  } else {                                                                                                \
-    WIN_EPI(WW, CC, GEO_2D)                                                                               \
-  }
-#define WIN_CASE(WW)                                                                                      \
-  case WW:                                                                                                \
-    if constexpr (BM == 256 || WW != 16) {                                                                \
-      if (cc) {                                                                                           \
-        WIN_GEO(WW, true)                                                                                 \
-      } else {                                                                                            \
-        WIN_GEO(WW, false)                                                                                \
-      }                                                                                                   \
-    } else {                                                                                              \
-      return hipErrorInvalidValue;                                                                        \
-    }                                                                                                     \
-    break;
-#define XF_EPI(WW, XFV)                                                                                       \
-  if (XFV == 1 && epi == EPI_STATS)                                                                           \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_STATS, GEO_2D, XFV>), dim3(grid), dim3(NTHR), 0, s, p); \
-  else if (XFV == 1 && epi == EPI_GENERIC)                                                                    \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_GENERIC, GEO_2D, XFV>), dim3(grid), dim3(NTHR), 0, s, p); \
-  else if (XFV == 2 && epi == EPI_DGRAD)                                                                      \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_2D, XFV>), dim3(grid), dim3(NTHR), 0, s, p); \
-  else if (XFV == 2 && epi == EPI_DGRAD_NORM)                                                                 \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD_NORM, GEO_2D, XFV>), dim3(grid), dim3(NTHR), 0, s, p); \
-  else                                                                                                        \
-    return hipErrorInvalidValue;
-#define XF_CASE(WW)                                                                                           \
-  case WW:                                                                                                    \
-    if constexpr (BM == 256 || WW != 16) {                                                                    \
-      if (p.xform == 1) {                                                                                     \
-        XF_EPI(WW, 1)                                                                                         \
-      } else {                                                                                                \
-        XF_EPI(WW, 2)                                                                                         \
-      }                                                                                                       \
-    } else {                                                                                                  \
-      return hipErrorInvalidValue;                                                                            \
-    }                                                                                                         \
-    break;
-  if (p.xform) {                        // operand transform: 2D single source (conv_fwd_prepare)
-    switch (W) {
-      XF_CASE(16)
-      XF_CASE(32)
-      XF_CASE(64)
-      XF_CASE(128)
-      default:
-        return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
-#undef XF_CASE
-#undef XF_EPI
-  if (geo == GEO_SEG) {                 // 3D volumes wider than 128 are not window-eligible
-    if (cc) {
-      WIN_EPI(128, true, GEO_SEG)
-    } else {
-      WIN_EPI(128, false, GEO_SEG)
-    }
-    return hipGetLastError();
-  }
-  switch (W) {
-    WIN_CASE(16)
-    WIN_CASE(32)
-    WIN_CASE(64)
-    WIN_CASE(128)
-    default:
-      return hipErrorInvalidValue;
-  }
-#undef WIN_CASE
-#undef WIN_GEO
-#undef WIN_EPI
-  return hipGetLastError();
-}
-
 }  // namespace
 
 // True when the row-window kernel can run this conv: 3x3 (2D) or 3x3x3 (3D) stride 1
@@ -1224,9 +738,8 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.Cout % 32) return "conv_fwd: Cout must be a multiple of 32";
   if (p.D1 <= 0 || p.D1 > p.Cout || (p.D1 % 8)) return "conv_fwd: bad channel split D1";
   if (p.D1 < p.Cout && !p.dst2) return "conv_fwd: dst2 missing for channel split";
-  if (p.up1 != 1 && p.up1 != 2) return "conv_fwd: up1 must be 1 or 2";
-  if (p.up1 == 2 && (p.stride != 1 || p.pad != 1 || p.KH != 3)) return "conv_fwd: upsample fold needs 3x3/s1/p1";
-  if (p.up1 == 2 && ((p.ID % 2 && p.ID != 1) || p.IH % 2 || p.IW % 2)) return "conv_fwd: upsample needs even dims";
+  // (nearest upsampling is materialised by elementwise.hip::ups_fwd; no folded source)
+  if (p.up1 != 1) return "conv_fwd: up1 must be 1";
   if (p.C2 > 0 && !p.src2) return "conv_fwd: src2 missing";
   if (p.shuffle && (p.Cout % (1 << p.shuffle))) return "conv_fwd: shuffle needs Cout % taps == 0";
   if (p.shuffle && ((p.Cout >> p.shuffle) % 8)) return "conv_fwd: shuffle channels must be multiples of 8";
@@ -1238,17 +751,18 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     return "conv_fwd: mask_bits marks a missing mask";
   if (p.xform) {
     const int ep = conv_epi_mode(p), t = conv_fwd_pick(p);
-    if (p.xform < 0 || p.xform > 2 || p.C2 || p.up1 != 1 || !p.xa || !p.xb || (p.xform == 2 && (!p.xc || !p.xz)) ||
-        p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) || (t != 6 && t != 12 && t != 13) ||
-        (p.xcs != 0 && p.xcs != p.C1) || p.head_w ||
-        (p.xform == 1 ? (ep != EPI_STATS && ep != EPI_GENERIC) : (ep != EPI_DGRAD && ep != EPI_DGRAD_NORM)))
-      return "conv_fwd: operand transform needs a 2D single-source row-window conv (norm-input forward / "
-             "norm-output data gradient)";
+    if (p.xform != 1 || p.C2 || !p.xa || !p.xb || p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) ||
+        (t != 6 && t != 12) || (p.xcs != 0 && p.xcs != p.C1) || p.head_w || (ep != EPI_STATS && ep != EPI_GENERIC))
+      return "conv_fwd: operand transform needs a 2D single-source row-window forward of a normalised input";
   }
+  if (p.hg.prob && (!p.hg.t || !p.hg.sums || !p.hg.w || !p.hg.bits || p.C1 != 32 || p.C2 || p.xform ||
+                    p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) || conv_epi_mode(p) != EPI_DGRAD ||
+                    p.route_gy || (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12)))
+    return "conv_fwd: head-on-load needs a 2D 32-channel row-window data gradient";
   if (p.route_gy && (!p.pool_code || (conv_epi_mode(p) != EPI_DGRAD && conv_epi_mode(p) != EPI_DGRAD_NORM) ||
                      !win_eligible(p) || p.KD != 1 || p.OD != 1 ||
                      p.OH % 2 || p.OW % 2 || p.D1 != p.Cout || p.pool_dst || p.mask_scale1 != 1.f ||
-                     (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12 && conv_fwd_pick(p) != 13)))
+                     (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12)))
     return "conv_fwd: fused pool backward needs a 2D row-window data gradient (even dims, one destination, codes)";
   if (p.pool_dst) {
     const int W = p.OW > 128 ? 128 : p.OW;
@@ -1257,8 +771,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
         p.OH % 2 || p.OW % 2 || p.Cout % 8 || p.head_w)
       return "conv_fwd: fused max-pool needs a 2D row-window ReLU forward (even rows, codes buffer)";
   }
-  if (p.tile < 0 || p.tile > 13) return "conv_fwd: bad tile id";
-  if (p.tile == 13 && !win_eligible(p)) return "conv_fwd: 256-pixel row-window tile not applicable";
+  if (p.tile < 0 || p.tile > 12) return "conv_fwd: bad tile id";
   if (p.tile == 12 && (!win_eligible(p) || p.Cout % 64 || p.head_w))
     return "conv_fwd: 64-wide row-window tile not applicable";
   if (p.tile == 10 && !tconv_fwd_eligible(p)) return "conv_fwd: transposed-conv window tile not applicable";
@@ -1274,7 +787,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.head_w) {
     if (!p.head_b || !p.head_logit) return "conv_fwd: fused head needs head_b / head_logit";
     if (p.Cout != 32 || p.drop_rate > 0.f || !p.relu || p.D1 != p.Cout || p.mask1 || p.out_scale != 1.f ||
-        conv_epi_mode(p) != EPI_FWD || (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 13))
+        conv_epi_mode(p) != EPI_FWD || conv_fwd_pick(p) != 6)
       return "conv_fwd: fused head needs a 32-channel ReLU row-window forward";
   }
   if ((long long)p.N * p.ID * p.IH * p.IW >= (1LL << 31) || (long long)p.N * p.OD * p.OH * p.OW >= (1LL << 31))
@@ -1316,7 +829,7 @@ int conv_fwd_pick(const ConvFwdParams& p) {
 
 int conv_fwd_grid(const ConvFwdParams& p) {
   const int t = conv_fwd_pick(p);
-  return (t == 6 || t == 12 || t == 13) ? win_grid(p) : 0;
+  return (t == 6 || t == 12) ? win_grid(p) : 0;
 }
 
 void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
@@ -1326,8 +839,7 @@ void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
   const bool smallc = (p.C1 == 4 || p.C1 == 8) && p.C2 == 0;
   switch (t) {
     case 6:
-    case 12:
-    case 13: {       // row window: R rows x (segment) width, tiles in (row group, segment) order
+    case 12: {       // row window: R rows x (segment) width, tiles in (row group, segment) order
       const int W = p.OW > 128 ? 128 : p.OW;
       const int R = win_rows(p);
       if (p.nz && p.C2) return;
@@ -1352,7 +864,7 @@ void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
     case 10:
       return;
     default: {
-      if (p.up1 != 1 || (p.nz && (smallc || p.C2))) return;
+      if (p.nz && (smallc || p.C2)) return;
       const int BM = (t == 3 || t == 5) ? 256 : 128;
       *rows = (M + BM - 1) / BM;
       *tile_px = BM;
@@ -1369,7 +881,6 @@ hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
     case 5: return launch_cfg<256, 64, 4, 1>(p, s);
     case 6:
     case 12:
-    case 13:
       if (win_bn(p) == 64) return launch_win<64, 256>(p, s);
       return win_bm(p) == 256 ? launch_win<32, 256>(p, s) : launch_win<32, 512>(p, s);
     case 9: return p.C1 == 4 ? launch_win_first<4>(p, s) : launch_win_first<8>(p, s);

@@ -7,6 +7,21 @@
 // builds' launchers take the same host types.
 namespace unet_types {
 
+// Gradient of the segmentation head's input formed on load (head-on-load): the consumer
+// kernel builds dY[p][c] = dlogit(p) * w[c] * (x[p][c] > 0) itself from the per-pixel
+// probability / target, the loss sums and the head input's ReLU bits, so the head
+// backward never writes the full-resolution dY (head.hip::head_dlogit is the formula).
+// prob == nullptr: off.
+struct HeadGrad {
+  const float* prob;          // [P] sigmoid outputs
+  const void* t;              // [P] 16-bit targets
+  const float* sums;          // {I, St, Sp, BCE} of the forward
+  const float* w;             // [C] fp32 head weights
+  const uint8_t* bits;        // [P][C / 8] ReLU bits of the head input
+  const float* gscale;        // device loss scale (nullptr: 1)
+  float inv_total, bce_w;     // 1 / (pixels of the batch), BCE weight (0: Dice only)
+};
+
 // Implicit-GEMM "NT" convolution: out[q][n] = epilogue(sum_{tap,c} X[q*s + tap - pad][c] * W[n][tap][c])
 // GEMM M = output pixels q over [N][OD][OH][OW], GEMM N = Cout, K = taps * Cin.
 // One kernel serves: conv forward, conv dgrad (flipped/transposed weights),
@@ -75,10 +90,8 @@ struct ConvFwdParams {
   // rewritten in LDS before the MFMAs, so a normalisation pass never runs on its own --
   //   xform 1: src1 = pre-norm z, operand y = relu(xa z + xb)   (forward of a normalised
   //            activation's consumer; eval / train alike)
-  //   xform 2: src1 = g (gradient of the norm's output), operand dz = xa g + xb z + xc
-  //            with z = xz (the norm backward's dz)
   // coefficients [C] (xcs = 0, BatchNorm) or [N][C] (xcs = C, GroupNorm; a window lies
-  // in one sample).  xout (optional): the transformed operand's own-window rows are also
+  // in one sample); xc / xz are unused by the conv.  xout (optional): the transformed operand's own-window rows are also
   // stored there (the weight gradient reads them), by output-channel tile 0.
   int xform, xcs;
   const float* xa;
@@ -94,6 +107,8 @@ struct ConvFwdParams {
   float* head_logit;
   int rev;                    // row-window kernels: windows in reverse order (the consumer starts
                               // where its producer ended, on the tail still in the Infinity Cache)
+  HeadGrad hg;                // 2D row-window data gradient of the head input: src1 (dY) formed
+                              // on load (one 32-channel chunk), see HeadGrad
   // filled by conv_fwd_prepare (host): K padded to 64, per-tap pixel deltas / offsets
   int Kpad;
   int tap_delta[27];
@@ -126,10 +141,6 @@ struct WgradParams {
   int bias_mode;
   float* bias_slab;           // [splits][tap_groups][M or Nc] fp32
   int win;                    // 0 = row-window kernel when eligible, -1 = never (A/B tests)
-  // A-operand transform on load (2D row-window kernel, single source, rows 32..128 wide):
-  // a1 = pre-norm z, operand y = relu(xa z + xb) formed in LDS -- the normalised
-  // activation of an 'a' conv is then never stored (its consumer conv normalises on load
-  // too, conv_params.h xform 1).  xa / xb: [M1] (xcs = 0) or [N][M1] (xcs = M1).
   // xform 2 (first-layer window wgrad): b = g (gradient of the normalised output) and the
   // B operand dz = xa g + xb z + xc (z = xz, the pre-norm output) is formed in LDS -- the
   // norm backward's dz of the first layer, read by nothing else, is never materialised
@@ -139,6 +150,8 @@ struct WgradParams {
   const float* xb;
   const float* xc;
   const void* xz;
+  HeadGrad hg;                // window wgrad of the head input conv: the B operand (dY, 32 channels)
+                              // formed on load, see HeadGrad
   // filled by the launcher
   int lqw, lqh, lqd;          // log2 of the pixel grid (power-of-two fast path)
   signed char tap_d[27], tap_h[27], tap_w[27];

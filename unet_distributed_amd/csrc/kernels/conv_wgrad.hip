@@ -24,6 +24,7 @@
 // Reference: the gradients TF computes for Conv2D / Conv2DTranspose kernels
 // and biases in `optimizer.compute_gradients` (`test_dist.py:248`).
 #include "common.h"
+#include "head_grad.h"
 #include "conv_params.h"
 
 namespace unet {
@@ -104,9 +105,6 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
   const int kbeg = split * per;
   const int kend = min(Q, kbeg + per);
   const int nks = kend > kbeg ? (kend - kbeg + BKW - 1) / BKW : 0;
-  const int upA = p.upA;
-  const int upAd = p.AD > 1 ? upA : 1;       // 2D: depth is never upsampled
-  const int AD1 = p.AD / upAd, AH1 = p.AH / upA, AW1 = p.AW / upA;
   const int padd = p.KD > 1 ? p.pad : 0;     // 2D: depth is not padded
   const int Cin_s = p.M1;                    // SMALLC: channels of the first-layer input
 
@@ -143,12 +141,6 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
     }
     const int bd = qd * p.stride - padd, bh = qh * p.stride - p.pad, bw = qw * p.stride - p.pad;
     const int pix0 = ((qn * p.AD + bd) * p.AH + bh) * p.AW + bw;     // window origin (full res)
-    int lo0 = 0, par = 0;
-    if (!SMALLC && upA == 2) {
-      const int cd = bd + padd, ch = bh + p.pad, cw = bw + p.pad;   // centre (stride 1 for the fold)
-      lo0 = ((qn * AD1 + cd / upAd) * AH1 + ch / 2) * AW1 + cw / 2;
-      par = ((cd & 1) << 2) | ((ch & 1) << 1) | (cw & 1);
-    }
     if constexpr (SMALLC) {
 #pragma unroll
       for (int i = 0; i < NA / 4; ++i) {
@@ -187,15 +179,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
         const bool ok = qok && (unsigned)(bd + kd) < (unsigned)p.AD && (unsigned)(bh + kh) < (unsigned)p.AH &&
                         (unsigned)(bw + kw) < (unsigned)p.AW;
         const int fpix = pix0 + (kd * p.AH + kh) * p.AW + kw;
-        int base1;
-        if (upA == 2) {
-          const int lh = (kh - p.pad + ((par >> 1) & 1)) >> 1;
-          const int lw = (kw - p.pad + (par & 1)) >> 1;
-          const int ld = p.AD > 1 ? ((kd - padd + ((par >> 2) & 1)) >> 1) : 0;
-          base1 = (lo0 + (ld * AH1 + lh) * AW1 + lw) * p.M1 * 2;
-        } else {
-          base1 = fpix * p.M1 * 2;
-        }
+        const int base1 = fpix * p.M1 * 2;
         const int base2 = (fpix * p.M2 - p.M1) * 2;
 #pragma unroll
         for (int ci = 0; ci < CPS; ++ci) {
@@ -507,7 +491,10 @@ hipError_t launch_wg(WgradParams p, hipStream_t s) {
 // GEO: 0 = 2D full rows, 1 = 2D segmented rows (Wf = p.QW > W), 2 = 3D (tap group =
 // depth tap); compile-time so the 2D full-row kernel carries no segment / depth state.
 enum { WGEO_2D = 0, WGEO_SEG = 1, WGEO_3D = 2 };
-template <int W, int QO, bool CONCAT, int GEO, int XF = 0>
+// HG: head-on-load (conv_params.h HeadGrad): the B operand (dY of the head input, 32
+// channels, 2D full rows) is formed per window from the head's per-pixel probability,
+// target and ReLU bits instead of being read from memory.
+template <int W, int QO, bool CONCAT, int GEO, bool HG = false>
 __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p) {
   constexpr int BMW = 256, R = BMW / W, HR = R + 2;
   constexpr int HWP = ((W + 2 + 15) / 16) * 16, IPR = HWP / 16, ROWB = HWP * 64;
@@ -517,6 +504,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   constexpr int REDB = 4 * 64 * 16 * 4;                 // one tap of every wave's partials
   constexpr int LDS_BYTES = (XB + YB > REDB) ? XB + YB : REDB;
   static_assert(W >= 8 && W <= 128 && (QO == 1 || QO == 2), "window wgrad shape");
+  static_assert(!HG || (QO == 1 && !CONCAT && GEO == WGEO_2D && BMW == NTHR), "head-on-load B: one 32-channel image");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   char* Xs = smem;
   char* Ys = smem + XB;
@@ -609,6 +597,8 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   // image are then DMA'd as zeros, as on the column-unit path).
   constexpr bool PAIR_PATH = W == 16 && GEO == WGEO_2D;
   constexpr bool pair_ok = PAIR_PATH;   // wgrad_win_eligible: QH % 16 == 0 for 16-wide rows
+  HeadGradCtx hctx{};
+  if constexpr (HG) hctx = head_grad_ctx(p.hg);
   for (int win = w_begin; win < w_end; ++win) {
     const int g0 = (GEO == WGEO_SEG ? win / nseg : win) * R;
     const int col0 = GEO == WGEO_SEG ? (win % nseg) * W : 0;
@@ -633,31 +623,19 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
                                                  off, 0, 0, 0);
       }
     }
-    // XF 2 (B transform, QO = 1, 2D full rows): the pre-norm z of this lane's dY chunks,
-    // loaded beside the DMA; dz = xa g + xb z + xc is formed in LDS below
-    u32x4 xzv[XF == 2 ? (YI + 3) / 4 : 1];
-    float bxa[8], bxb[8], bxc[8];
-    if constexpr (XF == 2) {
-      static_assert(QO == 1 && GEO == WGEO_2D, "B transform: one 32-channel dY image, 2D full rows");
-      const size_t crow = p.xcs ? (size_t)(g0 / H) * p.xcs : 0;
+    if constexpr (HG) {
+      // thread t forms window pixel t (slot t; logical chunk k at physical k ^ swizzle)
+      const int pix = g0 * W + tid;
+      u32x4 v[4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+      if (pix < Mq) head_grad_pixel(p.hg, hctx, pix, v);
+      const int sw = ((tid >> 3) & 1) << 1;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        bxa[e] = p.xa[crow + co0 + lchunk * 8 + e];
-        bxb[e] = p.xb[crow + co0 + lchunk * 8 + e];
-        bxc[e] = p.xc[crow + co0 + lchunk * 8 + e];
-      }
-#pragma unroll
-      for (int qq = 0; qq < (YI + 3) / 4; ++qq) {
-        const int k = wave + 4 * qq;
-        const int pix = g0 * W + k * 16 + lslot;
-        if (k < YI && pix < Mq)
-          xzv[qq] = *(const u32x4*)((const h16*)p.xz + (size_t)pix * p.Nc + co0 + lchunk * 8);
-      }
+      for (int k = 0; k < 4; ++k) *(u32x4*)(Ys + tid * 64 + 16 * (k ^ sw)) = v[k];
     }
 #pragma unroll
     for (int qq = 0; qq < (YI + 3) / 4; ++qq) {
       const int k = wave + 4 * qq;
-      if (k < YI) {
+      if (!HG && k < YI) {
         const int o = k / (BMW / 16), sb = (k - o * (BMW / 16)) * 16;   // image o, first slot
         // window slot sb -> row g0 + sb / W, column col0 + sb % W (W = 8: one segment,
         // the 16-slot run covers two consecutive rows contiguous in memory)
@@ -668,57 +646,6 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
       }
     }
     __syncthreads();
-    if constexpr (XF == 2) {
-#pragma unroll
-      for (int qq = 0; qq < (YI + 3) / 4; ++qq) {
-        const int k = wave + 4 * qq;
-        if (k < YI && g0 * W + k * 16 + lslot < Mq) {
-          char* a = Ys + k * 1024 + lslot * 64 + (lane & 3) * 16;
-          float gv[8], zv[8];
-          unpack8(*(const u32x4*)a, gv);
-          unpack8(xzv[qq], zv);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) gv[e] = fmaf(bxa[e], gv[e], fmaf(bxb[e], zv[e], bxc[e]));
-          *(u32x4*)a = pack8(gv);
-        }
-      }
-      __syncthreads();
-    }
-    if constexpr (XF == 1) {
-      // A operand normalised on load: y = relu(xa z + xb) of the halo image in place.  A
-      // thread keeps the DMA lane role of its lane (slot lane >> 2, physical chunk lane & 3,
-      // logical chunk = physical ^ swizzle), so its 8 channels are fixed; padding slots
-      // keep the DMA's zeros (the activation's zero padding).
-      static_assert(GEO == WGEO_2D && !CONCAT && !ROWSWZ, "A transform: 2D single-source rows >= 16");
-      const int xsl = lane >> 2, xpc = lane & 3;
-      const int xlc = xpc ^ (((xsl >> 3) & 1) << 1);
-      const size_t crow = p.xcs ? (size_t)(g0 / H) * p.xcs : 0;
-      float xa[8], xb[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        xa[e] = p.xa[crow + ca0 + xlc * 8 + e];
-        xb[e] = p.xb[crow + ca0 + xlc * 8 + e];
-      }
-#pragma unroll
-      for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
-        const int k = wave + 4 * qq;
-        if (k < XI) {
-          const int hr = k / IPR, j = k - hr * IPR;
-          const int gr = g0 - 1 + hr;
-          const int col = 16 * j + xsl - 1;
-          const bool row_in = (hr > 0 || top_in) && (hr < R + 1 || bot_in);
-          if (row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W) {
-            char* a = Xs + k * 1024 + xsl * 64 + xpc * 16;
-            float v[8];
-            unpack8(*(const u32x4*)a, v);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(xa[e], v[e], xb[e]), 0.f);
-            *(u32x4*)a = pack8(v);
-          }
-        }
-      }
-      __syncthreads();
-    }
     const char* Yq = Ys + qo * (BMW * 64);
     // (one column unit per wave: with two, the 128-wide QO = 2 case spills)
     if constexpr (UNITS_PATH) {
@@ -1324,21 +1251,13 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
 template <int W, int QO, int GEO>
 hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
   const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.KD * launch_splits(p);
-  if constexpr (GEO == WGEO_2D && W >= 32) {
-    if (p.xform == 1) {
-      hipLaunchKernelGGL((wgrad_win_kernel<W, QO, false, GEO, 1>), dim3(grid), dim3(NTHR), 0, s, p);
+  if constexpr (GEO == WGEO_2D && QO == 1) {
+    if (p.hg.prob) {
+      hipLaunchKernelGGL((wgrad_win_kernel<W, QO, false, GEO, true>), dim3(grid), dim3(NTHR), 0, s, p);
       return hipGetLastError();
     }
   }
-  if constexpr (GEO == WGEO_2D && W == 128 && QO == 1) {
-    if (p.xform == 2) {
-      if (p.M2 > 0)
-        hipLaunchKernelGGL((wgrad_win_kernel<W, QO, true, GEO, 2>), dim3(grid), dim3(NTHR), 0, s, p);
-      else
-        hipLaunchKernelGGL((wgrad_win_kernel<W, QO, false, GEO, 2>), dim3(grid), dim3(NTHR), 0, s, p);
-      return hipGetLastError();
-    }
-  }
+  if (p.hg.prob) return hipErrorInvalidValue;
   if (p.M2 > 0)
     hipLaunchKernelGGL((wgrad_win_kernel<W, QO, true, GEO>), dim3(grid), dim3(NTHR), 0, s, p);
   else
@@ -1421,15 +1340,14 @@ const char* wgrad_check(const WgradParams& p) {
     if (p.M1 % 8 || p.M2 % 8) return "wgrad: channel split must be a multiple of 8";
     if (KT % c.NTAP) return "wgrad: taps not divisible by the tap group";
   }
-  if (p.xform == 2 && ((!wgrad_win_first_eligible(p) && !(wgrad_win_eligible(p) && p.QW == 128 && p.QD == 1 &&
-                                                          p.KD == 1 && p.Nc % 64 != 0)) ||
-                       !p.xa || !p.xb || !p.xc || !p.xz || (p.xcs != 0 && p.xcs != p.Nc) ||
-                       (p.xcs && p.QH % (256 / p.QW))))
-    return "wgrad: B transform (dz on load) needs the first-layer or a 128-wide 32-channel window wgrad";
-  if (p.xform == 1 && (!wgrad_win_eligible(p) || p.M2 != 0 || p.KD != 1 || p.QD != 1 ||
-                  (p.QW != 32 && p.QW != 64 && p.QW != 128) || !p.xa || !p.xb || (p.xcs != 0 && p.xcs != p.M1)))
-    return "wgrad: A transform needs a 2D single-source row-window wgrad, rows 32 / 64 / 128 wide";
-  if (p.upA != 1 && p.upA != 2) return "wgrad: upA must be 1 or 2";
+  if (p.xform != 0 && p.xform != 2) return "wgrad: xform must be 0 or 2";
+  if (p.xform == 2 && (!wgrad_win_first_eligible(p) || !p.xa || !p.xb || !p.xc || !p.xz ||
+                       (p.xcs != 0 && p.xcs != p.Nc) || (p.xcs && p.QH % (256 / p.QW))))
+    return "wgrad: B transform (dz on load) needs the first-layer window wgrad";
+  if (p.upA != 1) return "wgrad: upA must be 1 (nearest upsampling is materialised)";
+  if (p.hg.prob && (!p.hg.t || !p.hg.sums || !p.hg.w || !p.hg.bits || !wgrad_win_eligible(p) || p.Nc != 32 ||
+                    p.M2 != 0 || p.KD != 1 || p.QD != 1 || p.QW > 128 || p.xform))
+    return "wgrad: head-on-load B needs a 2D single-source row-window wgrad with 32 output channels";
   if (p.splits < 1) return "wgrad: splits must be >= 1";
   if (p.split_lo < 0 || p.split_n < 0 || p.split_lo + launch_splits(p) > p.splits)
     return "wgrad: split range [split_lo, split_lo + split_n) outside [0, splits)";
@@ -1437,16 +1355,12 @@ const char* wgrad_check(const WgradParams& p) {
 }
 
 hipError_t wgrad_launch(const WgradParams& p0, hipStream_t s) {
-  // UNET_WGRAD_XCD: workgroup -> XCD map of the weight-gradient kernels (bit 0 window
-  // kernels, bit 1 tiled kernel; read once per process).  Default 1: same-box sweep of
-  // the headline step 43.4k -> 44.1k img/s (the 64 tiles of a split share one L2 instead
-  // of fetching each dY / input window into several); the tiled kernel's map is neutral.
-  static const int xcd = [] {
-    const char* e = getenv("UNET_WGRAD_XCD");
-    return e ? atoi(e) : 1;
-  }();
+  // workgroup -> XCD map of the window weight gradients: the 64 tiles of a split run on
+  // one XCD and share its L2 instead of fetching each dY / input window into several
+  // (same-box sweep of the headline step 43.4k -> 44.1k img/s; the tiled kernel's map
+  // measured neutral and stays off)
   WgradParams p = p0;
-  p.xcd = xcd;
+  p.xcd = 1;
   const WgradCfg c = wgrad_pick(p);
   if (wgrad_win_first_eligible(p)) return p.M1 == 4 ? launch_wgrad_win_first<4>(p, s) : launch_wgrad_win_first<8>(p, s);
   if (wgrad_tconv_win_eligible(p)) {

@@ -1,0 +1,508 @@
+// Row-window 3x3 conv kernels (fine UNet levels), shared by the instantiation units
+// conv_win_b32.hip (32-channel tiles) and conv_win_b64.hip (64-channel tiles): each
+// builds one launch_win<BN, BM> so the ~150 kernel variants compile in parallel.
+// conv_fwd.hip picks the tile (win_bn / win_bm) and dispatches.
+#pragma once
+#include "common.h"
+#include "conv_params.h"
+#include "conv_epilogue.h"
+#include "head_grad.h"
+
+namespace unet {
+
+// GEO: 0 = 2D full rows (Wf = W), 1 = 2D segmented rows (Wf = p.OW, a multiple of W),
+// 2 = 3D full rows (three depth taps).  Compile-time so the common 2D case carries no
+// segment / depth state (extra SGPR state spilled to VGPR lanes inside the chunk loop).
+enum { GEO_2D = 0, GEO_SEG = 1, GEO_3D = 2 };
+
+// Output-channel tile of the row-window conv: 64 on rows 16..64 wide where Cout allows
+// it (same-box sweep of the headline step: +2.8 % at W = 16, +0.5 % at 32, +0.4 % at 64,
+// -0.3 % at 128 -> 32 there), else 32; a fused head needs the 32-channel tile.  64
+// halves the halo image's LDS-DMA and fragment reads per MFMA and doubles the MFMA work
+// per synchronisation.  tile 12 / 6 force 64 / 32 (tests).
+inline int win_bn(const ConvFwdParams& p) {
+  if (p.tile == 12) return 64;
+  if (p.tile == 6) return 32;
+  const int W = p.OW > 128 ? 128 : p.OW;
+  return (p.Cout % 64 == 0 && W <= 64 && !p.head_w) ? 64 : 32;
+}
+// Window pixels: 256 for 16-wide rows and for the 64-channel tile (its accumulators,
+// 4 x 4 fragments per wave, and LDS then still fit two workgroups per CU), else 512.
+// (A 256-pixel 32-channel window on 32..128-wide rows -- three workgroups per CU --
+// measured -0.4 % at W = 64 and -1 % at 128 and was dropped.)
+inline int win_bm(const ConvFwdParams& p) {
+  const int W = p.OW > 128 ? 128 : p.OW;
+  return (W == 16 || win_bn(p) == 64) ? 256 : 512;
+}
+inline int win_rows(const ConvFwdParams& p) {
+  const int W = p.OW > 128 ? 128 : p.OW;
+  return win_bm(p) / W;
+}
+inline int win_grid(const ConvFwdParams& p) {
+  const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
+  const int rows = p.N * p.OD * p.OH;
+  const int R = win_rows(p);
+  return ((rows + R - 1) / R) * (p.OW / W) * (p.Cout / win_bn(p));
+}
+// (BN, BM, row width) combinations win_bn / win_bm can select (the 64-channel tile also
+// on 128-wide rows: tile 12 forces it there for tests)
+template <int BN, int BM>
+constexpr bool win_tile_built(int W) {
+  return BN == 64 ? BM == 256 : (BM == 256 ? W == 16 : W != 16);
+}
+
+template <int BN, int BM>
+hipError_t launch_win(const ConvFwdParams& p, hipStream_t s);
+
+#ifdef UNET_WIN_IMPL
+namespace {
+
+constexpr int NTHR = 256;
+
+// ---------------------------------------------------------------------------------
+// Row-window conv (fine UNet levels): 2D, 3x3, stride 1, 'same' padding, full-width rows.
+//
+// The implicit GEMM above re-gathers the input once per tap: at the 128^2 / 64^2
+// levels (Cin, Cout <= 64) that 9x L2->LDS traffic, not the MFMA, bounds it.  Here a
+// workgroup owns BM = 512 output pixels = R = 512/W whole rows of the flattened
+// (n, h) row space and BN output channels.  Per 32-channel input chunk it stages the
+// (R+2) x (W+2) halo image of those rows ONCE in LDS (zero columns at the left/right
+// border come free from out-of-range buffer loads), plus the chunk's 9 x BN weight
+// rows, and then runs all nine taps as MFMAs on shifted LDS addresses.  Rows that
+// cross an image boundary inside the window are handled by skipping the (wave-uniform)
+// MFMAs of taps whose input row falls outside the output row's image.
+//
+// LDS images: 64-byte pixel slots (32 bf16); the halo image has rows of HWP = W + 4
+// slots (a multiple of 4: every row starts on a 256-byte bank row) and stores 16-byte
+// chunk c of the pixel in column hc at c ^ ((hc >> 1) & 3).  Fragment reads are 16
+// consecutive columns from any start (any tap shift): conflict free, and because the
+// swizzle depends only on the column, a lane's address is one of three per-lane bases
+// (one per horizontal tap) plus a compile-time immediate (row, tile) -- no per-tap
+// address registers.  Weight rows (tap, n) use the same swizzle on the row index.
+
+// XF (2D, single source): operand transform of the src1 halo image in LDS before the
+// MFMAs -- 1: conv_params.h xform 1, y = relu(xa z + xb) (the window's own rows of the
+// transformed operand go to xout); 3: head-on-load, the halo image of dY (32 channels)
+// is formed from the head's per-pixel probability, target and ReLU bits (p.hg,
+// head_grad.h) instead of being read from memory.
+template <int W, int BN, int BM, bool CONCAT, int EPI, int GEO, int XF = 0>
+__global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
+  static_assert(BN == 32 || BN == 64, "row-window tile is 32 or 64 output channels wide");
+  static_assert(XF == 0 || ((XF == 1 || XF == 3) && GEO == GEO_2D && !CONCAT),
+                "operand transform: 2D single-source windows");
+  constexpr int R = BM / W, HR = R + 2;
+  // halo row pitch in 64-byte pixel slots: W + 2 columns rounded up to a multiple of 4
+  // (every row starts on a 256-byte bank row); the DMA fills the image as one linear
+  // run of slots, so rows need not align to the 16-slot DMA instructions
+  constexpr int HWP = W + 4;
+  constexpr int ROWB = HWP * 64;
+  constexpr int XI = (HR * HWP + 15) / 16, WI = 9 * BN / 16;
+  constexpr int XB = XI * 1024, WB = WI * 1024;
+  constexpr int EPIB = (EPI == EPI_STATS || EPI == EPI_DGRAD_NORM) ? epi_lds_bytes<BM, BN>() : BM * (BN + 4) * 2;
+  constexpr int LDS_BYTES = (XB + WB > EPIB) ? XB + WB : EPIB;
+  constexpr int WMP = BM / 4;                   // pixels per wave
+  constexpr int TM = WMP / 16, TN = BN / 16;
+  constexpr int TPR = W / 16;                   // 16-pixel tiles per row
+  static_assert(W >= 16 && W <= 128 && BM % W == 0 && WMP % 16 == 0, "row width");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  char* Xs = smem;
+  char* Ws = smem + XB;
+
+  // wave index as a scalar: every per-wave quantity below (rows, DMA slots) stays in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // Row space: rows g = (n, d, h) of Wf pixels.  Rows wider than 128 are cut into
+  // nseg W-wide segments (a window = R rows x one segment; its halo columns -1 / W are
+  // the neighbouring segments' pixels).  3D (KD = 3): depth tap dz reads the halo rows
+  // of slice d + dz - 1, i.e. row g + (dz - 1) H, as three more 32-channel K chunks.
+  constexpr int KD = GEO == GEO_3D ? 3 : 1;
+  const int H = p.OH;
+  const int D = GEO == GEO_3D ? p.OD : 1;
+  const int Wf = GEO == GEO_SEG ? p.OW : W;
+  const int nseg = GEO == GEO_SEG ? p.OW / W : 1;
+  const int rows_total = p.N * D * H;
+  const int M = rows_total * Wf;
+  const int tiles_n = p.Cout / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm0 = bid / tiles_n, tn = bid % tiles_n;
+  const int tm = p.rev ? (int)(gridDim.x / tiles_n) - 1 - tm0 : tm0;
+  const int rgi = GEO == GEO_SEG ? tm / nseg : tm;
+  const int g0 = rgi * R, col0 = GEO == GEO_SEG ? (tm - rgi * nseg) * W : 0;
+  const int n0 = tn * BN;
+  const int dsl = GEO == GEO_3D ? (g0 / H) % D : 0;   // depth slice of the window
+  const int Cin = p.C1 + p.C2;
+  const int nchunks = Cin >> 5;
+  constexpr int OOB = 0x7fffffff;
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)p.src1, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.src2 ? p.src2 : p.src1), (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
+
+  // Wave w owns an RW-row x 16 TC-column strip of the window (StripTiles): an A
+  // fragment read from halo row r at horizontal shift dw feeds the output rows r - dh
+  // of all three vertical taps, so per chunk a wave reads 3 (RW + 2) TC fragments
+  // instead of 9 RW TC (2-2.4x less LDS read traffic than one fragment per tap).
+  constexpr int TC = W >= 128 ? 2 : 1;            // 16-pixel column tiles per strip
+  constexpr int NCS = W / (16 * TC);              // column strips per window row
+  constexpr int RW = R / (4 / NCS);               // rows per strip
+  static_assert(NCS <= 4 && 4 % NCS == 0 && RW * TC == TM, "strip map");
+  using Map = StripTiles<W, RW, TC, NCS>;
+  const int r0 = (wave / NCS) * RW, c0 = (wave % NCS) * 16 * TC;
+  // H % R == 0 (win_eligible): a window never spans two images, so the only rows of
+  // another image are the halo rows above / below it, which the DMA fills with zeros
+  // (the 'same' padding) -- the tap loop needs no image-edge branches at all, and the
+  // whole chunk is one basic block the scheduler can pipeline LDS reads through.
+  const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int fsub = lane >> 4, fr = lane & 15;
+  // per-lane fragment bases: horizontal tap dw -> column c0 + fr + dw of halo row r0
+  // (c0 is a multiple of 16, so the swizzle only depends on fr + dw)
+  int xbase[3];
+#pragma unroll
+  for (int dw = 0; dw < 3; ++dw) {
+    const int hc = fr + dw;
+    xbase[dw] = r0 * ROWB + c0 * 64 + hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3));
+  }
+  const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
+  // one 32-channel chunk: per horizontal tap, the three vertical taps' weights are
+  // held in registers and every halo-row fragment feeds up to three output rows
+  auto chunk_mfmas = [&]() {
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw) {
+      h16x8 wf[3][TN];
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) wf[dh][j] = *(const h16x8*)(Ws + ((3 * dh + dw) * BN + 16 * j) * 64 + wbase);
+#pragma unroll
+      for (int hr = 0; hr < RW + 2; ++hr) {
+#pragma unroll
+        for (int ci = 0; ci < TC; ++ci) {
+          const h16x8 xf = *(const h16x8*)(Xs + xbase[dw] + hr * ROWB + ci * 16 * 64);
+#pragma unroll
+          for (int dh = 0; dh < 3; ++dh) {
+            const int ri = hr - dh;
+            if (ri < 0 || ri >= RW) continue;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[ri * TC + ci][j] = mfma16(wf[dh][j], xf, acc[ri * TC + ci][j]);
+          }
+        }
+      }
+    }
+  };
+  // LDS-DMA lane roles: lane l fills physical 16-byte chunk (l & 3) of slot (l >> 2) of a
+  // 16-slot run; it loads logical chunk (l & 3) ^ swizzle(slot), which depends only on l
+  // because every run starts at a multiple of 16 slots.
+  const int lslot = lane >> 2;
+  const int lchunk = (lane & 3) ^ ((lslot >> 1) & 3);
+
+  // one 32-channel chunk of depth tap kd (input rows shifted by gsh): stage, then MFMAs
+  auto run_chunk = [&](const int kc, const int kd, const int gsh) {
+      const bool from1 = !CONCAT || (kc << 5) < p.C1;
+      const int C = from1 ? p.C1 : p.C2;
+      const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
+      {
+        // halo image: row hr, slot hc holds pixel (g0 - 1 + hr + gsh, col0 + hc - 1);
+        // instruction (hr, j) covers slots 16j .. 16j + 15 of row hr.  Rows outside the
+        // tensor / image and columns outside [0, Wf) load zeros (out-of-range offsets).
+        const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
+#pragma unroll
+        for (int q = 0; q < (XI + 3) / 4; ++q) {
+          const int k = wave + 4 * q;
+          if (k < XI) {
+            const int sl = 16 * k + lslot;                  // this lane's halo slot
+            const int hr = sl / HWP, hc = sl - hr * HWP;    // its row / column
+            const int gr = g0 - 1 + hr + gsh;
+            const int col = col0 + hc - 1;
+            const bool row_in = hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in);   // same image
+            // (slots past W + 1 are never read: skip them, they would be real pixels of
+            // the next segment on segmented rows)
+            const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)Wf &&
+                            (GEO != GEO_SEG || hc <= W + 1);
+            const int lch = (lane & 3) ^ ((hc >> 1) & 3);
+            const int off = ok ? ((gr * Wf + col) * C + cb + lch * 8) * 2 : OOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
+                                                     16, off, 0, 0, 0);
+          }
+        }
+        // weight image: row r = tap * 32 + n (64 bytes = this chunk's 32 input channels)
+        const int wl = (lslot * p.Kpad + (kc << 5) + lchunk * 8) * 2;
+#pragma unroll
+        for (int q = 0; q < (WI + 3) / 4; ++q) {
+          const int k = wave + 4 * q;
+          if (k < WI) {
+            const int tap = k / (BN / 16), nb = (k % (BN / 16)) * 16;     // wave-uniform
+            const int off = ((n0 + nb) * p.Kpad + (kd * 9 + tap) * Cin) * 2 + wl;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024),
+                                                     16, off, 0, 0, 0);
+          }
+        }
+      }
+      __syncthreads();
+      chunk_mfmas();
+  };
+  if constexpr (GEO == GEO_3D) {
+    // depth taps whose input slice is padding contribute nothing: skip them
+    const int kd_lo = dsl == 0 ? 1 : 0, kd_hi = dsl == D - 1 ? 2 : 3;
+    for (int kd = kd_lo; kd < kd_hi; ++kd)
+      for (int kc = 0; kc < nchunks; ++kc) {
+        if (kc || kd != kd_lo) __syncthreads();   // previous chunk's fragment reads are done
+        run_chunk(kc, kd, (kd - 1) * H);
+      }
+  } else if constexpr (GEO == GEO_SEG) {
+    for (int kc = 0; kc < nchunks; ++kc) {
+      if (kc) __syncthreads();                    // previous chunk's fragment reads are done
+      run_chunk(kc, 0, 0);
+    }
+  } else {
+    // 2D full rows: the same staging with compile-time row pitch and no segment / depth
+    // offsets, spelled out (through run_chunk the scheduler keeps ~100 more scalar
+    // instructions per chunk and spills SGPRs to VGPR lanes: 2-4 % slower, A/B measured)
+    // operand transform: thread t owns logical 16-byte chunk xlc = t & 3 (channels
+    // cb + 8 xlc ..) of slots (t >> 2) + 64 j, so its 8 channels' coefficients are fixed
+    // per chunk; the slot's physical chunk is xlc ^ swizzle(column), as the DMA wrote it
+    constexpr int XNJ = XF == 1 ? (XI * 64 + NTHR - 1) / NTHR : 1;
+    const int xlc = tid & 3, xs0 = tid >> 2;
+    auto xslot = [&](const int j, int& hr, int& hc, int& gr, bool& ok) {
+      const int sl = xs0 + (NTHR / 4) * j;
+      hr = sl / HWP;
+      hc = sl - hr * HWP;
+      gr = g0 - 1 + hr;
+      ok = hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)gr < (unsigned)rows_total &&
+           (unsigned)(hc - 1) < (unsigned)W;
+      return sl;
+    };
+    const size_t xsample = XF == 1 ? (size_t)(g0 / H) * p.xcs : 0;   // the window's sample (GroupNorm rows)
+    for (int kc = 0; kc < nchunks; ++kc) {
+      const bool from1 = !CONCAT || (kc << 5) < p.C1;
+      const int C = from1 ? p.C1 : p.C2;
+      const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
+      if (kc) __syncthreads();
+      {
+        const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
+#pragma unroll
+        for (int q = 0; q < (XI + 3) / 4; ++q) {
+          const int k = wave + 4 * q;
+          if (XF != 3 && k < XI) {
+            const int sl = 16 * k + lslot;
+            const int hr = sl / HWP, hc = sl - hr * HWP;
+            const int gr = g0 - 1 + hr;
+            const int col = hc - 1;
+            const bool row_in = hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in);
+            const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+            const int lch = (lane & 3) ^ ((hc >> 1) & 3);
+            const int off = ok ? ((gr * W + col) * C + cb + lch * 8) * 2 : OOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
+                                                     16, off, 0, 0, 0);
+          }
+        }
+        const int wl = (lslot * p.Kpad + (kc << 5) + lchunk * 8) * 2;
+#pragma unroll
+        for (int q = 0; q < (WI + 3) / 4; ++q) {
+          const int k = wave + 4 * q;
+          if (k < WI) {
+            const int tap = k / (BN / 16), nb = (k % (BN / 16)) * 16;
+            const int off = ((n0 + nb) * p.Kpad + tap * Cin) * 2 + wl;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024),
+                                                     16, off, 0, 0, 0);
+          }
+        }
+      }
+      if constexpr (XF == 3) {
+        // head-on-load halo image (one 32-channel chunk): every slot of the image is
+        // written (zeros outside the tensor / image, like the DMA's out-of-range loads);
+        // a thread's slots' pixel data are loaded first, then formed and stored.  (One
+        // slot per thread: 3 loads per slot; a chunk per thread -- conflict-free 16-byte
+        // stores but 4x the loads -- measured -0.8 % on the step.)
+        constexpr int NSL = XI * 16, HJ = (NSL + NTHR - 1) / NTHR;
+        const HeadGradCtx hctx = head_grad_ctx(p.hg);
+        float hpr[HJ], htv[HJ];
+        uint32_t hbits[HJ];
+#pragma unroll
+        for (int j = 0; j < HJ; ++j) {
+          const int sl = tid + NTHR * j;
+          const int hr = sl / HWP, hc = sl - hr * HWP;
+          const int gr = g0 - 1 + hr, col = hc - 1;
+          const bool ok = sl < NSL && hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in) &&
+                          (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+          const int pix = ok ? gr * W + col : 0;
+          hpr[j] = p.hg.prob[pix];
+          htv[j] = bits2f(((const uint16_t*)p.hg.t)[pix]);
+          hbits[j] = ok ? ((const uint32_t*)p.hg.bits)[pix] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < HJ; ++j) {
+          const int sl = tid + NTHR * j;
+          if (sl >= NSL) continue;
+          const int hc = sl % HWP;
+          const float dz = head_dlogit(hpr[j], htv[j], hctx.a, hctx.bb, hctx.inv_total, hctx.bce_w, hctx.gscale);
+          const int sw = (hc >> 1) & 3;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float o[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float v = dz * hctx.w[8 * k + e];
+              o[e] = ((hbits[j] >> (8 * k + e)) & 1u) ? v : 0.f;
+            }
+            *(u32x4*)(Xs + sl * 64 + 16 * (k ^ sw)) = pack8(o);
+          }
+        }
+      }
+      __syncthreads();
+      if constexpr (XF == 1) {
+        float xa[8], xb[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const size_t ci = xsample + cb + xlc * 8 + e;
+          xa[e] = p.xa[ci];
+          xb[e] = p.xb[ci];
+        }
+#pragma unroll
+        for (int j = 0; j < XNJ; ++j) {
+          int hr, hc, gr;
+          bool ok;
+          const int sl = xslot(j, hr, hc, gr, ok);
+          if (!ok) continue;                              // padding stays the DMA's zeros
+          char* a = Xs + sl * 64 + 16 * (xlc ^ ((hc >> 1) & 3));
+          float v[8];
+          unpack8(*(const u32x4*)a, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(xa[e], v[e], xb[e]), 0.f);
+          const u32x4 o = pack8(v);
+          *(u32x4*)a = o;
+          // the window's own rows (once: output-channel tile 0) -> xout
+          if (p.xout && tn == 0 && hr >= 1 && hr <= R)
+            *(u32x4*)((h16*)p.xout + (size_t)(gr * W + hc - 1) * C + cb + xlc * 8) = o;
+        }
+        __syncthreads();
+      }
+      chunk_mfmas();
+    }
+  }
+  __syncthreads();
+  if constexpr (GEO == GEO_SEG)
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, W, W>(p, acc, smem, g0, n0, M, wave, 0, lane, tid, Wf,
+                                                                 col0, tm);
+  else if constexpr (GEO == GEO_2D)
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0,
+                                                                 0, tm);
+  else
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0, 0, tm);
+}
+
+}  // namespace
+
+template <int BN, int BM>
+hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
+  const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
+  const int grid = win_grid(p);
+  const bool cc = p.C2 > 0;
+  const int epi = conv_epi_mode(p);
+  const int geo = p.KD == 3 ? GEO_3D : (p.OW > W ? GEO_SEG : GEO_2D);
+#define WIN_EPI(WW, CC, GG)                                                                               \
+  if (epi == EPI_FWD)                                                                                     \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_FWD, GG>), dim3(grid), dim3(NTHR), 0, s, p);     \
+  else if (epi == EPI_DGRAD)                                                                              \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_DGRAD, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
+  else if (epi == EPI_STATS)                                                                              \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_STATS, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
+  else if (epi == EPI_DGRAD_NORM && !CC)                                                                  \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD_NORM, GG>), dim3(grid), dim3(NTHR), 0, s, p); \
+  else if (epi == EPI_DGRAD_NORM)                                                                         \
+    return hipErrorInvalidValue;                                                                          \
+  else                                                                                                    \
+    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_GENERIC, GG>), dim3(grid), dim3(NTHR), 0, s, p);
+#define WIN_GEO(WW, CC)                                                                                   \
+  if (geo == GEO_3D) {                                                                                    \
+    WIN_EPI(WW, CC, GEO_3D)                                                                               \
+  } else {                                                                                                \
+    WIN_EPI(WW, CC, GEO_2D)                                                                               \
+  }
+#define WIN_CASE(WW)                                                                                      \
+  case WW:                                                                                                \
+    if constexpr (win_tile_built<BN, BM>(WW)) {                                                           \
+      if (cc) {                                                                                           \
+        WIN_GEO(WW, true)                                                                                 \
+      } else {                                                                                            \
+        WIN_GEO(WW, false)                                                                                \
+      }                                                                                                   \
+    } else {                                                                                              \
+      return hipErrorInvalidValue;                                                                        \
+    }                                                                                                     \
+    break;
+#define XF_CASE(WW)                                                                                           \
+  case WW:                                                                                                    \
+    if constexpr (win_tile_built<BN, BM>(WW)) {                                                               \
+      if (epi == EPI_STATS)                                                                                   \
+        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_STATS, GEO_2D, 1>), dim3(grid), dim3(NTHR), 0, s, p); \
+      else if (epi == EPI_GENERIC)                                                                            \
+        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_GENERIC, GEO_2D, 1>), dim3(grid), dim3(NTHR), 0, s, p); \
+      else                                                                                                    \
+        return hipErrorInvalidValue;                                                                          \
+    } else {                                                                                                  \
+      return hipErrorInvalidValue;                                                                            \
+    }                                                                                                         \
+    break;
+  if (p.hg.prob) {                      // head-on-load data gradient (conv_fwd_prepare checks the shape)
+    if (epi != EPI_DGRAD || geo != GEO_2D) return hipErrorInvalidValue;
+    switch (W) {
+#define HG_CASE(WW)                                                                                       \
+  case WW:                                                                                                \
+    if constexpr (win_tile_built<BN, BM>(WW))                                                             \
+      hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_2D, 3>), dim3(grid), dim3(NTHR), 0, s, p); \
+    else                                                                                                  \
+      return hipErrorInvalidValue;                                                                        \
+    break;
+      HG_CASE(16)
+      HG_CASE(32)
+      HG_CASE(64)
+      HG_CASE(128)
+#undef HG_CASE
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  if (p.xform) {                        // operand transform: 2D single source (conv_fwd_prepare)
+    switch (W) {
+      XF_CASE(16)
+      XF_CASE(32)
+      XF_CASE(64)
+      XF_CASE(128)
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+#undef XF_CASE
+  if (geo == GEO_SEG) {                 // 3D volumes wider than 128 are not window-eligible
+    if constexpr (!win_tile_built<BN, BM>(128)) return hipErrorInvalidValue;
+    if (cc) {
+      WIN_EPI(128, true, GEO_SEG)
+    } else {
+      WIN_EPI(128, false, GEO_SEG)
+    }
+    return hipGetLastError();
+  }
+  switch (W) {
+    WIN_CASE(16)
+    WIN_CASE(32)
+    WIN_CASE(64)
+    WIN_CASE(128)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef WIN_CASE
+#undef WIN_GEO
+#undef WIN_EPI
+  return hipGetLastError();
+}
+#endif  // UNET_WIN_IMPL
+
+}  // namespace unet

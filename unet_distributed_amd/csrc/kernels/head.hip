@@ -11,6 +11,7 @@
 //   dx[p][c] = dz w[c] * (x[p][c] > 0)   (ReLU of conv9b folded in)
 //   dW[c] = sum dz x[p][c], db = sum dz   -> per-block partials, reduced deterministically.
 #include "common.h"
+#include "head_grad.h"
 
 namespace unet {
 
@@ -163,9 +164,7 @@ __global__ void __launch_bounds__(HT) head_bwd_kernel(const h16* __restrict__ x,
     const int p = (int)(i / CP);
     const float pr = prob[p];
     const float tv = (float)t[p];
-    float dz = (a * tv + bb) * pr * (1.f - pr);
-    dz += bce_w * (pr - tv) * inv_total;
-    dz *= gscale;
+    const float dz = head_dlogit(pr, tv, a, bb, inv_total, bce_w, gscale);
     if (cc == 0) gb += dz;
     float f[8], o[8];
     unpack8(*(const u32x4*)(x + i * 8), f);
@@ -174,7 +173,9 @@ __global__ void __launch_bounds__(HT) head_bwd_kernel(const h16* __restrict__ x,
       gw[e] += dz * f[e];
       o[e] = f[e] > 0.f ? dz * wr[e] : 0.f;      // ReLU of the head's input folded in
     }
-    *(u32x4*)(dx + i * 8) = pack8(o);
+    // dx == nullptr (head-on-load): the consumers form dx themselves (head_grad.h); only
+    // the head's weight / bias gradients are reduced here
+    if (dx) *(u32x4*)(dx + i * 8) = pack8(o);
   }
   // lanes l, l + CP, l + 2CP, ... hold the same channels: fold them, then across waves
 #pragma unroll

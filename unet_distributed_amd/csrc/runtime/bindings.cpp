@@ -58,6 +58,20 @@ const void* getp(const py::dict& d, const char* k) {
 
 hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// head-on-load fields (conv_params.h HeadGrad), hg_* keys of a conv / wgrad dict
+HeadGrad head_grad(const py::dict& d) {
+  HeadGrad h{};
+  h.prob = (const float*)getp(d, "hg_prob");
+  h.t = getp(d, "hg_t");
+  h.sums = (const float*)getp(d, "hg_sums");
+  h.w = (const float*)getp(d, "hg_w");
+  h.bits = (const uint8_t*)getp(d, "hg_bits");
+  h.gscale = (const float*)getp(d, "hg_gscale");
+  h.inv_total = get<float>(d, "hg_inv_total", 0.f);
+  h.bce_w = get<float>(d, "hg_bce_w", 0.f);
+  return h;
+}
+
 ConvFwdParams conv_params(const py::dict& d) {
   ConvFwdParams p{};
   p.N = get<int>(d, "N", 1);
@@ -118,6 +132,7 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.head_w = (const float*)getp(d, "head_w");
   p.head_b = (const float*)getp(d, "head_b");
   p.head_logit = (float*)const_cast<void*>(getp(d, "head_logit"));
+  p.hg = head_grad(d);
   if (!p.src1 || !p.wgt || !p.dst1) throw std::invalid_argument("conv_fwd: src1/wgt/dst1 required");
   check_msg(conv_fwd_prepare(p));
   return p;
@@ -158,6 +173,7 @@ WgradParams wgrad_params(const py::dict& d) {
   p.xb = (const float*)getp(d, "xb");
   p.xc = (const float*)getp(d, "xc");
   p.xz = getp(d, "xz");
+  p.hg = head_grad(d);
   if (p.bias_mode && !p.bias_slab) throw std::invalid_argument("wgrad: bias_slab required");
   if (!p.a1 || !p.b || !p.slab) throw std::invalid_argument("wgrad: a1/b/slab required");
   check_msg(wgrad_check(p));

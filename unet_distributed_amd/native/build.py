@@ -83,8 +83,9 @@ def build(verbose=True, jobs=None):
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")) +
                   glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     work = [(f, v) for f in srcs for v in (VARIANTS if f.endswith(".hip") else ["bf16"])]
-    # largest TUs first so the pool finishes together
-    work.sort(key=lambda j: -os.path.getsize(j[0]))
+    # costliest TUs first so the pool finishes together (the row-window conv units are
+    # small files that instantiate conv_win.h's ~150 kernels)
+    work.sort(key=lambda j: -(os.path.getsize(j[0]) + (10 ** 6 if "conv_win" in j[0] else 0)))
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
         results = list(ex.map(_compile, work))

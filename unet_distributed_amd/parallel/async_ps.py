@@ -24,6 +24,13 @@ freshly updated weights:
 
 Rank 0's own worker talks to the server in-process.  Message tags: GRAD (worker
 -> PS, followed by the gradient), DONE (worker -> PS, the done-queue token).
+
+Threads and communicators: on rank 0 only the server thread drives the control
+and data groups; on the other ranks only the main thread does.  The trainer's own
+collectives during the run (per-epoch evaluation sums, BatchNorm statistics) go
+over a third, gloo group on host copies (``dist.set_host_collectives``), so no
+rank ever drives two RCCL communicators from two threads without a cross-rank
+order (a deadlock pattern); the default group is used again after ``finish()``.
 """
 
 import threading
@@ -135,6 +142,10 @@ class AsyncPS:
         self.ctrl = dist.new_group(backend="gloo")                 # headers (any-source)
         self.rccl = ctx.backend == "nccl" and dev.type == "cuda"
         self.data = dist.new_group(backend="nccl") if self.rccl else self.ctrl
+        # the main thread's collectives while the server runs (module docstring)
+        self.coll = dist.new_group(backend="gloo")
+        from . import dist as D
+        D.set_host_collectives(self.coll)
         self.server: Optional[ParameterServer] = None
         self.thread = None
         # the data-plane buffers: device tensors over RCCL, host buffers over gloo
@@ -242,6 +253,7 @@ class AsyncPS:
 
     def finish(self):
         """Done-queue shutdown: workers enqueue a token; the PS waits for all of them."""
+        from . import dist as D
         if self.rank != 0:
             hdr = torch.tensor([MSG_DONE, 0], dtype=torch.int64)
             dist.send(hdr, dst=0, group=self.ctrl, tag=TAG_HDR)
@@ -250,6 +262,7 @@ class AsyncPS:
             self.snapshot_into_flat()
             if self.repack is not None:
                 self.repack()
+        D.set_host_collectives(None)       # the server is done: default group again
 
 
 class _Null:

@@ -42,7 +42,11 @@ def context() -> DistContext:
     return _CTX
 
 
-def init(device_pref: str = "auto", backend: str = "auto", timeout_s: float = 300.0) -> DistContext:
+def init(device_pref: str = "auto", backend: str = "auto", timeout_s: float = 300.0,
+         force: bool = False) -> DistContext:
+    """``force``: create the process group even at WORLD_SIZE 1 (RCCL accepts a
+    one-rank communicator), so every nccl-only code path -- ``device_id`` binding,
+    ``barrier(device_ids)``, ``ReduceOp.AVG`` buckets -- can run on a 1-GPU box."""
     ctx = _CTX
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -55,7 +59,7 @@ def init(device_pref: str = "auto", backend: str = "auto", timeout_s: float = 30
     else:
         ctx.device = torch.device("cpu")
     ctx.rank, ctx.world_size, ctx.local_rank = rank, world, local
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         # UNET_DIST_BACKEND=gloo forces gloo for GPU tensors too: lets several
         # ranks share ONE card (RCCL refuses duplicate devices) to rehearse the
         # multi-rank GPU path on a 1-GPU box.
@@ -76,6 +80,29 @@ def init(device_pref: str = "auto", backend: str = "auto", timeout_s: float = 30
     return ctx
 
 
+# Host collectives (set_host_collectives): while set, the module's collectives run
+# on CPU copies over this (gloo) group instead of the default one.
+_HOST_GROUP = None
+
+
+def set_host_collectives(group) -> None:
+    """Route allreduce_* / broadcast_ / allreduce_max_scalar through ``group`` on
+    CPU tensors (None restores the default group).  The async parameter server sets
+    it for the run: its RCCL data plane is driven by the server thread, and the
+    trainer's collectives (per-epoch evaluation, BatchNorm statistics) from the main
+    thread must not be a second RCCL communicator issued concurrently with no
+    cross-rank order -- a known deadlock pattern."""
+    global _HOST_GROUP
+    _HOST_GROUP = group
+
+
+def _host(t: torch.Tensor, fn):
+    h = t.detach().to("cpu", copy=True)
+    fn(h, _HOST_GROUP)
+    t.copy_(h)
+    return t
+
+
 def barrier():
     if _CTX.initialized:
         if _CTX.backend == "nccl":
@@ -88,17 +115,24 @@ def broadcast_(t: torch.Tensor, src: int = 0):
     """In-place broadcast (rank 0 -> all); used for initial parameters and
     restored checkpoints (replaces `prepare_or_wait_for_session`, test_dist.py:361)."""
     if _CTX.initialized and _CTX.world_size > 1:
+        if _HOST_GROUP is not None:
+            return _host(t, lambda h, g: dist.broadcast(h, src, group=g))
         dist.broadcast(t, src)
 
 
 def allreduce_sum_(t: torch.Tensor):
     if _CTX.initialized and _CTX.world_size > 1:
+        if _HOST_GROUP is not None:
+            return _host(t, lambda h, g: dist.all_reduce(h, op=dist.ReduceOp.SUM, group=g))
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t
 
 
 def allreduce_avg_(t: torch.Tensor):
     if _CTX.initialized and _CTX.world_size > 1:
+        if _HOST_GROUP is not None:
+            _host(t, lambda h, g: dist.all_reduce(h, op=dist.ReduceOp.SUM, group=g))
+            return t.div_(_CTX.world_size)
         if _CTX.backend == "nccl":
             dist.all_reduce(t, op=dist.ReduceOp.AVG)
         else:
@@ -110,6 +144,10 @@ def allreduce_avg_(t: torch.Tensor):
 def allreduce_max_scalar(x: float, device=None) -> float:
     if not (_CTX.initialized and _CTX.world_size > 1):
         return float(x)
+    if _HOST_GROUP is not None:
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=_HOST_GROUP)
+        return float(t.item())
     t = torch.tensor([float(x)], dtype=torch.float64, device=device or _CTX.device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

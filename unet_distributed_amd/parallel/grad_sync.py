@@ -67,13 +67,17 @@ def plan_buckets(flat, bucket_mb: float, tail_mb: float = 4.0) -> List[int]:
 
 
 class GradSync:
-    def __init__(self, flat, bounds: List[int], ctx: DistContext, overlap: bool = True):
+    def __init__(self, flat, bounds: List[int], ctx: DistContext, overlap: bool = True, force: bool = False):
+        """``force``: issue the bucket collectives even on a one-rank process group
+        (``dist.init(force=True)``), so the RCCL bucket path runs on a 1-GPU box."""
         self.flat = flat
         self.bounds = list(bounds)
         self.ctx = ctx
         self.overlap = overlap
         self.works = []
+        self.issued = set()
         self.world = ctx.world_size if ctx.initialized else 1
+        self.active = ctx.initialized and (self.world > 1 or force)
         self.avg_native = ctx.backend == "nccl"
 
     def _slice(self, i):
@@ -81,9 +85,13 @@ class GradSync:
         return self.flat.grad[s:self.bounds[i]]
 
     def on_segment(self, i: int):
-        """Called right after backward segment i (covering bucket i) was enqueued."""
-        if self.world == 1:
+        """Called right after backward segment i (covering bucket i) was enqueued, on
+        the stream the segment's gradients are ordered on (the executor's side stream
+        once it has joined the dgrad chain): the collective is ordered after them, and
+        finish() orders the caller's stream after the collective (work.wait())."""
+        if not self.active:
             return
+        self.issued.add(i)
         t = self._slice(i)
         op = dist.ReduceOp.AVG if self.avg_native else dist.ReduceOp.SUM
         if self.overlap:
@@ -100,6 +108,12 @@ class GradSync:
         self.finish()
 
     def finish(self):
+        # a bucket the backend did not hand over (fewer backward segments than buckets)
+        # is reduced now: every replica must end the step with the same gradient
+        for i in range(len(self.bounds)):
+            if self.active and i not in self.issued:
+                self.on_segment(i)
+        self.issued = set()
         for i, w in self.works:
             w.wait()
             if not self.avg_native:

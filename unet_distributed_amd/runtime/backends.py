@@ -23,7 +23,7 @@ from .params import FlatParams
 class TorchBackend:
     name = "torch"
 
-    def __init__(self, spec, flat: FlatParams, cfg, device, per_rank_batch: int):
+    def __init__(self, spec, flat: FlatParams, cfg, device, per_rank_batch: int, bounds=None):
         self.spec = spec
         self.flat = flat
         self.cfg = cfg
@@ -38,7 +38,9 @@ class TorchBackend:
                 if l.kind == "conv":
                     self.state[l.name + "/norm/moving_mean"] = torch.zeros(l.cout, device=self.device)
                     self.state[l.name + "/norm/moving_variance"] = torch.ones(l.cout, device=self.device)
-        self.bounds = [flat.numel]
+        # allreduce buckets: on_segment(k) is called once per bucket after the backward
+        # (the GradSync of the trainer is planned with the same bounds)
+        self.bounds = list(bounds) if bounds else [flat.numel]
 
     def set_buckets(self, bounds):
         self.bounds = list(bounds)
@@ -204,4 +206,4 @@ def make_backend(spec, flat, cfg, device, per_rank_batch, bounds=None):
         from .. import native
         native.require()
         return NativeBackend(spec, flat, cfg, device, per_rank_batch, bounds)
-    return TorchBackend(spec, flat, cfg, device, per_rank_batch)
+    return TorchBackend(spec, flat, cfg, device, per_rank_batch, bounds)

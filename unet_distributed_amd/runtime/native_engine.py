@@ -72,7 +72,6 @@ class NativeUNet:
         # backward is launched eagerly even in HIP-graph mode.
         self.dual_stream = os.environ.get("UNET_DUAL_STREAM", "1") != "0"
         self._side = None
-        self._chain = None
         self._groups: Dict[tuple, list] = {}
         # 16-bit element type of activations, gradients w.r.t. activations and the
         # weight copies: selects the bf16 or fp16 build of every kernel (common.h)
@@ -99,11 +98,13 @@ class NativeUNet:
         self.bufs: Dict[str, torch.Tensor] = {}
         # wgrad split-K grid target (workgroups per weight gradient): ~2 per CU.  Dual
         # stream at the default per-GPU batch 1024: 512 > 768 > 384 > 256 > 1024 >> 128
-        # (same-box sweep, +1.7 % over 256; at batch 256 the earlier sweep preferred 256)
-        self.wg_target = int(os.environ.get("UNET_WGRAD_WG_TARGET", "512"))
-        self._rev_mode = int(os.environ.get("UNET_WIN_REV", "3"))
-        # UNET_WGRAD_WIN=-1: never use the row-window wgrad kernel (A/B measurements)
-        self.wgrad_win = int(os.environ.get("UNET_WGRAD_WIN", "0"))
+        # (same-box sweep, +1.7 % over 256; 640 re-measured -0.4 % at the round-2 end)
+        self.wg_target = 512
+        # row-window convs walk their windows in the reverse of the order their input was
+        # written (bit 0 forward, bit 1 data gradients; see _rev_order)
+        self._rev_mode = 3
+        # -1: never use the row-window weight-gradient kernel (set by A/B tests)
+        self.wgrad_win = 0
         self._alloc_weights()
         self._alloc_activations()
         self.plan = self.C.Plan(self.dt_id)
@@ -239,10 +240,10 @@ class NativeUNet:
         # tensor graph: name -> (level, channels, produced_by_relu, dropout)
         self.tinfo: Dict[str, Tuple[int, int, bool, bool]] = {"x": (1, self.cpad, False, False)}
         self.inputs: Dict[str, Tuple] = {}
-        # upsampling decoder: materialise the nearest upsample (UNET_UPS_MATERIALIZE=1) so
-        # the decoder convs and their weight gradients run on the row-window kernels;
-        # 0 folds it into the implicit-GEMM address generation instead
-        self.ups_materialize = os.environ.get("UNET_UPS_MATERIALIZE", "1") != "0"
+        # upsampling decoder: the nearest upsample is materialised (elementwise ups_fwd) so
+        # the decoder convs and their weight gradients run on the row-window kernels (the
+        # round-1 address-generation fold measured slower and was removed)
+        self.ups_materialize = True
         self.pool_codes: Dict[str, torch.Tensor] = {}
         cur = "x"
         pending_up = None
@@ -282,17 +283,22 @@ class NativeUNet:
         # ReLU bit masks (conv_params.h relu_bits): the forward of every ReLU conv whose
         # output masks a data gradient also writes 1 bit per element, and those data
         # gradients read the bits instead of the 16-bit activation -- at b1024 ~8 GB
-        # less backward traffic (UNET_RELU_BITS=0 keeps the activation masks).  Pool
-        # outputs need no mask at all: the pool backward routes a gradient only where
-        # the window maximum is positive (code flag bits).  UNET_RELU_BITS = 1 (all
-        # levels), 0 (none) or a comma list of levels.
+        # less backward traffic.  Pool outputs need no mask at all: the pool backward
+        # routes a gradient only where the window maximum is positive (code flag bits).
         self.relu_bits: Dict[str, torch.Tensor] = {}
         self.pool_outs = {l.name for l in spec.layers if l.kind == "pool"}
-        rb = os.environ.get("UNET_RELU_BITS", "1")
-        rb_levels = None if rb == "1" else {int(v) for v in rb.split(",") if v.strip() and v != "0"}
+        # Head-on-load (head_grad.h): the head input's gradient dY = dlogit * w * (x > 0) is
+        # rank-1 per pixel, so its consumers -- the data and weight gradients of the head's
+        # input conv -- form it from the probability, target and the head input's ReLU bits
+        # instead of reading a materialised 32-channel dY; the head backward only reduces
+        # the Mask weight / bias gradients (on the side stream).  2D norm-free model with
+        # a 32-channel head input on 16..128-wide rows (UNET_HEAD_ONLOAD=0: materialised).
+        self.head_onload = (spec.norm == "none" and self.dims == 2 and self.tinfo[self.head_in][1] == 32
+                            and self.img in (16, 32, 64, 128) and self.wgrad_win >= 0
+                            and os.environ.get("UNET_HEAD_ONLOAD", "1") != "0")
         if spec.norm == "none":
             for l in spec.layers:
-                if l.kind == "conv" and l.name != self.head_in and (rb_levels is None or l.level in rb_levels):
+                if l.kind == "conv" and (l.name != self.head_in or self.head_onload):
                     self.relu_bits[l.name] = torch.zeros(self.npix(l.level) * l.cout // 8, dtype=torch.uint8,
                                                          device=self.device)
         P = self.npix(1)
@@ -337,7 +343,7 @@ class NativeUNet:
         # fused statistics (conv epilogues write per-tile partial sums): name -> buffer
         self._stat_bufs: Dict[str, torch.Tensor] = {}
         self._bwd_fused: Dict[str, Tuple[int, bool]] = {}
-        self.fuse_norm_stats = os.environ.get("UNET_NORM_FUSE", "1") != "0"
+        self.fuse_norm_stats = True
         if self.spec.norm == "none":
             return
         f32 = torch.float32
@@ -431,9 +437,8 @@ class NativeUNet:
             cstride = C
         if l.name in self._xf_fwd:
             return          # the consumer conv normalises z on load and writes the activation
-        if (l.name == self.head_in and not (l.dropout and dropout) and self.tinfo[l.name][1] in (16, 32, 64)
-                and os.environ.get("UNET_NORM_HEAD", "1") != "0"):
-            if train and os.environ.get("UNET_NORM_HEAD_LOSS", "1") != "0":
+        if l.name == self.head_in and not (l.dropout and dropout) and self.tinfo[l.name][1] in (16, 32, 64):
+            if train:
                 # training: normalisation, logits, sigmoid, loss sums and the nine per-channel
                 # pixel sums of the head's backward in one pass (head.hip norm_head_loss);
                 # the activation is not stored -- nothing downstream reads it
@@ -451,7 +456,7 @@ class NativeUNet:
             self._norm_head = True
             return
         pool = self._pool_of.get(l.name)
-        if pool is not None and not (l.dropout and dropout) and os.environ.get("UNET_NORM_POOL", "1") != "0":
+        if pool is not None and not (l.dropout and dropout):
             # convNb: normalisation and the 2x2 max-pool of its output in one pass
             dd, hh, ww = self.sdims(l.level)
             plan.add_generic("norm_pool", [_ptr(z), _ptr(fa), _ptr(fc), _ptr(b[l.name]), _ptr(b[pool]),
@@ -510,13 +515,20 @@ class NativeUNet:
         ops.append(emit)
         return ops
 
+    def _head_grad_fields(self):
+        """hg_* fields (conv_params.h HeadGrad) of the head input's gradient consumers."""
+        return dict(hg_prob=_ptr(self.prob), hg_t=_ptr(self.target), hg_sums=_ptr(self.sums),
+                    hg_w=self.master_ptr("Mask/kernel"), hg_bits=_ptr(self.relu_bits[self.head_in]),
+                    hg_gscale=_ptr(self.loss_scale_dev), hg_inv_total=1.0 / float(self.npix(1)),
+                    hg_bce_w=self.bce_weight)
+
     def _tail_halves(self, d, l, src1, skip, dy):
         """Two half-batch copies of dgrad dict `d` when its destination is the first
         layer's output (the last dgrad of the backward) and the halves line up with
         the first layer's weight-gradient splits (norm-free 2D model, even batch;
         UNET_TAIL_SPLIT=0 off), else None."""
         if (skip is not None or self.inputs.get(src1, ("",))[0] != "x" or self.spec.norm != "none"
-                or self.dims != 2 or self.B % 2 or os.environ.get("UNET_TAIL_SPLIT", "1") == "0"
+                or self.dims != 2 or self.B % 2
                 or self.img not in (16, 32, 64, 128) or self.cpad not in (4, 8) or self.wgrad_win < 0):
             return None      # (the first-layer row-window wgrad, whose split halves are image halves)
         b = self.bufs
@@ -539,10 +551,9 @@ class NativeUNet:
     def _skip_route(self, l, skip, c1, c2, dy):
         """(pool name, dgrad dict) of the deferred skip half of decoder conv l's data
         gradient when it can carry the pool backward of its skip source (2D row-window
-        data gradient, norm-free model; UNET_SKIP_ROUTE=0 keeps the dual-destination
-        dgrad + separate pool backward), else None.  Saves the skip-gradient tensor's
+        data gradient), else None (the dual-destination dgrad + separate pool backward).  Saves the skip-gradient tensor's
         write and re-read: the pool backward's read of it becomes a second read of dy."""
-        if self.dims != 2 or os.environ.get("UNET_SKIP_ROUTE", "1") == "0":
+        if self.dims != 2:
             return None
         if self.spec.norm != "none" and not (skip in self.norm_layers and self.fuse_norm_stats):
             return None
@@ -600,9 +611,6 @@ class NativeUNet:
                   nd_rate=self.spec.dropout if self.tinfo[tname][3] else 0.0, nd_salt=self._salt(tname))
         fused = self._fuse_stats(d2, "bst:" + tname, C, l.level)
         if fused is None:
-            if tname in self._xf_wg:     # the fallback masks with the (never stored) activation
-                raise RuntimeError("native engine: %s is normalised on load but its data gradient "
-                                   "cannot recompute the mask (unset UNET_NORM_XFORM_WG)" % tname)
             return
         d.clear()
         d.update(d2)
@@ -620,74 +628,11 @@ class NativeUNet:
     def _salt(self, lname):
         return [l.name for l in self.spec.layers].index(lname)
 
-    def _fwd_chunks(self):
-        """Batch chunks for the full-resolution forward layers.  A level-1 tensor of
-        the b256 step is 268 MB, more than the 256 MiB Infinity Cache, so conv1a ->
-        conv1b -> pool1 (and transConv9 -> conv9a -> conv9b) stream every
-        intermediate through HBM.  Run those layer runs chunk by chunk instead: a
-        chunk's output is re-read by the next layer while it is still resident
-        (UNET_FWD_CHUNK = number of chunks, 1 = off).  Batch statistics (BN) need
-        the whole batch, so only the plain and GN-free model is chunked."""
-        n = int(os.environ.get("UNET_FWD_CHUNK", "1"))
-        if n <= 1 or self.spec.norm != "none" or self.B % n:
-            return 1
-        return n
-
     def _toff(self, tname, c, nb):
         """Byte offset of image c*nb of activation tensor `tname`."""
         lvl, ch = self.tinfo[tname][0], self.tinfo[tname][1]
         d, h, w = self.sdims(lvl)
         return c * nb * d * h * w * ch * self.bufs[tname].element_size()
-
-    def _xf_bwd_fields(self, l):
-        """Operand-transform fields (conv_params.h xform 2) that let conv l's data
-        gradient form dz = ca g + cb z + cc on load and store it for the weight gradient
-        (no norm_bwd_apply pass), or None.  UNET_NORM_XFORM = fwd (default) | bwd | 1
-        (both) | 0: the backward transform measured -1.1 % on the BN b1024 step (the
-        fine-level dgrads are VALU-bound already; the separate pass streams at 5.3 TB/s),
-        the forward one +0.4 % (scripts/gpu_sweep_env.sh, same box)."""
-        if self.spec.norm == "none" or self.dims != 2 or os.environ.get("UNET_NORM_XFORM", "fwd") not in ("1", "bwd"):
-            return None
-        b = self.bufs
-        f = dict(xform=2, xa=_ptr(b["ca:" + l.name]), xb=_ptr(b["cb:" + l.name]), xc=_ptr(b["cc:" + l.name]),
-                 xz=_ptr(b["z:" + l.name]), xcs=0 if self.spec.norm == "batch" else l.cout,
-                 xout=_ptr(b["dz:" + l.name]))
-        d = self._conv_common(l.level, 3, 1, 1)
-        d.update(C1=l.cout, src1=_ptr(b["d:" + l.name]), wgt=self.wptr(l.name, "dg"), Cout=l.cin, relu=0,
-                 dst1=_ptr(b["dz:" + l.name]), **f)
-        try:
-            self.C.conv_fwd_grid(d)
-        except ValueError:
-            return None
-        return f
-
-    def _l1_xf_fields(self, l, first, hn):
-        """Level-1 norm layers (32 channels, 128-wide rows; not the first layer or the head
-        input, which have their own paths): the data gradient AND the window weight
-        gradient both form dz = ca g + cb z + cc on load, so dz is never stored and the
-        norm_bwd_apply pass is gone (UNET_NORM_L1_XF=1, opt-in: measured -1.2 % BN / -0.7 %
-        GN at b1024 -- the level-1 dgrads are VALU-bound and pay for the second operand),
-        or None."""
-        if (first or hn or self.spec.norm == "none" or self.dims != 2 or self.sdims(l.level)[2] != 128
-                or l.cout != 32 or self.wgrad_win < 0 or os.environ.get("UNET_NORM_L1_XF", "0") != "1"):
-            return None
-        f = self._xf_bwd_fields_any(l)
-        if f is None:
-            return None
-        return dict(f, xout=None)
-
-    def _xf_bwd_fields_any(self, l):
-        b = self.bufs
-        f = dict(xform=2, xa=_ptr(b["ca:" + l.name]), xb=_ptr(b["cb:" + l.name]), xc=_ptr(b["cc:" + l.name]),
-                 xz=_ptr(b["z:" + l.name]), xcs=0 if self.spec.norm == "batch" else l.cout)
-        d = self._conv_common(l.level, 3, 1, 1)
-        d.update(C1=l.cout, src1=_ptr(b["d:" + l.name]), wgt=self.wptr(l.name, "dg"), Cout=l.cin, relu=0,
-                 dst1=_ptr(b["dz:" + l.name]), **f)
-        try:
-            self.C.conv_fwd_grid(d)
-        except ValueError:
-            return None
-        return f
 
     def _xf_fwd_fields(self, src):
         """Operand-transform fields of a conv reading normalised activation `src` as the
@@ -695,21 +640,18 @@ class NativeUNet:
         b = self.bufs
         return dict(xform=1, xa=_ptr(b["fa:" + src]), xb=_ptr(b["fc:" + src]),
                     xcs=0 if self.spec.norm == "batch" else self.tinfo[src][1],
-                    xout=None if src in self._xf_wg else _ptr(b[src]))
+                    xout=_ptr(b[src]))
 
     def _plan_xforms(self):
         """Normalised activations whose only consumer is the next conv's first source
-        (the 'a' convs of each block, no dropout): that conv normalises z on load
-        (UNET_NORM_XFORM=0 or bwd keeps the separate norm_apply pass).  Decided once, for
-        the training and the evaluation plans alike."""
+        (the 'a' convs of each block, no dropout): that conv normalises z on load and
+        also stores the activation for its weight gradient (+0.4 % BN b1024 over a
+        separate norm_apply pass).  Decided once, for the training and the evaluation
+        plans alike.  (Measured and dropped in round 2: the consumer's weight gradient
+        normalising on load too, -1.3 % BN / -1.5 % GN; dz formed on load by the data
+        gradient, -1.1 % BN; level-1 dgrad + wgrad both forming dz, -1.2 % BN.)"""
         self._xf_fwd = set()
-        # ... and, opt-in (UNET_NORM_XFORM_WG=1), whose consumer's weight gradient
-        # normalises its A operand on load too (2D row-window wgrad, rows 32..128 wide), so
-        # the activation is never stored: measured -1.3 % BN / -1.5 % GN b1024 (the
-        # per-window transform pass and its barrier cost the side-stream weight gradients
-        # more than the skipped activation stores save)
-        self._xf_wg = set()
-        if self.spec.norm == "none" or self.dims != 2 or os.environ.get("UNET_NORM_XFORM", "fwd") not in ("1", "fwd"):
+        if self.spec.norm == "none" or self.dims != 2:
             return
         users: Dict[str, list] = {}
         for name, inp in self.inputs.items():
@@ -737,14 +679,14 @@ class NativeUNet:
             except ValueError:
                 continue
             self._xf_fwd.add(l.name)
-            if (self.sdims(l2.level)[2] in (32, 64, 128) and self.wgrad_win >= 0
-                    and os.environ.get("UNET_NORM_XFORM_WG", "0") == "1"):
-                self._xf_wg.add(l.name)
+
+    # second forward chunk starts after the first chunk's first 6 layers (offset sweep
+    # 3 / 6 / 9 / 13: -0.2 / +0.3 / . / -0.6 %)
+    FWD_OFFSET = 6
 
     def _fwd_streams(self, train):
         """2: the training forward runs as two half-batch chunks on two HIP streams, the
-        second chunk started once the first has finished the first `UNET_FWD_OFFSET`
-        layers, so kernels of different levels (bandwidth-bound full-resolution ones,
+        second chunk started once the first has finished its first FWD_OFFSET layers, so kernels of different levels (bandwidth-bound full-resolution ones,
         MFMA-bound coarse ones) share the GPU.  Norm-free 2D model with an even batch
         (BatchNorm needs whole-batch statistics); UNET_FWD_STREAMS=1 keeps one stream."""
         n = int(os.environ.get("UNET_FWD_STREAMS", "1"))
@@ -757,36 +699,19 @@ class NativeUNet:
         nst = self._fwd_streams(train) if plan is self.plan else 1
         if nst == 2:
             return self._build_forward_2s(plan, dropout, train)
-        nch = self._fwd_chunks()
         # fused head: the Mask 1x1 conv + sigmoid + loss partials run in the epilogue of
-        # the head's input conv (whole batch only; UNET_HEAD_FUSE=0 keeps the separate
-        # head launch)
+        # the head's input conv (UNET_HEAD_FUSE=0 keeps the separate head launch)
         self._head_fused_blocks = 0
         self._norm_head = False
         if train:
             self._norm_head_loss = False
-        self._fuse_head = nch == 1 and os.environ.get("UNET_HEAD_FUSE", "1") != "0"
-        # convNb -> pool fusion (UNET_POOL_FUSE=0 keeps the separate pool launch)
-        self._pool_of = {}
+        self._fuse_head = os.environ.get("UNET_HEAD_FUSE", "1") != "0"
+        # convNb -> 2x2 max-pool fused into the conv's epilogue where the kernel can
+        self._pool_of = {self.inputs[x.name][0]: x.name for x in spec.layers if x.kind == "pool"}
         self._pool_fused = set()
-        if os.environ.get("UNET_POOL_FUSE", "1") != "0":
-            self._pool_of = {self.inputs[x.name][0]: x.name for x in spec.layers if x.kind == "pool"}
-        layers = [l for l in spec.layers if l.kind != "up"]
-        i = 0
-        while i < len(layers):
-            l = layers[i]
-            if nch > 1 and l.kind != "mask" and l.level == 1:
-                j = i
-                while j < len(layers) and layers[j].kind != "mask" and layers[j].level == 1:
-                    j += 1
-                nb = self.B // nch
-                for c in range(nch):
-                    for ll in layers[i:j]:
-                        self._fwd_layer(plan, ll, dropout, train, c, nb)
-                i = j
-            else:
+        for l in spec.layers:
+            if l.kind != "up":
                 self._fwd_layer(plan, l, dropout, train, 0, self.B)
-                i += 1
 
     def _build_forward_2s(self, plan, dropout, train):
         """Plan order: chunk 0's layers, chunk 1's layers, then the head finish on the
@@ -796,13 +721,11 @@ class NativeUNet:
         self._head_fused_blocks = 0
         self._norm_head = False
         self._fuse_head = os.environ.get("UNET_HEAD_FUSE", "1") != "0"
-        self._pool_of = {}
+        self._pool_of = {self.inputs[x.name][0]: x.name for x in spec.layers if x.kind == "pool"}
         self._pool_fused = set()
-        if os.environ.get("UNET_POOL_FUSE", "1") != "0":
-            self._pool_of = {self.inputs[x.name][0]: x.name for x in spec.layers if x.kind == "pool"}
         layers = [l for l in spec.layers if l.kind not in ("up", "mask")]
         nb = self.B // 2
-        off = int(os.environ.get("UNET_FWD_OFFSET", "6"))
+        off = self.FWD_OFFSET
         self._fwd2 = []                      # (first op, op after the offset layers, end) per chunk
         for c in range(2):
             start = plan.size()
@@ -1019,12 +942,16 @@ class NativeUNet:
             elif l.kind == "mask":
                 hc = self.tinfo[self.head_in][1]
                 nb = self.head_nb
+                # head-on-load: no dY is written, only the Mask gradients are reduced, off
+                # the dgrad chain (side stream: "wgrad:" plan names)
                 emit_generic("head_bwd",
                              lambda hc=hc: [_ptr(b[self.head_in]), self.master_ptr("Mask/kernel"), _ptr(self.prob),
-                                            _ptr(self.target), _ptr(self.sums), _ptr(b["d:" + self.head_in]),
+                                            _ptr(self.target), _ptr(self.sums),
+                                            0 if self.head_onload else _ptr(b["d:" + self.head_in]),
                                             _ptr(self.head_partial), self.grad_ptr("Mask/kernel"),
                                             self.grad_ptr("Mask/bias"), _ptr(self.loss_scale_dev)],
-                             [P1, hc], [inv_total, self.bce_weight, 1.0], "bwd:Mask")
+                             [P1, hc], [inv_total, self.bce_weight, 1.0],
+                             "wgrad:Mask" if self.head_onload else "bwd:Mask")
                 done("Mask")
             elif l.kind == "conv":
                 src1, up1, skip = self.inputs[l.name]
@@ -1032,22 +959,17 @@ class NativeUNet:
                 c1 = self.tinfo[src1][1]
                 c2 = self.tinfo[skip][1] if skip else 0
                 dy = b["d:" + l.name]
-                xf_bwd = None
-                first_xf = l1_xf = None
+                first_xf = None
                 if spec.norm != "none":
-                    hn = self._norm_head_loss and l.name == self.head_in
-                    l1_xf = self._l1_xf_fields(l, first, hn)
-                    xf_bwd = self._xf_bwd_fields(l) if not (first or hn or l1_xf) else None
                     if (first and self.dims == 2 and self.img in (16, 32, 64, 128) and self.cpad in (4, 8)
-                            and self.wgrad_win >= 0 and os.environ.get("UNET_NORM_FIRST_XF", "1") != "0"):
+                            and self.wgrad_win >= 0):
                         # the first layer's dz is read only by its weight gradient: that kernel
                         # forms dz = ca g + cb z + cc on load (no norm_bwd_apply pass)
                         first_xf = dict(xform=2, xa=_ptr(b["ca:" + l.name]), xb=_ptr(b["cb:" + l.name]),
                                         xc=_ptr(b["cc:" + l.name]), xz=_ptr(b["z:" + l.name]),
                                         xcs=0 if spec.norm == "batch" else l.cout)
-                    ops.extend(self._norm_bwd_ops(l, apply=xf_bwd is None and first_xf is None and l1_xf is None))
-                    dy = b["dz:" + l.name] if (first_xf is None and l1_xf is None) else b["d:" + l.name]
-                wg_at = len(ops)
+                    ops.extend(self._norm_bwd_ops(l, apply=first_xf is None))
+                    dy = b["dz:" + l.name] if first_xf is None else b["d:" + l.name]
                 Q = self.npix(l.level)
                 # --- weight + bias gradient (fused column sums); the upsampling decoder's
                 # A operand is the materialised upsample when there is one
@@ -1061,12 +983,8 @@ class NativeUNet:
                           b=_ptr(dy))
                 if first_xf is not None:
                     kd.update(first_xf)
-                if l1_xf is not None:
-                    kd.update({k: v for k, v in l1_xf.items() if k != "xout"})
-                if src1 in self._xf_wg:
-                    # the activation was never stored: normalise its pre-norm z on load
-                    kd.update(a1=_ptr(b["z:" + src1]), xform=1, xa=_ptr(b["fa:" + src1]),
-                              xb=_ptr(b["fc:" + src1]), xcs=0 if spec.norm == "batch" else c1)
+                if l.name == self.head_in and self.head_onload:
+                    kd.update(self._head_grad_fields())
                 wspec = dict(lname=l.name, kd=kd, M1=c1, M2=c2, Nc=l.cout, KT=KT3, Q=Q,
                              QD=self.sdims(l.level)[0], QH=self.sdims(l.level)[1],
                              QW=self.sdims(l.level)[2], upA=upA,
@@ -1085,7 +1003,7 @@ class NativeUNet:
                     emit_wgrad(wspec)
                 # --- data gradient
                 if not first:
-                    def mk(l=l, src1=src1, up1=up1, skip=skip, c1=c1, c2=c2, dy=dy, l1_xf=l1_xf):
+                    def mk(l=l, src1=src1, up1=up1, skip=skip, c1=c1, c2=c2, dy=dy):
                         d = self._conv_common(l.level, 3, 1, 1)
                         d.update(name="dgrad:" + l.name, C1=l.cout, src1=_ptr(dy),
                                  wgt=self.wptr(l.name, "dg"), Cout=l.cin, relu=0)
@@ -1095,22 +1013,18 @@ class NativeUNet:
                             d.update(dst1=_ptr(b["d:" + src1]), D1=l.cin, mask1=m1, mask_bits=mb,
                                      mask_scale1=(1.0 / (1.0 - spec.dropout)) if drop else 1.0)
                             self._fuse_dgrad_norm(d, src1)
+                            if l.name == self.head_in and self.head_onload:
+                                d.update(self._head_grad_fields())
                         else:
                             if up1 == 2:
-                                dst1 = b["dfull:" + src1]          # full-res grad of the folded upsample
+                                dst1 = b["dfull:" + src1]          # full-res grad of the upsample
                             else:
                                 dst1 = b["d:" + src1]              # tconv output: linear, no mask
                             dsk = self._skip_route(l, skip, c1, c2, dy)
                             if dsk is not None:
                                 # the skip half runs later, fused with the pool backward
                                 d.update(Cout=c1, dst1=_ptr(dst1), D1=c1)
-                                if l1_xf is not None:      # it reads g too: dz formed on load
-                                    dsk[1].update(l1_xf, src1=_ptr(dy))
-                                    self.C.conv_fwd_grid(dsk[1])
                                 self._deferred_skip[dsk[0]] = dsk[1]
-                            elif l1_xf is not None:
-                                raise RuntimeError("UNET_NORM_L1_XF: %s's skip-half data gradient is not deferred"
-                                                   % l.name)
                             else:
                                 m2, mb = self._relu_mask(skip)
                                 d.update(dst1=_ptr(dst1), D1=c1, dst2=_ptr(b["dskip:" + skip]),
@@ -1119,17 +1033,6 @@ class NativeUNet:
                             self._rev_order(d, "g:" + l.name, "g:" + src1)
                         return d
                     dd_ = mk()                 # built now: it decides the fused norm backward
-                    if l1_xf is not None:
-                        # dz formed on load here and (independently) by the weight gradient
-                        dd_.update(l1_xf, src1=_ptr(b["d:" + l.name]))
-                        self.C.conv_fwd_grid(dd_)
-                    if xf_bwd is not None:
-                        # dz formed on load by this dgrad (which also stores it): the weight
-                        # gradient reading dz moves behind it
-                        dd_.update(xf_bwd, src1=_ptr(b["d:" + l.name]))
-                        self.C.conv_fwd_grid(dd_)          # validated in _xf_bwd_fields
-                        wg_ops = ops[wg_at:]
-                        del ops[wg_at:]
                     halves = self._tail_halves(dd_, l, src1, skip, dy)
                     if halves is None:
                         emit_conv(lambda dd_=dd_: dd_)
@@ -1141,8 +1044,6 @@ class NativeUNet:
                         tail_parts[src1] = len(ops)
                         ops.append(("placeholder",))
                         emit_conv(lambda h=halves[1]: h)
-                    if xf_bwd is not None:
-                        ops.extend(wg_ops)
                     if up1 == 2:
                         lvl = self.tinfo[src1][0]
                         dd, hh, ww = self.sdims(lvl)
@@ -1459,25 +1360,13 @@ class NativeUNet:
         gradient producers); bucket allreduces are issued from the side stream after
         it has also caught up with the chain, so the dgrad chain never waits for them;
         the caller's stream joins both at the end (the next forward overwrites
-        activations the side launches read).
-
-        UNET_BWD_PRIO: "dgrad" runs the dgrad chain on a high-priority stream (the
-        critical path wins the dispatcher; the weight gradients fill in), "wgrad" the
-        reverse, anything else leaves both at the default priority."""
+        activations the side launches read).  (Stream priorities for either chain
+        measured no effect in round 2.)"""
         main = stream if stream is not None else torch.cuda.current_stream()
         if self._side is None:
-            lo, hi = torch.cuda.Stream.priority_range()      # (lowest, highest) priority values
-            mode = os.environ.get("UNET_BWD_PRIO", "none")
-            ps = {"dgrad": (hi, lo), "wgrad": (lo, hi)}.get(mode)
-            if ps is None:
-                self._chain, self._side = None, torch.cuda.Stream(device=self.device)
-            else:
-                self._chain = torch.cuda.Stream(device=self.device, priority=ps[0])
-                self._side = torch.cuda.Stream(device=self.device, priority=ps[1])
-        chain = self._chain if self._chain is not None else main
+            self._side = torch.cuda.Stream(device=self.device)
+        chain = main
         side = self._side
-        if chain is not main:
-            chain.wait_stream(main)
         hm, hs = chain.cuda_stream, side.cuda_stream
         begin = self.fwd_end
         for k, end in enumerate(self.seg_ends):
@@ -1492,8 +1381,6 @@ class NativeUNet:
                 side.wait_stream(chain)
                 with torch.cuda.stream(side):
                     on_segment(k)
-        if chain is not main:
-            main.wait_stream(chain)
         main.wait_stream(side)
 
     def backward(self, on_segment=None, stream=None):

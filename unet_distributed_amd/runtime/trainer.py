@@ -243,20 +243,28 @@ class Trainer:
                 "batches": int(acc[4].item())}
 
     # ------------------------------------------------------------------ step
-    def _poison(self, step: int) -> None:
-        """--fault_inject_overflow_step: make this rank's gradient non-finite (fp16
-        overflow drill) on the given local step."""
+    def _poison_due(self, step: int) -> bool:
+        """--fault_inject_overflow_step: this rank's gradient is made non-finite (fp16
+        overflow drill) ONCE, at the first iteration of the given step.  (A skipped
+        step does not advance global_step, so the retried iteration carries the same
+        step number: a step-number test alone would poison every retry forever.)"""
         c = self.cfg
-        if c.fault_inject_overflow_step == step and c.fault_inject_rank in (-1, self.rank):
-            self.flat.grad[0] = float("inf")
+        return (not getattr(self, "_poisoned", False) and c.fault_inject_overflow_step == step
+                and c.fault_inject_rank in (-1, self.rank))
+
+    def _poison(self) -> None:
+        self._poisoned = True
+        self.flat.grad[0] = float("inf")
 
     def train_step(self, x, y, seed: int, step: int = -2) -> None:
         R = self.ranges
         scale = self.scaler.scale
+        poison = self._poison_due(step)
         if self.async_ps is not None:
             with R("forward_backward"):
                 self.backend.fwd_bwd(x, y, seed, on_segment=None, grad_scale=scale)
-            self._poison(step)
+            if poison:
+                self._poison()
             if self.scaler.enabled:
                 if not self.scaler.update(self.flat.grad):
                     self.async_ps.skip_step()   # fp16 overflow: nothing is pushed, the
@@ -265,9 +273,20 @@ class Trainer:
             with R("ps_push_pull"):
                 self.async_ps.push_pull()
             return
+        on_segment = self.sync.on_segment
+        if poison:
+            # sync mode: poison inside the bucket hook, on the hook's stream, BEFORE the
+            # allreduce of the bucket that holds flat offset 0 is issued -- so every rank
+            # sees the same non-finite average and skips the step together (a write
+            # after fwd_bwd would race the in-flight allreduce)
+            def on_segment(i, _f=self.sync.on_segment):
+                if i == 0:
+                    self._poison()
+                _f(i)
         with R("forward_backward"):
-            self.backend.fwd_bwd(x, y, seed, on_segment=self.sync.on_segment, grad_scale=scale)
-        self._poison(step)
+            self.backend.fwd_bwd(x, y, seed, on_segment=on_segment, grad_scale=scale)
+        if poison and not getattr(self, "_poisoned", False):
+            self._poison()                      # backend without bucket hooks
         with R("grad_sync"):
             self.sync.finish()
         if not self.scaler.update(self.flat.grad):
