@@ -2,6 +2,8 @@
 fp32 ATen reference of the same UNet, same weights, same batch, same dropout
 masks (shared counter hash)."""
 
+import os
+
 import pytest
 import torch
 
@@ -143,6 +145,7 @@ def test_native_inference_export_roundtrip(cuda_dev, tmp_path):
     flat = FlatParams(spec)
     flat.load_dict(reference.init_params(spec, seed=3))
     d = export_model(cfg, spec, flat)
+    os.remove(os.path.join(d, "saved_model.json"))          # the GraphDef alone describes the model
     model = load_saved_model(d, device=cuda_dev, batch=4)
     assert model.name == "native"
     x, _ = synthetic_brats(6, 64, 4, seed=2)
@@ -333,6 +336,7 @@ def test_native_inference_export_roundtrip_norm(cuda_dev, tmp_path, norm):
                 state[l.name + "/norm/moving_mean"] = 0.2 * torch.randn(l.cout, generator=g)
                 state[l.name + "/norm/moving_variance"] = 0.5 + torch.rand(l.cout, generator=g)
     d = export_model(cfg, spec, flat, extra_state=state)
+    os.remove(os.path.join(d, "saved_model.json"))
     model = load_saved_model(d, device=cuda_dev, batch=4)
     assert model.name == "native"
     x, _ = synthetic_brats(4, 64, 4, seed=2)

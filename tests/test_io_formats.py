@@ -151,6 +151,55 @@ def _map(entries):
 
 
 @pytest.mark.parametrize("kw", [dict(), dict(norm="batch"), dict(use_upsampling=True, in_channels=1),
+                                dict(dims=3, in_channels=4), dict(dims=3, in_channels=4, use_upsampling=True),
+                                dict(norm="group", groups=4)])
+def test_saved_model_names_resolve_and_spec_roundtrips(tmp_path, kw):
+    """Every name a TF loader looks up resolves to a node of the GraphDef: node inputs,
+    the VariableDefs of both variable collections (variable / initializer / snapshot),
+    the SaverDef's tensors and op, the SignatureDef's tensors -- in saved_model.pb and in
+    a checkpoint's .meta (Adam slots, beta powers, global_step included).  The
+    architecture recovered from the graph alone equals the exported spec."""
+    from unet_distributed_amd.utils import tf_graph
+    cfg = Config(checkpoint_dir=str(tmp_path), img_size=32 if kw.get("dims") == 3 else 64, save_model_secs=0, **kw)
+    spec = spec_from_config(cfg)
+    flat = FlatParams(spec)
+    d = export_model(cfg, spec, flat)
+    prefix = CheckpointManager(cfg, flat, True).save()
+    for path in (os.path.join(d, "saved_model.pb"), prefix + ".meta"):
+        raw = open(path, "rb").read()
+        mg = tf_bundle._parse(tf_bundle._parse(raw)[2][0]) if path.endswith(".pb") else tf_bundle._parse(raw)
+        nodes = tf_graph.graph_nodes(mg[2][0])
+
+        def resolves(tensor):
+            return tensor.lstrip("^").split(":")[0] in nodes
+
+        for n, v in nodes.items():
+            assert all(resolves(i) for i in v["inputs"]), (n, v["inputs"])
+        for e in mg.get(4, []):
+            kv = tf_bundle._parse(e)
+            for vd in tf_bundle._parse(tf_bundle._parse(kv[2][0])[2][0]).get(1, []):
+                f = tf_bundle._parse(vd)
+                for k in (1, 2, 3):
+                    assert resolves(f[k][0].decode()), (kv[1][0], k, f[k][0])
+                assert nodes[f[2][0].decode()]["op"] == "Assign"
+                assert nodes[f[3][0].decode().split(":")[0]]["op"] == "Identity"
+        sv = tf_bundle._parse(mg[3][0])
+        for k in (1, 2, 3):
+            assert resolves(sv[k][0].decode()), (k, sv[k][0])
+        for e in mg.get(5, []):
+            sd = tf_bundle._parse(tf_bundle._parse(e)[2][0])
+            for f in (1, 2):
+                for te in sd.get(f, []):
+                    info = tf_bundle._parse(tf_bundle._parse(te)[2][0])      # TensorInfo
+                    assert resolves(info[1][0].decode()), info[1][0]
+    sm = tf_graph.read_saved_model(os.path.join(d, "saved_model.pb"))
+    spec2, img = tf_graph.spec_from_graph(sm)
+    assert img == cfg.img_size
+    for k in ("in_channels", "n_cl_out", "base", "depth", "use_upsampling", "dims", "norm", "groups"):
+        assert getattr(spec2, k) == getattr(spec, k), k
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(norm="batch"), dict(use_upsampling=True, in_channels=1),
                                 dict(dims=3, in_channels=4)])
 def test_saved_model_pb_structure(tmp_path, kw):
     """export_model writes saved_model.pb: SavedModel {schema 1, MetaGraphDef tagged

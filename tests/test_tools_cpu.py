@@ -85,7 +85,10 @@ def test_export_then_sanity_check_matches_direct_forward(tmp_path, capsys):
     flat = FlatParams(spec)
     flat.load_dict(reference.init_params(spec, seed=3))
     d = export_model(cfg, spec, flat)
+    # the GraphDef is the consumed artefact: no JSON side-car needed (sanity_check_trained_model.py:37-41)
+    os.remove(os.path.join(d, "saved_model.json"))
     model = load_saved_model(d, device="cpu", batch=4)
+    assert (model.spec.in_channels, model.spec.base, model.img_size) == (4, 32, 32)
     x, y = synthetic_brats(10, 32, 4, seed=1)
     p = model.predict(x)
     with torch.no_grad():

@@ -1,11 +1,15 @@
 """Inference on an exported model (the reference's ``tf.saved_model.loader``
 flow, `sanity_check_trained_model.py:38-44`).
 
-:func:`load_saved_model` reads ``saved_model/saved_model.json`` (architecture +
-signature) and ``saved_model/variables/variables.{index,data-*}`` (TF bundle)
-written by :func:`utils.checkpoint.export_model`, and returns a
-:class:`Predictor` whose ``predict(x)`` maps NHWC(/NDHWC) float images to
-sigmoid probabilities -- the ``Placeholder:0 -> Mask/Sigmoid:0`` signature.
+:func:`load_saved_model` reads ``saved_model/saved_model.pb`` -- the ``serve`` tag, the
+``intel_unet_brats_model`` signature's input / output tensors (``Placeholder:0`` ->
+``Mask/Sigmoid:0``) and the UNet architecture recovered from the GraphDef
+(:func:`utils.tf_graph.spec_from_graph`: VariableV2 shapes, pool / upsample / norm
+nodes) -- and the weights from ``saved_model/variables/variables.{index,data-*}`` (TF
+bundle), both written by :func:`utils.checkpoint.export_model`; the JSON side-car is
+only a fallback for directories without a ``saved_model.pb``.  It returns a
+:class:`Predictor` whose ``predict(x)`` maps NHWC(/NDHWC) float images to sigmoid
+probabilities.
 
 On a GPU the native HIP executor's inference plan runs (forward only, dropout
 off, fused head+sigmoid) at a fixed micro-batch; a short last batch is padded.
@@ -80,18 +84,42 @@ class Predictor:
         return torch.cat(outs).numpy()
 
 
-def load_saved_model(export_dir: str, device=None, batch: int = 128, dtype: str = "bf16",
-                     backend: str = "auto") -> Predictor:
-    with open(os.path.join(export_dir, "saved_model.json")) as f:
+SIGNATURE = "intel_unet_brats_model"
+
+
+def _spec_from_pb(path: str):
+    from .utils import tf_graph
+    sm = tf_graph.read_saved_model(path)
+    if "serve" not in sm["tags"]:
+        raise ValueError("%s has no 'serve' meta graph" % path)
+    if SIGNATURE not in sm["signatures"]:
+        raise ValueError("%s has no %s signature" % (path, SIGNATURE))
+    sig = sm["signatures"][SIGNATURE]
+    if sig["inputs"]["image"]["name"] != "Placeholder:0" or sig["outputs"]["prediction"]["name"] != "Mask/Sigmoid:0":
+        raise ValueError("unexpected signature tensors %s" % sig)
+    return tf_graph.spec_from_graph(sm, SIGNATURE)
+
+
+def _spec_from_json(path: str):
+    with open(path) as f:
         meta = json.load(f)
     if "serve" not in meta.get("tags", []):
-        raise ValueError("export in %s has no 'serve' tag" % export_dir)
+        raise ValueError("export %s has no 'serve' tag" % path)
     m = meta["model"]
     spec = UNetSpec(in_channels=m["in_channels"], n_cl_out=m["n_cl_out"], base=m["base"], depth=m["depth"],
                     use_upsampling=m["use_upsampling"], dims=m["dims"], dropout=m["dropout"],
                     norm=m.get("norm", "none"), groups=m.get("groups", 8))
     sig = next(iter(meta["signature_def"].values()))
-    img_size = meta.get("img_size") or sig["inputs"]["image"]["shape"][1]
+    return spec, meta.get("img_size") or sig["inputs"]["image"]["shape"][1]
+
+
+def load_saved_model(export_dir: str, device=None, batch: int = 128, dtype: str = "bf16",
+                     backend: str = "auto") -> Predictor:
+    pb = os.path.join(export_dir, "saved_model.pb")
+    if os.path.exists(pb):
+        spec, img_size = _spec_from_pb(pb)
+    else:
+        spec, img_size = _spec_from_json(os.path.join(export_dir, "saved_model.json"))
     if device is None:
         device = "cuda:0" if torch.cuda.is_available() else "cpu"
     flat = FlatParams(spec, device=device)

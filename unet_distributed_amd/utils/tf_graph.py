@@ -12,11 +12,19 @@ Here the GraphDef is the inference graph of the UNet spec in TF 1.x op vocabular
 ``Conv2D``/``Conv3D`` + ``BiasAdd`` + ``Relu`` (BatchNorm / GroupNorm [EXT] as
 ``FusedBatchNorm`` inference / a ``GroupNorm`` placeholder op), ``MaxPool``,
 ``Conv2DBackpropInput`` for the transposed convs (output size from ``Shape`` of
-the input), ``ResizeNearestNeighbor`` for the upsampling variant, ``ConcatV2`` for
-the skips, ``Mask/Sigmoid`` at the end, plus the V2 Saver subgraph
-(``save/Const``, ``save/SaveV2``, ``save/RestoreV2``, ``save/Assign_*``,
-``save/restore_all``) that a SaverDef points at.  Dropout is not in the exported
-graph (inference mode).
+the input), ``ResizeNearestNeighbor`` for the 2D upsampling variant (3D: the
+nearest upsample as ``Reshape`` -> ``Tile`` -> ``Reshape``, TF 1.x has no 3D resize
+op), ``ConcatV2`` for the skips, ``Mask/Sigmoid`` at the end, plus the V2 Saver
+subgraph (``save/Const``, ``save/SaveV2``, ``save/RestoreV2``, ``save/Assign_*``,
+``save/restore_all``) that a SaverDef points at.  Every variable has the nodes its
+VariableDef names: ``<v>/Initializer/zeros`` -> ``<v>/Assign`` (initializer) and
+``<v>/read`` (snapshot).  Dropout is not in the exported graph (inference mode,
+SURVEY.md Q9).
+
+:func:`read_saved_model` parses the file back (tag, signature, GraphDef nodes and
+the VariableV2 shapes) and :func:`spec_from_graph` recovers the UNet architecture
+from the graph alone -- the exported ``saved_model.pb`` is the artefact
+``inference.load_saved_model`` consumes.
 
 Format parity is UNPINNED: TensorFlow is not installed, so the bytes are checked
 structurally (field numbers, names, shapes, signature) by tests/test_io_formats.py,
@@ -121,10 +129,24 @@ class _Graph:
         return b"".join(_fbytes(1, n) for n in self.nodes) + _fbytes(4, _fv(1, 24))
 
 
-def _variable(g: _Graph, name: str, shape) -> str:
-    g.node(name, "VariableV2", shape=_a_shape(shape), dtype=_a_type(DT_FLOAT), container=_a_s(""),
+def _tensor_zero(dtype: int, shape) -> bytes:
+    """TensorProto of `shape` filled with 0 (one value; TF repeats the last value)."""
+    import struct
+    val = _fbytes(10, b"\x00") if dtype == DT_INT64 else _fbytes(5, struct.pack("<f", 0.0))
+    return _fv(1, dtype) + _fbytes(2, _shape(shape)) + val
+
+
+def _variable(g: _Graph, name: str, shape, dtype: int = DT_FLOAT) -> str:
+    """VariableV2 + the nodes its VariableDef names: <v>/Initializer/zeros -> <v>/Assign
+    (initializer_name) and <v>/read (snapshot_name).  Returns the snapshot."""
+    loc = _fbytes(1, _fbytes(2, ("loc:@" + name).encode()))
+    g.node(name, "VariableV2", shape=_a_shape(shape), dtype=_a_type(dtype), container=_a_s(""),
            shared_name=_a_s(""))
-    return g.node(name + "/read", "Identity", [name], T=_a_type(DT_FLOAT), _class=_fbytes(1, _fbytes(2, ("loc:@" + name).encode())))
+    z = g.node(name + "/Initializer/zeros", "Const", dtype=_a_type(dtype), value=_a_tensor(_tensor_zero(dtype, shape)),
+               _class=loc)
+    g.node(name + "/Assign", "Assign", [name, z], T=_a_type(dtype), validate_shape=_a_b(True),
+           use_locking=_a_b(True), _class=loc)
+    return g.node(name + "/read", "Identity", [name], T=_a_type(dtype), _class=loc)
 
 
 def build_graph(spec, img_size: int, extra_vars: Sequence[Tuple[str, Tuple[int, ...]]] = ()) -> Tuple[_Graph, List[Tuple[str, Tuple[int, ...]]]]:
@@ -202,9 +224,21 @@ def build_graph(spec, img_size: int, extra_vars: Sequence[Tuple[str, Tuple[int, 
             pending_up = cur
         elif l.kind == "up":
             side = img_size >> (l.level - 1)
-            sz = g.const_i32(l.name + "/size", [side] * 2, [2])
-            cur = g.node(l.name + "/ResizeNearestNeighbor", "ResizeNearestNeighbor", [cur, sz],
-                         T=_a_type(DT_FLOAT), align_corners=_a_b(False))
+            if dims == 2:
+                sz = g.const_i32(l.name + "/size", [side] * 2, [2])
+                cur = g.node(l.name + "/ResizeNearestNeighbor", "ResizeNearestNeighbor", [cur, sz],
+                             T=_a_type(DT_FLOAT), align_corners=_a_b(False))
+            else:
+                # [N, D, H, W, C] -> [N, D, 1, H, 1, W, 1, C] -> tile x2 on the unit axes
+                # -> [N, 2D, 2H, 2W, C]: nearest-neighbour upsampling (UpSampling3D)
+                lo, c = side // 2, l.cin
+                s1 = g.const_i32(l.name + "/Reshape/shape", [-1, lo, 1, lo, 1, lo, 1, c], [8])
+                r1 = g.node(l.name + "/Reshape", "Reshape", [cur, s1], T=_a_type(DT_FLOAT), Tshape=_a_type(DT_INT32))
+                mu = g.const_i32(l.name + "/Tile/multiples", [1, 1, 2, 1, 2, 1, 2, 1], [8])
+                t = g.node(l.name + "/Tile", "Tile", [r1, mu], T=_a_type(DT_FLOAT), Tmultiples=_a_type(DT_INT32))
+                s2 = g.const_i32(l.name + "/Reshape_1/shape", [-1, side, side, side, c], [5])
+                cur = g.node(l.name + "/Reshape_1", "Reshape", [t, s2], T=_a_type(DT_FLOAT),
+                             Tshape=_a_type(DT_INT32))
             pending_up = cur
     if spec.norm == "batch":
         for l in spec.param_layers():
@@ -213,8 +247,7 @@ def build_graph(spec, img_size: int, extra_vars: Sequence[Tuple[str, Tuple[int, 
                               (l.name + "/norm/moving_variance", (l.cout,))]
     for n, shp in extra_vars:
         if n not in g.names:
-            dt = DT_INT64 if n == "global_step" else DT_FLOAT
-            g.node(n, "VariableV2", shape=_a_shape(shp), dtype=_a_type(dt), container=_a_s(""), shared_name=_a_s(""))
+            _variable(g, n, shp, DT_INT64 if n == "global_step" else DT_FLOAT)
         variables.append((n, tuple(shp)))
     _saver(g, [n for n, _ in variables])
     return g, variables
@@ -306,3 +339,86 @@ def write_meta(prefix: str, spec, img_size: int, var_shapes: Sequence[Tuple[str,
         f.write(mg)
     os.replace(tmp, path)
     return path
+
+
+# ------------------------------------------------------------------ reading it back
+def _i64(v: int) -> int:
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+def _parse_shape(b: bytes) -> List[int]:
+    from .tf_bundle import _parse
+    return [_i64(_parse(d).get(1, [0])[0]) for d in _parse(b).get(2, [])]
+
+
+def graph_nodes(graph_def: bytes) -> Dict[str, dict]:
+    """GraphDef bytes -> {name: {"op", "inputs", "attr": {key: AttrValue fields}}}."""
+    from .tf_bundle import _parse
+    out = {}
+    for nb in _parse(graph_def).get(1, []):
+        n = _parse(nb)
+        attrs = {}
+        for e in n.get(5, []):
+            kv = _parse(e)
+            attrs[kv[1][0].decode()] = _parse(kv[2][0]) if 2 in kv else {}
+        out[n[1][0].decode()] = {"op": n[2][0].decode(), "inputs": [i.decode() for i in n.get(3, [])],
+                                 "attr": attrs}
+    return out
+
+
+def read_saved_model(path: str) -> dict:
+    """saved_model.pb -> {"tags", "signatures": {name: {"inputs": {k: tensor}, "outputs":
+    {k: tensor}, "method"}}, "nodes", "variables": {name: shape}} of its first MetaGraph."""
+    from .tf_bundle import _parse
+    sm = _parse(open(path, "rb").read())
+    mg = _parse(sm[2][0])
+    info = _parse(mg[1][0])
+    sigs = {}
+    for e in mg.get(5, []):
+        kv = _parse(e)
+        sd = _parse(kv[2][0])
+        io = []
+        for f in (1, 2):
+            m = {}
+            for te in sd.get(f, []):
+                tkv = _parse(te)
+                ti = _parse(tkv[2][0])
+                m[tkv[1][0].decode()] = {"name": ti[1][0].decode(), "shape": _parse_shape(ti[3][0]) if 3 in ti else None}
+            io.append(m)
+        sigs[kv[1][0].decode()] = {"inputs": io[0], "outputs": io[1],
+                                   "method": sd[3][0].decode() if 3 in sd else ""}
+    nodes = graph_nodes(mg[2][0])
+    var_shapes = {k: _parse_shape(v["attr"]["shape"][7][0]) for k, v in nodes.items() if v["op"] == "VariableV2"}
+    return {"tags": [t.decode() for t in info.get(4, [])], "signatures": sigs, "nodes": nodes,
+            "variables": var_shapes, "meta_graph": mg}
+
+
+def spec_from_graph(sm: dict, signature: str = "intel_unet_brats_model"):
+    """(UNetSpec, img_size) of an exported inference graph: input channels / rank / size
+    from the signature's input placeholder, the base width from conv1a's kernel, the
+    depth from the max-pool count, the decoder variant from the transposed-conv /
+    upsampling nodes, the normalisation from FusedBatchNorm / GroupNorm nodes, the
+    classes from the Mask kernel.  (Dropout is not part of an inference graph: the
+    spec keeps the default rate, which only training uses.)"""
+    from ..models.spec import UNetSpec
+    nodes, var = sm["nodes"], sm["variables"]
+    sig = sm["signatures"].get(signature) or next(iter(sm["signatures"].values()))
+    inp = next(iter(sig["inputs"].values()))["name"].split(":")[0]
+    out = next(iter(sig["outputs"].values()))["name"].split(":")[0]
+    if inp not in nodes or out not in nodes:
+        raise ValueError("signature tensors %s / %s are not in the graph" % (inp, out))
+    shp = _parse_shape(nodes[inp]["attr"]["shape"][7][0])
+    dims = len(shp) - 2
+    ops = [v["op"] for v in nodes.values()]
+    depth = sum(1 for o in ops if o in ("MaxPool", "MaxPool3D"))
+    gn = [v for v in nodes.values() if v["op"] == "GroupNorm"]
+    norm = "batch" if "FusedBatchNorm" in ops else ("group" if gn else "none")
+    groups = _i64(gn[0]["attr"]["groups"][3][0]) if gn else 8
+    ups = any(k.startswith("up") for k, v in nodes.items() if v["op"] in ("ResizeNearestNeighbor", "Tile"))
+    spec = UNetSpec(in_channels=shp[-1], n_cl_out=var["Mask/kernel"][-1], base=var["conv1a/kernel"][-1],
+                    depth=depth, use_upsampling=ups, dims=dims, norm=norm, groups=groups)
+    for name, s in spec.variables():
+        if tuple(var.get(name, ())) != tuple(s):
+            raise ValueError("graph variable %s has shape %s, the recovered spec expects %s"
+                             % (name, var.get(name), s))
+    return spec, shp[1]
