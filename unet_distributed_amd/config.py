@@ -70,6 +70,7 @@ class Config:
     synthetic: bool = False
     synthetic_train: int = 2048
     synthetic_test: int = 256
+    synthetic_difficulty: str = "easy"   # easy | hard (datasets.synthetic_brats)
     data_on_device: str = "auto"     # auto | on | off: keep the train set resident in HBM
     data_path: str = settings.OUT_PATH
     steps: int = 0                   # >0 overrides epochs*num_batches
@@ -120,6 +121,7 @@ _CHOICES = {
     "device": ("auto", "cuda", "cpu"),
     "dist_backend": ("auto", "nccl", "gloo"),
     "data_on_device": ("auto", "on", "off"),
+    "synthetic_difficulty": ("easy", "hard"),
 }
 
 

@@ -196,9 +196,11 @@ class Trainer:
         if cfg.synthetic:
             n_tr = max(cfg.synthetic_train, cfg.batch_size)
             self.x_train, self.y_train = datasets.synthetic_brats(n_tr, cfg.img_size, cfg.in_channels,
-                                                                  cfg.dims, seed=cfg.seed)
+                                                                  cfg.dims, seed=cfg.seed,
+                                                                  difficulty=cfg.synthetic_difficulty)
             self.x_test, self.y_test = datasets.synthetic_brats(cfg.synthetic_test, cfg.img_size,
-                                                                cfg.in_channels, cfg.dims, seed=cfg.seed + 1)
+                                                                cfg.in_channels, cfg.dims, seed=cfg.seed + 1,
+                                                                difficulty=cfg.synthetic_difficulty)
         else:
             xi, yi = datasets.load_data(cfg.data_path, "_train")
             self.x_train, self.y_train = datasets.update_channels(xi, yi, cfg.in_channels, cfg.out_channels, cfg.mode)
