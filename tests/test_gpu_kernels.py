@@ -653,7 +653,7 @@ def test_conv_fwd_relu_bits(cuda_dev, N, H, Cin, Cout, tile, drop):
     assert torch.equal(bits, _pack_bits(y1))
 
 
-@pytest.mark.parametrize("tile", [6, 8, 12, 13])
+@pytest.mark.parametrize("tile", [6, 8, 12])
 def test_conv_dgrad_bit_masks_match_activation_masks(cuda_dev, tile):
     """Data gradient with two destinations whose ReLU masks come from bit tensors
     (mask_bits) equals the same launch masked by the 16-bit activations."""

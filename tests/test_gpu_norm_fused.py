@@ -296,55 +296,6 @@ def test_conv_fwd_operand_norm_on_load(cuda_dev, N, H, Cin, Cout, gn, tile, stat
         assert torch.allclose(tot[0], zf.sum(0), rtol=1e-3, atol=1e-2 * H)
 
 
-@pytest.mark.parametrize("N,H,Cg,Cy,gn,tile,norm_epi", [
-    (2, 128, 32, 32, False, 6, False),      # dgrad into a ReLU'd input (bit mask), BatchNorm dz
-    (2, 64, 64, 32, True, 0, True),         # dgrad into a normalised input (EPI_DGRAD_NORM), GroupNorm dz
-    (4, 16, 128, 128, False, 0, False),
-    (2, 128, 32, 64, True, 13, True),
-])
-def test_conv_dgrad_operand_dz_on_load(cuda_dev, N, H, Cg, Cy, gn, tile, norm_epi):
-    """xform 2: the data gradient reads g (the gradient of the norm's output) and the
-    pre-norm z, forms dz = a g + b z + c in LDS and convolves it; equals the dgrad of
-    the materialised dz, and xout holds dz."""
-    torch.manual_seed(51)
-    g = torch.randn(N, H, H, Cg, device=cuda_dev).bfloat16()
-    z = torch.randn(N, H, H, Cg, device=cuda_dev).bfloat16()
-    rows = N if gn else 1
-    ca = 0.5 + torch.rand(rows, Cg, device=cuda_dev)
-    cb = 0.2 * torch.randn(rows, Cg, device=cuda_dev)
-    cc = 0.1 * torch.randn(rows, Cg, device=cuda_dev)
-    v = lambda t: t.view(rows, 1, 1, Cg).double()
-    dz_ref = _bf((v(ca) * g.double() + (v(cb) * z.double() + v(cc))).float())
-    w = (torch.randn(3, 3, Cy, Cg, device=cuda_dev) * 0.1).bfloat16()
-    wp = pack_dgrad(w)
-    dx = torch.empty(N, H, H, Cy, device=cuda_dev, dtype=torch.bfloat16)
-    dzo = torch.full_like(g, float("nan"))
-    d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cg, src1=ptr(g), wgt=ptr(wp), Cout=Cy, relu=0,
-             dst1=ptr(dx), tile=tile, xform=2, xa=ptr(ca), xb=ptr(cb), xc=ptr(cc), xz=ptr(z),
-             xcs=Cg if gn else 0, xout=ptr(dzo))
-    zy = torch.randn(N, H, H, Cy, device=cuda_dev).bfloat16()         # pre-norm input of the conv
-    if norm_epi:
-        na = 0.5 + torch.rand(Cy, device=cuda_dev)
-        nc = 0.3 * torch.randn(Cy, device=cuda_dev)
-        d.update(nz=ptr(zy), na=ptr(na), nc=ptr(nc), ncs=0, npix=H * H)
-        nr, _ = C().conv_stat_tiles(dict(d, stats=1))
-        st = torch.zeros(nr, 2, Cy, device=cuda_dev)
-        d["stats"] = ptr(st)
-        mask = (na.view(1, 1, 1, Cy) * zy.float() + nc.view(1, 1, 1, Cy)) > 0
-    else:
-        d.update(mask1=ptr(zy))
-        mask = zy.float() > 0
-    C().conv_fwd(d, stream())
-    torch.cuda.synchronize()
-    xr = torch.zeros(N, Cy, H, H, device=cuda_dev, requires_grad=True)
-    (gref,) = torch.autograd.grad(F.conv2d(xr, w.float().permute(3, 2, 0, 1), padding=1), xr,
-                                  nchw(dz_ref.float()))
-    gref = nhwc(gref) * mask
-    assert rel_err(dx, gref) < 1e-2
-    assert torch.isfinite(dzo.float()).all()
-    assert (dzo.float() - dz_ref.float()).abs().max() <= 1e-2 * dz_ref.float().abs().max()
-
-
 @pytest.mark.parametrize("N,H,Ch,gn,dims3", [(2, 64, 32, False, 0), (3, 32, 64, True, 0), (2, 16, 32, True, 1)])
 def test_norm_pool_matches_apply_then_pool(cuda_dev, N, H, Ch, gn, dims3):
     """norm_pool (normalise a convNb output and max-pool it in one pass) writes the

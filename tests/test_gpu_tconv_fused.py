@@ -1,0 +1,119 @@
+"""Composite transposed-conv backward (tconv_fused.hip + conv_win.h XF 4) against an
+fp32 autograd reference of the decoder step u = tconv(b); z = conv3x3([u, skip]).
+
+The data gradient of b is one coarse 3x3 row-window conv over the space-to-depth image
+of dz with composed weights; the tconv weight / bias gradients come from the 4x4-tap
+stride-2 slab sums through the chain rule.  du is never formed."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def C():
+    from unet_distributed_amd import native
+    return native.require()
+
+
+def ptr(t):
+    return int(t.data_ptr())
+
+
+def stream():
+    return int(torch.cuda.current_stream().cuda_stream)
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1)
+
+
+def pack_bits(y):
+    pos = (y.float() > 0).to(torch.int32).reshape(*y.shape[:-1], y.shape[-1] // 8, 8)
+    return (pos << torch.arange(8, device=y.device, dtype=torch.int32)).sum(-1).to(torch.uint8)
+
+
+def _problem(dev, N, H, K, Cc, Cs, O, seed):
+    torch.manual_seed(seed)
+    b = F.relu(torch.randn(N, H, H, K, device=dev)).bfloat16()
+    skip = torch.randn(N, 2 * H, 2 * H, Cs, device=dev).bfloat16()
+    wt = torch.randn(2, 2, Cc, K, device=dev) * 0.1          # Keras Conv2DTranspose (kh, kw, Cout, Cin)
+    bt = torch.randn(Cc, device=dev) * 0.1
+    wa = torch.randn(3, 3, Cc + Cs, O, device=dev) * 0.1      # HWIO, u channels first
+    dz = torch.randn(N, 2 * H, 2 * H, O, device=dev).bfloat16()
+    return b, skip, wt, bt, wa, dz
+
+
+def _reference(b, skip, wt, bt, wa, dz):
+    bf = nchw(b.float()).requires_grad_(True)
+    wtr = wt.clone().requires_grad_(True)
+    btr = bt.clone().requires_grad_(True)
+    u = F.conv_transpose2d(bf, wtr.permute(3, 2, 0, 1), btr, stride=2)
+    z = F.conv2d(torch.cat([u, nchw(skip.float())], 1), wa.permute(3, 2, 0, 1), padding=1)
+    gb, gwt, gbt = torch.autograd.grad(z, (bf, wtr, btr), nchw(dz.float()))
+    return nhwc(gb) * (b.float() > 0), gwt, gbt
+
+
+@pytest.mark.parametrize("N,H,K,Cc,Cs,O", [(2, 64, 64, 32, 32, 32), (2, 32, 128, 64, 64, 64),
+                                            (3, 16, 64, 32, 32, 32), (1, 32, 64, 32, 0, 32)])
+def test_composite_tconv_dgrad(cuda_dev, N, H, K, Cc, Cs, O):
+    """db = S2D(dz) (*) compose(Wt, Wa), masked by the ReLU bits of b -- vs autograd."""
+    b, skip, wt, bt, wa, dz = _problem(cuda_dev, N, H, K, Cc, Cs, O, 11)
+    ref_db, _, _ = _reference(b, skip, wt, bt, wa, dz)
+    rs = (36 * O + 63) // 64 * 64
+    wg = torch.empty(K, rs, device=cuda_dev, dtype=torch.bfloat16)
+    C().generic("tconv_compose", [ptr(wt.reshape(4, Cc, K).contiguous()), ptr(wa.contiguous()), ptr(wg)],
+                [Cc, K, O, Cc + Cs, rs], [], stream())
+    bits = pack_bits(b)
+    db = torch.empty(N, H, H, K, device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=4 * O, s2d=O, src1=ptr(dz), wgt=ptr(wg),
+                      Cout=K, dst1=ptr(db), mask1=ptr(bits), mask_bits=1), stream())
+    torch.cuda.synchronize()
+    assert rel_err(db, ref_db) < 2e-2
+
+
+@pytest.mark.parametrize("N,H,K,Cc,Cs,O,splits,win", [(2, 64, 64, 32, 32, 32, 8, 0), (2, 64, 64, 32, 32, 32, 8, -1),
+                                                       (2, 32, 128, 64, 64, 64, 5, 0), (3, 32, 32, 32, 32, 32, 7, 0),
+                                                       (2, 32, 128, 64, 64, 64, 70, 0), (3, 16, 64, 32, 32, 32, 3, 0)])
+def test_composite_tconv_weight_grads(cuda_dev, N, H, K, Cc, Cs, O, splits, win):
+    """4x4-tap stride-2 slab sums H / per-tap bias sums Bs (coarse rows 32 / 64 wide: the
+    window kernel, win -1 / 16 wide: the tiled kernel) -> chain rule -> dWt, dbt."""
+    b, skip, wt, bt, wa, dz = _problem(cuda_dev, N, H, K, Cc, Cs, O, 12)
+    _, ref_wt, ref_bt = _reference(b, skip, wt, bt, wa, dz)
+    dev = cuda_dev
+    slab = torch.zeros(splits * 16 * O * K, device=dev)
+    bslab = torch.zeros(splits * 16 * O, device=dev)
+    C().wgrad(dict(N=N, QD=1, QH=H, QW=H, AD=1, AH=2 * H, AW=2 * H, KD=1, KH=4, KW=4, stride=2, pad=1,
+                   a1=ptr(dz), b=ptr(b), M1=O, M2=0, Nc=K, splits=splits, slab=ptr(slab), bias_slab=ptr(bslab),
+                   bias_mode=2, win=win), stream())
+    Hs = torch.zeros(16 * O * K, device=dev)
+    Bs = torch.zeros(16 * O, device=dev)
+    stage = torch.zeros(C().wgrad_reduce_stage_floats(max(splits, 64), 16, O, K) + 4096, device=dev)
+    C().generic("wgrad_reduce", [ptr(slab), ptr(Hs), ptr(stage)], [splits, 16, O, O, K], [1.0], stream())
+    C().generic("wgrad_reduce", [ptr(bslab), ptr(Bs), ptr(stage)], [splits, 1, 1, 1, 16 * O], [1.0], stream())
+    # the slab sums themselves: H[sh][sw][o][k] = sum_{h,w} dz[2h + sh - 1][2w + sw - 1][o] b[h][w][k]
+    dzp = F.pad(dz.float(), (0, 0, 1, 3, 1, 3))               # fine rows / cols -1 .. 2H + 1
+    for sh in range(4):
+        for sw in range(4):
+            sl = dzp[:, sh:sh + 2 * H:2, sw:sw + 2 * H:2, :]
+            ref_h = torch.einsum("nhwo,nhwk->ok", sl, b.float())
+            got = Hs.view(16, O, K)[sh * 4 + sw]
+            assert rel_err(got, ref_h) < 1e-3, (sh, sw)
+            assert rel_err(Bs.view(16, O)[sh * 4 + sw], sl.sum((0, 1, 2))) < 1e-3, (sh, sw)
+    dwt = torch.zeros(4, Cc, K, device=dev)
+    dbt = torch.zeros(Cc, device=dev)
+    C().generic("tconv_chain", [ptr(Hs), ptr(Bs), ptr(wa.contiguous()), ptr(dwt), ptr(dbt)], [Cc, K, O, Cc + Cs], [],
+                stream())
+    torch.cuda.synchronize()
+    assert rel_err(dwt, ref_wt.reshape(4, Cc, K)) < 1e-3
+    assert rel_err(dbt, ref_bt) < 1e-3

@@ -31,7 +31,17 @@ def test_plan_construction_dry_run(kw, img, dtype):
     names = e.plan.names()
     assert names[0] == "fwd:conv1a" and names[e.fwd_end - 1] == "fwd:Mask"
     # (head-on-load: the head backward only reduces the Mask gradients, on the side stream)
-    assert names[e.fwd_end] == ("wgrad:Mask" if e.head_onload else "bwd:Mask")
+    nc = len(e.tconv_fused)
+    assert [n for n in names[e.fwd_end:e.fwd_end + nc]] == ["compose:" + t for t in e.tconv_fused]
+    assert names[e.fwd_end + nc] == ("wgrad:Mask" if e.head_onload else "bwd:Mask")
+    # composite transposed convs (2D norm-free): no tconv data gradient, no fine output
+    # gradient, the chain rule after the reduction of their slab sums
+    if kw.get("dims", 2) == 2 and kw.get("norm", "none") == "none" and not kw.get("use_upsampling"):
+        assert sorted(e.tconv_fused) == ["transConv8", "transConv9"]
+    for t in e.tconv_fused:
+        assert "dgrad:" + t not in names and "d:" + t not in e.bufs
+        i = names.index("chain:" + t)
+        assert any(n.startswith("reduce:") and t in n[7:].split(",") for n in names[:i])
     # every conv / tconv gradient is reduced by exactly one batched reduce op
     reduced = [ln for n in names if n.startswith("reduce:") for ln in n[len("reduce:"):].split(",")]
     assert sorted(reduced) == sorted(l.name for l in spec.param_layers() if l.kind != "mask")
@@ -83,7 +93,7 @@ def test_engine_env_knobs_are_few():
     src = open(native_engine.__file__).read()
     knobs = set(re.findall(r'os\.environ\.get\("(UNET_[A-Z0-9_]+)"', src))
     assert knobs <= {"UNET_DUAL_STREAM", "UNET_CONV_TILE", "UNET_FWD_STREAMS", "UNET_HEAD_FUSE",
-                     "UNET_HEAD_ONLOAD"}, knobs
+                     "UNET_HEAD_ONLOAD", "UNET_TCONV_FUSED"}, knobs
 
 
 def test_fused_head_plan(monkeypatch):

@@ -150,7 +150,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
         float x = G ? acc[i][j][r] * p.out_scale + bsv[r] : acc[i][j][r] + bsv[r];
         if (kRelu) x = fmaxf(x, 0.f);
         if (kDrop) {
-          const uint32_t h = drop_hash((uint64_t)q * p.Cout + n + r, seed, p.salt);
+          const uint32_t h = drop_hash((uint64_t)q * p.Cout + n + r + p.drop_idx0, seed, p.salt);
           x = (h >= drop_thr) ? x * inv_keep : 0.f;
         }
         if (kMaskScale) x *= msc[r];

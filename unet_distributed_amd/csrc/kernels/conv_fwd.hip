@@ -759,6 +759,10 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
                     p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) || conv_epi_mode(p) != EPI_DGRAD ||
                     p.route_gy || (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12)))
     return "conv_fwd: head-on-load needs a 2D 32-channel row-window data gradient";
+  if (p.s2d && (p.s2d % 32 || p.C1 != 4 * p.s2d || p.C2 || p.xform || p.hg.prob || p.route_gy || p.KD != 1 ||
+                p.OD != 1 || p.OW > 128 || !win_eligible(p) || conv_epi_mode(p) != EPI_DGRAD ||
+                (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12)))
+    return "conv_fwd: space-to-depth source needs a 2D single-source row-window data gradient (C1 = 4 s2d)";
   if (p.route_gy && (!p.pool_code || (conv_epi_mode(p) != EPI_DGRAD && conv_epi_mode(p) != EPI_DGRAD_NORM) ||
                      !win_eligible(p) || p.KD != 1 || p.OD != 1 ||
                      p.OH % 2 || p.OW % 2 || p.D1 != p.Cout || p.pool_dst || p.mask_scale1 != 1.f ||

@@ -42,6 +42,9 @@ struct ConvFwdParams {
   float out_scale;
   float drop_rate;            // >0: inverted dropout on the output
   uint32_t seed, salt;
+  // element-index offset of the dropout hash: a launch over images [c nb, ..) of a batch
+  // draws the keep-mask of those elements of the whole-batch launch (two-stream forward)
+  unsigned long long drop_idx0;
   const uint32_t* seed_ptr;   // non-null: the per-step seed is read from device memory
                               // (HIP-graph replay, where kernel arguments are frozen)
   void* dst1;                 // channels [0, D1)
@@ -109,6 +112,12 @@ struct ConvFwdParams {
                               // where its producer ended, on the tail still in the Infinity Cache)
   HeadGrad hg;                // 2D row-window data gradient of the head input: src1 (dY) formed
                               // on load (one 32-channel chunk), see HeadGrad
+  // Space-to-depth source (2D row-window, composite transposed-conv data gradient):
+  // s2d = C > 0 -> src1 is a FINE [N][2H][2W][C] tensor read as the coarse H x W image
+  // with 4C channels (a, b, c) = src1[2h + a][2w + b][c]; C1 = 4C.  Each 32-channel chunk
+  // lies in one phase group (a, b) whose 3x3 taps are structurally zero outside the 2x2
+  // support dh in {1 - a, 2 - a}, dw in {1 - b, 2 - b}: those MFMAs are skipped.
+  int s2d;
   // filled by conv_fwd_prepare (host): K padded to 64, per-tap pixel deltas / offsets
   int Kpad;
   int tap_delta[27];

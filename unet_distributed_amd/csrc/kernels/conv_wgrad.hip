@@ -1248,6 +1248,158 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
   }
 }
 
+// Composite transposed-conv slab sums (tconv_fused.hip) on windows of whole coarse rows:
+//   slab[split][4 sh + sw][o][k] = sum_{coarse px (h, w)} dz[2h + sh - 1][2w + sw - 1][o] * b[h][w][k]
+//   bias_slab[split][4 sh + sw][o] = sum_{(h, w)} dz[2h + sh - 1][2w + sw - 1][o]
+// (the generic tiled kernel with 4x4 taps re-read the coarse operand once per tap).  Per
+// window of R = 128 / W coarse rows the workgroup LDS-DMAs the coarse b rows (QN 32-channel
+// blocks, read once for all 16 taps) and the 2R + 2 fine dz rows 2 g0 - 1 .. 2 g0 + 2R with
+// even / odd columns de-interleaved (even e = 0..W-1 at slots 0..W-1, zero at W; zero at
+// W + 1, odd o = 0..W-1 at W + 2..2W + 1), so every tap's pixels are consecutive slots.
+// Wave sh owns the four taps (sh, sw): column shift sw - 1 reads odd column w - 1 (sw 0),
+// even w (1), odd w (2), even w + 1 (3).  Both operands go through ds_read_b64_tr_b16.
+template <int W, int QN>
+__global__ void __launch_bounds__(NTHR) wgrad_s2d_win_kernel(const WgradParams p) {
+  constexpr int BMc = 128, R = BMc / W, FP = 2 * W + 2, FR = 2 * R + 2;
+  constexpr int XI = QN * BMc / 16, YI = (FR * FP + 15) / 16;
+  constexpr int XB = XI * 1024, YB = YI * 1024;
+  constexpr int KS = BMc / 32;
+  static_assert(W >= 32 && W <= 64, "composite window wgrad");
+  __shared__ __attribute__((aligned(1024))) char smem[XB + YB];
+  char* Xs = smem;
+  char* Ys = smem + XB;
+
+  const int tid = threadIdx.x, lane = tid & 63, sh = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = p.QH;
+  const int rows_total = p.N * H;
+  const int Mq = rows_total * W;
+  const int nwin = rows_total / R;                 // H % R == 0: windows never span images
+  const int O = p.M1, K = p.Nc;
+  const int kt = K / (32 * QN);
+  const int ntile = (O / 32) * kt;
+  const int bid = (p.xcd & 1) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int lsplit = bid / ntile, tile = bid - lsplit * ntile;
+  const int split = p.split_lo + lsplit;
+  const int o_blk = tile / kt, k_blk = tile - o_blk * kt;
+  const int o0 = o_blk * 32, k0 = k_blk * 32 * QN;
+  constexpr int OOB = 0x7fffffff;
+  const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc((void*)p.a1, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, OOB, 0x00020000);
+  const int w_begin = (int)((long long)split * nwin / p.splits);
+  const int w_end = (int)((long long)(split + 1) * nwin / p.splits);
+  const bool do_bias = p.bias_mode == 2 && k_blk == 0;
+
+  f32x4 acc[4][2][2 * QN];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2 * QN; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 bacc[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) bacc[t][0] = bacc[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const u32x4 ones_u = {kOnes2, kOnes2, kOnes2, kOnes2};
+  const h16x8 ones = __builtin_bit_cast(h16x8, ones_u);
+  const int lslot = lane >> 2;
+  const int lchunk = (lane & 3) ^ (((lslot >> 3) & 1) << 1);
+  const int G = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  auto tr_addr = [&](int slot, int ch) -> int {   // swizzle keyed on slot mod 16
+    return slot * 64 + ((((ch >> 3) ^ (((slot >> 3) & 1) << 1))) << 4) + ((ch & 7) << 1);
+  };
+  auto tr8 = [&](const char* base0, const char* base1) -> h16x8 {
+    const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base0));
+    const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base1));
+    const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+    const u32x4 v = {l2[0], l2[1], h2[0], h2[1]};
+    return __builtin_bit_cast(h16x8, v);
+  };
+  // slot of coarse column w for tap column sw within a staged fine row
+  auto col_slot = [&](const int sw, const int w) -> int {
+    return sw == 0 ? W + 1 + w : sw == 1 ? w : sw == 2 ? W + 2 + w : w + 1;
+  };
+
+  for (int win = w_begin; win < w_end; ++win) {
+    const int g0 = win * R;
+    const int fimg0 = 2 * (g0 - g0 % H);             // first fine row of the window's image
+    __syncthreads();
+#pragma unroll
+    for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
+      const int k = sh + 4 * qq;
+      if (k < XI) {
+        const int o = k / (BMc / 16), sb = (k - o * (BMc / 16)) * 16;   // x image o (channel block)
+        const int pix = g0 * W + sb + lslot;
+        const int off = pix < Mq ? (pix * K + k0 + 32 * o + lchunk * 8) * 2 : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsx, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int qq = 0; qq < (YI + 3) / 4; ++qq) {
+      const int k = sh + 4 * qq;
+      if (k < YI) {
+        const int sl = 16 * k + lslot;
+        const int fr = sl / FP, ps = sl - fr * FP;
+        const int gf = 2 * g0 - 1 + fr;                 // fine row
+        const bool odd = ps > W;
+        const int cc = odd ? ps - (W + 2) : ps;          // column index in its parity class
+        const bool ok = fr < FR && gf >= fimg0 && gf < fimg0 + 2 * H && (unsigned)cc < (unsigned)W;
+        const int col = odd ? 2 * cc + 1 : 2 * cc;
+        const int off = ok ? ((gf * (2 * W) + col) * O + o0 + lchunk * 8) * 2 : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsy, (__attribute__((address_space(3))) void*)(Ys + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int kk = 0; kk < KS; ++kk) {
+      const int px0 = kk * 32;
+      const int rr = px0 / W, c0 = px0 - rr * W;
+      h16x8 bf[2 * QN];
+#pragma unroll
+      for (int qn = 0; qn < QN; ++qn)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const char* Xq = Xs + qn * (BMc * 64);
+          const int s0 = px0 + 8 * G + q;
+          bf[2 * qn + j] = tr8(Xq + tr_addr(s0, 16 * j + 4 * pp), Xq + tr_addr(s0 + 4, 16 * j + 4 * pp));
+        }
+      const int rowb = (2 * rr + sh) * FP;              // staged row of fine row 2(g0 + rr) + sh - 1
+#pragma unroll
+      for (int sw = 0; sw < 4; ++sw) {
+        const int s0 = rowb + col_slot(sw, c0 + 8 * G + q);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const h16x8 af = tr8(Ys + tr_addr(s0, 16 * i + 4 * pp), Ys + tr_addr(s0 + 4, 16 * i + 4 * pp));
+#pragma unroll
+          for (int j = 0; j < 2 * QN; ++j) acc[sw][i][j] = mfma16(af, bf[j], acc[sw][i][j]);
+          if (do_bias) bacc[sw][i] = mfma16(af, ones, bacc[sw][i]);
+        }
+      }
+    }
+  }
+
+  // acc[sw][i][j][r] = slab[tap][o0 + 16i + 4(lane >> 4) + r][k0 + 16j + (lane & 15)]
+#pragma unroll
+  for (int sw = 0; sw < 4; ++sw) {
+    const int tap = sh * 4 + sw;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = o0 + 16 * i + 4 * (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < 2 * QN; ++j) {
+        float* o = p.slab + (((size_t)split * 16 + tap) * O + m) * K + k0 + 16 * j + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[(size_t)r * K] = acc[sw][i][j][r];
+      }
+      if (do_bias && (lane & 15) == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p.bias_slab[((size_t)split * 16 + tap) * O + m + r] = bacc[sw][i][r];
+      }
+    }
+  }
+}
+
 template <int W, int QO, int GEO>
 hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
   const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.KD * launch_splits(p);
@@ -1313,6 +1465,14 @@ static bool wgrad_tconv_win_eligible(const WgradParams& p) {
          (p.M1 % 32) == 0 && (p.Nc % 32) == 0 && p.bias_mode != 1;
 }
 
+// Composite transposed-conv slab sums (4x4 taps, stride 2, pad 1) on coarse rows 32 / 64 wide.
+static bool wgrad_s2d_win_eligible(const WgradParams& p) {
+  const int R = p.QW > 0 ? 128 / p.QW : 1;
+  return p.win >= 0 && (p.QW == 32 || p.QW == 64) && p.QD == 1 && p.KD == 1 && p.KH == 4 && p.KW == 4 &&
+         p.stride == 2 && p.pad == 1 && p.upA == 1 && p.AW == 2 * p.QW && p.AH == 2 * p.QH && p.QH % R == 0 &&
+         p.M2 == 0 && (p.M1 % 32) == 0 && (p.Nc % 32) == 0 && p.bias_mode != 1;
+}
+
 WgradCfg wgrad_pick(const WgradParams& p) {
   const int KT = p.KD * p.KH * p.KW;
   const int M = p.M1 + p.M2;
@@ -1320,7 +1480,12 @@ WgradCfg wgrad_pick(const WgradParams& p) {
   if (wgrad_win_first_eligible(p)) return {p.M1 == 4 ? 48 : 80, 32, 1, 1};      // first-layer window
   if (wgrad_tconv_win_eligible(p))                                                 // transposed-conv window
     return {32, p.Nc % 128 == 0 ? 128 : (p.Nc % 64 == 0 ? 64 : 32), 4, 0};
+  if (wgrad_s2d_win_eligible(p)) return {32, p.Nc % 64 == 0 ? 64 : 32, 16, 0};   // composite window
   if ((p.M1 == 4 || p.M1 == 8) && p.M2 == 0) return {64, 32, 1, 1};
+  // composite transposed-conv slab (tconv_fused.hip): 4x4 taps, stride 2, pad 1, one tap
+  // per tile so bias mode 2 yields the per-tap sums
+  if (p.KH == 4 && p.KW == 4 && p.KD == 1 && p.stride == 2 && p.pad == 1 && p.M1 % 32 == 0 && p.M2 == 0)
+    return {32, p.Nc % 64 == 0 ? 64 : 32, 1, 0};
   if (M <= 64 && p.Nc <= 64 && KT % 9 == 0) return {32, 32, 9, 0};
   if (M <= 64 && p.Nc <= 64 && KT % 4 == 0) return {32, 32, 4, 0};
   if (M % 128 == 0 && p.Nc % 128 == 0) return {128, 128, 1, 0};
@@ -1375,6 +1540,18 @@ hipError_t wgrad_launch(const WgradParams& p0, hipStream_t s) {
 #undef TW_CASE
     return hipGetLastError();
   }
+  if (wgrad_s2d_win_eligible(p)) {
+    const int qn = p.Nc % 64 == 0 ? 2 : 1;
+    const int grid = (p.M1 / 32) * (p.Nc / (32 * qn)) * launch_splits(p);
+#define SW_CASE(WW, QQ) hipLaunchKernelGGL((wgrad_s2d_win_kernel<WW, QQ>), dim3(grid), dim3(NTHR), 0, s, p)
+    if (p.QW == 32) {
+      if (qn == 2) SW_CASE(32, 2); else SW_CASE(32, 1);
+    } else {
+      if (qn == 2) SW_CASE(64, 2); else SW_CASE(64, 1);
+    }
+#undef SW_CASE
+    return hipGetLastError();
+  }
   if (wgrad_win_eligible(p)) {
     const bool q2 = c.BN == 64;
     switch (p.QW) {
@@ -1386,6 +1563,7 @@ hipError_t wgrad_launch(const WgradParams& p0, hipStream_t s) {
     }
   }
   if (c.smallc) return launch_wg<64, 32, 1, 2, 2, true>(p, s);
+  if (c.BM == 32 && c.NTAP == 1) return c.BN == 64 ? launch_wg<32, 64, 1, 2, 2>(p, s) : launch_wg<32, 32, 1, 2, 2>(p, s);
   if (c.BM == 32 && c.NTAP == 9) return launch_wg<32, 32, 9, 2, 2>(p, s);
   if (c.BM == 32 && c.NTAP == 4) return launch_wg<32, 32, 4, 2, 2>(p, s);
   if (c.BM == 128) return launch_wg<128, 128, 1, 2, 2>(p, s);

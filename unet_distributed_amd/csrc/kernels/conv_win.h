@@ -84,11 +84,12 @@ constexpr int NTHR = 256;
 // MFMAs -- 1: conv_params.h xform 1, y = relu(xa z + xb) (the window's own rows of the
 // transformed operand go to xout); 3: head-on-load, the halo image of dY (32 channels)
 // is formed from the head's per-pixel probability, target and ReLU bits (p.hg,
-// head_grad.h) instead of being read from memory.
+// head_grad.h) instead of being read from memory; 4: space-to-depth source (p.s2d: the
+// DMA gathers the fine pixels of each coarse slot, structurally zero taps skipped).
 template <int W, int BN, int BM, bool CONCAT, int EPI, int GEO, int XF = 0>
 __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   static_assert(BN == 32 || BN == 64, "row-window tile is 32 or 64 output channels wide");
-  static_assert(XF == 0 || ((XF == 1 || XF == 3) && GEO == GEO_2D && !CONCAT),
+  static_assert(XF == 0 || ((XF == 1 || XF == 3 || XF == 4) && GEO == GEO_2D && !CONCAT),
                 "operand transform: 2D single-source windows");
   constexpr int R = BM / W, HR = R + 2;
   // halo row pitch in 64-byte pixel slots: W + 2 columns rounded up to a multiple of 4
@@ -171,9 +172,12 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
   // one 32-channel chunk: per horizontal tap, the three vertical taps' weights are
   // held in registers and every halo-row fragment feeds up to three output rows
-  auto chunk_mfmas = [&]() {
+  // tmask: taps (bit 3 dh + dw) of this chunk that are not structurally zero (XF 4);
+  // a compile-time 0x1ff everywhere else, so the tests fold away
+  auto chunk_mfmas = [&](const uint32_t tmask) {
 #pragma unroll
     for (int dw = 0; dw < 3; ++dw) {
+      if (!((tmask >> dw) & 0x49u)) continue;     // no valid tap in this column
       h16x8 wf[3][TN];
 #pragma unroll
       for (int dh = 0; dh < 3; ++dh)
@@ -188,6 +192,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
           for (int dh = 0; dh < 3; ++dh) {
             const int ri = hr - dh;
             if (ri < 0 || ri >= RW) continue;
+            if (!((tmask >> (3 * dh + dw)) & 1u)) continue;
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[ri * TC + ci][j] = mfma16(wf[dh][j], xf, acc[ri * TC + ci][j]);
           }
@@ -244,7 +249,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
         }
       }
       __syncthreads();
-      chunk_mfmas();
+      chunk_mfmas(0x1ffu);
   };
   if constexpr (GEO == GEO_3D) {
     // depth taps whose input slice is padding contribute nothing: skip them
@@ -280,8 +285,12 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
     const size_t xsample = XF == 1 ? (size_t)(g0 / H) * p.xcs : 0;   // the window's sample (GroupNorm rows)
     for (int kc = 0; kc < nchunks; ++kc) {
       const bool from1 = !CONCAT || (kc << 5) < p.C1;
-      const int C = from1 ? p.C1 : p.C2;
-      const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
+      const int C = XF == 4 ? p.s2d : (from1 ? p.C1 : p.C2);
+      // XF 4: chunk kc = phase group (sa, sb) of the space-to-depth image, fine channels
+      // cb .. cb + 31; its valid taps dh in {1 - sa, 2 - sa}, dw in {1 - sb, 2 - sb}
+      const int sgrp = XF == 4 ? kc / (p.s2d >> 5) : 0, sa = sgrp >> 1, sb = sgrp & 1;
+      const int cb = XF == 4 ? (kc << 5) - sgrp * p.s2d : (from1 ? (kc << 5) : (kc << 5) - p.C1);
+      const uint32_t s2d_taps = 0x1bu << (3 * (1 - sa) + (1 - sb));   // the 2 x 2 tap block
       if (kc) __syncthreads();
       {
         const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
@@ -296,7 +305,9 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
             const bool row_in = hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in);
             const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
             const int lch = (lane & 3) ^ ((hc >> 1) & 3);
-            const int off = ok ? ((gr * W + col) * C + cb + lch * 8) * 2 : OOB;
+            // XF 4: the coarse slot's fine pixel (2 gr + sa, 2 col + sb) of the 2W-wide rows
+            const int pix = XF == 4 ? (2 * gr + sa) * (2 * W) + 2 * col + sb : gr * W + col;
+            const int off = ok ? (pix * C + cb + lch * 8) * 2 : OOB;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
                                                      16, off, 0, 0, 0);
           }
@@ -382,7 +393,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
         }
         __syncthreads();
       }
-      chunk_mfmas();
+      chunk_mfmas(XF == 4 ? s2d_taps : 0x1ffu);
     }
   }
   __syncthreads();
@@ -464,6 +475,26 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
       HG_CASE(64)
       HG_CASE(128)
 #undef HG_CASE
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  if (p.s2d) {                          // space-to-depth dgrad source (conv_fwd_prepare checks the shape)
+    if (epi != EPI_DGRAD || geo != GEO_2D) return hipErrorInvalidValue;
+    switch (W) {
+#define S2D_CASE(WW)                                                                                      \
+  case WW:                                                                                                \
+    if constexpr (win_tile_built<BN, BM>(WW))                                                             \
+      hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_2D, 4>), dim3(grid), dim3(NTHR), 0, s, p); \
+    else                                                                                                  \
+      return hipErrorInvalidValue;                                                                        \
+    break;
+      S2D_CASE(16)
+      S2D_CASE(32)
+      S2D_CASE(64)
+      S2D_CASE(128)
+#undef S2D_CASE
       default:
         return hipErrorInvalidValue;
     }

@@ -99,6 +99,7 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.drop_rate = get<float>(d, "drop_rate", 0.f);
   p.seed = get<uint32_t>(d, "seed", 0u);
   p.salt = get<uint32_t>(d, "salt", 0u);
+  p.drop_idx0 = get<unsigned long long>(d, "drop_idx0", 0ull);
   p.rev = get<int>(d, "rev", 0);
   p.dst1 = const_cast<void*>(getp(d, "dst1"));
   p.dst2 = const_cast<void*>(getp(d, "dst2"));
@@ -127,6 +128,7 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.xb = (const float*)getp(d, "xb");
   p.xc = (const float*)getp(d, "xc");
   p.xz = getp(d, "xz");
+  p.s2d = get<int>(d, "s2d", 0);
   p.xout = const_cast<void*>(getp(d, "xout"));
   p.tile = get<int>(d, "tile", 0);
   p.head_w = (const float*)getp(d, "head_w");
@@ -214,6 +216,8 @@ WgradParams wgrad_params(const py::dict& d) {
   X(gn_finalize_launch) \
   X(norm_apply_launch) \
   X(norm_bwd_apply_launch) \
+  X(tconv_compose_launch) \
+  X(tconv_chain_launch) \
   X(adam_pack_launch)
 
 struct KernelApi {
@@ -333,6 +337,25 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     if (!stage && !(identity && sp <= 16))
       throw std::invalid_argument("wgrad_reduce: stage buffer required for >16 splits or row remap");
     return [=](hipStream_t s) { return A->wgrad_reduce_launch(slab, sp, taps, mt, mo, nc, rg, rk, sc, out, stage, s); };
+  }
+  if (kind == "tconv_compose") {
+    // ptrs: Wt master [4][C][K], Wa master [3][3][Ca][O], out [K][rowstride]   ints: C, K, O, Ca, rowstride
+    need(3, 5, 0);
+    const float *wt = (const float*)vp(0), *wa = (const float*)vp(1);
+    void* out = vp(2);
+    int C = I[0], K = I[1], O = I[2], Ca = I[3], rs = I[4];
+    check_msg(tconv_fused_check(C, K, O, Ca));
+    if (rs < 36 * O) throw std::invalid_argument("tconv_compose: rowstride < 36 O");
+    return [=](hipStream_t s) { return A->tconv_compose_launch(wt, wa, C, K, O, Ca, rs, out, s); };
+  }
+  if (kind == "tconv_chain") {
+    // ptrs: H [16][O][K], Bs [16][O], Wa master, dWt [4][C][K], dbt [C]   ints: C, K, O, Ca
+    need(5, 4, 0);
+    const float *hs = (const float*)vp(0), *bs = (const float*)vp(1), *wa = (const float*)vp(2);
+    float *dwt = (float*)vp(3), *dbt = (float*)vp(4);
+    int C = I[0], K = I[1], O = I[2], Ca = I[3];
+    check_msg(tconv_fused_check(C, K, O, Ca));
+    return [=](hipStream_t s) { return A->tconv_chain_launch(hs, bs, wa, C, K, O, Ca, dwt, dbt, s); };
   }
   if (kind == "multi_reduce") {
     // ptrs: job table (device, ReduceJob[njobs])   ints: njobs, total1, total2
@@ -720,6 +743,14 @@ PYBIND11_MODULE(_C, m) {
           p.AW = p.AH = 2 * QW;
           p.stride = 2;
           p.pad = 0;
+          p.bias_mode = 2;
+        } else if (QW > 0 && KT == 16) {  // composite tconv slab: 4x4 taps, stride 2, pad 1
+          p.KH = p.KW = 4;
+          p.QD = p.AD = 1;
+          p.QW = p.QH = QW;
+          p.AW = p.AH = 2 * QW;
+          p.stride = 2;
+          p.pad = 1;
           p.bias_mode = 2;
         }
         WgradCfg c = wgrad_pick(p);

@@ -301,6 +301,7 @@ class NativeUNet:
                 if l.kind == "conv" and (l.name != self.head_in or self.head_onload):
                     self.relu_bits[l.name] = torch.zeros(self.npix(l.level) * l.cout // 8, dtype=torch.uint8,
                                                          device=self.device)
+        self._plan_tconv_fused()
         P = self.npix(1)
         self.prob = torch.zeros(P, dtype=torch.float32, device=self.device)
         nb = self.C.head_blocks(P)
@@ -310,8 +311,8 @@ class NativeUNet:
         self.sums = torch.zeros(4, dtype=torch.float32, device=self.device)
         # gradient buffers: d:<tensor>, dskip:<tensor>, dfull:<tensor> (upsample fold)
         for name, (lvl, ch, _, _) in list(self.tinfo.items()):
-            if name == "x":
-                continue
+            if name == "x" or name in self.tconv_fused:
+                continue            # (a fused transposed conv's output gradient is never formed)
             self.bufs["d:" + name] = torch.empty_like(self.bufs[name])
         for l in spec.layers:
             if l.kind == "conv" and l.skip_from is not None:
@@ -328,6 +329,50 @@ class NativeUNet:
         self.slab = None
         self.bias_slab = None
         self._alloc_norm()
+
+    def _plan_tconv_fused(self):
+        """Transposed convs whose backward runs composite (tconv_fused.hip): the data
+        gradient of the tconv input is one coarse row-window conv over the space-to-depth
+        image of the consumer conv's dz with weights composed from both layers (conv_win.h
+        XF 4), the tconv weight / bias gradients come from 4x4-tap stride-2 slab sums
+        through the chain rule -- the fine tconv output gradient (up to 1 GiB at b1024)
+        is never written or re-read.  2D norm-free model; the consumer is the decoder conv
+        whose skip-half data gradient rides on the pool backward.  UNET_TCONV_FUSED = the
+        deepest fine level fused (0 off)."""
+        self.tconv_fused: Dict[str, dict] = {}
+        self._tf_consumer: Dict[str, str] = {}
+        top = int(os.environ.get("UNET_TCONV_FUSED", "2"))
+        if self.dims != 2 or self.spec.norm != "none" or top <= 0:
+            return
+        for l in self.spec.layers:
+            if l.kind != "tconv" or l.level > top:
+                continue
+            cons = [x for x in self.spec.layers if x.kind == "conv" and self.inputs.get(x.name, ("",))[0] == l.name]
+            if len(cons) != 1:
+                continue
+            c = cons[0]
+            src1, up1, skip = self.inputs[c.name]
+            has_pool = any(x.kind == "pool" and self.inputs[x.name][0] == skip for x in self.spec.layers)
+            if up1 != 1 or skip is None or not has_pool or c.cout % 32 or l.cin % 32 or l.cout % 8:
+                continue
+            src = self.inputs[l.name][0]
+            lo = self.sdims(l.level + 1)
+            O, K = c.cout, l.cin
+            rs = _r64(36 * O)
+            probe = self._conv_common(l.level + 1, 3, 1, 1)
+            probe.update(C1=4 * O, s2d=O, src1=1, wgt=1, Cout=K, relu=0, dst1=1, D1=K, mask1=1,
+                         mask_bits=1 if src in self.relu_bits else 0)
+            try:
+                if self.C.conv_fwd_grid(probe) <= 0:
+                    continue
+            except ValueError:
+                continue
+            self.tconv_fused[l.name] = dict(consumer=c.name, src=src, C=l.cout, K=K, O=O, Ca=c.cin, rs=rs,
+                                            level=l.level,
+                                            wg=torch.zeros(K * rs, dtype=self.adt, device=self.device),
+                                            hs=torch.zeros(16 * O * K, dtype=torch.float32, device=self.device),
+                                            bs=torch.zeros(16 * O, dtype=torch.float32, device=self.device))
+            self._tf_consumer[c.name] = l.name
 
     # ------------------------------------------------------------------ normalisation
     NORM_EPS = 1e-3          # models/reference.py::_norm (Keras default epsilon)
@@ -688,8 +733,10 @@ class NativeUNet:
         """2: the training forward runs as two half-batch chunks on two HIP streams, the
         second chunk started once the first has finished its first FWD_OFFSET layers, so kernels of different levels (bandwidth-bound full-resolution ones,
         MFMA-bound coarse ones) share the GPU.  Norm-free 2D model with an even batch
-        (BatchNorm needs whole-batch statistics); UNET_FWD_STREAMS=1 keeps one stream."""
-        n = int(os.environ.get("UNET_FWD_STREAMS", "1"))
+        (BatchNorm needs whole-batch statistics); UNET_FWD_STREAMS=1 keeps one stream.
+        Default 2 since round 3: same-box interleaved A/B of the headline step +1.0 / +1.0 /
+        +0.6 % (44.2k -> 44.7k img/s, round 2 measured +0.9 % the same way)."""
+        n = int(os.environ.get("UNET_FWD_STREAMS", "2"))
         if n != 2 or not train or self.spec.norm != "none" or self.B % 2 or self.device.type != "cuda":
             return 1
         return 2
@@ -772,7 +819,7 @@ class NativeUNet:
                      Cout=l.cout, relu=0 if normed else 1,
                      dst1=_ptr(b["z:" + l.name]) if normed else P(l.name),
                      drop_rate=spec.dropout if (l.dropout and dropout and not normed) else 0.0,
-                     salt=(self._salt(l.name) + c * 0x9E3779B9) & 0xFFFFFFFF)
+                     salt=self._salt(l.name), drop_idx0=c * nb * (self.npix(l.level) // self.B) * l.cout)
             bits = self.relu_bits.get(l.name)
             if bits is not None and not normed:
                 d["relu_bits"] = _ptr(bits) + c * nb * (self.npix(l.level) // self.B) * l.cout // 8
@@ -922,6 +969,12 @@ class NativeUNet:
 
         self._deferred_skip = {}
         tail_parts = {}
+        for tname, tf in self.tconv_fused.items():
+            # composite data-gradient weights from this step's fp32 masters
+            emit_generic("tconv_compose",
+                         lambda tname=tname, tf=tf: [self.master_ptr(tname + "/kernel"),
+                                                     self.master_ptr(tf["consumer"] + "/kernel"), _ptr(tf["wg"])],
+                         [tf["C"], tf["K"], tf["O"], tf["Ca"], tf["rs"]], [], "compose:" + tname)
         for li in range(len(layers) - 1, -1, -1):
             l = layers[li]
             if l.kind == "mask" and self._norm_head_loss:
@@ -1016,11 +1069,27 @@ class NativeUNet:
                             if l.name == self.head_in and self.head_onload:
                                 d.update(self._head_grad_fields())
                         else:
+                            dsk = self._skip_route(l, skip, c1, c2, dy)
+                            tname = self._tf_consumer.get(l.name)
+                            if tname is not None:
+                                if dsk is None:
+                                    raise RuntimeError("fused transposed conv %s: skip route of %s failed"
+                                                       % (tname, l.name))
+                                tf = self.tconv_fused[tname]
+                                tsrc = tf["src"]
+                                tl = next(x for x in spec.layers if x.name == tname)
+                                d = self._conv_common(tl.level + 1, 3, 1, 1)
+                                m1, mb = self._relu_mask(tsrc)
+                                d.update(name="dgrad:" + l.name, C1=4 * l.cout, s2d=l.cout, src1=_ptr(dy),
+                                         wgt=_ptr(tf["wg"]), Cout=tf["K"], relu=0, dst1=_ptr(b["d:" + tsrc]),
+                                         D1=tf["K"], mask1=m1, mask_bits=mb)
+                                self._deferred_skip[dsk[0]] = dsk[1]
+                                self._rev_order(d, "g:" + l.name, "g:" + tsrc)
+                                return d
                             if up1 == 2:
                                 dst1 = b["dfull:" + src1]          # full-res grad of the upsample
                             else:
                                 dst1 = b["d:" + src1]              # tconv output: linear, no mask
-                            dsk = self._skip_route(l, skip, c1, c2, dy)
                             if dsk is not None:
                                 # the skip half runs later, fused with the pool backward
                                 d.update(Cout=c1, dst1=_ptr(dst1), D1=c1)
@@ -1079,6 +1148,18 @@ class NativeUNet:
                                                    _ptr(b["dskip:" + src]) if ("dskip:" + src) in b else 0,
                                                    _ptr(b["d:" + src]), _ptr(self.pool_codes[l.name])],
                              [self.B, dd, hh, ww, l.cout, int(self.dims == 3)], [], "bwd:" + l.name)
+            elif l.kind == "tconv" and l.name in self.tconv_fused:
+                tf = self.tconv_fused[l.name]
+                lo, hi = self.sdims(l.level + 1), self.sdims(l.level)
+                dz = b["d:" + tf["consumer"]]
+                kd = dict(N=self.B, QD=1, QH=lo[1], QW=lo[2], AD=1, AH=hi[1], AW=hi[2], KD=1, KH=4, KW=4,
+                          stride=2, pad=1, upA=1, a1=_ptr(dz), b=_ptr(b[tf["src"]]))
+                emit_wgrad(dict(lname=l.name, kd=kd, M1=tf["O"], M2=0, Nc=tf["K"], KT=16, QW=lo[2],
+                                Q=self.npix(l.level + 1), kernel=None, kernel_out=_ptr(tf["hs"]),
+                                bias=None, bias_out=_ptr(tf["bs"]), bias_mode=2, bias_width=16 * tf["O"],
+                                bias_per_tap=True, real_rows=None, bias_src=(dz, self.npix(l.level + 1)),
+                                chain=l.name))
+                done(l.name)
             elif l.kind == "tconv":
                 src = self.inputs[l.name][0]
                 du = b["d:" + l.name]
@@ -1172,11 +1253,14 @@ class NativeUNet:
             pending_layers.clear()
 
         slab0, bslab0, stage0 = _ptr(self.slab), _ptr(self.bias_slab), _ptr(self.red_stage)
+        chained = set()
         for op in ops:
             if callable(op):
                 op(plan)
             elif op[0] == "done":
-                if op[1] in wgrad_layers:
+                if op[1] in chained:
+                    pass                           # done after its chain rule
+                elif op[1] in wgrad_layers:
                     pending_layers.append(op[1])
                     if len(pending_layers) >= FLUSH_LAYERS:
                         flush()
@@ -1203,24 +1287,39 @@ class NativeUNet:
                 if part == 0:
                     continue                       # the reductions follow the last part
                 KT = w["KT"]
+                kout = w.get("kernel_out") or self.grad_ptr(w["kernel"])
+                bout = w.get("bias_out") or self.grad_ptr(w["bias"])
                 if smallc:
                     cpad, creal = w["real_rows"]
-                    pending_jobs.append(job(slab, self.grad_ptr(w["kernel"]), stage_k, splits, 1, Mtot, KT * creal,
-                                            w["Nc"], cpad, creal))
+                    pending_jobs.append(job(slab, kout, stage_k, splits, 1, Mtot, KT * creal, w["Nc"], cpad, creal))
                 else:
-                    pending_jobs.append(job(slab, self.grad_ptr(w["kernel"]), stage_k, splits, taps, Mtot, Mtot,
-                                            w["Nc"]))
+                    pending_jobs.append(job(slab, kout, stage_k, splits, taps, Mtot, Mtot, w["Nc"]))
                 bw = w["bias_width"]
                 if not fused_bias:
                     src, rows = w["bias_src"]
                     nb = self._colsum_blocks(rows, bw)
                     plan.add_generic("colsum", [_ptr(src), bslab], [rows, bw, nb], [], "bsum:" + w["lname"])
-                    pending_jobs.append(job(bslab, self.grad_ptr(w["bias"]), stage_b, nb, 1, 1, 1, bw))
+                    pending_jobs.append(job(bslab, bout, stage_b, nb, 1, 1, 1, bw))
                 elif w["bias_mode"] == 1:
-                    pending_jobs.append(job(bslab, self.grad_ptr(w["bias"]), stage_b, splits, 1, 1, 1, bw))
+                    pending_jobs.append(job(bslab, bout, stage_b, splits, 1, 1, 1, bw))
+                elif w.get("bias_per_tap"):
+                    # [splits][tg][Mtot] rows -> per-tap sums [tg][Mtot]
+                    pending_jobs.append(job(bslab, bout, stage_b, splits, 1, 1, 1, bw))
                 else:
                     # [splits*tg][Mtot] rows -> bias (Mtot == cout for tconv)
-                    pending_jobs.append(job(bslab, self.grad_ptr(w["bias"]), stage_b, splits * tg, 1, 1, 1, bw))
+                    pending_jobs.append(job(bslab, bout, stage_b, splits * tg, 1, 1, 1, bw))
+                if w.get("chain"):
+                    # the slab sums are reduced now; the chain rule writes the tconv gradients
+                    tname = w["chain"]
+                    tf = self.tconv_fused[tname]
+                    pending_layers.append(tname)
+                    flush()
+                    chained.add(tname)
+                    plan.add_generic("tconv_chain", [_ptr(tf["hs"]), _ptr(tf["bs"]),
+                                                     self.master_ptr(tf["consumer"] + "/kernel"),
+                                                     self.grad_ptr(tname + "/kernel"), self.grad_ptr(tname + "/bias")],
+                                     [tf["C"], tf["K"], tf["O"], tf["Ca"]], [], "chain:" + tname)
+                    self._layer_done_at[tname] = plan.size()
         flush()
 
     # ------------------------------------------------------------------ buckets
@@ -1333,7 +1432,7 @@ class NativeUNet:
             return
         self.plan.run(0, self.fwd_end, native.stream_handle(stream))
 
-    _SIDE_KINDS = ("wgrad:", "bsum:", "reduce:")
+    _SIDE_KINDS = ("wgrad:", "bsum:", "reduce:", "chain:")
 
     def _side_groups(self, begin, end):
         """[begin, end) as maximal runs of (on_side, i, j): weight-gradient launches
