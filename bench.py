@@ -245,6 +245,7 @@ def main():
                        "img_size": a.img_size, "in_channels": a.in_channels,
                        "parallelism": "dp%d" % N, "backend": backend.name},
             "train_dice_last_batch": round(dice, 5),
+            "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2) if torch.cuda.is_available() else None,
             "comm": comm,
         }
         print(json.dumps(rec), flush=True)

@@ -879,3 +879,38 @@ def test_head_onload_matches_materialised_head_gradient(cuda_dev, N, H, Cy, bce,
     assert torch.equal(dx0, dx1)
     assert torch.equal(g0, g1) and torch.equal(b0, b1)
     assert torch.equal(ow0, ow1) and torch.equal(ob0, ob1)
+
+
+def test_row_window_kernels_beyond_2gib(cuda_dev):
+    """Row-window forward / data gradient / weight gradient on a 32-channel tensor of
+    2.2 GB (image-relative 32-bit DMA offsets): equal to the same launches on the two
+    batch halves (each below 2 GiB) -- bit for bit for the convs, to fp32 summation
+    order for the weight gradient."""
+    torch.manual_seed(7)
+    N, H, Cc = 2112, 128, 32
+    h = N // 2
+    x = torch.randn(N, H, H, Cc, device=cuda_dev, dtype=torch.bfloat16)
+    assert x.numel() * 2 > 2 ** 31
+    w = (torch.randn(3, 3, Cc, Cc, device=cuda_dev) * 0.1).bfloat16()
+    b = torch.randn(Cc, device=cuda_dev)
+    wp = pack_fwd(w)
+    out = torch.empty_like(x)
+    base = dict(OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cc, wgt=ptr(wp), bias=ptr(b), Cout=Cc, relu=1)
+    C().conv_fwd(dict(base, N=N, src1=ptr(x), dst1=ptr(out)), stream())
+    assert C().conv_fwd_grid(dict(base, N=N, src1=ptr(x), dst1=ptr(out))) > 0
+    ref = torch.empty_like(x)
+    for k in range(2):
+        C().conv_fwd(dict(base, N=h, src1=ptr(x[k * h:]), dst1=ptr(ref[k * h:])), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    del out, ref
+    # weight gradient: a = x, b = dY (same shape)
+    dy = torch.randn(N, H, H, Cc, device=cuda_dev, dtype=torch.bfloat16)
+    kd = dict(QD=1, QH=H, QW=H, AD=1, AH=H, AW=H, KD=1, KH=3, KW=3, stride=1, pad=1, M1=Cc, M2=0, Nc=Cc,
+              bias_mode=1, win=0)
+    full, fb = _wgrad(dict(kd, N=N, a1=ptr(x), b=ptr(dy)), 64, 9, Cc, Cc, Cc, 9 * Cc * Cc, bias_w=(64, Cc))
+    parts = [_wgrad(dict(kd, N=h, a1=ptr(x[k * h:]), b=ptr(dy[k * h:])), 32, 9, Cc, Cc, Cc, 9 * Cc * Cc,
+                    bias_w=(32, Cc)) for k in range(2)]
+    torch.cuda.synchronize()
+    assert rel_err(full, parts[0][0] + parts[1][0]) < 1e-4
+    assert rel_err(fb, parts[0][1] + parts[1][1]) < 1e-4

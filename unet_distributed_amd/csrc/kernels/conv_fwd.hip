@@ -70,6 +70,11 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
   const int cc = tid & 7;                            // this thread's 16-byte chunk column
   const int padd = p.KD > 1 ? p.pad : 0;
 
+  // image-relative 32-bit offsets: the tile's rows start in image n_base (a tile spans at
+  // most BM / (OD OH OW) + 2 images, conv_fwd_prepare bounds their bytes), so a tensor may
+  // exceed 2 GiB
+  const int n_base = m0 / (p.OD * p.OH * p.OW);
+  const size_t base_px = (size_t)n_base * p.ID * p.IH * p.IW;
   // ---- per-row precomputation (hoisted out of the K loop)
   int a_pix[AR];      // full-res pixel index of the window origin (may be negative at the halo)
   int a_pb1[AR], a_pb2[AR];   // the same as byte offsets into src1 / src2
@@ -81,7 +86,7 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
     const bool ok = q < M;
     const PixCoord c = decompose(ok ? q : 0, p.OD, p.OH, p.OW);
     const int bd = c.d * p.stride - padd, bh = c.h * p.stride - p.pad, bw = c.w * p.stride - p.pad;
-    a_pix[i] = ((c.n * p.ID + bd) * p.IH + bh) * p.IW + bw;
+    a_pix[i] = (((c.n - n_base) * p.ID + bd) * p.IH + bh) * p.IW + bw;
     a_pb1[i] = a_pix[i] * p.C1 * 2;
     a_pb2[i] = a_pix[i] * p.C2 * 2;
     // in-bounds tap mask, taps ordered t = (kd*KH + kh)*KW + kw; kernel extents <= 3
@@ -103,9 +108,10 @@ __global__ void __launch_bounds__(NTHR) conv_fwd_kernel(const ConvFwdParams p) {
   // raw buffer resources: an offset past num_records returns zeros in hardware, so
   // halo taps, K padding and the M tail need no branches (cdna_hip_programming.md T8)
   constexpr int OOB = 0x7fffffff;
-  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)p.src1, (short)0, OOB, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs2 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.src2 ? p.src2 : p.src1), (short)0, OOB, 0x00020000);
+  const char* s1b = (const char*)p.src1 + base_px * 2 * p.C1;
+  const char* s2b = p.src2 ? (const char*)p.src2 + base_px * 2 * p.C2 : s1b;
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)s1b, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc((void*)s2b, (short)0, OOB, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
   int wofs[BR];
 #pragma unroll
@@ -796,9 +802,20 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   }
   if ((long long)p.N * p.ID * p.IH * p.IW >= (1LL << 31) || (long long)p.N * p.OD * p.OH * p.OW >= (1LL << 31))
     return "conv_fwd: too many pixels";
-  // buffer loads use 32-bit byte offsets: every source tensor must stay below 2 GiB
-  if ((long long)p.N * p.ID * p.IH * p.IW * (long long)(p.C1 > p.C2 ? p.C1 : p.C2) * 2 >= (1LL << 31) - 64)
-    return "conv_fwd: input tensor exceeds 2 GiB (split the batch)";
+  // buffer loads use 32-bit byte offsets: the row-window kernels count them from the
+  // window's image, the tiled kernels from the first image of the tile (a tile spans at
+  // most BM / image + 2 images), the transposed-conv / first-layer windows from the
+  // tensor start
+  {
+    const int t = conv_fwd_pick(p);
+    const long long img = (long long)p.ID * p.IH * p.IW * (long long)(p.C1 > p.C2 ? p.C1 : p.C2) * 2;
+    const long long opx = (long long)p.OD * p.OH * p.OW;
+    const long long lim = (1LL << 31) - 64;
+    long long span = img * p.N;                       // bytes a launch addresses from one base
+    if (t == 6 || t == 12) span = img;
+    else if (t >= 1 && t <= 5) span = img * (256 / opx + 2 < p.N ? 256 / opx + 2 : p.N);
+    if (span >= lim) return "conv_fwd: input exceeds the 2 GiB reach of one buffer base (split the batch)";
+  }
   p.Kpad = ((KT * Cin + 63) / 64) * 64;
   for (int t = 0; t < 27; ++t) {
     p.tap_d[t] = p.tap_h[t] = p.tap_w[t] = 0;

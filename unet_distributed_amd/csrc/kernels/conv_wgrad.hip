@@ -538,9 +538,10 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   const bool from1 = !CONCAT || ci0 < p.M1;
   const int CA = from1 ? p.M1 : p.M2, ca0 = from1 ? ci0 : ci0 - p.M1;
   constexpr int OOB = 0x7fffffff;
-  const __amdgpu_buffer_rsrc_t rsa =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(from1 ? p.a1 : p.a2), (short)0, OOB, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, OOB, 0x00020000);
+  // window-relative buffer bases (rebuilt per window, scalar): 32-bit DMA offsets count
+  // from the window's first halo row, so the tensors may exceed 2 GiB
+  const char* abase = (const char*)(from1 ? p.a1 : p.a2);
+  const char* bbase = (const char*)p.b;
   const int w_begin = (int)((long long)split * nwin / p.splits);
   const int w_end = (int)((long long)(split + 1) * nwin / p.splits);
   // bias: once per output-channel block, by the centre depth tap (it sees every window)
@@ -607,6 +608,11 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
     if (GEO == WGEO_3D && (unsigned)((g0 / H) % D + kd - 1) >= (unsigned)D) continue;
     const bool zero_halo = UNITS_PATH || pair_ok;
     const bool top_in = !zero_halo || (g0 % H) != 0, bot_in = !zero_halo || ((g0 + R) % H) != 0;
+    const int rb = max(g0 - 1 + gsh, 0);             // first halo row held by rsa
+    const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(abase + (size_t)rb * Wf * CA * 2), (short)0, OOB, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(bbase + (size_t)g0 * Wf * p.Nc * 2), (short)0, OOB, 0x00020000);
     __syncthreads();   // the previous window's fragment reads are done
 #pragma unroll
     for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
@@ -618,7 +624,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
         const bool row_in = (hr > 0 || top_in) && (hr < R + 1 || bot_in);
         const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)Wf &&
                         (GEO != WGEO_SEG || 16 * j + lslot <= W + 1);
-        const int off = ok ? (gr * Wf + col0 + 16 * j) * CA * 2 + ((ROWSWZ && (hr & 1)) ? xl_odd : xl) : OOB;
+        const int off = ok ? ((gr - rb) * Wf + col0 + 16 * j) * CA * 2 + ((ROWSWZ && (hr & 1)) ? xl_odd : xl) : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
                                                  off, 0, 0, 0);
       }
@@ -640,7 +646,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
         // window slot sb -> row g0 + sb / W, column col0 + sb % W (W = 8: one segment,
         // the 16-slot run covers two consecutive rows contiguous in memory)
         const int pix = GEO == WGEO_SEG ? (g0 + sb / W) * Wf + col0 + sb % W : g0 * W + sb;
-        const int off = (pix + lslot < Mq) ? (pix * p.Nc + 32 * o) * 2 + yl : OOB;
+        const int off = (pix + lslot < Mq) ? ((pix - g0 * Wf) * p.Nc + 32 * o) * 2 + yl : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (__attribute__((address_space(3))) void*)(Ys + k * 1024), 16,
                                                  off, 0, 0, 0);
       }
@@ -895,7 +901,6 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
   const int co0 = co_blk * 32;
   constexpr int OOB = 0x7fffffff;
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.a1, (short)0, OOB, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, OOB, 0x00020000);
   const int w_begin = (int)((long long)split * nwin / p.splits);
   const int w_end = (int)((long long)(split + 1) * nwin / p.splits);
   const bool do_bias = p.bias_mode == 1;
@@ -926,6 +931,9 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
   float xa[8], xb[8], xc[8];
   for (int win = w_begin; win < w_end; ++win) {
     const int g0 = win * R;
+    // dY window base (scalar): the 32-bit DMA offsets stay window-relative (> 2 GiB dY)
+    const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)p.b + (size_t)g0 * W * p.Nc * 2), (short)0, OOB, 0x00020000);
     __syncthreads();
     u32x4 xzv[(YI + 3) / 4];
     if constexpr (XF) {
@@ -964,7 +972,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
       const int k = wave + 4 * qq;
       if (k < YI) {
         const int pix = g0 * W + 16 * k;
-        const int off = (pix + lslot < Mq) ? pix * p.Nc * 2 + yl : OOB;
+        const int off = (pix + lslot < Mq) ? 16 * k * p.Nc * 2 + yl : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (__attribute__((address_space(3))) void*)(Ys + k * 1024), 16,
                                                  off, 0, 0, 0);
       }
@@ -1123,8 +1131,6 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
   const int co_blk = tile / cit, ci_blk = tile - co_blk * cit;
   const int co0 = co_blk * 32, ci0 = ci_blk * 32 * QN;
   constexpr int OOB = 0x7fffffff;
-  const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc((void*)p.a1, (short)0, OOB, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, OOB, 0x00020000);
   const int w_begin = (int)((long long)split * nwin / p.splits);
   const int w_end = (int)((long long)(split + 1) * nwin / p.splits);
   const bool do_bias = p.bias_mode == 2 && ci_blk == 0 && qn == 0;
@@ -1154,6 +1160,11 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
 
   for (int win = w_begin; win < w_end; ++win) {
     const int g0 = win * R;
+    // window-relative bases (scalar): 32-bit DMA offsets, tensors beyond 2 GiB
+    const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)p.b + (size_t)g0 * W * p.Nc * 2), (short)0, OOB, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)p.a1 + (size_t)2 * g0 * FW * Mtot * 2), (short)0, OOB, 0x00020000);
     __syncthreads();
 #pragma unroll
     for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
@@ -1161,7 +1172,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
       if (k < XI) {
         const int o = k / (BMc / 16), sb = (k - o * (BMc / 16)) * 16;   // x image o (channel block)
         const int pix = g0 * W + sb + lslot;
-        const int off = pix < Mq ? (pix * p.Nc + ci0 + 32 * o + lchunk * 8) * 2 : OOB;
+        const int off = pix < Mq ? ((sb + lslot) * p.Nc + ci0 + 32 * o + lchunk * 8) * 2 : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsx, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
                                                  off, 0, 0, 0);
       }
@@ -1174,7 +1185,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
         const int frr = sl / FW, s = sl - frr * FW;
         const int col = s < W ? 2 * s : 2 * (s - W) + 1;
         const int gf = 2 * g0 + frr;
-        const int off = gf < fine_rows_total ? ((gf * FW + col) * Mtot + co0 + lchunk * 8) * 2 : OOB;
+        const int off = gf < fine_rows_total ? ((frr * FW + col) * Mtot + co0 + lchunk * 8) * 2 : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsy, (__attribute__((address_space(3))) void*)(Ys + k * 1024), 16,
                                                  off, 0, 0, 0);
       }
@@ -1283,8 +1294,6 @@ __global__ void __launch_bounds__(NTHR) wgrad_s2d_win_kernel(const WgradParams p
   const int o_blk = tile / kt, k_blk = tile - o_blk * kt;
   const int o0 = o_blk * 32, k0 = k_blk * 32 * QN;
   constexpr int OOB = 0x7fffffff;
-  const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc((void*)p.a1, (short)0, OOB, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, (short)0, OOB, 0x00020000);
   const int w_begin = (int)((long long)split * nwin / p.splits);
   const int w_end = (int)((long long)(split + 1) * nwin / p.splits);
   const bool do_bias = p.bias_mode == 2 && k_blk == 0;
@@ -1322,6 +1331,11 @@ __global__ void __launch_bounds__(NTHR) wgrad_s2d_win_kernel(const WgradParams p
   for (int win = w_begin; win < w_end; ++win) {
     const int g0 = win * R;
     const int fimg0 = 2 * (g0 - g0 % H);             // first fine row of the window's image
+    // image-relative bases (scalar): 32-bit DMA offsets, tensors beyond 2 GiB
+    const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)p.b + (size_t)g0 * W * K * 2), (short)0, OOB, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)p.a1 + (size_t)fimg0 * (2 * W) * O * 2), (short)0, OOB, 0x00020000);
     __syncthreads();
 #pragma unroll
     for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
@@ -1329,7 +1343,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_s2d_win_kernel(const WgradParams p
       if (k < XI) {
         const int o = k / (BMc / 16), sb = (k - o * (BMc / 16)) * 16;   // x image o (channel block)
         const int pix = g0 * W + sb + lslot;
-        const int off = pix < Mq ? (pix * K + k0 + 32 * o + lchunk * 8) * 2 : OOB;
+        const int off = pix < Mq ? ((sb + lslot) * K + k0 + 32 * o + lchunk * 8) * 2 : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsx, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
                                                  off, 0, 0, 0);
       }
@@ -1345,7 +1359,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_s2d_win_kernel(const WgradParams p
         const int cc = odd ? ps - (W + 2) : ps;          // column index in its parity class
         const bool ok = fr < FR && gf >= fimg0 && gf < fimg0 + 2 * H && (unsigned)cc < (unsigned)W;
         const int col = odd ? 2 * cc + 1 : 2 * cc;
-        const int off = ok ? ((gf * (2 * W) + col) * O + o0 + lchunk * 8) * 2 : OOB;
+        const int off = ok ? (((gf - fimg0) * (2 * W) + col) * O + o0 + lchunk * 8) * 2 : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsy, (__attribute__((address_space(3))) void*)(Ys + k * 1024), 16,
                                                  off, 0, 0, 0);
       }
@@ -1513,6 +1527,17 @@ const char* wgrad_check(const WgradParams& p) {
   if (p.hg.prob && (!p.hg.t || !p.hg.sums || !p.hg.w || !p.hg.bits || !wgrad_win_eligible(p) || p.Nc != 32 ||
                     p.M2 != 0 || p.KD != 1 || p.QD != 1 || p.QW > 128 || p.xform))
     return "wgrad: head-on-load B needs a 2D single-source row-window wgrad with 32 output channels";
+  // 32-bit buffer offsets: the window kernels count them from each window's rows (one
+  // image must stay below 2 GiB), the tiled kernel from the tensor starts
+  {
+    const bool win = wgrad_win_eligible(p) || wgrad_win_first_eligible(p) || wgrad_tconv_win_eligible(p) ||
+                     wgrad_s2d_win_eligible(p);
+    const long long ia = (long long)p.AD * p.AH * p.AW * (p.M1 > p.M2 ? p.M1 : p.M2) * 2;
+    const long long ib = (long long)p.QD * p.QH * p.QW * p.Nc * 2;
+    const long long lim = (1LL << 31) - 64;
+    if (win ? (ia >= lim || ib >= lim) : (ia * p.N >= lim || ib * p.N >= lim))
+      return win ? "wgrad: one image of an operand exceeds 2 GiB" : "wgrad: operand tensor exceeds 2 GiB (split the batch)";
+  }
   if (p.splits < 1) return "wgrad: splits must be >= 1";
   if (p.split_lo < 0 || p.split_n < 0 || p.split_lo + launch_splits(p) > p.splits)
     return "wgrad: split range [split_lo, split_lo + split_n) outside [0, splits)";

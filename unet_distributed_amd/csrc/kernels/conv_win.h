@@ -133,9 +133,15 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   const int Cin = p.C1 + p.C2;
   const int nchunks = Cin >> 5;
   constexpr int OOB = 0x7fffffff;
-  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)p.src1, (short)0, OOB, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs2 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(p.src2 ? p.src2 : p.src1), (short)0, OOB, 0x00020000);
+  // image-relative buffer bases: a window's rows (halo included) never leave its image,
+  // so the 32-bit DMA offsets count from the image's first pixel and a whole tensor may
+  // exceed 2 GiB (conv_fwd_prepare bounds one image)
+  const int grow0 = (g0 / (D * H)) * (D * H);
+  const size_t img_px = (size_t)grow0 * Wf;
+  const char* s1b = (const char*)p.src1 + img_px * (XF == 4 ? 4 * p.s2d : p.C1) * 2;
+  const char* s2b = p.src2 ? (const char*)p.src2 + img_px * p.C2 * 2 : s1b;
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)s1b, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc((void*)s2b, (short)0, OOB, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
 
   // Wave w owns an RW-row x 16 TC-column strip of the window (StripTiles): an A
@@ -230,7 +236,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
             const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)Wf &&
                             (GEO != GEO_SEG || hc <= W + 1);
             const int lch = (lane & 3) ^ ((hc >> 1) & 3);
-            const int off = ok ? ((gr * Wf + col) * C + cb + lch * 8) * 2 : OOB;
+            const int off = ok ? (((gr - grow0) * Wf + col) * C + cb + lch * 8) * 2 : OOB;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
                                                      16, off, 0, 0, 0);
           }
@@ -306,7 +312,8 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
             const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
             const int lch = (lane & 3) ^ ((hc >> 1) & 3);
             // XF 4: the coarse slot's fine pixel (2 gr + sa, 2 col + sb) of the 2W-wide rows
-            const int pix = XF == 4 ? (2 * gr + sa) * (2 * W) + 2 * col + sb : gr * W + col;
+            const int lr = gr - grow0;                      // image-relative row
+            const int pix = XF == 4 ? (2 * lr + sa) * (2 * W) + 2 * col + sb : lr * W + col;
             const int off = ok ? (pix * C + cb + lch * 8) * 2 : OOB;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024),
                                                      16, off, 0, 0, 0);
