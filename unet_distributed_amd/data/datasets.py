@@ -59,9 +59,9 @@ def synthetic_brats(n: int, img: int = 128, channels: int = 4, dims: int = 2, se
 
     ``difficulty="hard"``: a segmentation task that does not saturate (its Dice
     plateau is in the reference's MODE-1 range, 0.78-0.80 on BraTS,
-    `settings_dist.py:30`): 1-4 small lesions (2-6 px radius), each visible in only
-    one or two modalities at low contrast (0.35-0.9 sigma of the noise), sigma 0.5
-    noise, a smooth per-sample intensity bias field, and look-alike blobs that are
+    `settings_dist.py:30`): 1-4 small lesions (3-7 px radius), each visible in only
+    one or two modalities at low contrast (0.27-0.6 before noise, 0.7-1.5 sigma of the
+    noise), sigma 0.4 noise, a smooth per-sample intensity bias field, and look-alike blobs that are
     bright in a single modality but are NOT lesions -- a lesion bright in one modality
     and a distractor differ only in shape / size statistics, so the errors at
     boundaries and on single-modality lesions remain."""
@@ -114,15 +114,15 @@ def _synthetic_hard(n, img, channels, dims, seed, dtype):
         x = (brain * bias)[..., None] * base
         m = np.zeros(sp, dtype=bool)
         for _ in range(rng.integers(1, 5)):
-            b = blob(rng.uniform(2.0, 6.0)) & (brain > 0)
+            b = blob(rng.uniform(3.0, 7.0)) & (brain > 0)
             chans = rng.choice(channels, size=rng.integers(1, min(2, channels) + 1), replace=False)
             for ch in chans:
-                x[..., ch] += b * rng.uniform(0.35, 0.9) * 0.5
+                x[..., ch] += b * rng.uniform(0.45, 1.0) * 0.6
             m |= b
         for _ in range(rng.integers(0, 3)):                   # single-modality look-alikes
             b = blob(rng.uniform(1.5, 4.0)) & (brain > 0) & ~m
             x[..., rng.integers(channels)] += b * rng.uniform(0.35, 0.9) * 0.5
-        x = x + 0.5 * rng.standard_normal(x.shape).astype(np.float32)
+        x = x + 0.4 * rng.standard_normal(x.shape).astype(np.float32)
         x = (x - x.mean()) / (x.std() + 1e-6)
         imgs[i] = x
         msks[i, ..., 0] = m
