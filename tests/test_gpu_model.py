@@ -377,6 +377,7 @@ def test_tconv_fused_step_matches_materialised(cuda_dev, monkeypatch, kw):
     same loss sums and probabilities, every parameter gradient within bf16 rounding of
     the other path (the composed weights round once instead of twice)."""
     outs = []
+    monkeypatch.setenv("UNET_TCONV_FWD", "0")             # (the composite forward: next test)
     for v in ("0", "2"):
         monkeypatch.setenv("UNET_TCONV_FUSED", v)
         spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
@@ -391,3 +392,42 @@ def test_tconv_fused_step_matches_materialised(cuda_dev, monkeypatch, kw):
         a, b = g1[k].float(), g0[k].float()
         err = ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
         assert err < 3e-2 and _cos(a, b) > 0.999, (k, err, _cos(a, b))
+
+
+@pytest.mark.parametrize("kw", [
+    dict(batch_size=4, img_size=64, in_channels=4),
+    dict(batch_size=4, img_size=128, in_channels=4, loss="dice_bce"),
+])
+def test_tconv_consumer_modes_step(cuda_dev, monkeypatch, kw):
+    """UNET_TCONV_FWD 0 (tconv + fine conv, full wgrad), 1 (default: the consumer's u-row
+    weight gradient from the slab sums, skip-only wgrad) and 2 (composite forward: conv{8,9}a
+    on the coarse grid, u never formed).  Mode 1 leaves the forward bit-identical; modes 1 / 2
+    round differently from mode 0 (u is never rounded to 16 bits on their u-row gradient /
+    forward paths), so each is held against the fp32 ATen step and must be as close to it as
+    mode 0 (per-gradient cosine distance at most 2x + 3e-4 of mode 0's)."""
+    outs = []
+    for v in ("0", "1", "2"):
+        monkeypatch.setenv("UNET_TCONV_FWD", v)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
+        e = nb.engine
+        fused = sorted(t for t, tf in e.tconv_fused.items() if "s2f" in tf)
+        assert fused == ([] if v != "2" else ["transConv8", "transConv9"])
+        assert sorted(e._wa_chain_of.values()) == ([] if v == "0" else ["transConv8", "transConv9"])
+        assert all(t not in e.bufs for t in fused)
+        nb.fwd_bwd(x, y, seed=91)
+        if v == "0":
+            tb.fwd_bwd(x, y, seed=91)
+            ref = (tb.sums().cpu(), {k: ft.view(ft.grad, k).clone() for k, *_ in ft.entries})
+        torch.cuda.synchronize()
+        outs.append((nb.sums().cpu(), e.prob.clone(), {k: fn.view(fn.grad, k).clone() for k, *_ in fn.entries}))
+    (s0, p0, g0), (s1, p1, g1), (s2, p2, g2) = outs
+    st, gt = ref
+    assert torch.equal(s0, s1) and torch.equal(p0, p1)
+    assert ((s2 - s0).abs() / s0.abs().clamp_min(1.0)).max().item() < 5e-3, (s0, s2)
+    assert torch.allclose(s2[:3], st[:3], rtol=3e-2, atol=1.0), (s2, st)
+    assert (p2 - p0).abs().max().item() < 2e-2
+    for k in g0:
+        d0 = 1.0 - _cos(g0[k].float(), gt[k])
+        for g in (g1, g2):
+            d = 1.0 - _cos(g[k].float(), gt[k])
+            assert d <= 2.0 * d0 + 3e-4, (k, d0, d)

@@ -29,7 +29,20 @@ def test_plan_construction_dry_run(kw, img, dtype):
     e = NativeUNet(spec, flat, 2, img, "cpu", bucket_bounds=b, dry_run=True, dtype=dtype)
     assert e.arena.dtype == e.adt and e.target.dtype == e.adt
     names = e.plan.names()
-    assert names[0] == "fwd:conv1a" and names[e.fwd_end - 1] == "fwd:Mask"
+    # composite transposed-conv forwards: their weights are composed first, the tconv
+    # itself never launches and its output u is never allocated
+    s2f = [t for t, tf in e.tconv_fused.items() if "s2f" in tf]
+    assert names[:len(s2f)] == ["fwd:compose:" + t for t in s2f]
+    assert names[len(s2f)] == "fwd:conv1a" and names[e.fwd_end - 1] == "fwd:Mask"
+    for t in s2f:
+        assert "fwd:" + t not in names and t not in e.bufs
+        assert "fwd:" + e.tconv_fused[t]["consumer"] in names
+    if kw.get("dims", 2) == 2 and kw.get("norm", "none") == "none" and not kw.get("use_upsampling"):
+        # default UNET_TCONV_FWD=1: the consumers' u-row weight gradients come from the chain
+        # rule (skip-only wgrad), the forward keeps the tconv (composite forward is mode 2)
+        assert s2f == [] and sorted(e._wa_chain_of.values()) == ["transConv8", "transConv9"]
+        for cons in e._wa_chain_of:
+            assert names.index("chain:" + e._wa_chain_of[cons]) > names.index("wgrad:" + cons)
     # (head-on-load: the head backward only reduces the Mask gradients, on the side stream)
     nc = len(e.tconv_fused)
     assert [n for n in names[e.fwd_end:e.fwd_end + nc]] == ["compose:" + t for t in e.tconv_fused]
@@ -85,6 +98,20 @@ def test_bucket_plan_is_layer_aligned_and_covers_buffer():
     assert (flat.numel - b[-2]) * 4 / 2 ** 20 <= 8.0
 
 
+def test_composite_forward_plan(monkeypatch):
+    """UNET_TCONV_FWD=2: conv{8,9}a run as coarse composite forwards (u never allocated),
+    their weights composed first in the forward."""
+    from unet_distributed_amd.runtime.native_engine import NativeUNet
+    monkeypatch.setenv("UNET_TCONV_FWD", "2")
+    spec = UNetSpec(in_channels=4)
+    e = NativeUNet(spec, FlatParams(spec), 2, 64, "cpu", dry_run=True)
+    names = e.plan.names()
+    assert sorted(e._s2f_of.values()) == ["transConv8", "transConv9"]
+    assert names[:2] == ["fwd:compose:transConv8", "fwd:compose:transConv9"]
+    for t in ("transConv8", "transConv9"):
+        assert "fwd:" + t not in names and t not in e.bufs
+
+
 def test_engine_env_knobs_are_few():
     """The executor's behaviour is fixed by its measured defaults: only the A/B knobs
     the GPU tests flip remain environment-driven (round-2 review: <= 12)."""
@@ -93,7 +120,7 @@ def test_engine_env_knobs_are_few():
     src = open(native_engine.__file__).read()
     knobs = set(re.findall(r'os\.environ\.get\("(UNET_[A-Z0-9_]+)"', src))
     assert knobs <= {"UNET_DUAL_STREAM", "UNET_CONV_TILE", "UNET_FWD_STREAMS", "UNET_HEAD_FUSE",
-                     "UNET_HEAD_ONLOAD", "UNET_TCONV_FUSED"}, knobs
+                     "UNET_HEAD_ONLOAD", "UNET_TCONV_FUSED", "UNET_TCONV_FWD"}, knobs
 
 
 def test_fused_head_plan(monkeypatch):

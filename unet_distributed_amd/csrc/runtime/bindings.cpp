@@ -129,6 +129,7 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.xc = (const float*)getp(d, "xc");
   p.xz = getp(d, "xz");
   p.s2d = get<int>(d, "s2d", 0);
+  p.s2f = get<int>(d, "s2f", 0);
   p.xout = const_cast<void*>(getp(d, "xout"));
   p.tile = get<int>(d, "tile", 0);
   p.head_w = (const float*)getp(d, "head_w");
@@ -218,6 +219,7 @@ WgradParams wgrad_params(const py::dict& d) {
   X(norm_bwd_apply_launch) \
   X(tconv_compose_launch) \
   X(tconv_chain_launch) \
+  X(s2f_compose_launch) \
   X(adam_pack_launch)
 
 struct KernelApi {
@@ -349,13 +351,36 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     return [=](hipStream_t s) { return A->tconv_compose_launch(wt, wa, C, K, O, Ca, rs, out, s); };
   }
   if (kind == "tconv_chain") {
-    // ptrs: H [16][O][K], Bs [16][O], Wa master, dWt [4][C][K], dbt [C]   ints: C, K, O, Ca
-    need(5, 4, 0);
+    // ptrs: H [16][O][K], Bs [16][O], Wa master, dWt [4][C][K], dbt [C]
+    //       [, Wt master, bt master, skip-row gradient [9][Ca - C][O], dWa [9][Ca][O]]   ints: C, K, O, Ca
+    if (P.size() != 5 && P.size() != 9) throw std::invalid_argument("tconv_chain: 5 or 9 pointers");
+    need((int)P.size(), 4, 0);
     const float *hs = (const float*)vp(0), *bs = (const float*)vp(1), *wa = (const float*)vp(2);
     float *dwt = (float*)vp(3), *dbt = (float*)vp(4);
+    const float* wt = P.size() == 9 ? (const float*)vp(5) : nullptr;
+    const float* bt = P.size() == 9 ? (const float*)vp(6) : nullptr;
+    const float* skg = P.size() == 9 ? (const float*)vp(7) : nullptr;
+    float* dwa = P.size() == 9 ? (float*)vp(8) : nullptr;
     int C = I[0], K = I[1], O = I[2], Ca = I[3];
     check_msg(tconv_fused_check(C, K, O, Ca));
-    return [=](hipStream_t s) { return A->tconv_chain_launch(hs, bs, wa, C, K, O, Ca, dwt, dbt, s); };
+    if (dwa && (!wt || !bt || (Ca > C && !skg))) throw std::invalid_argument("tconv_chain: dWa needs Wt, bt, skip rows");
+    return [=](hipStream_t s) {
+      return A->tconv_chain_launch(hs, bs, wa, C, K, O, Ca, dwt, dbt, wt, bt, skg, dwa, s);
+    };
+  }
+  if (kind == "s2f_compose") {
+    // ptrs: Wt master [4][C][K], bt [C], Wa master [3][3][Ca][O], ba [O], out bf16 [4 O][Kpad], btab [4][4 O]
+    // ints: C, K, O, Ca, Kpad
+    need(6, 5, 0);
+    const float *wt = (const float*)vp(0), *bt = (const float*)vp(1), *wa = (const float*)vp(2),
+                *ba = (const float*)vp(3);
+    void* out = vp(4);
+    float* btab = (float*)vp(5);
+    int C = I[0], K = I[1], O = I[2], Ca = I[3], kp = I[4];
+    check_msg(tconv_fused_check(C, K, O, Ca));
+    if ((Ca - C) % 32 || (Ca - C) <= 0 || kp < 9 * (4 * (Ca - C) + K) || kp % 64)
+      throw std::invalid_argument("s2f_compose: skip channels must be a positive multiple of 32, Kpad >= 9 Cin");
+    return [=](hipStream_t s) { return A->s2f_compose_launch(wt, bt, wa, ba, C, K, O, Ca, kp, out, btab, s); };
   }
   if (kind == "multi_reduce") {
     // ptrs: job table (device, ReduceJob[njobs])   ints: njobs, total1, total2

@@ -341,6 +341,8 @@ class NativeUNet:
         deepest fine level fused (0 off)."""
         self.tconv_fused: Dict[str, dict] = {}
         self._tf_consumer: Dict[str, str] = {}
+        self._s2f_of: Dict[str, str] = {}       # composite-forward consumer conv -> its tconv
+        self._wa_chain_of: Dict[str, str] = {}  # consumer conv whose u-row wgrad is chained -> tconv
         top = int(os.environ.get("UNET_TCONV_FUSED", "2"))
         if self.dims != 2 or self.spec.norm != "none" or top <= 0:
             return
@@ -373,6 +375,41 @@ class NativeUNet:
                                             hs=torch.zeros(16 * O * K, dtype=torch.float32, device=self.device),
                                             bs=torch.zeros(16 * O, dtype=torch.float32, device=self.device))
             self._tf_consumer[c.name] = l.name
+            self._plan_s2f(l, c, self.tconv_fused[l.name])
+
+    def _plan_s2f(self, l, c, tf):
+        """UNET_TCONV_FWD (default 1) -- what the consumer conv z = conv3x3([u, skip]) of a
+        composite-backward tconv u = tconv(b) does without u:
+          1: its weight gradient: the u rows come from the 4x4-tap slab sums H / Bs the
+             composite backward forms anyway (tconv_chain), the skip rows from a skip-only
+             weight gradient -- the u half of the wgrad (a 1 GiB re-read at level 1) is gone;
+          2: also its forward (conv_win.h XF 5): the conv runs on the coarse grid over the
+             space-to-depth skip and b with weights composed per step from both fp32 masters
+             (tconv_fused.hip::s2f_compose), each output stored to its fine pixel, so u is
+             never written or read (its buffer is freed).  Measured -0.9 % on the headline
+             step (six 32-channel chunks with mostly-zero composed taps per window cost more
+             than the tconv launch and the u traffic they replace), hence not the default;
+          0: neither."""
+        mode = int(os.environ.get("UNET_TCONV_FWD", "1"))
+        Cs, K, O = c.cin - l.cout, l.cin, c.cout
+        if mode <= 0 or Cs <= 0 or Cs % 32 or O % 16:
+            return
+        tf["wa"] = dict(Cs=Cs, skg=torch.zeros(9 * Cs * O, dtype=torch.float32, device=self.device))
+        self._wa_chain_of[c.name] = l.name
+        if mode < 2 or (c.dropout and self.spec.dropout > 0):
+            return
+        kpad = _r64(9 * (4 * Cs + K))
+        probe = self._conv_common(l.level + 1, 3, 1, 1)
+        probe.update(C1=4 * Cs, s2d=Cs, C2=K, src1=1, src2=1, wgt=1, bias=1, Cout=4 * O, relu=1, dst1=1, s2f=O)
+        try:
+            if self.C.conv_fwd_grid(probe) <= 0:
+                return
+        except ValueError:
+            return
+        tf["s2f"] = dict(kpad=kpad, Cs=Cs, w=torch.zeros(4 * O * kpad, dtype=self.adt, device=self.device),
+                         btab=torch.zeros(16 * O, dtype=torch.float32, device=self.device))
+        self._s2f_of[c.name] = l.name
+        self.bufs.pop(l.name, None)            # u is never formed
 
     # ------------------------------------------------------------------ normalisation
     NORM_EPS = 1e-3          # models/reference.py::_norm (Keras default epsilon)
@@ -756,6 +793,7 @@ class NativeUNet:
         # convNb -> 2x2 max-pool fused into the conv's epilogue where the kernel can
         self._pool_of = {self.inputs[x.name][0]: x.name for x in spec.layers if x.kind == "pool"}
         self._pool_fused = set()
+        self._s2f_compose(plan)
         for l in spec.layers:
             if l.kind != "up":
                 self._fwd_layer(plan, l, dropout, train, 0, self.B)
@@ -777,6 +815,8 @@ class NativeUNet:
         for c in range(2):
             start = plan.size()
             mark = start
+            if c == 0:
+                self._s2f_compose(plan)
             for k, l in enumerate(layers):
                 self._fwd_layer(plan, l, dropout, train, c, nb)
                 if k + 1 == off:
@@ -785,6 +825,18 @@ class NativeUNet:
         for l in spec.layers:
             if l.kind == "mask":
                 self._fwd_layer(plan, l, dropout, train, 0, self.B)
+
+    def _s2f_compose(self, plan):
+        """Composite-forward weights + border bias tables from this step's fp32 masters."""
+        for tname, tf in self.tconv_fused.items():
+            sf = tf.get("s2f")
+            if sf is None:
+                continue
+            cons = tf["consumer"]
+            plan.add_generic("s2f_compose", [self.master_ptr(tname + "/kernel"), self.master_ptr(tname + "/bias"),
+                                             self.master_ptr(cons + "/kernel"), self.master_ptr(cons + "/bias"),
+                                             _ptr(sf["w"]), _ptr(sf["btab"])],
+                             [tf["C"], tf["K"], tf["O"], tf["Ca"], sf["kpad"]], [], "fwd:compose:" + tname)
 
     def _fwd_layer(self, plan, l, dropout, train, c, nb):
         """Forward launches of layer `l` for images [c*nb, (c+1)*nb)."""
@@ -795,7 +847,24 @@ class NativeUNet:
         def P(t):
             return None if t is None else _ptr(b[t]) + self._toff(t, c, nb)
 
-        if l.kind == "conv":
+        if l.kind == "conv" and l.name in self._s2f_of:
+            # composite transposed-conv forward on the coarse grid (u never formed)
+            tname = self._s2f_of[l.name]
+            tf = self.tconv_fused[tname]
+            sf = tf["s2f"]
+            skip = self.inputs[l.name][2]
+            d = self._conv_common(l.level + 1, 3, 1, 1)
+            d.update(N=nb, name="fwd:" + l.name, C1=4 * sf["Cs"], s2d=sf["Cs"], C2=tf["K"], src1=P(skip),
+                     src2=P(tf["src"]), wgt=_ptr(sf["w"]), bias=_ptr(sf["btab"]), Cout=4 * l.cout, relu=1,
+                     dst1=P(l.name), s2f=l.cout)
+            bits = self.relu_bits.get(l.name)
+            if bits is not None:
+                d["relu_bits"] = _ptr(bits) + c * nb * (self.npix(l.level) // self.B) * l.cout // 8
+            self._rev_order(d, tf["src"], l.name)
+            plan.add_conv_fwd(d)
+        elif l.kind == "tconv" and l.name in self.tconv_fused and "s2f" in self.tconv_fused[l.name]:
+            pass                                 # folded into its consumer's composite forward
+        elif l.kind == "conv":
             src1, up1, skip = self.inputs[l.name]
             c1 = self.tinfo[src1][1]
             s1 = P(src1)
@@ -1026,24 +1095,32 @@ class NativeUNet:
                 Q = self.npix(l.level)
                 # --- weight + bias gradient (fused column sums); the upsampling decoder's
                 # A operand is the materialised upsample when there is one
-                a1, upA = b[src1], up1
+                wa_t = self._wa_chain_of.get(l.name)
+                if wa_t is not None:
+                    # composite forward: no u -- the weight gradient runs over the skip
+                    # source only; tconv_chain forms the u rows from H / Bs
+                    a1, upA, c1w, c2w, skw = b[skip], 1, c2, 0, None
+                else:
+                    a1, upA, c1w, c2w, skw = (b[src1] if src1 in b else None), up1, c1, c2, skip
                 if up1 == 2 and self.ups_materialize:
                     a1, upA = b["up:" + src1], 1
                 kd = dict(N=self.B, QD=self.sdims(l.level)[0], QH=self.sdims(l.level)[1],
                           QW=self.sdims(l.level)[2], AD=self.sdims(l.level)[0], AH=self.sdims(l.level)[1],
                           AW=self.sdims(l.level)[2], KD=3 if self.dims == 3 else 1, KH=3, KW=3, stride=1,
-                          pad=1, upA=upA, a1=_ptr(a1), a2=_ptr(b[skip]) if skip else None,
+                          pad=1, upA=upA, a1=_ptr(a1), a2=_ptr(b[skw]) if skw else None,
                           b=_ptr(dy))
                 if first_xf is not None:
                     kd.update(first_xf)
                 if l.name == self.head_in and self.head_onload:
                     kd.update(self._head_grad_fields())
-                wspec = dict(lname=l.name, kd=kd, M1=c1, M2=c2, Nc=l.cout, KT=KT3, Q=Q,
+                wspec = dict(lname=l.name, kd=kd, M1=c1w, M2=c2w, Nc=l.cout, KT=KT3, Q=Q,
                              QD=self.sdims(l.level)[0], QH=self.sdims(l.level)[1],
                              QW=self.sdims(l.level)[2], upA=upA,
                              kernel=l.name + "/kernel", bias=l.name + "/bias", bias_mode=1,
                              bias_width=l.cout, bias_src=(dy, Q),
                              real_rows=(self.cpad, spec.in_channels) if first else None)
+                if wa_t is not None:
+                    wspec["kernel_out"] = _ptr(self.tconv_fused[wa_t]["wa"]["skg"])
                 part_at = tail_parts.pop(l.name, None)
                 if part_at is not None:
                     # first half of this weight gradient at the placeholder between the two
@@ -1218,6 +1295,7 @@ class NativeUNet:
                            ("direct", "<i4"), ("pad", "<i4")])
         assert job_dt.itemsize == self.C.reduce_job_bytes()
         pending_jobs, pending_layers = [], []
+        pending_tags = []            # reduced here but complete only after a later chain rule
         wgrad_layers = {w["lname"] for w in wg_specs}
         FLUSH_LAYERS = 3
 
@@ -1246,20 +1324,24 @@ class NativeUNet:
             table = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
             self._job_tables.append(table)
             plan.add_generic("multi_reduce", [_ptr(table)], [len(pending_jobs), t1, t2], [],
-                             "reduce:" + ",".join(pending_layers))
+                             "reduce:" + ",".join(pending_layers + pending_tags))
             for ln in pending_layers:
                 self._layer_done_at[ln] = plan.size()
             pending_jobs.clear()
             pending_layers.clear()
+            pending_tags.clear()
 
         slab0, bslab0, stage0 = _ptr(self.slab), _ptr(self.bias_slab), _ptr(self.red_stage)
-        chained = set()
+        # layers whose gradients are complete only after a chain rule (a fused tconv; the
+        # consumer of a composite forward, whose u rows the chain writes)
+        chained = set(self._wa_chain_of)
         for op in ops:
             if callable(op):
                 op(plan)
             elif op[0] == "done":
                 if op[1] in chained:
-                    pass                           # done after its chain rule
+                    if op[1] in self._wa_chain_of:  # done after its chain rule
+                        pending_tags.append(op[1])
                 elif op[1] in wgrad_layers:
                     pending_layers.append(op[1])
                     if len(pending_layers) >= FLUSH_LAYERS:
@@ -1315,11 +1397,18 @@ class NativeUNet:
                     pending_layers.append(tname)
                     flush()
                     chained.add(tname)
-                    plan.add_generic("tconv_chain", [_ptr(tf["hs"]), _ptr(tf["bs"]),
-                                                     self.master_ptr(tf["consumer"] + "/kernel"),
-                                                     self.grad_ptr(tname + "/kernel"), self.grad_ptr(tname + "/bias")],
-                                     [tf["C"], tf["K"], tf["O"], tf["Ca"]], [], "chain:" + tname)
+                    ptrs = [_ptr(tf["hs"]), _ptr(tf["bs"]), self.master_ptr(tf["consumer"] + "/kernel"),
+                            self.grad_ptr(tname + "/kernel"), self.grad_ptr(tname + "/bias")]
+                    sf = tf.get("wa")
+                    if sf is not None:
+                        # + the consumer's weight gradient: u rows from H / Bs, skip rows copied
+                        assert tf["consumer"] not in pending_layers
+                        ptrs += [self.master_ptr(tname + "/kernel"), self.master_ptr(tname + "/bias"),
+                                 _ptr(sf["skg"]), self.grad_ptr(tf["consumer"] + "/kernel")]
+                    plan.add_generic("tconv_chain", ptrs, [tf["C"], tf["K"], tf["O"], tf["Ca"]], [], "chain:" + tname)
                     self._layer_done_at[tname] = plan.size()
+                    if sf is not None:
+                        self._layer_done_at[tf["consumer"]] = plan.size()
         flush()
 
     # ------------------------------------------------------------------ buckets
