@@ -41,8 +41,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--per_gpu_batch", type=int, default=1024,
-                   help="images per GPU (profiles/r2_batch_sweep.md: throughput saturates from 512)")
+    p.add_argument("--per_gpu_batch", type=int, default=None,
+                   help="images per GPU; default 1024 for 2D (profiles/r2_batch_sweep.md: throughput "
+                        "saturates from 512), 8 volumes for 3D (profiles/r3_bench_history.md 3D sweep: "
+                        "2 / 4 / 8 -> 236 / 258 / 271 vol/s)")
     p.add_argument("--img_size", type=int, default=128)
     p.add_argument("--in_channels", type=int, default=4)
     p.add_argument("--dims", type=int, default=2)
@@ -155,6 +157,8 @@ def main():
     N = ctx.world_size
     if world_env != a.gpus and ctx.rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d" % (a.gpus, world_env), file=sys.stderr)
+    if a.per_gpu_batch is None:
+        a.per_gpu_batch = 8 if a.dims == 3 else 1024
     cfg = Config(batch_size=a.per_gpu_batch * N, in_channels=a.in_channels, img_size=a.img_size,
                  dims=a.dims, use_upsampling=a.use_upsampling, backend=a.backend, dtype=a.dtype,
                  norm=a.norm, groups=a.groups,

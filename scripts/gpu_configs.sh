@@ -7,7 +7,7 @@ o=gpurun_out/configs.log; : > $o
 run() { timeout -k 10 240 python bench.py "$@" 2>/dev/null | grep metric >> $o || { echo "FAILED: $*" >> $o; exit 1; }; }
 run --steps 20 --warmup 5
 run --steps 20 --warmup 5 --per_gpu_batch 256
-run --dims 3 --per_gpu_batch 2 --steps 10 --warmup 3
+run --dims 3 --steps 6 --warmup 2
 run --img_size 512 --in_channels 1 --per_gpu_batch 16 --steps 10 --warmup 3
 run --dtype fp16 --norm group --per_gpu_batch 1024 --steps 10 --warmup 3
 run --norm batch --steps 10 --warmup 3

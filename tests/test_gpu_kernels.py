@@ -914,3 +914,65 @@ def test_row_window_kernels_beyond_2gib(cuda_dev):
     torch.cuda.synchronize()
     assert rel_err(full, parts[0][0] + parts[1][0]) < 1e-4
     assert rel_err(fb, parts[0][1] + parts[1][1]) < 1e-4
+
+
+@pytest.mark.parametrize("N,C1,C2,Cout,drop", [(5, 256, 0, 512, 0.0), (8, 512, 0, 512, 0.2), (3, 64, 64, 128, 0.0),
+                                              (4, 32, 0, 64, 0.0)])
+def test_conv_img8_forward(cuda_dev, N, C1, C2, Cout, drop):
+    """8x8 image-window kernel (tile 13, auto at 8x8): bias + ReLU (+ dropout, generic
+    epilogue) + ReLU bits vs the fp32 reference; a partial last workgroup (N % 4); the
+    dropout keep-mask equals the implicit-GEMM kernel's (tile 1 / 2)."""
+    torch.manual_seed(51)
+    dev = cuda_dev
+    x = torch.randn(N, 8, 8, C1, device=dev).bfloat16()
+    sk = torch.randn(N, 8, 8, C2, device=dev).bfloat16() if C2 else None
+    w = (torch.randn(3, 3, C1 + C2, Cout, device=dev) * 0.05).bfloat16()
+    b = torch.randn(Cout, device=dev) * 0.1
+    assert C().conv_fwd_pick(dict(N=N, OH=8, OW=8, IH=8, IW=8, KH=3, KW=3, pad=1, C1=C1, C2=C2, src1=1,
+                                  src2=1 if C2 else None, wgt=1, Cout=Cout, relu=1, dst1=1, drop_rate=drop)) == 13
+    outs = {}
+    for tile in (13, 2):
+        y = torch.full((N, 8, 8, Cout), float("nan"), device=dev, dtype=torch.bfloat16)
+        bits = torch.zeros(N, 8, 8, Cout // 8, device=dev, dtype=torch.uint8)
+        wp = pack_fwd(w)
+        C().conv_fwd(dict(N=N, OH=8, OW=8, IH=8, IW=8, KH=3, KW=3, pad=1, C1=C1, C2=C2, src1=ptr(x),
+                          src2=ptr(sk) if C2 else None, wgt=ptr(wp), bias=ptr(b), Cout=Cout, relu=1,
+                          drop_rate=drop, seed=7, salt=2, dst1=ptr(y), relu_bits=ptr(bits), tile=tile), stream())
+        torch.cuda.synchronize()
+        assert torch.equal(bits, _pack_bits(y))
+        outs[tile] = y
+    xin = torch.cat([x, sk], -1) if C2 else x
+    ref = nhwc(F.relu(F.conv2d(nchw(xin.float()), w.float().permute(3, 2, 0, 1), b, padding=1)))
+    y = outs[13]
+    if drop:
+        keep = outs[2].float() != 0
+        assert torch.equal(keep, y.float() != 0) or (keep ^ (y.float() != 0)).float().mean() < 1e-3
+        ref = ref * keep / (1 - drop)
+    assert rel_err(y, ref) < 1e-2
+    assert rel_err(y, outs[2]) < 1e-2
+
+
+def test_conv_img8_dgrad_dual_dest_bit_masks(cuda_dev):
+    """8x8 image-window data gradient: flipped weights, two destinations, ReLU bit masks
+    and a dropout rescale on the second."""
+    torch.manual_seed(52)
+    dev = cuda_dev
+    N, C1, C2, Co = 6, 256, 256, 512
+    m1 = torch.randn(N, 8, 8, C1, device=dev).bfloat16()
+    m2 = torch.randn(N, 8, 8, C2, device=dev).bfloat16()
+    w = (torch.randn(3, 3, C1 + C2, Co, device=dev) * 0.05).bfloat16()
+    dy = torch.randn(N, 8, 8, Co, device=dev).bfloat16()
+    d1 = torch.empty(N, 8, 8, C1, device=dev, dtype=torch.bfloat16)
+    d2 = torch.empty(N, 8, 8, C2, device=dev, dtype=torch.bfloat16)
+    b1, b2, wd = _pack_bits(m1), _pack_bits(m2), pack_dgrad(w)      # (kept alive across the launch)
+    d = dict(N=N, OH=8, OW=8, IH=8, IW=8, KH=3, KW=3, pad=1, C1=Co, src1=ptr(dy), wgt=ptr(wd),
+             Cout=C1 + C2, D1=C1, dst1=ptr(d1), dst2=ptr(d2), mask1=ptr(b1), mask2=ptr(b2),
+             mask_bits=3, mask_scale2=1.25)
+    assert C().conv_fwd_pick(d) == 13
+    C().conv_fwd(d, stream())
+    xr = torch.zeros(N, C1 + C2, 8, 8, device=dev, requires_grad=True)
+    (g,) = torch.autograd.grad(F.conv2d(xr, w.float().permute(3, 2, 0, 1), padding=1), xr, nchw(dy.float()))
+    g = nhwc(g)
+    torch.cuda.synchronize()
+    assert rel_err(d1, g[..., :C1] * (m1.float() > 0)) < 1e-2
+    assert rel_err(d2, g[..., C1:] * (m2.float() > 0) * 1.25) < 1e-2

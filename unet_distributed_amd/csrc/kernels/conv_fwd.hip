@@ -284,6 +284,134 @@ hipError_t launch_cfg(const ConvFwdParams& p, hipStream_t s) {
 
 
 // ---------------------------------------------------------------------------------
+// Image-window conv for 8 x 8 images (the deepest UNet level at 128^2 inputs: 2D 3x3
+// 'same', Cin / Cout multiples of 32 / 64).  The row-window kernel needs 16-pixel rows;
+// the implicit GEMM above re-gathers the input once per tap (9x the L2->LDS traffic)
+// through one register stage, which leaves these MFMA-bound layers latency-bound at
+// ~35 % MFMA utilisation.  Here a workgroup owns IMG8 = 4 whole images (256 pixels, one
+// per wave) x 64 output channels.  Per 32-channel chunk it LDS-DMAs each image with its
+// zero ring (10 x 10 slots at a 12-slot row pitch, OOB loads supply the zeros) plus the
+// chunk's 9 x 64 weight rows, and runs the nine taps on shifted LDS addresses: an MFMA
+// A fragment is 2 rows x 8 columns, lane fr reading slot (2 rp + fr / 8 + dh) x 12 +
+// fr % 8 + dw.  Chunk c of a slot sits at c ^ (((column >> 2) & 1) << 1): conflict-free
+// for every tap shift (tools/lds_bank_model.py search) and row independent, so a lane
+// needs one address per horizontal tap plus immediates.  A fragment of halo row k feeds
+// every (row pair rp, tap dh) with 2 rp + dh = k.
+constexpr int IMG8 = 4;
+
+template <int EPI>
+__global__ void __launch_bounds__(NTHR) conv_img8_kernel(const ConvFwdParams p) {
+  constexpr int BM = IMG8 * 64, BN = 64, PITCH = 12, ISL = 10 * PITCH;
+  constexpr int XI = IMG8 * ISL / 16, WI = 9 * BN / 16;
+  constexpr int XB = XI * 1024, WB = WI * 1024;
+  constexpr int EPIB = BM * (BN + 4) * 2;
+  constexpr int LDS_BYTES = (XB + WB > EPIB) ? XB + WB : EPIB;
+  constexpr int TM = 4, TN = BN / 16;
+  static_assert(IMG8 * ISL % 16 == 0, "DMA runs");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  char* Xs = smem;
+  char* Ws = smem + XB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_n = p.Cout / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int img0 = tm * IMG8, n0 = tn * BN;
+  const int M = p.N * 64;
+  const int Cin = p.C1 + p.C2;
+  const int nchunks = Cin >> 5;
+  constexpr int OOB = 0x7fffffff;
+  // workgroup-relative buffer bases (32-bit DMA offsets count from the tile's first image)
+  const char* s1b = (const char*)p.src1 + (size_t)img0 * 64 * p.C1 * 2;
+  const char* s2b = p.src2 ? (const char*)p.src2 + (size_t)img0 * 64 * p.C2 * 2 : s1b;
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)s1b, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc((void*)s2b, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int fsub = lane >> 4, fr = lane & 15;
+  int xbase[3];
+#pragma unroll
+  for (int dw = 0; dw < 3; ++dw) {
+    const int col = (fr & 7) + dw;
+    xbase[dw] = (wave * ISL + (fr >> 3) * PITCH + col) * 64 + 16 * (fsub ^ (((col >> 2) & 1) << 1));
+  }
+  const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
+  const int lslot = lane >> 2;
+  const int lchunk = (lane & 3) ^ ((lslot >> 1) & 3);
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const bool from1 = p.C2 == 0 || (kc << 5) < p.C1;
+    const int C = from1 ? p.C1 : p.C2;
+    const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
+    if (kc) __syncthreads();                      // the previous chunk's fragment reads are done
+    const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
+#pragma unroll
+    for (int q = 0; q < (XI + 3) / 4; ++q) {
+      const int k = wave + 4 * q;
+      if (k < XI) {
+        const int sl = 16 * k + lslot;
+        const int im = sl / ISL, rem = sl - im * ISL;
+        const int hr = rem / PITCH, hc = rem - hr * PITCH;
+        const int h = hr - 1, w = hc - 1;
+        const bool ok = (unsigned)h < 8u && (unsigned)w < 8u && img0 + im < p.N;
+        const int lch = (lane & 3) ^ (((hc >> 2) & 1) << 1);
+        const int off = ok ? (((im * 64 + h * 8 + w) * C) + cb + lch * 8) * 2 : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+    const int wl = (lslot * p.Kpad + (kc << 5) + lchunk * 8) * 2;
+#pragma unroll
+    for (int q = 0; q < (WI + 3) / 4; ++q) {
+      const int k = wave + 4 * q;
+      if (k < WI) {
+        const int tap = k / (BN / 16), nb = (k % (BN / 16)) * 16;
+        const int off = ((n0 + nb) * p.Kpad + tap * Cin) * 2 + wl;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024), 16,
+                                                 off, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw) {
+      h16x8 wf[3][TN];
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) wf[dh][j] = *(const h16x8*)(Ws + ((3 * dh + dw) * BN + 16 * j) * 64 + wbase);
+#pragma unroll
+      for (int hr = 0; hr < 2 * TM + 2; ++hr) {      // halo rows 0 .. 9 of the image
+        if (hr == 2 * TM + 1) continue;             // (row 9 only feeds pair 4 -- none)
+        const h16x8 xf = *(const h16x8*)(Xs + xbase[dw] + hr * PITCH * 64);
+#pragma unroll
+        for (int dh = 0; dh < 3; ++dh) {
+          const int r2 = hr - dh;
+          if (r2 < 0 || (r2 & 1) || r2 / 2 >= TM) continue;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[r2 / 2][j] = mfma16(wf[dh][j], xf, acc[r2 / 2][j]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  conv_epilogue<BM, BN, 64, BN, TM, TN, NTHR, EPI>(p, acc, smem, img0 * 64, n0, M, wave, 0, lane, tid, 0, 0, tm);
+}
+
+hipError_t launch_img8(const ConvFwdParams& p, hipStream_t s) {
+  const int grid = ((p.N + IMG8 - 1) / IMG8) * (p.Cout / 64);
+  switch (conv_epi_mode(p)) {
+    case EPI_FWD: hipLaunchKernelGGL((conv_img8_kernel<EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case EPI_DGRAD: hipLaunchKernelGGL((conv_img8_kernel<EPI_DGRAD>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case EPI_GENERIC: hipLaunchKernelGGL((conv_img8_kernel<EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
 // First-layer row-window conv (Cin = 4 or 8 after channel padding, 2D 3x3 'same').
 //
 // K = 9 taps x CIN is tiny, so the implicit GEMM above spends its time on per-tap
@@ -725,6 +853,16 @@ static bool tconv_dgrad_eligible(const ConvFwdParams& p) {
 
 int conv_fwd_pick(const ConvFwdParams& p);
 
+// 2D 8 x 8 images, 3x3 'same', plain / concat source, no normalisation statistics or
+// fused extras (the image-window kernel above).
+static bool img8_eligible(const ConvFwdParams& p) {
+  const int ep = conv_epi_mode(p);
+  return p.OW == 8 && p.OH == 8 && p.IW == 8 && p.IH == 8 && p.KD == 1 && p.OD == 1 && p.ID == 1 && p.KH == 3 &&
+         p.KW == 3 && p.stride == 1 && p.pad == 1 && p.up1 == 1 && !p.shuffle && p.C1 > 0 && (p.C1 % 32) == 0 &&
+         (p.C2 % 32) == 0 && (p.Cout % 64) == 0 && (ep == EPI_FWD || ep == EPI_DGRAD || ep == EPI_GENERIC) &&
+         !p.route_gy && !p.pool_dst && !p.head_w && !p.xform && !p.hg.prob && !p.s2d && !p.s2f;
+}
+
 // Fills the tap tables and Kpad; returns nullptr on success or a message describing
 // why the shape is unsupported.
 const char* conv_fwd_prepare(ConvFwdParams& p) {
@@ -787,15 +925,16 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
         p.OH % 2 || p.OW % 2 || p.Cout % 8 || p.head_w)
       return "conv_fwd: fused max-pool needs a 2D row-window ReLU forward (even rows, codes buffer)";
   }
-  if (p.tile < 0 || p.tile > 12) return "conv_fwd: bad tile id";
+  if (p.tile < 0 || p.tile > 13) return "conv_fwd: bad tile id";
   if (p.tile == 12 && (!win_eligible(p) || p.Cout % 64 || p.head_w))
     return "conv_fwd: 64-wide row-window tile not applicable";
   if (p.tile == 10 && !tconv_fwd_eligible(p)) return "conv_fwd: transposed-conv window tile not applicable";
   if (p.tile == 11 && !tconv_dgrad_eligible(p)) return "conv_fwd: transposed-conv dgrad tile not applicable";
   if (p.tile == 9 && !win_first_eligible(p)) return "conv_fwd: first-layer window tile not applicable";
+  if (p.tile == 13 && !img8_eligible(p)) return "conv_fwd: 8x8 image-window tile not applicable";
   {
     const int t = p.tile ? p.tile : 0;
-    const int bn = t == 1 ? 128 : (t == 2 || t == 5 || t == 7 || t == 12) ? 64 : 32;
+    const int bn = t == 1 ? 128 : (t == 2 || t == 5 || t == 7 || t == 12 || t == 13) ? 64 : 32;
     if (t && p.Cout % bn) return "conv_fwd: forced tile does not divide Cout";
     if (t == 7) return "conv_fwd: tile 7 (row-window 512x64: 268 registers, 92 KB LDS, 1 wave/SIMD) is not built";
     if (t == 6 && !win_eligible(p)) return "conv_fwd: row-window tile not applicable";
@@ -818,7 +957,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     const long long opx = (long long)p.OD * p.OH * p.OW;
     const long long lim = (1LL << 31) - 64;
     long long span = img * p.N;                       // bytes a launch addresses from one base
-    if (t == 6 || t == 12) span = img;
+    if (t == 6 || t == 12 || t == 13) span = img;
     else if (t >= 1 && t <= 5) span = img * (256 / opx + 2 < p.N ? 256 / opx + 2 : p.N);
     if (span >= lim) return "conv_fwd: input exceeds the 2 GiB reach of one buffer base (split the batch)";
   }
@@ -838,7 +977,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
 }
 
 // tile ids: 1 = 128x128, 2 = 128x64, 3 = 256x32, 4 = 128x32, 5 = 256x64 (4 waves each);
-// 6 = row-window 512 x 32; 8 = auto but never row-window (A/B tests)
+// 6 = row-window 512 x 32; 8 = auto but never row-window (A/B tests); 13 = 8x8 image window
 int conv_fwd_pick(const ConvFwdParams& p) {
   const int M = p.N * p.OD * p.OH * p.OW;
   if (p.tile && p.tile != 8) return p.tile;
@@ -847,6 +986,7 @@ int conv_fwd_pick(const ConvFwdParams& p) {
   // variant needs 287 registers (1 wave/SIMD) and never wins
   if (p.tile != 8 && win_eligible(p)) return 6;
   if (p.tile != 8 && win_first_eligible(p)) return 9;
+  if (p.tile != 8 && img8_eligible(p)) return 13;
   if (p.tile != 8 && tconv_fwd_eligible(p)) return 10;
   if (p.tile != 8 && tconv_dgrad_eligible(p)) return 11;
   if (p.Cout % 128 == 0 && M >= 8192) return 1;
@@ -912,6 +1052,7 @@ hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
       return win_bm(p) == 256 ? launch_win<32, 256>(p, s) : launch_win<32, 512>(p, s);
     case 9: return p.C1 == 4 ? launch_win_first<4>(p, s) : launch_win_first<8>(p, s);
     case 10: return launch_tconv_fwd(p, s);
+    case 13: return launch_img8(p, s);
     case 11: return launch_tconv_dgrad(p, s);
     default: return launch_cfg<128, 32, 4, 1>(p, s);
   }

@@ -703,6 +703,8 @@ PYBIND11_MODULE(_C, m) {
   // workgroups of a row-window conv launch (0 for other kernels): sizes per-block
   // partial buffers of fused epilogues (the fused head); raises if the dict is invalid
   m.def("conv_fwd_grid", [](const py::dict& d) { return unet::conv_fwd_grid(conv_params(d)); }, py::arg("params"));
+  // kernel / tile id a conv launch dispatches to (conv_fwd.hip conv_fwd_pick; tests)
+  m.def("conv_fwd_pick", [](const py::dict& d) { return unet::conv_fwd_pick(conv_params(d)); }, py::arg("params"));
   // (rows, pixels per tile) of the per-tile statistics the conv's epilogue writes
   // (rows 0: no statistics epilogue for this shape -> separate moments pass)
   m.def("conv_stat_tiles", [](const py::dict& d) {
