@@ -431,3 +431,32 @@ def test_tconv_consumer_modes_step(cuda_dev, monkeypatch, kw):
         for g in (g1, g2):
             d = 1.0 - _cos(g[k].float(), gt[k])
             assert d <= 2.0 * d0 + 3e-4, (k, d0, d)
+
+
+@pytest.mark.parametrize("norm", ["batch", "group"])
+def test_tconv_fused_norm_step(cuda_dev, monkeypatch, norm):
+    """Composite transposed-conv backward with BatchNorm / GroupNorm (the S2D data gradient
+    carries the tconv input's dgrad-norm epilogue; the consumer's u-row weight gradient
+    from the slab sums) vs the materialised tconv backward (UNET_TCONV_FUSED=0): both held
+    against the fp32 ATen step, the composite at most 2x + 1e-3 the materialised path's
+    per-gradient cosine distance."""
+    outs = []
+    for v in ("0", "2"):
+        monkeypatch.setenv("UNET_TCONV_FUSED", v)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, batch_size=4, img_size=64, in_channels=4, norm=norm)
+        e = nb.engine
+        assert sorted(e.tconv_fused) == ([] if v == "0" else ["transConv8", "transConv9"])
+        nb.fwd_bwd(x, y, seed=93)
+        if v == "0":
+            tb.fwd_bwd(x, y, seed=93)
+            ref = {k: ft.view(ft.grad, k).clone() for k, *_ in ft.entries}
+        torch.cuda.synchronize()
+        outs.append((nb.sums().cpu(), {k: fn.view(fn.grad, k).clone() for k, *_ in fn.entries}))
+    (s0, g0), (s2, g2) = outs
+    assert torch.equal(s0, s2)                               # the forward is unchanged
+    for k in g0:
+        if ref[k].norm() < 1e-6:
+            continue
+        d0 = 1.0 - _cos(g0[k].float(), ref[k])
+        d2 = 1.0 - _cos(g2[k].float(), ref[k])
+        assert d2 <= 2.0 * d0 + 1e-3, (k, d0, d2)

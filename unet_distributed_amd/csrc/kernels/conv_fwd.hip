@@ -910,7 +910,8 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     return "conv_fwd: composite transposed-conv forward needs a 2D two-source ReLU row-window forward "
            "(C1 = 4 s2d, Cout = 4 s2f, bias tables)";
   if (p.s2d && !p.s2f && (p.s2d % 32 || p.C1 != 4 * p.s2d || p.C2 || p.xform || p.hg.prob || p.route_gy || p.KD != 1 ||
-                p.OD != 1 || p.OW > 128 || !win_eligible(p) || conv_epi_mode(p) != EPI_DGRAD ||
+                p.OD != 1 || p.OW > 128 || !win_eligible(p) ||
+                (conv_epi_mode(p) != EPI_DGRAD && conv_epi_mode(p) != EPI_DGRAD_NORM) ||
                 (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12)))
     return "conv_fwd: space-to-depth source needs a 2D single-source row-window data gradient (C1 = 4 s2d)";
   if (p.route_gy && (!p.pool_code || (conv_epi_mode(p) != EPI_DGRAD && conv_epi_mode(p) != EPI_DGRAD_NORM) ||

@@ -540,14 +540,19 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
     return hipGetLastError();
   }
   if (p.s2d) {                          // space-to-depth dgrad source (conv_fwd_prepare checks the shape)
-    if (epi != EPI_DGRAD || geo != GEO_2D) return hipErrorInvalidValue;
+    if ((epi != EPI_DGRAD && epi != EPI_DGRAD_NORM) || geo != GEO_2D) return hipErrorInvalidValue;
     switch (W) {
 #define S2D_CASE(WW)                                                                                      \
   case WW:                                                                                                \
-    if constexpr (win_tile_built<BN, BM>(WW))                                                             \
-      hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_2D, 4>), dim3(grid), dim3(NTHR), 0, s, p); \
-    else                                                                                                  \
+    if constexpr (win_tile_built<BN, BM>(WW)) {                                                           \
+      if (epi == EPI_DGRAD)                                                                               \
+        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_2D, 4>), dim3(grid), dim3(NTHR), 0, s, p); \
+      else                                                                                                \
+        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD_NORM, GEO_2D, 4>), dim3(grid), dim3(NTHR), 0, s, \
+                           p);                                                                            \
+    } else {                                                                                              \
       return hipErrorInvalidValue;                                                                        \
+    }                                                                                                     \
     break;
       S2D_CASE(16)
       S2D_CASE(32)

@@ -344,7 +344,7 @@ class NativeUNet:
         self._s2f_of: Dict[str, str] = {}       # composite-forward consumer conv -> its tconv
         self._wa_chain_of: Dict[str, str] = {}  # consumer conv whose u-row wgrad is chained -> tconv
         top = int(os.environ.get("UNET_TCONV_FUSED", "2"))
-        if self.dims != 2 or self.spec.norm != "none" or top <= 0:
+        if self.dims != 2 or top <= 0 or (self.spec.norm != "none" and not self.fuse_norm_stats_planned()):
             return
         for l in self.spec.layers:
             if l.kind != "tconv" or l.level > top:
@@ -364,6 +364,10 @@ class NativeUNet:
             probe = self._conv_common(l.level + 1, 3, 1, 1)
             probe.update(C1=4 * O, s2d=O, src1=1, wgt=1, Cout=K, relu=0, dst1=1, D1=K, mask1=1,
                          mask_bits=1 if src in self.relu_bits else 0)
+            if self.spec.norm != "none":
+                # normalised tconv input: the composite dgrad's epilogue is the dgrad-norm one
+                probe.update(mask1=None, mask_bits=0, nz=1, na=1, nc=1, stats=1, npix=1,
+                             ncs=0 if self.spec.norm == "batch" else K)
             try:
                 if self.C.conv_fwd_grid(probe) <= 0:
                     continue
@@ -376,6 +380,11 @@ class NativeUNet:
                                             bs=torch.zeros(16 * O, dtype=torch.float32, device=self.device))
             self._tf_consumer[c.name] = l.name
             self._plan_s2f(l, c, self.tconv_fused[l.name])
+
+    def fuse_norm_stats_planned(self):
+        """Normalised model: every conv epilogue writes its statistics (the composite
+        transposed-conv data gradient then carries the tconv input's norm backward rows)."""
+        return getattr(self, "fuse_norm_stats", True)
 
     def _plan_s2f(self, l, c, tf):
         """UNET_TCONV_FWD (default 1) -- what the consumer conv z = conv3x3([u, skip]) of a
@@ -1160,8 +1169,12 @@ class NativeUNet:
                                 d.update(name="dgrad:" + l.name, C1=4 * l.cout, s2d=l.cout, src1=_ptr(dy),
                                          wgt=_ptr(tf["wg"]), Cout=tf["K"], relu=0, dst1=_ptr(b["d:" + tsrc]),
                                          D1=tf["K"], mask1=m1, mask_bits=mb)
+                                self._fuse_dgrad_norm(d, tsrc)
+                                if spec.norm != "none" and not d.get("nz"):
+                                    raise RuntimeError("fused transposed conv %s: no dgrad-norm epilogue" % tname)
                                 self._deferred_skip[dsk[0]] = dsk[1]
-                                self._rev_order(d, "g:" + l.name, "g:" + tsrc)
+                                if spec.norm == "none":
+                                    self._rev_order(d, "g:" + l.name, "g:" + tsrc)
                                 return d
                             if up1 == 2:
                                 dst1 = b["dfull:" + src1]          # full-res grad of the upsample
@@ -1228,7 +1241,8 @@ class NativeUNet:
             elif l.kind == "tconv" and l.name in self.tconv_fused:
                 tf = self.tconv_fused[l.name]
                 lo, hi = self.sdims(l.level + 1), self.sdims(l.level)
-                dz = b["d:" + tf["consumer"]]
+                # the consumer's pre-activation gradient (its norm backward's dz when normalised)
+                dz = b[("dz:" if spec.norm != "none" else "d:") + tf["consumer"]]
                 kd = dict(N=self.B, QD=1, QH=lo[1], QW=lo[2], AD=1, AH=hi[1], AW=hi[2], KD=1, KH=4, KW=4,
                           stride=2, pad=1, upA=1, a1=_ptr(dz), b=_ptr(b[tf["src"]]))
                 emit_wgrad(dict(lname=l.name, kd=kd, M1=tf["O"], M2=0, Nc=tf["K"], KT=16, QW=lo[2],
