@@ -976,3 +976,40 @@ def test_conv_img8_dgrad_dual_dest_bit_masks(cuda_dev):
     torch.cuda.synchronize()
     assert rel_err(d1, g[..., :C1] * (m1.float() > 0)) < 1e-2
     assert rel_err(d2, g[..., C1:] * (m2.float() > 0) * 1.25) < 1e-2
+
+
+def test_conv_img8_norm_statistics(cuda_dev):
+    """8x8 image window with the fused-normalisation epilogues (BatchNorm): the pre-norm
+    forward's per-tile {sum z, sum z^2} rows and the dgrad-norm epilogue's masked gradient
+    + {sum g, sum g z} rows reduce to the implicit-GEMM kernel's (tile 2) totals."""
+    torch.manual_seed(53)
+    dev, N, Ci, Co = cuda_dev, 6, 256, 512
+    x = torch.randn(N, 8, 8, Ci, device=dev).bfloat16()
+    w = (torch.randn(3, 3, Ci, Co, device=dev) * 0.05).bfloat16()
+    b = torch.randn(Co, device=dev) * 0.1
+    wp = pack_fwd(w)
+    na, nc = torch.rand(Co, device=dev) + 0.5, torch.randn(Co, device=dev) * 0.1
+    dy = torch.randn(N, 8, 8, Co, device=dev).bfloat16()
+    w2 = (torch.randn(3, 3, Co, Co, device=dev) * 0.05).bfloat16()
+    wd = pack_dgrad(w2)
+    res = {}
+    for tile in (13, 2):
+        geo = dict(N=N, OH=8, OW=8, IH=8, IW=8, KH=3, KW=3, pad=1, tile=tile)
+        df = dict(geo, C1=Ci, src1=ptr(x), wgt=ptr(wp), bias=ptr(b), Cout=Co, relu=0, stats=1, dst1=1)
+        rows, _ = C().conv_stat_tiles(df)
+        z = torch.empty(N, 8, 8, Co, device=dev, dtype=torch.bfloat16)
+        st = torch.zeros(rows, 2, Co, device=dev)
+        C().conv_fwd(dict(df, dst1=ptr(z), stats=ptr(st)), stream())
+        dd = dict(geo, C1=Co, src1=ptr(dy), wgt=ptr(wd), Cout=Co, relu=0, stats=1, nz=ptr(z), na=ptr(na), nc=ptr(nc),
+                  npix=64, dst1=1)
+        rows2, _ = C().conv_stat_tiles(dd)
+        g = torch.empty(N, 8, 8, Co, device=dev, dtype=torch.bfloat16)
+        st2 = torch.zeros(rows2, 2, Co, device=dev)
+        C().conv_fwd(dict(dd, dst1=ptr(g), stats=ptr(st2)), stream())
+        torch.cuda.synchronize()
+        res[tile] = (z, st.sum(0), g, st2.sum(0))
+    (z0, s0, g0, t0), (z1, s1, g1, t1) = res[13], res[2]
+    assert rel_err(z0, z1) < 1e-2 and rel_err(g0, g1) < 1e-2
+    assert rel_err(s0, s1) < 1e-2 and rel_err(t0, t1) < 1e-2
+    zf = z0.float().reshape(-1, Co)
+    assert rel_err(s0[0], zf.sum(0)) < 1e-3 and rel_err(s0[1], (zf * zf).sum(0)) < 1e-3

@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(NTHR) conv_img8_kernel(const ConvFwdParams p) 
   constexpr int BM = IMG8 * 64, BN = 64, PITCH = 12, ISL = 10 * PITCH;
   constexpr int XI = IMG8 * ISL / 16, WI = 9 * BN / 16;
   constexpr int XB = XI * 1024, WB = WI * 1024;
-  constexpr int EPIB = BM * (BN + 4) * 2;
+  constexpr int EPIB = (EPI == EPI_STATS || EPI == EPI_DGRAD_NORM) ? epi_lds_bytes<BM, BN>() : BM * (BN + 4) * 2;
   constexpr int LDS_BYTES = (XB + WB > EPIB) ? XB + WB : EPIB;
   constexpr int TM = 4, TN = BN / 16;
   static_assert(IMG8 * ISL % 16 == 0, "DMA runs");
@@ -406,6 +406,10 @@ hipError_t launch_img8(const ConvFwdParams& p, hipStream_t s) {
     case EPI_FWD: hipLaunchKernelGGL((conv_img8_kernel<EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p); break;
     case EPI_DGRAD: hipLaunchKernelGGL((conv_img8_kernel<EPI_DGRAD>), dim3(grid), dim3(NTHR), 0, s, p); break;
     case EPI_GENERIC: hipLaunchKernelGGL((conv_img8_kernel<EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case EPI_STATS: hipLaunchKernelGGL((conv_img8_kernel<EPI_STATS>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case EPI_DGRAD_NORM:
+      hipLaunchKernelGGL((conv_img8_kernel<EPI_DGRAD_NORM>), dim3(grid), dim3(NTHR), 0, s, p);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -853,13 +857,14 @@ static bool tconv_dgrad_eligible(const ConvFwdParams& p) {
 
 int conv_fwd_pick(const ConvFwdParams& p);
 
-// 2D 8 x 8 images, 3x3 'same', plain / concat source, no normalisation statistics or
-// fused extras (the image-window kernel above).
+// 2D 8 x 8 images, 3x3 'same', plain / concat source, no fused pool / head / transform
+// (the image-window kernel above); normalisation statistics per 4-image tile.
 static bool img8_eligible(const ConvFwdParams& p) {
   const int ep = conv_epi_mode(p);
   return p.OW == 8 && p.OH == 8 && p.IW == 8 && p.IH == 8 && p.KD == 1 && p.OD == 1 && p.ID == 1 && p.KH == 3 &&
          p.KW == 3 && p.stride == 1 && p.pad == 1 && p.up1 == 1 && !p.shuffle && p.C1 > 0 && (p.C1 % 32) == 0 &&
-         (p.C2 % 32) == 0 && (p.Cout % 64) == 0 && (ep == EPI_FWD || ep == EPI_DGRAD || ep == EPI_GENERIC) &&
+         (p.C2 % 32) == 0 && (p.Cout % 64) == 0 && !(p.nz && (p.C2 || p.ncs)) &&
+         (ep == EPI_FWD || ep == EPI_DGRAD || ep == EPI_GENERIC || ep == EPI_STATS || ep == EPI_DGRAD_NORM) &&
          !p.route_gy && !p.pool_dst && !p.head_w && !p.xform && !p.hg.prob && !p.s2d && !p.s2f;
 }
 
@@ -1030,6 +1035,10 @@ void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
       return;
     }
     case 10:
+      return;
+    case 13:               // 8x8 image window: 4 whole images per tile
+      *rows = (p.N + IMG8 - 1) / IMG8;
+      *tile_px = IMG8 * 64;
       return;
     default: {
       if (p.nz && (smallc || p.C2)) return;
