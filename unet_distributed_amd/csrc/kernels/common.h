@@ -107,6 +107,24 @@ __device__ __forceinline__ uint32_t pos_bits(const u32x4& v) {
   }
   return b;
 }
+// pos_bits of ReLU outputs (every element +0 or positive, never -0 or negative, e.g.
+// relu2h's): nonzero <=> positive, so a packed unsigned min with 1 gives each 16-bit
+// half's bit in place and three shift-ors gather them -- 8 VALU instead of ~24.  Bits
+// above 7 of the result are not zero (callers store the low byte).
+__device__ __forceinline__ uint32_t pos_bits_relu(const u32x4& v) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  uint32_t m[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    // (through a scalar copy: __builtin_bit_cast of the vector element lvalue v[e]
+    // reads element 0 for every e with this clang)
+    const uint32_t w = v[e];
+    m[e] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, w), (u16x2){1, 1}));
+  }
+  // bit 2e: element 2e (low half of word e); bit 16 + 2e: element 2e + 1 (high half)
+  const uint32_t c = (m[0] | (m[1] << 2)) | ((m[2] | (m[3] << 2)) << 4);
+  return c | (c >> 15);
+}
 // v with element e zeroed unless bit e of `bits` is set
 __device__ __forceinline__ u32x4 keep_bits(u32x4 v, uint32_t bits) {
 #pragma unroll

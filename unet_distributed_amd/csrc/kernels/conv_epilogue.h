@@ -507,7 +507,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       v = mbit ? keep_bits(v, ((const uint8_t*)mk)[off >> 3]) : keep_pos(v, *(const u32x4*)((const h16*)mk + off));
     }
     *(u32x4*)(dst + off) = v;
-    if ((EPI == EPI_FWD || G) && p.relu_bits) p.relu_bits[off >> 3] = (uint8_t)pos_bits(v);
+    // (EPI_FWD: ReLU outputs from relu2h, never -0 -- the cheap form)
+    if (EPI == EPI_FWD && p.relu_bits) p.relu_bits[off >> 3] = (uint8_t)pos_bits_relu(v);
+    if (G && p.relu_bits) p.relu_bits[off >> 3] = (uint8_t)pos_bits(v);
     if constexpr (kHeadable) {
       if (kHead) {
         float f[8];

@@ -99,7 +99,14 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   // halo row pitch in 64-byte pixel slots: W + 2 columns rounded up to a multiple of 4
   // (every row starts on a 256-byte bank row); the DMA fills the image as one linear
   // run of slots, so rows need not align to the 16-slot DMA instructions
-  constexpr int HWP = W + 4;
+  // ALR (2D, 128-wide rows: one or two chunks per window, so the DMA address set-up is
+  // not amortised): rows padded to whole 16-slot DMA pieces -- a piece then lies in one
+  // halo row, its row checks and row offset are wave-uniform (scalar), and a lane's
+  // column / swizzle part is the same for every piece: a few VALU per piece instead of a
+  // division by the pitch and 64-bit address math (73.7 KB LDS, still two WGs per CU)
+  constexpr bool ALR = GEO == GEO_2D && W == 128;
+  constexpr int HWP = ALR ? (W + 2 + 15) / 16 * 16 : W + 4;
+  constexpr int PPR = HWP / 16;                 // DMA pieces per halo row (ALR)
   constexpr int ROWB = HWP * 64;
   constexpr int XI = (HR * HWP + 15) / 16, WI = 9 * BN / 16;
   constexpr int XB = XI * 1024, WB = WI * 1024;
@@ -334,13 +341,21 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
         for (int q = 0; q < (XI + 3) / 4; ++q) {
           const int k = wave + 4 * q;
           if (XF != 3 && k < XI) {
-            const int sl = 16 * k + lslot;
-            const int hr = sl / HWP, hc = sl - hr * HWP;
+            int hr, hc;
+            if constexpr (ALR) {
+              hr = k / PPR;                                 // wave-uniform
+              hc = 16 * (k - hr * PPR) + lslot;
+            } else {
+              const int sl = 16 * k + lslot;
+              hr = sl / HWP;
+              hc = sl - hr * HWP;
+            }
             const int gr = g0 - 1 + hr;
             const int col = hc - 1;
             const bool row_in = hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in);
             const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
-            const int lch = (lane & 3) ^ ((hc >> 1) & 3);
+            // (ALR: pieces start on 16-slot boundaries, so the swizzle is lchunk's)
+            const int lch = ALR ? lchunk : (lane & 3) ^ ((hc >> 1) & 3);
             // XF 4: the coarse slot's fine pixel (2 gr + sa, 2 col + sb) of the 2W-wide rows
             const int lr = gr - grow0;                      // image-relative row
             const int pix = s2 ? (2 * lr + sa) * (2 * W) + 2 * col + sb : lr * W + col;
