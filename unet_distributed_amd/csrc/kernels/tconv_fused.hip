@@ -57,41 +57,53 @@ __global__ void __launch_bounds__(256) tconv_compose_kernel(const float* __restr
   out[idx] = f2h(acc);
 }
 
-// blocks [0, nw): dWt elements (t, c, k), k fastest; the last block: dbt[c]
+// blocks [0, nw): dWt elements (t, c, k), k fastest, 4 partial sums over o per element
+// (lane bits 4-5: the o quarter, combined by two xor shuffles) -- 4x the threads and a
+// quarter of the dependent-load chain of one thread per element (the kernel is latency-
+// bound: a few MB of operands); blocks [nw, nw + C): dbt[c], the 9 O products of one c
+// summed by the whole block
 __global__ void __launch_bounds__(256) tconv_chain_kernel(const float* __restrict__ Hs, const float* __restrict__ bs,
                                                           const float* __restrict__ wa, int C, int K, int O, int Ca,
                                                           int nw, float* __restrict__ dwt, float* __restrict__ dbt) {
   if ((int)blockIdx.x < nw) {
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= 4 * C * K) return;
-    const int k = idx % K, c = (idx / K) % C, t = idx / (C * K);
-    const int a = t >> 1, b = t & 1;
+    const int lane = threadIdx.x & 63, part = lane >> 4;
+    const int idx = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + (lane & 15);
+    const bool ok = idx < 4 * C * K;                 // (K % 16 == 0: whole 16-lane groups)
+    const int e = ok ? idx : 0;
+    const int k = e % K, c = (e / K) % C, t = e / (C * K);
+    const int a = t >> 1, b = t & 1, oq = O >> 2, o0 = part * oq;
     float acc = 0.f;
     for (int dh = 0; dh < 3; ++dh)
       for (int dw = 0; dw < 3; ++dw) {
-        const float* wap = wa + ((size_t)(dh * 3 + dw) * Ca + c) * O;
-        const float* hp = Hs + (size_t)((a - dh + 2) * 4 + (b - dw + 2)) * O * K + k;
-        for (int o = 0; o < O; ++o) acc = fmaf(wap[o], hp[(size_t)o * K], acc);
+        const float* wap = wa + ((size_t)(dh * 3 + dw) * Ca + c) * O + o0;
+        const float* hp = Hs + ((size_t)((a - dh + 2) * 4 + (b - dw + 2)) * O + o0) * K + k;
+#pragma unroll 4
+        for (int o = 0; o < oq; ++o) acc = fmaf(wap[o], hp[(size_t)o * K], acc);
       }
-    dwt[idx] = acc;
+    acc += __shfl_xor(acc, 16, 64);
+    acc += __shfl_xor(acc, 32, 64);
+    if (ok && part == 0) dwt[idx] = acc;
     return;
   }
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float acc = 0.f;
-    for (int dh = 0; dh < 3; ++dh)
-      for (int dw = 0; dw < 3; ++dw) {
-        const float* wap = wa + ((size_t)(dh * 3 + dw) * Ca + c) * O;
-        for (int o = 0; o < O; ++o) {
-          float s = 0.f;
+  __shared__ float red[256];
+  const int c = blockIdx.x - nw;
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < 9 * O; i += 256) {
+    const int tap = i / O, o = i - tap * O, dh = tap / 3, dw = tap - 3 * dh;
+    float sb = 0.f;
 #pragma unroll
-          for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int b = 0; b < 2; ++b) s += bs[((a - dh + 2) * 4 + (b - dw + 2)) * O + o];
-          acc = fmaf(wap[o], s, acc);
-        }
-      }
-    dbt[c] = acc;
+      for (int b = 0; b < 2; ++b) sb += bs[((a - dh + 2) * 4 + (b - dw + 2)) * O + o];
+    acc = fmaf(wa[((size_t)tap * Ca + c) * O + o], sb, acc);
   }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dbt[c] = red[0];
 }
 
 // Composite FORWARD (conv_win.h XF 5): z(2h + a, 2w + b) = relu(sum_{Th,Tw} [S2D(skip) | b](h + Th - 1,
@@ -221,8 +233,8 @@ hipError_t tconv_compose_launch(const float* wt, const float* wa, int C, int K, 
 hipError_t tconv_chain_launch(const float* Hs, const float* bs, const float* wa, int C, int K, int O, int Ca,
                               float* dwt, float* dbt, const float* wt, const float* bt, const float* skg, float* dwa,
                               hipStream_t s) {
-  const int nw = (4 * C * K + 255) / 256;
-  hipLaunchKernelGGL(tconv_chain_kernel, dim3(nw + 1), dim3(256), 0, s, Hs, bs, wa, C, K, O, Ca, nw, dwt, dbt);
+  const int nw = (4 * C * K + 63) / 64;            // 64 elements (x 4 o quarters) per block
+  hipLaunchKernelGGL(tconv_chain_kernel, dim3(nw + C), dim3(256), 0, s, Hs, bs, wa, C, K, O, Ca, nw, dwt, dbt);
   if (dwa) {
     const int n = 9 * Ca * O;
     hipLaunchKernelGGL(tconv_chain_wa_kernel, dim3((n + 15) / 16), dim3(256), 0, s, Hs, bs, wt, bt, skg, C, K, O,
