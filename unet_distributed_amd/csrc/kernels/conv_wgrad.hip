@@ -374,15 +374,17 @@ __global__ void __launch_bounds__(256) multi_reduce1_kernel(const ReduceJob* __r
   const long long i = local - (long long)g * J.n4;
   const int s0 = g * RED_G, s1 = min(J.splits, s0 + RED_G);
   const f32x4* src = (const f32x4*)J.slab + i;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  int s = s0;
-  for (; s + 4 <= s1; s += 4) {
-    const f32x4 a = src[(size_t)s * J.n4], b = src[(size_t)(s + 1) * J.n4];
-    const f32x4 c = src[(size_t)(s + 2) * J.n4], d = src[(size_t)(s + 3) * J.n4];
-    acc += (a + b) + (c + d);
-  }
-  for (; s < s1; ++s) acc += src[(size_t)s * J.n4];
-  ((f32x4*)(J.direct ? J.out : J.stage))[(size_t)g * J.n4 + i] = acc;
+  // all RED_G loads issued before the first add (one memory round trip; the kernel is
+  // latency-bound), then a fixed pairwise tree (deterministic)
+  f32x4 v[RED_G];
+#pragma unroll
+  for (int k = 0; k < RED_G; ++k)
+    v[k] = s0 + k < s1 ? src[(size_t)(s0 + k) * J.n4] : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int w = 1; w < RED_G; w <<= 1)
+#pragma unroll
+    for (int k = 0; k + w < RED_G; k += 2 * w) v[k] += v[k + w];
+  ((f32x4*)(J.direct ? J.out : J.stage))[(size_t)g * J.n4 + i] = v[0];
 }
 
 __global__ void __launch_bounds__(256) multi_reduce2_kernel(const ReduceJob* __restrict__ jobs, int njobs,
@@ -401,8 +403,16 @@ __global__ void __launch_bounds__(256) multi_reduce2_kernel(const ReduceJob* __r
   const int t = r / J.Mout;
   const int m = (mo / J.rkeep) * J.rg + (mo % J.rkeep);
   const size_t src = (((size_t)t * J.Mtot + m) * J.Nc + n) / 4;
+  const f32x4* st = (const f32x4*)J.stage + src;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int y = 0; y < J.groups; ++y) acc += ((const f32x4*)J.stage)[(size_t)y * J.n4 + src];
+  int y = 0;
+  for (; y + 8 <= J.groups; y += 8) {                 // 8 loads in flight per round trip
+    f32x4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = st[(size_t)(y + k) * J.n4];
+    acc += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+  }
+  for (; y < J.groups; ++y) acc += st[(size_t)y * J.n4];
   ((f32x4*)J.out)[i] = acc;
 }
 

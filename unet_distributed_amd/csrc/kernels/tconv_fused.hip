@@ -50,6 +50,7 @@ __global__ void __launch_bounds__(256) tconv_compose_kernel(const float* __restr
         if (dw < 0 || dw > 2) continue;
         const float* wap = wa + (size_t)(dh * 3 + dw) * Ca * O + o;
         const float* wtp = wt + (size_t)(2 * a + b) * C * K + k;
+#pragma unroll 8
         for (int c = 0; c < C; ++c) acc = fmaf(wap[(size_t)c * O], wtp[(size_t)c * K], acc);
       }
     }
@@ -206,6 +207,7 @@ __global__ void __launch_bounds__(256) tconv_chain_wa_kernel(const float* __rest
       const int sl = (a - dh + 2) * 4 + (b - dw + 2);
       const float* hp = Hs + ((size_t)sl * O + o) * K;
       const float* wtp = wt + ((size_t)(2 * a + b) * C + c) * K;
+#pragma unroll 4
       for (int k = l16; k < K; k += 16) acc = fmaf(wtp[k], hp[k], acc);
       bsum += bs[sl * O + o];
     }
