@@ -364,12 +364,15 @@ __global__ void __launch_bounds__(256) slab_final_kernel(const float* __restrict
 // the (few dozen) prefix offsets.
 __global__ void __launch_bounds__(256) multi_reduce1_kernel(const ReduceJob* __restrict__ jobs, int njobs,
                                                             long long total) {
-  const long long gi = blockIdx.x * 256LL + threadIdx.x;
+  // job ranges start on 256-thread boundaries (native_engine flush): the job is
+  // block-uniform, so the scan and the job fields are scalar loads
+  const long long b0 = blockIdx.x * 256LL, gi = b0 + threadIdx.x;
   if (gi >= total) return;
   int j = 0;
-  while (j + 1 < njobs && jobs[j + 1].p1_begin <= gi) ++j;
+  while (j + 1 < njobs && jobs[j + 1].p1_begin <= b0) ++j;
   const ReduceJob& J = jobs[j];
   const long long local = gi - J.p1_begin;
+  if (local >= (long long)J.groups * J.n4) return;   // the job range's padding
   const int g = (int)(local / J.n4);
   const long long i = local - (long long)g * J.n4;
   const int s0 = g * RED_G, s1 = min(J.splits, s0 + RED_G);
@@ -389,10 +392,10 @@ __global__ void __launch_bounds__(256) multi_reduce1_kernel(const ReduceJob* __r
 
 __global__ void __launch_bounds__(256) multi_reduce2_kernel(const ReduceJob* __restrict__ jobs, int njobs,
                                                             long long total) {
-  const long long gi = blockIdx.x * 256LL + threadIdx.x;
+  const long long b0 = blockIdx.x * 256LL, gi = b0 + threadIdx.x;
   if (gi >= total) return;
   int j = 0;
-  while (j + 1 < njobs && jobs[j + 1].p2_begin <= gi) ++j;
+  while (j + 1 < njobs && jobs[j + 1].p2_begin <= b0) ++j;
   const ReduceJob& J = jobs[j];
   const long long i = gi - J.p2_begin;
   if (J.direct || i >= J.n4o) return;

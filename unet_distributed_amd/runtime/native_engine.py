@@ -1333,8 +1333,9 @@ class NativeUNet:
                           "rg", "rkeep", "direct"):
                     arr[k][f] = j[f]
                 arr[k]["p1"], arr[k]["p2"] = t1, t2
-                t1 += j["groups"] * j["n4"]
-                t2 += 0 if j["direct"] else j["n4o"]
+                # (ranges padded to whole 256-thread blocks: block-uniform job lookup)
+                t1 += -(-j["groups"] * j["n4"] // 256) * 256
+                t2 += 0 if j["direct"] else -(-j["n4o"] // 256) * 256
             table = torch.from_numpy(arr.view(np.uint8).copy()).to(self.device)
             self._job_tables.append(table)
             plan.add_generic("multi_reduce", [_ptr(table)], [len(pending_jobs), t1, t2], [],
