@@ -806,6 +806,8 @@ hipError_t launch_tconv_dgrad(const ConvFwdParams& p, hipStream_t s) {
       hipLaunchKernelGGL((tconv_dgrad_kernel<WW, 64, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p);     \
     break;
   switch (W) {
+    TD_CASE(8)
+    TD_CASE(16)
     TD_CASE(32)
     TD_CASE(64)
     default:
@@ -849,7 +851,7 @@ static bool tconv_fwd_eligible(const ConvFwdParams& p) {
 // 2D transposed-conv data gradient (2x2 stride-2 conv of the fine gradient); coarse rows
 // 32 / 64 wide (narrower levels measured faster on the implicit-GEMM kernel).
 static bool tconv_dgrad_eligible(const ConvFwdParams& p) {
-  const bool w_ok = p.OW == 32 || p.OW == 64;
+  const bool w_ok = p.OW == 8 || p.OW == 16 || p.OW == 32 || p.OW == 64;
   return !p.shuffle && p.KD == 1 && p.KH == 2 && p.KW == 2 && p.stride == 2 && p.pad == 0 && p.OD == 1 &&
          p.ID == 1 && w_ok && p.IW == 2 * p.OW && p.IH == 2 * p.OH && p.up1 == 1 && p.C2 == 0 &&
          (p.C1 % 32) == 0 && (p.Cout % 64) == 0 && (!p.stats || p.nz) && p.drop_rate == 0.f;
