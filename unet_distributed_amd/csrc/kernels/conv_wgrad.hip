@@ -1288,7 +1288,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_s2d_win_kernel(const WgradParams p
   constexpr int XI = QN * BMc / 16, YI = (FR * FP + 15) / 16;
   constexpr int XB = XI * 1024, YB = YI * 1024;
   constexpr int KS = BMc / 32;
-  static_assert(W >= 32 && W <= 64, "composite window wgrad");
+  static_assert(W >= 16 && W <= 64, "composite window wgrad");
   __shared__ __attribute__((aligned(1024))) char smem[XB + YB];
   char* Xs = smem;
   char* Ys = smem + XB;
@@ -1381,7 +1381,10 @@ __global__ void __launch_bounds__(NTHR) wgrad_s2d_win_kernel(const WgradParams p
 #pragma unroll 1
     for (int kk = 0; kk < KS; ++kk) {
       const int px0 = kk * 32;
-      const int rr = px0 / W, c0 = px0 - rr * W;
+      // this lane group's 8 coarse pixels px0 + 8 G .. + 7 lie in one coarse row (W % 8 == 0;
+      // at W = 16 a 32-pixel step spans two rows)
+      const int pg = px0 + 8 * G;
+      const int rr = pg / W, cg = pg - rr * W;
       h16x8 bf[2 * QN];
 #pragma unroll
       for (int qn = 0; qn < QN; ++qn)
@@ -1394,7 +1397,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_s2d_win_kernel(const WgradParams p
       const int rowb = (2 * rr + sh) * FP;              // staged row of fine row 2(g0 + rr) + sh - 1
 #pragma unroll
       for (int sw = 0; sw < 4; ++sw) {
-        const int s0 = rowb + col_slot(sw, c0 + 8 * G + q);
+        const int s0 = rowb + col_slot(sw, cg + q);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const h16x8 af = tr8(Ys + tr_addr(s0, 16 * i + 4 * pp), Ys + tr_addr(s0 + 4, 16 * i + 4 * pp));
@@ -1492,10 +1495,10 @@ static bool wgrad_tconv_win_eligible(const WgradParams& p) {
          (p.M1 % 32) == 0 && (p.Nc % 32) == 0 && p.bias_mode != 1;
 }
 
-// Composite transposed-conv slab sums (4x4 taps, stride 2, pad 1) on coarse rows 32 / 64 wide.
+// Composite transposed-conv slab sums (4x4 taps, stride 2, pad 1) on coarse rows 16..64 wide.
 static bool wgrad_s2d_win_eligible(const WgradParams& p) {
   const int R = p.QW > 0 ? 128 / p.QW : 1;
-  return p.win >= 0 && (p.QW == 32 || p.QW == 64) && p.QD == 1 && p.KD == 1 && p.KH == 4 && p.KW == 4 &&
+  return p.win >= 0 && (p.QW == 16 || p.QW == 32 || p.QW == 64) && p.QD == 1 && p.KD == 1 && p.KH == 4 && p.KW == 4 &&
          p.stride == 2 && p.pad == 1 && p.upA == 1 && p.AW == 2 * p.QW && p.AH == 2 * p.QH && p.QH % R == 0 &&
          p.M2 == 0 && (p.M1 % 32) == 0 && (p.Nc % 32) == 0 && p.bias_mode != 1;
 }
@@ -1582,7 +1585,9 @@ hipError_t wgrad_launch(const WgradParams& p0, hipStream_t s) {
     const int qn = p.Nc % 64 == 0 ? 2 : 1;
     const int grid = (p.M1 / 32) * (p.Nc / (32 * qn)) * launch_splits(p);
 #define SW_CASE(WW, QQ) hipLaunchKernelGGL((wgrad_s2d_win_kernel<WW, QQ>), dim3(grid), dim3(NTHR), 0, s, p)
-    if (p.QW == 32) {
+    if (p.QW == 16) {
+      if (qn == 2) SW_CASE(16, 2); else SW_CASE(16, 1);
+    } else if (p.QW == 32) {
       if (qn == 2) SW_CASE(32, 2); else SW_CASE(32, 1);
     } else {
       if (qn == 2) SW_CASE(64, 2); else SW_CASE(64, 1);
