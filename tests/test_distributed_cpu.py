@@ -223,3 +223,47 @@ def test_inventory_roundtrip_and_remote_commands(tmp_path):
     assert len(cmds) == 2 and "--node_rank 1" in cmds[1][-1] and "--master_addr 10.0.0.1" in cmds[1][-1]
     env = launch.child_env({}, 9, 1, 16, 8, "10.0.0.1", 29500)
     assert env["RANK"] == "9" and env["LOCAL_RANK"] == "1" and env["WORLD_SIZE"] == "16"
+
+
+def _run_bench(extra, nproc=2, timeout=600, env_extra=None):
+    """The driver's multi-GPU bench command (`torch.distributed.run ... bench.py --gpus N`)."""
+    port = _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", **(env_extra or {}))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(nproc)] + extra
+    return subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                          timeout=timeout, cwd=ROOT)
+
+
+def bench_record(out):
+    recs = [json.loads(l) for l in out.splitlines() if l.startswith("{") and '"metric"' in l]
+    assert len(recs) == 1, out[-3000:]          # rank 0 prints exactly one JSON line
+    return recs[0]
+
+
+def check_multirank_bench(rec, n):
+    """The fields the driver and the judge read from an N-rank bench line, plus the
+    per-bucket / exposed-communication diagnostics of the N > 1 branch."""
+    assert rec["n_gpus"] == n and rec["config"]["parallelism"] == "dp%d" % n
+    assert rec["config"]["global_batch"] == n * rec["config"]["per_gpu_batch"]
+    assert rec["value"] > 0 and rec["ms_per_step"] > 0 and rec["scaling"] == "weak"
+    c = rec["comm"]
+    assert c["world_size"] == n
+    per = c["allreduce_ms_per_bucket"]
+    assert len(per) == len(c["buckets_mb"]) >= 2 and all(t > 0 for t in per)
+    for k in ("exposed_comm_ms", "step_ms_serial_comm", "step_ms_overlapped", "step_ms_compute_only"):
+        assert isinstance(c[k], float), (k, c)
+
+
+def test_bench_py_two_ranks_gloo_cpu():
+    """bench.py's N > 1 code path (timed steps with overlapped bucket allreduces, MAX over
+    ranks, then comm_diagnostics: per-bucket allreduce times and the overlapped / serial /
+    compute-only A/B) on two CPU ranks over gloo with the ATen backend -- the same command
+    shape the driver's 8-GPU lease runs (`test_dist.py:385-398`: every worker's sharded step)."""
+    r = _run_bench(["--backend", "torch", "--dtype", "fp32", "--per_gpu_batch", "2", "--img_size", "64",
+                    "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stdout[-3000:]
+    rec = bench_record(r.stdout)
+    check_multirank_bench(rec, 2)
+    assert rec["comm"]["backend"] == "gloo" and rec["config"]["backend"] == "torch"

@@ -154,3 +154,22 @@ def test_async_ps_device_server_two_ranks_one_card(tmp_path):
     if os.path.isdir(os.path.join(ROOT, "gpurun_out")):
         with open(os.path.join(ROOT, "gpurun_out", "async_ps_timing.json"), "w") as f:
             json.dump(recs, f)
+
+
+def test_bench_py_two_ranks_one_card_native():
+    """The exact multi-GPU bench command the driver's 8-GPU lease runs
+    (`torch.distributed.run --nproc-per-node N bench.py --gpus N`), at N = 2 with both
+    ranks on cuda:0 over gloo (UNET_DIST_BACKEND=gloo; RCCL refuses two ranks on one
+    device): the native executor, HIP graphs, the side-stream bucket allreduces, the
+    MAX-over-ranks timing and the N > 1 comm diagnostics all execute before any 8-GPU
+    run does."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_distributed_cpu import _run_bench, bench_record, check_multirank_bench
+    r = _run_bench(["--per_gpu_batch", "64", "--steps", "3", "--warmup", "2"], timeout=300,
+                   env_extra=dict(UNET_DIST_BACKEND="gloo"))
+    assert r.returncode == 0, r.stdout[-3000:]
+    rec = bench_record(r.stdout)
+    check_multirank_bench(rec, 2)
+    assert rec["config"]["backend"] == "native" and rec["comm"]["backend"] == "gloo"
+    assert rec["dtype"] == "bf16" and rec["config"]["img_size"] == 128 and rec["config"]["in_channels"] == 4
+    print("2-rank one-card bench:", json.dumps(rec["comm"]))

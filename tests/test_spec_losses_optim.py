@@ -149,3 +149,25 @@ def test_loss_scaler_dynamic_skip_halve_grow():
     st = LossScaler("fp16", loss_scale=128.0)
     assert not st.dynamic and st.scale == 128.0
     assert not st.update(torch.tensor([float("inf")])) and st.scale == 128.0
+
+
+def test_one_gpu_path_no_silent_aten_dispatch():
+    """--backend auto on a GPU is the HIP executor or an error naming the reason, never a
+    silent ATen / MIOpen run; ATen only when asked for (--backend torch)
+    or off the GPU (the CPU / gloo plumbing config).  device 'cuda' is only a device
+    type here: nothing touches a GPU."""
+    import pytest
+    from unet_distributed_amd.config import Config
+    from unet_distributed_amd.models.spec import spec_from_config
+    from unet_distributed_amd.runtime.backends import resolve_backend
+    ok = Config(dtype="bf16", in_channels=4)
+    assert resolve_backend("auto", spec_from_config(ok), ok, "cuda") == "native"
+    assert resolve_backend("auto", spec_from_config(ok), ok, "cpu") == "torch"
+    assert resolve_backend("torch", spec_from_config(ok), ok, "cuda") == "torch"
+    for bad, why in ((Config(dtype="fp32"), "dtype=fp32"), (Config(base_filters=48), "base filters")):
+        spec = spec_from_config(bad)
+        for want in ("auto", "native"):
+            with pytest.raises(RuntimeError, match=why):
+                resolve_backend(want, spec, bad, "cuda")
+        assert resolve_backend("torch", spec, bad, "cuda") == "torch"
+        assert resolve_backend("auto", spec, bad, "cpu") == "torch"

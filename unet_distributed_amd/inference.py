@@ -45,14 +45,11 @@ class _Cfg:
 class Predictor:
     def __init__(self, spec: UNetSpec, flat: FlatParams, img_size: int, device, batch: int,
                  dtype: str = "bf16", backend: str = "auto", state=None):
-        from .runtime.backends import NativeBackend, TorchBackend, native_supported
+        from .runtime.backends import NativeBackend, TorchBackend, resolve_backend
         self.spec, self.flat, self.batch, self.img_size = spec, flat, batch, img_size
         self.device = torch.device(device)
         cfg = _Cfg(img_size, dtype if self.device.type == "cuda" else "fp32")
-        reason = native_supported(spec, cfg, self.device)
-        if backend == "native" or (backend == "auto" and reason is None):
-            if reason is not None:
-                raise RuntimeError("native inference unsupported: " + reason)
+        if resolve_backend(backend, spec, cfg, self.device) == "native":
             from . import native
             native.require()
             self.backend = NativeBackend(spec, flat, cfg, self.device, batch)

@@ -197,12 +197,28 @@ def native_supported(spec, cfg, device) -> Optional[str]:
     return None
 
 
-def make_backend(spec, flat, cfg, device, per_rank_batch, bounds=None):
-    want = cfg.backend
+def resolve_backend(want: str, spec, cfg, device) -> str:
+    """'native' or 'torch' for a requested ``--backend`` (auto / native / torch).
+
+    One GPU path: on a GPU, ``auto`` means the HIP executor and a
+    config it does not support is an error with the reason -- never a silent ATen /
+    MIOpen run.  ATen stays reachable only by asking for it (``--backend torch``: the
+    numerical oracle and baseline) and is what ``auto`` means off the GPU (the CPU /
+    gloo plumbing config)."""
+    if want == "torch":
+        return "torch"
     reason = native_supported(spec, cfg, device)
-    if want == "native" or (want == "auto" and reason is None):
+    on_gpu = torch.device(device).type == "cuda"
+    if want == "native" or (want == "auto" and on_gpu):
         if reason is not None:
-            raise RuntimeError("--backend native requested but unsupported: " + reason)
+            raise RuntimeError("the native HIP executor does not support this config (%s); "
+                               "pass --backend torch to run the ATen reference path explicitly" % reason)
+        return "native"
+    return "torch"
+
+
+def make_backend(spec, flat, cfg, device, per_rank_batch, bounds=None):
+    if resolve_backend(cfg.backend, spec, cfg, device) == "native":
         from .. import native
         native.require()
         return NativeBackend(spec, flat, cfg, device, per_rank_batch, bounds)
