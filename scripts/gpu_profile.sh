@@ -12,7 +12,7 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $o/ks 
   python bench.py --steps 5 --warmup 2 > $o/ks.log 2>&1 || exit $?
 f=$(find $o/ks -name "*kernel_stats.csv" | head -1); cp $f $o/prof_kernel_stats.csv
 python tools/prof_summary.py $o 7 "bench.py 2D 128x128x4 b${BATCH:-1024} bf16 ($tag)" > $o/kernel_stats.md || exit $?
-UNET_FWD_STREAMS=1 timeout -k 10 300 python tools/layer_times.py --batch ${BATCH:-1024} --img 128 --out $o/layer_times.md > $o/lt.log 2>&1 || exit $?
+UNET_ENGINE=fwd_streams=1 timeout -k 10 300 python tools/layer_times.py --batch ${BATCH:-1024} --img 128 --out $o/layer_times.md > $o/lt.log 2>&1 || exit $?
 pass=0
 for ctr in "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_BUSY_CYCLES" "FETCH_SIZE" "WRITE_SIZE"; do
   pass=$((pass+1))

@@ -213,7 +213,7 @@ def test_hip_graph_replay_equals_eager(cuda_dev, monkeypatch, norm):
     device memory) is bit-identical to eager plan replay over several steps with
     changing dropout seeds and learning rates.  (One-stream forward: the two-stream
     forward is launched eagerly even in graph mode.)"""
-    monkeypatch.setenv("UNET_FWD_STREAMS", "1")
+    monkeypatch.setenv("UNET_ENGINE", "fwd_streams=1")
     from unet_distributed_amd.config import Config
     from unet_distributed_amd.data.datasets import synthetic_brats
     from unet_distributed_amd.models import reference
@@ -263,13 +263,13 @@ def test_hip_graph_replay_equals_eager(cuda_dev, monkeypatch, norm):
     dict(batch_size=4, img_size=64, in_channels=4),
 ])
 def test_two_stream_forward_equals_one_stream(cuda_dev, monkeypatch, kw):
-    """UNET_FWD_STREAMS=2 runs the training forward as two half-batch chunks on two
+    """fwd_streams=2 runs the training forward as two half-batch chunks on two
     streams (fused pools / head logits written at the chunk's offset): activations,
     loss sums and gradients are bit-identical to the one-stream forward, dropout
     included (each chunk hashes its elements' whole-batch indices, drop_idx0)."""
     outs = []
     for n in ("1", "2"):
-        monkeypatch.setenv("UNET_FWD_STREAMS", n)
+        monkeypatch.setenv("UNET_ENGINE", "fwd_streams=" + n)
         spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
         assert (getattr(nb.engine, "_fwd2", None) is not None) == (n == "2")
         for seed in (77, 0x9E3779B9):
@@ -289,12 +289,12 @@ def test_two_stream_forward_equals_one_stream(cuda_dev, monkeypatch, kw):
     dict(batch_size=2, img_size=32, in_channels=4, dims=3),
 ])
 def test_fused_head_matches_separate_head(cuda_dev, monkeypatch, kw):
-    """The head fused into the head-input conv's epilogue (UNET_HEAD_FUSE=1) gives the
+    """The head fused into the head-input conv's epilogue (head_fuse=1) gives the
     separate head kernel's probabilities, loss sums and gradients up to fp32
     summation order."""
     outs = []
     for f in ("0", "1"):
-        monkeypatch.setenv("UNET_HEAD_FUSE", f)
+        monkeypatch.setenv("UNET_ENGINE", "head_fuse=" + f)
         spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
         assert bool(nb.engine._head_fused_blocks) == (f == "1")
         nb.fwd_bwd(x, y, seed=77)
@@ -348,12 +348,12 @@ def test_native_inference_export_roundtrip_norm(cuda_dev, tmp_path, norm):
     dict(batch_size=4, img_size=128, in_channels=4, loss="dice_bce", hip_graph=True),
 ])
 def test_head_onload_step_equals_materialised(cuda_dev, monkeypatch, kw):
-    """UNET_HEAD_ONLOAD=1 (default: the head input's gradient formed on load by its
+    """head_onload=1 (default: the head input's gradient formed on load by its
     consumers, no dY tensor) gives the materialised-dY step bit for bit: loss sums,
     probabilities and every parameter gradient."""
     outs = []
     for v in ("0", "1"):
-        monkeypatch.setenv("UNET_HEAD_ONLOAD", v)
+        monkeypatch.setenv("UNET_ENGINE", "head_onload=" + v)
         spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
         e = nb.engine
         assert e.head_onload == (v == "1")
@@ -373,13 +373,13 @@ def test_head_onload_step_equals_materialised(cuda_dev, monkeypatch, kw):
 ])
 def test_tconv_fused_step_matches_materialised(cuda_dev, monkeypatch, kw):
     """Composite transposed-conv backward (default, levels 1-2: no fine tconv output
-    gradient) vs UNET_TCONV_FUSED=0 (dgrad into d:transConv, tconv dgrad / wgrad):
+    gradient) vs tconv_fused=0 (dgrad into d:transConv, tconv dgrad / wgrad):
     same loss sums and probabilities, every parameter gradient within bf16 rounding of
     the other path (the composed weights round once instead of twice)."""
     outs = []
-    monkeypatch.setenv("UNET_TCONV_FWD", "0")             # (the composite forward: next test)
     for v in ("0", "2"):
-        monkeypatch.setenv("UNET_TCONV_FUSED", v)
+        # (tconv_wa=0: the consumer's full weight gradient; the chained one: next test)
+        monkeypatch.setenv("UNET_ENGINE", "tconv_wa=0,tconv_fused=" + v)
         spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
         e = nb.engine
         assert sorted(e.tconv_fused) == ([] if v == "0" else ["transConv8", "transConv9"])
@@ -399,50 +399,42 @@ def test_tconv_fused_step_matches_materialised(cuda_dev, monkeypatch, kw):
     dict(batch_size=4, img_size=128, in_channels=4, loss="dice_bce"),
 ])
 def test_tconv_consumer_modes_step(cuda_dev, monkeypatch, kw):
-    """UNET_TCONV_FWD 0 (tconv + fine conv, full wgrad), 1 (default: the consumer's u-row
-    weight gradient from the slab sums, skip-only wgrad) and 2 (composite forward: conv{8,9}a
-    on the coarse grid, u never formed).  Mode 1 leaves the forward bit-identical; modes 1 / 2
-    round differently from mode 0 (u is never rounded to 16 bits on their u-row gradient /
-    forward paths), so each is held against the fp32 ATen step and must be as close to it as
-    mode 0 (per-gradient cosine distance at most 2x + 3e-4 of mode 0's)."""
+    """tconv_wa 0 (tconv + fine conv, full wgrad) and 1 (default: the consumer's u-row
+    weight gradient from the slab sums, skip-only wgrad).  The forward is bit-identical; mode 1
+    rounds differently from mode 0 (u is never rounded to 16 bits on its u-row gradient path),
+    so both are held against the fp32 ATen step and mode 1 must be as close to it as mode 0
+    (per-gradient cosine distance at most 2x + 3e-4 of mode 0's)."""
     outs = []
-    for v in ("0", "1", "2"):
-        monkeypatch.setenv("UNET_TCONV_FWD", v)
+    for v in ("0", "1"):
+        monkeypatch.setenv("UNET_ENGINE", "tconv_wa=" + v)
         spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
         e = nb.engine
-        fused = sorted(t for t, tf in e.tconv_fused.items() if "s2f" in tf)
-        assert fused == ([] if v != "2" else ["transConv8", "transConv9"])
         assert sorted(e._wa_chain_of.values()) == ([] if v == "0" else ["transConv8", "transConv9"])
-        assert all(t not in e.bufs for t in fused)
         nb.fwd_bwd(x, y, seed=91)
         if v == "0":
             tb.fwd_bwd(x, y, seed=91)
             ref = (tb.sums().cpu(), {k: ft.view(ft.grad, k).clone() for k, *_ in ft.entries})
         torch.cuda.synchronize()
         outs.append((nb.sums().cpu(), e.prob.clone(), {k: fn.view(fn.grad, k).clone() for k, *_ in fn.entries}))
-    (s0, p0, g0), (s1, p1, g1), (s2, p2, g2) = outs
+    (s0, p0, g0), (s1, p1, g1) = outs
     st, gt = ref
     assert torch.equal(s0, s1) and torch.equal(p0, p1)
-    assert ((s2 - s0).abs() / s0.abs().clamp_min(1.0)).max().item() < 5e-3, (s0, s2)
-    assert torch.allclose(s2[:3], st[:3], rtol=3e-2, atol=1.0), (s2, st)
-    assert (p2 - p0).abs().max().item() < 2e-2
     for k in g0:
         d0 = 1.0 - _cos(g0[k].float(), gt[k])
-        for g in (g1, g2):
-            d = 1.0 - _cos(g[k].float(), gt[k])
-            assert d <= 2.0 * d0 + 3e-4, (k, d0, d)
+        d = 1.0 - _cos(g1[k].float(), gt[k])
+        assert d <= 2.0 * d0 + 3e-4, (k, d0, d)
 
 
 @pytest.mark.parametrize("norm", ["batch", "group"])
 def test_tconv_fused_norm_step(cuda_dev, monkeypatch, norm):
     """Composite transposed-conv backward with BatchNorm / GroupNorm (the S2D data gradient
     carries the tconv input's dgrad-norm epilogue; the consumer's u-row weight gradient
-    from the slab sums) vs the materialised tconv backward (UNET_TCONV_FUSED=0): both held
+    from the slab sums) vs the materialised tconv backward (tconv_fused=0): both held
     against the fp32 ATen step, the composite at most 2x + 1e-3 the materialised path's
     per-gradient cosine distance."""
     outs = []
     for v in ("0", "2"):
-        monkeypatch.setenv("UNET_TCONV_FUSED", v)
+        monkeypatch.setenv("UNET_ENGINE", "tconv_fused=" + v)
         spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, batch_size=4, img_size=64, in_channels=4, norm=norm)
         e = nb.engine
         assert sorted(e.tconv_fused) == ([] if v == "0" else ["transConv8", "transConv9"])

@@ -122,7 +122,7 @@ def test_composite_tconv_weight_grads(cuda_dev, N, H, K, Cc, Cs, O, splits, win)
     torch.cuda.synchronize()
     assert rel_err(dwt, ref_wt.reshape(4, Cc, K)) < 1e-3
     assert rel_err(dbt, ref_bt) < 1e-3
-    # the consumer conv's weight gradient without u (composite forward): the u rows from
+    # the consumer conv's weight gradient without its u half: the u rows from
     # H / Bs through Wt, bt; the skip rows copied from their own gradient
     dwa = torch.full((3, 3, Cc + Cs, O), float("nan"), device=dev)
     skg = ref_wa[:, :, Cc:, :].contiguous()
@@ -133,31 +133,3 @@ def test_composite_tconv_weight_grads(cuda_dev, N, H, K, Cc, Cs, O, splits, win)
     assert rel_err(dwa, ref_wa) < 1e-3
     assert torch.equal(dwa[:, :, Cc:, :], skg)
 
-
-@pytest.mark.parametrize("N,H,K,Cc,Cs,O", [(2, 64, 64, 32, 32, 32), (2, 32, 128, 64, 64, 64),
-                                            (3, 16, 64, 32, 32, 32), (1, 128, 64, 32, 32, 32)])
-def test_composite_tconv_forward(cuda_dev, N, H, K, Cc, Cs, O):
-    """z = relu(conv3x3([tconv(b), skip]) + ba) as one coarse row-window conv (XF 5) over the
-    space-to-depth skip and b with composed weights + border bias tables -- u never formed."""
-    b, skip, wt, bt, wa, _ = _problem(cuda_dev, N, H, K, Cc, Cs, O, 13)
-    dev = cuda_dev
-    ba = torch.randn(O, device=dev) * 0.1
-    u = F.conv_transpose2d(nchw(b.float()), wt.permute(3, 2, 0, 1), bt, stride=2)
-    ref = nhwc(F.relu(F.conv2d(torch.cat([u, nchw(skip.float())], 1), wa.permute(3, 2, 0, 1), ba, padding=1)))
-    kpad = (9 * (4 * Cs + K) + 63) // 64 * 64
-    wf = torch.empty(4 * O, kpad, device=dev, dtype=torch.bfloat16)
-    btab = torch.empty(4, 4 * O, device=dev)
-    C().generic("s2f_compose", [ptr(wt.reshape(4, Cc, K).contiguous()), ptr(bt), ptr(wa.contiguous()), ptr(ba),
-                                ptr(wf), ptr(btab)], [Cc, K, O, Cc + Cs, kpad], [], stream())
-    out = torch.full((N, 2 * H, 2 * H, O), float("nan"), device=dev, dtype=torch.bfloat16)
-    bits = torch.zeros(N * 4 * H * H * O // 8, device=dev, dtype=torch.uint8)
-    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=4 * Cs, s2d=Cs, C2=K, src1=ptr(skip),
-                      src2=ptr(b), wgt=ptr(wf), bias=ptr(btab), Cout=4 * O, relu=1, dst1=ptr(out), s2f=O,
-                      relu_bits=ptr(bits)), stream())
-    torch.cuda.synchronize()
-    assert torch.isfinite(out.float()).all()
-    assert rel_err(out, ref) < 2e-2
-    # the border pixels carry the padding-corrected tconv bias
-    assert rel_err(out[:, [0, -1]], ref[:, [0, -1]]) < 2e-2
-    assert rel_err(out[:, :, [0, -1]], ref[:, :, [0, -1]]) < 2e-2
-    assert torch.equal(bits, pack_bits(out).reshape(-1))

@@ -29,18 +29,11 @@ def test_plan_construction_dry_run(kw, img, dtype):
     e = NativeUNet(spec, flat, 2, img, "cpu", bucket_bounds=b, dry_run=True, dtype=dtype)
     assert e.arena.dtype == e.adt and e.target.dtype == e.adt
     names = e.plan.names()
-    # composite transposed-conv forwards: their weights are composed first, the tconv
-    # itself never launches and its output u is never allocated
-    s2f = [t for t, tf in e.tconv_fused.items() if "s2f" in tf]
-    assert names[:len(s2f)] == ["fwd:compose:" + t for t in s2f]
-    assert names[len(s2f)] == "fwd:conv1a" and names[e.fwd_end - 1] == "fwd:Mask"
-    for t in s2f:
-        assert "fwd:" + t not in names and t not in e.bufs
-        assert "fwd:" + e.tconv_fused[t]["consumer"] in names
-    if kw.get("dims", 2) == 2 and kw.get("norm", "none") == "none" and not kw.get("use_upsampling"):
-        # default UNET_TCONV_FWD=1: the consumers' u-row weight gradients come from the chain
-        # rule (skip-only wgrad), the forward keeps the tconv (composite forward is mode 2)
-        assert s2f == [] and sorted(e._wa_chain_of.values()) == ["transConv8", "transConv9"]
+    assert names[0] == "fwd:conv1a" and names[e.fwd_end - 1] == "fwd:Mask"
+    if kw.get("dims", 2) == 2 and not kw.get("use_upsampling"):
+        # default tconv_wa=1: the consumers' u-row weight gradients come from the chain rule
+        # (skip-only wgrad); the forward keeps the tconv
+        assert sorted(e._wa_chain_of.values()) == ["transConv8", "transConv9"]
         for cons in e._wa_chain_of:
             assert names.index("chain:" + e._wa_chain_of[cons]) > names.index("wgrad:" + cons)
     # (head-on-load: the head backward only reduces the Mask gradients, on the side stream)
@@ -98,35 +91,40 @@ def test_bucket_plan_is_layer_aligned_and_covers_buffer():
     assert (flat.numel - b[-2]) * 4 / 2 ** 20 <= 8.0
 
 
-def test_composite_forward_plan(monkeypatch):
-    """UNET_TCONV_FWD=2: conv{8,9}a run as coarse composite forwards (u never allocated),
-    their weights composed first in the forward."""
-    from unet_distributed_amd.runtime.native_engine import NativeUNet
-    monkeypatch.setenv("UNET_TCONV_FWD", "2")
-    spec = UNetSpec(in_channels=4)
-    e = NativeUNet(spec, FlatParams(spec), 2, 64, "cpu", dry_run=True)
-    names = e.plan.names()
-    assert sorted(e._s2f_of.values()) == ["transConv8", "transConv9"]
-    assert names[:2] == ["fwd:compose:transConv8", "fwd:compose:transConv9"]
-    for t in ("transConv8", "transConv9"):
-        assert "fwd:" + t not in names and t not in e.bufs
-
-
-def test_engine_env_knobs_are_few():
-    """The executor's behaviour is fixed by its measured defaults: only the A/B knobs
-    the GPU tests flip remain environment-driven (round-2 review: <= 12)."""
+def test_engine_reads_one_env_var(monkeypatch):
+    """The executor's behaviour is fixed by its measured defaults (ENGINE_DEFAULTS); the one
+    environment variable it reads, UNET_ENGINE, overrides them for A/B runs, and unknown or
+    removed options (the composite forward, level-3 composite backward) are errors."""
     import re
     from unet_distributed_amd.runtime import native_engine
     src = open(native_engine.__file__).read()
-    knobs = set(re.findall(r'os\.environ\.get\("(UNET_[A-Z0-9_]+)"', src))
-    assert knobs <= {"UNET_DUAL_STREAM", "UNET_CONV_TILE", "UNET_FWD_STREAMS", "UNET_HEAD_FUSE",
-                     "UNET_HEAD_ONLOAD", "UNET_TCONV_FUSED", "UNET_TCONV_FWD"}, knobs
+    assert set(re.findall(r'os\.environ\.get\("([A-Z0-9_]+)"', src)) == {"UNET_ENGINE"}
+    assert "os.getenv" not in src and "os.environ[" not in src
+    assert native_engine.engine_options() == native_engine.ENGINE_DEFAULTS
+    monkeypatch.setenv("UNET_ENGINE", "fwd_streams=1,head_fuse=0")
+    o = native_engine.engine_options(dict(dual_stream=0))
+    assert (o["fwd_streams"], o["head_fuse"], o["dual_stream"], o["tconv_fused"]) == (1, 0, 0, 2)
+    for bad in ("tconv_fwd=2", "tconv_fused=3"):
+        monkeypatch.setenv("UNET_ENGINE", bad)
+        with pytest.raises(ValueError):
+            native_engine.engine_options()
 
 
-def test_fused_head_plan(monkeypatch):
+def test_head_onload_plan_allocates_no_head_input_gradient():
+    """Head-on-load: nothing reads or writes the head input's gradient, so it is not
+    allocated (1 GiB at b1024); the materialised path keeps it."""
+    from unet_distributed_amd.runtime.native_engine import NativeUNet
+    spec = UNetSpec(in_channels=4)
+    e = NativeUNet(spec, FlatParams(spec), 2, 64, "cpu", dry_run=True)
+    assert e.head_onload and "d:" + e.head_in not in e.bufs
+    e0 = NativeUNet(spec, FlatParams(spec), 2, 64, "cpu", dry_run=True, opts=dict(head_onload=0))
+    assert not e0.head_onload and "d:" + e0.head_in in e0.bufs
+
+
+def test_fused_head_plan():
     """The Mask head rides on the 32-channel row-window forward of its input conv
-    (fwd:Mask is then only the partial reduction); norm layers or UNET_HEAD_FUSE=0
-    keep the separate head launch."""
+    (fwd:Mask is then only the partial reduction); norm layers or head_fuse=0 keep the
+    separate head launch."""
     from unet_distributed_amd.runtime.native_engine import NativeUNet
     for kw, img, fused in [(dict(in_channels=4), 64, True), (dict(in_channels=4, dims=3), 32, True),
                            (dict(in_channels=4, norm="batch"), 64, False)]:
@@ -134,7 +132,6 @@ def test_fused_head_plan(monkeypatch):
         e = NativeUNet(spec, FlatParams(spec), 2, img, "cpu", dry_run=True)
         assert bool(e._head_fused_blocks) == fused, kw
         assert e.plan.names()[e.fwd_end - 1] == "fwd:Mask"
-    monkeypatch.setenv("UNET_HEAD_FUSE", "0")
     spec = UNetSpec(in_channels=4)
-    e = NativeUNet(spec, FlatParams(spec), 2, 64, "cpu", dry_run=True)
+    e = NativeUNet(spec, FlatParams(spec), 2, 64, "cpu", dry_run=True, opts=dict(head_fuse=0))
     assert e._head_fused_blocks == 0

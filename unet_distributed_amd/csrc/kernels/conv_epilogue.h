@@ -87,18 +87,12 @@ struct StripTiles {
 // SEGW == 0: tile pixel ml is output pixel m0 + ml.
 // stat_row: this tile's row of p.stats (modes 3 / 4).  TROW > 0: the tile is BM / TROW
 // whole rows of TROW pixels (row-window kernels; enables the fused max-pool).
-// S2F (EPI_FWD, TROW = the coarse row width): composite transposed-conv forward
-// (conv_params.h s2f) -- channel n = (phase P, o), P = n / s2f, goes to fine pixel
-// (2 row + (P >> 1), 2 col + (P & 1)) of s2f channels; p.bias holds [4][Cout]: the bias
-// with every tap's tconv-bias term, and the row-edge / column-edge / corner terms the
-// zero padding removes at the image border (subtracted there, before the ReLU).
 template <int BM, int BN, int WM, int WN, int TM, int TN, int NTHR, int EPI = EPI_GENERIC,
-          class MapM = LinearTiles<WM>, int SEGW = 0, int TROW = 0, bool S2F = false>
+          class MapM = LinearTiles<WM>, int SEGW = 0, int TROW = 0>
 __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc)[TM][TN], char* smem,
                                               const int m0, const int n0, const int M, const int wm,
                                               const int wn, const int lane, const int tid,
                                               const int pitch = 0, const int col0 = 0, const int stat_row = 0) {
-  static_assert(!S2F || (EPI == EPI_FWD && TROW > 0 && SEGW == 0), "composite forward: row-window EPI_FWD");
   auto qof = [&](int ml) -> int {
     if constexpr (SEGW > 0) return (m0 + ml / SEGW) * pitch + col0 + (ml % SEGW);
     else return m0 + ml;
@@ -134,45 +128,11 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       // bias + ReLU: packed fp32 adds, the ReLU on the packed 16-bit pair (relu2h; the
       // same bits as clamping before the rounding)
       const f32x2 b01 = {bsv[0], bsv[1]}, b23 = {bsv[2], bsv[3]};
-      f32x2 er01, er23, ec01, ec23, ex01, ex23;
-      int eh = 0, ew = 0;
-      if constexpr (S2F) {
-        const float* bt = p.bias + n;
-        const int C = p.Cout;
-        er01 = (f32x2){bt[C], bt[C + 1]};
-        er23 = (f32x2){bt[C + 2], bt[C + 3]};
-        ec01 = (f32x2){bt[2 * C], bt[2 * C + 1]};
-        ec23 = (f32x2){bt[2 * C + 2], bt[2 * C + 3]};
-        ex01 = (f32x2){bt[3 * C], bt[3 * C + 1]};
-        ex23 = (f32x2){bt[3 * C + 2], bt[3 * C + 3]};
-        const int P = n / p.s2f;                        // (4 channels never straddle a phase)
-        eh = (P >> 1) ? p.OH - 1 : 0;                   // the coarse row / column whose fine
-        ew = (P & 1) ? TROW - 1 : 0;                    // pixels of this phase touch the border
-      }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int ml = MapM::base(wm, i) + (lane & 15);
         f32x2 a01 = (f32x2){acc[i][j][0], acc[i][j][1]} + b01;
         f32x2 a23 = (f32x2){acc[i][j][2], acc[i][j][3]} + b23;
-        if constexpr (S2F) {
-          const int q = qof(ml);
-          const int g = q / TROW, w = q - g * TROW;
-          const bool re = (g % p.OH) == eh, ce = w == ew;
-          if (re || ce) {
-            if (re) {
-              a01 -= er01;
-              a23 -= er23;
-            }
-            if (ce) {
-              a01 -= ec01;
-              a23 -= ec23;
-            }
-            if (re && ce) {
-              a01 += ex01;
-              a23 += ex23;
-            }
-          }
-        }
         u32x2 pk;
         pk[0] = relu2h(pack2h(a01[0], a01[1]));
         pk[1] = relu2h(pack2h(a23[0], a23[1]));
@@ -427,7 +387,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
   // 1x1 head weights (the same bf16-rounded activations head.hip::head_fwd_kernel
   // reads) and combine by two lane swaps; the fp32 logit is stored per pixel -- the
   // 268 MB re-read of a separate head launch becomes a 17 MB one.
-  constexpr bool kHeadable = EPI == EPI_FWD && BN == 32 && NTHR % CPR == 0 && !S2F;
+  constexpr bool kHeadable = EPI == EPI_FWD && BN == 32 && NTHR % CPR == 0;
   const bool kHead = kHeadable && p.head_w != nullptr;
   float hw[8], hb = 0.f;
   constexpr int HIT = kHeadable ? NCHUNK / NTHR : 1;     // chunk iterations per thread
@@ -462,13 +422,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     h16* dst;
     const void* mk;
     bool mbit = false;
-    if (S2F) {
-      const int P = n / p.s2f, co = n - P * p.s2f;
-      const int g = q / TROW, w = q - g * TROW;
-      off = ((size_t)(2 * g + (P >> 1)) * (2 * TROW) + 2 * w + (P & 1)) * p.s2f + co;
-      dst = (h16*)p.dst1;
-      mk = nullptr;
-    } else if (EPI == EPI_FWD || EPI == EPI_STATS) {
+    if (EPI == EPI_FWD || EPI == EPI_STATS) {
       off = (size_t)q * p.Cout + n;
       dst = (h16*)p.dst1;
       mk = nullptr;
@@ -543,7 +497,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       }
     }
   }
-  if constexpr (EPI == EPI_FWD && !S2F && TROW > 0 && (BM / TROW) % 2 == 0 && TROW % 2 == 0) {
+  if constexpr (EPI == EPI_FWD && TROW > 0 && (BM / TROW) % 2 == 0 && TROW % 2 == 0) {
     if (p.pool_dst) {
       // 2x2 max-pool of the tile's complete row pairs (a window starts on an even row
       // and holds an even number of rows): max + first-argmax code per channel, the

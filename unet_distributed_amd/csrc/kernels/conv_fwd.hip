@@ -867,7 +867,7 @@ static bool img8_eligible(const ConvFwdParams& p) {
          p.KW == 3 && p.stride == 1 && p.pad == 1 && p.up1 == 1 && !p.shuffle && p.C1 > 0 && (p.C1 % 32) == 0 &&
          (p.C2 % 32) == 0 && (p.Cout % 64) == 0 && !(p.nz && (p.C2 || p.ncs)) &&
          (ep == EPI_FWD || ep == EPI_DGRAD || ep == EPI_GENERIC || ep == EPI_STATS || ep == EPI_DGRAD_NORM) &&
-         !p.route_gy && !p.pool_dst && !p.head_w && !p.xform && !p.hg.prob && !p.s2d && !p.s2f;
+         !p.route_gy && !p.pool_dst && !p.head_w && !p.xform && !p.hg.prob && !p.s2d;
 }
 
 // Fills the tap tables and Kpad; returns nullptr on success or a message describing
@@ -910,13 +910,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
                     p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) || conv_epi_mode(p) != EPI_DGRAD ||
                     p.route_gy || (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12)))
     return "conv_fwd: head-on-load needs a 2D 32-channel row-window data gradient";
-  if (p.s2f && (p.s2f % 16 || !p.s2d || p.s2d % 32 || p.C1 != 4 * p.s2d || p.C2 <= 0 || !p.src2 ||
-                p.Cout != 4 * p.s2f || p.D1 != p.Cout || !p.bias || !p.relu || conv_epi_mode(p) != EPI_FWD ||
-                p.xform || p.hg.prob || p.route_gy || p.pool_dst || p.head_w || p.stats || p.KD != 1 || p.OD != 1 ||
-                p.OW > 128 || !win_eligible(p) || (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12)))
-    return "conv_fwd: composite transposed-conv forward needs a 2D two-source ReLU row-window forward "
-           "(C1 = 4 s2d, Cout = 4 s2f, bias tables)";
-  if (p.s2d && !p.s2f && (p.s2d % 32 || p.C1 != 4 * p.s2d || p.C2 || p.xform || p.hg.prob || p.route_gy || p.KD != 1 ||
+  if (p.s2d && (p.s2d % 32 || p.C1 != 4 * p.s2d || p.C2 || p.xform || p.hg.prob || p.route_gy || p.KD != 1 ||
                 p.OD != 1 || p.OW > 128 || !win_eligible(p) ||
                 (conv_epi_mode(p) != EPI_DGRAD && conv_epi_mode(p) != EPI_DGRAD_NORM) ||
                 (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12)))

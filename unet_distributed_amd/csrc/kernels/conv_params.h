@@ -118,14 +118,6 @@ struct ConvFwdParams {
   // lies in one phase group (a, b) whose 3x3 taps are structurally zero outside the 2x2
   // support dh in {1 - a, 2 - a}, dw in {1 - b, 2 - b}: those MFMAs are skipped.
   int s2d;
-  // Composite transposed-conv FORWARD (2D row-window, conv_win.h XF 5): the decoder conv
-  // z = relu(conv3x3([u, skip]) + ba) with u = tconv(b) runs on the COARSE grid with
-  // s2f = O > 0 fine output channels per phase: src1 = the fine skip read space-to-depth
-  // (s2d = its channels, C1 = 4 s2d), src2 = the coarse tconv input b (C2 channels), Cout =
-  // 4 O output channels (phase (a, b), o) stored to the fine pixel (2h + a, 2w + b) -- u is
-  // never formed.  wgt: tconv_fused.hip::s2f_compose; bias: [4][Cout] {full bias, row-edge,
-  // column-edge, corner corrections} of the tconv bias seen through the zero padding.
-  int s2f;
   // filled by conv_fwd_prepare (host): K padded to 64, per-tap pixel deltas / offsets
   int Kpad;
   int tap_delta[27];

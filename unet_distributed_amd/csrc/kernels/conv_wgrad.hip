@@ -1540,9 +1540,12 @@ const char* wgrad_check(const WgradParams& p) {
                        (p.xcs != 0 && p.xcs != p.Nc) || (p.xcs && p.QH % (256 / p.QW))))
     return "wgrad: B transform (dz on load) needs the first-layer window wgrad";
   if (p.upA != 1) return "wgrad: upA must be 1 (nearest upsampling is materialised)";
+  // (the head-on-load instantiation is the 2D full-row window, launch_wgrad_win_g<W, 1,
+  // WGEO_2D>, on the 16..128-wide rows the executor plans it for)
   if (p.hg.prob && (!p.hg.t || !p.hg.sums || !p.hg.w || !p.hg.bits || !wgrad_win_eligible(p) || p.Nc != 32 ||
-                    p.M2 != 0 || p.KD != 1 || p.QD != 1 || p.QW > 128 || p.xform))
-    return "wgrad: head-on-load B needs a 2D single-source row-window wgrad with 32 output channels";
+                    p.M2 != 0 || p.KD != 1 || p.QD != 1 || p.QW < 16 || p.QW > 128 || p.xform))
+    return "wgrad: head-on-load B needs a 2D single-source row-window wgrad with 32 output channels on rows "
+           "16..128 wide";
   // 32-bit buffer offsets: the window kernels count them from each window's rows (one
   // image must stay below 2 GiB), the tiled kernel from the tensor starts
   {

@@ -85,16 +85,12 @@ constexpr int NTHR = 256;
 // transformed operand go to xout); 3: head-on-load, the halo image of dY (32 channels)
 // is formed from the head's per-pixel probability, target and ReLU bits (p.hg,
 // head_grad.h) instead of being read from memory; 4: space-to-depth source (p.s2d: the
-// DMA gathers the fine pixels of each coarse slot, structurally zero taps skipped);
-// 5: composite transposed-conv forward (p.s2f, conv_params.h): src1 = the fine skip read
-// space-to-depth, src2 = the coarse tconv input, per-output-phase tap masks, outputs
-// stored to their fine pixels by the epilogue.
+// DMA gathers the fine pixels of each coarse slot, structurally zero taps skipped).
 template <int W, int BN, int BM, bool CONCAT, int EPI, int GEO, int XF = 0>
 __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   static_assert(BN == 32 || BN == 64, "row-window tile is 32 or 64 output channels wide");
-  static_assert(XF == 0 || ((XF == 1 || XF == 3 || XF == 4) && GEO == GEO_2D && !CONCAT) ||
-                    (XF == 5 && GEO == GEO_2D && CONCAT && EPI == EPI_FWD),
-                "operand transform: 2D single-source windows (XF 5: the two-source composite forward)");
+  static_assert(XF == 0 || ((XF == 1 || XF == 3 || XF == 4) && GEO == GEO_2D && !CONCAT),
+                "operand transform: 2D single-source windows");
   constexpr int R = BM / W, HR = R + 2;
   // halo row pitch in 64-byte pixel slots: W + 2 columns rounded up to a multiple of 4
   // (every row starts on a 256-byte bank row); the DMA fills the image as one linear
@@ -149,7 +145,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   // exceed 2 GiB (conv_fwd_prepare bounds one image)
   const int grow0 = (g0 / (D * H)) * (D * H);
   const size_t img_px = (size_t)grow0 * Wf;
-  const char* s1b = (const char*)p.src1 + img_px * ((XF == 4 || XF == 5) ? 4 * p.s2d : p.C1) * 2;
+  const char* s1b = (const char*)p.src1 + img_px * (XF == 4 ? 4 * p.s2d : p.C1) * 2;
   const char* s2b = p.src2 ? (const char*)p.src2 + img_px * p.C2 * 2 : s1b;
   const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)s1b, (short)0, OOB, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc((void*)s2b, (short)0, OOB, 0x00020000);
@@ -191,9 +187,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   // held in registers and every halo-row fragment feeds up to three output rows
   // tmask: taps (bit 3 dh + dw) of this chunk that are not structurally zero (XF 4);
   // a compile-time 0x1ff everywhere else, so the tests fold away
-  // jm (XF 5): per output-channel tile j, bits 9 j + tap -- the taps of this chunk that
-  // are not structurally zero for that tile's output phase (~0 everywhere else)
-  auto chunk_mfmas = [&](const uint32_t tmask, const uint64_t jm) {
+  auto chunk_mfmas = [&](const uint32_t tmask) {
 #pragma unroll
     for (int dw = 0; dw < 3; ++dw) {
       if (!((tmask >> dw) & 0x49u)) continue;     // no valid tap in this column
@@ -213,10 +207,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
             if (ri < 0 || ri >= RW) continue;
             if (!((tmask >> (3 * dh + dw)) & 1u)) continue;
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              if (XF == 5 && !((jm >> (9 * j + 3 * dh + dw)) & 1u)) continue;
-              acc[ri * TC + ci][j] = mfma16(wf[dh][j], xf, acc[ri * TC + ci][j]);
-            }
+            for (int j = 0; j < TN; ++j) acc[ri * TC + ci][j] = mfma16(wf[dh][j], xf, acc[ri * TC + ci][j]);
           }
         }
       }
@@ -271,7 +262,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
         }
       }
       __syncthreads();
-      chunk_mfmas(0x1ffu, ~0ull);
+      chunk_mfmas(0x1ffu);
   };
   if constexpr (GEO == GEO_3D) {
     // depth taps whose input slice is padding contribute nothing: skip them
@@ -307,33 +298,14 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
     const size_t xsample = XF == 1 ? (size_t)(g0 / H) * p.xcs : 0;   // the window's sample (GroupNorm rows)
     for (int kc = 0; kc < nchunks; ++kc) {
       const bool from1 = !CONCAT || (kc << 5) < p.C1;
-      // space-to-depth gathered chunk: every chunk of XF 4, the src1 (fine skip) chunks of XF 5
-      const bool s2 = XF == 4 || (XF == 5 && from1);
+      // space-to-depth gathered chunk: every chunk of XF 4
+      constexpr bool s2 = XF == 4;
       const int C = s2 ? p.s2d : (from1 ? p.C1 : p.C2);
       // XF 4: chunk kc = phase group (sa, sb) of the space-to-depth image, fine channels
       // cb .. cb + 31; its valid taps dh in {1 - sa, 2 - sa}, dw in {1 - sb, 2 - sb}
       const int sgrp = s2 ? kc / (p.s2d >> 5) : 0, sa = sgrp >> 1, sb = sgrp & 1;
       const int cb = s2 ? (kc << 5) - sgrp * p.s2d : (from1 ? (kc << 5) : (kc << 5) - p.C1);
       const uint32_t s2d_taps = 0x1bu << (3 * (1 - sa) + (1 - sb));   // the 2 x 2 tap block
-      // XF 5: output tile j is fine phase (a, b) = P >> 1, P & 1 (P = channel / s2f); the
-      // fine row 2h + a + dh - 1 of tap dh lies in coarse row h + Th - 1 of phase
-      // a' = (a + dh - 1) & 1, so a skip phase plane a' feeds coarse rows Th = {1} when
-      // a' == a, else {0, 1} (a = 0) / {1, 2} (a = 1) -- as do the coarse b chunks
-      uint32_t tm5 = 0x1ffu;
-      uint64_t jm = ~0ull;
-      if constexpr (XF == 5) {
-        tm5 = 0;
-        jm = 0;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int P = (n0 + 16 * j) / p.s2f, a = P >> 1, b = P & 1;
-          const uint32_t rs = (from1 && a == sa) ? 2u : (a ? 6u : 3u);
-          const uint32_t cs = (from1 && b == sb) ? 2u : (b ? 6u : 3u);
-          const uint32_t m = ((rs & 1u) ? cs : 0u) | ((rs & 2u) ? cs << 3 : 0u) | ((rs & 4u) ? cs << 6 : 0u);
-          jm |= (uint64_t)m << (9 * j);
-          tm5 |= m;
-        }
-      }
       if (kc) __syncthreads();
       {
         const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
@@ -368,9 +340,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
 #pragma unroll
         for (int q = 0; q < (WI + 3) / 4; ++q) {
           const int k = wave + 4 * q;
-          // (XF 5: taps that are structurally zero for every phase of the tile are not
-          // staged -- their LDS rows are read but feed no MFMA)
-          if (k < WI && (XF != 5 || ((tm5 >> (k / (BN / 16))) & 1u))) {
+          if (k < WI) {
             const int tap = k / (BN / 16), nb = (k % (BN / 16)) * 16;
             const int off = ((n0 + nb) * p.Kpad + tap * Cin) * 2 + wl;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024),
@@ -447,7 +417,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
         }
         __syncthreads();
       }
-      chunk_mfmas(XF == 4 ? s2d_taps : tm5, jm);
+      chunk_mfmas(XF == 4 ? s2d_taps : 0x1ffu);
     }
   }
   __syncthreads();
@@ -455,8 +425,8 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
     conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, W, W>(p, acc, smem, g0, n0, M, wave, 0, lane, tid, Wf,
                                                                  col0, tm);
   else if constexpr (GEO == GEO_2D)
-    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W, XF == 5>(p, acc, smem, g0 * W, n0, M, wave, 0, lane,
-                                                                          tid, 0, 0, tm);
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0, 0,
+                                                                  tm);
   else
     conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0, 0, tm);
 }
@@ -529,26 +499,6 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
       HG_CASE(64)
       HG_CASE(128)
 #undef HG_CASE
-      default:
-        return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
-  if (p.s2f) {                          // composite transposed-conv forward (conv_fwd_prepare checks the shape)
-    if (epi != EPI_FWD || geo != GEO_2D || !cc) return hipErrorInvalidValue;
-    switch (W) {
-#define S2F_CASE(WW)                                                                                      \
-  case WW:                                                                                                \
-    if constexpr (win_tile_built<BN, BM>(WW))                                                             \
-      hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, true, EPI_FWD, GEO_2D, 5>), dim3(grid), dim3(NTHR), 0, s, p); \
-    else                                                                                                  \
-      return hipErrorInvalidValue;                                                                        \
-    break;
-      S2F_CASE(16)
-      S2F_CASE(32)
-      S2F_CASE(64)
-      S2F_CASE(128)
-#undef S2F_CASE
       default:
         return hipErrorInvalidValue;
     }

@@ -107,81 +107,6 @@ __global__ void __launch_bounds__(256) tconv_chain_kernel(const float* __restric
   if (threadIdx.x == 0) dbt[c] = red[0];
 }
 
-// Composite FORWARD (conv_win.h XF 5): z(2h + a, 2w + b) = relu(sum_{Th,Tw} [S2D(skip) | b](h + Th - 1,
-// w + Tw - 1) . Wf[P = 2a + b][Th][Tw] + bias(P, border)) on the coarse grid.  Row n = P O + o of
-// the row-window layout [4 O][Kpad], K index = (3 Th + Tw) Cin + ci, Cin = 4 Cs + K:
-//   skip plane g = (a', b'), channel c:  Wa[dh][dw][C + c][o],  dh = 2 Th + a' - a - 1 (0..2, else 0)
-//   coarse b channel k:  sum over the fine taps (dh, dw) of coarse tap (Th, Tw) -- fine offset
-//       f = a + dh - 1 = 2 (Th - 1) + a' -- of sum_c Wa[dh][dw][c][o] Wt[2 a' + b'][c][k]
-// Bias tables btab[4][4 O]: the tconv bias reaches z through every fine tap whose u pixel is
-// inside the image, V[dh][dw][o] = sum_c Wa[dh][dw][c][o] bt[c]; full = ba + sum V, and at the
-// border (fine row 0 for a = 0, last row for a = 1; likewise columns) the epilogue subtracts
-// the missing tap row / column sums and adds back their corner.
-__global__ void __launch_bounds__(256) s2f_compose_kernel(const float* __restrict__ wt, const float* __restrict__ bt,
-                                                          const float* __restrict__ wa, const float* __restrict__ ba,
-                                                          int C, int K, int O, int Ca, int Kpad, int nw,
-                                                          h16* __restrict__ out, float* __restrict__ btab) {
-  const int Cs = Ca - C, Cin = 4 * Cs + K, NO = 4 * O;
-  if ((int)blockIdx.x >= nw) {
-    const int n = (blockIdx.x - nw) * 256 + threadIdx.x;
-    if (n >= NO) return;
-    const int P = n / O, o = n - P * O, dhe = (P >> 1) ? 2 : 0, dwe = (P & 1) ? 2 : 0;
-    float V[3][3], full = ba[o];
-#pragma unroll
-    for (int dh = 0; dh < 3; ++dh)
-#pragma unroll
-      for (int dw = 0; dw < 3; ++dw) {
-        const float* wap = wa + (size_t)(dh * 3 + dw) * Ca * O + o;
-        float acc = 0.f;
-        for (int c = 0; c < C; ++c) acc = fmaf(wap[(size_t)c * O], bt[c], acc);
-        V[dh][dw] = acc;
-        full += acc;
-      }
-    float er = 0.f, ec = 0.f;
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      er += V[dhe][t];
-      ec += V[t][dwe];
-    }
-    btab[n] = full;
-    btab[NO + n] = er;
-    btab[2 * NO + n] = ec;
-    btab[3 * NO + n] = V[dhe][dwe];
-    return;
-  }
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= NO * Kpad) return;
-  const int n = idx / Kpad, kk = idx - n * Kpad;
-  const int P = n / O, o = n - P * O, a = P >> 1, b = P & 1;
-  float acc = 0.f;
-  if (kk < 9 * Cin) {
-    const int T = kk / Cin, ci = kk - T * Cin, Th = T / 3, Tw = T - 3 * Th;
-    if (ci < 4 * Cs) {
-      const int g = ci / Cs, c = ci - g * Cs;
-      const int dh = 2 * Th + (g >> 1) - a - 1, dw = 2 * Tw + (g & 1) - b - 1;
-      if (dh >= 0 && dh <= 2 && dw >= 0 && dw <= 2) acc = wa[((size_t)(dh * 3 + dw) * Ca + C + c) * O + o];
-    } else {
-      const int k = ci - 4 * Cs;
-#pragma unroll
-      for (int dh = 0; dh < 3; ++dh) {
-        const int fh = a + dh - 1;                      // = 2 (Th - 1) + a'
-        if ((fh >> 1) != Th - 1) continue;
-        const int ap = fh & 1;
-#pragma unroll
-        for (int dw = 0; dw < 3; ++dw) {
-          const int fw = b + dw - 1;
-          if ((fw >> 1) != Tw - 1) continue;
-          const int bp = fw & 1;
-          const float* wap = wa + (size_t)(dh * 3 + dw) * Ca * O + o;
-          const float* wtp = wt + (size_t)(2 * ap + bp) * C * K + k;
-          for (int c = 0; c < C; ++c) acc = fmaf(wap[(size_t)c * O], wtp[(size_t)c * K], acc);
-        }
-      }
-    }
-  }
-  out[idx] = f2h(acc);
-}
-
 // Weight gradient of the consumer conv when u was never formed (composite forward):
 // dWa[dh][dw][c][o] (HWIO) = sum_{a,b} sum_k Wt[2a + b][c][k] H[a - dh + 2][b - dw + 2][o][k]
 //                          + bt[c] Bs[a - dh + 2][b - dw + 2][o]       for the u rows c < C,
@@ -242,15 +167,6 @@ hipError_t tconv_chain_launch(const float* Hs, const float* bs, const float* wa,
     hipLaunchKernelGGL(tconv_chain_wa_kernel, dim3((n + 15) / 16), dim3(256), 0, s, Hs, bs, wt, bt, skg, C, K, O,
                        Ca, dwa);
   }
-  return hipGetLastError();
-}
-
-hipError_t s2f_compose_launch(const float* wt, const float* bt, const float* wa, const float* ba, int C, int K, int O,
-                              int Ca, int Kpad, void* out, float* btab, hipStream_t s) {
-  const int nw = (4 * O * Kpad + 255) / 256;
-  const int nb = (4 * O + 255) / 256;
-  hipLaunchKernelGGL(s2f_compose_kernel, dim3(nw + nb), dim3(256), 0, s, wt, bt, wa, ba, C, K, O, Ca, Kpad, nw,
-                     (h16*)out, btab);
   return hipGetLastError();
 }
 

@@ -129,7 +129,6 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.xc = (const float*)getp(d, "xc");
   p.xz = getp(d, "xz");
   p.s2d = get<int>(d, "s2d", 0);
-  p.s2f = get<int>(d, "s2f", 0);
   p.xout = const_cast<void*>(getp(d, "xout"));
   p.tile = get<int>(d, "tile", 0);
   p.head_w = (const float*)getp(d, "head_w");
@@ -219,7 +218,6 @@ WgradParams wgrad_params(const py::dict& d) {
   X(norm_bwd_apply_launch) \
   X(tconv_compose_launch) \
   X(tconv_chain_launch) \
-  X(s2f_compose_launch) \
   X(adam_pack_launch)
 
 struct KernelApi {
@@ -367,20 +365,6 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     return [=](hipStream_t s) {
       return A->tconv_chain_launch(hs, bs, wa, C, K, O, Ca, dwt, dbt, wt, bt, skg, dwa, s);
     };
-  }
-  if (kind == "s2f_compose") {
-    // ptrs: Wt master [4][C][K], bt [C], Wa master [3][3][Ca][O], ba [O], out bf16 [4 O][Kpad], btab [4][4 O]
-    // ints: C, K, O, Ca, Kpad
-    need(6, 5, 0);
-    const float *wt = (const float*)vp(0), *bt = (const float*)vp(1), *wa = (const float*)vp(2),
-                *ba = (const float*)vp(3);
-    void* out = vp(4);
-    float* btab = (float*)vp(5);
-    int C = I[0], K = I[1], O = I[2], Ca = I[3], kp = I[4];
-    check_msg(tconv_fused_check(C, K, O, Ca));
-    if ((Ca - C) % 32 || (Ca - C) <= 0 || kp < 9 * (4 * (Ca - C) + K) || kp % 64)
-      throw std::invalid_argument("s2f_compose: skip channels must be a positive multiple of 32, Kpad >= 9 Cin");
-    return [=](hipStream_t s) { return A->s2f_compose_launch(wt, bt, wa, ba, C, K, O, Ca, kp, out, btab, s); };
   }
   if (kind == "multi_reduce") {
     // ptrs: job table (device, ReduceJob[njobs])   ints: njobs, total1, total2

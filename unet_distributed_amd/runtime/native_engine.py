@@ -49,14 +49,44 @@ def _r64(k: int) -> int:
     return (k + 63) // 64 * 64
 
 
+# Executor options, each fixed at its measured default (profiles/r*_bench_history.md);
+# UNET_ENGINE="key=value,..." overrides them for same-box A/B runs, and tests pass
+# ``opts`` to NativeUNet directly.  The only environment variable the executor reads.
+#   dual_stream  weight-gradient launches on a side stream during the backward (1)
+#   fwd_streams  training forward as two half-batch chunks on two streams (2)
+#   head_fuse    Mask head in the epilogue of its input conv's forward (1)
+#   head_onload  the head input's gradient formed on load by its consumers (1)
+#   tconv_fused  deepest fine level whose transposed conv runs the composite backward (2; 0 off)
+#   tconv_wa     the consumer conv's u-row weight gradient from the composite backward's
+#                slab sums (1; 0: full weight gradient over u)
+ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1)
+
+
+def engine_options(overrides: Optional[Dict[str, int]] = None) -> Dict[str, int]:
+    opts = dict(ENGINE_DEFAULTS)
+    for kv in filter(None, os.environ.get("UNET_ENGINE", "").split(",")):
+        k, v = kv.split("=")
+        if k.strip() not in opts:
+            raise ValueError("UNET_ENGINE: unknown option %r (known: %s)" % (k, ", ".join(opts)))
+        opts[k.strip()] = int(v)
+    for k, v in (overrides or {}).items():
+        if k not in opts:
+            raise ValueError("engine option %r unknown (known: %s)" % (k, ", ".join(opts)))
+        opts[k] = int(v)
+    if opts["tconv_fused"] not in (0, 1, 2):
+        raise ValueError("tconv_fused must be 0..2 (level 3 measured -2.4 %% / +0.2 %%: removed)")
+    return opts
+
+
 class NativeUNet:
     """Plans and runs forward + backward of one UNet micro-batch on the GPU."""
 
     def __init__(self, spec: UNetSpec, flat: FlatParams, batch: int, img: int,
                  device, loss: str = "dice", bce_weight: float = 1.0,
                  bucket_bounds: Optional[Sequence[int]] = None, eval_dropout: bool = False,
-                 dry_run: bool = False, dtype: str = "bf16"):
+                 dry_run: bool = False, dtype: str = "bf16", opts: Optional[Dict[str, int]] = None):
         self.C = native.require()
+        self.opts = engine_options(opts)
         if spec.norm not in ("none", "batch", "group"):
             raise NotImplementedError("native executor: norm=%s" % spec.norm)
         if spec.n_cl_out != 1:
@@ -66,11 +96,11 @@ class NativeUNet:
         self.graphs = None      # HIP-graph cache (enable_graphs)
         # Weight-gradient launches (wgrad / bias colsum / split-K reduce) are off the
         # backward critical path (the dgrad chain): run them on a side stream so they
-        # overlap the memory-bound dgrads (UNET_DUAL_STREAM=0 disables; measured
+        # overlap the memory-bound dgrads (option dual_stream=0 disables; measured
         # 5.09 -> 4.83 ms per backward at b256, scripts/dual_stream_probe.py).  HIP graph
         # replay serialises parallel branches on this stack, so the dual-stream
         # backward is launched eagerly even in HIP-graph mode.
-        self.dual_stream = os.environ.get("UNET_DUAL_STREAM", "1") != "0"
+        self.dual_stream = bool(self.opts["dual_stream"])
         self._side = None
         self._groups: Dict[tuple, list] = {}
         # 16-bit element type of activations, gradients w.r.t. activations and the
@@ -292,10 +322,10 @@ class NativeUNet:
         # input conv -- form it from the probability, target and the head input's ReLU bits
         # instead of reading a materialised 32-channel dY; the head backward only reduces
         # the Mask weight / bias gradients (on the side stream).  2D norm-free model with
-        # a 32-channel head input on 16..128-wide rows (UNET_HEAD_ONLOAD=0: materialised).
+        # a 32-channel head input on 16..128-wide rows (option head_onload=0: materialised).
         self.head_onload = (spec.norm == "none" and self.dims == 2 and self.tinfo[self.head_in][1] == 32
                             and self.img in (16, 32, 64, 128) and self.wgrad_win >= 0
-                            and os.environ.get("UNET_HEAD_ONLOAD", "1") != "0")
+                            and bool(self.opts["head_onload"]))
         if spec.norm == "none":
             for l in spec.layers:
                 if l.kind == "conv" and (l.name != self.head_in or self.head_onload):
@@ -313,7 +343,12 @@ class NativeUNet:
         for name, (lvl, ch, _, _) in list(self.tinfo.items()):
             if name == "x" or name in self.tconv_fused:
                 continue            # (a fused transposed conv's output gradient is never formed)
+            if name == self.head_in and self.head_onload:
+                continue            # (head-on-load: the head input's gradient is formed by its consumers)
             self.bufs["d:" + name] = torch.empty_like(self.bufs[name])
+        # stand-in operand pointer of the head input's dgrad / wgrad under head-on-load
+        # (never read: dY comes from prob / target / bits, the bias from the fused tile)
+        self._no_dy = torch.zeros(64, dtype=self.adt, device=self.device)
         for l in spec.layers:
             if l.kind == "conv" and l.skip_from is not None:
                 self.bufs["dskip:" + l.skip_from] = torch.empty_like(self.bufs[l.skip_from])
@@ -337,13 +372,12 @@ class NativeUNet:
         XF 4), the tconv weight / bias gradients come from 4x4-tap stride-2 slab sums
         through the chain rule -- the fine tconv output gradient (up to 1 GiB at b1024)
         is never written or re-read.  2D norm-free model; the consumer is the decoder conv
-        whose skip-half data gradient rides on the pool backward.  UNET_TCONV_FUSED = the
+        whose skip-half data gradient rides on the pool backward.  Option tconv_fused = the
         deepest fine level fused (0 off)."""
         self.tconv_fused: Dict[str, dict] = {}
         self._tf_consumer: Dict[str, str] = {}
-        self._s2f_of: Dict[str, str] = {}       # composite-forward consumer conv -> its tconv
         self._wa_chain_of: Dict[str, str] = {}  # consumer conv whose u-row wgrad is chained -> tconv
-        top = int(os.environ.get("UNET_TCONV_FUSED", "2"))
+        top = self.opts["tconv_fused"]
         if self.dims != 2 or top <= 0 or (self.spec.norm != "none" and not self.fuse_norm_stats_planned()):
             return
         for l in self.spec.layers:
@@ -379,46 +413,26 @@ class NativeUNet:
                                             hs=torch.zeros(16 * O * K, dtype=torch.float32, device=self.device),
                                             bs=torch.zeros(16 * O, dtype=torch.float32, device=self.device))
             self._tf_consumer[c.name] = l.name
-            self._plan_s2f(l, c, self.tconv_fused[l.name])
+            self._plan_wa_chain(l, c, self.tconv_fused[l.name])
 
     def fuse_norm_stats_planned(self):
         """Normalised model: every conv epilogue writes its statistics (the composite
         transposed-conv data gradient then carries the tconv input's norm backward rows)."""
         return getattr(self, "fuse_norm_stats", True)
 
-    def _plan_s2f(self, l, c, tf):
-        """UNET_TCONV_FWD (default 1) -- what the consumer conv z = conv3x3([u, skip]) of a
-        composite-backward tconv u = tconv(b) does without u:
-          1: its weight gradient: the u rows come from the 4x4-tap slab sums H / Bs the
-             composite backward forms anyway (tconv_chain), the skip rows from a skip-only
-             weight gradient -- the u half of the wgrad (a 1 GiB re-read at level 1) is gone;
-          2: also its forward (conv_win.h XF 5): the conv runs on the coarse grid over the
-             space-to-depth skip and b with weights composed per step from both fp32 masters
-             (tconv_fused.hip::s2f_compose), each output stored to its fine pixel, so u is
-             never written or read (its buffer is freed).  Measured -0.9 % on the headline
-             step (six 32-channel chunks with mostly-zero composed taps per window cost more
-             than the tconv launch and the u traffic they replace), hence not the default;
-          0: neither."""
-        mode = int(os.environ.get("UNET_TCONV_FWD", "1"))
-        Cs, K, O = c.cin - l.cout, l.cin, c.cout
-        if mode <= 0 or Cs <= 0 or Cs % 32 or O % 16:
+    def _plan_wa_chain(self, l, c, tf):
+        """Option tconv_wa (default 1): the weight gradient of the consumer conv
+        z = conv3x3([u, skip]) of a composite-backward tconv u = tconv(b) takes its u rows
+        from the 4x4-tap slab sums H / Bs the composite backward forms anyway (tconv_chain)
+        and its skip rows from a skip-only weight gradient -- the u half of the wgrad (a
+        1 GiB re-read at level 1) is gone (+3.0..3.2 %, r3_bench_history.md).  (The
+        composite FORWARD on the coarse grid with composed weights measured -0.5..-1.2 %
+        and was removed in round 4.)"""
+        Cs, O = c.cin - l.cout, c.cout
+        if not self.opts["tconv_wa"] or Cs <= 0 or Cs % 32 or O % 16:
             return
         tf["wa"] = dict(Cs=Cs, skg=torch.zeros(9 * Cs * O, dtype=torch.float32, device=self.device))
         self._wa_chain_of[c.name] = l.name
-        if mode < 2 or (c.dropout and self.spec.dropout > 0):
-            return
-        kpad = _r64(9 * (4 * Cs + K))
-        probe = self._conv_common(l.level + 1, 3, 1, 1)
-        probe.update(C1=4 * Cs, s2d=Cs, C2=K, src1=1, src2=1, wgt=1, bias=1, Cout=4 * O, relu=1, dst1=1, s2f=O)
-        try:
-            if self.C.conv_fwd_grid(probe) <= 0:
-                return
-        except ValueError:
-            return
-        tf["s2f"] = dict(kpad=kpad, Cs=Cs, w=torch.zeros(4 * O * kpad, dtype=self.adt, device=self.device),
-                         btab=torch.zeros(16 * O, dtype=torch.float32, device=self.device))
-        self._s2f_of[c.name] = l.name
-        self.bufs.pop(l.name, None)            # u is never formed
 
     # ------------------------------------------------------------------ normalisation
     NORM_EPS = 1e-3          # models/reference.py::_norm (Keras default epsilon)
@@ -712,9 +726,8 @@ class NativeUNet:
         od, oh, ow = self.sdims(out_level or level)
         idd, ih, iw = self.sdims(in_level or level)
         kd = K if self.dims == 3 else 1
-        # UNET_CONV_TILE: force a conv tile id for A/B measurements (8 = no row-window)
         return dict(N=self.B, OD=od, OH=oh, OW=ow, ID=idd, IH=ih, IW=iw, KD=kd, KH=K, KW=K,
-                    stride=stride, pad=pad, tile=int(os.environ.get("UNET_CONV_TILE", "0")))
+                    stride=stride, pad=pad, tile=0)
 
     def _salt(self, lname):
         return [l.name for l in self.spec.layers].index(lname)
@@ -779,10 +792,10 @@ class NativeUNet:
         """2: the training forward runs as two half-batch chunks on two HIP streams, the
         second chunk started once the first has finished its first FWD_OFFSET layers, so kernels of different levels (bandwidth-bound full-resolution ones,
         MFMA-bound coarse ones) share the GPU.  Norm-free 2D model with an even batch
-        (BatchNorm needs whole-batch statistics); UNET_FWD_STREAMS=1 keeps one stream.
+        (BatchNorm needs whole-batch statistics); option fwd_streams=1 keeps one stream.
         Default 2 since round 3: same-box interleaved A/B of the headline step +1.0 / +1.0 /
         +0.6 % (44.2k -> 44.7k img/s, round 2 measured +0.9 % the same way)."""
-        n = int(os.environ.get("UNET_FWD_STREAMS", "2"))
+        n = self.opts["fwd_streams"]
         if n != 2 or not train or self.spec.norm != "none" or self.B % 2 or self.device.type != "cuda":
             return 1
         return 2
@@ -793,16 +806,15 @@ class NativeUNet:
         if nst == 2:
             return self._build_forward_2s(plan, dropout, train)
         # fused head: the Mask 1x1 conv + sigmoid + loss partials run in the epilogue of
-        # the head's input conv (UNET_HEAD_FUSE=0 keeps the separate head launch)
+        # the head's input conv (option head_fuse=0 keeps the separate head launch)
         self._head_fused_blocks = 0
         self._norm_head = False
         if train:
             self._norm_head_loss = False
-        self._fuse_head = os.environ.get("UNET_HEAD_FUSE", "1") != "0"
+        self._fuse_head = bool(self.opts["head_fuse"])
         # convNb -> 2x2 max-pool fused into the conv's epilogue where the kernel can
         self._pool_of = {self.inputs[x.name][0]: x.name for x in spec.layers if x.kind == "pool"}
         self._pool_fused = set()
-        self._s2f_compose(plan)
         for l in spec.layers:
             if l.kind != "up":
                 self._fwd_layer(plan, l, dropout, train, 0, self.B)
@@ -814,7 +826,7 @@ class NativeUNet:
         spec = self.spec
         self._head_fused_blocks = 0
         self._norm_head = False
-        self._fuse_head = os.environ.get("UNET_HEAD_FUSE", "1") != "0"
+        self._fuse_head = bool(self.opts["head_fuse"])
         self._pool_of = {self.inputs[x.name][0]: x.name for x in spec.layers if x.kind == "pool"}
         self._pool_fused = set()
         layers = [l for l in spec.layers if l.kind not in ("up", "mask")]
@@ -824,8 +836,6 @@ class NativeUNet:
         for c in range(2):
             start = plan.size()
             mark = start
-            if c == 0:
-                self._s2f_compose(plan)
             for k, l in enumerate(layers):
                 self._fwd_layer(plan, l, dropout, train, c, nb)
                 if k + 1 == off:
@@ -834,18 +844,6 @@ class NativeUNet:
         for l in spec.layers:
             if l.kind == "mask":
                 self._fwd_layer(plan, l, dropout, train, 0, self.B)
-
-    def _s2f_compose(self, plan):
-        """Composite-forward weights + border bias tables from this step's fp32 masters."""
-        for tname, tf in self.tconv_fused.items():
-            sf = tf.get("s2f")
-            if sf is None:
-                continue
-            cons = tf["consumer"]
-            plan.add_generic("s2f_compose", [self.master_ptr(tname + "/kernel"), self.master_ptr(tname + "/bias"),
-                                             self.master_ptr(cons + "/kernel"), self.master_ptr(cons + "/bias"),
-                                             _ptr(sf["w"]), _ptr(sf["btab"])],
-                             [tf["C"], tf["K"], tf["O"], tf["Ca"], sf["kpad"]], [], "fwd:compose:" + tname)
 
     def _fwd_layer(self, plan, l, dropout, train, c, nb):
         """Forward launches of layer `l` for images [c*nb, (c+1)*nb)."""
@@ -856,24 +854,7 @@ class NativeUNet:
         def P(t):
             return None if t is None else _ptr(b[t]) + self._toff(t, c, nb)
 
-        if l.kind == "conv" and l.name in self._s2f_of:
-            # composite transposed-conv forward on the coarse grid (u never formed)
-            tname = self._s2f_of[l.name]
-            tf = self.tconv_fused[tname]
-            sf = tf["s2f"]
-            skip = self.inputs[l.name][2]
-            d = self._conv_common(l.level + 1, 3, 1, 1)
-            d.update(N=nb, name="fwd:" + l.name, C1=4 * sf["Cs"], s2d=sf["Cs"], C2=tf["K"], src1=P(skip),
-                     src2=P(tf["src"]), wgt=_ptr(sf["w"]), bias=_ptr(sf["btab"]), Cout=4 * l.cout, relu=1,
-                     dst1=P(l.name), s2f=l.cout)
-            bits = self.relu_bits.get(l.name)
-            if bits is not None:
-                d["relu_bits"] = _ptr(bits) + c * nb * (self.npix(l.level) // self.B) * l.cout // 8
-            self._rev_order(d, tf["src"], l.name)
-            plan.add_conv_fwd(d)
-        elif l.kind == "tconv" and l.name in self.tconv_fused and "s2f" in self.tconv_fused[l.name]:
-            pass                                 # folded into its consumer's composite forward
-        elif l.kind == "conv":
+        if l.kind == "conv":
             src1, up1, skip = self.inputs[l.name]
             c1 = self.tinfo[src1][1]
             s1 = P(src1)
@@ -957,7 +938,7 @@ class NativeUNet:
                              [P1, hc], [], "fwd:Mask")
 
     def _rev_order(self, d, src, out, *also):
-        """UNET_WIN_REV bit 0 (forward) / bit 1 (data gradients): a row-window conv
+        """_rev_mode bit 0 (forward) / bit 1 (data gradients): a row-window conv
         walks its windows in the reverse of the order its input was written in, so it
         starts on the producer's most recent output -- still in the Infinity Cache at
         sizes far beyond it.  Records the order `out` (and `also`) were written in.
@@ -1089,7 +1070,8 @@ class NativeUNet:
                 first = src1 == "x"
                 c1 = self.tinfo[src1][1]
                 c2 = self.tinfo[skip][1] if skip else 0
-                dy = b["d:" + l.name]
+                onload = l.name == self.head_in and self.head_onload
+                dy = self._no_dy if onload else b["d:" + l.name]
                 first_xf = None
                 if spec.norm != "none":
                     if (first and self.dims == 2 and self.img in (16, 32, 64, 128) and self.cpad in (4, 8)
@@ -1106,8 +1088,8 @@ class NativeUNet:
                 # A operand is the materialised upsample when there is one
                 wa_t = self._wa_chain_of.get(l.name)
                 if wa_t is not None:
-                    # composite forward: no u -- the weight gradient runs over the skip
-                    # source only; tconv_chain forms the u rows from H / Bs
+                    # chained u rows: the weight gradient runs over the skip source only;
+                    # tconv_chain forms the u rows from H / Bs
                     a1, upA, c1w, c2w, skw = b[skip], 1, c2, 0, None
                 else:
                     a1, upA, c1w, c2w, skw = (b[src1] if src1 in b else None), up1, c1, c2, skip
@@ -1375,6 +1357,9 @@ class NativeUNet:
                 # the 128x128 tile has no register room for the fused ones-MFMA bias sums:
                 # those (level >= 3, small dY) use a separate column-sum pass instead
                 fused_bias = BM < 128
+                if w["lname"] == self.head_in and self.head_onload and not fused_bias:
+                    raise RuntimeError("head-on-load: the head input's weight gradient needs the fused-bias "
+                                       "tile (its dY is never materialised for a column-sum pass)")
                 d.update(name="wgrad:" + w["lname"], M1=w["M1"], M2=w["M2"], Nc=w["Nc"], splits=splits,
                          win=self.wgrad_win, slab=slab, bias_mode=w["bias_mode"] if fused_bias else 0,
                          bias_slab=bslab)
