@@ -38,11 +38,11 @@ __device__ __forceinline__ PixCoord decompose(int q, int OD, int OH, int OW) {
 // kernel as fixed-order per-tile partials (no atomics, bit-reproducible).
 enum { EPI_GENERIC = 0, EPI_FWD = 1, EPI_DGRAD = 2, EPI_STATS = 3, EPI_DGRAD_NORM = 4 };
 
-// LDS of the epilogue: the BM x BN staging tile plus [4 waves][2][BN] fp32 of
+// LDS of the epilogue: the BM x BN staging tile plus [waves][2][BN] fp32 of
 // statistics partials (modes 3 / 4)
-template <int BM, int BN>
+template <int BM, int BN, int NTHR = 256>
 constexpr int epi_lds_bytes() {
-  return BM * (BN + 4) * 2 + 4 * 2 * BN * 4;
+  return BM * (BN + 4) * 2 + (NTHR / 64) * 2 * BN * 4;
 }
 
 // nullptr when the normalisation fields of p form a supported epilogue

@@ -31,6 +31,7 @@
 #include "conv_params.h"
 #include "conv_epilogue.h"
 #include "conv_win.h"
+#include "conv_pipe.h"
 
 namespace unet {
 
@@ -858,6 +859,7 @@ static bool tconv_dgrad_eligible(const ConvFwdParams& p) {
 }
 
 int conv_fwd_pick(const ConvFwdParams& p);
+static bool win_tile(int t) { return t == 6 || t == 12 || t == 14; }
 
 // 2D 8 x 8 images, 3x3 'same', plain / concat source, no fused pool / head / transform
 // (the image-window kernel above); normalisation statistics per 4-image tile.
@@ -903,22 +905,22 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.xform) {
     const int ep = conv_epi_mode(p), t = conv_fwd_pick(p);
     if (p.xform != 1 || p.C2 || !p.xa || !p.xb || p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) ||
-        (t != 6 && t != 12) || (p.xcs != 0 && p.xcs != p.C1) || p.head_w || (ep != EPI_STATS && ep != EPI_GENERIC))
+        (t != 6 && t != 12 && t != 14) || (p.xcs != 0 && p.xcs != p.C1) || p.head_w || (ep != EPI_STATS && ep != EPI_GENERIC))
       return "conv_fwd: operand transform needs a 2D single-source row-window forward of a normalised input";
   }
   if (p.hg.prob && (!p.hg.t || !p.hg.sums || !p.hg.w || !p.hg.bits || p.C1 != 32 || p.C2 || p.xform ||
                     p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) || conv_epi_mode(p) != EPI_DGRAD ||
-                    p.route_gy || (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12)))
+                    p.route_gy || !win_tile(conv_fwd_pick(p))))
     return "conv_fwd: head-on-load needs a 2D 32-channel row-window data gradient";
   if (p.s2d && (p.s2d % 32 || p.C1 != 4 * p.s2d || p.C2 || p.xform || p.hg.prob || p.route_gy || p.KD != 1 ||
                 p.OD != 1 || p.OW > 128 || !win_eligible(p) ||
                 (conv_epi_mode(p) != EPI_DGRAD && conv_epi_mode(p) != EPI_DGRAD_NORM) ||
-                (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12)))
+                !win_tile(conv_fwd_pick(p))))
     return "conv_fwd: space-to-depth source needs a 2D single-source row-window data gradient (C1 = 4 s2d)";
   if (p.route_gy && (!p.pool_code || (conv_epi_mode(p) != EPI_DGRAD && conv_epi_mode(p) != EPI_DGRAD_NORM) ||
                      !win_eligible(p) || p.KD != 1 || p.OD != 1 ||
                      p.OH % 2 || p.OW % 2 || p.D1 != p.Cout || p.pool_dst || p.mask_scale1 != 1.f ||
-                     (conv_fwd_pick(p) != 6 && conv_fwd_pick(p) != 12)))
+                     !win_tile(conv_fwd_pick(p))))
     return "conv_fwd: fused pool backward needs a 2D row-window data gradient (even dims, one destination, codes)";
   if (p.pool_dst) {
     const int W = p.OW > 128 ? 128 : p.OW;
@@ -927,8 +929,8 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
         p.OH % 2 || p.OW % 2 || p.Cout % 8 || p.head_w)
       return "conv_fwd: fused max-pool needs a 2D row-window ReLU forward (even rows, codes buffer)";
   }
-  if (p.tile < 0 || p.tile > 13) return "conv_fwd: bad tile id";
-  if (p.tile == 12 && (!win_eligible(p) || p.Cout % 64 || p.head_w))
+  if (p.tile < 0 || p.tile > 14) return "conv_fwd: bad tile id";
+  if ((p.tile == 12 || p.tile == 14) && (!win_eligible(p) || p.Cout % 64 || p.head_w))
     return "conv_fwd: 64-wide row-window tile not applicable";
   if (p.tile == 10 && !tconv_fwd_eligible(p)) return "conv_fwd: transposed-conv window tile not applicable";
   if (p.tile == 11 && !tconv_dgrad_eligible(p)) return "conv_fwd: transposed-conv dgrad tile not applicable";
@@ -936,7 +938,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.tile == 13 && !img8_eligible(p)) return "conv_fwd: 8x8 image-window tile not applicable";
   {
     const int t = p.tile ? p.tile : 0;
-    const int bn = t == 1 ? 128 : (t == 2 || t == 5 || t == 7 || t == 12 || t == 13) ? 64 : 32;
+    const int bn = t == 1 ? 128 : (t == 2 || t == 5 || t == 7 || t == 12 || t == 13 || t == 14) ? 64 : 32;
     if (t && p.Cout % bn) return "conv_fwd: forced tile does not divide Cout";
     if (t == 7) return "conv_fwd: tile 7 (row-window 512x64: 268 registers, 92 KB LDS, 1 wave/SIMD) is not built";
     if (t == 6 && !win_eligible(p)) return "conv_fwd: row-window tile not applicable";
@@ -959,7 +961,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     const long long opx = (long long)p.OD * p.OH * p.OW;
     const long long lim = (1LL << 31) - 64;
     long long span = img * p.N;                       // bytes a launch addresses from one base
-    if (t == 6 || t == 12 || t == 13) span = img;
+    if (win_tile(t) || t == 13) span = img;
     else if (t >= 1 && t <= 5) span = img * (256 / opx + 2 < p.N ? 256 / opx + 2 : p.N);
     if (span >= lim) return "conv_fwd: input exceeds the 2 GiB reach of one buffer base (split the batch)";
   }
@@ -979,7 +981,9 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
 }
 
 // tile ids: 1 = 128x128, 2 = 128x64, 3 = 256x32, 4 = 128x32, 5 = 256x64 (4 waves each);
-// 6 = row-window 512 x 32; 8 = auto but never row-window (A/B tests); 13 = 8x8 image window
+// 6 = row-window (auto tile width); 8 = auto but never row-window (A/B tests); 12 = row
+// window, 64-channel tile; 13 = 8x8 image window; 14 = row window, 4-wave 64-channel tile
+// (never the pipelined 8-wave window, conv_pipe.h)
 int conv_fwd_pick(const ConvFwdParams& p) {
   const int M = p.N * p.OD * p.OH * p.OW;
   if (p.tile && p.tile != 8) return p.tile;
@@ -998,7 +1002,7 @@ int conv_fwd_pick(const ConvFwdParams& p) {
 
 int conv_fwd_grid(const ConvFwdParams& p) {
   const int t = conv_fwd_pick(p);
-  return (t == 6 || t == 12) ? win_grid(p) : 0;
+  return win_tile(t) ? win_grid(p) : 0;
 }
 
 void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
@@ -1008,7 +1012,8 @@ void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
   const bool smallc = (p.C1 == 4 || p.C1 == 8) && p.C2 == 0;
   switch (t) {
     case 6:
-    case 12: {       // row window: R rows x (segment) width, tiles in (row group, segment) order
+    case 12:
+    case 14: {       // row window: R rows x (segment) width, tiles in (row group, segment) order
       const int W = p.OW > 128 ? 128 : p.OW;
       const int R = win_rows(p);
       if (p.nz && p.C2) return;
@@ -1054,6 +1059,8 @@ hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
     case 5: return launch_cfg<256, 64, 4, 1>(p, s);
     case 6:
     case 12:
+    case 14:
+      if (win_pipe(p)) return launch_pipe(p, s);
       if (win_bn(p) == 64) return launch_win<64, 256>(p, s);
       return win_bm(p) == 256 ? launch_win<32, 256>(p, s) : launch_win<32, 512>(p, s);
     case 9: return p.C1 == 4 ? launch_win_first<4>(p, s) : launch_win_first<8>(p, s);

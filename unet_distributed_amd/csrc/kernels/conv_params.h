@@ -108,6 +108,7 @@ struct ConvFwdParams {
   const float* head_w;
   const float* head_b;
   float* head_logit;
+  int pipe_off;               // 1: never the pipelined 8-wave window (conv_pipe.h; A/B runs)
   int rev;                    // row-window kernels: windows in reverse order (the consumer starts
                               // where its producer ended, on the tail still in the Infinity Cache)
   HeadGrad hg;                // 2D row-window data gradient of the head input: src1 (dY) formed

@@ -21,17 +21,26 @@ enum { GEO_2D = 0, GEO_SEG = 1, GEO_3D = 2 };
 // halves the halo image's LDS-DMA and fragment reads per MFMA and doubles the MFMA work
 // per synchronisation.  tile 12 / 6 force 64 / 32 (tests).
 inline int win_bn(const ConvFwdParams& p) {
-  if (p.tile == 12) return 64;
+  if (p.tile == 12 || p.tile == 14) return 64;
   if (p.tile == 6) return 32;
   const int W = p.OW > 128 ? 128 : p.OW;
   return (p.Cout % 64 == 0 && W <= 64 && !p.head_w) ? 64 : 32;
 }
-// Window pixels: 256 for 16-wide rows and for the 64-channel tile (its accumulators,
-// 4 x 4 fragments per wave, and LDS then still fit two workgroups per CU), else 512.
-// (A 256-pixel 32-channel window on 32..128-wide rows -- three workgroups per CU --
-// measured -0.4 % at W = 64 and -1 % at 128 and was dropped.)
+// The 64-channel tile on 2D rows 16..64 wide runs the pipelined 8-wave window
+// (conv_pipe.h: double-buffered chunks, 512 pixels on 32 / 64-wide rows, 256 on 16-wide
+// ones) unless an operand transform / head-on-load needs the 4-wave kernel; tile 14
+// forces the 4-wave 64-channel window (bit-exactness tests), pipe_off = 1 keeps the 4-wave
+// kernel wherever the tile is auto (executor option conv_pipe=0: same-box A/B runs).
+inline bool win_pipe(const ConvFwdParams& p) {
+  return p.tile != 14 && !p.pipe_off && p.KD == 1 && p.OW <= 64 && win_bn(p) == 64 && !p.xform && !p.hg.prob;
+}
+// Window pixels: 256 for 16-wide rows and for the 4-wave 64-channel tile (its
+// accumulators, 4 x 4 fragments per wave, and LDS then still fit two workgroups per CU),
+// else 512.  (A 256-pixel 32-channel window on 32..128-wide rows -- three workgroups per
+// CU -- measured -0.4 % at W = 64 and -1 % at 128 and was dropped.)
 inline int win_bm(const ConvFwdParams& p) {
   const int W = p.OW > 128 ? 128 : p.OW;
+  if (win_pipe(p)) return W == 16 ? 256 : 512;
   return (W == 16 || win_bn(p) == 64) ? 256 : 512;
 }
 inline int win_rows(const ConvFwdParams& p) {

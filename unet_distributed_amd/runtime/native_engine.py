@@ -59,7 +59,10 @@ def _r64(k: int) -> int:
 #   tconv_fused  deepest fine level whose transposed conv runs the composite backward (2; 0 off)
 #   tconv_wa     the consumer conv's u-row weight gradient from the composite backward's
 #                slab sums (1; 0: full weight gradient over u)
-ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1)
+#   conv_pipe    64-channel row windows on 16..64-wide rows run the pipelined 8-wave kernel
+#                (conv_pipe.h: double-buffered chunks; 0: the 4-wave window)
+ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
+                       conv_pipe=1)
 
 
 def engine_options(overrides: Optional[Dict[str, int]] = None) -> Dict[str, int]:
@@ -727,7 +730,7 @@ class NativeUNet:
         idd, ih, iw = self.sdims(in_level or level)
         kd = K if self.dims == 3 else 1
         return dict(N=self.B, OD=od, OH=oh, OW=ow, ID=idd, IH=ih, IW=iw, KD=kd, KH=K, KW=K,
-                    stride=stride, pad=pad, tile=0)
+                    stride=stride, pad=pad, tile=0, pipe_off=1 - self.opts["conv_pipe"])
 
     def _salt(self, lname):
         return [l.name for l in self.spec.layers].index(lname)
