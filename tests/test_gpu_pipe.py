@@ -199,3 +199,31 @@ def test_conv_pipe_reverse_order_and_tail_windows(cuda_dev):
     assert torch.equal(outs[0], outs[1])
     ref = nhwc(F.relu(F.conv2d(nchw(x.float()), w.float().permute(3, 2, 0, 1), b, padding=1)))
     assert rel_err(outs[0], ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,C1,C2,Cout,splits", [
+    (4, 64, 64, 0, 64, 3), (3, 64, 64, 64, 64, 9), (2, 64, 32, 0, 64, 2), (5, 32, 64, 0, 128, 4),
+    (2, 32, 128, 128, 128, 3), (3, 32, 32, 0, 32, 40), (4, 16, 64, 0, 64, 3), (3, 16, 128, 128, 128, 5),
+    (2, 16, 256, 0, 256, 70), (2, 64, 64, 0, 32, 4)])
+def test_wgrad_pipe_matches_window_kernel(cuda_dev, N, H, C1, C2, Cout, splits):
+    """The pipelined 8-wave window weight gradient (wgrad_pipe.hip, default on 16..64-wide
+    rows) against the 4-wave window (win 2) and the fp32 autograd reference: kernel and
+    fused bias sums, concat sources, more splits than windows (empty splits write zeros)."""
+    from test_gpu_kernels import _wgrad
+    torch.manual_seed(N + H + C1 + C2 + Cout + splits)
+    a = F.relu(torch.randn(N, H, H, C1, device=cuda_dev)).bfloat16()
+    b2 = F.relu(torch.randn(N, H, H, max(C2, 1), device=cuda_dev)).bfloat16()
+    dy = torch.randn(N, H, H, Cout, device=cuda_dev).bfloat16()
+    Mt = C1 + C2
+    d = dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=C1, M2=C2, a1=ptr(a),
+             a2=ptr(b2) if C2 else None, b=ptr(dy), Nc=Cout, bias_mode=1)
+    gw0, gb0 = _wgrad(dict(d, win=0), splits, 9, Mt, Mt, Cout, 9 * Mt * Cout, bias_w=(splits, Cout))
+    gw2, gb2 = _wgrad(dict(d, win=2), splits, 9, Mt, Mt, Cout, 9 * Mt * Cout, bias_w=(splits, Cout))
+    torch.cuda.synchronize()
+    assert rel_err(gw0, gw2) < 1e-5 and rel_err(gb0, gb2) < 1e-5
+    inp = nchw(a.float()) if not C2 else torch.cat([nchw(a.float()), nchw(b2.float())], 1)
+    w = torch.zeros(Cout, Mt, 3, 3, device=cuda_dev, requires_grad=True)
+    bb = torch.zeros(Cout, device=cuda_dev, requires_grad=True)
+    gwr, gbr = torch.autograd.grad(F.conv2d(inp, w, bb, padding=1), [w, bb], nchw(dy.float()))
+    assert rel_err(gw0, gwr.permute(2, 3, 1, 0).reshape(-1)) < 2e-3
+    assert rel_err(gb0, gbr) < 2e-3

@@ -61,8 +61,10 @@ def _r64(k: int) -> int:
 #                slab sums (1; 0: full weight gradient over u)
 #   conv_pipe    64-channel row windows on 16..64-wide rows run the pipelined 8-wave kernel
 #                (conv_pipe.h: double-buffered chunks; 0: the 4-wave window)
+#   wgrad_pipe   row-window weight gradients on 16..64-wide rows run the pipelined 8-wave
+#                kernel (wgrad_pipe.hip: double-buffered windows; 0: the 4-wave window)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
-                       conv_pipe=1)
+                       conv_pipe=1, wgrad_pipe=1)
 
 
 def engine_options(overrides: Optional[Dict[str, int]] = None) -> Dict[str, int]:
@@ -1364,7 +1366,8 @@ class NativeUNet:
                     raise RuntimeError("head-on-load: the head input's weight gradient needs the fused-bias "
                                        "tile (its dY is never materialised for a column-sum pass)")
                 d.update(name="wgrad:" + w["lname"], M1=w["M1"], M2=w["M2"], Nc=w["Nc"], splits=splits,
-                         win=self.wgrad_win, slab=slab, bias_mode=w["bias_mode"] if fused_bias else 0,
+                         win=self.wgrad_win if (self.wgrad_win < 0 or self.opts["wgrad_pipe"]) else 2,
+                         slab=slab, bias_mode=w["bias_mode"] if fused_bias else 0,
                          bias_slab=bslab)
                 if part is not None:
                     d.update(split_lo=part * splits // 2, split_n=splits // 2)
