@@ -2,9 +2,14 @@
 usage: python scripts/dice_parity_summary.py <seeds...>  (runs of one seed may come from separate GPU calls)"""
 import json, statistics, sys
 seeds = [int(s) for s in sys.argv[1:]]
+import os
 runs = [("native bf16, DP=1", "native_dp1"), ("ATen fp32, DP=1", "aten_fp32_dp1"),
         ("native bf16, DP=2 (gloo, 1 card)", "native_dp2"), ("native fp16 + GroupNorm", "native_gn16"),
-        ("ATen fp32 + GroupNorm", "aten_gn32")]
+        ("ATen fp32 + GroupNorm", "aten_gn32"),
+        ("native bf16, upsampling decoder, 1 channel", "native_ups"),
+        ("ATen fp32, upsampling decoder, 1 channel", "aten_ups")]
+# (runs of a path that was not run -- e.g. PAIRS=ups -- are left out)
+runs = [r for r in runs if all(os.path.exists("gpurun_out/dice/%s_s%d.jsonl" % (r[1], s)) for s in seeds)]
 rows, finals, losses = [], {}, {}
 for label, f in runs:
     for seed in seeds:
@@ -36,7 +41,10 @@ out += ["", "| pair | |seed-mean Dice diff| | bound | mean |loss diff| / loss, l
         "|---|---|---|---|---|---|"]
 for la, a, b in (("native bf16 vs ATen fp32", "native_dp1", "aten_fp32_dp1"),
                  ("native DP=1 vs DP=2", "native_dp1", "native_dp2"),
-                 ("native fp16+GN vs ATen fp32 GN", "native_gn16", "aten_gn32")):
+                 ("native fp16+GN vs ATen fp32 GN", "native_gn16", "aten_gn32"),
+                 ("upsampling decoder: native bf16 vs ATen fp32", "native_ups", "aten_ups")):
+    if a not in mean or b not in mean:
+        continue
     d = abs(mean[a] - mean[b])
     g = loss_gap(a, b)
     out.append("| %s | %.4f | 0.02 | %.3f | 0.10 | %s |" % (la, d, g, "pass" if d <= 0.02 and g <= 0.10 else "FAIL"))

@@ -6,7 +6,8 @@
 #   (a) native HIP, bf16, DP=1           (b) ATen (PyTorch) fp32, DP=1
 #   (c) native bf16, DP=2 (2 ranks, gloo on one card, 16 per rank)
 #   (d) native fp16 + GroupNorm, DP=1    (e) ATen fp32 + GroupNorm, DP=1
-# for the seeds given (default 1 2 3).  Writes gpurun_out/dice_parity.md: per-epoch test Dice,
+#   (f) native bf16, upsampling decoder, 1 input channel   (g) the same on ATen fp32
+# for the seeds given (default 1 2 3).  PAIRS="ups" runs only (f) / (g).  Writes gpurun_out/dice_parity.md: per-epoch test Dice,
 # final Dice, seed means against the 0.02 bound, and the mean |delta| of the per-step
 # training loss over the last 100 steps relative to the loss.
 #   bash scripts/gpu_dice_parity.sh [steps] [seeds...]
@@ -24,7 +25,11 @@ run() {   # name timeout args...
   timeout -k 10 $to "$@" --log_jsonl gpurun_out/dice/$name.jsonl > gpurun_out/dice/$name.log 2>&1 \
     || { tail -20 gpurun_out/dice/$name.log; exit 1; }
 }
+UPS="--use_upsampling --in_channels 1"
 for seed in $seeds; do
+  run native_ups_s$seed 300 python train.py $COMMON $UPS --seed $seed --backend native --dtype bf16
+  run aten_ups_s$seed 500 python train.py $COMMON $UPS --seed $seed --backend torch --dtype fp32
+  if [ "${PAIRS:-all}" = ups ]; then echo seed $seed done; continue; fi
   run native_dp1_s$seed 300 python train.py $COMMON --seed $seed --backend native --dtype bf16
   run aten_fp32_dp1_s$seed 500 python train.py $COMMON --seed $seed --backend torch --dtype fp32
   port=$((port + 1))

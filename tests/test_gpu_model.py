@@ -38,6 +38,34 @@ def _cos(a, b):
     return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
 
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _grad_parity(fn, ft, tag):
+    """Per-variable (1 - cosine, |norm ratio - 1|) of the native gradients against the fp32
+    ATen step; logged (and written to gpurun_out/parity.jsonl on the GPU box) so the bounds
+    below track the observed worst case (about 2x of it)."""
+    import json
+    rows = {}
+    for name, shape, off, n in fn.entries:
+        gn, gt = fn.grad[off:off + n], ft.grad[off:off + n]
+        if gt.norm() < 1e-6:          # conv bias under BatchNorm: exactly 0 in exact arithmetic
+            assert gn.norm() < 1e-3, (name, gn.norm().item())
+            continue
+        rows[name] = (1.0 - _cos(gn, gt), abs((gn.norm() / (gt.norm() + 1e-30)).item() - 1.0))
+    worst_k = max((v[0], k) for k, v in rows.items() if not k.endswith("/bias"))
+    worst_b = max(((v[0], k) for k, v in rows.items() if k.endswith("/bias")), default=(0.0, None))
+    worst_r = max((v[1], k) for k, v in rows.items())
+    rec = dict(tag=tag, worst_cos_dist_kernel=worst_k, worst_cos_dist_bias=worst_b, worst_ratio_dev=worst_r,
+               total_cos_dist=1.0 - _cos(fn.grad, ft.grad))
+    print("parity", json.dumps(rec))
+    out = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(out):
+        with open(os.path.join(out, "parity.jsonl"), "a") as f:
+            f.write(json.dumps(rec) + "\n")
+    return rows, rec
+
+
 @pytest.mark.parametrize("kw", [
     dict(batch_size=4, img_size=64, in_channels=4),
     dict(batch_size=2, img_size=64, in_channels=1, use_upsampling=True),
@@ -52,27 +80,20 @@ def test_native_step_matches_reference(cuda_dev, kw):
     torch.cuda.synchronize()
     sn, st = nb.sums().cpu(), tb.sums().cpu()
     assert torch.allclose(sn[:3], st[:3], rtol=3e-2, atol=1.0), (sn, st)
-    for name, shape, off, n in fn.entries:
-        gn, gt = fn.grad[off:off + n], ft.grad[off:off + n]
-        if gt.norm() < 1e-6:          # conv bias under BatchNorm: exactly 0 in exact arithmetic
-            assert gn.norm() < 1e-3, (name, gn.norm().item())
-            continue
-        c = _cos(gn, gt)
-        # bias grads are plain sums of bf16 dY over few pixels at the coarse levels; the
-        # normalisation backward (g - mean g - x^ mean g x^) cancels terms, which amplifies
-        # the bf16 storage rounding of g and z
-        tol = 0.95 if name.endswith("/bias") else 0.98
-        assert c > tol, (name, c, gn.norm().item(), gt.norm().item())
-        r = (gn.norm() / (gt.norm() + 1e-30)).item()
-        assert 0.9 < r < 1.1, (name, r)
-    assert _cos(fn.grad, ft.grad) > 0.99
+    rows, rec = _grad_parity(fn, ft, "step:" + ",".join("%s=%s" % kv for kv in sorted(kw.items())))
+    for name, (dc, dr) in rows.items():
+        # bias grads are plain sums of bf16 dY over few pixels at the coarse levels
+        assert dc < (0.05 if name.endswith("/bias") else 0.02), (name, dc)
+        assert dr < 0.1, (name, dr)
+    assert rec["total_cos_dist"] < 0.01
 
 
-def test_native_step_matches_reference_at_shipped_shape(cuda_dev):
-    """The benchmarked configuration itself: 128x128x4, bf16, per-GPU batch 64 with the
-    production split-K sizing (wg_target), dual-stream backward, HIP-graph forward and
-    the fused segmentation head; gradients vs the fp32 ATen step."""
-    spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, batch_size=64, img_size=128, in_channels=4,
+@pytest.mark.parametrize("B", [64, 1024])
+def test_native_step_matches_reference_at_shipped_shape(cuda_dev, B):
+    """The benchmarked configuration itself: 128x128x4, bf16, per-GPU batch 1024 (and 64)
+    with the production split-K sizing (wg_target), dual-stream backward, HIP-graph forward
+    and the fused segmentation head; gradients vs the fp32 ATen step."""
+    spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, batch_size=B, img_size=128, in_channels=4,
                                               hip_graph=True)
     e = nb.engine
     assert e.dual_stream and e._head_fused_blocks > 0 and e.graphs is not None
@@ -82,15 +103,11 @@ def test_native_step_matches_reference_at_shipped_shape(cuda_dev):
     torch.cuda.synchronize()
     sn, st = nb.sums().cpu(), tb.sums().cpu()
     assert torch.allclose(sn[:3], st[:3], rtol=2e-2, atol=1.0), (sn, st)
-    worst = 1.0
-    for name, shape, off, n in fn.entries:
-        gn, gt = fn.grad[off:off + n], ft.grad[off:off + n]
-        c = _cos(gn, gt)
-        worst = min(worst, c)
-        assert c > (0.95 if name.endswith("/bias") else 0.98), (name, c)
-        r = (gn.norm() / (gt.norm() + 1e-30)).item()
-        assert 0.9 < r < 1.1, (name, r)
-    assert _cos(fn.grad, ft.grad) > 0.99, worst
+    rows, rec = _grad_parity(fn, ft, "shipped:B=%d" % B)
+    for name, (dc, dr) in rows.items():
+        assert dc < (0.05 if name.endswith("/bias") else 0.02), (name, dc)
+        assert dr < 0.1, (name, dr)
+    assert rec["total_cos_dist"] < 0.01
 
 
 def test_native_adam_matches_reference(cuda_dev):

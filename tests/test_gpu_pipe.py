@@ -227,3 +227,42 @@ def test_wgrad_pipe_matches_window_kernel(cuda_dev, N, H, C1, C2, Cout, splits):
     gwr, gbr = torch.autograd.grad(F.conv2d(inp, w, bb, padding=1), [w, bb], nchw(dy.float()))
     assert rel_err(gw0, gwr.permute(2, 3, 1, 0).reshape(-1)) < 2e-3
     assert rel_err(gb0, gbr) < 2e-3
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,gn,stats", [(2, 64, 64, 64, False, True), (3, 32, 128, 128, True, True),
+                                                   (4, 16, 256, 256, False, False), (2, 32, 64, 128, True, False)])
+def test_conv_pipe_normalise_on_load(cuda_dev, N, H, Cin, Cout, gn, stats):
+    """XF 1 (the input normalised on load, y = relu(a z + c), y of the window's own rows to
+    xout) on the pipelined window: output, xout and statistics equal the 4-wave window's."""
+    torch.manual_seed(17 + H)
+    z = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
+    rows = N if gn else 1
+    a = 0.5 + torch.rand(rows, Cin, device=cuda_dev)
+    b = 0.3 * torch.randn(rows, Cin, device=cuda_dev)
+    w = (torch.randn(3, 3, Cin, Cout, device=cuda_dev) * 0.06).bfloat16()
+    bias = torch.randn(Cout, device=cuda_dev) * 0.1
+    wp = pack_fwd(w)
+    d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(z), wgt=ptr(wp), bias=ptr(bias),
+             Cout=Cout, relu=0, xform=1, xa=ptr(a), xb=ptr(b), xcs=Cin if gn else 0)
+    res = []
+    for tile in (12, 14):
+        out = torch.empty(N, H, H, Cout, device=cuda_dev, dtype=torch.bfloat16)
+        yo = torch.full_like(z, float("nan"))
+        dd = dict(d, tile=tile, dst1=ptr(out), xout=ptr(yo))
+        st = None
+        if stats:
+            nr, _ = C().conv_stat_tiles(dict(dd, stats=1))
+            st = torch.zeros(nr, 2, Cout, device=cuda_dev)
+            dd["stats"] = ptr(st)
+        else:
+            dd.update(relu=0, drop_rate=0.0, out_scale=1.0)
+        C().conv_fwd(dd, stream())
+        torch.cuda.synchronize()
+        res.append((out, yo, None if st is None else st.view(N, -1, 2, Cout).sum(1)))
+    (o0, y0, s0), (o1, y1, s1) = res
+    assert torch.equal(o0, o1) and torch.equal(y0, y1) and torch.isfinite(y0.float()).all()
+    if stats:
+        assert torch.allclose(s0, s1, rtol=1e-5, atol=1e-3)
+    yr = torch.clamp(a.view(rows, 1, 1, Cin) * z.float() + b.view(rows, 1, 1, Cin), min=0).bfloat16()
+    ref = nhwc(F.conv2d(nchw(yr.float()), w.float().permute(3, 2, 0, 1), bias, padding=1))
+    assert rel_err(o0, ref) < 1e-2

@@ -25,6 +25,9 @@
 //           8 waves split the 64 channels in two halves of 32 (4 pixel strips x 2)
 // XF 4: space-to-depth source (conv_params.h s2d, the composite transposed-conv data
 // gradient): the DMA gathers the fine pixels of each coarse slot, zero taps skipped.
+// XF 1: operand transform (conv_params.h xform 1, normalised input read as the pre-norm
+// z): each landed chunk is normalised in LDS, y = relu(xa z + xb), before its MFMAs
+// (a second barrier per chunk), and the window's own rows of y go to xout.
 #pragma once
 #include "common.h"
 #include "conv_params.h"
@@ -67,11 +70,17 @@ __global__ void __launch_bounds__(PIPE_NTHR) conv_pipe_kernel(const ConvFwdParam
   using G = PipeGeo<W>;
   constexpr int BN = G::BN, BM = G::BM, R = G::R, HR = G::HR, HWP = G::HWP, ROWB = G::ROWB;
   constexpr int XI = G::XI, WI = G::WI, XB = G::XB, TM = G::TM, TN = G::TN, NCS = G::NCS, RW = G::RW;
-  static_assert(XF == 0 || (XF == 4 && !CONCAT), "pipelined window: plain / concat / space-to-depth source");
+  static_assert(XF == 0 || ((XF == 1 || XF == 4) && !CONCAT),
+                "pipelined window: plain / concat / normalised / space-to-depth source");
   // two stages as two LDS objects: their accesses carry distinct alias scopes, so the
   // fragment reads of one stage never wait for the DMA in flight into the other
   __shared__ __attribute__((aligned(1024))) char lds0[G::STAGE];
   __shared__ __attribute__((aligned(1024))) char lds1[G::STAGE];
+  // XF 1: the normalisation coefficients {xa, xb} of the window's sample (<= 256 channels),
+  // staged once before any DMA -- a global load consumed while an LDS-DMA is in flight
+  // would make the compiler drain it (vmcnt(0)) and serialise the pipeline
+  __shared__ float xco[XF == 1 ? 2 * 256 : 1];
+  static_assert(2 * G::STAGE + (XF == 1 ? 2048 : 0) <= 160 * 1024, "stages + coefficients fit the 160 KB LDS");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = p.OH;
@@ -154,6 +163,39 @@ __global__ void __launch_bounds__(PIPE_NTHR) conv_pipe_kernel(const ConvFwdParam
       }
     }
   };
+  // XF 1: normalise chunk kc of stage `st` in place (thread t: logical 16-byte chunk
+  // t & 3 of slots (t >> 2) + 128 j; padding slots keep the DMA's zeros)
+  const size_t xsample = XF == 1 ? (size_t)(g0 / H) * p.xcs : 0;   // the window's sample (GroupNorm rows)
+  auto xform = [&](const int kc, char* st) {
+    constexpr int XNJ = (XI * 64 + PIPE_NTHR - 1) / PIPE_NTHR;
+    const int xlc = tid & 3, xs0 = tid >> 2;
+    const int cb = kc << 5;
+    float xa[8], xb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xa[e] = xco[cb + xlc * 8 + e];
+      xb[e] = xco[256 + cb + xlc * 8 + e];
+    }
+#pragma unroll
+    for (int j = 0; j < XNJ; ++j) {
+      const int sl = xs0 + (PIPE_NTHR / 4) * j;
+      const int hr = sl / HWP, hc = sl - hr * HWP;
+      const int gr = g0 - 1 + hr;
+      const bool ok = hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)gr < (unsigned)rows_total &&
+                      (unsigned)(hc - 1) < (unsigned)W;
+      if (!ok) continue;
+      char* a = st + sl * 64 + 16 * (xlc ^ ((hc >> 1) & 3));
+      float v[8];
+      unpack8(*(const u32x4*)a, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(xa[e], v[e], xb[e]), 0.f);
+      const u32x4 o = pack8(v);
+      *(u32x4*)a = o;
+      // the window's own rows (once: output-channel tile 0) -> xout
+      if (p.xout && tn == 0 && hr >= 1 && hr <= R)
+        *(u32x4*)((h16*)p.xout + (size_t)(gr * W + hc - 1) * p.C1 + cb + xlc * 8) = o;
+    }
+  };
   // chunk kc's MFMAs from stage `st` (the loop nest of conv_win_kernel's chunk_mfmas)
   auto mfmas = [&](const int kc, const char* st) {
     uint32_t tmask = 0x1ffu;
@@ -186,14 +228,28 @@ __global__ void __launch_bounds__(PIPE_NTHR) conv_pipe_kernel(const ConvFwdParam
     }
   };
 
+  if constexpr (XF == 1) {
+    for (int c = tid; c < p.C1; c += PIPE_NTHR) {
+      xco[c] = p.xa[xsample + c];
+      xco[256 + c] = p.xb[xsample + c];
+    }
+  }
   stage(0, lds0);
   for (int kc = 0; kc < nchunks; kc += 2) {
     __syncthreads();                 // chunk kc landed (vmcnt(0) + barrier); stage 1 free
     if (kc + 1 < nchunks) stage(kc + 1, lds1);
+    if constexpr (XF == 1) {
+      xform(kc, lds0);
+      __syncthreads();
+    }
     mfmas(kc, lds0);
     if (kc + 1 < nchunks) {
       __syncthreads();               // chunk kc + 1 landed; stage 0 free
       if (kc + 2 < nchunks) stage(kc + 2, lds0);
+      if constexpr (XF == 1) {
+        xform(kc + 1, lds1);
+        __syncthreads();
+      }
       mfmas(kc + 1, lds1);
     }
   }
@@ -211,6 +267,13 @@ hipError_t launch_pipe_w(const ConvFwdParams& p, hipStream_t s) {
   const int epi = conv_epi_mode(p);
 #define PIPE_L(CC, E, XX) \
   hipLaunchKernelGGL((conv_pipe_kernel<W, CC, E, XX>), dim3(grid), dim3(PIPE_NTHR), 0, s, p)
+  if (p.xform) {                      // (conv_fwd_prepare: xform 1, single source, STATS / GENERIC)
+    if (cc || p.xform != 1 || p.C1 > 256) return hipErrorInvalidValue;
+    if (epi == EPI_STATS) PIPE_L(false, EPI_STATS, 1);
+    else if (epi == EPI_GENERIC) PIPE_L(false, EPI_GENERIC, 1);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if (p.s2d) {
     if (cc) return hipErrorInvalidValue;
     if (epi == EPI_DGRAD) PIPE_L(false, EPI_DGRAD, 4);

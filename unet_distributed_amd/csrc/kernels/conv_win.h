@@ -28,11 +28,12 @@ inline int win_bn(const ConvFwdParams& p) {
 }
 // The 64-channel tile on 2D rows 16..64 wide runs the pipelined 8-wave window
 // (conv_pipe.h: double-buffered chunks, 512 pixels on 32 / 64-wide rows, 256 on 16-wide
-// ones) unless an operand transform / head-on-load needs the 4-wave kernel; tile 14
+// ones) unless head-on-load needs the 4-wave kernel; tile 14
 // forces the 4-wave 64-channel window (bit-exactness tests), pipe_off = 1 keeps the 4-wave
 // kernel wherever the tile is auto (executor option conv_pipe=0: same-box A/B runs).
 inline bool win_pipe(const ConvFwdParams& p) {
-  return p.tile != 14 && !p.pipe_off && p.KD == 1 && p.OW <= 64 && win_bn(p) == 64 && !p.xform && !p.hg.prob;
+  return p.tile != 14 && !p.pipe_off && p.KD == 1 && p.OW <= 64 && win_bn(p) == 64 && (!p.xform || (p.xform == 1 && p.C1 <= 256)) &&
+         !p.hg.prob;
 }
 // Window pixels: 256 for 16-wide rows and for the 4-wave 64-channel tile (its
 // accumulators, 4 x 4 fragments per wave, and LDS then still fit two workgroups per CU),
