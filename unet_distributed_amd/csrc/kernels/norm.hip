@@ -386,6 +386,15 @@ __device__ __forceinline__ float slice_sum(const float* __restrict__ sl, int nsl
   return (a[0] + a[1]) + (a[2] + a[3]);
 }
 
+__device__ __forceinline__ void bn_final_channel(int c, float s1, float s2, float count, int mode,
+                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                 float eps, float momentum, float* __restrict__ run_mean,
+                                                 float* __restrict__ run_var, float* __restrict__ mean,
+                                                 float* __restrict__ rstd, float* __restrict__ fa,
+                                                 float* __restrict__ fc, float* __restrict__ ca, float* __restrict__ cb,
+                                                 float* __restrict__ cc, float* __restrict__ dgamma,
+                                                 float* __restrict__ dbeta);
+
 // BatchNorm coefficients from the slices; grid ceil(C / 32), 256 threads = 32 channels x
 // 2 moments x 4 slice lanes.  mode 0: forward (batch stats, running stats, fa / fc);
 // 1: backward (ca / cb / cc, dgamma / dbeta); 2: forward inference (running stats; no
@@ -408,6 +417,25 @@ __global__ void __launch_bounds__(NT) bn_final_kernel(const float* __restrict__ 
   }
   if (threadIdx.x >= 32 || c >= C) return;
   const int i = t;      // channel lane (mom 0)
+  float s1 = 0.f, s2 = 0.f;
+  if (mode != 2) {
+    s1 = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    s2 = red[0][i + 32] + red[1][i + 32] + red[2][i + 32] + red[3][i + 32];
+  }
+  bn_final_channel(c, s1, s2, count, mode, gamma, beta, eps, momentum, run_mean, run_var, mean, rstd, fa, fc, ca, cb, cc,
+                   dgamma, dbeta);
+}
+
+// one channel of bn_final from its column sums s1 = sum x, s2 = sum x^2 (forward) or
+// s1 = sum g, s2 = sum g z (backward)
+__device__ __forceinline__ void bn_final_channel(const int c, const float s1, const float s2, const float count,
+                                                 const int mode, const float* __restrict__ gamma,
+                                                 const float* __restrict__ beta, const float eps, const float momentum,
+                                                 float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                 float* __restrict__ mean, float* __restrict__ rstd,
+                                                 float* __restrict__ fa, float* __restrict__ fc, float* __restrict__ ca,
+                                                 float* __restrict__ cb, float* __restrict__ cc,
+                                                 float* __restrict__ dgamma, float* __restrict__ dbeta) {
   if (mode == 2) {
     const float mu = run_mean[c], r = rsqrtf(run_var[c] + eps);
     mean[c] = mu;
@@ -416,8 +444,6 @@ __global__ void __launch_bounds__(NT) bn_final_kernel(const float* __restrict__ 
     fc[c] = beta[c] - mu * gamma[c] * r;
     return;
   }
-  const float s1 = red[0][i] + red[1][i] + red[2][i] + red[3][i];
-  const float s2 = red[0][i + 32] + red[1][i + 32] + red[2][i + 32] + red[3][i + 32];
   if (mode == 3) {
     dbeta[c] = s1;
     dgamma[c] = s2;
@@ -443,6 +469,91 @@ __global__ void __launch_bounds__(NT) bn_final_kernel(const float* __restrict__ 
     cb[c] = -gm * r * r * m2;
     cc[c] = -gm * r * m1 + gm * r * r * mu * m2;
   }
+}
+
+// Single-launch BatchNorm statistics (forward / backward / plain column sums, modes 0 / 1
+// / 3): phase 1 as row_slices (block (sl, cb) sums rpb rows of 64 columns into slice sl),
+// then the LAST block to finish -- told by the value its agent-scope counter add returns
+// -- sums the slices of every column and finalises all channels (bn_final_channel).  The
+// hand-off follows MI355X_MICROARCH.md's sc1 recipe: every slice store and every slice
+// load of the last block is an agent-scope relaxed atomic (global_store / global_load
+// sc1: written through, L1 bypassed), every storing wave waits vmcnt(0) before the
+// workgroup barrier behind which one lane adds to the counter, and the last block's waves
+// load only after the barrier its adding lane joins.  The last block resets the counter
+// (graph replays).  Fixed summation order: deterministic, no float atomics.  Replaces the
+// row_slices + bn_final pair (72 -> 36 launches per BatchNorm step).
+__global__ void __launch_bounds__(NT) bn_stats_fused_kernel(const float* __restrict__ rows, int R, int C, int rpb,
+                                                            float* __restrict__ slices, int* __restrict__ counter,
+                                                            float count, int mode, const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float eps, float momentum,
+                                                            float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                            float* __restrict__ mean, float* __restrict__ rstd,
+                                                            float* __restrict__ fa, float* __restrict__ fc,
+                                                            float* __restrict__ ca, float* __restrict__ cb,
+                                                            float* __restrict__ cc, float* __restrict__ dgamma,
+                                                            float* __restrict__ dbeta) {
+  __shared__ float red[4][64];
+  __shared__ int last;
+  const int W = 2 * C;
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  {
+    const int col = blockIdx.y * 64 + cl, sl = blockIdx.x;
+    const int r0 = sl * rpb, r1 = min(R, r0 + rpb);
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (col < W) {
+      int r = r0 + rl;
+      for (; r + 28 < r1; r += 32)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] += rows[(size_t)(r + 4 * k) * W + col];
+      for (; r < r1; r += 4) a[0] += rows[(size_t)r * W + col];
+    }
+    red[rl][cl] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    __syncthreads();
+    if (rl == 0 && col < W)
+      __hip_atomic_store(slices + (size_t)sl * W + col, red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl],
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int done = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = done == (int)(gridDim.x * gridDim.y) - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  const int nsl = gridDim.x;
+  const int t = threadIdx.x & 63;
+  const int mom = t >> 5;
+  for (int c0 = 0; c0 < C; c0 += 32) {
+    const int c = c0 + (t & 31);
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (c < C) {
+      const float* sp = slices + mom * C + c;
+      int sl = rl;
+      for (; sl + 28 < nsl; sl += 32)
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          a[k] += __hip_atomic_load(sp + (size_t)(sl + 4 * k) * W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (; sl < nsl; sl += 4) a[0] += __hip_atomic_load(sp + (size_t)sl * W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();                                   // (previous channel block's red reads done)
+    red[rl][t] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    __syncthreads();
+    if (threadIdx.x < 32 && c < C) {
+      const float s1 = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+      const float s2 = red[0][t + 32] + red[1][t + 32] + red[2][t + 32] + red[3][t + 32];
+      bn_final_channel(c, s1, s2, count, mode, gamma, beta, eps, momentum, run_mean, run_var, mean, rstd, fa, fc, ca,
+                       cb, cc, dgamma, dbeta);
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// rows per phase-1 block of bn_stats_fused: at most 128 slices for the last block to sum
+int fused_rows_per_block(int R) {
+  int rpb = (R + 127) / 128;
+  rpb = (rpb + 15) / 16 * 16;
+  return rpb < 32 ? 32 : rpb;
 }
 
 // GroupNorm per sample: block n sums its rps rows (sample n) into S[2][C] in LDS, then
@@ -621,11 +732,19 @@ hipError_t bn_stats_launch(const float* rows, int R, int C, float count, int mod
                            const float* beta, float eps, float momentum, float* run_mean, float* run_var, float* mean,
                            float* rstd, float* fa, float* fc, float* ca, float* cb, float* cc, float* dgamma,
                            float* dbeta, float* slices, hipStream_t s) {
-  const int nsl = row_slices(R);
-  if (mode != 2)
-    hipLaunchKernelGGL(row_slices_kernel, dim3(nsl, (2 * C + 63) / 64), dim3(NT), 0, s, rows, R, 2 * C, slices);
-  hipLaunchKernelGGL(bn_final_kernel, dim3((C + 31) / 32), dim3(NT), 0, s, slices, nsl, C, count, mode, gamma, beta,
-                     eps, momentum, run_mean, run_var, mean, rstd, fa, fc, ca, cb, cc, dgamma, dbeta);
+  if (mode == 2) {                  // inference: running statistics only
+    hipLaunchKernelGGL(bn_final_kernel, dim3((C + 31) / 32), dim3(NT), 0, s, slices, 0, C, count, mode, gamma, beta,
+                       eps, momentum, run_mean, run_var, mean, rstd, fa, fc, ca, cb, cc, dgamma, dbeta);
+    return hipGetLastError();
+  }
+  // one launch: slices, then the finalize by the last block; the counter lives just past
+  // the row_slices(R) * 2C slice floats of the workspace (zeroed once, reset every use)
+  const int rpb = fused_rows_per_block(R);
+  const int nsl = (R + rpb - 1) / rpb;
+  int* counter = (int*)(slices + (size_t)row_slices(R) * 2 * C);
+  hipLaunchKernelGGL(bn_stats_fused_kernel, dim3(nsl, (2 * C + 63) / 64), dim3(NT), 0, s, rows, R, C, rpb, slices,
+                     counter, count, mode, gamma, beta, eps, momentum, run_mean, run_var, mean, rstd, fa, fc, ca, cb, cc,
+                     dgamma, dbeta);
   return hipGetLastError();
 }
 
@@ -639,14 +758,15 @@ hipError_t gn_stats_launch(const float* rows, int N, int rps, int C, int G, int 
   hipLaunchKernelGGL(gn_sample_kernel, dim3(N), dim3(NT), lds, s, rows, rps, C, G, (float)P, mode, gamma, beta, eps,
                      mean, rstd, fa, fc, ca, cb, cc, work);
   if (mode == 1) {
+    // dgamma / dbeta = column sums of the per-sample contributions (fused single launch)
     float* slices = work + (size_t)N * 2 * C;
-    const int nsl = row_slices(N);
-    hipLaunchKernelGGL(row_slices_kernel, dim3(nsl, (2 * C + 63) / 64), dim3(NT), 0, s, (const float*)work, N, 2 * C,
-                       slices);
-    hipLaunchKernelGGL(bn_final_kernel, dim3((C + 31) / 32), dim3(NT), 0, s, (const float*)slices, nsl, C, 1.f, 3,
-                       gamma, beta, eps, 0.f, (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr,
-                       (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr, dgamma,
-                       dbeta);
+    const int rpb = fused_rows_per_block(N);
+    const int nsl = (N + rpb - 1) / rpb;
+    int* counter = (int*)(slices + (size_t)row_slices(N) * 2 * C);
+    hipLaunchKernelGGL(bn_stats_fused_kernel, dim3(nsl, (2 * C + 63) / 64), dim3(NT), 0, s, (const float*)work, N, C,
+                       rpb, slices, counter, 1.f, 3, gamma, beta, eps, 0.f, (float*)nullptr, (float*)nullptr,
+                       (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr,
+                       (float*)nullptr, (float*)nullptr, dgamma, dbeta);
   }
   return hipGetLastError();
 }

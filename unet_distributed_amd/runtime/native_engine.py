@@ -513,7 +513,8 @@ class NativeUNet:
     def _stat_work(self, key, R, C):
         """Workspace of bn_stats / gn_stats (slices of R rows, or GroupNorm's per-sample
         parameter-gradient rows + their slices)."""
-        n = max(self.C.row_slices(R), 1) * 2 * C + self.B * 2 * C + self.C.row_slices(self.B) * 2 * C
+        # (+64: the single-launch finalize's hand-off counter past the slices, norm.hip)
+        n = max(self.C.row_slices(R), 1) * 2 * C + self.B * 2 * C + self.C.row_slices(self.B) * 2 * C + 64
         return self._stat_buf("w" + key, n)
 
     def _norm_fwd(self, plan, l, dropout, train, fused=None):
