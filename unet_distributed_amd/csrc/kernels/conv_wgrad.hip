@@ -650,8 +650,17 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
       u32x4 v[4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
       if (pix < Mq) head_grad_pixel(p.hg, hctx, pix, v);
       const int sw = ((tid >> 3) & 1) << 1;
+      // store order rotated by (t / 2) mod 4: the 8 lanes of a store group then write 8
+      // different 16-byte bank groups (same order in every lane: 2-way conflicted, 41 %
+      // LDS conflict cycles on this kernel, r3_pmc_table.md); values picked by selects, not
+      // a dynamically indexed register array
+      const int rot = (tid >> 1) & 3;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) *(u32x4*)(Ys + tid * 64 + 16 * (k ^ sw)) = v[k];
+      for (int k = 0; k < 4; ++k) {
+        const int kk = (k + rot) & 3;
+        const u32x4 w = kk == 0 ? v[0] : (kk == 1 ? v[1] : (kk == 2 ? v[2] : v[3]));
+        *(u32x4*)(Ys + tid * 64 + 16 * (kk ^ sw)) = w;
+      }
     }
 #pragma unroll
     for (int qq = 0; qq < (YI + 3) / 4; ++qq) {

@@ -387,6 +387,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
           const int hc = sl % HWP;
           const float dz = head_dlogit(hpr[j], htv[j], hctx.a, hctx.bb, hctx.inv_total, hctx.bce_w, hctx.gscale);
           const int sw = (hc >> 1) & 3;
+          u32x4 ck[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             float o[8];
@@ -395,7 +396,17 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
               const float v = dz * hctx.w[8 * k + e];
               o[e] = ((hbits[j] >> (8 * k + e)) & 1u) ? v : 0.f;
             }
-            *(u32x4*)(Xs + sl * 64 + 16 * (k ^ sw)) = pack8(o);
+            ck[k] = pack8(o);
+          }
+          // store order rotated by (slot / 2) mod 4: consecutive lanes' slots are 64 B
+          // apart, so in one order lanes t and t + 4 hit the same banks; rotated, the 8
+          // lanes of a store group write 8 different 16-byte bank groups
+          const int rot = (sl >> 1) & 3;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int kk = (k + rot) & 3;
+            const u32x4 w = kk == 0 ? ck[0] : (kk == 1 ? ck[1] : (kk == 2 ? ck[2] : ck[3]));
+            *(u32x4*)(Xs + sl * 64 + 16 * (kk ^ sw)) = w;
           }
         }
       }
