@@ -902,7 +902,15 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     return "conv_fwd: relu_bits needs an unsplit ReLU forward";
   if ((p.mask_bits & ~3) || ((p.mask_bits & 1) && !p.mask1) || ((p.mask_bits & 2) && !p.mask2))
     return "conv_fwd: mask_bits marks a missing mask";
-  if (p.xform) {
+  if (p.xform == 3) {
+    // first layer on load (conv_win.h XF 6): a 32-channel first-conv output formed per
+    // window from the 4-channel input
+    const int t = conv_fwd_pick(p);
+    if (p.C1 != 32 || p.C2 || !p.fw || !p.fb || p.fcin != 4 || p.fkpad < 64 || p.fkpad % 64 || p.KD != 1 ||
+        p.OD != 1 || p.OW > 128 || !win_eligible(p) || (t != 6 && t != 12 && t != 14) || win_pipe(p) ||
+        conv_epi_mode(p) != EPI_FWD || p.head_w)
+      return "conv_fwd: first layer on load needs a 2D 32-channel ReLU row-window forward over a 4-channel input";
+  } else if (p.xform) {
     const int ep = conv_epi_mode(p), t = conv_fwd_pick(p);
     if (p.xform != 1 || p.C2 || !p.xa || !p.xb || p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) ||
         (t != 6 && t != 12 && t != 14) || (p.xcs != 0 && p.xcs != p.C1) || p.head_w || (ep != EPI_STATS && ep != EPI_GENERIC))

@@ -131,6 +131,11 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.xz = getp(d, "xz");
   p.s2d = get<int>(d, "s2d", 0);
   p.xout = const_cast<void*>(getp(d, "xout"));
+  p.fw = getp(d, "fw");
+  p.fb = (const float*)getp(d, "fb");
+  p.fbits = (uint8_t*)const_cast<void*>(getp(d, "fbits"));
+  p.fcin = get<int>(d, "fcin", 0);
+  p.fkpad = get<int>(d, "fkpad", 0);
   p.tile = get<int>(d, "tile", 0);
   p.head_w = (const float*)getp(d, "head_w");
   p.head_b = (const float*)getp(d, "head_b");
