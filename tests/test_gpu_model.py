@@ -469,29 +469,3 @@ def test_tconv_fused_norm_step(cuda_dev, monkeypatch, norm):
         d0 = 1.0 - _cos(g0[k].float(), ref[k])
         d2 = 1.0 - _cos(g2[k].float(), ref[k])
         assert d2 <= 2.0 * d0 + 1e-3, (k, d0, d2)
-
-
-@pytest.mark.parametrize("kw", [
-    dict(batch_size=4, img_size=64, in_channels=4),
-    dict(batch_size=4, img_size=128, in_channels=4, loss="dice_bce", hip_graph=True),
-    dict(batch_size=3, img_size=32, in_channels=1, use_upsampling=True),
-])
-def test_first_onload_step_equals_separate_first_conv(cuda_dev, monkeypatch, kw):
-    """first_onload=1 (default: the first conv computed per window inside conv1b's forward,
-    conv_win.h XF 6, which also stores its own-row outputs and ReLU bits) gives the
-    separate first-conv launch's step bit for bit: the first conv's output and bits, loss
-    sums, probabilities and every parameter gradient."""
-    outs = []
-    for v in ("0", "1"):
-        monkeypatch.setenv("UNET_ENGINE", "first_onload=" + v)
-        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
-        e = nb.engine
-        assert (e._first_onload is not None) == (v == "1")
-        assert ("fwd:conv1a" in e.plan.names()) == (v == "0")
-        for seed in (77, 78):
-            nb.fwd_bwd(x, y, seed=seed)
-        torch.cuda.synchronize()
-        outs.append((e.bufs["conv1a"].clone(), e.relu_bits["conv1a"].clone(), nb.sums().cpu(), e.prob.clone(),
-                     fn.grad.clone()))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)

@@ -29,12 +29,7 @@ def test_plan_construction_dry_run(kw, img, dtype):
     e = NativeUNet(spec, flat, 2, img, "cpu", bucket_bounds=b, dry_run=True, dtype=dtype)
     assert e.arena.dtype == e.adt and e.target.dtype == e.adt
     names = e.plan.names()
-    # (first_onload: the first conv runs inside conv1b's forward window, norm-free 2D
-    # models with a 4-channel padded input)
-    assert names[0] == ("fwd:conv1b" if e._first_onload else "fwd:conv1a") and names[e.fwd_end - 1] == "fwd:Mask"
-    assert ("fwd:conv1a" in names) == (e._first_onload is None)
-    assert (e._first_onload is not None) == (kw.get("dims", 2) == 2 and kw.get("norm", "none") == "none"
-                                             and kw["in_channels"] <= 4)
+    assert names[0] == "fwd:conv1a" and names[e.fwd_end - 1] == "fwd:Mask"
     if kw.get("dims", 2) == 2 and not kw.get("use_upsampling"):
         # default tconv_wa=1: the consumers' u-row weight gradients come from the chain rule
         # (skip-only wgrad); the forward keeps the tconv

@@ -31,7 +31,6 @@
 #include "conv_params.h"
 #include "conv_epilogue.h"
 #include "conv_win.h"
-#include "conv_pipe.h"
 
 namespace unet {
 
@@ -859,7 +858,7 @@ static bool tconv_dgrad_eligible(const ConvFwdParams& p) {
 }
 
 int conv_fwd_pick(const ConvFwdParams& p);
-static bool win_tile(int t) { return t == 6 || t == 12 || t == 14; }
+static bool win_tile(int t) { return t == 6 || t == 12; }
 
 // 2D 8 x 8 images, 3x3 'same', plain / concat source, no fused pool / head / transform
 // (the image-window kernel above); normalisation statistics per 4-image tile.
@@ -902,18 +901,10 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     return "conv_fwd: relu_bits needs an unsplit ReLU forward";
   if ((p.mask_bits & ~3) || ((p.mask_bits & 1) && !p.mask1) || ((p.mask_bits & 2) && !p.mask2))
     return "conv_fwd: mask_bits marks a missing mask";
-  if (p.xform == 3) {
-    // first layer on load (conv_win.h XF 6): a 32-channel first-conv output formed per
-    // window from the 4-channel input
-    const int t = conv_fwd_pick(p);
-    if (p.C1 != 32 || p.C2 || !p.fw || !p.fb || p.fcin != 4 || p.fkpad < 64 || p.fkpad % 64 || p.KD != 1 ||
-        p.OD != 1 || p.OW > 128 || !win_eligible(p) || (t != 6 && t != 12 && t != 14) || win_pipe(p) ||
-        conv_epi_mode(p) != EPI_FWD || p.head_w)
-      return "conv_fwd: first layer on load needs a 2D 32-channel ReLU row-window forward over a 4-channel input";
-  } else if (p.xform) {
+  if (p.xform) {
     const int ep = conv_epi_mode(p), t = conv_fwd_pick(p);
     if (p.xform != 1 || p.C2 || !p.xa || !p.xb || p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) ||
-        (t != 6 && t != 12 && t != 14) || (p.xcs != 0 && p.xcs != p.C1) || p.head_w || (ep != EPI_STATS && ep != EPI_GENERIC))
+        (t != 6 && t != 12) || (p.xcs != 0 && p.xcs != p.C1) || p.head_w || (ep != EPI_STATS && ep != EPI_GENERIC))
       return "conv_fwd: operand transform needs a 2D single-source row-window forward of a normalised input";
   }
   if (p.hg.prob && (!p.hg.t || !p.hg.sums || !p.hg.w || !p.hg.bits || p.C1 != 32 || p.C2 || p.xform ||
@@ -937,8 +928,8 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
         p.OH % 2 || p.OW % 2 || p.Cout % 8 || p.head_w)
       return "conv_fwd: fused max-pool needs a 2D row-window ReLU forward (even rows, codes buffer)";
   }
-  if (p.tile < 0 || p.tile > 14) return "conv_fwd: bad tile id";
-  if ((p.tile == 12 || p.tile == 14) && (!win_eligible(p) || p.Cout % 64 || p.head_w))
+  if (p.tile < 0 || p.tile > 13) return "conv_fwd: bad tile id";
+  if (p.tile == 12 && (!win_eligible(p) || p.Cout % 64 || p.head_w))
     return "conv_fwd: 64-wide row-window tile not applicable";
   if (p.tile == 10 && !tconv_fwd_eligible(p)) return "conv_fwd: transposed-conv window tile not applicable";
   if (p.tile == 11 && !tconv_dgrad_eligible(p)) return "conv_fwd: transposed-conv dgrad tile not applicable";
@@ -946,7 +937,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.tile == 13 && !img8_eligible(p)) return "conv_fwd: 8x8 image-window tile not applicable";
   {
     const int t = p.tile ? p.tile : 0;
-    const int bn = t == 1 ? 128 : (t == 2 || t == 5 || t == 7 || t == 12 || t == 13 || t == 14) ? 64 : 32;
+    const int bn = t == 1 ? 128 : (t == 2 || t == 5 || t == 7 || t == 12 || t == 13) ? 64 : 32;
     if (t && p.Cout % bn) return "conv_fwd: forced tile does not divide Cout";
     if (t == 7) return "conv_fwd: tile 7 (row-window 512x64: 268 registers, 92 KB LDS, 1 wave/SIMD) is not built";
     if (t == 6 && !win_eligible(p)) return "conv_fwd: row-window tile not applicable";
@@ -990,8 +981,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
 
 // tile ids: 1 = 128x128, 2 = 128x64, 3 = 256x32, 4 = 128x32, 5 = 256x64 (4 waves each);
 // 6 = row-window (auto tile width); 8 = auto but never row-window (A/B tests); 12 = row
-// window, 64-channel tile; 13 = 8x8 image window; 14 = row window, 4-wave 64-channel tile
-// (never the pipelined 8-wave window, conv_pipe.h)
+// window, 64-channel tile; 13 = 8x8 image window
 int conv_fwd_pick(const ConvFwdParams& p) {
   const int M = p.N * p.OD * p.OH * p.OW;
   if (p.tile && p.tile != 8) return p.tile;
@@ -1020,8 +1010,7 @@ void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
   const bool smallc = (p.C1 == 4 || p.C1 == 8) && p.C2 == 0;
   switch (t) {
     case 6:
-    case 12:
-    case 14: {       // row window: R rows x (segment) width, tiles in (row group, segment) order
+    case 12: {       // row window: R rows x (segment) width, tiles in (row group, segment) order
       const int W = p.OW > 128 ? 128 : p.OW;
       const int R = win_rows(p);
       if (p.nz && p.C2) return;
@@ -1067,8 +1056,6 @@ hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
     case 5: return launch_cfg<256, 64, 4, 1>(p, s);
     case 6:
     case 12:
-    case 14:
-      if (win_pipe(p)) return launch_pipe(p, s);
       if (win_bn(p) == 64) return launch_win<64, 256>(p, s);
       return win_bm(p) == 256 ? launch_win<32, 256>(p, s) : launch_win<32, 512>(p, s);
     case 9: return p.C1 == 4 ? launch_win_first<4>(p, s) : launch_win_first<8>(p, s);

@@ -96,28 +96,18 @@ struct ConvFwdParams {
   // coefficients [C] (xcs = 0, BatchNorm) or [N][C] (xcs = C, GroupNorm; a window lies
   // in one sample); xc / xz are unused by the conv.  xout (optional): the transformed operand's own-window rows are also
   // stored there (the weight gradient reads them), by output-channel tile 0.
-  //   xform 3: first layer on load (2D row-window forward of the first block's second conv,
-  //            32-channel operand): src1 = the network input x (fcin = 4 / 8 padded
-  //            channels), and the operand y = relu(conv3x3(x, fw) + fb) -- the first conv's
-  //            output -- is computed per window into the halo image by MFMAs; its own-row
-  //            values go to xout and their ReLU bits to fbits (output-channel tile 0).
   int xform, xcs;
   const float* xa;
   const float* xb;
   const float* xc;
   const void* xz;
   void* xout;
-  const void* fw;             // xform 3: first-conv weights [32][fkpad] (its forward layout)
-  const float* fb;            // xform 3: first-conv bias [32]
-  uint8_t* fbits;             // xform 3: first-conv ReLU bits (own rows)
-  int fcin, fkpad;
   int tile;                  // 0 = auto, else forced tile config id (tuning / A-B tests)
   // Fused segmentation head (row-window forward, Cout == 32, EPI_FWD only): per pixel
   // z = sum_c out[c] head_w[c] + head_b -> head_logit (fp32) for head_finish
   const float* head_w;
   const float* head_b;
   float* head_logit;
-  int pipe_off;               // 1: never the pipelined 8-wave window (conv_pipe.h; A/B runs)
   int rev;                    // row-window kernels: windows in reverse order (the consumer starts
                               // where its producer ended, on the tail still in the Infinity Cache)
   HeadGrad hg;                // 2D row-window data gradient of the head input: src1 (dY) formed

@@ -29,8 +29,6 @@
 
 namespace unet {
 
-hipError_t launch_wgrad_pipe(const WgradParams& p, hipStream_t s);   // wgrad_pipe.hip
-
 // splits handled by one launch: [split_lo, split_lo + split_n) of p.splits (0 = all)
 static inline int launch_splits(const WgradParams& p) { return p.split_n > 0 ? p.split_n : p.splits - p.split_lo; }
 
@@ -1610,10 +1608,6 @@ hipError_t wgrad_launch(const WgradParams& p0, hipStream_t s) {
     return hipGetLastError();
   }
   if (wgrad_win_eligible(p)) {
-    // 2D rows 16..64 wide: the pipelined 8-wave window (wgrad_pipe.hip; win 2 keeps the
-    // 4-wave kernel for A/B runs)
-    if (p.win == 0 && p.KD == 1 && p.QD == 1 && p.QW >= 16 && p.QW <= 64 && !p.hg.prob && !p.xform)
-      return launch_wgrad_pipe(p, s);
     const bool q2 = c.BN == 64;
     switch (p.QW) {
       case 8: return q2 ? launch_wgrad_win<8, 2>(p, s) : launch_wgrad_win<8, 1>(p, s);

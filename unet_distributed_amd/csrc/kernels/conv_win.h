@@ -21,27 +21,20 @@ enum { GEO_2D = 0, GEO_SEG = 1, GEO_3D = 2 };
 // halves the halo image's LDS-DMA and fragment reads per MFMA and doubles the MFMA work
 // per synchronisation.  tile 12 / 6 force 64 / 32 (tests).
 inline int win_bn(const ConvFwdParams& p) {
-  if (p.tile == 12 || p.tile == 14) return 64;
+  if (p.tile == 12) return 64;
   if (p.tile == 6) return 32;
   const int W = p.OW > 128 ? 128 : p.OW;
   return (p.Cout % 64 == 0 && W <= 64 && !p.head_w) ? 64 : 32;
 }
-// The 64-channel tile on 2D rows 16..64 wide runs the pipelined 8-wave window
-// (conv_pipe.h: double-buffered chunks, 512 pixels on 32 / 64-wide rows, 256 on 16-wide
-// ones) unless head-on-load needs the 4-wave kernel; tile 14
-// forces the 4-wave 64-channel window (bit-exactness tests), pipe_off = 1 keeps the 4-wave
-// kernel wherever the tile is auto (executor option conv_pipe=0: same-box A/B runs).
-inline bool win_pipe(const ConvFwdParams& p) {
-  return p.tile != 14 && !p.pipe_off && p.KD == 1 && p.OW <= 64 && win_bn(p) == 64 && (!p.xform || (p.xform == 1 && p.C1 <= 256)) &&
-         !p.hg.prob;
-}
-// Window pixels: 256 for 16-wide rows and for the 4-wave 64-channel tile (its
-// accumulators, 4 x 4 fragments per wave, and LDS then still fit two workgroups per CU),
-// else 512.  (A 256-pixel 32-channel window on 32..128-wide rows -- three workgroups per
-// CU -- measured -0.4 % at W = 64 and -1 % at 128 and was dropped.)
+// Window pixels: 256 for 16-wide rows and for the 64-channel tile (its accumulators,
+// 4 x 4 fragments per wave, and LDS then still fit two workgroups per CU), else 512.
+// (A 256-pixel 32-channel window on 32..128-wide rows -- three workgroups per CU --
+// measured -0.4 % at W = 64 and -1 % at 128 and was dropped; a pipelined 8-wave window
+// with double-buffered chunks, one workgroup per CU, measured -2..-21 % per launch at
+// levels 2-4 in round 4: two independent workgroups per CU already overlap one's DMA
+// wait with the other's MFMAs, AND its prologue / epilogue, which one workgroup cannot.)
 inline int win_bm(const ConvFwdParams& p) {
   const int W = p.OW > 128 ? 128 : p.OW;
-  if (win_pipe(p)) return W == 16 ? 256 : 512;
   return (W == 16 || win_bn(p) == 64) ? 256 : 512;
 }
 inline int win_rows(const ConvFwdParams& p) {
@@ -95,15 +88,11 @@ constexpr int NTHR = 256;
 // transformed operand go to xout); 3: head-on-load, the halo image of dY (32 channels)
 // is formed from the head's per-pixel probability, target and ReLU bits (p.hg,
 // head_grad.h) instead of being read from memory; 4: space-to-depth source (p.s2d: the
-// DMA gathers the fine pixels of each coarse slot, structurally zero taps skipped);
-// 6: first layer on load (conv_params.h xform 3): the halo image of the first conv's
-// 32-channel output is computed here from the 4-channel network input by MFMAs (the
-// first-layer window kernel's fragments and epilogue, bit for bit) -- that conv never
-// runs on its own and its output is never re-read by this one.
+// DMA gathers the fine pixels of each coarse slot, structurally zero taps skipped).
 template <int W, int BN, int BM, bool CONCAT, int EPI, int GEO, int XF = 0>
 __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   static_assert(BN == 32 || BN == 64, "row-window tile is 32 or 64 output channels wide");
-  static_assert(XF == 0 || ((XF == 1 || XF == 3 || XF == 4 || XF == 6) && GEO == GEO_2D && !CONCAT),
+  static_assert(XF == 0 || ((XF == 1 || XF == 3 || XF == 4) && GEO == GEO_2D && !CONCAT),
                 "operand transform: 2D single-source windows");
   constexpr int R = BM / W, HR = R + 2;
   // halo row pitch in 64-byte pixel slots: W + 2 columns rounded up to a multiple of 4
@@ -114,18 +103,14 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   // halo row, its row checks and row offset are wave-uniform (scalar), and a lane's
   // column / swizzle part is the same for every piece: a few VALU per piece instead of a
   // division by the pitch and 64-bit address math (73.7 KB LDS, still two WGs per CU)
-  constexpr bool ALR = GEO == GEO_2D && W == 128 && XF != 6;   // (XF 6: no halo DMA)
+  constexpr bool ALR = GEO == GEO_2D && W == 128;
   constexpr int HWP = ALR ? (W + 2 + 15) / 16 * 16 : W + 4;
   constexpr int PPR = HWP / 16;                 // DMA pieces per halo row (ALR)
   constexpr int ROWB = HWP * 64;
   constexpr int XI = (HR * HWP + 15) / 16, WI = 9 * BN / 16;
   constexpr int XB = XI * 1024, WB = WI * 1024;
   constexpr int EPIB = (EPI == EPI_STATS || EPI == EPI_DGRAD_NORM) ? epi_lds_bytes<BM, BN>() : BM * (BN + 4) * 2;
-  // XF 6: the network input's (R + 4)-row halo in the first-layer kernel's 8-byte slot
-  // layout (row pitch W + 4: [0] zero, [1] column -1, [2 .. W + 1] columns 0 .. W - 1, ...)
-  constexpr int FRS = W + 4;
-  constexpr int FXB = XF == 6 ? ((R + 4) * FRS * 8 + 1023) / 1024 * 1024 : 0;
-  constexpr int LDS_BYTES = (XB + WB + FXB > EPIB) ? XB + WB + FXB : EPIB;
+  constexpr int LDS_BYTES = (XB + WB > EPIB) ? XB + WB : EPIB;
   constexpr int WMP = BM / 4;                   // pixels per wave
   constexpr int TM = WMP / 16, TN = BN / 16;
   constexpr int TPR = W / 16;                   // 16-pixel tiles per row
@@ -325,49 +310,12 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
       const int cb = s2 ? (kc << 5) - sgrp * p.s2d : (from1 ? (kc << 5) : (kc << 5) - p.C1);
       const uint32_t s2d_taps = 0x1bu << (3 * (1 - sa) + (1 - sb));   // the 2 x 2 tap block
       if (kc) __syncthreads();
-      // XF 6: the first conv's weight fragments (A operand: its 32 output channels x
-      // K = 9 taps x 4 channels in two 32-wide K steps) and bias, from global
-      h16x8 fwf[2][2];
-      float fbias[2][4];
-      if constexpr (XF == 6) {
-        const __amdgpu_buffer_rsrc_t rsf = __builtin_amdgcn_make_buffer_rsrc((void*)p.fw, (short)0, OOB, 0x00020000);
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            fwf[s][j] = __builtin_bit_cast(
-                h16x8, __builtin_amdgcn_raw_buffer_load_b128(rsf, ((16 * j + fr) * p.fkpad + 32 * s + 8 * fsub) * 2, 0, 0));
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) fbias[j][r] = p.fb[16 * j + 4 * fsub + r];
-        // the input halo: 16-byte chunk u = two 8-byte slots of row u / FCPR (columns
-        // 2c - 2, 2c - 1 of input row g0 - 2 + row)
-        constexpr int FCPR = FRS * 8 / 16, FXI = ((R + 4) * FCPR + 63) / 64;
-        const char* xb0 = (const char*)p.src1 + (size_t)grow0 * W * 8;
-        const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc((void*)xb0, (short)0, OOB, 0x00020000);
-#pragma unroll
-        for (int q = 0; q < (FXI + 3) / 4; ++q) {
-          const int k = wave + 4 * q;
-          if (k < FXI) {
-            const int u = 64 * k + lane;
-            const int hr = u / FCPR, c = u - hr * FCPR;
-            const int gr = g0 - 2 + hr;
-            const int col = 2 * c - 2;
-            const bool ok = hr < R + 4 && gr >= grow0 && gr < grow0 + H && (unsigned)gr < (unsigned)rows_total &&
-                            (unsigned)col < (unsigned)W;
-            const int off = ok ? ((gr - grow0) * W + col) * 8 : OOB;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rsx, (__attribute__((address_space(3))) void*)(smem + XB + WB + k * 1024), 16, off, 0, 0, 0);
-          }
-        }
-      }
       {
         const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
 #pragma unroll
         for (int q = 0; q < (XI + 3) / 4; ++q) {
           const int k = wave + 4 * q;
-          if (XF != 3 && XF != 6 && k < XI) {
+          if (XF != 3 && k < XI) {
             int hr, hc;
             if constexpr (ALR) {
               hr = k / PPR;                                 // wave-uniform
@@ -456,59 +404,6 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
         }
       }
       __syncthreads();
-      if constexpr (XF == 6) {
-        // first conv, one 16-pixel tile of one halo row per step: y = relu(conv(x) + b)
-        // for halo rows inside the window's image, zero elsewhere (the 'same' padding of
-        // this conv's input); columns -1 / W (slots 0, W + 1) are zeroed below
-        const char* Fx = smem + XB + WB;
-        constexpr int NT1 = HR * TPR;
-#pragma unroll 1
-        for (int t = wave; t < NT1; t += 4) {
-          const int hr = t / TPR, cw = (t - hr * TPR) * 16 + fr;
-          const int gr = g0 - 1 + hr;
-          const bool row_ok = (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)gr < (unsigned)rows_total;
-          const int h = gr - grow0;                           // row within the image
-          const bool tok = h > 0, bok = h < H - 1;
-          f32x4 a1[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            u32x4 v;
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-              const int tp = 8 * s + 2 * fsub + hh;           // tap of this 4-channel half
-              const int dh = tp / 3, dw = tp - 3 * dh;
-              const bool ok = tp < 9 && (dh != 0 || tok) && (dh != 2 || bok);
-              const int slot = (hr + dh) * FRS + cw + dw + 1;
-              const u32x2 h2 = *(const u32x2*)(Fx + (ok ? slot * 8 : 0));
-              v[2 * hh] = h2[0];
-              v[2 * hh + 1] = h2[1];
-            }
-            const h16x8 xf = __builtin_bit_cast(h16x8, v);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) a1[j] = mfma16(fwf[s][j], xf, a1[j]);
-          }
-          // lane: pixel cw, channels 16 j + 4 fsub .. + 3 -> half (fsub & 1) of chunk
-          // 2 j + (fsub >> 1) of slot (hr, cw + 1)
-          const int hc = cw + 1;
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const f32x2 a01 = (f32x2){a1[j][0], a1[j][1]} + (f32x2){fbias[j][0], fbias[j][1]};
-            const f32x2 a23 = (f32x2){a1[j][2], a1[j][3]} + (f32x2){fbias[j][2], fbias[j][3]};
-            u32x2 pk;
-            pk[0] = row_ok ? relu2h(pack2h(a01[0], a01[1])) : 0u;
-            pk[1] = row_ok ? relu2h(pack2h(a23[0], a23[1])) : 0u;
-            const int c = 2 * j + (fsub >> 1);
-            *(u32x2*)(Xs + (hr * HWP + hc) * 64 + 16 * (c ^ ((hc >> 1) & 3)) + 8 * (fsub & 1)) = pk;
-          }
-        }
-        // the padding columns -1 and W of every halo row
-        if (tid < HR * 2 * 4) {
-          const int hr = tid >> 3, side = (tid >> 2) & 1, k = tid & 3;
-          const int hc = side ? W + 1 : 0;
-          *(u32x4*)(Xs + (hr * HWP + hc) * 64 + 16 * k) = (u32x4){0u, 0u, 0u, 0u};
-        }
-        __syncthreads();
-      }
       if constexpr (XF == 1) {
         float xa[8], xb[8];
 #pragma unroll
@@ -537,36 +432,6 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
         __syncthreads();
       }
       chunk_mfmas(XF == 4 ? s2d_taps : 0x1ffu);
-      if constexpr (XF == 6) {
-        // the first conv's own-row outputs (output-channel tile 0): values -> xout (the
-        // weight gradient reads them), ReLU bits -> fbits (its data gradient's mask)
-        if (tn == 0) {
-#pragma unroll
-          for (int j = 0; j < (R * W + NTHR - 1) / NTHR; ++j) {
-            const int pp = tid + NTHR * j;
-            if (pp >= R * W) break;
-            const int rr = pp / W, col = pp - rr * W;
-            const int gr = g0 + rr;
-            if (gr >= rows_total) continue;
-            const int hc = col + 1, sw = (hc >> 1) & 3;
-            const char* sp = Xs + ((rr + 1) * HWP + hc) * 64;
-            u32x4 v[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = *(const u32x4*)(sp + 16 * (k ^ sw));
-            const size_t q = (size_t)gr * W + col;
-            if (p.xout) {
-#pragma unroll
-              for (int k = 0; k < 4; ++k) *(u32x4*)((h16*)p.xout + q * 32 + 8 * k) = v[k];
-            }
-            if (p.fbits) {
-              uint32_t b = 0;
-#pragma unroll
-              for (int k = 0; k < 4; ++k) b |= (pos_bits_relu(v[k]) & 0xffu) << (8 * k);
-              ((uint32_t*)p.fbits)[q] = b;
-            }
-          }
-        }
-      }
     }
   }
   __syncthreads();
@@ -623,12 +488,7 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
 #define XF_CASE(WW)                                                                                           \
   case WW:                                                                                                    \
     if constexpr (win_tile_built<BN, BM>(WW)) {                                                               \
-      if (p.xform == 3) {                                                                                     \
-        if (epi == EPI_FWD)                                                                                   \
-          hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_FWD, GEO_2D, 6>), dim3(grid), dim3(NTHR), 0, s, p); \
-        else                                                                                                  \
-          return hipErrorInvalidValue;                                                                        \
-      } else if (epi == EPI_STATS)                                                                            \
+      if (epi == EPI_STATS)                                                                                   \
         hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_STATS, GEO_2D, 1>), dim3(grid), dim3(NTHR), 0, s, p); \
       else if (epi == EPI_GENERIC)                                                                            \
         hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_GENERIC, GEO_2D, 1>), dim3(grid), dim3(NTHR), 0, s, p); \

@@ -101,7 +101,6 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.salt = get<uint32_t>(d, "salt", 0u);
   p.drop_idx0 = get<unsigned long long>(d, "drop_idx0", 0ull);
   p.rev = get<int>(d, "rev", 0);
-  p.pipe_off = get<int>(d, "pipe_off", 0);
   p.dst1 = const_cast<void*>(getp(d, "dst1"));
   p.dst2 = const_cast<void*>(getp(d, "dst2"));
   p.D1 = get<int>(d, "D1", p.Cout);
@@ -131,11 +130,6 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.xz = getp(d, "xz");
   p.s2d = get<int>(d, "s2d", 0);
   p.xout = const_cast<void*>(getp(d, "xout"));
-  p.fw = getp(d, "fw");
-  p.fb = (const float*)getp(d, "fb");
-  p.fbits = (uint8_t*)const_cast<void*>(getp(d, "fbits"));
-  p.fcin = get<int>(d, "fcin", 0);
-  p.fkpad = get<int>(d, "fkpad", 0);
   p.tile = get<int>(d, "tile", 0);
   p.head_w = (const float*)getp(d, "head_w");
   p.head_b = (const float*)getp(d, "head_b");

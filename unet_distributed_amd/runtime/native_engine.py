@@ -59,14 +59,7 @@ def _r64(k: int) -> int:
 #   tconv_fused  deepest fine level whose transposed conv runs the composite backward (2; 0 off)
 #   tconv_wa     the consumer conv's u-row weight gradient from the composite backward's
 #                slab sums (1; 0: full weight gradient over u)
-#   conv_pipe    64-channel row windows on 16..64-wide rows run the pipelined 8-wave kernel
-#                (conv_pipe.h: double-buffered chunks; 0: the 4-wave window)
-#   wgrad_pipe   row-window weight gradients on 16..64-wide rows run the pipelined 8-wave
-#                kernel (wgrad_pipe.hip: double-buffered windows; 0: the 4-wave window)
-#   first_onload the first conv's output is formed on load inside the second conv's forward
-#                (conv_win.h XF 6): no separate first-conv launch, no re-read of its output
-ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
-                       conv_pipe=1, wgrad_pipe=1, first_onload=1)
+ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1)
 
 
 def engine_options(overrides: Optional[Dict[str, int]] = None) -> Dict[str, int]:
@@ -339,7 +332,6 @@ class NativeUNet:
                     self.relu_bits[l.name] = torch.zeros(self.npix(l.level) * l.cout // 8, dtype=torch.uint8,
                                                          device=self.device)
         self._plan_tconv_fused()
-        self._plan_first_onload()
         P = self.npix(1)
         self.prob = torch.zeros(P, dtype=torch.float32, device=self.device)
         nb = self.C.head_blocks(P)
@@ -422,29 +414,6 @@ class NativeUNet:
                                             bs=torch.zeros(16 * O, dtype=torch.float32, device=self.device))
             self._tf_consumer[c.name] = l.name
             self._plan_wa_chain(l, c, self.tconv_fused[l.name])
-
-    def _plan_first_onload(self):
-        """Option first_onload: the first conv (4-channel input -> 32 channels, norm-free
-        2D model) runs inside its consumer's forward window (conv_win.h XF 6); that
-        consumer also stores the first conv's own-row outputs (its weight gradient's A
-        operand) and ReLU bits (its data gradient's mask)."""
-        self._first_onload = None
-        first = self.spec.layers[0]
-        if (not self.opts["first_onload"] or self.dims != 2 or self.spec.norm != "none" or self.cpad != 4
-                or first.kind != "conv" or first.cout != 32 or self.img not in (16, 32, 64, 128)):
-            return
-        cons = [l for l in self.spec.layers if l.kind == "conv" and self.inputs.get(l.name, ("",))[0] == first.name]
-        if len(cons) != 1 or self.inputs[cons[0].name][2] is not None or (first.dropout and self.spec.dropout > 0):
-            return
-        c = cons[0]
-        d = self._conv_common(c.level, 3, 1, 1)
-        d.update(C1=32, src1=1, wgt=1, bias=1, Cout=c.cout, relu=1, dst1=1, xform=3, fw=1, fb=1, fcin=4, fkpad=64)
-        try:
-            if self.C.conv_fwd_grid(d) <= 0:
-                return
-        except ValueError:
-            return
-        self._first_onload = (first.name, c.name)
 
     def fuse_norm_stats_planned(self):
         """Normalised model: every conv epilogue writes its statistics (the composite
@@ -759,7 +728,7 @@ class NativeUNet:
         idd, ih, iw = self.sdims(in_level or level)
         kd = K if self.dims == 3 else 1
         return dict(N=self.B, OD=od, OH=oh, OW=ow, ID=idd, IH=ih, IW=iw, KD=kd, KH=K, KW=K,
-                    stride=stride, pad=pad, tile=0, pipe_off=1 - self.opts["conv_pipe"])
+                    stride=stride, pad=pad, tile=0)
 
     def _salt(self, lname):
         return [l.name for l in self.spec.layers].index(lname)
@@ -886,10 +855,7 @@ class NativeUNet:
         def P(t):
             return None if t is None else _ptr(b[t]) + self._toff(t, c, nb)
 
-        fo = getattr(self, "_first_onload", None)
-        if l.kind == "conv" and fo is not None and l.name == fo[0]:
-            pass                                 # formed on load by its consumer's forward
-        elif l.kind == "conv":
+        if l.kind == "conv":
             src1, up1, skip = self.inputs[l.name]
             c1 = self.tinfo[src1][1]
             s1 = P(src1)
@@ -917,13 +883,6 @@ class NativeUNet:
             bits = self.relu_bits.get(l.name)
             if bits is not None and not normed:
                 d["relu_bits"] = _ptr(bits) + c * nb * (self.npix(l.level) // self.B) * l.cout // 8
-            if fo is not None and l.name == fo[1]:
-                # the first conv on load: src1 is the network input; its outputs of this
-                # window's rows and their ReLU bits are stored for the backward
-                first = fo[0]
-                d.update(xform=3, src1=P("x"), fw=self.wptr(first), fb=self.master_ptr(first + "/bias"), fcin=4,
-                         fkpad=_r64(9 * 4), xout=P(first),
-                         fbits=_ptr(self.relu_bits[first]) + c * nb * (self.npix(1) // self.B) * 32 // 8)
             pool = self._pool_of.get(l.name)
             if pool is not None and not normed and (nch == 1 or self._fwd2_active(plan)):
                 # fused 2x2 max-pool: the epilogue writes the pooled tensor + argmax codes
@@ -1403,8 +1362,7 @@ class NativeUNet:
                     raise RuntimeError("head-on-load: the head input's weight gradient needs the fused-bias "
                                        "tile (its dY is never materialised for a column-sum pass)")
                 d.update(name="wgrad:" + w["lname"], M1=w["M1"], M2=w["M2"], Nc=w["Nc"], splits=splits,
-                         win=self.wgrad_win if (self.wgrad_win < 0 or self.opts["wgrad_pipe"]) else 2,
-                         slab=slab, bias_mode=w["bias_mode"] if fused_bias else 0,
+                         win=self.wgrad_win, slab=slab, bias_mode=w["bias_mode"] if fused_bias else 0,
                          bias_slab=bslab)
                 if part is not None:
                     d.update(split_lo=part * splits // 2, split_n=splits // 2)
