@@ -97,7 +97,26 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     if constexpr (SEGW > 0) return (m0 + ml / SEGW) * pitch + col0 + (ml % SEGW);
     else return m0 + ml;
   };
-  constexpr int EPI_STRIDE = (BN + 4) * 2;          // bytes; 8B-aligned, conflict-free b64 writes
+  // Staging tile rows (pixels).  BN = 32: unpadded 64-byte rows, 16-byte chunk c of pixel ml
+  // at c ^ ((ml >> 2) & 3) -- conflict-free for the register phase's 8-byte writes (16
+  // pixels x 2 halves of one chunk per 32 lanes) and for the 16-byte chunk reads of the
+  // coalesced phase (4 lanes per pixel); the padded 72-byte rows it replaces left 2-way
+  // conflicts in both (15-23 % LDS conflict cycles on the level-1 windows, r3_pmc_table.md).
+  // Wider tiles: rows padded by 8 bytes.
+  constexpr bool ESWZ = BN == 32;
+  constexpr int EPI_STRIDE = ESWZ ? 64 : (BN + 4) * 2;
+  auto eoff = [](const int ml, const int chunk) -> int {
+    return ESWZ ? ml * 64 + 16 * (chunk ^ ((ml >> 2) & 3)) : ml * EPI_STRIDE + 16 * chunk;
+  };
+  auto eread = [&](const int ml, const int chunk) -> u32x4 {
+    if constexpr (ESWZ) {
+      return *(const u32x4*)(smem + eoff(ml, chunk));
+    } else {
+      const u32x2 lo = *(const u32x2*)(smem + eoff(ml, chunk));
+      const u32x2 hi = *(const u32x2*)(smem + eoff(ml, chunk) + 8);
+      return (u32x4){lo[0], lo[1], hi[0], hi[1]};
+    }
+  };
   // register phase: acc[i][j][r] = out[pixel = m0 + wm*WM + i*16 + (lane&15)]
   //                                   [chan  = n0 + wn*WN + j*16 + (lane>>4)*4 + r]
   char* E = smem;
@@ -136,7 +155,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
         u32x2 pk;
         pk[0] = relu2h(pack2h(a01[0], a01[1]));
         pk[1] = relu2h(pack2h(a23[0], a23[1]));
-        *(u32x2*)(E + ml * EPI_STRIDE + nl * 2) = pk;
+        *(u32x2*)(E + eoff(ml, nl >> 3) + 2 * (nl & 7)) = pk;
       }
       continue;
     }
@@ -159,7 +178,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       u32x2 pk;
       pk[0] = pack2h(v[0], v[1]);
       pk[1] = pack2h(v[2], v[3]);
-      *(u32x2*)(E + ml * EPI_STRIDE + nl * 2) = pk;
+      *(u32x2*)(E + eoff(ml, nl >> 3) + 2 * (nl & 7)) = pk;
     }
   }
   __syncthreads();
@@ -211,9 +230,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       const int ml = ml0 + it * RPI;
       const int q = qof(ml);
       if (q >= M) continue;
-      const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
-      const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
-      const u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
+      const u32x4 v = eread(ml, cb);
       *(u32x4*)(dst + (size_t)q * p.Cout + n) = v;
       float f[8];
       unpack8(v, f);
@@ -280,10 +297,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       const int ml = ml0 + it * RPI;
       const int q = qof(ml);
       if (q >= M) continue;
-      const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
-      const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
       float g[8], z[8];
-      unpack8((u32x4){lo[0], lo[1], hi[0], hi[1]}, g);
+      unpack8(eread(ml, cb), g);
       unpack8(zv[it], z);
       if (route) {
         float gg[8];
@@ -361,9 +376,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       const int ml = ml0 + it * RPI;
       const int q = qof(ml);
       if (q >= M) continue;
-      const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
-      const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
-      u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
+      u32x4 v = eread(ml, cb);
       if (mk) v = mbit ? keep_bits(v, mb[it]) : keep_pos(v, mv[it]);
       if (route) {
         // the (masked, 16-bit rounded) skip gradient plus the routed pool gradient,
@@ -415,9 +428,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     const int q = qof(ml);
     if (q >= M) continue;
     const int n = n0 + cb * 8;
-    const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
-    const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
-    u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
+    u32x4 v = eread(ml, cb);
     size_t off;
     h16* dst;
     const void* mk;
@@ -520,9 +531,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           const int ml = ml00 + (kk >> 1) * TROW + (kk & 1);
-          const u32x2 lo = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16);
-          const u32x2 hi = *(const u32x2*)(E + ml * EPI_STRIDE + cb * 16 + 8);
-          const u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
+          const u32x4 v = eread(ml, cb);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             key[2 * e] = max(key[2 * e], (int32_t)((v[e] << 16) | (3u - kk)));
