@@ -133,3 +133,69 @@ def test_composite_tconv_weight_grads(cuda_dev, N, H, K, Cc, Cs, O, splits, win)
     assert rel_err(dwa, ref_wa) < 1e-3
     assert torch.equal(dwa[:, :, Cc:, :], skg)
 
+
+
+def _pad64(m):
+    k = m.shape[1]
+    out = torch.zeros(m.shape[0], (k + 63) // 64 * 64, dtype=m.dtype, device=m.device)
+    out[:, :k] = m
+    return out
+
+
+@pytest.mark.parametrize("N,H,K,Cc,Cs,O,epi", [(2, 64, 64, 32, 32, 32, "fwd"), (2, 32, 128, 64, 64, 64, "fwd"),
+                                                (3, 16, 64, 32, 32, 64, "fwd"), (2, 64, 64, 32, 32, 32, "stats"),
+                                                (2, 32, 128, 64, 64, 64, "generic"), (2, 32, 32, 32, 32, 32, "fwd")])
+def test_tconv_onload_forward(cuda_dev, N, H, K, Cc, Cs, O, epi):
+    """Decoder forward z = conv3x3([tconv(b) + bt, skip]) with u formed on load from the
+    coarse b (conv_win.h XF 5, fine rows 32..128 wide): bit-identical to the
+    materialised tconv_fwd + concat conv (same MFMA operands and order), and vs fp32
+    ATen conv_transpose2d + conv2d.  epi: ReLU forward with bits, normalisation
+    statistics (pre-norm z), dropout (generic epilogue)."""
+    b, skip, wt, bt, wa, _ = _problem(cuda_dev, N, H, K, Cc, Cs, O, 21)
+    dev = cuda_dev
+    F2 = 2 * H
+    wtp = _pad64(wt.reshape(4 * Cc, K).bfloat16())                      # [tap][co] rows, K padded
+    wap = _pad64(wa.bfloat16().permute(3, 0, 1, 2).reshape(O, 9 * (Cc + Cs)))
+    ba = torch.randn(O, device=dev) * 0.1
+    u = torch.empty(N, F2, F2, Cc, device=dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(N=N, OH=H, OW=H, IH=H, IW=H, C1=K, src1=ptr(b), wgt=ptr(wtp), bias=ptr(bt), Cout=4 * Cc,
+                      shuffle=2, dst1=ptr(u)), stream())
+    base = dict(N=N, OH=F2, OW=F2, IH=F2, IW=F2, KH=3, KW=3, pad=1, C1=Cc, C2=Cs, src2=ptr(skip), wgt=ptr(wap),
+                bias=ptr(ba), Cout=O)
+    outs = []
+    for onload in (False, True):
+        z = torch.full((N, F2, F2, O), float("nan"), device=dev, dtype=torch.bfloat16)
+        d = dict(base, dst1=ptr(z))
+        extra = []
+        if epi == "fwd":
+            bits = torch.zeros(N * F2 * F2 * O // 8, device=dev, dtype=torch.uint8)
+            d.update(relu=1, relu_bits=ptr(bits))
+            extra.append(bits)
+        elif epi == "stats":
+            rows, _ = C().conv_stat_tiles(dict(d, src1=1, stats=1))
+            st = torch.zeros(rows * 2 * O, device=dev)
+            d.update(stats=ptr(st))
+            extra.append(st)
+        else:
+            d.update(relu=1, drop_rate=0.25, seed=7, salt=3)
+        if onload:
+            d.update(src1=ptr(b), ut_x=ptr(b), ut_w=ptr(wtp), ut_b=ptr(bt), ut_C=K, ut_kpad=wtp.shape[1])
+        else:
+            d.update(src1=ptr(u))
+        C().conv_fwd(d, stream())
+        torch.cuda.synchronize()
+        outs.append([z] + extra)
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
+    ref_u = F.conv_transpose2d(nchw(b.float()), wt.bfloat16().float().permute(3, 2, 0, 1), bt, stride=2)
+    ref = F.conv2d(torch.cat([ref_u, nchw(skip.float())], 1), wa.bfloat16().float().permute(3, 2, 0, 1), ba,
+                   padding=1)
+    z = outs[1][0].float()
+    if epi == "fwd":
+        assert rel_err(z, nhwc(F.relu(ref))) < 2e-2
+    elif epi == "stats":
+        assert rel_err(z, nhwc(ref)) < 2e-2
+    else:
+        kept = z != 0
+        assert rel_err(z[kept] * 0.75, nhwc(F.relu(ref))[kept]) < 2e-2
+

@@ -32,10 +32,14 @@ def test_plan_construction_dry_run(kw, img, dtype):
     assert names[0] == "fwd:conv1a" and names[e.fwd_end - 1] == "fwd:Mask"
     if kw.get("dims", 2) == 2 and not kw.get("use_upsampling"):
         # default tconv_wa=1: the consumers' u-row weight gradients come from the chain rule
-        # (skip-only wgrad); the forward keeps the tconv
+        # (skip-only wgrad); tconv_onload=1: nothing else reads u, so the consumers' forwards
+        # form it on load -- no tconv forward launch, no fine tconv output
         assert sorted(e._wa_chain_of.values()) == ["transConv8", "transConv9"]
         for cons in e._wa_chain_of:
             assert names.index("chain:" + e._wa_chain_of[cons]) > names.index("wgrad:" + cons)
+        assert sorted(e._ut_onload.values()) == ["transConv9"]          # (default: level 1)
+        for t in e._ut_onload.values():
+            assert "fwd:" + t not in names and t not in e.bufs
     # (head-on-load: the head backward only reduces the Mask gradients, on the side stream)
     nc = len(e.tconv_fused)
     assert [n for n in names[e.fwd_end:e.fwd_end + nc]] == ["compose:" + t for t in e.tconv_fused]
@@ -79,6 +83,19 @@ def test_host_side_shape_validation_rejects_bad_shapes():
         C.generic("pool_fwd", [1, 1], [1, 1, 8, 8, 12, 0], [], 0)
 
 
+def test_tconv_onload_host_checks():
+    """Transposed-conv source on load (conv_win.h XF 5): a 2D concat row-window forward,
+    rows 32..128 wide, (W / 32) (C / 32) <= 8 coarse-fragment registers per row."""
+    C = native.require()
+    base = dict(N=1, OH=128, OW=128, IH=128, IW=128, KH=3, KW=3, pad=1, C1=32, C2=32, src1=1, src2=1, wgt=1,
+                dst1=1, Cout=32, relu=1, ut_x=1, ut_w=1, ut_b=1, ut_C=64, ut_kpad=64)
+    assert C.conv_fwd_grid(base) == 32
+    for bad in (dict(ut_C=128, ut_kpad=128), dict(C2=0, src2=None), dict(OH=16, OW=16, IH=16, IW=16),
+                dict(ut_C=48), dict(ut_kpad=32)):
+        with pytest.raises(ValueError):
+            C.conv_fwd_grid(dict(base, **bad))
+
+
 def test_bucket_plan_is_layer_aligned_and_covers_buffer():
     spec = UNetSpec()
     flat = FlatParams(spec)
@@ -119,6 +136,25 @@ def test_head_onload_plan_allocates_no_head_input_gradient():
     assert e.head_onload and "d:" + e.head_in not in e.bufs
     e0 = NativeUNet(spec, FlatParams(spec), 2, 64, "cpu", dry_run=True, opts=dict(head_onload=0))
     assert not e0.head_onload and "d:" + e0.head_in in e0.bufs
+
+
+def test_tconv_onload_plan_option():
+    """tconv_onload=0 (or no chained u-row weight gradient, which reads u) keeps the
+    materialised transposed-conv forward and its output tensor."""
+    from unet_distributed_amd.runtime.native_engine import NativeUNet
+    spec = UNetSpec(in_channels=4)
+    for opts in (dict(tconv_onload=0), dict(tconv_wa=0)):
+        e = NativeUNet(spec, FlatParams(spec), 2, 64, "cpu", dry_run=True, opts=opts)
+        names = e.plan.names()
+        assert not e._ut_onload
+        for t in ("transConv8", "transConv9"):
+            assert "fwd:" + t in names and t in e.bufs
+    e = NativeUNet(spec, FlatParams(spec), 2, 128, "cpu", dry_run=True, opts=dict(tconv_onload=2))
+    assert sorted(e._ut_onload) == ["conv8a", "conv9a"]
+    # (the eval plan forms u on load too)
+    assert not {"fwd:transConv8", "fwd:transConv9"} & set(e.eval_plan.names())
+    e = NativeUNet(spec, FlatParams(spec), 2, 128, "cpu", dry_run=True)
+    assert sorted(e._ut_onload) == ["conv9a"] and "transConv8" in e.bufs
 
 
 def test_fused_head_plan():

@@ -427,122 +427,147 @@ hipError_t launch_img8(const ConvFwdParams& p, hipStream_t s) {
 // Taps past the ninth and taps whose input row leaves the output row's image read the
 // always-zero slot 0.  Halo slot layout per row: [0] zero, [1] column -1 (zero),
 // [2 .. W+1] columns 0 .. W-1, [W+2] column W (zero), [W+3] pad.
+//
+// A workgroup runs FWPW consecutive windows: the next window's halo (6 KB) is loaded into
+// registers while the current one's MFMAs and epilogue run, and written to LDS after the
+// epilogue -- the load latency a one-window workgroup exposes before its few MFMAs is
+// hidden, and the epilogue's stores stream back to back.  (Register staging, not LDS-DMA:
+// the compiler then counts the loads past the epilogue's stores itself.)
+constexpr int FWPW = 8;
 template <int W, int CIN, int EPI>
-__global__ void __launch_bounds__(NTHR) conv_win_first_kernel(const ConvFwdParams p) {
+__global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) conv_win_first_kernel(const ConvFwdParams p) {
   constexpr int BM = 512, R = BM / W, HR = R + 2, RS = W + 4;   // row pitch in slots
   constexpr int SB = 2 * CIN;                                  // slot bytes
   constexpr int ROWB = RS * SB;
   constexpr int CPR = ROWB / 16;                               // 16-byte chunks per halo row
-  constexpr int XI = (HR * CPR + 63) / 64;                     // LDS-DMA wave-instructions
-  constexpr int XB = XI * 1024;
+  constexpr int NCH = HR * CPR;                                // halo chunks
+  constexpr int CPT = (NCH + NTHR - 1) / NTHR;                 // chunks per thread
+  constexpr int XB = (NCH * 16 + 1023) / 1024 * 1024;
   constexpr int BN = 32, TM = 8, TN = 2;
   constexpr int KS = (9 * CIN + 31) / 32;                      // MFMA K-steps
   constexpr int EPIB = (EPI == EPI_STATS) ? epi_lds_bytes<BM, BN>() : BM * (BN + 4) * 2;
-  constexpr int LDS_BYTES = XB > EPIB ? XB : EPIB;
   constexpr int TPR = W / 16;
   static_assert((CIN == 4 || CIN == 8) && W >= 16 && W <= 128 && BM % W == 0, "first-layer window");
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  __shared__ __attribute__((aligned(1024))) char smem[XB + EPIB];
   char* Xs = smem;
+  char* Es = smem + XB;                                        // epilogue staging
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = p.OH;
   const int rows_total = p.N * H;
   const int M = rows_total * W;
   const int tiles_n = p.Cout / BN;
+  const int nwin = ((rows_total + R - 1) / R) * tiles_n;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
-  const int g0 = tm * R;
-  const int m0 = g0 * W, n0 = tn * BN;
+  const int w_lo = bid * FWPW, w_hi = w_lo + FWPW < nwin ? w_lo + FWPW : nwin;
   constexpr int OOB = 0x7fffffff;
   const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)p.src1, (short)0, OOB, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
 
-  // halo DMA: chunk u of the image = row u / CPR, 16 bytes = slots covering columns
-  // (CIN 4) 2c - 2, 2c - 1  or  (CIN 8) c - 2, c = u % CPR
+  // halo chunk u = row u / CPR, 16 bytes = slots covering columns (CIN 4) 2c - 2, 2c - 1
+  // or (CIN 8) c - 2, c = u % CPR; out-of-range chunks load zeros
+  u32x4 hv[CPT];
+  auto load_halo = [&](const int w) {
+    const int g0 = (w / tiles_n) * R;
 #pragma unroll
-  for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
-    const int k = wave + 4 * qq;
-    if (k < XI) {
-      const int u = 64 * k + lane;
-      const int hr = u / CPR, c = u - hr * CPR;
+    for (int c = 0; c < CPT; ++c) {
+      const int u = tid + NTHR * c;
+      const int hr = u / CPR, cc = u - hr * CPR;
       const int gr = g0 - 1 + hr;
-      const int col = CIN == 4 ? 2 * c - 2 : c - 2;
-      const bool ok = hr < HR && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
-      const int off = ok ? ((gr * W + col) * CIN) * 2 : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs1, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16, off,
-                                               0, 0, 0);
+      const int col = CIN == 4 ? 2 * cc - 2 : cc - 2;
+      const bool ok = u < NCH && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+      hv[c] = __builtin_amdgcn_raw_buffer_load_b128(rs1, ok ? ((gr * W + col) * CIN) * 2 : OOB, 0, 0);
     }
-  }
+  };
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int u = tid + NTHR * c;
+      if (u < NCH) *(u32x4*)(Xs + u * 16) = hv[c];
+    }
+  };
   // weight fragments (B operand: k = 32 s + 8 (lane >> 4) .. + 7, n = lane & 15), from global
   const int fsub = lane >> 4, fr = lane & 15;
   h16x8 wf[KS][TN];
+  auto load_w = [&](const int n0) {
 #pragma unroll
-  for (int s = 0; s < KS; ++s)
+    for (int s = 0; s < KS; ++s)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
-          rsw, ((n0 + 16 * j + fr) * p.Kpad + 32 * s + 8 * fsub) * 2, 0, 0);
-      wf[s][j] = __builtin_bit_cast(h16x8, v);
-    }
-
-  const int rw0 = (128 * wave) / W;
-  uint32_t top_ok = 0, bot_ok = 0, live = 0;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int g = g0 + rw0 + (i / TPR);
-    const int h = g % H;
-    if (g < rows_total) live |= 1u << i;
-    if (h > 0) top_ok |= 1u << i;
-    if (h < H - 1) bot_ok |= 1u << i;
-  }
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < TN; ++j) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+            rsw, ((n0 + 16 * j + fr) * p.Kpad + 32 * s + 8 * fsub) * 2, 0, 0);
+        wf[s][j] = __builtin_bit_cast(h16x8, v);
+      }
+  };
+  if (w_lo >= w_hi) return;
+  load_halo(w_lo);
+  load_w((w_lo % tiles_n) * BN);
+  store_halo();
   __syncthreads();
-
+  const int rw0 = (128 * wave) / W;
+  for (int w = w_lo; w < w_hi; ++w) {
+    const int tm = w / tiles_n, tn = w - tm * tiles_n;
+    const int g0 = tm * R, m0 = g0 * W, n0 = tn * BN;
+    if (w > w_lo && tiles_n > 1) load_w(n0);
+    if (w + 1 < w_hi) load_halo(w + 1);                      // lands under this window's work
+    uint32_t top_ok = 0, bot_ok = 0, live = 0;
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    if (!((live >> i) & 1u)) continue;
-    const int rr = rw0 + i / TPR;                       // window row of this 16-pixel tile
-    const int cw = ((128 * wave) % W) + (i % TPR) * 16 + fr;   // this lane's output column
-    const bool tok = (top_ok >> i) & 1u, bok = (bot_ok >> i) & 1u;
+    for (int i = 0; i < TM; ++i) {
+      const int g = g0 + rw0 + (i / TPR);
+      const int h = g % H;
+      if (g < rows_total) live |= 1u << i;
+      if (h > 0) top_ok |= 1u << i;
+      if (h < H - 1) bot_ok |= 1u << i;
+    }
+    f32x4 acc[TM][TN];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      u32x4 v;
-      if constexpr (CIN == 4) {
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int t = 8 * s + 2 * fsub + hh;            // tap of this 4-channel half
+      for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if (!((live >> i) & 1u)) continue;
+      const int rr = rw0 + i / TPR;                       // window row of this 16-pixel tile
+      const int cw = ((128 * wave) % W) + (i % TPR) * 16 + fr;   // this lane's output column
+      const bool tok = (top_ok >> i) & 1u, bok = (bot_ok >> i) & 1u;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        u32x4 v;
+        if constexpr (CIN == 4) {
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int t = 8 * s + 2 * fsub + hh;            // tap of this 4-channel half
+            const int dh = t / 3, dw = t - 3 * dh;
+            const bool ok = t < 9 && (dh != 0 || tok) && (dh != 2 || bok);
+            const int slot = (rr + dh) * RS + cw + dw + 1;
+            const u32x2 h2 = *(const u32x2*)(Xs + (ok ? slot * SB : 0));
+            v[2 * hh] = h2[0];
+            v[2 * hh + 1] = h2[1];
+          }
+        } else {
+          const int t = 4 * s + fsub;
           const int dh = t / 3, dw = t - 3 * dh;
           const bool ok = t < 9 && (dh != 0 || tok) && (dh != 2 || bok);
           const int slot = (rr + dh) * RS + cw + dw + 1;
-          const u32x2 h2 = *(const u32x2*)(Xs + (ok ? slot * SB : 0));
-          v[2 * hh] = h2[0];
-          v[2 * hh + 1] = h2[1];
+          v = *(const u32x4*)(Xs + (ok ? slot * SB : 0));
         }
-      } else {
-        const int t = 4 * s + fsub;
-        const int dh = t / 3, dw = t - 3 * dh;
-        const bool ok = t < 9 && (dh != 0 || tok) && (dh != 2 || bok);
-        const int slot = (rr + dh) * RS + cw + dw + 1;
-        v = *(const u32x4*)(Xs + (ok ? slot * SB : 0));
-      }
-      const h16x8 xf = __builtin_bit_cast(h16x8, v);
+        const h16x8 xf = __builtin_bit_cast(h16x8, v);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[s][j], xf, acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[s][j], xf, acc[i][j]);
+      }
     }
+    __syncthreads();                                     // halo reads done; previous epilogue's staging reads done
+    conv_epilogue<BM, BN, 128, BN, TM, TN, NTHR, EPI>(p, acc, Es, m0, n0, M, wave, 0, lane, tid, 0, 0, tm);
+    if (w + 1 < w_hi) store_halo();
+    __syncthreads();
   }
-  __syncthreads();
-  conv_epilogue<BM, BN, 128, BN, TM, TN, NTHR, EPI>(p, acc, smem, m0, n0, M, wave, 0, lane, tid, 0, 0, tm);
 }
 
 template <int CIN>
 hipError_t launch_win_first(const ConvFwdParams& p, hipStream_t s) {
   const int W = p.OW;
   const int R = 512 / W;
-  const int grid = ((p.N * p.OH + R - 1) / R) * (p.Cout / 32);
+  const int grid = (((p.N * p.OH + R - 1) / R) * (p.Cout / 32) + FWPW - 1) / FWPW;
   const int epi = conv_epi_mode(p);
   const bool fwd = epi == EPI_FWD;
 #define WF_CASE(WW)                                                                                        \
@@ -868,7 +893,7 @@ static bool img8_eligible(const ConvFwdParams& p) {
          p.KW == 3 && p.stride == 1 && p.pad == 1 && p.up1 == 1 && !p.shuffle && p.C1 > 0 && (p.C1 % 32) == 0 &&
          (p.C2 % 32) == 0 && (p.Cout % 64) == 0 && !(p.nz && (p.C2 || p.ncs)) &&
          (ep == EPI_FWD || ep == EPI_DGRAD || ep == EPI_GENERIC || ep == EPI_STATS || ep == EPI_DGRAD_NORM) &&
-         !p.route_gy && !p.pool_dst && !p.head_w && !p.xform && !p.hg.prob && !p.s2d;
+         !p.route_gy && !p.pool_dst && !p.head_w && !p.xform && !p.hg.prob && !p.s2d && !p.ut.x;
 }
 
 // Fills the tap tables and Kpad; returns nullptr on success or a message describing
@@ -916,6 +941,16 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
                 (conv_epi_mode(p) != EPI_DGRAD && conv_epi_mode(p) != EPI_DGRAD_NORM) ||
                 !win_tile(conv_fwd_pick(p))))
     return "conv_fwd: space-to-depth source needs a 2D single-source row-window data gradient (C1 = 4 s2d)";
+  if (p.ut.x) {
+    const int ep = conv_epi_mode(p);
+    if (!p.ut.w || !p.ut.b || (p.ut.C != 32 && p.ut.C != 64 && p.ut.C != 128) || p.ut.kpad < p.ut.C ||
+        (p.OW / 32) * (p.ut.C / 32) > 8 ||
+        p.C2 <= 0 || p.xform || p.hg.prob || p.s2d || p.route_gy || p.pool_dst || p.head_w || p.KD != 1 ||
+        p.OD != 1 || p.OW > 128 || p.OW < 32 || p.OH % 2 || !win_eligible(p) || !win_tile(conv_fwd_pick(p)) ||
+        win_rows(p) % 2 || (ep != EPI_FWD && ep != EPI_STATS && ep != EPI_GENERIC))
+      return "conv_fwd: transposed-conv source on load needs a 2D concat row-window forward (rows 32..128 wide, "
+             "32 / 64 / 128 coarse channels, (W / 32) (C / 32) <= 8)";
+  }
   if (p.route_gy && (!p.pool_code || (conv_epi_mode(p) != EPI_DGRAD && conv_epi_mode(p) != EPI_DGRAD_NORM) ||
                      !win_eligible(p) || p.KD != 1 || p.OD != 1 ||
                      p.OH % 2 || p.OW % 2 || p.D1 != p.Cout || p.pool_dst || p.mask_scale1 != 1.f ||

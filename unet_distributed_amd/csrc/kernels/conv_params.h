@@ -22,6 +22,18 @@ struct HeadGrad {
   float inv_total, bce_w;     // 1 / (pixels of the batch), BCE weight (0: Dice only)
 };
 
+// Transposed-conv source on load (2D row-window forward of a decoder conv whose first
+// source u = tconv2x2s2(x) + b is read by nothing else -- the composite backward never
+// re-reads it): each 32-channel chunk of u is formed in LDS from the coarse input
+// (conv_win.h XF 5), so u is never written to or read from memory and the transposed
+// conv's own forward launch disappears.  x == nullptr: off.
+struct TconvSrc {
+  const void* x;              // [N][OH/2][OW/2][C] 16-bit coarse input
+  const void* w;              // 16-bit [4][C1][kpad]: tap (th, tw) = 2 th + tw, u channel, coarse channel
+  const float* b;             // [C1] fp32 bias
+  int C, kpad;                // coarse channels (32, 64 or 128), weight row pitch
+};
+
 // Implicit-GEMM "NT" convolution: out[q][n] = epilogue(sum_{tap,c} X[q*s + tap - pad][c] * W[n][tap][c])
 // GEMM M = output pixels q over [N][OD][OH][OW], GEMM N = Cout, K = taps * Cin.
 // One kernel serves: conv forward, conv dgrad (flipped/transposed weights),
@@ -118,6 +130,7 @@ struct ConvFwdParams {
   // lies in one phase group (a, b) whose 3x3 taps are structurally zero outside the 2x2
   // support dh in {1 - a, 2 - a}, dw in {1 - b, 2 - b}: those MFMAs are skipped.
   int s2d;
+  TconvSrc ut;                // src1 = transposed conv of ut.x formed on load (see TconvSrc)
   // filled by conv_fwd_prepare (host): K padded to 64, per-tap pixel deltas / offsets
   int Kpad;
   int tap_delta[27];

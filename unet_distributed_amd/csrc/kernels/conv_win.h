@@ -7,6 +7,7 @@
 #include "conv_params.h"
 #include "conv_epilogue.h"
 #include "head_grad.h"
+#include <type_traits>
 
 namespace unet {
 
@@ -88,12 +89,15 @@ constexpr int NTHR = 256;
 // transformed operand go to xout); 3: head-on-load, the halo image of dY (32 channels)
 // is formed from the head's per-pixel probability, target and ReLU bits (p.hg,
 // head_grad.h) instead of being read from memory; 4: space-to-depth source (p.s2d: the
-// DMA gathers the fine pixels of each coarse slot, structurally zero taps skipped).
+// DMA gathers the fine pixels of each coarse slot, structurally zero taps skipped); 5
+// (2D concat): the src1 chunks are the transposed conv u = tconv2x2s2(p.ut.x) + b formed
+// in LDS (conv_params.h TconvSrc), the src2 (skip) chunks are DMA'd as usual.
 template <int W, int BN, int BM, bool CONCAT, int EPI, int GEO, int XF = 0>
 __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   static_assert(BN == 32 || BN == 64, "row-window tile is 32 or 64 output channels wide");
-  static_assert(XF == 0 || ((XF == 1 || XF == 3 || XF == 4) && GEO == GEO_2D && !CONCAT),
-                "operand transform: 2D single-source windows");
+  static_assert(XF == 0 || ((XF == 1 || XF == 3 || XF == 4) && GEO == GEO_2D && !CONCAT) ||
+                    (XF == 5 && GEO == GEO_2D && CONCAT),
+                "operand transform: 2D single-source windows (tconv on load: 2D concat)");
   constexpr int R = BM / W, HR = R + 2;
   // halo row pitch in 64-byte pixel slots: W + 2 columns rounded up to a multiple of 4
   // (every row starts on a 256-byte bank row); the DMA fills the image as one linear
@@ -299,6 +303,90 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
       return sl;
     };
     const size_t xsample = XF == 1 ? (size_t)(g0 / H) * p.xcs : 0;   // the window's sample (GroupNorm rows)
+    // XF 5: u channels cb .. cb + 31 of the halo image from the coarse input.  The HR fine
+    // halo rows come from NCR = R / 2 + 2 coarse rows (R even); wave w takes coarse rows
+    // cq = w, w + 4, ..: it loads the row's B fragments (16 coarse pixels x 32 coarse
+    // channels each, straight from global memory -- one HBM round trip per coarse row)
+    // and forms the fine rows 2 cq - 1 + th inside the halo for the four phases
+    // t = (th, tw) = 2 th + tw, one 16 x 16 x 32 MFMA chain per (16 coarse pixels, 16 u
+    // channels) with the tap's weight rows as A (L2-resident; the next tap's are loaded
+    // under the current tap's MFMAs where registers allow).  Same operands and
+    // accumulation order as tconv_fwd_kernel, so u is bit-identical to the materialised
+    // one.  Every slot a fragment read touches is written: rows outside the image and the
+    // columns -1 / W are zeros, as the DMA's out-of-range loads would have left them.
+    auto ut_chunk = [&](const int cb, auto ksc) {
+      constexpr int KS = decltype(ksc)::value;    // 32-channel K steps of the coarse input
+      constexpr int CW = W / 2, PB = XF == 5 ? CW / 16 : 1, NCR = R / 2 + 2;
+      static_assert(XF != 5 || (R % 2 == 0 && CW % 16 == 0), "tconv on load: even window rows, coarse rows 16k wide");
+      if constexpr (PB * KS <= 8) {               // (conv_fwd_prepare: (W / 32) (C / 32) <= 8)
+        constexpr int NAB = KS <= 2 ? 2 : 1;      // tap weight buffers (two: next tap prefetched)
+        const int Cc = KS * 32;
+        const h16* wt = (const h16*)p.ut.w + (size_t)(cb + fr) * p.ut.kpad + 8 * fsub;
+        // the window's image in the coarse tensor (H even: fine row g -> coarse row g / 2)
+        const h16* ub = (const h16*)p.ut.x + (size_t)(grow0 >> 1) * CW * Cc + (size_t)fr * Cc + 8 * fsub;
+        float bs[2][4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) bs[j][i] = p.ut.b[cb + 16 * j + 4 * fsub + i];
+        h16x8 xb[PB][KS];
+        h16x8 wa[NAB][2][KS];
+        auto load_a = [&](const int t, h16x8 (&dst)[2][KS]) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+              dst[j][ks] = *(const h16x8*)(wt + (size_t)(t * p.C1 + 16 * j) * p.ut.kpad + 32 * ks);
+        };
+        for (int cq = wave; cq < NCR; cq += 4) {
+          // fine halo rows hr = 2 cq - 1 + th of this coarse row; in the image <=> the
+          // coarse row is (window rows never leave their image, conv_fwd_prepare)
+          const int crow = (g0 >> 1) - 1 + cq;                   // global coarse row
+          const int gr0 = 2 * crow;
+          const bool in = (2 * cq - 1 >= 1 || top_in) && (2 * cq <= R || bot_in) &&
+                          (unsigned)gr0 < (unsigned)rows_total;
+          if (in) {
+            const h16* rp = ub + (size_t)(crow - (grow0 >> 1)) * CW * Cc;
+#pragma unroll
+            for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+              for (int ks = 0; ks < KS; ++ks) xb[pb][ks] = *(const h16x8*)(rp + (size_t)(16 * pb) * Cc + 32 * ks);
+          }
+          const int t_lo = cq == 0 ? 2 : 0, t_hi = cq == NCR - 1 ? 2 : 4;   // taps whose rows are halo rows
+          if (in) load_a(t_lo, wa[0]);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (t < t_lo || t >= t_hi) continue;
+            const int ab = NAB == 2 ? (t - t_lo) & 1 : 0;
+            if constexpr (NAB == 2) {
+              if (in && t + 1 < t_hi) load_a(t + 1, wa[ab ^ 1]);
+            } else if (in && t > t_lo) {
+              load_a(t, wa[0]);
+            }
+            const int th = t >> 1, tw = t & 1;
+            char* xrow = Xs + (2 * cq - 1 + th) * ROWB;
+#pragma unroll
+            for (int pb = 0; pb < PB; ++pb) {
+              const int hc = 2 * (16 * pb + fr) + tw + 1;
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                u32x2 pk = {0u, 0u};
+                if (in) {
+                  f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                  for (int ks = 0; ks < KS; ++ks) a = mfma16(wa[ab][j][ks], xb[pb][ks], a);
+                  pk[0] = pack2h(a[0] + bs[j][0], a[1] + bs[j][1]);
+                  pk[1] = pack2h(a[2] + bs[j][2], a[3] + bs[j][3]);
+                }
+                const int ch = 2 * j + (fsub >> 1);
+                *(u32x2*)(xrow + hc * 64 + 16 * (ch ^ ((hc >> 1) & 3)) + 8 * (fsub & 1)) = pk;
+              }
+            }
+            if (lane < 4) *(u32x4*)(xrow + (tw ? W + 1 : 0) * 64 + 16 * lane) = (u32x4){0u, 0u, 0u, 0u};
+          }
+        }
+      }
+    };
     for (int kc = 0; kc < nchunks; ++kc) {
       const bool from1 = !CONCAT || (kc << 5) < p.C1;
       // space-to-depth gathered chunk: every chunk of XF 4
@@ -315,7 +403,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
 #pragma unroll
         for (int q = 0; q < (XI + 3) / 4; ++q) {
           const int k = wave + 4 * q;
-          if (XF != 3 && k < XI) {
+          if (XF != 3 && !(XF == 5 && from1) && k < XI) {
             int hr, hc;
             if constexpr (ALR) {
               hr = k / PPR;                                 // wave-uniform
@@ -349,6 +437,16 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024),
                                                      16, off, 0, 0, 0);
           }
+        }
+      }
+      if constexpr (XF == 5) {
+        if (from1) {
+          if (p.ut.C == 64)
+            ut_chunk(cb, std::integral_constant<int, 2>{});
+          else if (p.ut.C == 128)
+            ut_chunk(cb, std::integral_constant<int, 4>{});
+          else
+            ut_chunk(cb, std::integral_constant<int, 1>{});
         }
       }
       if constexpr (XF == 3) {
@@ -538,6 +636,33 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
       S2D_CASE(64)
       S2D_CASE(128)
 #undef S2D_CASE
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  if (p.ut.x) {                         // transposed-conv source on load (conv_fwd_prepare checks the shape)
+    if (!cc || geo != GEO_2D) return hipErrorInvalidValue;
+    switch (W) {
+#define UT_CASE(WW)                                                                                       \
+  case WW:                                                                                                \
+    if constexpr (WW >= 32 && win_tile_built<BN, BM>(WW) && (BM / WW) % 2 == 0) {                          \
+      if (epi == EPI_FWD)                                                                                 \
+        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, true, EPI_FWD, GEO_2D, 5>), dim3(grid), dim3(NTHR), 0, s, p); \
+      else if (epi == EPI_STATS)                                                                          \
+        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, true, EPI_STATS, GEO_2D, 5>), dim3(grid), dim3(NTHR), 0, s, p); \
+      else if (epi == EPI_GENERIC)                                                                        \
+        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, true, EPI_GENERIC, GEO_2D, 5>), dim3(grid), dim3(NTHR), 0, s, p); \
+      else                                                                                                \
+        return hipErrorInvalidValue;                                                                      \
+    } else {                                                                                              \
+      return hipErrorInvalidValue;                                                                        \
+    }                                                                                                     \
+    break;
+      UT_CASE(32)
+      UT_CASE(64)
+      UT_CASE(128)
+#undef UT_CASE
       default:
         return hipErrorInvalidValue;
     }

@@ -129,6 +129,11 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.xc = (const float*)getp(d, "xc");
   p.xz = getp(d, "xz");
   p.s2d = get<int>(d, "s2d", 0);
+  p.ut.x = getp(d, "ut_x");
+  p.ut.w = getp(d, "ut_w");
+  p.ut.b = (const float*)getp(d, "ut_b");
+  p.ut.C = get<int>(d, "ut_C", 0);
+  p.ut.kpad = get<int>(d, "ut_kpad", 0);
   p.xout = const_cast<void*>(getp(d, "xout"));
   p.tile = get<int>(d, "tile", 0);
   p.head_w = (const float*)getp(d, "head_w");

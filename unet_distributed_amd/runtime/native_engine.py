@@ -59,7 +59,10 @@ def _r64(k: int) -> int:
 #   tconv_fused  deepest fine level whose transposed conv runs the composite backward (2; 0 off)
 #   tconv_wa     the consumer conv's u-row weight gradient from the composite backward's
 #                slab sums (1; 0: full weight gradient over u)
-ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1)
+#   tconv_onload deepest fine level whose transposed-conv output u is formed on load by its
+#                consumer's forward where nothing else reads it (1; 0: materialised)
+ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
+                       tconv_onload=1)
 
 
 def engine_options(overrides: Optional[Dict[str, int]] = None) -> Dict[str, int]:
@@ -377,6 +380,7 @@ class NativeUNet:
         self.tconv_fused: Dict[str, dict] = {}
         self._tf_consumer: Dict[str, str] = {}
         self._wa_chain_of: Dict[str, str] = {}  # consumer conv whose u-row wgrad is chained -> tconv
+        self._ut_onload: Dict[str, str] = {}    # consumer conv that forms u on load -> tconv
         top = self.opts["tconv_fused"]
         if self.dims != 2 or top <= 0 or (self.spec.norm != "none" and not self.fuse_norm_stats_planned()):
             return
@@ -414,6 +418,7 @@ class NativeUNet:
                                             bs=torch.zeros(16 * O, dtype=torch.float32, device=self.device))
             self._tf_consumer[c.name] = l.name
             self._plan_wa_chain(l, c, self.tconv_fused[l.name])
+            self._plan_ut_onload(l, c, self.tconv_fused[l.name])
 
     def fuse_norm_stats_planned(self):
         """Normalised model: every conv epilogue writes its statistics (the composite
@@ -433,6 +438,35 @@ class NativeUNet:
             return
         tf["wa"] = dict(Cs=Cs, skg=torch.zeros(9 * Cs * O, dtype=torch.float32, device=self.device))
         self._wa_chain_of[c.name] = l.name
+
+    def _ut_fields(self, tl, x_ptr):
+        """conv_params.h TconvSrc fields: the consumer's src1 = tconv `tl` of x formed on load."""
+        return dict(ut_x=x_ptr, ut_w=self.wptr(tl.name), ut_b=self.master_ptr(tl.name + "/bias"),
+                    ut_C=tl.cin, ut_kpad=_r64(tl.cin))
+
+    def _plan_ut_onload(self, l, c, tf):
+        """Option tconv_onload (default 1): with the composite backward and the chained
+        u-row weight gradient nothing but the consumer's forward reads u = tconv(b), so
+        that forward forms each 32-channel chunk of u in LDS from b (conv_win.h XF 5): the
+        transposed conv's forward launch and its fine output tensor (1 GiB at level 1,
+        b1024) are gone, and the consumer reads the 4x smaller coarse b instead of u."""
+        if l.level > self.opts["tconv_onload"] or "wa" not in tf:
+            return
+        normed = self.spec.norm != "none"
+        d = self._conv_common(c.level, 3, 1, 1)
+        d.update(C1=l.cout, C2=c.cin - l.cout, src1=1, src2=1, wgt=1, bias=1, Cout=c.cout,
+                 relu=0 if normed else 1, dst1=1, **self._ut_fields(l, 1))
+        if normed:
+            d["stats"] = 1
+        try:
+            if self.C.conv_fwd_grid(d) <= 0:
+                return
+        except ValueError:
+            return
+        tf["ut"] = True
+        self._ut_onload[c.name] = l.name
+        # the fine output is never formed (no forward writes it, no backward reads it)
+        self.bufs.pop(l.name, None)
 
     # ------------------------------------------------------------------ normalisation
     NORM_EPS = 1e-3          # models/reference.py::_norm (Keras default epsilon)
@@ -858,7 +892,7 @@ class NativeUNet:
         if l.kind == "conv":
             src1, up1, skip = self.inputs[l.name]
             c1 = self.tinfo[src1][1]
-            s1 = P(src1)
+            s1 = None if l.name in self._ut_onload else P(src1)
             if up1 == 2 and self.ups_materialize:
                 lvl = self.tinfo[src1][0]
                 dd, hh, ww = self.sdims(lvl)
@@ -870,6 +904,11 @@ class NativeUNet:
             d = self._conv_common(l.level, 3, 1, 1)
             d["N"] = nb
             normed = spec.norm != "none"
+            ut = self._ut_onload.get(l.name)
+            if ut is not None:
+                tl = next(x for x in spec.layers if x.name == ut)
+                d.update(self._ut_fields(tl, P(self.inputs[ut][0])))
+                s1 = d["ut_x"]
             if src1 in self._xf_fwd:
                 d.update(self._xf_fwd_fields(src1))
                 s1 = _ptr(b["z:" + src1])
@@ -916,6 +955,8 @@ class NativeUNet:
             code = _ptr(self.pool_codes[l.name]) + c * nb * pd * ph * pw * (l.cout // 8) * 4
             plan.add_generic("pool_fwd", [P(src), P(l.name), code],
                              [nb, dd, hh, ww, l.cout, int(self.dims == 3)], [], "fwd:" + l.name)
+        elif l.kind == "tconv" and l.name in self._ut_onload.values():
+            pass                                 # formed on load by its consumer's forward
         elif l.kind == "tconv":
             src = self.inputs[l.name][0]
             d = self._conv_common(l.level + 1, 1, 1, 0)
