@@ -21,5 +21,6 @@ for args in "" "--norm batch --steps 10 --warmup 3" "--norm group --dtype fp16 -
   grep metric gpurun_out/r4_b.log >> gpurun_out/r4_benches.jsonl
   python -c "import json,sys; d=json.loads([l for l in open('gpurun_out/r4_b.log') if l.startswith('{')][0]); print(d['config']['model'], d['value'], d['ms_per_step'], d.get('train_dice_last_batch'))"
 done
+[ "${SKIP_DICE:-0}" = 1 ] && exit 0
 PAIRS=ups timeout -k 10 1200 bash scripts/gpu_dice_parity.sh 300 1 2 3 > gpurun_out/r4_dice.log 2>&1 || { echo "dice rc=$?"; tail -20 gpurun_out/r4_dice.log; exit 1; }
 tail -8 gpurun_out/dice_parity.md

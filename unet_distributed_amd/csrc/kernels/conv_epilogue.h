@@ -417,6 +417,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     for (int e = 0; e < 8; ++e) hw[e] = p.head_w[(tid % CPR) * 8 + e];
     hb = p.head_b[0];
   }
+  // head-gradient sums (p.head_sums): this thread's 8 channels, 4 moments, plus the
+  // per-pixel scalars on the chunk-0 lanes (column BN)
+  const bool kHS = kHeadable && kHead && p.head_sums != nullptr;
+  float hs[kHeadable ? 4 : 1][8], hs1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < (kHeadable ? 4 : 1); ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) hs[k][e] = 0.f;
   // (fully unrolled with the fused head, whose per-iteration logits live in registers)
   constexpr int NITER = (NCHUNK + NTHR - 1) / NTHR;
   constexpr int UNR = kHeadable ? NITER : 2;
@@ -486,6 +494,26 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
         z += __shfl_xor(z, 2, 64);
         hz[it] = z + hb;
         hq[it] = q;
+        if (kHS) {
+          // p exactly as head.hip::head_finish computes it from the stored logit
+          const float zl = z + hb;
+          const float pr = 1.f / (1.f + __expf(-zl));
+          const float tv = bits2f(((const uint16_t*)p.head_t)[q]);
+          const float qq = pr * (1.f - pr), tq = tv * qq;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            hs[0][e] = __builtin_fmaf(tq, f[e], hs[0][e]);
+            hs[1][e] = __builtin_fmaf(qq, f[e], hs[1][e]);
+            hs[2][e] = __builtin_fmaf(pr, f[e], hs[2][e]);
+            hs[3][e] = __builtin_fmaf(tv, f[e], hs[3][e]);
+          }
+          if (cb == 0) {
+            hs1[0] += tq;
+            hs1[1] += qq;
+            hs1[2] += pr;
+            hs1[3] += tv;
+          }
+        }
       }
     }
   }
@@ -505,6 +533,36 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
           q = cb == r ? hq[CPR * k + r] : q;
         }
         if (q < M) p.head_logit[q] = z;
+      }
+      if (kHS) {
+        // lanes congruent mod CPR hold the same channels: fold them, then the waves in
+        // fixed order through LDS (past the staging tile) -> one row per window
+        constexpr int HW = 4 * (BN + 1);
+#pragma unroll
+        for (int o = CPR; o < 64; o <<= 1) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) hs[k][e] += __shfl_xor(hs[k][e], o, 64);
+            hs1[k] += __shfl_xor(hs1[k], o, 64);
+          }
+        }
+        const int wv = tid >> 6, ln = tid & 63;
+        if (ln < CPR) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) SP[wv * HW + k * (BN + 1) + ln * 8 + e] = hs[k][e];
+            if (ln == 0) SP[wv * HW + k * (BN + 1) + BN] = hs1[k];
+          }
+        }
+        __syncthreads();
+        for (int j = tid; j < HW; j += NTHR) {
+          float a = 0.f;
+#pragma unroll
+          for (int w = 0; w < NTHR / 64; ++w) a += SP[w * HW + j];
+          p.head_sums[(size_t)stat_row * HW + j] = a;
+        }
       }
     }
   }
