@@ -420,7 +420,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
   // head-gradient sums (p.head_sums): this thread's 8 channels, 4 moments, plus the
   // per-pixel scalars on the chunk-0 lanes (column BN)
   const bool kHS = kHeadable && kHead && p.head_sums != nullptr;
-  float hs[kHeadable ? 4 : 1][8], hs1[4] = {0.f, 0.f, 0.f, 0.f};
+  float hs[kHeadable ? 4 : 1][8], hs1[4] = {0.f, 0.f, 0.f, 0.f}, hl[2] = {0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < (kHeadable ? 4 : 1); ++k)
 #pragma unroll
@@ -500,6 +500,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
           const float pr = 1.f / (1.f + __expf(-zl));
           const float tv = bits2f(((const uint16_t*)p.head_t)[q]);
           const float qq = pr * (1.f - pr), tq = tv * qq;
+          hz[it] = pr;                 // (head_logit receives the probability)
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             hs[0][e] = __builtin_fmaf(tq, f[e], hs[0][e]);
@@ -512,6 +513,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
             hs1[1] += qq;
             hs1[2] += pr;
             hs1[3] += tv;
+            hl[0] += tv * pr;
+            hl[1] += fmaxf(zl, 0.f) - zl * tv + log1pf(__expf(-fabsf(zl)));
           }
         }
       }
@@ -537,7 +540,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       if (kHS) {
         // lanes congruent mod CPR hold the same channels: fold them, then the waves in
         // fixed order through LDS (past the staging tile) -> one row per window
-        constexpr int HW = 4 * (BN + 1);
+        constexpr int HW = 4 * (BN + 1) + 4;
 #pragma unroll
         for (int o = CPR; o < 64; o <<= 1) {
 #pragma unroll
@@ -546,6 +549,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
             for (int e = 0; e < 8; ++e) hs[k][e] += __shfl_xor(hs[k][e], o, 64);
             hs1[k] += __shfl_xor(hs1[k], o, 64);
           }
+          hl[0] += __shfl_xor(hl[0], o, 64);
+          hl[1] += __shfl_xor(hl[1], o, 64);
         }
         const int wv = tid >> 6, ln = tid & 63;
         if (ln < CPR) {
@@ -554,6 +559,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
 #pragma unroll
             for (int e = 0; e < 8; ++e) SP[wv * HW + k * (BN + 1) + ln * 8 + e] = hs[k][e];
             if (ln == 0) SP[wv * HW + k * (BN + 1) + BN] = hs1[k];
+          }
+          if (ln == 0) {               // loss partials in head_finish's order {I, St, Sp, BCE}
+            SP[wv * HW + 4 * (BN + 1) + 0] = hl[0];
+            SP[wv * HW + 4 * (BN + 1) + 1] = hs1[3];
+            SP[wv * HW + 4 * (BN + 1) + 2] = hs1[2];
+            SP[wv * HW + 4 * (BN + 1) + 3] = hl[1];
           }
         }
         __syncthreads();

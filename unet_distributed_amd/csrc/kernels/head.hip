@@ -253,7 +253,7 @@ hipError_t head_fwd_launch(const void* x, const float* w, const float* b, const 
 }
 
 // Head weight / bias gradients from the fused-head forward's per-window sums (conv_params.h
-// head_sums): column j of the rows [nrows][4][C + 1] summed in fixed order (thread-strided
+// head_sums): column j of the rows [nrows][4 (C + 1) + 4] summed in fixed order (thread-strided
 // rows, then a fixed tree), then
 //   g_j = gscale (a S_tqx + bb S_qx + bce_w inv_total (S_px - S_tx))
 // -- the same affine form head_grad.h::head_dlogit has in t and q = p (1 - p).  One block
@@ -264,7 +264,7 @@ __global__ void __launch_bounds__(256) head_sums_grad_kernel(const float* __rest
                                                             const float* __restrict__ gscale_ptr,
                                                             float* __restrict__ gw, float* __restrict__ gb) {
   __shared__ float red[4][256];
-  const int j = blockIdx.x, W = 4 * (C + 1);
+  const int j = blockIdx.x, W = 4 * (C + 1) + 4;
   float s[4] = {0.f, 0.f, 0.f, 0.f};
   for (int r = threadIdx.x; r < nrows; r += 256) {
 #pragma unroll
@@ -319,8 +319,8 @@ hipError_t head_bwd_launch(const void* x, const float* w, const float* prob, con
   return hipGetLastError();
 }
 
-hipError_t partial_reduce_launch(const float* partial, int nb, int width, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(partial_reduce_kernel, dim3(width), dim3(256), 0, s, partial, nb, width, out);
+hipError_t partial_reduce_launch(const float* partial, int nb, int width, float* out, hipStream_t s, int ncols) {
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3(ncols > 0 ? ncols : width), dim3(256), 0, s, partial, nb, width, out);
   return hipGetLastError();
 }
 

@@ -466,7 +466,9 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     const float* part = (const float*)vp(0);
     float* out = (float*)vp(1);
     int nb = I[0], width = I[1];
-    return [=](hipStream_t s) { return A->partial_reduce_launch(part, nb, width, out, s); };
+    const int ncols = I.size() > 2 ? I[2] : 0;     // optional: columns [0, ncols) of width-wide rows
+    if (ncols < 0 || ncols > width) throw std::invalid_argument("partial_reduce: 0 <= ncols <= width");
+    return [=](hipStream_t s) { return A->partial_reduce_launch(part, nb, width, out, s, ncols); };
   }
   if (kind == "head_fwd") {
     need(7, 2, 0);

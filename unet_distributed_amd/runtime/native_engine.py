@@ -969,6 +969,11 @@ class NativeUNet:
                      bias=self.master_ptr(l.name + "/bias"), Cout=(2 ** self.dims) * l.cout,
                      relu=0, shuffle=self.dims, dst1=P(l.name))
             plan.add_conv_fwd(d)
+        elif l.kind == "mask" and train and plan is self.plan and getattr(self, "_head_sums_rows", 0):
+            # loss partials of the fused-head windows -> sums (probabilities already stored)
+            w = self._head_sums_width()
+            plan.add_generic("partial_reduce", [_ptr(self.head_srows) + 4 * (w - 4), _ptr(self.sums)],
+                             [self._head_sums_rows, w, 4], [], "fwd:Mask")
         elif l.kind == "mask" and train and self._norm_head_loss:
             pass                                 # loss sums written by norm_head_loss
         elif l.kind == "mask" and (self._head_fused_blocks or self._norm_head):
@@ -983,13 +988,18 @@ class NativeUNet:
                                           _ptr(self.prob), _ptr(part), _ptr(self.sums)],
                              [P1, hc], [], "fwd:Mask")
 
+    def _head_sums_width(self):
+        """Floats per window row of the fused-head sums: [4][C + 1] moments + 4 loss partials."""
+        return 4 * (self.tinfo[self.head_in][1] + 1) + 4
+
     def _head_sums_fields(self, d, c, nb):
         """Fused-head forward of chunk c (images [c nb, (c + 1) nb)) also accumulates the
-        head's weight / bias gradient sums per window (conv_params.h head_sums); the
-        backward's head_sums_grad combines them with the loss scalars."""
+        head's weight / bias gradient sums and the loss partials per window and stores
+        probabilities (conv_params.h head_sums): the forward's head_finish pass becomes a
+        reduction of the rows, the backward's head pass head_sums_grad."""
         rows, _ = self.C.conv_stat_tiles(d)
         hc = self.tinfo[self.head_in][1]
-        width = 4 * (hc + 1)
+        width = self._head_sums_width()
         nch = self.B // nb
         if getattr(self, "head_srows", None) is None or self.head_srows.numel() != nch * rows * width:
             self.head_srows = torch.zeros(nch * rows * width, dtype=torch.float32, device=self.device)
