@@ -514,7 +514,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
             hs1[2] += pr;
             hs1[3] += tv;
             hl[0] += tv * pr;
-            hl[1] += fmaxf(zl, 0.f) - zl * tv + log1pf(__expf(-fabsf(zl)));
+            if (p.head_bce) hl[1] += fmaxf(zl, 0.f) - zl * tv + log1pf(__expf(-fabsf(zl)));
           }
         }
       }

@@ -130,6 +130,7 @@ struct ConvFwdParams {
   // head_logit receives the probabilities (no head_finish pass).  nullptr: off.
   float* head_sums;
   const void* head_t;         // [pixels] 16-bit targets of the launch's pixels (head_sums)
+  int head_bce;               // head_sums: also the BCE partial (else 0; only Dice + BCE reads it)
   int rev;                    // row-window kernels: windows in reverse order (the consumer starts
                               // where its producer ended, on the tail still in the Infinity Cache)
   HeadGrad hg;                // 2D row-window data gradient of the head input: src1 (dY) formed
