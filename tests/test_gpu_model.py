@@ -432,7 +432,7 @@ def test_head_sums_step_matches_head_pass(cuda_dev, monkeypatch, kw):
     for k in g0:
         a, b = g0[k], g1[k]
         err = ((a - b).norm() / (a.norm() + 1e-30)).item()
-        assert err < (1e-4 if k.startswith("Mask/") else 2e-3), (k, err)
+        assert err < (1e-4 if k.startswith("Mask/") else 1e-2), (k, err)
 
 
 @pytest.mark.parametrize("kw", [

@@ -479,7 +479,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       // (off is a multiple of 8: the bit tensor's byte of these 8 channels is off / 8)
       v = mbit ? keep_bits(v, ((const uint8_t*)mk)[off >> 3]) : keep_pos(v, *(const u32x4*)((const h16*)mk + off));
     }
-    *(u32x4*)(dst + off) = v;
+    if (!(kHeadable && kHead && p.head_nostore)) *(u32x4*)(dst + off) = v;
     // (EPI_FWD: ReLU outputs from relu2h, never -0 -- the cheap form)
     if (EPI == EPI_FWD && p.relu_bits) p.relu_bits[off >> 3] = (uint8_t)pos_bits_relu(v);
     if (G && p.relu_bits) p.relu_bits[off >> 3] = (uint8_t)pos_bits(v);

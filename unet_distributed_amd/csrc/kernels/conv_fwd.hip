@@ -978,6 +978,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     if (t == 6 && !win_eligible(p)) return "conv_fwd: row-window tile not applicable";
   }
   if (p.head_sums && (!p.head_w || !p.head_t)) return "conv_fwd: head sums need the fused head and head_t";
+  if (p.head_nostore && !p.head_sums) return "conv_fwd: head_nostore needs head_sums (the head backward reads y)";
   if (p.head_w) {
     if (!p.head_b || !p.head_logit) return "conv_fwd: fused head needs head_b / head_logit";
     if (p.Cout != 32 || p.drop_rate > 0.f || !p.relu || p.D1 != p.Cout || p.mask1 || p.out_scale != 1.f ||

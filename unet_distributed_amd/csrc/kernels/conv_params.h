@@ -131,6 +131,8 @@ struct ConvFwdParams {
   float* head_sums;
   const void* head_t;         // [pixels] 16-bit targets of the launch's pixels (head_sums)
   int head_bce;               // head_sums: also the BCE partial (else 0; only Dice + BCE reads it)
+  int head_nostore;           // fused head: the activation itself is not stored (nothing reads it:
+                              // head-on-load backward + head_sums); ReLU bits still are
   int rev;                    // row-window kernels: windows in reverse order (the consumer starts
                               // where its producer ended, on the tail still in the Infinity Cache)
   HeadGrad hg;                // 2D row-window data gradient of the head input: src1 (dY) formed

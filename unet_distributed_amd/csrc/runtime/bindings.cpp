@@ -142,6 +142,7 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.head_sums = (float*)const_cast<void*>(getp(d, "head_sums"));
   p.head_t = getp(d, "head_t");
   p.head_bce = get<int>(d, "head_bce", 1);
+  p.head_nostore = get<int>(d, "head_nostore", 0);
   p.hg = head_grad(d);
   if (!p.src1 || !p.wgt || !p.dst1) throw std::invalid_argument("conv_fwd: src1/wgt/dst1 required");
   check_msg(conv_fwd_prepare(p));

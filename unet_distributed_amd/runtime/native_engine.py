@@ -1004,7 +1004,9 @@ class NativeUNet:
         if getattr(self, "head_srows", None) is None or self.head_srows.numel() != nch * rows * width:
             self.head_srows = torch.zeros(nch * rows * width, dtype=torch.float32, device=self.device)
         self._head_sums_rows = nch * rows
+        # (head-on-load + head sums: nothing reads the head input itself -- only its ReLU bits)
         d.update(head_sums=_ptr(self.head_srows) + 4 * c * rows * width, head_bce=int(self.loss == "dice_bce"),
+                 head_nostore=1,
                  head_t=_ptr(self.target) + self.target.element_size() * c * nb * (self.npix(1) // self.B))
 
     def _rev_order(self, d, src, out, *also):
