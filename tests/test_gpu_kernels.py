@@ -1016,59 +1016,3 @@ def test_conv_img8_norm_statistics(cuda_dev):
     assert rel_err(s0, s1) < 1e-2 and rel_err(t0, t1) < 1e-2
     zf = z0.float().reshape(-1, Co)
     assert rel_err(s0[0], zf.sum(0)) < 1e-3 and rel_err(s0[1], (zf * zf).sum(0)) < 1e-3
-
-
-@pytest.mark.parametrize("N,H,bce", [(2, 128, 0.0), (3, 64, 0.5), (4, 32, 1.0)])
-def test_fused_head_gradient_sums(cuda_dev, N, H, bce):
-    """Fused-head conv forward with head_sums (conv_epilogue.h): probabilities stored, the
-    per-window rows {t q x, q x, p x, t x} (+ x = 1 column) and loss partials {I, St, Sp,
-    BCE}; partial_reduce -> the loss sums, head_sums_grad -> the Mask weight / bias
-    gradients of -log Dice (+ BCE) -- vs autograd on the stored bf16 activation."""
-    torch.manual_seed(12)
-    Cin, Co = 32, 32
-    x = F.relu(torch.randn(N, H, H, Cin, device=cuda_dev)).bfloat16()
-    wgt = (torch.randn(3, 3, Cin, Co, device=cuda_dev) * 0.1).bfloat16()
-    b = torch.randn(Co, device=cuda_dev) * 0.1
-    hw = torch.randn(Co, device=cuda_dev) * 0.3
-    hb = torch.randn(1, device=cuda_dev)
-    t = (torch.rand(N * H * H, device=cuda_dev) > 0.7).bfloat16()
-    y = torch.empty(N, H, H, Co, device=cuda_dev, dtype=torch.bfloat16)
-    prob = torch.empty(N * H * H, device=cuda_dev)
-    d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(x), wgt=ptr(pack_fwd(wgt)),
-             bias=ptr(b), Cout=Co, relu=1, dst1=ptr(y), head_w=ptr(hw), head_b=ptr(hb), head_logit=ptr(prob),
-             head_t=ptr(t))
-    rows, _ = C().conv_stat_tiles(d)
-    W = 4 * (Co + 1) + 4
-    srows = torch.full((rows * W,), float("nan"), device=cuda_dev)
-    C().conv_fwd(dict(d, head_sums=ptr(srows)), stream())
-    P = N * H * H
-    sums = torch.empty(4, device=cuda_dev)
-    C().generic("partial_reduce", [ptr(srows) + 4 * (W - 4), ptr(sums)], [rows, W, 4], [], stream())
-    gw = torch.empty(Co, device=cuda_dev)
-    gb = torch.empty(1, device=cuda_dev)
-    C().generic("head_sums_grad", [ptr(srows), ptr(sums), ptr(gw), ptr(gb)], [rows, Co], [1.0 / P, bce, 1.0],
-                stream())
-    torch.cuda.synchronize()
-    xs = y.float().reshape(P, Co)
-    wr = hw.clone().requires_grad_(True)
-    br = hb.clone().requires_grad_(True)
-    z = xs @ wr + br
-    p = torch.sigmoid(z)
-    tf = t.float()
-    I, St, Sp = (tf * p).sum(), tf.sum(), p.sum()
-    bsum = F.binary_cross_entropy_with_logits(z, tf, reduction="sum")
-    assert rel_err(prob, p) < 1e-4
-    assert rel_err(sums, torch.stack([I, St, Sp, bsum])) < 1e-4
-    loss = -torch.log(2 * I + 1) + torch.log(St + Sp + 1)
-    if bce:
-        loss = loss + bce * bsum / P
-    rw, rb = torch.autograd.grad(loss, [wr, br])
-    assert rel_err(gw, rw) < 2e-3
-    assert rel_err(gb, rb) < 2e-3
-    # the raw moments: column sums over the rows
-    S = srows.view(rows, W)[:, :4 * (Co + 1)].reshape(rows, 4, Co + 1).sum(0)
-    q = (p * (1 - p)).detach()
-    xe = torch.cat([xs, torch.ones(P, 1, device=cuda_dev)], 1)
-    ref = torch.stack([((tf * q)[:, None] * xe).sum(0), (q[:, None] * xe).sum(0),
-                       (p.detach()[:, None] * xe).sum(0), (tf[:, None] * xe).sum(0)])
-    assert rel_err(S, ref) < 1e-3

@@ -417,14 +417,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     for (int e = 0; e < 8; ++e) hw[e] = p.head_w[(tid % CPR) * 8 + e];
     hb = p.head_b[0];
   }
-  // head-gradient sums (p.head_sums): this thread's 8 channels, 4 moments, plus the
-  // per-pixel scalars on the chunk-0 lanes (column BN)
-  const bool kHS = kHeadable && kHead && p.head_sums != nullptr;
-  float hs[kHeadable ? 4 : 1][8], hs1[4] = {0.f, 0.f, 0.f, 0.f}, hl[2] = {0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < (kHeadable ? 4 : 1); ++k)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) hs[k][e] = 0.f;
   // (fully unrolled with the fused head, whose per-iteration logits live in registers)
   constexpr int NITER = (NCHUNK + NTHR - 1) / NTHR;
   constexpr int UNR = kHeadable ? NITER : 2;
@@ -479,7 +471,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       // (off is a multiple of 8: the bit tensor's byte of these 8 channels is off / 8)
       v = mbit ? keep_bits(v, ((const uint8_t*)mk)[off >> 3]) : keep_pos(v, *(const u32x4*)((const h16*)mk + off));
     }
-    if (!(kHeadable && kHead && p.head_nostore)) *(u32x4*)(dst + off) = v;
+    *(u32x4*)(dst + off) = v;
     // (EPI_FWD: ReLU outputs from relu2h, never -0 -- the cheap form)
     if (EPI == EPI_FWD && p.relu_bits) p.relu_bits[off >> 3] = (uint8_t)pos_bits_relu(v);
     if (G && p.relu_bits) p.relu_bits[off >> 3] = (uint8_t)pos_bits(v);
@@ -494,29 +486,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
         z += __shfl_xor(z, 2, 64);
         hz[it] = z + hb;
         hq[it] = q;
-        if (kHS) {
-          // p exactly as head.hip::head_finish computes it from the stored logit
-          const float zl = z + hb;
-          const float pr = 1.f / (1.f + __expf(-zl));
-          const float tv = bits2f(((const uint16_t*)p.head_t)[q]);
-          const float qq = pr * (1.f - pr), tq = tv * qq;
-          hz[it] = pr;                 // (head_logit receives the probability)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            hs[0][e] = __builtin_fmaf(tq, f[e], hs[0][e]);
-            hs[1][e] = __builtin_fmaf(qq, f[e], hs[1][e]);
-            hs[2][e] = __builtin_fmaf(pr, f[e], hs[2][e]);
-            hs[3][e] = __builtin_fmaf(tv, f[e], hs[3][e]);
-          }
-          if (cb == 0) {
-            hs1[0] += tq;
-            hs1[1] += qq;
-            hs1[2] += pr;
-            hs1[3] += tv;
-            hl[0] += tv * pr;
-            if (p.head_bce) hl[1] += fmaxf(zl, 0.f) - zl * tv + log1pf(__expf(-fabsf(zl)));
-          }
-        }
       }
     }
   }
@@ -536,44 +505,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
           q = cb == r ? hq[CPR * k + r] : q;
         }
         if (q < M) p.head_logit[q] = z;
-      }
-      if (kHS) {
-        // lanes congruent mod CPR hold the same channels: fold them, then the waves in
-        // fixed order through LDS (past the staging tile) -> one row per window
-        constexpr int HW = 4 * (BN + 1) + 4;
-#pragma unroll
-        for (int o = CPR; o < 64; o <<= 1) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) hs[k][e] += __shfl_xor(hs[k][e], o, 64);
-            hs1[k] += __shfl_xor(hs1[k], o, 64);
-          }
-          hl[0] += __shfl_xor(hl[0], o, 64);
-          hl[1] += __shfl_xor(hl[1], o, 64);
-        }
-        const int wv = tid >> 6, ln = tid & 63;
-        if (ln < CPR) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) SP[wv * HW + k * (BN + 1) + ln * 8 + e] = hs[k][e];
-            if (ln == 0) SP[wv * HW + k * (BN + 1) + BN] = hs1[k];
-          }
-          if (ln == 0) {               // loss partials in head_finish's order {I, St, Sp, BCE}
-            SP[wv * HW + 4 * (BN + 1) + 0] = hl[0];
-            SP[wv * HW + 4 * (BN + 1) + 1] = hs1[3];
-            SP[wv * HW + 4 * (BN + 1) + 2] = hs1[2];
-            SP[wv * HW + 4 * (BN + 1) + 3] = hl[1];
-          }
-        }
-        __syncthreads();
-        for (int j = tid; j < HW; j += NTHR) {
-          float a = 0.f;
-#pragma unroll
-          for (int w = 0; w < NTHR / 64; ++w) a += SP[w * HW + j];
-          p.head_sums[(size_t)stat_row * HW + j] = a;
-        }
       }
     }
   }

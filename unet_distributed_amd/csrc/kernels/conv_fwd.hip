@@ -977,8 +977,6 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     if (t == 7) return "conv_fwd: tile 7 (row-window 512x64: 268 registers, 92 KB LDS, 1 wave/SIMD) is not built";
     if (t == 6 && !win_eligible(p)) return "conv_fwd: row-window tile not applicable";
   }
-  if (p.head_sums && (!p.head_w || !p.head_t)) return "conv_fwd: head sums need the fused head and head_t";
-  if (p.head_nostore && !p.head_sums) return "conv_fwd: head_nostore needs head_sums (the head backward reads y)";
   if (p.head_w) {
     if (!p.head_b || !p.head_logit) return "conv_fwd: fused head needs head_b / head_logit";
     if (p.Cout != 32 || p.drop_rate > 0.f || !p.relu || p.D1 != p.Cout || p.mask1 || p.out_scale != 1.f ||

@@ -120,19 +120,6 @@ struct ConvFwdParams {
   const float* head_w;
   const float* head_b;
   float* head_logit;
-  // Forward-side sums of the head's weight / bias gradients and of the loss (fused head,
-  // training): per window (statistics row) [4][Cout + 1] fp32 = {sum t q x, sum q x,
-  // sum p x, sum t x} over the window's pixels (p = sigmoid(logit), q = p (1 - p),
-  // t = target, x = head input; column Cout: x = 1), then the loss partials {sum t p,
-  // sum t, sum p, sum BCE} (head.hip::head_finish's).  The head's dlogit is affine in t and
-  // q (head_grad.h), so head.hip::head_sums_grad turns the moments into dW / db with the
-  // loss scalars -- the backward's 1 GiB re-read of the head input disappears -- and
-  // head_logit receives the probabilities (no head_finish pass).  nullptr: off.
-  float* head_sums;
-  const void* head_t;         // [pixels] 16-bit targets of the launch's pixels (head_sums)
-  int head_bce;               // head_sums: also the BCE partial (else 0; only Dice + BCE reads it)
-  int head_nostore;           // fused head: the activation itself is not stored (nothing reads it:
-                              // head-on-load backward + head_sums); ReLU bits still are
   int rev;                    // row-window kernels: windows in reverse order (the consumer starts
                               // where its producer ended, on the tail still in the Infinity Cache)
   HeadGrad hg;                // 2D row-window data gradient of the head input: src1 (dY) formed

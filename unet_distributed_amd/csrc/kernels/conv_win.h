@@ -122,8 +122,6 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   char* Xs = smem;
   char* Ws = smem + XB;
-  // (fused head: the head-gradient sums' wave rows sit past the 64-byte staging rows)
-  static_assert(!(EPI == EPI_FWD && BN == 32) || BM * 64 + 4 * (4 * (BN + 1) + 4) * 4 <= LDS_BYTES, "head sums LDS");
 
   // wave index as a scalar: every per-wave quantity below (rows, DMA slots) stays in SGPRs
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);

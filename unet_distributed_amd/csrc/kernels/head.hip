@@ -252,52 +252,6 @@ hipError_t head_fwd_launch(const void* x, const float* w, const float* b, const 
   return hipGetLastError();
 }
 
-// Head weight / bias gradients from the fused-head forward's per-window sums (conv_params.h
-// head_sums): column j of the rows [nrows][4 (C + 1) + 4] summed in fixed order (thread-strided
-// rows, then a fixed tree), then
-//   g_j = gscale (a S_tqx + bb S_qx + bce_w inv_total (S_px - S_tx))
-// -- the same affine form head_grad.h::head_dlogit has in t and q = p (1 - p).  One block
-// per column; column C (x = 1) is the bias.
-__global__ void __launch_bounds__(256) head_sums_grad_kernel(const float* __restrict__ rows, int nrows, int C,
-                                                            const float* __restrict__ sums, float inv_total,
-                                                            float bce_w, float gscale,
-                                                            const float* __restrict__ gscale_ptr,
-                                                            float* __restrict__ gw, float* __restrict__ gb) {
-  __shared__ float red[4][256];
-  const int j = blockIdx.x, W = 4 * (C + 1) + 4;
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int r = threadIdx.x; r < nrows; r += 256) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) s[k] += rows[(size_t)r * W + k * (C + 1) + j];
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = s[k];
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    if (gscale_ptr) gscale = *gscale_ptr;
-    const float I = sums[0], St = sums[1], Sp = sums[2];
-    const float a = -2.f / (2.f * I + 1.f);
-    const float bb = 1.f / (St + Sp + 1.f);
-    const float g = gscale * (a * red[0][0] + bb * red[1][0] + bce_w * inv_total * (red[2][0] - red[3][0]));
-    if (j < C) gw[j] = g;
-    else *gb = g;
-  }
-}
-
-hipError_t head_sums_grad_launch(const float* rows, int nrows, int C, const float* sums, float inv_total, float bce_w,
-                                 float gscale, const float* gscale_ptr, float* gw, float* gb, hipStream_t s) {
-  hipLaunchKernelGGL(head_sums_grad_kernel, dim3(C + 1), dim3(256), 0, s, rows, nrows, C, sums, inv_total, bce_w,
-                     gscale, gscale_ptr, gw, gb);
-  return hipGetLastError();
-}
-
 hipError_t head_bwd_launch(const void* x, const float* w, const float* prob, const void* t, const float* sums, int P,
                            int C, float inv_total, float bce_w, float gscale, const float* gscale_ptr, void* dx,
                            float* partial, float* gw, float* gb, hipStream_t s) {
@@ -319,8 +273,8 @@ hipError_t head_bwd_launch(const void* x, const float* w, const float* prob, con
   return hipGetLastError();
 }
 
-hipError_t partial_reduce_launch(const float* partial, int nb, int width, float* out, hipStream_t s, int ncols) {
-  hipLaunchKernelGGL(partial_reduce_kernel, dim3(ncols > 0 ? ncols : width), dim3(256), 0, s, partial, nb, width, out);
+hipError_t partial_reduce_launch(const float* partial, int nb, int width, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3(width), dim3(256), 0, s, partial, nb, width, out);
   return hipGetLastError();
 }
 

@@ -139,10 +139,6 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.head_w = (const float*)getp(d, "head_w");
   p.head_b = (const float*)getp(d, "head_b");
   p.head_logit = (float*)const_cast<void*>(getp(d, "head_logit"));
-  p.head_sums = (float*)const_cast<void*>(getp(d, "head_sums"));
-  p.head_t = getp(d, "head_t");
-  p.head_bce = get<int>(d, "head_bce", 1);
-  p.head_nostore = get<int>(d, "head_nostore", 0);
   p.hg = head_grad(d);
   if (!p.src1 || !p.wgt || !p.dst1) throw std::invalid_argument("conv_fwd: src1/wgt/dst1 required");
   check_msg(conv_fwd_prepare(p));
@@ -210,7 +206,6 @@ WgradParams wgrad_params(const py::dict& d) {
   X(upsample2_fwd_launch) \
   X(head_fwd_launch) \
   X(head_bwd_launch) \
-  X(head_sums_grad_launch) \
   X(partial_reduce_launch) \
   X(head_finish_launch) \
   X(norm_head_launch) \
@@ -468,9 +463,7 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     const float* part = (const float*)vp(0);
     float* out = (float*)vp(1);
     int nb = I[0], width = I[1];
-    const int ncols = I.size() > 2 ? I[2] : 0;     // optional: columns [0, ncols) of width-wide rows
-    if (ncols < 0 || ncols > width) throw std::invalid_argument("partial_reduce: 0 <= ncols <= width");
-    return [=](hipStream_t s) { return A->partial_reduce_launch(part, nb, width, out, s, ncols); };
+    return [=](hipStream_t s) { return A->partial_reduce_launch(part, nb, width, out, s); };
   }
   if (kind == "head_fwd") {
     need(7, 2, 0);
@@ -499,18 +492,6 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     return [=](hipStream_t s) {
       return A->head_bwd_launch(x, w, prob, t, sums, P_, C, it, bw, gs, gsp, dx, part, gw, gb, s);
     };
-  }
-  if (kind == "head_sums_grad") {
-    // ptrs: rows, sums, gw, gb [, gscale_ptr]   ints: nrows, C   floats: inv_total, bce_w, gscale
-    need(4, 2, 3);
-    const float *rows = (const float*)vp(0), *sums = (const float*)vp(1);
-    float *gw = (float*)vp(2), *gb = (float*)vp(3);
-    const float* gsp = P.size() > 4 ? (const float*)vp(4) : nullptr;
-    int nr = I[0], C = I[1];
-    check_msg(head_check(C));
-    if (nr <= 0) throw std::invalid_argument("head_sums_grad: nrows > 0");
-    float it = (float)F[0], bw = (float)F[1], gs = (float)F[2];
-    return [=](hipStream_t s) { return A->head_sums_grad_launch(rows, nr, C, sums, it, bw, gs, gsp, gw, gb, s); };
   }
   if (kind == "norm_moments") {
     // ptrs: A, B, partial, S   ints: N, P, C    (S[n][2][C] = per-sample sums of A and A*B)

@@ -61,10 +61,8 @@ def _r64(k: int) -> int:
 #                slab sums (1; 0: full weight gradient over u)
 #   tconv_onload deepest fine level whose transposed-conv output u is formed on load by its
 #                consumer's forward where nothing else reads it (1; 0: materialised)
-#   head_sums    the Mask head's weight / bias gradients from per-window sums the fused-head
-#                forward accumulates (1; 0: head backward pass over the head input)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
-                       tconv_onload=1, head_sums=1)
+                       tconv_onload=1)
 
 
 def engine_options(overrides: Optional[Dict[str, int]] = None) -> Dict[str, int]:
@@ -941,8 +939,6 @@ class NativeUNet:
                     d.update(head_w=self.master_ptr("Mask/kernel"), head_b=self.master_ptr("Mask/bias"),
                              head_logit=_ptr(self.prob) + 4 * c * nb * (self.npix(1) // self.B))
                     self._head_fused_blocks = nbk
-                    if train and plan is self.plan and self.head_onload and self.opts["head_sums"]:
-                        self._head_sums_fields(d, c, nb)
             self._rev_order(d, src1, l.name, pool if pool in self._pool_fused else None)
             fused = None
             if normed and (train or spec.norm == "group"):
@@ -969,11 +965,6 @@ class NativeUNet:
                      bias=self.master_ptr(l.name + "/bias"), Cout=(2 ** self.dims) * l.cout,
                      relu=0, shuffle=self.dims, dst1=P(l.name))
             plan.add_conv_fwd(d)
-        elif l.kind == "mask" and train and plan is self.plan and getattr(self, "_head_sums_rows", 0):
-            # loss partials of the fused-head windows -> sums (probabilities already stored)
-            w = self._head_sums_width()
-            plan.add_generic("partial_reduce", [_ptr(self.head_srows) + 4 * (w - 4), _ptr(self.sums)],
-                             [self._head_sums_rows, w, 4], [], "fwd:Mask")
         elif l.kind == "mask" and train and self._norm_head_loss:
             pass                                 # loss sums written by norm_head_loss
         elif l.kind == "mask" and (self._head_fused_blocks or self._norm_head):
@@ -987,27 +978,6 @@ class NativeUNet:
                                           self.master_ptr("Mask/bias"), _ptr(self.target),
                                           _ptr(self.prob), _ptr(part), _ptr(self.sums)],
                              [P1, hc], [], "fwd:Mask")
-
-    def _head_sums_width(self):
-        """Floats per window row of the fused-head sums: [4][C + 1] moments + 4 loss partials."""
-        return 4 * (self.tinfo[self.head_in][1] + 1) + 4
-
-    def _head_sums_fields(self, d, c, nb):
-        """Fused-head forward of chunk c (images [c nb, (c + 1) nb)) also accumulates the
-        head's weight / bias gradient sums and the loss partials per window and stores
-        probabilities (conv_params.h head_sums): the forward's head_finish pass becomes a
-        reduction of the rows, the backward's head pass head_sums_grad."""
-        rows, _ = self.C.conv_stat_tiles(d)
-        hc = self.tinfo[self.head_in][1]
-        width = self._head_sums_width()
-        nch = self.B // nb
-        if getattr(self, "head_srows", None) is None or self.head_srows.numel() != nch * rows * width:
-            self.head_srows = torch.zeros(nch * rows * width, dtype=torch.float32, device=self.device)
-        self._head_sums_rows = nch * rows
-        # (head-on-load + head sums: nothing reads the head input itself -- only its ReLU bits)
-        d.update(head_sums=_ptr(self.head_srows) + 4 * c * rows * width, head_bce=int(self.loss == "dice_bce"),
-                 head_nostore=1,
-                 head_t=_ptr(self.target) + self.target.element_size() * c * nb * (self.npix(1) // self.B))
 
     def _rev_order(self, d, src, out, *also):
         """_rev_mode bit 0 (forward) / bit 1 (data gradients): a row-window conv
@@ -1122,15 +1092,6 @@ class NativeUNet:
                                             _ptr(self.loss_scale_dev)],
                              [Nb, Pb, hc, 0 if spec.norm == "batch" else hc], [inv_total, self.bce_weight, 1.0],
                              "bwd:Mask")
-                done("Mask")
-            elif l.kind == "mask" and getattr(self, "_head_sums_rows", 0):
-                # head gradients from the forward's per-window sums: no pass over the head
-                # input (side stream)
-                hc = self.tinfo[self.head_in][1]
-                emit_generic("head_sums_grad",
-                             lambda hc=hc: [_ptr(self.head_srows), _ptr(self.sums), self.grad_ptr("Mask/kernel"),
-                                            self.grad_ptr("Mask/bias"), _ptr(self.loss_scale_dev)],
-                             [self._head_sums_rows, hc], [inv_total, self.bce_weight, 1.0], "wgrad:Mask")
                 done("Mask")
             elif l.kind == "mask":
                 hc = self.tinfo[self.head_in][1]
