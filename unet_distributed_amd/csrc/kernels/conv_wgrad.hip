@@ -431,6 +431,9 @@ __global__ void __launch_bounds__(256) colsum_kernel(const h16* __restrict__ x, 
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
   if (rr < rpi) {
+    // (unrolled: 8 row loads in flight per thread instead of one dependent load per add;
+    // the adds keep their row order)
+#pragma unroll 8
     for (int r = r0 + rr; r < r1; r += rpi) {
       const u32x4 v = *(const u32x4*)(x + (size_t)r * C + cc * 8);
       float f[8];
