@@ -13,6 +13,8 @@
 #   bash scripts/gpu_dice_parity.sh [steps] [seeds...]
 set -o pipefail
 export TMPDIR=/tmp
+# (the ATen fp32 arms: immediate-mode MIOpen kernel choice, no per-shape search)
+export MIOPEN_FIND_MODE=${MIOPEN_FIND_MODE:-FAST}
 steps=${1:-300}; shift || true
 seeds=${@:-1 2 3}
 mkdir -p gpurun_out/dice

@@ -12,3 +12,4 @@ bash scripts/gpu_timeline.sh r4 || exit 1
 bash scripts/gpu_stall_pmc.sh r4 || exit 1
 python tools/stall_table.py $(find gpurun_out/stall_r4/pmc1 -name "*.db" | head -1) > gpurun_out/stall_r4/stall_table.md || exit 1
 bash scripts/gpu_scale.sh gpurun_out/scale_r4.md || exit 1
+bash scripts/gpu_profile.sh r4 || exit 1

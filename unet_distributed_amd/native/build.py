@@ -78,6 +78,20 @@ def _compile(job):
     return obj, True
 
 
+def _check_kernel_stubs(so):
+    """Every launched kernel's host stub must be defined in the library: clang can drop a
+    kernel's stub silently (e.g. a lambda call inside a target builtin's argument list),
+    which only surfaces as an undefined symbol when the extension is imported."""
+    import shutil
+    nm = shutil.which("nm") or shutil.which("llvm-nm")
+    if nm is None:
+        return
+    r = subprocess.run([nm, "-u", "-C", so], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    bad = [ln.strip() for ln in r.stdout.splitlines() if "__device_stub__" in ln]
+    if bad:
+        raise RuntimeError("undefined kernel stubs in %s:\n%s" % (so, "\n".join(bad[:20])))
+
+
 def build(verbose=True, jobs=None):
     os.makedirs(OBJDIR, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")) +
@@ -104,6 +118,7 @@ def build(verbose=True, jobs=None):
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed: %s\n%s" % (" ".join(cmd), r.stdout))
+        _check_kernel_stubs(out + ".tmp")
         os.replace(out + ".tmp", out)
         with open(manifest, "w") as f:
             f.write(want)
