@@ -389,7 +389,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
     };
     // PF (p.win_pf; 2D rows <= 64 wide, no operand transform): register-staged double
     // buffering of the chunk loop -- chunk kc + 1's halo and weight pieces (the same 16-byte
-    // units, offsets and out-of-range zeros as the LDS-DMA) are loaded into registers while
+    // units, offsets and out-of-range zeros as the LDS-DMA; plain global loads) are loaded into registers while
     // chunk kc's MFMAs run, and written to LDS after them; chunk 0 is DMA'd as usual.  Two
     // workgroups per CU stay (LDS unchanged, +<= 64 VGPRs).  (Plain loads survive the
     // barriers: no LDS-DMA is in flight after chunk 0's wait.)
@@ -448,8 +448,8 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
             if (k < XI) {
               bool f1;
               const int off = x_off(kc + 1, k, f1);
-              const __amdgpu_buffer_rsrc_t rs = f1 ? rs1 : rs2;
-              px[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+              const char* base = f1 ? s1b : s2b;
+              px[q] = off != OOB ? *(const u32x4*)(base + off) : (u32x4){0u, 0u, 0u, 0u};
             }
           }
 #pragma unroll
@@ -457,7 +457,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
             const int k = wave + 4 * q;
             if (k < WI) {
               const int wo = w_off(kc + 1, k);
-              pw[q] = __builtin_amdgcn_raw_buffer_load_b128(rsw, wo, 0, 0);
+              pw[q] = *(const u32x4*)((const char*)p.wgt + wo);
             }
           }
         }
