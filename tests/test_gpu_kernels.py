@@ -1030,8 +1030,9 @@ def test_window_register_prefetch_bit_identical(cuda_dev, N, H, C1, C2, Co):
     x2 = F.relu(torch.randn(N, H, H, C2, device=dev)).bfloat16() if C2 else None
     w = (torch.randn(3, 3, C1 + C2, Co, device=dev) * 0.1).bfloat16()
     b = torch.randn(Co, device=dev)
+    wp = pack_fwd(w)                    # (kept alive: the dict holds raw pointers)
     base = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=C1, C2=C2, src1=ptr(x1),
-                src2=ptr(x2) if C2 else None, wgt=ptr(pack_fwd(w)), Cout=Co)
+                src2=ptr(x2) if C2 else None, wgt=ptr(wp), Cout=Co)
     for mode in ("fwd", "stats", "dgrad"):
         outs = []
         for pf in (0, 1):
