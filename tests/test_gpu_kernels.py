@@ -1033,6 +1033,7 @@ def test_window_register_prefetch_bit_identical(cuda_dev, N, H, C1, C2, Co):
     wp = pack_fwd(w)                    # (kept alive: the dict holds raw pointers)
     base = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=C1, C2=C2, src1=ptr(x1),
                 src2=ptr(x2) if C2 else None, wgt=ptr(wp), Cout=Co)
+    m = (torch.rand(N * H * H * Co // 8, device=dev) * 255).to(torch.uint8)     # dgrad ReLU bits
     for mode in ("fwd", "stats", "dgrad"):
         outs = []
         for pf in (0, 1):
@@ -1049,7 +1050,6 @@ def test_window_register_prefetch_bit_identical(cuda_dev, N, H, C1, C2, Co):
                 d.update(bias=ptr(b), stats=ptr(st))
                 extra.append(st)
             else:
-                m = (torch.rand(N * H * H * Co // 8, device=dev) * 255).to(torch.uint8)
                 d.update(mask1=ptr(m), mask_bits=1)
             assert C().conv_fwd_grid(d) > 0
             C().conv_fwd(d, stream())
