@@ -387,13 +387,16 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
         }
       }
     };
-    // PF (p.win_pf; 2D rows <= 64 wide, no operand transform): register-staged double
+    // PF (p.win_pf; 2D 64-wide rows, single source, no operand transform): register-staged double
     // buffering of the chunk loop -- chunk kc + 1's halo and weight pieces (the same 16-byte
     // units, offsets and out-of-range zeros as the LDS-DMA; plain global loads) are loaded into registers while
     // chunk kc's MFMAs run, and written to LDS after them; chunk 0 is DMA'd as usual.  Two
     // workgroups per CU stay (LDS unchanged, +<= 64 VGPRs).  (Plain loads survive the
     // barriers: no LDS-DMA is in flight after chunk 0's wait.)
-    constexpr bool PFOK = GEO == GEO_2D && XF == 0 && W <= 64;
+    // (measured per launch, round 4: -4..-10 % on the 64-wide single-source convs with 2 chunks;
+    // +4..+19 % on 16 / 32-wide rows and on dual-source windows, whose MFMA-bound chunk
+    // loops pay for the extra address VALU and LDS writes -- those keep the DMA loop)
+    constexpr bool PFOK = GEO == GEO_2D && XF == 0 && W == 64 && !CONCAT;
     bool pf_done = false;
     if constexpr (PFOK) {
     if (p.win_pf && nchunks > 1) {

@@ -61,8 +61,8 @@ def _r64(k: int) -> int:
 #                slab sums (1; 0: full weight gradient over u)
 #   tconv_onload deepest fine level whose transposed-conv output u is formed on load by its
 #                consumer's forward where nothing else reads it (1; 0: materialised)
-#   win_pf       row-window convs on rows <= 64 wide load chunk k + 1 into registers under
-#                chunk k's MFMAs (conv_win.h PF; 1)
+#   win_pf       64-wide single-source row-window convs load chunk k + 1 into registers
+#                under chunk k's MFMAs (conv_win.h PF; 1)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
                        tconv_onload=1, win_pf=1)
 
