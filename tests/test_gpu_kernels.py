@@ -1017,48 +1017,3 @@ def test_conv_img8_norm_statistics(cuda_dev):
     zf = z0.float().reshape(-1, Co)
     assert rel_err(s0[0], zf.sum(0)) < 1e-3 and rel_err(s0[1], (zf * zf).sum(0)) < 1e-3
 
-
-@pytest.mark.parametrize("N,H,C1,C2,Co", [(2, 64, 64, 0, 64), (3, 64, 128, 0, 64), (2, 64, 64, 0, 32),
-                                          (5, 64, 32, 0, 64), (2, 32, 64, 64, 64)])
-def test_window_register_prefetch_bit_identical(cuda_dev, N, H, C1, C2, Co):
-    """win_pf=1 (conv_win.h PF: chunk k + 1 loaded into registers under chunk k's MFMAs,
-    64-wide single-source rows; elsewhere the flag is ignored) gives the single-buffered
-    kernel's results bit for bit: forward with
-    bias / ReLU / bits, statistics epilogue, masked data gradient."""
-    torch.manual_seed(21)
-    dev = cuda_dev
-    x1 = F.relu(torch.randn(N, H, H, C1, device=dev)).bfloat16()
-    x2 = F.relu(torch.randn(N, H, H, C2, device=dev)).bfloat16() if C2 else None
-    w = (torch.randn(3, 3, C1 + C2, Co, device=dev) * 0.1).bfloat16()
-    b = torch.randn(Co, device=dev)
-    wp = pack_fwd(w)                    # (kept alive: the dict holds raw pointers)
-    base = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=C1, C2=C2, src1=ptr(x1),
-                src2=ptr(x2) if C2 else None, wgt=ptr(wp), Cout=Co)
-    m = (torch.rand(N * H * H * Co // 8, device=dev) * 255).to(torch.uint8)     # dgrad ReLU bits
-    for mode in ("fwd", "stats", "dgrad"):
-        outs = []
-        for pf in (0, 1):
-            y = torch.full((N, H, H, Co), float("nan"), device=dev, dtype=torch.bfloat16)
-            extra = []
-            d = dict(base, dst1=ptr(y), win_pf=pf)
-            if mode == "fwd":
-                bits = torch.zeros(N * H * H * Co // 8, device=dev, dtype=torch.uint8)
-                d.update(bias=ptr(b), relu=1, relu_bits=ptr(bits))
-                extra.append(bits)
-            elif mode == "stats":
-                rows, _ = C().conv_stat_tiles(dict(d, stats=1))
-                st = torch.zeros(rows * 2 * Co, device=dev)
-                d.update(bias=ptr(b), stats=ptr(st))
-                extra.append(st)
-            else:
-                d.update(mask1=ptr(m), mask_bits=1)
-            assert C().conv_fwd_grid(d) > 0
-            C().conv_fwd(d, stream())
-            torch.cuda.synchronize()
-            outs.append([y] + extra)
-        for a, c in zip(outs[0], outs[1]):
-            assert torch.equal(a, c), mode
-        if mode == "fwd":
-            xin = nchw(torch.cat([x1, x2], -1).float() if C2 else x1.float())
-            ref = nhwc(F.relu(F.conv2d(xin, w.float().permute(3, 2, 0, 1), b, padding=1)))
-            assert rel_err(outs[1][0], ref) < 1e-2

@@ -115,7 +115,6 @@ struct ConvFwdParams {
   const void* xz;
   void* xout;
   int tile;                  // 0 = auto, else forced tile config id (tuning / A-B tests)
-  int win_pf;                // row-window kernels on rows <= 64 wide: register-prefetched chunk loop
   // Fused segmentation head (row-window forward, Cout == 32, EPI_FWD only): per pixel
   // z = sum_c out[c] head_w[c] + head_b -> head_logit (fp32) for head_finish
   const float* head_w;

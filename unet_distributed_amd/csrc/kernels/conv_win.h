@@ -387,102 +387,6 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
         }
       }
     };
-    // PF (p.win_pf; 2D 64-wide rows, single source, no operand transform): register-staged double
-    // buffering of the chunk loop -- chunk kc + 1's halo and weight pieces (the same 16-byte
-    // units, offsets and out-of-range zeros as the LDS-DMA; plain global loads) are loaded into registers while
-    // chunk kc's MFMAs run, and written to LDS after them; chunk 0 is DMA'd as usual.  Two
-    // workgroups per CU stay (LDS unchanged, +<= 64 VGPRs).  (Plain loads survive the
-    // barriers: no LDS-DMA is in flight after chunk 0's wait.)
-    // (measured per launch, round 4: -4..-10 % on the 64-wide single-source convs with 2 chunks;
-    // +4..+19 % on 16 / 32-wide rows and on dual-source windows, whose MFMA-bound chunk
-    // loops pay for the extra address VALU and LDS writes -- those keep the DMA loop)
-    constexpr bool PFOK = GEO == GEO_2D && XF == 0 && W == 64 && !CONCAT;
-    bool pf_done = false;
-    if constexpr (PFOK) {
-    if (p.win_pf && nchunks > 1) {
-      pf_done = true;
-      constexpr int NX = (XI + 3) / 4, NW = (WI + 3) / 4;
-      u32x4 px[NX], pw[NW];
-      auto x_off = [&](const int kc, const int k, bool& f1) -> int {
-        f1 = !CONCAT || (kc << 5) < p.C1;
-        const int C = f1 ? p.C1 : p.C2, cb = f1 ? (kc << 5) : (kc << 5) - p.C1;
-        const int sl = 16 * k + lslot;
-        const int hr = sl / HWP, hc = sl - hr * HWP;
-        const int gr = g0 - 1 + hr, col = hc - 1;
-        const bool row_in = hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in);
-        const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
-        const int lch = (lane & 3) ^ ((hc >> 1) & 3);
-        return ok ? (((gr - grow0) * W + col) * C + cb + lch * 8) * 2 : OOB;
-      };
-      auto w_off = [&](const int kc, const int k) -> int {
-        const int tap = k / (BN / 16), nb = (k % (BN / 16)) * 16;
-        return ((n0 + nb) * p.Kpad + tap * Cin) * 2 + (lslot * p.Kpad + (kc << 5) + lchunk * 8) * 2;
-      };
-      // chunk 0: LDS-DMA
-#pragma unroll
-      for (int q = 0; q < NX; ++q) {
-        const int k = wave + 4 * q;
-        if (k < XI) {
-          bool f1;
-          const int off = x_off(0, k, f1);
-          const __amdgpu_buffer_rsrc_t rs = f1 ? rs1 : rs2;
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16, off,
-                                                   0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        const int k = wave + 4 * q;
-        if (k < WI) {
-          // (offsets into locals first: a lambda call inside a builtin's argument list makes
-          // clang drop the kernel's host stub -- an undefined symbol at load time)
-          const int wo = w_off(0, k);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024), 16, wo,
-                                                   0, 0, 0);
-        }
-      }
-      __syncthreads();
-      for (int kc = 0; kc < nchunks; ++kc) {
-        const bool more = kc + 1 < nchunks;
-        if (more) {
-#pragma unroll
-          for (int q = 0; q < NX; ++q) {
-            const int k = wave + 4 * q;
-            if (k < XI) {
-              bool f1;
-              const int off = x_off(kc + 1, k, f1);
-              const char* base = f1 ? s1b : s2b;
-              px[q] = off != OOB ? *(const u32x4*)(base + off) : (u32x4){0u, 0u, 0u, 0u};
-            }
-          }
-#pragma unroll
-          for (int q = 0; q < NW; ++q) {
-            const int k = wave + 4 * q;
-            if (k < WI) {
-              const int wo = w_off(kc + 1, k);
-              pw[q] = *(const u32x4*)((const char*)p.wgt + wo);
-            }
-          }
-        }
-        chunk_mfmas(0x1ffu);
-        if (more) {
-          __syncthreads();                          // every wave is done reading chunk kc
-#pragma unroll
-          for (int q = 0; q < NX; ++q) {
-            const int k = wave + 4 * q;
-            if (k < XI) *(u32x4*)(Xs + k * 1024 + lane * 16) = px[q];
-          }
-#pragma unroll
-          for (int q = 0; q < NW; ++q) {
-            const int k = wave + 4 * q;
-            if (k < WI) *(u32x4*)(Ws + k * 1024 + lane * 16) = pw[q];
-          }
-          __syncthreads();
-        }
-      }
-    }
-    }
-    if (!pf_done)
     for (int kc = 0; kc < nchunks; ++kc) {
       const bool from1 = !CONCAT || (kc << 5) < p.C1;
       // space-to-depth gathered chunk: every chunk of XF 4

@@ -136,7 +136,6 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.ut.kpad = get<int>(d, "ut_kpad", 0);
   p.xout = const_cast<void*>(getp(d, "xout"));
   p.tile = get<int>(d, "tile", 0);
-  p.win_pf = get<int>(d, "win_pf", 0);
   p.head_w = (const float*)getp(d, "head_w");
   p.head_b = (const float*)getp(d, "head_b");
   p.head_logit = (float*)const_cast<void*>(getp(d, "head_logit"));

@@ -61,10 +61,8 @@ def _r64(k: int) -> int:
 #                slab sums (1; 0: full weight gradient over u)
 #   tconv_onload deepest fine level whose transposed-conv output u is formed on load by its
 #                consumer's forward where nothing else reads it (1; 0: materialised)
-#   win_pf       64-wide single-source row-window convs load chunk k + 1 into registers
-#                under chunk k's MFMAs (conv_win.h PF; 1)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
-                       tconv_onload=1, win_pf=1)
+                       tconv_onload=1)
 
 
 def engine_options(overrides: Optional[Dict[str, int]] = None) -> Dict[str, int]:
@@ -764,7 +762,7 @@ class NativeUNet:
         idd, ih, iw = self.sdims(in_level or level)
         kd = K if self.dims == 3 else 1
         return dict(N=self.B, OD=od, OH=oh, OW=ow, ID=idd, IH=ih, IW=iw, KD=kd, KH=K, KW=K,
-                    stride=stride, pad=pad, tile=0, win_pf=self.opts["win_pf"])
+                    stride=stride, pad=pad, tile=0)
 
     def _salt(self, lname):
         return [l.name for l in self.spec.layers].index(lname)
