@@ -61,8 +61,10 @@ def _r64(k: int) -> int:
 #                slab sums (1; 0: full weight gradient over u)
 #   tconv_onload deepest fine level whose transposed-conv output u is formed on load by its
 #                consumer's forward where nothing else reads it (1; 0: materialised)
+#   fwd_offset   layers of chunk 0 before the second forward chunk starts (6)
+#   wg_target    weight-gradient split-K grid target, workgroups per gradient (512)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
-                       tconv_onload=1)
+                       tconv_onload=1, fwd_offset=6, wg_target=512)
 
 
 def engine_options(overrides: Optional[Dict[str, int]] = None) -> Dict[str, int]:
@@ -132,7 +134,7 @@ class NativeUNet:
         # wgrad split-K grid target (workgroups per weight gradient): ~2 per CU.  Dual
         # stream at the default per-GPU batch 1024: 512 > 768 > 384 > 256 > 1024 >> 128
         # (same-box sweep, +1.7 % over 256; 640 re-measured -0.4 % at the round-2 end)
-        self.wg_target = 512
+        self.wg_target = self.opts["wg_target"]
         # row-window convs walk their windows in the reverse of the order their input was
         # written (bit 0 forward, bit 1 data gradients; see _rev_order)
         self._rev_mode = 3
@@ -819,13 +821,12 @@ class NativeUNet:
                 continue
             self._xf_fwd.add(l.name)
 
-    # second forward chunk starts after the first chunk's first 6 layers (offset sweep
-    # 3 / 6 / 9 / 13: -0.2 / +0.3 / . / -0.6 %)
-    FWD_OFFSET = 6
+    # (option fwd_offset: the second forward chunk starts after the first chunk's first
+    # fwd_offset layers; round-2 sweep 3 / 6 / 9 / 13: -0.2 / +0.3 / . / -0.6 %)
 
     def _fwd_streams(self, train):
         """2: the training forward runs as two half-batch chunks on two HIP streams, the
-        second chunk started once the first has finished its first FWD_OFFSET layers, so kernels of different levels (bandwidth-bound full-resolution ones,
+        second chunk started once the first has finished its first fwd_offset layers, so kernels of different levels (bandwidth-bound full-resolution ones,
         MFMA-bound coarse ones) share the GPU.  Norm-free 2D model with an even batch
         (BatchNorm needs whole-batch statistics); option fwd_streams=1 keeps one stream.
         Default 2 since round 3: same-box interleaved A/B of the headline step +1.0 / +1.0 /
@@ -866,7 +867,7 @@ class NativeUNet:
         self._pool_fused = set()
         layers = [l for l in spec.layers if l.kind not in ("up", "mask")]
         nb = self.B // 2
-        off = self.FWD_OFFSET
+        off = self.opts["fwd_offset"]
         self._fwd2 = []                      # (first op, op after the offset layers, end) per chunk
         for c in range(2):
             start = plan.size()
