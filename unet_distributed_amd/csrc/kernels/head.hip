@@ -369,7 +369,7 @@ __device__ __forceinline__ void hn_scalars(const float* __restrict__ sums, float
 }
 
 template <int C>
-__global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(3))) norm_head_loss_kernel(const h16* __restrict__ z, const float* __restrict__ fa,
+__global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) norm_head_loss_kernel(const h16* __restrict__ z, const float* __restrict__ fa,
                                                             const float* __restrict__ fc, int cstride, int npix,
                                                             const float* __restrict__ w, const float* __restrict__ b,
                                                             const h16* __restrict__ t, h16* __restrict__ y,
@@ -394,7 +394,20 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(3))) no
   float su = 0.f, sv = 0.f, sw = 0.f, sI = 0.f, sT = 0.f, sP = 0.f, sB = 0.f;
   const int p0 = (int)((long long)blk * npix / nbp), p1 = (int)((long long)(blk + 1) * npix / nbp);
   const size_t sb = (size_t)n * npix;
-  auto pixel = [&](const u32x4 raw, const float tv, const size_t q) {
+  // per-pixel scalar terms (probability store, loss sums, BCE): one lane's share
+  auto scalars = [&](const float zl, const float pr, const float tv, const size_t q) {
+    const float vv = pr * (1.f - pr), uu = tv * vv, ww = pr - tv;
+    prob[q] = pr;
+    su += uu;
+    sv += vv;
+    sw += ww;
+    sI += tv * pr;
+    sT += tv;
+    sP += pr;
+    sB += fmaxf(zl, 0.f) - zl * tv + log1pf(__expf(-fabsf(zl)));
+  };
+  // channel sums of one pixel (every lane of the pixel holds its logit zl / probability pr)
+  auto pixel = [&](const u32x4 raw, const float tv, const size_t q, float& zl_out, float& pr_out) {
     float zf[8], v[8], yv[8];
     unpack8(raw, zf);
 #pragma unroll
@@ -424,25 +437,20 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(3))) no
       acc[4][e] = fmaf(mz, vv, acc[4][e]);
       acc[5][e] = fmaf(mz, ww, acc[5][e]);
     }
-    if (cc == 0) {
-      prob[q] = pr;
-      su += uu;
-      sv += vv;
-      sw += ww;
-      sI += tv * pr;
-      sT += tv;
-      sP += pr;
-      sB += fmaxf(zl, 0.f) - zl * tv + log1pf(__expf(-fabsf(zl)));
-    }
+    zl_out = zl;
+    pr_out = pr;
   };
-  // the CP lanes of one pixel are adjacent and always take the same path; KU pixel
-  // steps' loads are issued before any of them is used (memory-level parallelism: the
-  // per-pixel chain load -> dot -> shuffles -> sigmoid is long)
-  constexpr int KU = 2;
+  // the CP lanes of one pixel are adjacent and always take the same path.  KU = CP pixel
+  // steps per iteration, their loads issued before any is used (memory-level parallelism:
+  // the per-pixel chain load -> dot -> shuffles -> sigmoid is long); the scalar terms of
+  // step u are formed by lane cc = u of each pixel group, so the transcendental tail runs
+  // once per pixel across the group instead of on one lane while the other CP - 1 idle
+  // (it was most of the kernel's VALU time)
+  constexpr int KU = CP;
   int p = p0 + pr0;
   for (; p + (KU - 1) * PPB < p1; p += KU * PPB) {
     u32x4 raw[KU];
-    float tv[KU];
+    float tv[KU], zl[KU], pr[KU];
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
       const size_t q = sb + p + u * PPB;
@@ -450,11 +458,22 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(3))) no
       tv[u] = (float)t[q];
     }
 #pragma unroll
-    for (int u = 0; u < KU; ++u) pixel(raw[u], tv[u], sb + p + u * PPB);
+    for (int u = 0; u < KU; ++u) pixel(raw[u], tv[u], sb + p + u * PPB, zl[u], pr[u]);
+    float zs = zl[0], ps = pr[0], ts = tv[0];
+#pragma unroll
+    for (int u = 1; u < KU; ++u) {
+      zs = cc == u ? zl[u] : zs;
+      ps = cc == u ? pr[u] : ps;
+      ts = cc == u ? tv[u] : ts;
+    }
+    scalars(zs, ps, ts, sb + p + cc * PPB);
   }
   for (; p < p1; p += PPB) {
     const size_t q = sb + p;
-    pixel(*(const u32x4*)(z + q * C + c0), (float)t[q], q);
+    const float tq = (float)t[q];
+    float zl, pr;
+    pixel(*(const u32x4*)(z + q * C + c0), tq, q, zl, pr);
+    if (cc == 0) scalars(zl, pr, tq, q);
   }
   // lanes l, l + CP, l + 2 CP, ... of a wave hold the same channels
 #pragma unroll
