@@ -16,6 +16,7 @@ from pmc_summary import summary  # noqa: E402
 
 def short(name):
     """Readable kernel name: the function name plus its leading template arguments."""
+    name = name.replace("(anonymous namespace)::", "")
     m = re.search(r"(\w+)<([^<>]*)", name)
     if m:
         return "%s<%s>" % (m.group(1).split("::")[-1], m.group(2)[:40])
