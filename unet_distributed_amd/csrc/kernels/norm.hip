@@ -320,8 +320,10 @@ __global__ void __launch_bounds__(NT) norm_bwd_apply_kernel(const h16* __restric
     u32x4 rg[kUnroll], rz[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      rg[u] = *(const u32x4*)(g + base + (size_t)(p + u * rstep) * C);
-      rz[u] = *(const u32x4*)(z + base + (size_t)(p + u * rstep) * C);
+      // streaming reads (read once): non-temporal, so they do not evict the freshly
+      // written tensors the next kernels read from the last-level cache
+      rg[u] = __builtin_nontemporal_load((const u32x4*)(g + base + (size_t)(p + u * rstep) * C));
+      rz[u] = __builtin_nontemporal_load((const u32x4*)(z + base + (size_t)(p + u * rstep) * C));
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
