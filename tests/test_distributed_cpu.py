@@ -228,7 +228,8 @@ def test_inventory_roundtrip_and_remote_commands(tmp_path):
 def _run_bench(extra, nproc=2, timeout=600, env_extra=None):
     """The driver's multi-GPU bench command (`torch.distributed.run ... bench.py --gpus N`)."""
     port = _free_port()
-    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2", **(env_extra or {}))
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    env.update(env_extra or {})
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
            "--gpus", str(nproc)] + extra
@@ -267,3 +268,39 @@ def test_bench_py_two_ranks_gloo_cpu():
     rec = bench_record(r.stdout)
     check_multirank_bench(rec, 2)
     assert rec["comm"]["backend"] == "gloo" and rec["config"]["backend"] == "torch"
+
+
+@pytest.mark.slow
+def test_bench_py_eight_ranks_gloo_cpu():
+    """Rehearsal of the driver's 8-GPU lease command shape (`torch.distributed.run
+    --nproc-per-node 8 bench.py --gpus 8`) at world 8 on CPU/gloo: rank 0 prints one
+    line with n_gpus / global_batch / parallelism of the 8-rank job, every bucket gets an
+    allreduce time and the exposed-communication A/B is reported (`test_dist.py:385-398`)."""
+    r = _run_bench(["--backend", "torch", "--dtype", "fp32", "--per_gpu_batch", "1", "--img_size", "32",
+                    "--steps", "2", "--warmup", "1", "--bucket_mb", "4"], nproc=8,
+                   env_extra={"OMP_NUM_THREADS": "1"})
+    assert r.returncode == 0, r.stdout[-3000:]
+    rec = bench_record(r.stdout)
+    check_multirank_bench(rec, 8)
+    assert rec["config"]["global_batch"] == 8 and rec["comm"]["backend"] == "gloo"
+    assert len(rec["comm"]["buckets_mb"]) >= 4          # 29.6 MiB of fp32 gradients in 4 MiB buckets
+
+
+@pytest.mark.slow
+def test_train_py_four_ranks_kill_and_resume(tmp_path):
+    """SURVEY §4 tier 5 at world 4: a rank dies mid-run (the job fails fast, nothing
+    hangs), the relaunched job restores the last periodic checkpoint written before the
+    fault and trains only the remaining steps (`test_dist.py:347-362,380-381`)."""
+    extra = ["--steps", "6", "--save_model_secs", "0", "--dist_timeout_s", "60"]
+    r = _run_train(tmp_path, extra + ["--fault_inject_step", "3", "--fault_inject_rank", "2"], nproc=4,
+                   timeout=300)
+    assert r.returncode != 0 and "fault injected at step 3 on rank 2" in r.stdout, r.stdout[-3000:]
+    logdir = tmp_path / "ck" / "unet,lr=0.0005,conv2DTranspose,intra=50,inter=2"
+    assert "model_checkpoint_path: \"model.ckpt-3\"" in (logdir / "checkpoint").read_text()
+    r2 = _run_train(tmp_path, extra, nproc=4, timeout=300)
+    assert r2.returncode == 0, r2.stdout[-3000:]
+    assert "Restored checkpoint at global_step 3" in r2.stdout
+    recs = [json.loads(l) for l in open(tmp_path / "m.jsonl")]
+    steps = [x["step"] for x in recs if x["kind"] == "train"]
+    assert steps[:3] == [1, 2, 3] and steps[3:] == [4, 5, 6]
+    assert [x["step"] for x in recs if x["kind"] == "test_final"] == [6]

@@ -440,3 +440,94 @@ def test_first_layer_wgrad_dz_on_load(cuda_dev, N, H, Cpad, gn, splits):
     torch.cuda.synchronize()
     assert rel_err(g1, g0) < 1e-2, rel_err(g1, g0)
     assert rel_err(b1, b0) < 1e-2, rel_err(b1, b0)
+
+
+def _stats_ref(rows, Ch):
+    s = rows.double().reshape(-1, 2, Ch).sum(0)
+    return s[0], s[1]
+
+
+@pytest.mark.parametrize("R,Ch", [(128 * 37 + 5, 32), (20000 + 13, 64), (4096 * 9 + 1, 512), (31, 256)])
+def test_bn_stats_single_launch_many_slices(cuda_dev, R, Ch):
+    """bn_stats_fused_kernel directly (norm.hip): R rows large enough that the phase-1 grid
+    has far more than 32 slices with a ragged last slice (the 8-way unrolled slice loop and
+    its tail both run), modes 0 (forward) and 1 (backward), each launched twice on the same
+    workspace (the last block must reset the hand-off counter)."""
+    g = torch.Generator(device="cuda").manual_seed(R)
+    dev = cuda_dev
+    rows = torch.randn(R, 2, Ch, device=dev, generator=g)
+    rows[:, 1] = rows[:, 1].abs() * 3 + 2          # second moment rows: keep var > 0
+    count = float(R * 16)
+    eps, mom = 1e-3, 0.01
+    gamma = torch.rand(Ch, device=dev, generator=g) + 0.5
+    beta = torch.randn(Ch, device=dev, generator=g)
+    ws = torch.zeros(C().row_slices(R) * 2 * Ch + 64, device=dev)
+    f = lambda: torch.zeros(Ch, device=dev)
+    mean, rstd, fa, fc, ca, cb, cc, dg, db = (f() for _ in range(9))
+    rm, rv = f(), torch.ones(Ch, device=dev)
+    s1, s2 = _stats_ref(rows, Ch)
+    mu = s1 / count
+    var = (s2 / count - mu * mu).clamp_min(0)
+    r = torch.rsqrt(var + eps)
+    rm_ref, rv_ref = rm.double().clone(), rv.double().clone()
+    for rep in range(2):
+        C().generic("bn_stats", [ptr(rows), ptr(gamma), ptr(beta), ptr(rm), ptr(rv), ptr(mean), ptr(rstd), ptr(fa),
+                                 ptr(fc), 0, 0, 0, 0, 0, ptr(ws)], [R, Ch, 0], [count, eps, mom], stream())
+        torch.cuda.synchronize()
+        rm_ref = (1 - mom) * rm_ref + mom * mu
+        rv_ref = (1 - mom) * rv_ref + mom * var * (count / (count - 1))
+        assert torch.allclose(mean.double(), mu, rtol=1e-5, atol=1e-6), rep
+        assert torch.allclose(rstd.double(), r, rtol=1e-4), rep
+        assert torch.allclose(fa.double(), gamma.double() * r, rtol=1e-4), rep
+        assert torch.allclose(fc.double(), beta.double() - mu * gamma.double() * r, rtol=1e-4, atol=1e-5), rep
+        assert torch.allclose(rm.double(), rm_ref, rtol=1e-5, atol=1e-6), rep
+        assert torch.allclose(rv.double(), rv_ref, rtol=1e-5, atol=1e-6), rep
+        assert ws[-64:].abs().sum().item() == 0, "hand-off counter not reset"
+    # backward (mode 1): rows = {sum g, sum g z}; mean / rstd from the forward above
+    grows = torch.randn(R, 2, Ch, device=dev, generator=g)
+    t1, t2 = _stats_ref(grows, Ch)
+    gm, mu_, r_ = gamma.double(), mean.double(), rstd.double()
+    sgx = r_ * (t2 - mu_ * t1)
+    for rep in range(2):
+        C().generic("bn_stats", [ptr(grows), ptr(gamma), ptr(beta), 0, 0, ptr(mean), ptr(rstd), 0, 0, ptr(ca),
+                                 ptr(cb), ptr(cc), ptr(dg), ptr(db), ptr(ws)], [R, Ch, 1], [count, eps, mom], stream())
+        torch.cuda.synchronize()
+        tol = dict(rtol=1e-4, atol=1e-3 * (t1.abs().max().item() + 1) / count + 1e-6)
+        assert torch.allclose(db.double(), t1, rtol=1e-5, atol=1e-3), rep
+        assert torch.allclose(dg.double(), sgx, rtol=1e-4, atol=1e-3), rep
+        assert torch.allclose(ca.double(), gm * r_, rtol=1e-5), rep
+        assert torch.allclose(cb.double(), -gm * r_ * r_ * sgx / count, **tol), rep
+        assert torch.allclose(cc.double(), -gm * r_ * t1 / count + gm * r_ * r_ * mu_ * sgx / count, **tol), rep
+        assert ws[-64:].abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("N,rps,Ch,G", [(4100, 2, 32, 8), (37, 3, 512, 32)])
+def test_gn_stats_backward_parameter_grads_many_samples(cuda_dev, N, rps, Ch, G):
+    """gn_stats mode 1: per-sample backward coefficients, and the dgamma / dbeta column sums
+    of the per-sample contributions through the single-launch slice reduction (N = 4100
+    samples: more than 32 slices, ragged last), launched twice on one workspace."""
+    g = torch.Generator(device="cuda").manual_seed(N)
+    dev = cuda_dev
+    P = 64
+    Cg = Ch // G
+    mean = torch.randn(N, G, device=dev, generator=g).repeat_interleave(Cg, 1).contiguous()
+    rstd = (torch.rand(N, G, device=dev, generator=g) + 0.5).repeat_interleave(Cg, 1).contiguous()
+    gamma = torch.rand(Ch, device=dev, generator=g) + 0.5
+    beta = torch.zeros(Ch, device=dev)
+    rows = torch.randn(N * rps, 2, Ch, device=dev, generator=g)
+    S = rows.double().reshape(N, rps, 2, Ch).sum(1)                  # [N, 2, Ch]
+    mu, r = mean.double(), rstd.double()
+    contrib1 = S[:, 0]
+    contrib2 = r * (S[:, 1] - mu * S[:, 0])
+    db_ref, dg_ref = contrib1.sum(0), contrib2.sum(0)
+    work = torch.zeros(N * 2 * Ch + C().row_slices(N) * 2 * Ch + C().row_slices(N) * 2 * Ch + 64, device=dev)
+    f = lambda: torch.zeros(N * Ch, device=dev)
+    ca, cb, cc = f(), f(), f()
+    dg, db = torch.zeros(Ch, device=dev), torch.zeros(Ch, device=dev)
+    for rep in range(2):
+        C().generic("gn_stats", [ptr(rows), ptr(gamma), ptr(beta), ptr(mean), ptr(rstd), 0, 0, ptr(ca), ptr(cb),
+                                 ptr(cc), ptr(dg), ptr(db), ptr(work)], [N, rps, Ch, G, P, 1], [1e-3], stream())
+        torch.cuda.synchronize()
+        assert torch.allclose(db.double(), db_ref, rtol=1e-4, atol=1e-2), rep
+        assert torch.allclose(dg.double(), dg_ref, rtol=1e-4, atol=1e-2), rep
+        assert torch.allclose(ca.double().view(N, Ch), gamma.double() * r, rtol=1e-5), rep

@@ -1,0 +1,102 @@
+"""Static validation of the native executor's plans across the config space (no GPU):
+every fusion the planner applies meets its declarative precondition (native_engine.FUSIONS),
+every planned launch resolves to a built kernel (dry dispatch), every buffer an op reads was
+written earlier in the same plan (or is a step input), and every parameter gradient is
+written -- for norm x decoder x dims x image size (runtime/plan_check.py)."""
+import copy
+import itertools
+
+import pytest
+
+from unet_distributed_amd.models.spec import UNetSpec
+from unet_distributed_amd.parallel.grad_sync import plan_buckets
+from unet_distributed_amd.runtime import native_engine as ne
+from unet_distributed_amd.runtime.params import FlatParams
+from unet_distributed_amd.runtime.plan_check import check_engine
+
+CONFIGS = [(norm, ups, 2, img) for norm, ups, img in itertools.product(("none", "batch", "group"), (False, True),
+                                                                      (32, 64, 128, 256))]
+CONFIGS += [(norm, ups, 3, img) for norm, ups, img in itertools.product(("none", "batch"), (False, True), (16, 32))]
+
+
+def _engine(norm, ups, dims, img, batch=2, opts=None, in_channels=None):
+    cin = in_channels or (1 if ups else 4)
+    spec = UNetSpec(in_channels=cin, use_upsampling=ups, norm=norm, dims=dims)
+    flat = FlatParams(spec)
+    dtype = "fp16" if norm == "group" else "bf16"
+    return ne.NativeUNet(spec, flat, batch, img, "cpu", bucket_bounds=plan_buckets(flat, 4.0), dry_run=True,
+                         dtype=dtype, opts=opts)
+
+
+@pytest.mark.parametrize("norm,ups,dims,img", CONFIGS)
+def test_every_plan_validates(norm, ups, dims, img):
+    e = _engine(norm, ups, dims, img)
+    errs = check_engine(e)
+    assert errs == {"train": [], "eval": []}, errs
+    for name, layers in e.fusions.items():
+        f = ne.FUSIONS[name]
+        assert not f.unmet(e), (name, f.unmet(e))
+        for l in layers:
+            for n in f.needs:
+                assert l in e.fusions.get(n, ()), (name, l, n)
+
+
+def test_headline_plan_applies_the_measured_fusions():
+    e = _engine("none", False, 2, 128)
+    assert sorted(e.fusions) == sorted(["head_onload", "head_fuse", "pool_epilogue", "tconv_fused", "tconv_wa",
+                                        "tconv_onload", "skip_route", "tail_halves"])
+    assert e.fusions["tconv_onload"] == ["transConv9"]
+
+
+def _broken(name, **change):
+    f = copy.copy(ne.FUSIONS[name])
+    for k, v in change.items():
+        setattr(f, k, v)
+    return f
+
+
+def test_validator_catches_a_broken_precondition(monkeypatch):
+    """Dropping the norm restriction of the batch-half split of the last data gradient plans
+    the first layer's weight gradient ahead of the norm backward that forms its operand
+    coefficients: the plan builds and every kernel exists, but the weight gradient would
+    read stale coefficients -- only the def-use check sees it."""
+    assert check_engine(_engine("batch", False, 2, 64)) == {"train": [], "eval": []}
+    monkeypatch.setitem(ne.FUSIONS, "tail_halves", _broken("tail_halves", norm=None))
+    e = _engine("batch", False, 2, 64)
+    errs = check_engine(e)["train"]
+    assert errs and all("before any op writes it" in x for x in errs), errs
+    assert any("wgrad:conv1a" in x and "ca:conv1a" in x for x in errs)
+
+
+def test_tconv_onload_needs_the_chained_weight_gradient(monkeypatch):
+    """A transposed conv formed on load leaves nothing to read its output: without the
+    chained u-row weight gradient (tconv_wa=0) the consumer's weight gradient would read
+    the never-formed u.  The declared `needs` keeps the planner from doing that; with it
+    removed, planning fails loudly rather than planning a read of a dropped buffer."""
+    e = _engine("none", False, 2, 64, opts=dict(tconv_wa=0))
+    assert "tconv_onload" not in e.fusions and check_engine(e)["train"] == []
+    monkeypatch.setitem(ne.FUSIONS, "tconv_onload", _broken("tconv_onload", needs=()))
+    try:
+        e = _engine("none", False, 2, 64, opts=dict(tconv_wa=0))
+    except ValueError as ex:
+        assert "a1" in str(ex)
+    else:
+        assert check_engine(e)["train"], "a read of the never-formed u went unnoticed"
+
+
+def test_dry_dispatch_reports_a_missing_kernel():
+    """A conv the host-side check accepts but no launcher instantiation takes is reported by
+    Plan.check_dispatch (the dispatch runs on the CPU, nothing is launched)."""
+    from unet_distributed_amd import native
+    C = native.require()
+    p = C.Plan(0)
+    # dgrad-norm epilogue on a dual-source (concat) row window: accepted by
+    # conv_fwd_prepare's shape checks, never instantiated (conv_win.h WIN_EPI)
+    base = dict(N=1, OH=64, OW=64, IH=64, IW=64, KH=3, KW=3, pad=1, C1=32, C2=32, src1=1, src2=1, wgt=1,
+                dst1=1, Cout=32, nz=1, na=1, nc=1, stats=1, npix=64 * 64, name="bad")
+    try:
+        p.add_conv_fwd(base)
+    except ValueError:
+        pytest.skip("host check rejects this combination up front")
+    bad = p.check_dispatch(0, p.size())
+    assert [b[1] for b in bad] == ["bad"]

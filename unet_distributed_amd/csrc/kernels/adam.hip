@@ -197,9 +197,9 @@ hipError_t adam_pack_launch(float* w, const float* g, float* m, float* v, int n_
   int grid = (n_total / 1024 + 255) / 256 * 256;
   if (grid > 4096) grid = 4096;
   if (grid < 256) grid = 256;
-  hipLaunchKernelGGL(adam_pack_kernel, dim3(grid), dim3(256), 0, s, w, g, m, v, n_total, (const PackSeg*)segs, nseg,
+  UNET_LAUNCH(adam_pack_kernel, dim3(grid), dim3(256), 0, s, w, g, m, v, n_total, (const PackSeg*)segs, nseg,
                      lr_t, b1, b2, eps, gscale, do_adam, dev_scalars, (h16*)arena);
-  return hipGetLastError();
+  return launch_status();
 }
 
 }  // namespace unet

@@ -7,6 +7,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "conv_params.h"
+
+// Kernel launch of every launcher (skipped under dry dispatch, conv_params.h)
+#define UNET_LAUNCH(...)                                        \
+  do {                                                          \
+    if (!::unet_types::dry_dispatch()) hipLaunchKernelGGL(__VA_ARGS__); \
+  } while (0)
+
 // 16-bit activation / weight-copy element type.  Every kernel TU is compiled twice
 // (native/build.py): as bf16 in namespace `unet` and, with -DUNET_FP16
 // -Dunet=unet_f16, as IEEE fp16 in namespace `unet_f16`.  The two builds share the
@@ -37,6 +45,9 @@ constexpr uint32_t kOnes2 = 0x3F803F80u;   // two bf16 1.0
 #endif
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+// status of the launches a launcher just issued (success under dry dispatch)
+inline hipError_t launch_status() { return ::unet_types::dry_dispatch() ? hipSuccess : hipGetLastError(); }
 
 __device__ __forceinline__ float h2f(h16 x) { return (float)x; }
 __device__ __forceinline__ h16 f2h(float x) { return (h16)x; }

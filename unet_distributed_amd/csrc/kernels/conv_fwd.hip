@@ -258,28 +258,28 @@ hipError_t launch_cfg(const ConvFwdParams& p, hipStream_t s) {
   if (epi == EPI_STATS || epi == EPI_DGRAD_NORM) {
     // fused-normalisation epilogues: plain (MODE 0) or first-layer (MODE 2) sources
     if (epi == EPI_DGRAD_NORM && !smallc && p.C2 == 0)
-      hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, false, EPI_DGRAD_NORM>), dim3(grid), dim3(NTHR),
+      UNET_LAUNCH((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, false, EPI_DGRAD_NORM>), dim3(grid), dim3(NTHR),
                          0, s, p);
     else if (epi == EPI_STATS && smallc)
-      hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 2, false, EPI_STATS>), dim3(grid), dim3(NTHR), 0,
+      UNET_LAUNCH((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 2, false, EPI_STATS>), dim3(grid), dim3(NTHR), 0,
                          s, p);
     else if (epi == EPI_STATS && p.C2 > 0)
-      hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, true, EPI_STATS>), dim3(grid), dim3(NTHR), 0, s,
+      UNET_LAUNCH((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, true, EPI_STATS>), dim3(grid), dim3(NTHR), 0, s,
                          p);
     else if (epi == EPI_STATS)
-      hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, false, EPI_STATS>), dim3(grid), dim3(NTHR), 0,
+      UNET_LAUNCH((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, false, EPI_STATS>), dim3(grid), dim3(NTHR), 0,
                          s, p);
     else
       return hipErrorInvalidValue;
-    return hipGetLastError();
+    return launch_status();
   }
   if (smallc)
-    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 2, false>), dim3(grid), dim3(NTHR), 0, s, p);
+    UNET_LAUNCH((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 2, false>), dim3(grid), dim3(NTHR), 0, s, p);
   else if (p.C2 > 0)
-    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, true>), dim3(grid), dim3(NTHR), 0, s, p);
+    UNET_LAUNCH((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, true>), dim3(grid), dim3(NTHR), 0, s, p);
   else
-    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, false>), dim3(grid), dim3(NTHR), 0, s, p);
-  return hipGetLastError();
+    UNET_LAUNCH((conv_fwd_kernel<BM, BN, WAVES_M, WAVES_N, 0, false>), dim3(grid), dim3(NTHR), 0, s, p);
+  return launch_status();
 }
 
 
@@ -403,16 +403,16 @@ __global__ void __launch_bounds__(NTHR) conv_img8_kernel(const ConvFwdParams p) 
 hipError_t launch_img8(const ConvFwdParams& p, hipStream_t s) {
   const int grid = ((p.N + IMG8 - 1) / IMG8) * (p.Cout / 64);
   switch (conv_epi_mode(p)) {
-    case EPI_FWD: hipLaunchKernelGGL((conv_img8_kernel<EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p); break;
-    case EPI_DGRAD: hipLaunchKernelGGL((conv_img8_kernel<EPI_DGRAD>), dim3(grid), dim3(NTHR), 0, s, p); break;
-    case EPI_GENERIC: hipLaunchKernelGGL((conv_img8_kernel<EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p); break;
-    case EPI_STATS: hipLaunchKernelGGL((conv_img8_kernel<EPI_STATS>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case EPI_FWD: UNET_LAUNCH((conv_img8_kernel<EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case EPI_DGRAD: UNET_LAUNCH((conv_img8_kernel<EPI_DGRAD>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case EPI_GENERIC: UNET_LAUNCH((conv_img8_kernel<EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case EPI_STATS: UNET_LAUNCH((conv_img8_kernel<EPI_STATS>), dim3(grid), dim3(NTHR), 0, s, p); break;
     case EPI_DGRAD_NORM:
-      hipLaunchKernelGGL((conv_img8_kernel<EPI_DGRAD_NORM>), dim3(grid), dim3(NTHR), 0, s, p);
+      UNET_LAUNCH((conv_img8_kernel<EPI_DGRAD_NORM>), dim3(grid), dim3(NTHR), 0, s, p);
       break;
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 // ---------------------------------------------------------------------------------
@@ -573,11 +573,11 @@ hipError_t launch_win_first(const ConvFwdParams& p, hipStream_t s) {
 #define WF_CASE(WW)                                                                                        \
   case WW:                                                                                                 \
     if (fwd)                                                                                               \
-      hipLaunchKernelGGL((conv_win_first_kernel<WW, CIN, EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p);     \
+      UNET_LAUNCH((conv_win_first_kernel<WW, CIN, EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p);     \
     else if (epi == EPI_STATS)                                                                             \
-      hipLaunchKernelGGL((conv_win_first_kernel<WW, CIN, EPI_STATS>), dim3(grid), dim3(NTHR), 0, s, p);   \
+      UNET_LAUNCH((conv_win_first_kernel<WW, CIN, EPI_STATS>), dim3(grid), dim3(NTHR), 0, s, p);   \
     else                                                                                                   \
-      hipLaunchKernelGGL((conv_win_first_kernel<WW, CIN, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p); \
+      UNET_LAUNCH((conv_win_first_kernel<WW, CIN, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p); \
     break;
   switch (W) {
     WF_CASE(16)
@@ -588,7 +588,7 @@ hipError_t launch_win_first(const ConvFwdParams& p, hipStream_t s) {
       return hipErrorInvalidValue;
   }
 #undef WF_CASE
-  return hipGetLastError();
+  return launch_status();
 }
 
 
@@ -805,13 +805,13 @@ hipError_t launch_tconv_fwd(const ConvFwdParams& p, hipStream_t s) {
   const int R = 128 / W;
   const int grid = ((p.N * p.OH + R - 1) / R) * ((p.Cout >> 2) / 32);
   switch (W) {
-    case 8: hipLaunchKernelGGL((tconv_fwd_kernel<8, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
-    case 16: hipLaunchKernelGGL((tconv_fwd_kernel<16, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
-    case 32: hipLaunchKernelGGL((tconv_fwd_kernel<32, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
-    case 64: hipLaunchKernelGGL((tconv_fwd_kernel<64, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 8: UNET_LAUNCH((tconv_fwd_kernel<8, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 16: UNET_LAUNCH((tconv_fwd_kernel<16, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 32: UNET_LAUNCH((tconv_fwd_kernel<32, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 64: UNET_LAUNCH((tconv_fwd_kernel<64, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 // data gradient: 64 input channels per workgroup (one dy image feeds 4 MFMA columns)
@@ -824,11 +824,11 @@ hipError_t launch_tconv_dgrad(const ConvFwdParams& p, hipStream_t s) {
 #define TD_CASE(WW)                                                                                          \
   case WW:                                                                                                   \
     if (dg)                                                                                                  \
-      hipLaunchKernelGGL((tconv_dgrad_kernel<WW, 64, EPI_DGRAD>), dim3(grid), dim3(NTHR), 0, s, p);       \
+      UNET_LAUNCH((tconv_dgrad_kernel<WW, 64, EPI_DGRAD>), dim3(grid), dim3(NTHR), 0, s, p);       \
     else if (epi == EPI_DGRAD_NORM)                                                                          \
-      hipLaunchKernelGGL((tconv_dgrad_kernel<WW, 64, EPI_DGRAD_NORM>), dim3(grid), dim3(NTHR), 0, s, p);  \
+      UNET_LAUNCH((tconv_dgrad_kernel<WW, 64, EPI_DGRAD_NORM>), dim3(grid), dim3(NTHR), 0, s, p);  \
     else                                                                                                     \
-      hipLaunchKernelGGL((tconv_dgrad_kernel<WW, 64, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p);     \
+      UNET_LAUNCH((tconv_dgrad_kernel<WW, 64, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p);     \
     break;
   switch (W) {
     TD_CASE(8)
@@ -839,7 +839,7 @@ hipError_t launch_tconv_dgrad(const ConvFwdParams& p, hipStream_t s) {
       return hipErrorInvalidValue;
   }
 #undef TD_CASE
-  return hipGetLastError();
+  return launch_status();
 }
 
 }  // namespace

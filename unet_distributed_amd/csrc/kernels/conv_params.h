@@ -7,6 +7,13 @@
 // builds' launchers take the same host types.
 namespace unet_types {
 
+// Dry dispatch (host): while set, the kernel launchers resolve their dispatch -- template
+// instantiation, tile, epilogue -- and return the status they would return, without
+// launching (UNET_LAUNCH / launch_status in common.h).  The executor's plan validation
+// uses it on a CPU host to prove every planned launch has a built kernel
+// (runtime/plan_check.py).  Defined in runtime/bindings.cpp.
+bool dry_dispatch();
+
 // Gradient of the segmentation head's input formed on load (head-on-load): the consumer
 // kernel builds dY[p][c] = dlogit(p) * w[c] * (x[p][c] > 0) itself from the per-pixel
 // probability / target, the loss sums and the head input's ReLU bits, so the head

@@ -474,16 +474,16 @@ hipError_t launch_wg(WgradParams p, hipStream_t s) {
   p.lqd = lg(p.QD);
   if (p.bias_mode) {
     if (p2)
-      hipLaunchKernelGGL((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, true, true>), dim3(grid), dim3(NTHR), 0, s, p);
+      UNET_LAUNCH((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, true, true>), dim3(grid), dim3(NTHR), 0, s, p);
     else
-      hipLaunchKernelGGL((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, true, false>), dim3(grid), dim3(NTHR), 0, s, p);
+      UNET_LAUNCH((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, true, false>), dim3(grid), dim3(NTHR), 0, s, p);
   } else {
     if (p2)
-      hipLaunchKernelGGL((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, false, true>), dim3(grid), dim3(NTHR), 0, s, p);
+      UNET_LAUNCH((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, false, true>), dim3(grid), dim3(NTHR), 0, s, p);
     else
-      hipLaunchKernelGGL((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, false, false>), dim3(grid), dim3(NTHR), 0, s, p);
+      UNET_LAUNCH((wgrad_kernel<BM, BN, NTAP, WAVES_M, WAVES_N, SMALLC, false, false>), dim3(grid), dim3(NTHR), 0, s, p);
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 
@@ -1100,20 +1100,20 @@ hipError_t launch_wgrad_win_first(const WgradParams& p, hipStream_t s) {
   const int grid = (p.Nc / 32) * launch_splits(p);
   if (p.xform == 2) {         // dz formed on load (norm backward of the first layer)
     switch (p.QW) {
-      case 16: hipLaunchKernelGGL((wgrad_win_first_kernel<16, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
-      case 32: hipLaunchKernelGGL((wgrad_win_first_kernel<32, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
-      case 64: hipLaunchKernelGGL((wgrad_win_first_kernel<64, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
-      default: hipLaunchKernelGGL((wgrad_win_first_kernel<128, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      case 16: UNET_LAUNCH((wgrad_win_first_kernel<16, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      case 32: UNET_LAUNCH((wgrad_win_first_kernel<32, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      case 64: UNET_LAUNCH((wgrad_win_first_kernel<64, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      default: UNET_LAUNCH((wgrad_win_first_kernel<128, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
     }
-    return hipGetLastError();
+    return launch_status();
   }
   switch (p.QW) {
-    case 16: hipLaunchKernelGGL((wgrad_win_first_kernel<16, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
-    case 32: hipLaunchKernelGGL((wgrad_win_first_kernel<32, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
-    case 64: hipLaunchKernelGGL((wgrad_win_first_kernel<64, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
-    default: hipLaunchKernelGGL((wgrad_win_first_kernel<128, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 16: UNET_LAUNCH((wgrad_win_first_kernel<16, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 32: UNET_LAUNCH((wgrad_win_first_kernel<32, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 64: UNET_LAUNCH((wgrad_win_first_kernel<64, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    default: UNET_LAUNCH((wgrad_win_first_kernel<128, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 
@@ -1447,16 +1447,16 @@ hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
   const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.KD * launch_splits(p);
   if constexpr (GEO == WGEO_2D && QO == 1) {
     if (p.hg.prob) {
-      hipLaunchKernelGGL((wgrad_win_kernel<W, QO, false, GEO, true>), dim3(grid), dim3(NTHR), 0, s, p);
-      return hipGetLastError();
+      UNET_LAUNCH((wgrad_win_kernel<W, QO, false, GEO, true>), dim3(grid), dim3(NTHR), 0, s, p);
+      return launch_status();
     }
   }
   if (p.hg.prob) return hipErrorInvalidValue;
   if (p.M2 > 0)
-    hipLaunchKernelGGL((wgrad_win_kernel<W, QO, true, GEO>), dim3(grid), dim3(NTHR), 0, s, p);
+    UNET_LAUNCH((wgrad_win_kernel<W, QO, true, GEO>), dim3(grid), dim3(NTHR), 0, s, p);
   else
-    hipLaunchKernelGGL((wgrad_win_kernel<W, QO, false, GEO>), dim3(grid), dim3(NTHR), 0, s, p);
-  return hipGetLastError();
+    UNET_LAUNCH((wgrad_win_kernel<W, QO, false, GEO>), dim3(grid), dim3(NTHR), 0, s, p);
+  return launch_status();
 }
 
 template <int W, int QO>
@@ -1587,19 +1587,19 @@ hipError_t wgrad_launch(const WgradParams& p0, hipStream_t s) {
   if (wgrad_tconv_win_eligible(p)) {
     const int qn = p.Nc % 128 == 0 ? 4 : (p.Nc % 64 == 0 ? 2 : 1);
     const int grid = (p.M1 / 32) * (p.Nc / (32 * qn)) * launch_splits(p);
-#define TW_CASE(WW, QQ) hipLaunchKernelGGL((wgrad_tconv_win_kernel<WW, QQ>), dim3(grid), dim3(NTHR), 0, s, p)
+#define TW_CASE(WW, QQ) UNET_LAUNCH((wgrad_tconv_win_kernel<WW, QQ>), dim3(grid), dim3(NTHR), 0, s, p)
     if (p.QW == 32) {
       if (qn == 4) TW_CASE(32, 4); else if (qn == 2) TW_CASE(32, 2); else TW_CASE(32, 1);
     } else {
       if (qn == 4) TW_CASE(64, 4); else if (qn == 2) TW_CASE(64, 2); else TW_CASE(64, 1);
     }
 #undef TW_CASE
-    return hipGetLastError();
+    return launch_status();
   }
   if (wgrad_s2d_win_eligible(p)) {
     const int qn = p.Nc % 64 == 0 ? 2 : 1;
     const int grid = (p.M1 / 32) * (p.Nc / (32 * qn)) * launch_splits(p);
-#define SW_CASE(WW, QQ) hipLaunchKernelGGL((wgrad_s2d_win_kernel<WW, QQ>), dim3(grid), dim3(NTHR), 0, s, p)
+#define SW_CASE(WW, QQ) UNET_LAUNCH((wgrad_s2d_win_kernel<WW, QQ>), dim3(grid), dim3(NTHR), 0, s, p)
     if (p.QW == 16) {
       if (qn == 2) SW_CASE(16, 2); else SW_CASE(16, 1);
     } else if (p.QW == 32) {
@@ -1608,7 +1608,7 @@ hipError_t wgrad_launch(const WgradParams& p0, hipStream_t s) {
       if (qn == 2) SW_CASE(64, 2); else SW_CASE(64, 1);
     }
 #undef SW_CASE
-    return hipGetLastError();
+    return launch_status();
   }
   if (wgrad_win_eligible(p)) {
     const bool q2 = c.BN == 64;
@@ -1643,34 +1643,34 @@ hipError_t wgrad_reduce_launch(const float* slab, int splits, int taps, int Mtot
   const size_t n4 = (size_t)taps * Mtot * Nc / 4;
   const dim3 g1((unsigned)((n4 + 255) / 256), (unsigned)groups);
   if (groups == 1 && identity) {
-    hipLaunchKernelGGL(slab_partial_kernel, g1, dim3(256), 0, s, slab, splits, n4, out, scale);
-    return hipGetLastError();
+    UNET_LAUNCH(slab_partial_kernel, g1, dim3(256), 0, s, slab, splits, n4, out, scale);
+    return launch_status();
   }
   if (!stage) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(slab_partial_kernel, g1, dim3(256), 0, s, slab, splits, n4, stage, scale);
+  UNET_LAUNCH(slab_partial_kernel, g1, dim3(256), 0, s, slab, splits, n4, stage, scale);
   const size_t n4o = (size_t)taps * Mout * Nc / 4;
-  hipLaunchKernelGGL(slab_final_kernel, dim3((unsigned)((n4o + 255) / 256)), dim3(256), 0, s, stage, groups, taps,
+  UNET_LAUNCH(slab_final_kernel, dim3((unsigned)((n4o + 255) / 256)), dim3(256), 0, s, stage, groups, taps,
                      Mtot, Mout, Nc, rg, rkeep, out);
-  return hipGetLastError();
+  return launch_status();
 }
 
 int reduce_groups(int splits) { return (splits + RED_G - 1) / RED_G; }
 
 hipError_t multi_reduce_launch(const void* jobs, int njobs, long long total1, long long total2, hipStream_t s) {
   if (total1 > 0)
-    hipLaunchKernelGGL(multi_reduce1_kernel, dim3((unsigned)((total1 + 255) / 256)), dim3(256), 0, s,
+    UNET_LAUNCH(multi_reduce1_kernel, dim3((unsigned)((total1 + 255) / 256)), dim3(256), 0, s,
                        (const ReduceJob*)jobs, njobs, total1);
   if (total2 > 0)
-    hipLaunchKernelGGL(multi_reduce2_kernel, dim3((unsigned)((total2 + 255) / 256)), dim3(256), 0, s,
+    UNET_LAUNCH(multi_reduce2_kernel, dim3((unsigned)((total2 + 255) / 256)), dim3(256), 0, s,
                        (const ReduceJob*)jobs, njobs, total2);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t colsum_launch(const void* x, int rows, int C, int blocks, float* partial, hipStream_t s) {
   const int rpb = (rows + blocks - 1) / blocks;
-  hipLaunchKernelGGL(colsum_kernel, dim3(blocks), dim3(256), 256 * 8 * sizeof(float), s, (const h16*)x, rows, C,
+  UNET_LAUNCH(colsum_kernel, dim3(blocks), dim3(256), 256 * 8 * sizeof(float), s, (const h16*)x, rows, C,
                      rpb, partial);
-  return hipGetLastError();
+  return launch_status();
 }
 
 }  // namespace unet

@@ -554,17 +554,17 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
   const int geo = p.KD == 3 ? GEO_3D : (p.OW > W ? GEO_SEG : GEO_2D);
 #define WIN_EPI(WW, CC, GG)                                                                               \
   if (epi == EPI_FWD)                                                                                     \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_FWD, GG>), dim3(grid), dim3(NTHR), 0, s, p);     \
+    UNET_LAUNCH((conv_win_kernel<WW, BN, BM, CC, EPI_FWD, GG>), dim3(grid), dim3(NTHR), 0, s, p);     \
   else if (epi == EPI_DGRAD)                                                                              \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_DGRAD, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
+    UNET_LAUNCH((conv_win_kernel<WW, BN, BM, CC, EPI_DGRAD, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
   else if (epi == EPI_STATS)                                                                              \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_STATS, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
+    UNET_LAUNCH((conv_win_kernel<WW, BN, BM, CC, EPI_STATS, GG>), dim3(grid), dim3(NTHR), 0, s, p);   \
   else if (epi == EPI_DGRAD_NORM && !CC)                                                                  \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD_NORM, GG>), dim3(grid), dim3(NTHR), 0, s, p); \
+    UNET_LAUNCH((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD_NORM, GG>), dim3(grid), dim3(NTHR), 0, s, p); \
   else if (epi == EPI_DGRAD_NORM)                                                                         \
     return hipErrorInvalidValue;                                                                          \
   else                                                                                                    \
-    hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, CC, EPI_GENERIC, GG>), dim3(grid), dim3(NTHR), 0, s, p);
+    UNET_LAUNCH((conv_win_kernel<WW, BN, BM, CC, EPI_GENERIC, GG>), dim3(grid), dim3(NTHR), 0, s, p);
 #define WIN_GEO(WW, CC)                                                                                   \
   if (geo == GEO_3D) {                                                                                    \
     WIN_EPI(WW, CC, GEO_3D)                                                                               \
@@ -587,9 +587,9 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
   case WW:                                                                                                    \
     if constexpr (win_tile_built<BN, BM>(WW)) {                                                               \
       if (epi == EPI_STATS)                                                                                   \
-        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_STATS, GEO_2D, 1>), dim3(grid), dim3(NTHR), 0, s, p); \
+        UNET_LAUNCH((conv_win_kernel<WW, BN, BM, false, EPI_STATS, GEO_2D, 1>), dim3(grid), dim3(NTHR), 0, s, p); \
       else if (epi == EPI_GENERIC)                                                                            \
-        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_GENERIC, GEO_2D, 1>), dim3(grid), dim3(NTHR), 0, s, p); \
+        UNET_LAUNCH((conv_win_kernel<WW, BN, BM, false, EPI_GENERIC, GEO_2D, 1>), dim3(grid), dim3(NTHR), 0, s, p); \
       else                                                                                                    \
         return hipErrorInvalidValue;                                                                          \
     } else {                                                                                                  \
@@ -602,7 +602,7 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
 #define HG_CASE(WW)                                                                                       \
   case WW:                                                                                                \
     if constexpr (win_tile_built<BN, BM>(WW))                                                             \
-      hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_2D, 3>), dim3(grid), dim3(NTHR), 0, s, p); \
+      UNET_LAUNCH((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_2D, 3>), dim3(grid), dim3(NTHR), 0, s, p); \
     else                                                                                                  \
       return hipErrorInvalidValue;                                                                        \
     break;
@@ -614,7 +614,7 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
       default:
         return hipErrorInvalidValue;
     }
-    return hipGetLastError();
+    return launch_status();
   }
   if (p.s2d) {                          // space-to-depth dgrad source (conv_fwd_prepare checks the shape)
     if ((epi != EPI_DGRAD && epi != EPI_DGRAD_NORM) || geo != GEO_2D) return hipErrorInvalidValue;
@@ -623,9 +623,9 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
   case WW:                                                                                                \
     if constexpr (win_tile_built<BN, BM>(WW)) {                                                           \
       if (epi == EPI_DGRAD)                                                                               \
-        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_2D, 4>), dim3(grid), dim3(NTHR), 0, s, p); \
+        UNET_LAUNCH((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_2D, 4>), dim3(grid), dim3(NTHR), 0, s, p); \
       else                                                                                                \
-        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD_NORM, GEO_2D, 4>), dim3(grid), dim3(NTHR), 0, s, \
+        UNET_LAUNCH((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD_NORM, GEO_2D, 4>), dim3(grid), dim3(NTHR), 0, s, \
                            p);                                                                            \
     } else {                                                                                              \
       return hipErrorInvalidValue;                                                                        \
@@ -639,7 +639,7 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
       default:
         return hipErrorInvalidValue;
     }
-    return hipGetLastError();
+    return launch_status();
   }
   if (p.ut.x) {                         // transposed-conv source on load (conv_fwd_prepare checks the shape)
     if (!cc || geo != GEO_2D) return hipErrorInvalidValue;
@@ -648,11 +648,11 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
   case WW:                                                                                                \
     if constexpr (WW >= 32 && win_tile_built<BN, BM>(WW) && (BM / WW) % 2 == 0) {                          \
       if (epi == EPI_FWD)                                                                                 \
-        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, true, EPI_FWD, GEO_2D, 5>), dim3(grid), dim3(NTHR), 0, s, p); \
+        UNET_LAUNCH((conv_win_kernel<WW, BN, BM, true, EPI_FWD, GEO_2D, 5>), dim3(grid), dim3(NTHR), 0, s, p); \
       else if (epi == EPI_STATS)                                                                          \
-        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, true, EPI_STATS, GEO_2D, 5>), dim3(grid), dim3(NTHR), 0, s, p); \
+        UNET_LAUNCH((conv_win_kernel<WW, BN, BM, true, EPI_STATS, GEO_2D, 5>), dim3(grid), dim3(NTHR), 0, s, p); \
       else if (epi == EPI_GENERIC)                                                                        \
-        hipLaunchKernelGGL((conv_win_kernel<WW, BN, BM, true, EPI_GENERIC, GEO_2D, 5>), dim3(grid), dim3(NTHR), 0, s, p); \
+        UNET_LAUNCH((conv_win_kernel<WW, BN, BM, true, EPI_GENERIC, GEO_2D, 5>), dim3(grid), dim3(NTHR), 0, s, p); \
       else                                                                                                \
         return hipErrorInvalidValue;                                                                      \
     } else {                                                                                              \
@@ -666,7 +666,7 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
       default:
         return hipErrorInvalidValue;
     }
-    return hipGetLastError();
+    return launch_status();
   }
   if (p.xform) {                        // operand transform: 2D single source (conv_fwd_prepare)
     switch (W) {
@@ -677,7 +677,7 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
       default:
         return hipErrorInvalidValue;
     }
-    return hipGetLastError();
+    return launch_status();
   }
 #undef XF_CASE
   if (geo == GEO_SEG) {                 // 3D volumes wider than 128 are not window-eligible
@@ -687,7 +687,7 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
     } else {
       WIN_EPI(128, false, GEO_SEG)
     }
-    return hipGetLastError();
+    return launch_status();
   }
   switch (W) {
     WIN_CASE(16)
@@ -700,7 +700,7 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
 #undef WIN_CASE
 #undef WIN_GEO
 #undef WIN_EPI
-  return hipGetLastError();
+  return launch_status();
 }
 #endif  // UNET_WIN_IMPL
 

@@ -461,70 +461,70 @@ inline int grid_for(long long work, int per_block = 256) {
 }  // namespace
 
 hipError_t cast_input_launch(const float* x, int P, int Cin, int Cpad, void* y, hipStream_t s) {
-  hipLaunchKernelGGL(cast_input_kernel, dim3(grid_for((long long)P * Cpad)), dim3(256), 0, s, x, P, Cin, Cpad,
+  UNET_LAUNCH(cast_input_kernel, dim3(grid_for((long long)P * Cpad)), dim3(256), 0, s, x, P, Cin, Cpad,
                      (h16*)y);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t gather_batch_launch(const float* x_all, const float* y_all, const long long* idx, int B, int P, int Cin,
                                int Cpad, void* xb, void* tb, hipStream_t s) {
-  hipLaunchKernelGGL(gather_batch_kernel, dim3(grid_for((long long)B * P)), dim3(256), 0, s, x_all, y_all, idx, B, P,
+  UNET_LAUNCH(gather_batch_kernel, dim3(grid_for((long long)B * P)), dim3(256), 0, s, x_all, y_all, idx, B, P,
                      Cin, Cpad, (h16*)xb, (h16*)tb);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t maxpool2_fwd_launch(const void* x, int N, int D, int H, int W, int C, int dims3, void* y, void* code,
                                hipStream_t s) {
   const long long work = (long long)N * (dims3 ? D / 2 : 1) * (H / 2) * (W / 2) * (C / 8);
-  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, N, D, H, W, C,
+  UNET_LAUNCH(maxpool2_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, N, D, H, W, C,
                      dims3, (h16*)y, (uint32_t*)code);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t norm_pool_launch(const void* z, const float* fa, const float* fc, int cstride, int N, int D, int H, int W,
                             int C, int dims3, void* y, void* py, void* code, hipStream_t s) {
   const long long work = (long long)N * (dims3 ? D / 2 : 1) * (H / 2) * (W / 2) * (C / 8);
   if (dims3)
-    hipLaunchKernelGGL(norm_pool_kernel<true>, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)z, fa, fc, cstride,
+    UNET_LAUNCH(norm_pool_kernel<true>, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)z, fa, fc, cstride,
                        N, D, H, W, C, (h16*)y, (h16*)py, (uint32_t*)code);
   else
-    hipLaunchKernelGGL(norm_pool_kernel<false>, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)z, fa, fc,
+    UNET_LAUNCH(norm_pool_kernel<false>, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)z, fa, fc,
                        cstride, N, D, H, W, C, (h16*)y, (h16*)py, (uint32_t*)code);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t maxpool2_bwd_launch(const void* x, const void* code, const void* dy, const void* skip, int N, int D, int H,
                                int W, int C, int dims3, void* dx, hipStream_t s) {
   const long long work = (long long)N * (dims3 ? D / 2 : 1) * (H / 2) * (W / 2) * (C / 8);
   if (code)
-    hipLaunchKernelGGL(maxpool2_bwd_code_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const uint32_t*)code,
+    UNET_LAUNCH(maxpool2_bwd_code_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const uint32_t*)code,
                        (const h16*)dy, (const h16*)skip, N, D, H, W, C, dims3, (h16*)dx);
   else
-    hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, (const h16*)dy,
+    UNET_LAUNCH(maxpool2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, (const h16*)dy,
                        (const h16*)skip, N, D, H, W, C, dims3, (h16*)dx);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t maxpool2_bwd_norm_launch(const void* code, const void* dy, const void* skip, const void* z, int N, int D,
                                     int H, int W, int C, int dims3, int nbp, void* dx, float* rows, hipStream_t s) {
-  hipLaunchKernelGGL(maxpool2_bwd_norm_kernel, dim3(nbp, N), dim3(256), 0, s, (const uint32_t*)code, (const h16*)dy,
+  UNET_LAUNCH(maxpool2_bwd_norm_kernel, dim3(nbp, N), dim3(256), 0, s, (const uint32_t*)code, (const h16*)dy,
                      (const h16*)skip, (const h16*)z, D, H, W, C, dims3, (h16*)dx, rows);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t upsample2_fwd_launch(const void* x, int N, int D, int H, int W, int C, int dims3, void* y, hipStream_t s) {
   const long long work = (long long)N * D * H * W * (C / 8);
-  hipLaunchKernelGGL(upsample2_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, N, D, H, W, C, dims3,
+  UNET_LAUNCH(upsample2_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)x, N, D, H, W, C, dims3,
                      (h16*)y);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t upsample2_bwd_launch(const void* dup, const void* mask, int N, int D, int H, int W, int C, int dims3,
                                 void* dlow, hipStream_t s) {
   const long long work = (long long)N * D * H * W * (C / 8);
-  hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)dup,
+  UNET_LAUNCH(upsample2_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, s, (const h16*)dup,
                      (const h16*)mask, N, D, H, W, C, dims3, (h16*)dlow);
-  return hipGetLastError();
+  return launch_status();
 }
 
 }  // namespace unet

@@ -237,19 +237,19 @@ hipError_t head_fwd_launch(const void* x, const float* w, const float* b, const 
   const int nb = head_blocks(P);
   switch (C) {
     case 16:
-      hipLaunchKernelGGL(head_fwd_kernel<16>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, b, (const h16*)t, P,
+      UNET_LAUNCH(head_fwd_kernel<16>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, b, (const h16*)t, P,
                          prob, partial);
       break;
     case 32:
-      hipLaunchKernelGGL(head_fwd_kernel<32>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, b, (const h16*)t, P,
+      UNET_LAUNCH(head_fwd_kernel<32>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, b, (const h16*)t, P,
                          prob, partial);
       break;
     default:
-      hipLaunchKernelGGL(head_fwd_kernel<64>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, b, (const h16*)t, P,
+      UNET_LAUNCH(head_fwd_kernel<64>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, b, (const h16*)t, P,
                          prob, partial);
   }
-  hipLaunchKernelGGL(partial_reduce_kernel, dim3(4), dim3(256), 0, s, partial, nb, 4, sums);
-  return hipGetLastError();
+  UNET_LAUNCH(partial_reduce_kernel, dim3(4), dim3(256), 0, s, partial, nb, 4, sums);
+  return launch_status();
 }
 
 hipError_t head_bwd_launch(const void* x, const float* w, const float* prob, const void* t, const float* sums, int P,
@@ -258,24 +258,24 @@ hipError_t head_bwd_launch(const void* x, const float* w, const float* prob, con
   const int nb = head_blocks(P);
   switch (C) {
     case 16:
-      hipLaunchKernelGGL(head_bwd_kernel<16>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, prob, (const h16*)t,
+      UNET_LAUNCH(head_bwd_kernel<16>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, prob, (const h16*)t,
                          sums, P, inv_total, bce_w, gscale, gscale_ptr, (h16*)dx, partial);
       break;
     case 32:
-      hipLaunchKernelGGL(head_bwd_kernel<32>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, prob, (const h16*)t,
+      UNET_LAUNCH(head_bwd_kernel<32>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, prob, (const h16*)t,
                          sums, P, inv_total, bce_w, gscale, gscale_ptr, (h16*)dx, partial);
       break;
     default:
-      hipLaunchKernelGGL(head_bwd_kernel<64>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, prob, (const h16*)t,
+      UNET_LAUNCH(head_bwd_kernel<64>, dim3(nb), dim3(HT), 0, s, (const h16*)x, w, prob, (const h16*)t,
                          sums, P, inv_total, bce_w, gscale, gscale_ptr, (h16*)dx, partial);
   }
-  hipLaunchKernelGGL(head_grad_reduce_kernel, dim3(C + 1), dim3(256), 0, s, partial, nb, C, gw, gb);
-  return hipGetLastError();
+  UNET_LAUNCH(head_grad_reduce_kernel, dim3(C + 1), dim3(256), 0, s, partial, nb, C, gw, gb);
+  return launch_status();
 }
 
 hipError_t partial_reduce_launch(const float* partial, int nb, int width, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(partial_reduce_kernel, dim3(width), dim3(256), 0, s, partial, nb, width, out);
-  return hipGetLastError();
+  UNET_LAUNCH(partial_reduce_kernel, dim3(width), dim3(256), 0, s, partial, nb, width, out);
+  return launch_status();
 }
 
 // Normalised head input in one pass (norm mode): y = relu(fa z + fc) of the head's
@@ -319,18 +319,18 @@ hipError_t norm_head_launch(const void* z, const float* fa, const float* fc, int
   const int nb = head_blocks(P * (C / 8) / 4 + 1);
   switch (C) {
     case 16:
-      hipLaunchKernelGGL(norm_head_kernel<16>, dim3(nb), dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
+      UNET_LAUNCH(norm_head_kernel<16>, dim3(nb), dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
                          P, (h16*)y, logit);
       break;
     case 32:
-      hipLaunchKernelGGL(norm_head_kernel<32>, dim3(nb), dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
+      UNET_LAUNCH(norm_head_kernel<32>, dim3(nb), dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
                          P, (h16*)y, logit);
       break;
     default:
-      hipLaunchKernelGGL(norm_head_kernel<64>, dim3(nb), dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
+      UNET_LAUNCH(norm_head_kernel<64>, dim3(nb), dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
                          P, (h16*)y, logit);
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 // ---------------------------------------------------------------------------------
@@ -635,21 +635,21 @@ hipError_t norm_head_loss_launch(const void* z, const float* fa, const float* fc
   const dim3 grid(nbp, N);
   switch (C) {
     case 16:
-      hipLaunchKernelGGL(norm_head_loss_kernel<16>, grid, dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
+      UNET_LAUNCH(norm_head_loss_kernel<16>, grid, dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
                          (const h16*)t, (h16*)y, prob, partial);
       break;
     case 32:
-      hipLaunchKernelGGL(norm_head_loss_kernel<32>, grid, dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
+      UNET_LAUNCH(norm_head_loss_kernel<32>, grid, dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
                          (const h16*)t, (h16*)y, prob, partial);
       break;
     default:
-      hipLaunchKernelGGL(norm_head_loss_kernel<64>, grid, dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
+      UNET_LAUNCH(norm_head_loss_kernel<64>, grid, dim3(HT), 0, s, (const h16*)z, fa, fc, cstride, npix, w, b,
                          (const h16*)t, (h16*)y, prob, partial);
   }
   // loss sums {I, St, Sp, BCE}: columns 6C + 3 .. 6C + 6 of the block rows
-  hipLaunchKernelGGL(partial_reduce_kernel, dim3(4), dim3(256), 0, s, partial + 6 * C + 3, N * nbp, hn_width(C),
+  UNET_LAUNCH(partial_reduce_kernel, dim3(4), dim3(256), 0, s, partial + 6 * C + 3, N * nbp, hn_width(C),
                      sums);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t head_norm_coef_launch(const float* partial, int N, int npix, int C, const float* sums, const float* w,
@@ -659,9 +659,9 @@ hipError_t head_norm_coef_launch(const float* partial, int N, int npix, int C, c
   const int nbp = hn_blocks_per_sample(N, npix), nb = N * nbp;
   long long eb = ((long long)nb * C + 255) / 256;
   if (eb > 2048) eb = 2048;
-  hipLaunchKernelGGL(head_norm_coef_kernel, dim3(C + 1 + (int)eb), dim3(256), 0, s, partial, nb, nbp, C, sums, w, fa,
+  UNET_LAUNCH(head_norm_coef_kernel, dim3(C + 1 + (int)eb), dim3(256), 0, s, partial, nb, nbp, C, sums, w, fa,
                      fc, cstride, inv_total, bce_w, gscale, gscale_ptr, rows, gw, gb);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t head_norm_bwd_launch(const void* z, const float* prob, const void* t, const float* sums, const float* w,
@@ -671,9 +671,9 @@ hipError_t head_norm_bwd_launch(const void* z, const float* prob, const void* t,
   int nbp = (1024 + N - 1) / N;
   const int maxb = (P + 255) / 256;
   nbp = nbp > maxb ? maxb : (nbp < 1 ? 1 : nbp);
-  hipLaunchKernelGGL(head_norm_bwd_kernel, dim3(nbp, N), dim3(256), 0, s, (const h16*)z, prob, (const h16*)t, sums, w,
+  UNET_LAUNCH(head_norm_bwd_kernel, dim3(nbp, N), dim3(256), 0, s, (const h16*)z, prob, (const h16*)t, sums, w,
                      fa, fc, ca, cb, cc, cstride, P, C, inv_total, bce_w, gscale, gscale_ptr, (h16*)dz);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t head_finish_launch(float* prob, const void* t, int P, float* partial, float* sums, hipStream_t s) {
@@ -683,9 +683,9 @@ hipError_t head_finish_launch(float* prob, const void* t, int P, float* partial,
   int nb = (P / 4 + HT - 1) / HT;
   nb = nb > 4096 ? 4096 : (nb < 1 ? 1 : nb);
   if (nb > 5 * head_blocks(P)) nb = 5 * head_blocks(P);
-  hipLaunchKernelGGL(head_finish_kernel, dim3(nb), dim3(HT), 0, s, prob, (const h16*)t, P, partial);
-  hipLaunchKernelGGL(partial_reduce_kernel, dim3(4), dim3(256), 0, s, partial, nb, 4, sums);
-  return hipGetLastError();
+  UNET_LAUNCH(head_finish_kernel, dim3(nb), dim3(HT), 0, s, prob, (const h16*)t, P, partial);
+  UNET_LAUNCH(partial_reduce_kernel, dim3(4), dim3(256), 0, s, partial, nb, 4, sums);
+  return launch_status();
 }
 
 }  // namespace unet

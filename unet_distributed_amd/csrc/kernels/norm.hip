@@ -476,14 +476,20 @@ __device__ __forceinline__ void bn_final_channel(const int c, const float s1, co
 // Single-launch BatchNorm statistics (forward / backward / plain column sums, modes 0 / 1
 // / 3): phase 1 as row_slices (block (sl, cb) sums rpb rows of 64 columns into slice sl),
 // then the LAST block to finish -- told by the value its agent-scope counter add returns
-// -- sums the slices of every column and finalises all channels (bn_final_channel).  The
-// hand-off follows MI355X_MICROARCH.md's sc1 recipe: every slice store and every slice
-// load of the last block is an agent-scope relaxed atomic (global_store / global_load
-// sc1: written through, L1 bypassed), every storing wave waits vmcnt(0) before the
-// workgroup barrier behind which one lane adds to the counter, and the last block's waves
-// load only after the barrier its adding lane joins.  The last block resets the counter
-// (graph replays).  Fixed summation order: deterministic, no float atomics.  Replaces the
-// row_slices + bn_final pair (72 -> 36 launches per BatchNorm step).
+// -- sums the slices of every column and finalises all channels (bn_final_channel).
+// Hand-off (HIP scoped memory model, no reliance on undocumented hardware ordering):
+//   * every slice value is stored by an agent-scope atomic store (written through to the
+//     device-coherent level: the 8 XCDs have separate L2s, so a plain store could sit in
+//     the producing XCD's L2);
+//   * every thread then executes an agent-scope RELEASE fence and the workgroup barrier,
+//     after which one lane does the counter add with ACQ_REL semantics (the fences of all
+//     threads happen-before the add through the barrier);
+//   * the last block's lane observes the final count (its add acquires every earlier
+//     block's release), the barrier hands that to the block, and every thread executes an
+//     agent-scope ACQUIRE fence before its agent-scope atomic loads of the slices.
+// The last block resets the counter (graph replays).  Fixed summation order:
+// deterministic, no float atomics.  Replaces the row_slices + bn_final pair (72 -> 36
+// launches per BatchNorm step).
 __global__ void __launch_bounds__(NT) bn_stats_fused_kernel(const float* __restrict__ rows, int R, int C, int rpb,
                                                             float* __restrict__ slices, int* __restrict__ counter,
                                                             float count, int mode, const float* __restrict__ gamma,
@@ -515,14 +521,15 @@ __global__ void __launch_bounds__(NT) bn_stats_fused_kernel(const float* __restr
       __hip_atomic_store(slices + (size_t)sl * W + col, red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl],
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int done = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int done = __hip_atomic_fetch_add(counter, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     last = done == (int)(gridDim.x * gridDim.y) - 1;
   }
   __syncthreads();
   if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const int nsl = gridDim.x;
   const int t = threadIdx.x & 63;
   const int mom = t >> 5;
@@ -682,19 +689,19 @@ const char* norm_check(int C, int G) {
 hipError_t norm_moments_launch(const void* A, const void* B, int N, int P, int C, float* partial, float* S,
                                hipStream_t s) {
   const int nbp = norm_blocks_per_sample(N, P);
-  hipLaunchKernelGGL(chan_moments_kernel, dim3(N * nbp), dim3(NT), NT * 2 * 8 * sizeof(float), s,
+  UNET_LAUNCH(chan_moments_kernel, dim3(N * nbp), dim3(NT), NT * 2 * 8 * sizeof(float), s,
                      (const h16*)A, (const h16*)B, P, C, nbp, partial);
-  hipLaunchKernelGGL(moments_collect_kernel, dim3(ew_grid((long long)N * 2 * C)), dim3(NT), 0, s, partial, N, C, nbp,
+  UNET_LAUNCH(moments_collect_kernel, dim3(ew_grid((long long)N * 2 * C)), dim3(NT), 0, s, partial, N, C, nbp,
                      S);
-  return hipGetLastError();
+  return launch_status();
 }
 
 // S[n][2][C] = sum of the nbp consecutive partial rows of sample n (rows written by
 // a conv epilogue's per-tile statistics, conv_epilogue.h EPI_STATS / EPI_DGRAD_NORM)
 hipError_t moments_collect_launch(const float* partial, int N, int C, int nbp, float* S, hipStream_t s) {
-  hipLaunchKernelGGL(moments_collect_kernel, dim3(ew_grid((long long)N * 2 * C)), dim3(NT), 0, s, partial, N, C, nbp,
+  UNET_LAUNCH(moments_collect_kernel, dim3(ew_grid((long long)N * 2 * C)), dim3(NT), 0, s, partial, N, C, nbp,
                      S);
-  return hipGetLastError();
+  return launch_status();
 }
 
 int sample_slices(int N) { return N < 64 ? N : 64; }
@@ -705,26 +712,26 @@ hipError_t bn_finalize_launch(const float* S, int N, int C, float count, int mod
                               float* fa, float* fc, hipStream_t s) {
   const int nsl = sample_slices(N);
   if (mode != 2)
-    hipLaunchKernelGGL(sample_slices_kernel, dim3((C + 63) / 64, nsl), dim3(NT), 0, s, S, N, C, nsl,
+    UNET_LAUNCH(sample_slices_kernel, dim3((C + 63) / 64, nsl), dim3(NT), 0, s, S, N, C, nsl,
                        (const float*)nullptr, (const float*)nullptr, partial);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, partial, nsl, C, count, mode, gamma,
+  UNET_LAUNCH(bn_finalize_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, partial, nsl, C, count, mode, gamma,
                      eps, momentum, run_mean, run_var, mean, rstd, ca, cb, cc, dgamma, dbeta, beta, fa, fc);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t gn_finalize_launch(const float* S, int N, int C, int G, int P, int mode, const float* gamma, float eps,
                               float* mean, float* rstd, float* ca, float* cb, float* cc, float* dgamma, float* dbeta,
                               float* partial, const float* beta, float* fa, float* fc, hipStream_t s) {
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3((N * G + NT - 1) / NT), dim3(NT), 0, s, S, N, C, G, (float)P, mode,
+  UNET_LAUNCH(gn_finalize_kernel, dim3((N * G + NT - 1) / NT), dim3(NT), 0, s, S, N, C, G, (float)P, mode,
                      gamma, eps, mean, rstd, ca, cb, cc, beta, fa, fc);
   if (mode == 1) {
     const int nsl = sample_slices(N);
-    hipLaunchKernelGGL(sample_slices_kernel, dim3((C + 63) / 64, nsl), dim3(NT), 0, s, S, N, C, nsl,
+    UNET_LAUNCH(sample_slices_kernel, dim3((C + 63) / 64, nsl), dim3(NT), 0, s, S, N, C, nsl,
                        (const float*)mean, (const float*)rstd, partial);
-    hipLaunchKernelGGL(gn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, (const float*)partial, nsl, C,
+    UNET_LAUNCH(gn_param_grad_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, s, (const float*)partial, nsl, C,
                        dgamma, dbeta);
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 int row_slices(int R) { return (R + SL_ROWS - 1) / SL_ROWS; }
@@ -735,19 +742,19 @@ hipError_t bn_stats_launch(const float* rows, int R, int C, float count, int mod
                            float* rstd, float* fa, float* fc, float* ca, float* cb, float* cc, float* dgamma,
                            float* dbeta, float* slices, hipStream_t s) {
   if (mode == 2) {                  // inference: running statistics only
-    hipLaunchKernelGGL(bn_final_kernel, dim3((C + 31) / 32), dim3(NT), 0, s, slices, 0, C, count, mode, gamma, beta,
+    UNET_LAUNCH(bn_final_kernel, dim3((C + 31) / 32), dim3(NT), 0, s, slices, 0, C, count, mode, gamma, beta,
                        eps, momentum, run_mean, run_var, mean, rstd, fa, fc, ca, cb, cc, dgamma, dbeta);
-    return hipGetLastError();
+    return launch_status();
   }
   // one launch: slices, then the finalize by the last block; the counter lives just past
   // the row_slices(R) * 2C slice floats of the workspace (zeroed once, reset every use)
   const int rpb = fused_rows_per_block(R);
   const int nsl = (R + rpb - 1) / rpb;
   int* counter = (int*)(slices + (size_t)row_slices(R) * 2 * C);
-  hipLaunchKernelGGL(bn_stats_fused_kernel, dim3(nsl, (2 * C + 63) / 64), dim3(NT), 0, s, rows, R, C, rpb, slices,
+  UNET_LAUNCH(bn_stats_fused_kernel, dim3(nsl, (2 * C + 63) / 64), dim3(NT), 0, s, rows, R, C, rpb, slices,
                      counter, count, mode, gamma, beta, eps, momentum, run_mean, run_var, mean, rstd, fa, fc, ca, cb, cc,
                      dgamma, dbeta);
-  return hipGetLastError();
+  return launch_status();
 }
 
 // GroupNorm from partial rows [N * rps][2][C] (rows of sample n consecutive).  mode 1 also
@@ -757,7 +764,7 @@ hipError_t gn_stats_launch(const float* rows, int N, int rps, int C, int G, int 
                            const float* beta, float eps, float* mean, float* rstd, float* fa, float* fc, float* ca,
                            float* cb, float* cc, float* dgamma, float* dbeta, float* work, hipStream_t s) {
   const size_t lds = (4 * C + (4 * G > 4 * 64 ? 4 * G : 4 * 64)) * sizeof(float);
-  hipLaunchKernelGGL(gn_sample_kernel, dim3(N), dim3(NT), lds, s, rows, rps, C, G, (float)P, mode, gamma, beta, eps,
+  UNET_LAUNCH(gn_sample_kernel, dim3(N), dim3(NT), lds, s, rows, rps, C, G, (float)P, mode, gamma, beta, eps,
                      mean, rstd, fa, fc, ca, cb, cc, work);
   if (mode == 1) {
     // dgamma / dbeta = column sums of the per-sample contributions (fused single launch)
@@ -765,35 +772,35 @@ hipError_t gn_stats_launch(const float* rows, int N, int rps, int C, int G, int 
     const int rpb = fused_rows_per_block(N);
     const int nsl = (N + rpb - 1) / rpb;
     int* counter = (int*)(slices + (size_t)row_slices(N) * 2 * C);
-    hipLaunchKernelGGL(bn_stats_fused_kernel, dim3(nsl, (2 * C + 63) / 64), dim3(NT), 0, s, (const float*)work, N, C,
+    UNET_LAUNCH(bn_stats_fused_kernel, dim3(nsl, (2 * C + 63) / 64), dim3(NT), 0, s, (const float*)work, N, C,
                        rpb, slices, counter, 1.f, 3, gamma, beta, eps, 0.f, (float*)nullptr, (float*)nullptr,
                        (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr,
                        (float*)nullptr, (float*)nullptr, dgamma, dbeta);
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 // chan_moments only (no collect): partial rows [N * nbp][2][C] for bn/gn_stats
 hipError_t norm_rows_launch(const void* A, const void* B, int N, int P, int C, float* rows, hipStream_t s) {
   const int nbp = norm_blocks_per_sample(N, P);
-  hipLaunchKernelGGL(chan_moments_kernel, dim3(N * nbp), dim3(NT), NT * 2 * 8 * sizeof(float), s, (const h16*)A,
+  UNET_LAUNCH(chan_moments_kernel, dim3(N * nbp), dim3(NT), NT * 2 * 8 * sizeof(float), s, (const h16*)A,
                      (const h16*)B, P, C, nbp, rows);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t norm_apply_launch(const void* z, int N, int P, int C, const float* mean, const float* rstd, int cstride,
                              const float* gamma, const float* beta, int relu, float drop_rate, uint32_t seed,
                              const uint32_t* seed_ptr, uint32_t salt, void* y, hipStream_t s) {
-  hipLaunchKernelGGL(norm_apply_kernel, dim3(norm_blocks_per_sample(N, P), N), dim3(NT), 0, s, (const h16*)z, P, C,
+  UNET_LAUNCH(norm_apply_kernel, dim3(norm_blocks_per_sample(N, P), N), dim3(NT), 0, s, (const h16*)z, P, C,
                      mean, rstd, cstride, gamma, beta, relu, drop_rate, seed, seed_ptr, salt, (h16*)y);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t norm_bwd_apply_launch(const void* g, const void* z, int N, int P, int C, const float* ca, const float* cb,
                                  const float* cc, int cstride, void* dz, hipStream_t s) {
-  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(norm_blocks_per_sample(N, P), N), dim3(NT), 0, s, (const h16*)g,
+  UNET_LAUNCH(norm_bwd_apply_kernel, dim3(norm_blocks_per_sample(N, P), N), dim3(NT), 0, s, (const h16*)g,
                      (const h16*)z, P, C, ca, cb, cc, cstride, (h16*)dz);
-  return hipGetLastError();
+  return launch_status();
 }
 
 }  // namespace unet

@@ -152,22 +152,22 @@ const char* tconv_fused_check(int C, int K, int O, int Ca) {
 hipError_t tconv_compose_launch(const float* wt, const float* wa, int C, int K, int O, int Ca, int rowstride,
                                 void* out, hipStream_t s) {
   const int n = K * rowstride;
-  hipLaunchKernelGGL(tconv_compose_kernel, dim3((n + 255) / 256), dim3(256), 0, s, wt, wa, C, K, O, Ca, rowstride,
+  UNET_LAUNCH(tconv_compose_kernel, dim3((n + 255) / 256), dim3(256), 0, s, wt, wa, C, K, O, Ca, rowstride,
                      (h16*)out);
-  return hipGetLastError();
+  return launch_status();
 }
 
 hipError_t tconv_chain_launch(const float* Hs, const float* bs, const float* wa, int C, int K, int O, int Ca,
                               float* dwt, float* dbt, const float* wt, const float* bt, const float* skg, float* dwa,
                               hipStream_t s) {
   const int nw = (4 * C * K + 63) / 64;            // 64 elements (x 4 o quarters) per block
-  hipLaunchKernelGGL(tconv_chain_kernel, dim3(nw + C), dim3(256), 0, s, Hs, bs, wa, C, K, O, Ca, nw, dwt, dbt);
+  UNET_LAUNCH(tconv_chain_kernel, dim3(nw + C), dim3(256), 0, s, Hs, bs, wa, C, K, O, Ca, nw, dwt, dbt);
   if (dwa) {
     const int n = 9 * Ca * O;
-    hipLaunchKernelGGL(tconv_chain_wa_kernel, dim3((n + 15) / 16), dim3(256), 0, s, Hs, bs, wt, bt, skg, C, K, O,
+    UNET_LAUNCH(tconv_chain_wa_kernel, dim3((n + 15) / 16), dim3(256), 0, s, Hs, bs, wt, bt, skg, C, K, O,
                        Ca, dwa);
   }
-  return hipGetLastError();
+  return launch_status();
 }
 
 }  // namespace unet

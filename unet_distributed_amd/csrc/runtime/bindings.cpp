@@ -22,6 +22,7 @@
 #include <functional>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "launch_api.h"
@@ -618,12 +619,20 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     need(1, 1, 0);
     void* p = vp(0);
     size_t bytes = (size_t)I[0];
-    return [=](hipStream_t s) { return hipMemsetAsync(p, 0, bytes, s); };
+    return [=](hipStream_t s) { return unet_types::dry_dispatch() ? hipSuccess : hipMemsetAsync(p, 0, bytes, s); };
   }
   throw std::invalid_argument("unknown generic op '" + kind + "'");
 }
 
 int head_blocks_py(int P) { return head_blocks(P); }
+
+thread_local bool g_dry = false;
+
+// sets dry dispatch for the current thread while alive (Plan::check_dispatch)
+struct DryScope {
+  DryScope() { g_dry = true; }
+  ~DryScope() { g_dry = false; }
+};
 
 class Plan {
  public:
@@ -657,6 +666,20 @@ class Plan {
     names_.push_back(name.empty() ? kind : name);
     return (int)ops_.size() - 1;
   }
+  // Dry dispatch of ops [begin, end) (conv_params.h dry_dispatch): every launcher resolves
+  // its kernel instantiation and returns its status without launching -- no GPU needed.
+  // Returns (op index, name, error) of every op whose launcher has no kernel for its
+  // parameters (e.g. a combination conv_fwd_prepare accepts that launch_win never built).
+  std::vector<std::tuple<int, std::string, std::string>> check_dispatch(int begin, int end) {
+    if (begin < 0 || end > (int)ops_.size() || begin > end) throw std::out_of_range("Plan.check_dispatch: bad range");
+    std::vector<std::tuple<int, std::string, std::string>> bad;
+    DryScope dry;
+    for (int i = begin; i < end; ++i) {
+      hipError_t e = ops_[i](nullptr);
+      if (e != hipSuccess) bad.emplace_back(i, names_[i], hipGetErrorName(e));
+    }
+    return bad;
+  }
   void set_seed(uint32_t s) { seed_ = s; }
   // device address of a uint32 seed: dropout kernels read it at run time (graph mode)
   void set_seed_ptr(uintptr_t p) { seed_dev_ = reinterpret_cast<const uint32_t*>(p); }
@@ -681,6 +704,10 @@ class Plan {
 };
 
 }  // namespace
+
+namespace unet_types {
+bool dry_dispatch() { return g_dry; }
+}  // namespace unet_types
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X (gfx950) HIP kernels and launch-plan executor for the UNet trainer";
@@ -798,6 +825,7 @@ PYBIND11_MODULE(_C, m) {
       .def("add_wgrad", &Plan::add_wgrad)
       .def("add_generic", &Plan::add_generic, py::arg("kind"), py::arg("ptrs"), py::arg("ints"),
            py::arg("floats"), py::arg("name") = "")
+      .def("check_dispatch", &Plan::check_dispatch)
       .def("set_seed", &Plan::set_seed)
       .def("set_seed_ptr", &Plan::set_seed_ptr)
       .def("size", &Plan::size)

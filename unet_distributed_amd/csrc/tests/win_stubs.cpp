@@ -4,6 +4,10 @@
 // sanitizer build from compiling ~150 gfx950 kernel variants it would not run.
 #include "conv_win.h"
 
+namespace unet_types {
+bool dry_dispatch() { return false; }
+}  // namespace unet_types
+
 namespace unet {
 template <int BN, int BM>
 hipError_t launch_win(const ConvFwdParams&, hipStream_t) {

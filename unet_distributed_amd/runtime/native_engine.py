@@ -38,6 +38,7 @@ import torch
 from .. import native
 from ..models.spec import UNetSpec
 from .params import FlatParams
+from .plan_check import RecordingPlan
 
 
 
@@ -65,6 +66,71 @@ def _r64(k: int) -> int:
 #   wg_target    weight-gradient split-K grid target, workgroups per gradient (512)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
                        tconv_onload=1, fwd_offset=6, wg_target=512)
+
+
+class Fusion:
+    """Declarative precondition of one planner fusion: the config-level conditions under
+    which the planner may apply it.  Each decision site first asks ``_fusion_ok(name)``;
+    only per-layer structure (channel multiples, a single consumer, ...) and the kernel
+    probe (``conv_fwd_grid``) stay at the site.  `needs`: fusions that must be active for
+    the same layer (a tconv on load reads nothing but what the chained weight gradient
+    leaves unread).  tests/test_plan_check.py enumerates norm x decoder x dims x img and
+    validates every plan statically (runtime/plan_check.py)."""
+
+    def __init__(self, doc, norm=None, dims=None, decoder=None, img=None, option=None, needs=(),
+                 even_batch=False, cpad=None, when=None):
+        self.doc, self.norm, self.dims, self.decoder, self.img = doc, norm, dims, decoder, img
+        self.option, self.needs, self.even_batch, self.cpad, self.when = option, tuple(needs), even_batch, cpad, when
+
+    def unmet(self, e) -> List[str]:
+        """Conditions this config violates (empty: the fusion may apply)."""
+        out = []
+        if self.norm is not None and e.spec.norm not in self.norm:
+            out.append("norm=%s" % e.spec.norm)
+        if self.dims is not None and e.dims not in self.dims:
+            out.append("dims=%d" % e.dims)
+        dec = "upsampling" if e.spec.use_upsampling else "transposed"
+        if self.decoder is not None and dec not in self.decoder:
+            out.append("decoder=%s" % dec)
+        if self.img is not None and e.img not in self.img:
+            out.append("img=%d" % e.img)
+        if self.option is not None and not e.opts[self.option]:
+            out.append("option %s=0" % self.option)
+        if self.even_batch and e.B % 2:
+            out.append("odd batch")
+        if self.cpad is not None and e.cpad not in self.cpad:
+            out.append("padded input channels %d" % e.cpad)
+        if self.when is not None and not self.when(e):
+            out.append("structure")
+        return out
+
+
+_ROW_IMGS = (16, 32, 64, 128)       # 2D images whose rows the row-window kernels take whole
+FUSIONS: Dict[str, Fusion] = {
+    "head_onload": Fusion("head input gradient formed on load by its consumers (head_grad.h)",
+                          norm={"none"}, dims={2}, img=_ROW_IMGS, option="head_onload",
+                          when=lambda e: e.tinfo[e.head_in][1] == 32 and e.wgrad_win >= 0),
+    "head_fuse": Fusion("Mask head in the epilogue of its input conv's forward",
+                        norm={"none"}, option="head_fuse", when=lambda e: e.tinfo[e.head_in][1] == 32),
+    "pool_epilogue": Fusion("2x2 max-pool in the convNb forward epilogue", norm={"none"}),
+    "fwd_2streams": Fusion("training forward as two half-batch chunks on two streams",
+                           norm={"none"}, even_batch=True, when=lambda e: e.opts["fwd_streams"] == 2),
+    "tconv_fused": Fusion("composite transposed-conv backward (tconv_fused.hip)", dims={2},
+                          option="tconv_fused"),
+    "tconv_wa": Fusion("consumer's u-row weight gradient chained from the slab sums", dims={2},
+                       option="tconv_wa", needs=("tconv_fused",)),
+    "tconv_onload": Fusion("transposed conv formed on load by its consumer's forward (XF 5)", dims={2},
+                           option="tconv_onload", needs=("tconv_wa",)),
+    "norm_onload": Fusion("normalisation of an 'a' conv's output on load by its consumer (XF 1)",
+                          norm={"batch", "group"}, dims={2}),
+    "skip_route": Fusion("skip-half data gradient with the pool backward in its epilogue", dims={2}),
+    "tail_halves": Fusion("last data gradient in two batch halves (first-layer wgrad overlap)",
+                          norm={"none"}, dims={2}, img=_ROW_IMGS, even_batch=True, cpad=(4, 8),
+                          when=lambda e: e.wgrad_win >= 0),
+    "first_dz_onload": Fusion("first layer's norm-backward dz formed by its window wgrad (XF 2)",
+                              norm={"batch", "group"}, dims={2}, img=_ROW_IMGS, cpad=(4, 8),
+                              when=lambda e: e.wgrad_win >= 0),
+}
 
 
 def engine_options(overrides: Optional[Dict[str, int]] = None) -> Dict[str, int]:
@@ -140,10 +206,13 @@ class NativeUNet:
         self._rev_mode = 3
         # -1: never use the row-window weight-gradient kernel (set by A/B tests)
         self.wgrad_win = 0
+        # fusion name -> layers it was applied to (FUSIONS; plan validation and tests)
+        self.fusions: Dict[str, List[str]] = {}
         self._alloc_weights()
         self._alloc_activations()
-        self.plan = self.C.Plan(self.dt_id)
-        self.eval_plan = self.C.Plan(self.dt_id)
+        # (each op's parameters are kept for the static plan validation, runtime/plan_check.py)
+        self.plan = RecordingPlan(self.C.Plan(self.dt_id))
+        self.eval_plan = RecordingPlan(self.C.Plan(self.dt_id))
         self._plan_xforms()
         self._norm_head_loss = False
         self._build_forward(self.plan, dropout=True)
@@ -156,6 +225,22 @@ class NativeUNet:
         self.set_buckets(bucket_bounds)
         if not dry_run:          # dry_run: plan construction only (CPU tests, no GPU launches)
             self.repack()
+
+    # ------------------------------------------------------------------ fusion preconditions
+    def _fusion_ok(self, name: str, layer: Optional[str] = None) -> bool:
+        """Config-level preconditions of fusion `name` (FUSIONS) hold, and for a per-layer
+        fusion every fusion it needs is active for `layer`."""
+        f = FUSIONS[name]
+        if f.unmet(self):
+            return False
+        return all(layer in self.fusions.get(n, ()) for n in f.needs) if layer is not None else \
+            all(self.fusions.get(n) for n in f.needs)
+
+    def _fusion_on(self, name: str, layer: str):
+        """Record that the planner applied fusion `name` to `layer`."""
+        self.fusions.setdefault(name, [])
+        if layer not in self.fusions[name]:
+            self.fusions[name].append(layer)
 
     # ------------------------------------------------------------------ shapes
     def sdims(self, level: int) -> Tuple[int, int, int]:
@@ -328,9 +413,9 @@ class NativeUNet:
         # instead of reading a materialised 32-channel dY; the head backward only reduces
         # the Mask weight / bias gradients (on the side stream).  2D norm-free model with
         # a 32-channel head input on 16..128-wide rows (option head_onload=0: materialised).
-        self.head_onload = (spec.norm == "none" and self.dims == 2 and self.tinfo[self.head_in][1] == 32
-                            and self.img in (16, 32, 64, 128) and self.wgrad_win >= 0
-                            and bool(self.opts["head_onload"]))
+        self.head_onload = self._fusion_ok("head_onload")
+        if self.head_onload:
+            self._fusion_on("head_onload", self.head_in)
         if spec.norm == "none":
             for l in spec.layers:
                 if l.kind == "conv" and (l.name != self.head_in or self.head_onload):
@@ -380,11 +465,12 @@ class NativeUNet:
         whose skip-half data gradient rides on the pool backward.  Option tconv_fused = the
         deepest fine level fused (0 off)."""
         self.tconv_fused: Dict[str, dict] = {}
+        self._dropped: Dict[str, torch.Tensor] = {}
         self._tf_consumer: Dict[str, str] = {}
         self._wa_chain_of: Dict[str, str] = {}  # consumer conv whose u-row wgrad is chained -> tconv
         self._ut_onload: Dict[str, str] = {}    # consumer conv that forms u on load -> tconv
         top = self.opts["tconv_fused"]
-        if self.dims != 2 or top <= 0 or (self.spec.norm != "none" and not self.fuse_norm_stats_planned()):
+        if not self._fusion_ok("tconv_fused") or (self.spec.norm != "none" and not self.fuse_norm_stats_planned()):
             return
         for l in self.spec.layers:
             if l.kind != "tconv" or l.level > top:
@@ -419,6 +505,7 @@ class NativeUNet:
                                             hs=torch.zeros(16 * O * K, dtype=torch.float32, device=self.device),
                                             bs=torch.zeros(16 * O, dtype=torch.float32, device=self.device))
             self._tf_consumer[c.name] = l.name
+            self._fusion_on("tconv_fused", l.name)
             self._plan_wa_chain(l, c, self.tconv_fused[l.name])
             self._plan_ut_onload(l, c, self.tconv_fused[l.name])
 
@@ -436,10 +523,11 @@ class NativeUNet:
         composite FORWARD on the coarse grid with composed weights measured -0.5..-1.2 %
         and was removed in round 4.)"""
         Cs, O = c.cin - l.cout, c.cout
-        if not self.opts["tconv_wa"] or Cs <= 0 or Cs % 32 or O % 16:
+        if not self._fusion_ok("tconv_wa", l.name) or Cs <= 0 or Cs % 32 or O % 16:
             return
         tf["wa"] = dict(Cs=Cs, skg=torch.zeros(9 * Cs * O, dtype=torch.float32, device=self.device))
         self._wa_chain_of[c.name] = l.name
+        self._fusion_on("tconv_wa", l.name)
 
     def _ut_fields(self, tl, x_ptr):
         """conv_params.h TconvSrc fields: the consumer's src1 = tconv `tl` of x formed on load."""
@@ -452,7 +540,7 @@ class NativeUNet:
         that forward forms each 32-channel chunk of u in LDS from b (conv_win.h XF 5): the
         transposed conv's forward launch and its fine output tensor (1 GiB at level 1,
         b1024) are gone, and the consumer reads the 4x smaller coarse b instead of u."""
-        if l.level > self.opts["tconv_onload"] or "wa" not in tf:
+        if l.level > self.opts["tconv_onload"] or not self._fusion_ok("tconv_onload", l.name):
             return
         normed = self.spec.norm != "none"
         d = self._conv_common(c.level, 3, 1, 1)
@@ -467,8 +555,10 @@ class NativeUNet:
             return
         tf["ut"] = True
         self._ut_onload[c.name] = l.name
-        # the fine output is never formed (no forward writes it, no backward reads it)
-        self.bufs.pop(l.name, None)
+        self._fusion_on("tconv_onload", l.name)
+        # the fine output is never formed (no forward writes it, no backward reads it);
+        # kept aside so the plan validation can flag any op that would still read it
+        self._dropped[l.name] = self.bufs.pop(l.name, None)
 
     # ------------------------------------------------------------------ normalisation
     NORM_EPS = 1e-3          # models/reference.py::_norm (Keras default epsilon)
@@ -667,11 +757,9 @@ class NativeUNet:
     def _tail_halves(self, d, l, src1, skip, dy):
         """Two half-batch copies of dgrad dict `d` when its destination is the first
         layer's output (the last dgrad of the backward) and the halves line up with
-        the first layer's weight-gradient splits (norm-free 2D model, even batch;
-        UNET_TAIL_SPLIT=0 off), else None."""
-        if (skip is not None or self.inputs.get(src1, ("",))[0] != "x" or self.spec.norm != "none"
-                or self.dims != 2 or self.B % 2
-                or self.img not in (16, 32, 64, 128) or self.cpad not in (4, 8) or self.wgrad_win < 0):
+        the first layer's weight-gradient splits (norm-free 2D model, even batch), else
+        None."""
+        if skip is not None or self.inputs.get(src1, ("",))[0] != "x" or not self._fusion_ok("tail_halves"):
             return None      # (the first-layer row-window wgrad, whose split halves are image halves)
         b = self.bufs
 
@@ -688,6 +776,7 @@ class NativeUNet:
                 self.C.conv_fwd_grid(h)
         except ValueError:
             return None
+        self._fusion_on("tail_halves", l.name)
         return h1, h2
 
     def _skip_route(self, l, skip, c1, c2, dy):
@@ -695,7 +784,7 @@ class NativeUNet:
         gradient when it can carry the pool backward of its skip source (2D row-window
         data gradient), else None (the dual-destination dgrad + separate pool backward).  Saves the skip-gradient tensor's
         write and re-read: the pool backward's read of it becomes a second read of dy."""
-        if self.dims != 2:
+        if not self._fusion_ok("skip_route"):
             return None
         if self.spec.norm != "none" and not (skip in self.norm_layers and self.fuse_norm_stats):
             return None
@@ -726,6 +815,7 @@ class NativeUNet:
             return None
         if self.spec.norm == "none":
             self._rev_order(d, "g:" + l.name, "g:" + skip)
+        self._fusion_on("skip_route", l.name)
         return pool, d
 
     def _relu_mask(self, tname):
@@ -792,7 +882,7 @@ class NativeUNet:
         normalising on load too, -1.3 % BN / -1.5 % GN; dz formed on load by the data
         gradient, -1.1 % BN; level-1 dgrad + wgrad both forming dz, -1.2 % BN.)"""
         self._xf_fwd = set()
-        if self.spec.norm == "none" or self.dims != 2:
+        if not self._fusion_ok("norm_onload"):
             return
         users: Dict[str, list] = {}
         for name, inp in self.inputs.items():
@@ -820,6 +910,7 @@ class NativeUNet:
             except ValueError:
                 continue
             self._xf_fwd.add(l.name)
+            self._fusion_on("norm_onload", l.name)
 
     # (option fwd_offset: the second forward chunk starts after the first chunk's first
     # fwd_offset layers; round-2 sweep 3 / 6 / 9 / 13: -0.2 / +0.3 / . / -0.6 %)
@@ -831,8 +922,7 @@ class NativeUNet:
         (BatchNorm needs whole-batch statistics); option fwd_streams=1 keeps one stream.
         Default 2 since round 3: same-box interleaved A/B of the headline step +1.0 / +1.0 /
         +0.6 % (44.2k -> 44.7k img/s, round 2 measured +0.9 % the same way)."""
-        n = self.opts["fwd_streams"]
-        if n != 2 or not train or self.spec.norm != "none" or self.B % 2 or self.device.type != "cuda":
+        if not train or not self._fusion_ok("fwd_2streams") or self.device.type != "cuda":
             return 1
         return 2
 
@@ -847,7 +937,7 @@ class NativeUNet:
         self._norm_head = False
         if train:
             self._norm_head_loss = False
-        self._fuse_head = bool(self.opts["head_fuse"])
+        self._fuse_head = self._fusion_ok("head_fuse")
         # convNb -> 2x2 max-pool fused into the conv's epilogue where the kernel can
         self._pool_of = {self.inputs[x.name][0]: x.name for x in spec.layers if x.kind == "pool"}
         self._pool_fused = set()
@@ -862,7 +952,7 @@ class NativeUNet:
         spec = self.spec
         self._head_fused_blocks = 0
         self._norm_head = False
-        self._fuse_head = bool(self.opts["head_fuse"])
+        self._fuse_head = self._fusion_ok("head_fuse")
         self._pool_of = {self.inputs[x.name][0]: x.name for x in spec.layers if x.kind == "pool"}
         self._pool_fused = set()
         layers = [l for l in spec.layers if l.kind not in ("up", "mask")]
@@ -924,7 +1014,7 @@ class NativeUNet:
             if bits is not None and not normed:
                 d["relu_bits"] = _ptr(bits) + c * nb * (self.npix(l.level) // self.B) * l.cout // 8
             pool = self._pool_of.get(l.name)
-            if pool is not None and not normed and (nch == 1 or self._fwd2_active(plan)):
+            if pool is not None and self._fusion_ok("pool_epilogue") and (nch == 1 or self._fwd2_active(plan)):
                 # fused 2x2 max-pool: the epilogue writes the pooled tensor + argmax codes
                 pcode = _ptr(self.pool_codes[pool]) + c * nb * (self.npix(l.level + 1) // self.B) * (l.cout // 8) * 4
                 dp = dict(d, pool_dst=P(pool), pool_code=pcode)
@@ -932,11 +1022,13 @@ class NativeUNet:
                     self.C.conv_fwd_grid(dp)
                     d = dp
                     self._pool_fused.add(pool)
+                    self._fusion_on("pool_epilogue", l.name)
                 except ValueError:
                     pass
-            if l.name == self.head_in and self._fuse_head and not normed and not d["drop_rate"]:
+            if l.name == self.head_in and self._fuse_head and not d["drop_rate"]:
                 nbk = self._head_grid(d)
                 if nbk:
+                    self._fusion_on("head_fuse", l.name)
                     d.update(head_w=self.master_ptr("Mask/kernel"), head_b=self.master_ptr("Mask/bias"),
                              head_logit=_ptr(self.prob) + 4 * c * nb * (self.npix(1) // self.B))
                     self._head_fused_blocks = nbk
@@ -1117,8 +1209,8 @@ class NativeUNet:
                 dy = self._no_dy if onload else b["d:" + l.name]
                 first_xf = None
                 if spec.norm != "none":
-                    if (first and self.dims == 2 and self.img in (16, 32, 64, 128) and self.cpad in (4, 8)
-                            and self.wgrad_win >= 0):
+                    if first and self._fusion_ok("first_dz_onload"):
+                        self._fusion_on("first_dz_onload", l.name)
                         # the first layer's dz is read only by its weight gradient: that kernel
                         # forms dz = ca g + cb z + cc on load (no norm_bwd_apply pass)
                         first_xf = dict(xform=2, xa=_ptr(b["ca:" + l.name]), xb=_ptr(b["cb:" + l.name]),
@@ -1365,6 +1457,10 @@ class NativeUNet:
             self._job_tables.append(table)
             plan.add_generic("multi_reduce", [_ptr(table)], [len(pending_jobs), t1, t2], [],
                              "reduce:" + ",".join(pending_layers + pending_tags))
+            # (the stage is written by the op's phase 1 and read by its phase 2)
+            plan.annotate(reads=[j["slab"] for j in pending_jobs],
+                          writes=[j["out"] for j in pending_jobs] +
+                          [j["stage"] for j in pending_jobs if not j["direct"]])
             for ln in pending_layers:
                 self._layer_done_at[ln] = plan.size()
             pending_jobs.clear()
