@@ -4,7 +4,7 @@
 #   bash scripts/gpu_r5_configs.sh ["512 batches"] ["3d batches"]
 set -o pipefail
 export TMPDIR=/tmp
-b512=${1:-16 32 64 128}; b3=${2:-8 12 16}
+b512=${1-16 32 64 128}; b3=${2-8 12 16}
 o=gpurun_out/r5cfg; mkdir -p $o; : > $o/configs.jsonl
 run() { tag=$1; shift
   timeout -k 10 300 python bench.py "$@" > $o/$tag.log 2>&1 || { echo "bench $tag rc=$?"; tail -20 $o/$tag.log; exit 1; }
@@ -23,9 +23,9 @@ print(json.dumps(r))
 PY
   tail -1 $o/configs.jsonl | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['tag'], d['value'], d['ms_per_step'], d['tflops'], 'TF/s', d.get('train_dice_last_batch'))"
 }
-run headline --steps 20 --warmup 5
+[ -n "$SKIP_MAIN" ] || { run headline --steps 20 --warmup 5
 run bn --norm batch --steps 10 --warmup 3
 run gn16 --norm group --dtype fp16 --steps 10 --warmup 3
-run ups --use_upsampling --in_channels 1 --steps 10 --warmup 3
+run ups --use_upsampling --in_channels 1 --steps 10 --warmup 3; }
 for b in $b512; do run s512_b$b --img_size 512 --in_channels 1 --per_gpu_batch $b --steps 8 --warmup 3; done
 for b in $b3; do run d3_b$b --dims 3 --per_gpu_batch $b --steps 5 --warmup 2; done

@@ -1,0 +1,239 @@
+"""fp32 kernels (f32.hip, v_mfma_f32_16x16x4_f32) against fp32 ATen: the reference's own
+precision (`test_dist.py:196-202`).  Products are exact in fp32 MFMA, so only the
+summation order differs from ATen: relative error <= 1e-4 (observed ~1e-6)."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from test_gpu_kernels import C, nchw, nhwc, ptr, stream
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-30)).item()
+
+
+def transpose(w, T, A, B, flip):
+    out = torch.empty(T * A * B, device=w.device)
+    C().generic("f32_transpose", [ptr(w), ptr(out)], [T, A, B, int(flip)], [], stream())
+    return out
+
+
+@pytest.mark.parametrize("N,H,C1,C2,Co,relu", [(2, 16, 32, 32, 64, 1), (1, 32, 4, 0, 32, 1), (2, 8, 1, 0, 32, 0),
+                                               (3, 16, 64, 0, 48, 1)])
+def test_f32_conv3x3_fwd(cuda_dev, N, H, C1, C2, Co, relu):
+    torch.manual_seed(H + C1)
+    dev = cuda_dev
+    a = torch.randn(N, H, H, C1, device=dev)
+    b = torch.randn(N, H, H, C2, device=dev) if C2 else None
+    w = torch.randn(3, 3, C1 + C2, Co, device=dev) * 0.1
+    bias = torch.randn(Co, device=dev)
+    out = torch.empty(N, H, H, Co, device=dev)
+    C().f32_conv(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=C1, C2=C2, src1=ptr(a),
+                      src2=ptr(b) if C2 else None, wgt=ptr(w), bias=ptr(bias), Cout=Co, relu=relu, dst1=ptr(out)),
+                 stream())
+    xin = nchw(a) if not C2 else torch.cat([nchw(a), nchw(b)], 1)
+    ref = nhwc(F.conv2d(xin, w.permute(3, 2, 0, 1), bias, padding=1))
+    if relu:
+        ref = F.relu(ref)
+    assert rel(out, ref) < TOL
+
+
+def test_f32_conv3d_fwd(cuda_dev):
+    torch.manual_seed(3)
+    dev = cuda_dev
+    N, D, Ci, Co = 2, 8, 32, 32
+    x = torch.randn(N, D, D, D, Ci, device=dev)
+    w = torch.randn(3, 3, 3, Ci, Co, device=dev) * 0.05
+    out = torch.empty(N, D, D, D, Co, device=dev)
+    C().f32_conv(dict(N=N, OD=D, OH=D, OW=D, ID=D, IH=D, IW=D, KD=3, KH=3, KW=3, pad=1, C1=Ci, src1=ptr(x),
+                      wgt=ptr(w), Cout=Co, relu=0, dst1=ptr(out)), stream())
+    ref = F.conv3d(x.permute(0, 4, 1, 2, 3), w.permute(4, 3, 0, 1, 2), padding=1).permute(0, 2, 3, 4, 1)
+    assert rel(out, ref) < TOL
+
+
+def test_f32_conv_dgrad_and_wgrad(cuda_dev):
+    """Data gradient = conv of dY with the flipped, transposed kernel (f32_transpose) and the
+    ReLU mask of the producer; weight gradient = per-tap split-K slabs (+ the fixed-order
+    slab reduction)."""
+    torch.manual_seed(4)
+    dev = cuda_dev
+    N, H, C1, C2, Co = 2, 32, 32, 32, 32
+    xa = F.relu(torch.randn(N, H, H, C1, device=dev))
+    xb = F.relu(torch.randn(N, H, H, C2, device=dev))
+    w = torch.randn(3, 3, C1 + C2, Co, device=dev) * 0.1
+    dy = torch.randn(N, H, H, Co, device=dev)
+    wd = transpose(w.reshape(-1), 9, C1 + C2, Co, True)          # [tap'][co][ci]
+    dx = torch.empty(N, H, H, C1 + C2, device=dev)
+    mask = torch.cat([xa, xb], -1).contiguous()
+    C().f32_conv(dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Co, src1=ptr(dy), wgt=ptr(wd),
+                      Cout=C1 + C2, dst1=ptr(dx), mask1=ptr(mask)), stream())
+    xr = torch.cat([nchw(xa), nchw(xb)], 1).requires_grad_(True)
+    wr = w.permute(3, 2, 0, 1).clone().requires_grad_(True)
+    y = F.conv2d(xr, wr, padding=1)
+    gx, gw = torch.autograd.grad(y, (xr, wr), nchw(dy))
+    assert rel(dx, nhwc(gx) * (mask > 0)) < TOL
+    splits = 5
+    slab = torch.empty(splits, 9, C1 + C2, Co, device=dev)
+    C().f32_wgrad(dict(N=N, QH=H, QW=H, AH=H, AW=H, KH=3, KW=3, pad=1, M1=C1, M2=C2, Nc=Co, a1=ptr(xa), a2=ptr(xb),
+                       b=ptr(dy), slab=ptr(slab), splits=splits), stream())
+    assert rel(slab.sum(0), gw.permute(2, 3, 1, 0).reshape(9, C1 + C2, Co)) < TOL
+
+
+@pytest.mark.parametrize("dims", [2, 3])
+def test_f32_tconv_fwd_dgrad_wgrad(cuda_dev, dims):
+    torch.manual_seed(5 + dims)
+    dev = cuda_dev
+    N, Hc, Ci, Co = 2, 8, 64, 32
+    T = 2 ** dims
+    sp = (Hc,) * dims
+    x = torch.randn((N,) + sp + (Ci,), device=dev)
+    wt = torch.randn((2,) * dims + (Co, Ci), device=dev) * 0.1      # TF (kh, kw, Cout, Cin)
+    bias = torch.randn(Co, device=dev)
+    # forward: 1x1 GEMM [Ci] x [Ci][tap Co] + pixel shuffle
+    wf = transpose(wt.reshape(-1), 1, T * Co, Ci, False)           # [Ci][tap][Co]
+    out = torch.empty((N,) + tuple(2 * s for s in sp) + (Co,), device=dev)
+    d = dict(N=N, OH=Hc, OW=Hc, IH=Hc, IW=Hc, KH=1, KW=1, C1=Ci, src1=ptr(x), wgt=ptr(wf), bias=ptr(bias),
+             Cout=T * Co, shuffle=dims, dst1=ptr(out))
+    if dims == 3:
+        d.update(OD=Hc, ID=Hc)
+    C().f32_conv(d, stream())
+    perm_in = (0, 4, 1, 2, 3) if dims == 3 else (0, 3, 1, 2)
+    perm_out = (0, 2, 3, 4, 1) if dims == 3 else (0, 2, 3, 1)
+    wtorch = wt.permute(*((dims + 1, dims) + tuple(range(dims))))  # (Cin, Cout, k...)
+    xr = x.permute(*perm_in).clone().requires_grad_(True)
+    wr = wtorch.clone().requires_grad_(True)
+    tfn = F.conv_transpose3d if dims == 3 else F.conv_transpose2d
+    y = tfn(xr, wr, bias, stride=2)
+    assert rel(out, y.permute(*perm_out)) < TOL
+    g = torch.randn_like(y)
+    gx, gw = torch.autograd.grad(y, (xr, wr), g)
+    gf = g.permute(*perm_out).contiguous()                          # fine gradient, channels last
+    # data gradient: 2x2 stride-2 conv of the fine gradient with W[tap][co][ci] (the TF layout)
+    dx = torch.empty_like(x)
+    d = dict(N=N, OH=Hc, OW=Hc, IH=2 * Hc, IW=2 * Hc, KH=2, KW=2, stride=2, pad=0, C1=Co, src1=ptr(gf),
+             wgt=ptr(wt), Cout=Ci, dst1=ptr(dx))
+    if dims == 3:
+        d.update(OD=Hc, ID=2 * Hc, KD=2)
+    C().f32_conv(d, stream())
+    assert rel(dx, gx.permute(*perm_out)) < TOL
+    # weight gradient: A = fine gradient (m = Co, taps at 2 q + tap), B = x (n = Ci)
+    splits = 3
+    slab = torch.empty(splits, T, Co, Ci, device=dev)
+    d = dict(N=N, QH=Hc, QW=Hc, AH=2 * Hc, AW=2 * Hc, KH=2, KW=2, stride=2, pad=0, M1=Co, Nc=Ci, a1=ptr(gf),
+             b=ptr(x), slab=ptr(slab), splits=splits)
+    if dims == 3:
+        d.update(QD=Hc, AD=2 * Hc, KD=2)
+    C().f32_wgrad(d, stream())
+    ref = gw.permute(*(tuple(range(2, dims + 2)) + (1, 0))).reshape(T, Co, Ci)
+    assert rel(slab.sum(0), ref) < TOL
+
+
+@pytest.mark.parametrize("dims", [2, 3])
+def test_f32_pool_ups_head(cuda_dev, dims):
+    torch.manual_seed(9 + dims)
+    dev = cuda_dev
+    N, S, Cc = 2, 16, 32
+    D = S if dims == 3 else 1
+    sp = (S,) * dims
+    x = F.relu(torch.randn((N,) + sp + (Cc,), device=dev))
+    y = torch.empty((N,) + tuple(s // 2 for s in sp) + (Cc,), device=dev)
+    C().generic("f32_pool_fwd", [ptr(x), ptr(y)], [N, D, S, S, Cc, int(dims == 3)], [], stream())
+    pool = F.max_pool3d if dims == 3 else F.max_pool2d
+    perm_in = (0, 4, 1, 2, 3) if dims == 3 else (0, 3, 1, 2)
+    perm_out = (0, 2, 3, 4, 1) if dims == 3 else (0, 2, 3, 1)
+    xr = x.permute(*perm_in).clone().requires_grad_(True)
+    yr = pool(xr, 2)
+    assert torch.equal(y, yr.permute(*perm_out))
+    gy = torch.randn_like(y)
+    skip = torch.randn_like(x)
+    dx = torch.empty_like(x)
+    C().generic("f32_pool_bwd", [ptr(x), ptr(gy), ptr(skip), ptr(dx)], [N, D, S, S, Cc, int(dims == 3)], [],
+                stream())
+    (g,) = torch.autograd.grad(yr, xr, gy.permute(*perm_in))
+    ref = (g.permute(*perm_out) + skip) * (x > 0)
+    assert rel(dx, ref) < 1e-6
+    # nearest upsample and its backward (sum of children, masked)
+    up = torch.empty_like(x)
+    C().generic("f32_ups_fwd", [ptr(y), ptr(up)], [N, max(D // 2, 1), S // 2, S // 2, Cc, int(dims == 3)], [],
+                stream())
+    assert torch.equal(up, F.interpolate(y.permute(*perm_in), scale_factor=2, mode="nearest").permute(*perm_out))
+    dl = torch.empty_like(y)
+    C().generic("f32_ups_bwd", [ptr(skip), ptr(y), ptr(dl)], [N, max(D // 2, 1), S // 2, S // 2, Cc,
+                                                               int(dims == 3)], [], stream())
+    k = 2
+    sm = skip.permute(*perm_in)
+    sm = (F.avg_pool3d(sm, k) if dims == 3 else F.avg_pool2d(sm, k)) * (k ** dims)
+    assert rel(dl, sm.permute(*perm_out) * (y > 0)) < 1e-6
+    # head: logits, sigmoid, Dice + BCE sums and the backward
+    P = x.numel() // Cc
+    w = torch.randn(Cc, device=dev) * 0.1
+    b = torch.randn(1, device=dev)
+    t = (torch.rand(P, device=dev) > 0.7).float()
+    nb = C().f32_head_blocks(P)
+    prob = torch.empty(P, device=dev)
+    part = torch.empty(nb * (Cc + 1) + Cc + 1, device=dev)
+    sums = torch.empty(4, device=dev)
+    C().generic("f32_head_fwd", [ptr(x), ptr(w), ptr(b), ptr(t), ptr(prob), ptr(part), ptr(sums)], [P, Cc], [],
+                stream())
+    xf = x.reshape(P, Cc).clone().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    z = xf @ wr + br
+    pr = torch.sigmoid(z)
+    I, St, Sp = (t * pr).sum(), t.sum(), pr.sum()
+    bce = F.binary_cross_entropy_with_logits(z, t, reduction="sum")
+    assert rel(prob, pr) < 1e-6
+    assert rel(sums, torch.stack([I, St, Sp, bce])) < 1e-5
+    bce_w = 0.5
+    loss = -torch.log(2 * I + 1) + torch.log(St + Sp + 1) + bce_w * bce / P
+    gx, gw, gb = torch.autograd.grad(loss, (xf, wr, br))
+    dxh = torch.empty_like(x)
+    gwk, gbk = torch.empty(Cc, device=dev), torch.empty(1, device=dev)
+    C().generic("f32_head_bwd", [ptr(x), ptr(w), ptr(prob), ptr(t), ptr(sums), ptr(dxh), ptr(part), ptr(gwk),
+                                 ptr(gbk)], [P, Cc], [1.0 / P, bce_w], stream())
+    assert rel(dxh.reshape(P, Cc), gx * (xf > 0)) < 1e-5
+    assert rel(gwk, gw) < 1e-5 and rel(gbk, gb) < 1e-5
+    # column sums (bias gradients)
+    cs = torch.empty(Cc, device=dev)
+    cpart = torch.empty(64 * Cc, device=dev)
+    C().generic("f32_colsum", [ptr(x), ptr(cpart), ptr(cs)], [P, Cc, 64], [], stream())
+    assert rel(cs, x.reshape(P, Cc).sum(0)) < 1e-6
+
+
+@pytest.mark.parametrize("kw", [
+    dict(batch_size=2, img_size=64, in_channels=4),
+    dict(batch_size=2, img_size=64, in_channels=1, use_upsampling=True, loss="dice_bce"),
+    dict(batch_size=2, img_size=16, in_channels=4, dims=3),
+    dict(batch_size=3, img_size=128, in_channels=1),
+])
+def test_f32_native_step_matches_aten_fp32(cuda_dev, kw):
+    """The whole fp32 training step (runtime/f32_engine.py: forward with dropout, Dice (+ BCE)
+    loss, backward) against the fp32 ATen step on the same batch and weights: loss sums
+    and every parameter gradient within fp32 summation-order noise."""
+    from test_gpu_model import _setup
+    from unet_distributed_amd.runtime.f32_engine import NativeUNetF32
+    spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, dtype="fp32", backend="native", **kw)
+    assert isinstance(nb.engine, NativeUNetF32)
+    nb.fwd_bwd(x, y, seed=17)
+    tb.fwd_bwd(x, y, seed=17)
+    torch.cuda.synchronize()
+    assert rel(nb.sums().cpu(), tb.sums().cpu()) < 1e-5
+    worst = 0.0
+    for name, shape, off, n in fn.entries:
+        g, r = fn.grad[off:off + n], ft.grad[off:off + n]
+        e = rel(g, r)
+        worst = max(worst, e)
+        assert e < 2e-4, (name, e)
+    print("fp32 step worst per-tensor relative error %.2e" % worst)
+    # the Adam step (TF semantics, shared fused launch) keeps the replicas identical
+    from unet_distributed_amd.runtime.optim import TFAdam
+    from unet_distributed_amd.runtime.trainer import _NativeOpt
+    opt_n, opt_t = TFAdam(fn, cfg, native=_NativeOpt(nb)), TFAdam(ft, cfg)
+    opt_n.step()
+    opt_t.step()
+    torch.cuda.synchronize()
+    assert rel(fn.master, ft.master) < 1e-5

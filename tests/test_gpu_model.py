@@ -391,7 +391,9 @@ def test_head_onload_step_equals_materialised(cuda_dev, monkeypatch, kw):
     probabilities and every parameter gradient."""
     outs = []
     for v in ("0", "1"):
-        monkeypatch.setenv("UNET_ENGINE", "head_onload=" + v)
+        # (dw_fuse=0: with head_onload=0 the head input conv's weight gradient would run in
+        # the fused data + weight gradient kernel, a different fp32 summation order)
+        monkeypatch.setenv("UNET_ENGINE", "dw_fuse=0,head_onload=" + v)
         spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
         e = nb.engine
         assert e.head_onload == (v == "1")
@@ -490,3 +492,38 @@ def test_tconv_fused_norm_step(cuda_dev, monkeypatch, norm):
         d0 = 1.0 - _cos(g0[k].float(), ref[k])
         d2 = 1.0 - _cos(g2[k].float(), ref[k])
         assert d2 <= 2.0 * d0 + 1e-3, (k, d0, d2)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(batch_size=4, img_size=128, in_channels=4),
+    dict(batch_size=3, img_size=128, in_channels=4, loss="dice_bce", hip_graph=True),
+])
+def test_fused_dgrad_wgrad_step(cuda_dev, monkeypatch, kw):
+    """dw_fuse=1 (default: conv1b's data and weight gradients from one staged dY halo,
+    conv_dw.hip) vs dw_fuse=0: the forward, every data gradient and every other parameter
+    gradient are bit-identical; the fused layers' weight / bias gradients differ only by
+    fp32 summation order."""
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("UNET_ENGINE", "dw_fuse=" + v)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
+        e = nb.engine
+        fused = e.fusions.get("dw_fused", [])
+        assert (fused == ["conv1b"]) == (v == "1"), fused
+        for seed in (31, 32):
+            nb.fwd_bwd(x, y, seed=seed)
+        torch.cuda.synchronize()
+        outs.append((nb.sums().cpu(), e.prob.clone(), e.bufs["d:conv1a"].clone(),
+                     {k: fn.view(fn.grad, k).clone() for k, *_ in fn.entries}))
+    (s0, p0, d0, g0), (s1, p1, d1, g1) = outs
+    assert torch.equal(s0, s1) and torch.equal(p0, p1) and torch.equal(d0, d1)
+    for k in g0:
+        if k.startswith("conv1b/"):
+            assert rel_err_(g1[k], g0[k]) < 1e-5, (k, rel_err_(g1[k], g0[k]))
+        else:
+            assert torch.equal(g0[k], g1[k]), k
+
+
+def rel_err_(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-30)).item()

@@ -171,3 +171,15 @@ def test_fused_head_plan():
     spec = UNetSpec(in_channels=4)
     e = NativeUNet(spec, FlatParams(spec), 2, 64, "cpu", dry_run=True, opts=dict(head_fuse=0))
     assert e._head_fused_blocks == 0
+
+
+def test_fused_dgrad_wgrad_host_checks():
+    """conv_dw.hip takes 2D 32 -> 32 channel data gradients on 128-wide rows only."""
+    C = native.require()
+    base = dict(N=1, OH=128, OW=128, IH=128, IW=128, KH=3, KW=3, pad=1, C1=32, src1=1, wgt=1, Cout=32, relu=0,
+                dst1=1, fw_x=1, fw_slab=1, fw_bias_slab=1, fw_Cx=32, fw_nsplit=4)
+    assert C.conv_fwd_grid(base) == 4
+    for bad in (dict(OW=64, IW=64), dict(C1=64), dict(Cout=64, D1=64), dict(fw_nsplit=0), dict(fw_slab=None),
+                dict(relu=1, bias=1)):
+        with pytest.raises(ValueError):
+            C.conv_fwd_grid(dict(base, **bad))

@@ -954,7 +954,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if (p.route_gy && (!p.pool_code || (conv_epi_mode(p) != EPI_DGRAD && conv_epi_mode(p) != EPI_DGRAD_NORM) ||
                      !win_eligible(p) || p.KD != 1 || p.OD != 1 ||
                      p.OH % 2 || p.OW % 2 || p.D1 != p.Cout || p.pool_dst || p.mask_scale1 != 1.f ||
-                     !win_tile(conv_fwd_pick(p))))
+                     !(win_tile(conv_fwd_pick(p)) || conv_fwd_pick(p) == 14)))
     return "conv_fwd: fused pool backward needs a 2D row-window data gradient (even dims, one destination, codes)";
   if (p.pool_dst) {
     const int W = p.OW > 128 ? 128 : p.OW;
@@ -963,7 +963,12 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
         p.OH % 2 || p.OW % 2 || p.Cout % 8 || p.head_w)
       return "conv_fwd: fused max-pool needs a 2D row-window ReLU forward (even rows, codes buffer)";
   }
-  if (p.tile < 0 || p.tile > 13) return "conv_fwd: bad tile id";
+  if (p.fw.x) {
+    if (const char* m = conv_dw_check(p)) return m;
+  } else if (p.tile == 14) {
+    return "conv_fwd: tile 14 (fused weight gradient) needs the fw fields";
+  }
+  if (p.tile < 0 || p.tile > 14) return "conv_fwd: bad tile id";
   if (p.tile == 12 && (!win_eligible(p) || p.Cout % 64 || p.head_w))
     return "conv_fwd: 64-wide row-window tile not applicable";
   if (p.tile == 10 && !tconv_fwd_eligible(p)) return "conv_fwd: transposed-conv window tile not applicable";
@@ -995,7 +1000,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     const long long opx = (long long)p.OD * p.OH * p.OW;
     const long long lim = (1LL << 31) - 64;
     long long span = img * p.N;                       // bytes a launch addresses from one base
-    if (win_tile(t) || t == 13) span = img;
+    if (win_tile(t) || t == 13 || t == 14) span = img;
     else if (t >= 1 && t <= 5) span = img * (256 / opx + 2 < p.N ? 256 / opx + 2 : p.N);
     if (span >= lim) return "conv_fwd: input exceeds the 2 GiB reach of one buffer base (split the batch)";
   }
@@ -1019,6 +1024,7 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
 // window, 64-channel tile; 13 = 8x8 image window
 int conv_fwd_pick(const ConvFwdParams& p) {
   const int M = p.N * p.OD * p.OH * p.OW;
+  if (p.fw.x) return 14;
   if (p.tile && p.tile != 8) return p.tile;
   // row-window 512x32 wins at every level it applies to (16..128 wide), measured
   // 1.1-2.1x over the implicit-GEMM tiles (profiles/r1_conv_tiles.md); the 512x64
@@ -1035,6 +1041,7 @@ int conv_fwd_pick(const ConvFwdParams& p) {
 
 int conv_fwd_grid(const ConvFwdParams& p) {
   const int t = conv_fwd_pick(p);
+  if (t == 14) return conv_dw_grid(p);
   return win_tile(t) ? win_grid(p) : 0;
 }
 
@@ -1068,6 +1075,7 @@ void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
       return;
     }
     case 10:
+    case 14:
       return;
     case 13:               // 8x8 image window: 4 whole images per tile
       *rows = (p.N + IMG8 - 1) / IMG8;
@@ -1097,6 +1105,7 @@ hipError_t conv_fwd_launch(const ConvFwdParams& p, hipStream_t s) {
     case 10: return launch_tconv_fwd(p, s);
     case 13: return launch_img8(p, s);
     case 11: return launch_tconv_dgrad(p, s);
+    case 14: return launch_conv_dw(p, s);
     default: return launch_cfg<128, 32, 4, 1>(p, s);
   }
 }

@@ -41,6 +41,21 @@ struct TconvSrc {
   int C, kpad;                // coarse channels (32, 64 or 128), weight row pitch
 };
 
+// Weight gradient fused into a row-window data gradient (conv_dw.hip): the data
+// gradient dX = conv(dY, W_flipped) of a 3x3 conv stages the dY halo image of each window
+// in LDS; the same image gives the conv's weight-gradient partials
+//   dW[tap][ci][co] += sum_{q in window} x[q][ci] dY[q - tap + 1][co]
+// against the window's own pixels of the conv's forward input x -- dY is read once for
+// both.  Each workgroup walks a contiguous window range, keeps its dW partial in
+// registers and writes one fp32 slab row (the wgrad_win slab layout, reduced in fixed
+// order by multi_reduce).  x == nullptr: off.
+struct FusedWgrad {
+  const void* x;              // [N][H][W][Cx] 16-bit forward input of the conv
+  float* slab;                // [split_lo + nsplit rows at least][9][Cx][C1] fp32
+  float* bias_slab;           // [.. rows][C1] fp32 column sums of dY (the bias gradient)
+  int Cx, nsplit, split_lo;   // x channels, workgroups (slab rows) of this launch, first row
+};
+
 // Implicit-GEMM "NT" convolution: out[q][n] = epilogue(sum_{tap,c} X[q*s + tap - pad][c] * W[n][tap][c])
 // GEMM M = output pixels q over [N][OD][OH][OW], GEMM N = Cout, K = taps * Cin.
 // One kernel serves: conv forward, conv dgrad (flipped/transposed weights),
@@ -138,6 +153,7 @@ struct ConvFwdParams {
   // support dh in {1 - a, 2 - a}, dw in {1 - b, 2 - b}: those MFMAs are skipped.
   int s2d;
   TconvSrc ut;                // src1 = transposed conv of ut.x formed on load (see TconvSrc)
+  FusedWgrad fw;              // weight-gradient partials from the same dY halo (see FusedWgrad)
   // filled by conv_fwd_prepare (host): K padded to 64, per-tap pixel deltas / offsets
   int Kpad;
   int tap_delta[27];
@@ -184,6 +200,40 @@ struct WgradParams {
   // filled by the launcher
   int lqw, lqh, lqd;          // log2 of the pixel grid (power-of-two fast path)
   signed char tap_d[27], tap_h[27], tap_w[27];
+};
+
+// fp32 path (f32.hip): implicit-GEMM convolution out[q][n] = epi(sum_k A[q][k] W[k][n]),
+// A = im2col of src1 | src2 (k = tap * (C1 + C2) + c, forward-conv tap semantics:
+// input = output * stride + tap - pad), W = [K][Cout] row-major (the TF HWIO kernel
+// flattened, or a transposed / flipped copy for data gradients and transposed convs).
+struct F32Conv {
+  int N, OD, OH, OW, ID, IH, IW, KD, KH, KW, stride, pad;
+  int C1, C2, Cout;
+  const float* src1;
+  const float* src2;
+  const float* wgt;
+  const float* bias;           // [Cout] (shuffle: [Cout >> shuffle]) or nullptr
+  float* dst;
+  int relu;
+  float drop_rate;             // inverted dropout (drop_hash of the bf16 path)
+  uint32_t seed, salt;
+  unsigned long long drop_idx0;
+  const uint32_t* seed_ptr;
+  const float* mask;           // consumer ReLU mask: out = mask > 0 ? out * mask_scale : 0
+  float mask_scale;
+  int shuffle;                 // 2 / 3: transposed-conv pixel-shuffle store, Cout = taps * channels
+  int ldw;                     // weight row stride (>= Cout: a column range of a wider kernel)
+};
+
+// fp32 weight gradient: slab[split][tap][m][n] = sum_{q in split} A[q * stride + tap - pad][m] B[q][n]
+struct F32Wgrad {
+  int N, QD, QH, QW, AD, AH, AW, KD, KH, KW, stride, pad;
+  int M1, M2, Nc;
+  const float* a1;
+  const float* a2;
+  const float* b;
+  float* slab;                 // [splits][taps][M1 + M2][Nc]
+  int splits;
 };
 
 // Tile configuration chosen for a wgrad problem (shared with the host planner).

@@ -58,6 +58,11 @@ constexpr bool win_tile_built(int W) {
 template <int BN, int BM>
 hipError_t launch_win(const ConvFwdParams& p, hipStream_t s);
 
+// fused data + weight gradient window (conv_dw.hip, tile 14; conv_params.h FusedWgrad)
+const char* conv_dw_check(const ConvFwdParams& p);
+int conv_dw_grid(const ConvFwdParams& p);
+hipError_t launch_conv_dw(const ConvFwdParams& p, hipStream_t s);
+
 #ifdef UNET_WIN_IMPL
 namespace {
 

@@ -135,6 +135,12 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.ut.b = (const float*)getp(d, "ut_b");
   p.ut.C = get<int>(d, "ut_C", 0);
   p.ut.kpad = get<int>(d, "ut_kpad", 0);
+  p.fw.x = getp(d, "fw_x");
+  p.fw.slab = (float*)const_cast<void*>(getp(d, "fw_slab"));
+  p.fw.bias_slab = (float*)const_cast<void*>(getp(d, "fw_bias_slab"));
+  p.fw.Cx = get<int>(d, "fw_Cx", 0);
+  p.fw.nsplit = get<int>(d, "fw_nsplit", 0);
+  p.fw.split_lo = get<int>(d, "fw_split_lo", 0);
   p.xout = const_cast<void*>(getp(d, "xout"));
   p.tile = get<int>(d, "tile", 0);
   p.head_w = (const float*)getp(d, "head_w");
@@ -185,6 +191,67 @@ WgradParams wgrad_params(const py::dict& d) {
   if (p.bias_mode && !p.bias_slab) throw std::invalid_argument("wgrad: bias_slab required");
   if (!p.a1 || !p.b || !p.slab) throw std::invalid_argument("wgrad: a1/b/slab required");
   check_msg(wgrad_check(p));
+  return p;
+}
+
+F32Conv f32_conv_params(const py::dict& d) {
+  F32Conv p{};
+  p.N = get<int>(d, "N", 1);
+  p.OD = get<int>(d, "OD", 1);
+  p.OH = get<int>(d, "OH", 1);
+  p.OW = get<int>(d, "OW", 1);
+  p.ID = get<int>(d, "ID", 1);
+  p.IH = get<int>(d, "IH", 1);
+  p.IW = get<int>(d, "IW", 1);
+  p.KD = get<int>(d, "KD", 1);
+  p.KH = get<int>(d, "KH", 1);
+  p.KW = get<int>(d, "KW", 1);
+  p.stride = get<int>(d, "stride", 1);
+  p.pad = get<int>(d, "pad", 0);
+  p.C1 = get<int>(d, "C1", 0);
+  p.C2 = get<int>(d, "C2", 0);
+  p.Cout = get<int>(d, "Cout", 0);
+  p.src1 = (const float*)getp(d, "src1");
+  p.src2 = (const float*)getp(d, "src2");
+  p.wgt = (const float*)getp(d, "wgt");
+  p.bias = (const float*)getp(d, "bias");
+  p.dst = (float*)const_cast<void*>(getp(d, "dst1"));
+  p.relu = get<int>(d, "relu", 0);
+  p.drop_rate = get<float>(d, "drop_rate", 0.f);
+  p.seed = get<uint32_t>(d, "seed", 0u);
+  p.salt = get<uint32_t>(d, "salt", 0u);
+  p.drop_idx0 = get<unsigned long long>(d, "drop_idx0", 0ull);
+  p.mask = (const float*)getp(d, "mask1");
+  p.mask_scale = get<float>(d, "mask_scale1", 1.f);
+  p.shuffle = get<int>(d, "shuffle", 0);
+  p.ldw = get<int>(d, "ldw", p.Cout);
+  check_msg(unet::f32_conv_check(p));
+  return p;
+}
+
+F32Wgrad f32_wgrad_params(const py::dict& d) {
+  F32Wgrad p{};
+  p.N = get<int>(d, "N", 1);
+  p.QD = get<int>(d, "QD", 1);
+  p.QH = get<int>(d, "QH", 1);
+  p.QW = get<int>(d, "QW", 1);
+  p.AD = get<int>(d, "AD", 1);
+  p.AH = get<int>(d, "AH", 1);
+  p.AW = get<int>(d, "AW", 1);
+  p.KD = get<int>(d, "KD", 1);
+  p.KH = get<int>(d, "KH", 1);
+  p.KW = get<int>(d, "KW", 1);
+  p.stride = get<int>(d, "stride", 1);
+  p.pad = get<int>(d, "pad", 0);
+  p.M1 = get<int>(d, "M1", 0);
+  p.M2 = get<int>(d, "M2", 0);
+  p.Nc = get<int>(d, "Nc", 0);
+  p.a1 = (const float*)getp(d, "a1");
+  p.a2 = (const float*)getp(d, "a2");
+  p.b = (const float*)getp(d, "b");
+  p.slab = (float*)const_cast<void*>(getp(d, "slab"));
+  p.splits = get<int>(d, "splits", 1);
+  check_msg(unet::f32_wgrad_check(p));
   return p;
 }
 
@@ -621,6 +688,68 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     size_t bytes = (size_t)I[0];
     return [=](hipStream_t s) { return unet_types::dry_dispatch() ? hipSuccess : hipMemsetAsync(p, 0, bytes, s); };
   }
+  // fp32 path (f32.hip; element-type independent, from the bf16 build)
+  auto fp = [&](int i) { return reinterpret_cast<float*>(P[i]); };
+  if (kind == "f32_pool_fwd" || kind == "f32_ups_fwd") {
+    // ptrs: x, y   ints: N, D, H, W (input resolution; ups: the low one), C, dims3
+    need(2, 6, 0);
+    const float* x = fp(0);
+    float* y = fp(1);
+    int n = I[0], dd = I[1], hh = I[2], ww = I[3], c = I[4], d3 = I[5];
+    if (kind == "f32_pool_fwd") return [=](hipStream_t s) { return unet::f32_pool_fwd_launch(x, n, dd, hh, ww, c, d3, y, s); };
+    return [=](hipStream_t s) { return unet::f32_ups_launch(x, nullptr, n, dd, hh, ww, c, d3, 0, y, s); };
+  }
+  if (kind == "f32_pool_bwd") {
+    // ptrs: x (pool input), dy (pooled gradient), skip (or 0), dx   ints: N, D, H, W, C, dims3
+    need(4, 6, 0);
+    const float *x = fp(0), *dy = fp(1), *sk = fp(2);
+    float* dx = fp(3);
+    int n = I[0], dd = I[1], hh = I[2], ww = I[3], c = I[4], d3 = I[5];
+    return [=](hipStream_t s) { return unet::f32_pool_bwd_launch(x, dy, sk, n, dd, hh, ww, c, d3, dx, s); };
+  }
+  if (kind == "f32_ups_bwd") {
+    // ptrs: full-resolution gradient, low-resolution mask (or 0), low-resolution gradient
+    // ints: N, D, H, W (low resolution), C, dims3
+    need(3, 6, 0);
+    const float *g = fp(0), *mk = fp(1);
+    float* dl = fp(2);
+    int n = I[0], dd = I[1], hh = I[2], ww = I[3], c = I[4], d3 = I[5];
+    return [=](hipStream_t s) { return unet::f32_ups_launch(g, mk, n, dd, hh, ww, c, d3, 1, dl, s); };
+  }
+  if (kind == "f32_head_fwd") {
+    // ptrs: x, w, b, t (or 0), prob, partial, sums   ints: P, C
+    need(7, 2, 0);
+    const float *x = fp(0), *w = fp(1), *b = fp(2), *t = fp(3);
+    float *pr = fp(4), *pa = fp(5), *su = fp(6);
+    int np = I[0], c = I[1];
+    return [=](hipStream_t s) { return unet::f32_head_fwd_launch(x, w, b, t, np, c, pr, pa, su, s); };
+  }
+  if (kind == "f32_head_bwd") {
+    // ptrs: x, w, prob, t, sums, dx (or 0), partial, gw, gb   ints: P, C   floats: inv_total, bce_w
+    need(9, 2, 2);
+    const float *x = fp(0), *w = fp(1), *pr = fp(2), *t = fp(3), *su = fp(4);
+    float *dx = fp(5), *pa = fp(6), *gw = fp(7), *gb = fp(8);
+    int np = I[0], c = I[1];
+    float it = (float)F[0], bw = (float)F[1];
+    return [=](hipStream_t s) { return unet::f32_head_bwd_launch(x, w, pr, t, su, np, c, it, bw, dx, pa, gw, gb, s); };
+  }
+  if (kind == "f32_colsum") {
+    // ptrs: x [rows][C], partial [blocks][C], out [C]   ints: rows, C, blocks
+    need(3, 3, 0);
+    const float* x = fp(0);
+    float *pa = fp(1), *out = fp(2);
+    long long rows = I[0];
+    int c = I[1], nb = I[2];
+    return [=](hipStream_t s) { return unet::f32_colsum_launch(x, rows, c, nb, pa, out, s); };
+  }
+  if (kind == "f32_transpose") {
+    // ptrs: src [T][A][B], dst [T][B][A] (tap order reversed if flip)   ints: T, A, B, flip
+    need(2, 4, 0);
+    const float* src = fp(0);
+    float* dst = fp(1);
+    int t = I[0], a = I[1], b = I[2], fl = I[3];
+    return [=](hipStream_t s) { return unet::f32_transpose_launch(src, t, a, b, fl, dst, s); };
+  }
   throw std::invalid_argument("unknown generic op '" + kind + "'");
 }
 
@@ -658,6 +787,27 @@ class Plan {
     const KernelApi* A = A_;
     ops_.push_back([p, A](hipStream_t s) { return A->wgrad_launch(p, s); });
     names_.push_back(get<std::string>(d, "name", "wgrad"));
+    return (int)ops_.size() - 1;
+  }
+  int add_f32_conv(const py::dict& d) {
+    F32Conv p = f32_conv_params(d);
+    const bool seeded = p.drop_rate > 0.f;
+    const uint32_t* seedp = &seed_;
+    const uint32_t* const* seed_devp = &seed_dev_;
+    ops_.push_back([p, seeded, seedp, seed_devp](hipStream_t s) mutable {
+      if (seeded) {
+        p.seed = *seedp;
+        p.seed_ptr = *seed_devp;
+      }
+      return unet::f32_conv_launch(p, s);
+    });
+    names_.push_back(get<std::string>(d, "name", "f32_conv"));
+    return (int)ops_.size() - 1;
+  }
+  int add_f32_wgrad(const py::dict& d) {
+    F32Wgrad p = f32_wgrad_params(d);
+    ops_.push_back([p](hipStream_t s) { return unet::f32_wgrad_launch(p, s); });
+    names_.push_back(get<std::string>(d, "name", "f32_wgrad"));
     return (int)ops_.size() - 1;
   }
   int add_generic(const std::string& kind, const std::vector<uintptr_t>& P, const std::vector<long long>& I,
@@ -748,6 +898,15 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("w"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("n_total"), py::arg("segs"), py::arg("nseg"),
      py::arg("lr_t"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("gscale"), py::arg("do_adam"),
      py::arg("arena"), py::arg("stream"), py::arg("scalars") = 0, py::arg("dtype") = 0);
+  m.def("f32_conv", [](const py::dict& d, uintptr_t stream) {
+    F32Conv p = f32_conv_params(d);
+    check(unet::f32_conv_launch(p, as_stream(stream)), "f32_conv");
+  }, py::arg("params"), py::arg("stream") = 0);
+  m.def("f32_wgrad", [](const py::dict& d, uintptr_t stream) {
+    F32Wgrad p = f32_wgrad_params(d);
+    check(unet::f32_wgrad_launch(p, as_stream(stream)), "f32_wgrad");
+  }, py::arg("params"), py::arg("stream") = 0);
+  m.def("f32_head_blocks", &unet::f32_head_blocks);
   m.def("head_blocks", &head_blocks_py);
   m.def("norm_blocks_per_sample", &norm_blocks_per_sample);
   m.def("sample_slices", &sample_slices);
@@ -823,6 +982,8 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<int>(), py::arg("dtype") = 0)
       .def("add_conv_fwd", &Plan::add_conv_fwd)
       .def("add_wgrad", &Plan::add_wgrad)
+      .def("add_f32_conv", &Plan::add_f32_conv)
+      .def("add_f32_wgrad", &Plan::add_f32_wgrad)
       .def("add_generic", &Plan::add_generic, py::arg("kind"), py::arg("ptrs"), py::arg("ints"),
            py::arg("floats"), py::arg("name") = "")
       .def("check_dispatch", &Plan::check_dispatch)

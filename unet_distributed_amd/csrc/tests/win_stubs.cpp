@@ -16,4 +16,9 @@ hipError_t launch_win(const ConvFwdParams&, hipStream_t) {
 template hipError_t launch_win<32, 512>(const ConvFwdParams&, hipStream_t);
 template hipError_t launch_win<32, 256>(const ConvFwdParams&, hipStream_t);
 template hipError_t launch_win<64, 256>(const ConvFwdParams&, hipStream_t);
+const char* conv_dw_check(const ConvFwdParams& p) {
+  return p.fw.x ? "host-check build: no fused weight-gradient kernel" : nullptr;
+}
+int conv_dw_grid(const ConvFwdParams& p) { return p.fw.nsplit; }
+hipError_t launch_conv_dw(const ConvFwdParams&, hipStream_t) { return hipErrorNotSupported; }
 }  // namespace unet

@@ -96,7 +96,9 @@ def build(verbose=True, jobs=None):
     os.makedirs(OBJDIR, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")) +
                   glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
-    work = [(f, v) for f in srcs for v in (VARIANTS if f.endswith(".hip") else ["bf16"])]
+    # (f32*.hip: fp32 kernels, element-type independent -- the bf16 build only)
+    work = [(f, v) for f in srcs
+            for v in (VARIANTS if f.endswith(".hip") and not os.path.basename(f).startswith("f32") else ["bf16"])]
     # costliest TUs first so the pool finishes together (the row-window conv units are
     # small files that instantiate conv_win.h's ~150 kernels)
     work.sort(key=lambda j: -(os.path.getsize(j[0]) + (10 ** 6 if "conv_win" in j[0] else 0)))

@@ -106,11 +106,18 @@ class NativeBackend:
 
     def __init__(self, spec, flat: FlatParams, cfg, device, per_rank_batch: int, bounds=None):
         from .native_engine import NativeUNet
+        from .f32_engine import NativeUNetF32
         self.cfg = cfg
         self.flat = flat
-        self.engine = NativeUNet(spec, flat, per_rank_batch, cfg.img_size, device, loss=cfg.loss,
-                                 bce_weight=cfg.bce_weight, bucket_bounds=bounds,
-                                 eval_dropout=cfg.eval_dropout, dtype=cfg.dtype)
+        if cfg.dtype == "fp32":
+            # the reference's precision (test_dist.py:196-202): fp32 storage, fp32 MFMA
+            self.engine = NativeUNetF32(spec, flat, per_rank_batch, cfg.img_size, device, loss=cfg.loss,
+                                        bce_weight=cfg.bce_weight, bucket_bounds=bounds,
+                                        eval_dropout=cfg.eval_dropout)
+        else:
+            self.engine = NativeUNet(spec, flat, per_rank_batch, cfg.img_size, device, loss=cfg.loss,
+                                     bce_weight=cfg.bce_weight, bucket_bounds=bounds,
+                                     eval_dropout=cfg.eval_dropout, dtype=cfg.dtype)
         self.B = per_rank_batch
         if getattr(cfg, "hip_graph", False):
             self.engine.enable_graphs()
@@ -183,10 +190,17 @@ def native_supported(spec, cfg, device) -> Optional[str]:
     """None if the native executor supports this config, else the reason."""
     if torch.device(device).type != "cuda":
         return "not on a GPU"
-    if cfg.dtype not in ("bf16", "fp16"):
-        return "native kernels are bf16 / fp16 (dtype=%s)" % cfg.dtype
+    if cfg.dtype not in ("bf16", "fp16", "fp32"):
+        return "native kernels are bf16 / fp16 / fp32 (dtype=%s)" % cfg.dtype
     if spec.n_cl_out != 1:
         return "n_cl_out != 1"
+    if cfg.dtype == "fp32":
+        # (runtime/f32_engine.py: the reference's own configuration family)
+        if spec.norm != "none":
+            return "the fp32 executor runs the reference's norm-free model (norm=%s: use bf16 / fp16)" % spec.norm
+        if spec.base not in (16, 32, 64):
+            return "fp32 head input channels must be 16, 32 or 64 (base %d)" % spec.base
+        return None
     if spec.base not in (32, 64):
         # the fused head / head kernels take 16, 32 or 64 head-input channels and the
         # row-window kernels 32-channel chunks

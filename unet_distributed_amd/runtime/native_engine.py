@@ -64,8 +64,11 @@ def _r64(k: int) -> int:
 #                consumer's forward where nothing else reads it (1; 0: materialised)
 #   fwd_offset   layers of chunk 0 before the second forward chunk starts (6)
 #   wg_target    weight-gradient split-K grid target, workgroups per gradient (512)
+#   dw_fuse      data + weight gradient of a 32 -> 32 channel conv on 128-wide rows in one kernel
+#                reading dY once (conv_dw.hip) (1)
+#   dw_wgs       workgroups (= slab rows) per fused data + weight gradient launch (512)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
-                       tconv_onload=1, fwd_offset=6, wg_target=512)
+                       tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512)
 
 
 class Fusion:
@@ -127,6 +130,8 @@ FUSIONS: Dict[str, Fusion] = {
     "tail_halves": Fusion("last data gradient in two batch halves (first-layer wgrad overlap)",
                           norm={"none"}, dims={2}, img=_ROW_IMGS, even_batch=True, cpad=(4, 8),
                           when=lambda e: e.wgrad_win >= 0),
+    "dw_fused": Fusion("data + weight gradient from one staged dY halo (conv_dw.hip)", norm={"none"}, dims={2},
+                       img=(128,), option="dw_fuse", when=lambda e: e.wgrad_win >= 0),
     "first_dz_onload": Fusion("first layer's norm-backward dz formed by its window wgrad (XF 2)",
                               norm={"batch", "group"}, dims={2}, img=_ROW_IMGS, cpad=(4, 8),
                               when=lambda e: e.wgrad_win >= 0),
@@ -779,6 +784,35 @@ class NativeUNet:
         self._fusion_on("tail_halves", l.name)
         return h1, h2
 
+    def _plan_dw_fuse(self, l, src1, skip, parts, wspec):
+        """Fused data + weight gradient (conv_dw.hip, FUSIONS['dw_fused']): the data
+        gradient dict(s) `parts` of conv `l` (one, or the two batch halves of the tail split)
+        also produce the weight-gradient partials of `wspec` from the dY halo they stage --
+        dY (1 GiB at level 1, b1024) is read once instead of twice.  Returns the dicts with
+        the fw_* fields (slab pointers filled at emission), or None."""
+        if (not self._fusion_ok("dw_fused") or skip is not None or l.cin != 32 or l.cout != 32
+                or wspec.get("kernel_out") or wspec["kd"].get("xform") or wspec["kd"].get("hg_prob")
+                or wspec["M1"] != 32 or wspec["M2"] or src1 not in self.bufs):
+            return None
+        nsplit = self.opts["dw_wgs"]
+        b = self.bufs
+        half = b[src1].numel() * b[src1].element_size() // len(parts)
+        out = []
+        for k, d in enumerate(parts):
+            if d.get("nz") or d.get("hg_prob") or d.get("route_gy"):
+                return None
+            f = dict(d, rev=0, fw_x=_ptr(b[src1]) + k * half, fw_Cx=l.cin, fw_nsplit=nsplit, fw_split_lo=k * nsplit,
+                     name=d["name"])
+            try:
+                if self.C.conv_fwd_grid(dict(f, fw_slab=1, fw_bias_slab=1)) != nsplit:
+                    return None
+            except ValueError:
+                return None
+            out.append(f)
+        wspec["dw"] = dict(rows=nsplit * len(parts))
+        self._fusion_on("dw_fused", l.name)
+        return out
+
     def _skip_route(self, l, skip, c1, c2, dy):
         """(pool name, dgrad dict) of the deferred skip half of decoder conv l's data
         gradient when it can carry the pool backward of its skip source (2D row-window
@@ -1310,16 +1344,24 @@ class NativeUNet:
                         return d
                     dd_ = mk()                 # built now: it decides the fused norm backward
                     halves = self._tail_halves(dd_, l, src1, skip, dy)
+                    parts = self._plan_dw_fuse(l, src1, skip, [dd_] if halves is None else list(halves), wspec)
+                    if parts is not None:
+                        halves = None if len(parts) == 1 else parts
+                        dd_ = parts[0]
+
+                    def fin(h, w=wspec):
+                        # fused weight gradient: the slab rows of this layer's weight-gradient spec
+                        return dict(h, fw_slab=w["slab_ptrs"][0], fw_bias_slab=w["slab_ptrs"][1]) if "dw" in w else h
                     if halves is None:
-                        emit_conv(lambda dd_=dd_: dd_)
+                        emit_conv(lambda dd_=dd_, fin=fin: fin(dd_))
                     else:
                         # the last dgrad of the chain in two batch halves: the first layer's
                         # weight gradient (the backward's tail, alone on the GPU otherwise)
                         # starts on the side stream as soon as the first half is written
-                        emit_conv(lambda h=halves[0]: h)
+                        emit_conv(lambda h=halves[0], fin=fin: fin(h))
                         tail_parts[src1] = len(ops)
                         ops.append(("placeholder",))
-                        emit_conv(lambda h=halves[1]: h)
+                        emit_conv(lambda h=halves[1], fin=fin: fin(h))
                     if up1 == 2:
                         lvl = self.tinfo[src1][0]
                         dd, hh, ww = self.sdims(lvl)
@@ -1404,6 +1446,8 @@ class NativeUNet:
             if w.get("parts"):                     # each half keeps the full grid
                 sp = sized[k]
                 sized[k] = (2 * sp[0],) + tuple(sp[1:])
+            if "dw" in w:                          # fused into the data gradient: its slab rows
+                sized[k] = (w["dw"]["rows"], w["M1"], KT3, 1, 0)
         stot = btot = sttot = 0
         regions = []
         for w, (splits, Mtot, taps, tg, smallc) in zip(wg_specs, sized):
@@ -1504,7 +1548,12 @@ class NativeUNet:
                          bias_slab=bslab)
                 if part is not None:
                     d.update(split_lo=part * splits // 2, split_n=splits // 2)
-                plan.add_wgrad(d)
+                if "dw" in w:
+                    # computed by the fused data-gradient launch(es) that follow in the plan;
+                    # only the slab reduction is planned here
+                    w["slab_ptrs"] = (slab, bslab)
+                else:
+                    plan.add_wgrad(d)
                 if part == 0:
                     continue                       # the reductions follow the last part
                 KT = w["KT"]

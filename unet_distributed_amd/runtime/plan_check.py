@@ -27,8 +27,8 @@ import torch
 
 _HG = ("hg_prob", "hg_t", "hg_sums", "hg_w", "hg_bits", "hg_gscale")
 CONV_READS = ("src1", "src2", "wgt", "bias", "mask1", "mask2", "route_gy", "nz", "na", "nc", "xa", "xb", "xc", "xz",
-              "ut_x", "ut_w", "ut_b", "head_w", "head_b") + _HG
-CONV_WRITES = ("dst1", "dst2", "stats", "relu_bits", "pool_dst", "head_logit", "xout")
+              "ut_x", "ut_w", "ut_b", "head_w", "head_b", "fw_x") + _HG
+CONV_WRITES = ("dst1", "dst2", "stats", "relu_bits", "pool_dst", "head_logit", "xout", "fw_slab", "fw_bias_slab")
 WGRAD_READS = ("a1", "a2", "b", "xa", "xb", "xc", "xz") + _HG
 WGRAD_WRITES = ("slab", "bias_slab")
 
@@ -86,6 +86,20 @@ def _generic_rw(kind: str, p: List[int], ints: List[int]) -> Tuple[List[int], Li
         return _sel(p, [0, 1]), _sel(p, [2])
     if kind == "tconv_chain":
         return _sel(p, [0, 1, 2, 5, 6, 7]), _sel(p, [3, 4, 8])
+    if kind == "wgrad_reduce":
+        return _sel(p, [0]), _sel(p, [1, 2])
+    if kind in ("f32_pool_fwd", "f32_ups_fwd", "f32_transpose"):
+        return _sel(p, [0]), _sel(p, [1])
+    if kind == "f32_pool_bwd":
+        return _sel(p, [0, 1, 2]), _sel(p, [3])
+    if kind == "f32_ups_bwd":
+        return _sel(p, [0, 1]), _sel(p, [2])
+    if kind == "f32_head_fwd":
+        return _sel(p, [0, 1, 2, 3]), _sel(p, [4, 5, 6])
+    if kind == "f32_head_bwd":
+        return _sel(p, [0, 1, 2, 3, 4]), _sel(p, [5, 6, 7, 8])
+    if kind == "f32_colsum":
+        return _sel(p, [0]), _sel(p, [1, 2])
     if kind == "multi_reduce":
         return _sel(p, [0]), []          # slab / out pointers: the op's annotation (RecordingPlan.annotate)
     raise KeyError("plan_check: no read/write layout for generic op %r" % kind)
@@ -110,6 +124,19 @@ class RecordingPlan:
         i = self._plan.add_wgrad(d)
         self.ops.append(dict(name=d.get("name", "wgrad"), reads=[d.get(k) for k in WGRAD_READS],
                              writes=[d.get(k) for k in WGRAD_WRITES]))
+        return i
+
+    def add_f32_conv(self, d):
+        i = self._plan.add_f32_conv(d)
+        self.ops.append(dict(name=d.get("name", "f32_conv"), reads=[d.get(k) for k in ("src1", "src2", "wgt", "bias",
+                                                                                        "mask1")],
+                             writes=[d.get("dst1")]))
+        return i
+
+    def add_f32_wgrad(self, d):
+        i = self._plan.add_f32_wgrad(d)
+        self.ops.append(dict(name=d.get("name", "f32_wgrad"), reads=[d.get(k) for k in ("a1", "a2", "b")],
+                             writes=[d.get("slab")]))
         return i
 
     def add_generic(self, kind, ptrs, ints, floats, name=""):
@@ -151,11 +178,16 @@ def engine_regions(e) -> Tuple[_Regions, set]:
     for k, t in e.bufs.items():
         R.add(k, t)
     inputs.add("x")
-    for k, t in e.relu_bits.items():
+    for k, t in getattr(e, "relu_bits", {}).items():
         R.add("bits:" + k, t)
-    for k, t in e.pool_codes.items():
+    for k, t in getattr(e, "pool_codes", {}).items():
         R.add("code:" + k, t)
-    for k, t in e._stat_bufs.items():
+    for k, t in getattr(e, "wcopy", {}).items():          # fp32 executor: per-step weight layouts
+        R.add("wcopy:" + k, t)
+    for i, t in enumerate(getattr(e, "_keep", [])):         # fp32 executor: slabs / reduction stages
+        R.add("keep%d" % i, t)
+    R.add("colsum_part", getattr(e, "_colsum_part", None))
+    for k, t in getattr(e, "_stat_bufs", {}).items():
         R.add("stat:" + k, t)
         if k.startswith("w"):                    # bn/gn_stats workspaces (self-contained)
             inputs.add("stat:" + k)
@@ -169,7 +201,7 @@ def engine_regions(e) -> Tuple[_Regions, set]:
     for i, t in enumerate(getattr(e, "_job_tables", [])):
         R.add("jobs%d" % i, t)
         inputs.add("jobs%d" % i)
-    for tn, tf in e.tconv_fused.items():
+    for tn, tf in getattr(e, "tconv_fused", {}).items():
         for k in ("wg", "hs", "bs"):
             R.add("tf:%s:%s" % (tn, k), tf[k])
         if "wa" in tf:
