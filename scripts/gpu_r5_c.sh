@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 5 check C: GPU suite subsets touched this round, the fp32 bench against ATen fp32,
+# per-launch times of the headline, the big-batch configs (chunked wgrad), the upsampling
+# decoder Dice experiment at the reference's defaults.
+set -o pipefail
+export TMPDIR=/tmp
+o=gpurun_out/r5c; mkdir -p $o
+timeout -k 10 900 python -u -m pytest tests/test_gpu_f32.py tests/test_gpu_model.py tests/test_gpu_kernels.py \
+  tests/test_gpu_conv_dw.py -q -s --timeout 300 --timeout-method thread > $o/tests.log 2>&1; rc=$?
+grep -E "passed|failed|worst" $o/tests.log | tail -8
+[ $rc -gt 1 ] && { echo "tests crashed rc=$rc"; tail -30 $o/tests.log; exit 1; }
+[ $rc -eq 1 ] && grep -E "^FAILED|Error" $o/tests.log | head -20
+timeout -k 10 300 python bench.py --dtype fp32 --backend torch --steps 3 --warmup 1 > $o/bench_aten32.log 2>&1 || { echo "aten fp32 bench rc=$?"; tail -5 $o/bench_aten32.log; }
+grep '^{' $o/bench_aten32.log | cut -c1-300
+timeout -k 10 240 python bench.py > $o/bench.log 2>&1 || { echo "bench rc=$?"; tail -20 $o/bench.log; exit 1; }
+grep '^{' $o/bench.log | cut -c1-200
+UNET_ENGINE="fwd_streams=1" timeout -k 10 300 python tools/layer_times.py --batch 1024 --img 128 --out $o/lt.md > $o/lt.log 2>&1 || { echo "lt rc=$?"; tail -20 $o/lt.log; exit 1; }
+head -3 $o/lt.md
+SKIP_MAIN=1 bash scripts/gpu_r5_configs.sh "128" "16" || echo "configs failed"
+timeout -k 10 1500 bash scripts/gpu_r5_ups_dice.sh 200 1 2 3 > $o/dice.log 2>&1 || { echo "dice rc=$?"; tail -20 $o/dice.log; exit 1; }
+tail -12 gpurun_out/dice_ups/summary.md

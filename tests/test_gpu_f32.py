@@ -212,28 +212,55 @@ def test_f32_pool_ups_head(cuda_dev, dims):
 ])
 def test_f32_native_step_matches_aten_fp32(cuda_dev, kw):
     """The whole fp32 training step (runtime/f32_engine.py: forward with dropout, Dice (+ BCE)
-    loss, backward) against the fp32 ATen step on the same batch and weights: loss sums
-    and every parameter gradient within fp32 summation-order noise."""
+    loss, backward) against the fp32 ATen step on the same batch and weights, both scored
+    against a float64 CPU oracle of the same step.  (MIOpen's fp32 3x3 algorithms include
+    Winograd transforms, ~1e-3 relative, so the GPU ATen step is no exact-fp32 oracle; and
+    two exact fp32 steps still differ where a pre-activation within rounding of zero flips a
+    ReLU mask -- ~1e-4 relative on a level's weight gradient at 128^2, more than the
+    summation order.)  Loss sums within 1e-5; every parameter gradient as close to float64
+    as the ATen fp32 CPU step's, up to 2x + 1e-4."""
     from test_gpu_model import _setup
+    from unet_distributed_amd.config import Config
+    from unet_distributed_amd.models import reference
+    from unet_distributed_amd.runtime.backends import TorchBackend
     from unet_distributed_amd.runtime.f32_engine import NativeUNetF32
+    from unet_distributed_amd.runtime.params import FlatParams
     spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, dtype="fp32", backend="native", **kw)
     assert isinstance(nb.engine, NativeUNetF32)
+    ft = FlatParams(spec)
+    ft.master.copy_(fn.master.cpu())
+    tb = TorchBackend(spec, ft, Config(**dict(kw, dtype="fp32")), "cpu", kw["batch_size"])
     nb.fwd_bwd(x, y, seed=17)
-    tb.fwd_bwd(x, y, seed=17)
+    tb.fwd_bwd(x.cpu(), y.cpu(), seed=17)
     torch.cuda.synchronize()
     assert rel(nb.sums().cpu(), tb.sums().cpu()) < 1e-5
+    # float64 oracle: same leaves, batch, dropout masks (hash of seed and layer, dtype-free)
+    names = [e[0] for e in ft.entries]
+    leaves = {n: ft.view(ft.master, n).double().requires_grad_(True) for n in names}
+    logits = reference.forward(spec, leaves, x.cpu().double(), train=True, dropout=True, seed=17, state={},
+                               return_logits=True)
+    t64 = y.cpu().double()
+    p64 = torch.sigmoid(logits)           # (ops/losses.py total_loss, without its fp32 casts)
+    loss = -torch.log(2 * (t64 * p64).sum() + 1) + torch.log(t64.sum() + p64.sum() + 1)
+    if cfg.loss == "dice_bce":
+        loss = loss + cfg.bce_weight * F.binary_cross_entropy_with_logits(logits, t64)
+    g64 = dict(zip(names, torch.autograd.grad(loss, [leaves[n] for n in names])))
     worst = 0.0
     for name, shape, off, n in fn.entries:
-        g, r = fn.grad[off:off + n], ft.grad[off:off + n]
-        e = rel(g, r)
-        worst = max(worst, e)
-        assert e < 2e-4, (name, e)
-    print("fp32 step worst per-tensor relative error %.2e" % worst)
-    # the Adam step (TF semantics, shared fused launch) keeps the replicas identical
+        g, r = fn.grad[off:off + n].cpu(), ft.grad[off:off + n]
+        o = g64[name].reshape(-1)
+        e_nat, e_aten = rel(g, o), rel(r, o)
+        worst = max(worst, e_nat)
+        assert e_nat < 2 * e_aten + 1e-4, (name, e_nat, e_aten)
+    print("fp32 step worst per-tensor relative error vs float64 %.2e" % worst)
+    # the fused TF-Adam launch on the fp32 master (no 16-bit repack) against the torch
+    # TF-Adam on the same gradient (Adam's first step is ~lr sign(g): gradients within
+    # rounding of zero would flip it, so both updates see the native gradient)
     from unet_distributed_amd.runtime.optim import TFAdam
     from unet_distributed_amd.runtime.trainer import _NativeOpt
+    ft.grad.copy_(fn.grad.cpu())
     opt_n, opt_t = TFAdam(fn, cfg, native=_NativeOpt(nb)), TFAdam(ft, cfg)
     opt_n.step()
     opt_t.step()
     torch.cuda.synchronize()
-    assert rel(fn.master, ft.master) < 1e-5
+    assert rel(fn.master.cpu(), ft.master) < 1e-6

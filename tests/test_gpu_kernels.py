@@ -793,7 +793,9 @@ def test_window_conv_reverse_order_same_result(cuda_dev, N, H, Cin, Cout, tile):
     for rev in (0, 1):
         y = torch.empty(N, H, H, Cout, device=cuda_dev, dtype=torch.bfloat16)
         bits = torch.zeros(N * H * H * Cout // 8, device=cuda_dev, dtype=torch.uint8)
-        pooled = torch.empty(N, H // 2, H // 2, Cout, device=cuda_dev, dtype=torch.bfloat16)
+        # (zero-filled: at H = 256 no pool is fused and these stay unwritten -- uninitialised
+        # memory of two allocations would differ)
+        pooled = torch.zeros(N, H // 2, H // 2, Cout, device=cuda_dev, dtype=torch.bfloat16)
         codes = torch.zeros(N * (H // 2) ** 2 * Cout // 8, device=cuda_dev, dtype=torch.int32)
         d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(x), wgt=ptr(wp), bias=ptr(b),
                  Cout=Cout, relu=1, dst1=ptr(y), relu_bits=ptr(bits), tile=tile, rev=rev)

@@ -164,7 +164,9 @@ def test_one_gpu_path_no_silent_aten_dispatch():
     assert resolve_backend("auto", spec_from_config(ok), ok, "cuda") == "native"
     assert resolve_backend("auto", spec_from_config(ok), ok, "cpu") == "torch"
     assert resolve_backend("torch", spec_from_config(ok), ok, "cuda") == "torch"
-    for bad, why in ((Config(dtype="fp32"), "dtype=fp32"), (Config(base_filters=48), "base filters")):
+    fp32 = Config(dtype="fp32", in_channels=4)          # the fp32 executor (runtime/f32_engine.py)
+    assert resolve_backend("auto", spec_from_config(fp32), fp32, "cuda") == "native"
+    for bad, why in ((Config(dtype="fp32", norm="batch"), "norm-free"), (Config(base_filters=48), "base filters")):
         spec = spec_from_config(bad)
         for want in ("auto", "native"):
             with pytest.raises(RuntimeError, match=why):

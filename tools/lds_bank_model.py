@@ -104,10 +104,38 @@ def check_tr(BM):
     return worst, wworst
 
 
+# ---------------------------------------------------------------- conv_win XF 5 u stores
+# tconv-on-load (conv_win.h ut_chunk): lane (fr = l & 15, fsub = l >> 4) holds u channels
+# 8 fsub .. + 7 of coarse pixel 16 pb + fr for both column phases tw; fine halo column
+# hc = 2 (16 pb + fr) + tw + 1, 64-byte slots, physical chunk fsub ^ ((hc >> 1) & 3).
+def check_ut_store():
+    """(ways of the old 8-byte per-tile stores, ways of one phase per 16-byte store,
+    ways of the phase-interleaved 16-byte stores)."""
+    def a16(fr, fsub, tw, pb):
+        hc = 2 * (16 * pb + fr) + tw + 1
+        return hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3))
+    old = one = inter = 1
+    for pb in range(4):
+        for tw in range(2):
+            for j in range(2):        # old: chunk 2 j + (fsub >> 1), half fsub & 1
+                addrs = []
+                for l in range(64):
+                    fr, fsub = l & 15, l >> 4
+                    hc = 2 * (16 * pb + fr) + tw + 1
+                    ch = 2 * j + (fsub >> 1)
+                    addrs.append(hc * 64 + 16 * (ch ^ ((hc >> 1) & 3)) + 8 * (fsub & 1))
+                old = max(old, write_b64(addrs))
+            one = max(one, write_b128([a16(l & 15, l >> 4, tw, pb) for l in range(64)]))
+        for s in range(2):
+            inter = max(inter, write_b128([a16(l & 15, l >> 4, s ^ (((l & 15) >> 2) & 1), pb) for l in range(64)]))
+    return old, one, inter
+
+
 if __name__ == "__main__":
     print("fwd b128 read/write worst ways:", check_fwd())
     for BM in (32, 64, 128, 256):
         print("tr BM=%d read/write ways:" % BM, check_tr(BM))
+    print("XF 5 u stores (old b64, one-phase b128, interleaved b128) ways:", check_ut_store())
 
 
 # ---------------------------------------------------------------- 128-byte rows (BK = 64)

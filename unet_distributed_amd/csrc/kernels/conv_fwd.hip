@@ -436,7 +436,14 @@ hipError_t launch_img8(const ConvFwdParams& p, hipStream_t s) {
 constexpr int FWPW = 8;
 template <int W, int CIN, int EPI>
 __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) conv_win_first_kernel(const ConvFwdParams p) {
-  constexpr int BM = 512, R = BM / W, HR = R + 2, RS = W + 4;   // row pitch in slots
+  // Row pitch in slots.  CIN 4 (8-byte slots): a half-wave's two 16-lane groups read 128
+  // consecutive bytes each, at taps whose slots differ by Delta; they share no bank iff
+  // 8 Delta == 128 (mod 256).  With the pitch == 16 (mod 32) slots and the K order below
+  // pairing vertically adjacent taps (Delta = RS) in every half-wave, the halo reads are
+  // conflict-free (round 4: W + 4 = 132 slots and taps t, t + 2 paired -- 34.6 % of the
+  // kernel's LDS cycles were bank conflicts, r4_pmc_table.md).
+  constexpr int BM = 512, R = BM / W, HR = R + 2;
+  constexpr int RS = CIN == 4 ? ((W + 4 + 15) / 32) * 32 + 16 : W + 4;
   constexpr int SB = 2 * CIN;                                  // slot bytes
   constexpr int ROWB = RS * SB;
   constexpr int CPR = ROWB / 16;                               // 16-byte chunks per halo row
@@ -486,7 +493,14 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) 
       if (u < NCH) *(u32x4*)(Xs + u * 16) = hv[c];
     }
   };
-  // weight fragments (B operand: k = 32 s + 8 (lane >> 4) .. + 7, n = lane & 15), from global
+  // weight fragments (A operand: k = 32 s + 8 (lane >> 4) .. + 7, m = lane & 15), from global.
+  // CIN 4: k slot i = 8 s + 2 (lane >> 4) + hh holds tap KPERM[i] (4 bits each; 9..15 are
+  // zero taps): the half-wave pairs (KPERM[i], KPERM[i + 2]) are the vertical neighbours
+  // (0, 3), (1, 4), (2, 5), then 6, 7, 8 with zero taps -- see RS above.  A zero tap (zero
+  // weights) reads its partner's slots + 16 (the other half of the banks) instead of the
+  // broadcast zero slot, which would share banks with the partner's 128 bytes.
+  constexpr unsigned long long KPERM = 0xFEDCBA87'95624310ull;
+  auto ktap = [](const int i) -> int { return CIN == 4 ? (int)((KPERM >> (4 * i)) & 15ull) : i; };
   const int fsub = lane >> 4, fr = lane & 15;
   h16x8 wf[KS][TN];
   auto load_w = [&](const int n0) {
@@ -494,9 +508,23 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) 
     for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
-            rsw, ((n0 + 16 * j + fr) * p.Kpad + 32 * s + 8 * fsub) * 2, 0, 0);
-        wf[s][j] = __builtin_bit_cast(h16x8, v);
+        if constexpr (CIN == 4) {
+          u32x4 v;
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int t = ktap(8 * s + 2 * fsub + hh);
+            const u32x2 h2 = __builtin_bit_cast(
+                u32x2, __builtin_amdgcn_raw_buffer_load_b64(rsw, t < 9 ? ((n0 + 16 * j + fr) * p.Kpad + 4 * t) * 2 : OOB,
+                                                            0, 0));
+            v[2 * hh] = h2[0];
+            v[2 * hh + 1] = h2[1];
+          }
+          wf[s][j] = __builtin_bit_cast(h16x8, v);
+        } else {
+          const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+              rsw, ((n0 + 16 * j + fr) * p.Kpad + 32 * s + 8 * fsub) * 2, 0, 0);
+          wf[s][j] = __builtin_bit_cast(h16x8, v);
+        }
       }
   };
   if (w_lo >= w_hi) return;
@@ -536,10 +564,12 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) 
         if constexpr (CIN == 4) {
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
-            const int t = 8 * s + 2 * fsub + hh;            // tap of this 4-channel half
+            int t = ktap(8 * s + 2 * fsub + hh);            // tap of this 4-channel half
+            const bool zt = t >= 9;                         // zero tap: the partner's tap, other banks
+            if (zt) t = ktap(8 * s + 2 * (fsub ^ 1) + hh);
             const int dh = t / 3, dw = t - 3 * dh;
             const bool ok = t < 9 && (dh != 0 || tok) && (dh != 2 || bok);
-            const int slot = (rr + dh) * RS + cw + dw + 1;
+            const int slot = ((rr + dh) * RS + cw + dw + 1) ^ (zt ? 16 : 0);
             const u32x2 h2 = *(const u32x2*)(Xs + (ok ? slot * SB : 0));
             v[2 * hh] = h2[0];
             v[2 * hh + 1] = h2[1];
@@ -693,7 +723,11 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
       u32x2 pk;
       pk[0] = pack2h(acc[i][j][0] + bs[0], acc[i][j][1] + bs[1]);
       pk[1] = pack2h(acc[i][j][2] + bs[2], acc[i][j][3] + bs[3]);
-      *(u32x2*)(E + fp * FST + nl * 2) = pk;
+      // 8-byte half of the 16-byte chunk swapped on bit 4 of the fine pixel: the 16 lanes
+      // of a store group hold fine pixels 2 apart (72-byte rows: 144 B apart), so lanes
+      // fr and fr + 8 hit the same banks unless their halves differ (2-way -> conflict
+      // free for rows of 16+ coarse pixels, tools/lds_bank_model.py)
+      *(u32x2*)(E + fp * FST + (nl >> 3) * 16 + 8 * (((nl >> 2) & 1) ^ ((fp >> 4) & 1))) = pk;
     }
   }
   __syncthreads();
@@ -706,8 +740,9 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
     const int fp = c >> 2, q = c & 3;
     const size_t gp = fine0 + fp;
     if (gp >= fine_total) continue;
-    const u32x2 lo = *(const u32x2*)(E + fp * FST + q * 16);
-    const u32x2 hi = *(const u32x2*)(E + fp * FST + q * 16 + 8);
+    const int hs = 8 * ((fp >> 4) & 1);
+    const u32x2 lo = *(const u32x2*)(E + fp * FST + q * 16 + hs);
+    const u32x2 hi = *(const u32x2*)(E + fp * FST + q * 16 + (8 - hs));
     const u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
     *(u32x4*)((h16*)p.dst1 + gp * cof + n0 + q * 8) = v;
   }

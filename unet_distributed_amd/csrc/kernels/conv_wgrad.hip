@@ -900,7 +900,13 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
 // past the ninth and taps whose input row leaves the pixel's image address slot 0.
 template <int W, int CIN, bool XF = false>
 __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams p) {
-  constexpr int BMW = 256, R = BMW / W, HR = R + 2, RS = W + 4, SB = 2 * CIN, ROWB = RS * SB;
+  // Row pitch in slots: CIN 4 (8-byte slots) pads it to == 16 (mod 32) -- the four taps of
+  // an A fragment (4 mt .. 4 mt + 3) then read slot sets that never share banks (a vertical
+  // neighbour RS slots on lands 64 bytes x 2 away from the row's own slots), and GEMM rows
+  // past the ninth tap (discarded) read 16 slots on instead of the broadcast zero slot
+  // (round 4: W + 4 = 132 -- 37.5 % of the kernel's LDS cycles were conflicts).
+  constexpr int BMW = 256, R = BMW / W, HR = R + 2, SB = 2 * CIN;
+  constexpr int RS = CIN == 4 ? ((W + 4 + 15) / 32) * 32 + 16 : W + 4, ROWB = RS * SB;
   constexpr int CPR = ROWB / 16;
   constexpr int XI = (HR * CPR + 63) / 64, YI = BMW / 16;
   constexpr int XB = XI * 1024, YB = YI * 1024;
@@ -1053,7 +1059,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           const bool ok = t < 9 && !(dh == 0 && hlp[hh] == 0) && !(dh == 2 && hlp[hh] == H - 1);
-          a[hh] = ok ? (slotp[hh] + dh * RS + dw) * SB + chb : 0;
+          a[hh] = ok ? (slotp[hh] + dh * RS + dw) * SB + chb : (t >= 9 && CIN == 4 ? (slotp[hh] + 16) * SB : 0);
         }
         const h16x8 af = tr8(Xs + a[0], Xs + a[1]);
 #pragma unroll

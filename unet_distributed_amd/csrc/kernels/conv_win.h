@@ -324,25 +324,27 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
       constexpr int CW = W / 2, PB = XF == 5 ? CW / 16 : 1, NCR = R / 2 + 2;
       static_assert(XF != 5 || (R % 2 == 0 && CW % 16 == 0), "tconv on load: even window rows, coarse rows 16k wide");
       if constexpr (PB * KS <= 8) {               // (conv_fwd_prepare: (W / 32) (C / 32) <= 8)
-        constexpr int NAB = KS <= 2 ? 2 : 1;      // tap weight buffers (two: next tap prefetched)
         const int Cc = KS * 32;
-        const h16* wt = (const h16*)p.ut.w + (size_t)(cb + fr) * p.ut.kpad + 8 * fsub;
+        // A rows permuted so that a lane's two 16 x 16 tiles hold 8 consecutive u channels:
+        // tile j row fr = channel 8 (fr >> 2) + 4 j + (fr & 3), so output rows 4 fsub + i of
+        // tile j are channels 8 fsub + 4 j + i -- logical 16-byte chunk fsub of the pixel,
+        // one 16-byte store.  (Each output element keeps its operands and accumulation
+        // order: still bit-identical to tconv_fwd_kernel.)
+        const h16* wt = (const h16*)p.ut.w + (size_t)(cb + 8 * (fr >> 2) + (fr & 3)) * p.ut.kpad + 8 * fsub;
         // the window's image in the coarse tensor (H even: fine row g -> coarse row g / 2)
         const h16* ub = (const h16*)p.ut.x + (size_t)(grow0 >> 1) * CW * Cc + (size_t)fr * Cc + 8 * fsub;
-        float bs[2][4];
+        float bs[8];
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) bs[j][i] = p.ut.b[cb + 16 * j + 4 * fsub + i];
+        for (int i = 0; i < 8; ++i) bs[i] = p.ut.b[cb + 8 * fsub + i];
         h16x8 xb[PB][KS];
-        h16x8 wa[NAB][2][KS];
-        auto load_a = [&](const int t, h16x8 (&dst)[2][KS]) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
-              dst[j][ks] = *(const h16x8*)(wt + (size_t)(t * p.C1 + 16 * j) * p.ut.kpad + 32 * ks);
-        };
+        h16x8 wa[2][2][KS];                       // [tw][j][ks]: both column phases of a tap row
+        // store roles: in store s, lane fr writes column phase tw = s ^ ((fr >> 2) & 1).  The 8
+        // lanes of a 16-byte store group (fr 0-3 / 4-7 of one fsub) then cover both 64-byte
+        // halves of the 32-bank window (fine column parity) and all four swizzles
+        // (column >> 1) & 3: conflict-free (tools/lds_bank_model.py check_ut_store).  With
+        // one phase per store only 4 of the 8 slots are reachable (2-way); the previous
+        // 8-byte per-tile stores were 4-way conflicted (35 % conflict cycles, r5 PMC).
+        const int tsel = (fr >> 2) & 1;
         for (int cq = wave; cq < NCR; cq += 4) {
           // fine halo rows hr = 2 cq - 1 + th of this coarse row; in the image <=> the
           // coarse row is (window rows never leave their image, conv_fwd_prepare)
@@ -357,37 +359,46 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
 #pragma unroll
               for (int ks = 0; ks < KS; ++ks) xb[pb][ks] = *(const h16x8*)(rp + (size_t)(16 * pb) * Cc + 32 * ks);
           }
-          const int t_lo = cq == 0 ? 2 : 0, t_hi = cq == NCR - 1 ? 2 : 4;   // taps whose rows are halo rows
-          if (in) load_a(t_lo, wa[0]);
+          const int th_lo = cq == 0 ? 1 : 0, th_hi = cq == NCR - 1 ? 1 : 2;   // tap rows inside the halo
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            if (t < t_lo || t >= t_hi) continue;
-            const int ab = NAB == 2 ? (t - t_lo) & 1 : 0;
-            if constexpr (NAB == 2) {
-              if (in && t + 1 < t_hi) load_a(t + 1, wa[ab ^ 1]);
-            } else if (in && t > t_lo) {
-              load_a(t, wa[0]);
+          for (int th = 0; th < 2; ++th) {
+            if (th < th_lo || th >= th_hi) continue;
+            if (in) {
+#pragma unroll
+              for (int tw = 0; tw < 2; ++tw)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                  for (int ks = 0; ks < KS; ++ks)
+                    wa[tw][j][ks] = *(const h16x8*)(wt + (size_t)((2 * th + tw) * p.C1 + 4 * j) * p.ut.kpad + 32 * ks);
             }
-            const int th = t >> 1, tw = t & 1;
             char* xrow = Xs + (2 * cq - 1 + th) * ROWB;
 #pragma unroll
             for (int pb = 0; pb < PB; ++pb) {
-              const int hc = 2 * (16 * pb + fr) + tw + 1;
+              u32x4 pk[2] = {(u32x4){0u, 0u, 0u, 0u}, (u32x4){0u, 0u, 0u, 0u}};
+              if (in) {
 #pragma unroll
-              for (int j = 0; j < 2; ++j) {
-                u32x2 pk = {0u, 0u};
-                if (in) {
-                  f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+                for (int tw = 0; tw < 2; ++tw)
 #pragma unroll
-                  for (int ks = 0; ks < KS; ++ks) a = mfma16(wa[ab][j][ks], xb[pb][ks], a);
-                  pk[0] = pack2h(a[0] + bs[j][0], a[1] + bs[j][1]);
-                  pk[1] = pack2h(a[2] + bs[j][2], a[3] + bs[j][3]);
-                }
-                const int ch = 2 * j + (fsub >> 1);
-                *(u32x2*)(xrow + hc * 64 + 16 * (ch ^ ((hc >> 1) & 3)) + 8 * (fsub & 1)) = pk;
+                  for (int j = 0; j < 2; ++j) {
+                    // (packed at once: one live accumulator keeps the W = 128 instance at
+                    // 191 VGPRs + 64 AGPRs, two waves per SIMD; both tiles live -> 260)
+                    f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int ks = 0; ks < KS; ++ks) a = mfma16(wa[tw][j][ks], xb[pb][ks], a);
+                    pk[tw][2 * j] = pack2h(a[0] + bs[4 * j], a[1] + bs[4 * j + 1]);
+                    pk[tw][2 * j + 1] = pack2h(a[2] + bs[4 * j + 2], a[3] + bs[4 * j + 3]);
+                  }
+              }
+#pragma unroll
+              for (int s = 0; s < 2; ++s) {
+                const int tw = s ^ tsel;
+                const int hc = 2 * (16 * pb + fr) + tw + 1;
+                *(u32x4*)(xrow + hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3))) = tw ? pk[1] : pk[0];
               }
             }
-            if (lane < 4) *(u32x4*)(xrow + (tw ? W + 1 : 0) * 64 + 16 * lane) = (u32x4){0u, 0u, 0u, 0u};
+            // halo columns 0 and W + 1 of the row (lanes 0-3 / 4-7: one 16-byte chunk each)
+            if (lane < 8) *(u32x4*)(xrow + ((lane >> 2) ? W + 1 : 0) * 64 + 16 * (lane & 3)) = (u32x4){0u, 0u, 0u, 0u};
           }
         }
       }
@@ -494,16 +505,14 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
             }
             ck[k] = pack8(o);
           }
-          // store order rotated by (slot / 2) mod 4: consecutive lanes' slots are 64 B
-          // apart, so in one order lanes t and t + 4 hit the same banks; rotated, the 8
-          // lanes of a store group write 8 different 16-byte bank groups
-          const int rot = (sl >> 1) & 3;
+          // logical chunk k in store k: the 8 lanes of a store group hold 8 consecutive
+          // slots whose swizzle sw = (column >> 1) & 3 takes each value twice (once per
+          // slot parity), so the physical chunks k ^ sw land in 8 different 16-byte bank
+          // groups (tools/lds_bank_model.py).  (Round 4 rotated the order by (slot >> 1) & 3
+          // as the wgrad's head-on-load B does -- under THIS swizzle the rotation cancels
+          // it, k + r ^ r, and every store was 4-way conflicted: 39.8 % conflict cycles.)
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int kk = (k + rot) & 3;
-            const u32x4 w = kk == 0 ? ck[0] : (kk == 1 ? ck[1] : (kk == 2 ? ck[2] : ck[3]));
-            *(u32x4*)(Xs + sl * 64 + 16 * (kk ^ sw)) = w;
-          }
+          for (int k = 0; k < 4; ++k) *(u32x4*)(Xs + sl * 64 + 16 * (k ^ sw)) = ck[k];
         }
       }
       __syncthreads();

@@ -1553,7 +1553,8 @@ class NativeUNet:
                     # only the slab reduction is planned here
                     w["slab_ptrs"] = (slab, bslab)
                 else:
-                    plan.add_wgrad(d)
+                    self._add_wgrad_chunked(plan, d, taps * Mtot * w["Nc"],
+                                            (w["bias_width"] if w["bias_mode"] == 1 else Mtot) * tg)
                 if part == 0:
                     continue                       # the reductions follow the last part
                 KT = w["KT"]
@@ -1598,6 +1599,38 @@ class NativeUNet:
                     if sf is not None:
                         self._layer_done_at[tf["consumer"]] = plan.size()
         flush()
+
+    def _add_wgrad_chunked(self, plan, d, row_floats, brow_floats):
+        """plan.add_wgrad(d); a tiled (non-window) weight gradient whose operand tensors
+        exceed the 2 GiB reach of one 32-bit buffer base (3D 128^3 at 16 volumes, 512^2 at 128
+        images: the first layer's) runs as batch chunks instead -- chunk k takes images
+        [k N / c, (k + 1) N / c) and slab rows [k S / c, (k + 1) S / c) of the same slabs, so
+        the fixed-order reduction is unchanged."""
+        try:
+            return plan.add_wgrad(d)
+        except ValueError as ex:
+            if "2 GiB" not in str(ex) or d.get("xform") or d.get("hg_prob") or d.get("split_n") or d.get("upA", 1) != 1:
+                raise
+        N, S = d["N"], d["splits"]
+        a_img = d.get("AD", 1) * d.get("AH", 1) * d.get("AW", 1) * 2
+        b_img = d.get("QD", 1) * d.get("QH", 1) * d.get("QW", 1) * d["Nc"] * 2
+        lim = (1 << 31) - 64
+        per = max(a_img * max(d["M1"], d.get("M2") or 0), b_img)
+        c = 2
+        while (N + c - 1) // c * per >= lim:
+            c += 1
+        if c > min(N, S):
+            raise ValueError("wgrad: cannot chunk the batch under the 2 GiB buffer reach")
+        for k in range(c):
+            n0, n1 = k * N // c, (k + 1) * N // c
+            s0, s1 = k * S // c, (k + 1) * S // c
+            dk = dict(d, N=n1 - n0, splits=s1 - s0, a1=d["a1"] + n0 * a_img * d["M1"],
+                      b=d["b"] + n0 * b_img, slab=d["slab"] + 4 * s0 * row_floats)
+            if d.get("a2"):
+                dk["a2"] = d["a2"] + n0 * a_img * d["M2"]
+            if d.get("bias_mode"):
+                dk["bias_slab"] = d["bias_slab"] + 4 * s0 * brow_floats
+            plan.add_wgrad(dk)
 
     # ------------------------------------------------------------------ buckets
     def set_buckets(self, bounds: Optional[Sequence[int]]):
