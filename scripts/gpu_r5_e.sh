@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 5 check E: XF 5 (tconv on load) conflict-free u stores, the float64-oracle fp32
+# Round 5 check E: the GPU suite after the XF 5 (tconv on load) u-store and epilogue-staging
+# conflict fixes, the float64-oracle fp32
 # step test, headline bench + profile, per-launch times of the 512^2 and 3D configs
 # (limiting kernels), and the upsampling-decoder Dice seeds 2-3.
 set -o pipefail
@@ -8,10 +9,7 @@ o=gpurun_out/r5e; mkdir -p $o
 ( while sleep 50; do date >> gpurun_out/heartbeat.txt; done ) &
 hb=$!
 trap "kill $hb 2>/dev/null" EXIT
-timeout -k 10 600 python -u -m pytest tests/test_gpu_tconv_fused.py tests/test_gpu_f32.py \
-  "tests/test_gpu_kernels.py::test_window_conv_reverse_order_same_result" \
-  "tests/test_gpu_model.py::test_tconv_fused_step_matches_materialised" -q -s --timeout 300 \
-  --timeout-method thread > $o/tests.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -s --timeout 300 --timeout-method thread > $o/tests.log 2>&1; rc=$?
 grep -E "passed|failed|worst" $o/tests.log | tail -8
 [ $rc -gt 1 ] && { echo "tests crashed rc=$rc"; tail -30 $o/tests.log; exit 1; }
 [ $rc -eq 1 ] && grep -E "^FAILED|Error" $o/tests.log | head -20

@@ -251,8 +251,18 @@ def test_f32_native_step_matches_aten_fp32(cuda_dev, kw):
         o = g64[name].reshape(-1)
         e_nat, e_aten = rel(g, o), rel(r, o)
         worst = max(worst, e_nat)
-        assert e_nat < 2 * e_aten + 1e-4, (name, e_nat, e_aten)
-    print("fp32 step worst per-tensor relative error vs float64 %.2e" % worst)
+        # (+5e-4: a bias gradient is a sum over every pixel with heavy cancellation, so one
+        # ReLU flip near zero moves its max-norm error by up to ~1e-4 -- observed 1.3e-4 on
+        # conv8a/bias at 3 x 128^2, where the CPU step happened to flip none)
+        assert e_nat < 2 * e_aten + 5e-4, (name, e_nat, e_aten)
+    g64_all = torch.cat([g64[e[0]].reshape(-1) for e in fn.entries])
+
+    def l2(a):
+        return ((a.double() - g64_all).norm() / g64_all.norm()).item()
+    e_all, e_all_aten = l2(fn.grad.cpu()), l2(ft.grad)
+    print("fp32 step vs float64: worst per-tensor %.2e, all gradients L2 %.2e (ATen fp32 CPU %.2e)"
+          % (worst, e_all, e_all_aten))
+    assert e_all < 2 * e_all_aten + 1e-5
     # the fused TF-Adam launch on the fp32 master (no 16-bit repack) against the torch
     # TF-Adam on the same gradient (Adam's first step is ~lr sign(g): gradients within
     # rounding of zero would flip it, so both updates see the native gradient)

@@ -131,10 +131,89 @@ def check_ut_store():
     return old, one, inter
 
 
+# ---------------------------------------------------------------- conv epilogue staging (BN = 32)
+# conv_epilogue.h: 64-byte pixel rows, chunk c of pixel ml at c ^ ((ml >> 2) & 3); the
+# register phase writes 8-byte halves (lane: pixel base + (l & 15), channels 16 j + 4 (l >> 4)),
+# the coalesced phase reads 16-byte chunks (thread t: pixel t >> 2, chunk t & 3).
+def check_epi(half_swap=True):
+    """(write ways, read ways) of the staging tile."""
+    def eoff(ml, ch):
+        return ml * 64 + 16 * (ch ^ ((ml >> 2) & 3))
+    w = r = 1
+    for base in range(0, 512, 16):
+        for j in range(2):
+            addrs = []
+            for l in range(64):
+                ml, nl = base + (l & 15), 16 * j + 4 * (l >> 4)
+                h = (2 * (nl & 7)) ^ (8 * ((ml >> 1) & 1) if half_swap else 0)
+                addrs.append(eoff(ml, nl >> 3) + h)
+            w = max(w, write_b64(addrs))
+    for base in range(0, 2048, 64):
+        r = max(r, read_b128([eoff((base + l) >> 2, (base + l) & 3) for l in range(64)]))
+    return w, r
+
+
+# ---------------------------------------------------------------- generic wgrad_kernel stores
+# conv_wgrad.hip wgrad_kernel: 4 threads per pixel row k (tid >> 2), thread's chunk group c
+# (chunks sub + 4 c of the row) -> [k][W] transposed-read image; SWP: odd rows take c ^ 1.
+def check_wgrad_store(W, swap=True):
+    worst = 1
+    for wave in range(4):
+        for c in range(W // 32):
+            addrs = []
+            for l in range(64):
+                tid = 64 * wave + l
+                k, sub = tid >> 2, tid & 3
+                cc = c ^ (k & 1) if swap else c
+                addrs.append(tr_addr(k, 8 * (sub + 4 * cc), W))
+            worst = max(worst, write_b128(addrs))
+    return worst
+
+
+# ---------------------------------------------------------------- tconv_fwd epilogue staging
+# conv_fwd.hip tconv_fwd_kernel: register phase, wave = tap (th, tw), lane: coarse pixel
+# 16 i + (l & 15) -> fine pixel fp (2 apart along a fine row), 8-byte half h of chunk c of
+# channels 16 j + 4 (l >> 4); coalesced phase: thread t -> fine pixel t >> 2, chunk t & 3.
+# 64-byte rows: fine pixel fp in row fp ^ ((fp >> 1) & 1), chunk c ^ ((fp >> 2) & 3), half
+# h ^ ((fp >> 4) ^ (fp >> 5)) & 1; `padded`: the previous 72-byte rows (half ^ (fp >> 4) & 1).
+def check_tconv_epi(W, padded=False):
+    def off(fp, c, h):
+        if padded:
+            return fp * 72 + 16 * c + 8 * (h ^ ((fp >> 4) & 1))
+        return (fp ^ ((fp >> 1) & 1)) * 64 + 16 * (c ^ ((fp >> 2) & 3)) + 8 * (h ^ (((fp >> 4) ^ (fp >> 5)) & 1))
+    w = 1
+    for wave in range(4):
+        th, tw = wave >> 1, wave & 1
+        for i in range(8):
+            for j in range(2):
+                addrs = []
+                for l in range(64):
+                    pl = 16 * i + (l & 15)
+                    rr, x = divmod(pl, W)
+                    fp = (2 * rr + th) * (2 * W) + 2 * x + tw
+                    nl = 16 * j + 4 * (l >> 4)
+                    addrs.append(off(fp, nl >> 3, (nl >> 2) & 1))
+                w = max(w, write_b64(addrs))
+    r = 1
+    for base in range(0, 2048, 64):
+        if padded:      # two 8-byte reads per chunk (72-byte rows are not 16-byte aligned)
+            for hh in range(2):
+                addrs = [off((base + l) >> 2, (base + l) & 3, hh) for l in range(64)]
+                r = max(r, ways(addrs, 8, HALVES, 64))
+        else:
+            r = max(r, read_b128([off((base + l) >> 2, (base + l) & 3, 0) for l in range(64)]))
+    return w, r
+
+
 if __name__ == "__main__":
     print("fwd b128 read/write worst ways:", check_fwd())
     for BM in (32, 64, 128, 256):
         print("tr BM=%d read/write ways:" % BM, check_tr(BM))
+    print("epilogue staging (write, read) ways, half swap / none:", check_epi(), check_epi(False))
+    print("wgrad_kernel stores W=64/128/256 (swap, none):",
+          [(check_wgrad_store(w), check_wgrad_store(w, False)) for w in (64, 128, 256)])
+    print("tconv_fwd staging W=8..64 (new, padded):",
+          [(check_tconv_epi(w), check_tconv_epi(w, True)) for w in (8, 16, 32, 64)])
     print("XF 5 u stores (old b64, one-phase b128, interleaved b128) ways:", check_ut_store())
 
 

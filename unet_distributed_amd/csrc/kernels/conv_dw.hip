@@ -252,12 +252,11 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
   const int n_base = lane & 15, m_base = 4 * (lane >> 4);
   auto reduce_store = [&](const f32x4 (&v4)[2][2], const int t) {
     __syncthreads();
-    if (wave > 0) {
-      float* dst = red + (wave * 64 + lane) * 16;
+    if (wave > 0) {     // red[fragment][wave * 64 + lane]: lanes 16 bytes apart, conflict-free
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) *(f32x4*)(dst + (i * 2 + j) * 4) = v4[i][j];
+        for (int j = 0; j < 2; ++j) *(f32x4*)(red + ((i * 2 + j) * 256 + wave * 64 + lane) * 4) = v4[i][j];
     }
     __syncthreads();
     if (wave == 0) {
@@ -267,7 +266,7 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
         for (int j = 0; j < 2; ++j) {
           f32x4 v = v4[i][j];
 #pragma unroll
-          for (int o = 1; o < 4; ++o) v += *(const f32x4*)(red + (o * 64 + lane) * 16 + (i * 2 + j) * 4);
+          for (int o = 1; o < 4; ++o) v += *(const f32x4*)(red + ((i * 2 + j) * 256 + o * 64 + lane) * 4);
           if (t < 9) {
             float* dst = p.fw.slab + (((size_t)row * 9 + t) * Cx + m_base + 16 * i) * C + n_base + 16 * j;
 #pragma unroll

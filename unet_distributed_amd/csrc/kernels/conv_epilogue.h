@@ -98,19 +98,28 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     else return m0 + ml;
   };
   // Staging tile rows (pixels).  BN = 32: unpadded 64-byte rows, 16-byte chunk c of pixel ml
-  // at c ^ ((ml >> 2) & 3) -- conflict-free for the register phase's 8-byte writes (16
-  // pixels x 2 halves of one chunk per 32 lanes) and for the 16-byte chunk reads of the
-  // coalesced phase (4 lanes per pixel); the padded 72-byte rows it replaces left 2-way
-  // conflicts in both (15-23 % LDS conflict cycles on the level-1 windows, r3_pmc_table.md).
+  // at c ^ ((ml >> 2) & 3), its two 8-byte halves swapped when (ml >> 1) & 1.  The register
+  // phase's 8-byte writes go 16 lanes at a time over 32 banks (16 consecutive pixels, one
+  // half of one chunk): pixel parity picks the 64-byte half of the bank window, (ml >> 2) & 3
+  // the chunk, (ml >> 1) & 1 the half -- 16 distinct slots, conflict-free.  Without the half
+  // swap only 8 slots are reachable (2-way: 17-18 % conflict cycles on the level-1 windows,
+  // r5 PMC pass; tools/lds_bank_model.py check_epi).  The coalesced phase's 16-byte chunk
+  // reads (4 lanes per pixel) are unaffected and swap the halves back in registers.
   // Wider tiles: rows padded by 8 bytes.
   constexpr bool ESWZ = BN == 32;
   constexpr int EPI_STRIDE = ESWZ ? 64 : (BN + 4) * 2;
   auto eoff = [](const int ml, const int chunk) -> int {
     return ESWZ ? ml * 64 + 16 * (chunk ^ ((ml >> 2) & 3)) : ml * EPI_STRIDE + 16 * chunk;
   };
+  // byte offset of the 8-byte half of channels nl .. nl + 3 (nl % 4 == 0) of pixel ml
+  auto ehalf = [](const int ml, const int nl) -> int {
+    return ESWZ ? ml * 64 + 16 * ((nl >> 3) ^ ((ml >> 2) & 3)) + ((2 * (nl & 7)) ^ (8 * ((ml >> 1) & 1)))
+                : ml * EPI_STRIDE + 2 * nl;
+  };
   auto eread = [&](const int ml, const int chunk) -> u32x4 {
     if constexpr (ESWZ) {
-      return *(const u32x4*)(smem + eoff(ml, chunk));
+      const u32x4 v = *(const u32x4*)(smem + eoff(ml, chunk));
+      return ((ml >> 1) & 1) ? (u32x4){v[2], v[3], v[0], v[1]} : v;
     } else {
       const u32x2 lo = *(const u32x2*)(smem + eoff(ml, chunk));
       const u32x2 hi = *(const u32x2*)(smem + eoff(ml, chunk) + 8);
@@ -155,7 +164,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
         u32x2 pk;
         pk[0] = relu2h(pack2h(a01[0], a01[1]));
         pk[1] = relu2h(pack2h(a23[0], a23[1]));
-        *(u32x2*)(E + eoff(ml, nl >> 3) + 2 * (nl & 7)) = pk;
+        *(u32x2*)(E + ehalf(ml, nl)) = pk;
       }
       continue;
     }
@@ -178,7 +187,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       u32x2 pk;
       pk[0] = pack2h(v[0], v[1]);
       pk[1] = pack2h(v[2], v[3]);
-      *(u32x2*)(E + eoff(ml, nl >> 3) + 2 * (nl & 7)) = pk;
+      *(u32x2*)(E + ehalf(ml, nl)) = pk;
     }
   }
   __syncthreads();

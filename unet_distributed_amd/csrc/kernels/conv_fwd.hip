@@ -640,8 +640,7 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
   constexpr int BMc = 128, R = BMc / W;
   constexpr int XI = BMc / 16, WI = 4 * 32 / 16;   // 1 KB DMA instructions per chunk
   constexpr int XB = XI * 1024, WB = WI * 1024;
-  constexpr int FST = 32 * 2 + 8;                   // fine staging row stride (bytes)
-  constexpr int EPIB = 4 * BMc * FST;
+  constexpr int EPIB = 4 * BMc * 64;                // fine staging: 64-byte pixel rows
   constexpr int LDS_BYTES = (XB + WB > EPIB) ? XB + WB : EPIB;
   constexpr int TM = BMc / 16, TN = 2;
   static_assert(BMc % W == 0 && W >= 8 && W <= 128, "tconv window");
@@ -707,7 +706,17 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
   }
   __syncthreads();
   // register phase: acc[i][j][r] = out(coarse px 16i + (lane&15), tap = wave)[co = 16j + 4(lane>>4) + r]
+  // Staging: fine pixel fp in 64-byte row fp ^ ((fp >> 1) & 1), 16-byte chunk c at
+  // c ^ ((fp >> 2) & 3), its 8-byte halves swapped when ((fp >> 4) ^ (fp >> 5)) & 1.  A
+  // register-phase store group (16 lanes, fine pixels 2 apart: fp bits 1-4 = the lane, bit 0
+  // the tap column, fixed) then maps its lanes one-to-one onto the 16 8-byte slots of the 32
+  // banks (row parity x chunk x half), and the coalesced phase's 16-byte reads of 4
+  // consecutive pixels fill 4 distinct 64-byte bank segments: both conflict-free
+  // (tools/lds_bank_model.py check_tconv_epi).  The 72-byte padded rows this replaces needed
+  // two 8-byte reads per chunk, 2-way conflicted (30.8 % conflict cycles, r5 PMC pass).
   char* E = smem;
+  auto tc_off = [](const int fp, const int c) { return (fp ^ ((fp >> 1) & 1)) * 64 + 16 * (c ^ ((fp >> 2) & 3)); };
+  auto tc_half = [](const int fp) { return ((fp >> 4) ^ (fp >> 5)) & 1; };
   const int th = wave >> 1, tw = wave & 1;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -723,11 +732,7 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
       u32x2 pk;
       pk[0] = pack2h(acc[i][j][0] + bs[0], acc[i][j][1] + bs[1]);
       pk[1] = pack2h(acc[i][j][2] + bs[2], acc[i][j][3] + bs[3]);
-      // 8-byte half of the 16-byte chunk swapped on bit 4 of the fine pixel: the 16 lanes
-      // of a store group hold fine pixels 2 apart (72-byte rows: 144 B apart), so lanes
-      // fr and fr + 8 hit the same banks unless their halves differ (2-way -> conflict
-      // free for rows of 16+ coarse pixels, tools/lds_bank_model.py)
-      *(u32x2*)(E + fp * FST + (nl >> 3) * 16 + 8 * (((nl >> 2) & 1) ^ ((fp >> 4) & 1))) = pk;
+      *(u32x2*)(E + tc_off(fp, nl >> 3) + 8 * (((nl >> 2) & 1) ^ tc_half(fp))) = pk;
     }
   }
   __syncthreads();
@@ -740,10 +745,8 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
     const int fp = c >> 2, q = c & 3;
     const size_t gp = fine0 + fp;
     if (gp >= fine_total) continue;
-    const int hs = 8 * ((fp >> 4) & 1);
-    const u32x2 lo = *(const u32x2*)(E + fp * FST + q * 16 + hs);
-    const u32x2 hi = *(const u32x2*)(E + fp * FST + q * 16 + (8 - hs));
-    const u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
+    u32x4 v = *(const u32x4*)(E + tc_off(fp, q));
+    if (tc_half(fp)) v = (u32x4){v[2], v[3], v[0], v[1]};
     *(u32x4*)((h16*)p.dst1 + gp * cof + n0 + q * 8) = v;
   }
 }

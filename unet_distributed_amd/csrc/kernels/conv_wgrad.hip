@@ -109,6 +109,13 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
   const int Cin_s = p.M1;                    // SMALLC: channels of the first-layer input
 
   const int krow = tid >> 2, sub = tid & 3;
+  // SWP: odd pixel rows take their chunk groups in pair-swapped order (group c <-> c ^ 1,
+  // same in load and store).  Rows are whole multiples of 128 bytes and the transposed-read
+  // swizzle moves rows 2r, 2r + 1 by only one 32-byte block, so the 8 lanes of a 16-byte
+  // store group (two rows x four chunks) otherwise land in one 64-byte half: 2-way
+  // conflicted stores, 33 % conflict cycles on wgrad_kernel<128, 128> (r5 PMC pass).
+  constexpr bool SWP = !SMALLC && (BM / 32) % 2 == 0 && (BN / 32) % 2 == 0;
+  const int rsw = SWP ? (krow & 1) : 0;
   // bias partial sums: mode 1 once per (n-tile, split) [tm == 0, tg == 0]; mode 2 once per (m-tile, tg, split) [tn == 0]
   const bool bias_on = BIAS && ((p.bias_mode == 1 && tmi == 0 && tg == 0) || (p.bias_mode == 2 && tn == 0));
 
@@ -183,7 +190,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
         const int base2 = (fpix * p.M2 - p.M1) * 2;
 #pragma unroll
         for (int ci = 0; ci < CPS; ++ci) {
-          const int m = m0 + (sub + 4 * ci) * 8;
+          const int m = m0 + (sub + 4 * (ci ^ rsw)) * 8;
           const int i = tl * CPS + ci;
           if (p.M2 == 0) {
             reg[i] = __builtin_amdgcn_raw_buffer_load_b128(ra1, ok ? base1 + m * 2 : OOB, 0, 0);
@@ -198,7 +205,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
     const int bbase = q * p.Nc * 2 + n0 * 2;
 #pragma unroll
     for (int i = NA / 4; i < CPT; ++i) {
-      const int col = sub + 4 * (i - NA / 4);
+      const int col = sub + 4 * ((i - NA / 4) ^ rsw);
       reg[i] = __builtin_amdgcn_raw_buffer_load_b128(rbb, qok ? bbase + col * 16 : OOB, 0, 0);
     }
   };
@@ -208,10 +215,10 @@ __global__ void __launch_bounds__(NTHR) wgrad_kernel(const WgradParams p) {
     for (int i = 0; i < CPT; ++i) {
       const int j = sub + 4 * i;
       if (j < NA) {
-        const int tl = (4 * i) / (BM / 8), col = j - tl * (BM / 8);
+        const int tl = (4 * i) / (BM / 8), col = sub + 4 * ((i - tl * (BM / 32)) ^ rsw);
         *(u32x4*)(S + tl * A_IMG + tr_off<BM>(krow, col * 8)) = reg[i];
       } else {
-        const int col = j - NA;
+        const int col = sub + 4 * ((i - NA / 4) ^ rsw);
         *(u32x4*)(S + NTAP * A_IMG + tr_off<BN>(krow, col * 8)) = reg[i];
       }
     }
@@ -853,12 +860,14 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   const int m_base = ci0 + 4 * (lane >> 4);
   auto reduce_store = [&](const f32x4 (&v4)[2][2], const int t) {
     __syncthreads();
+    // red[fragment (i, j)][wave * 64 + lane]: consecutive lanes 16 bytes apart (a lane-major
+    // [lane][4 fragments] layout puts the 8 lanes of a 16-byte store group 64 bytes apart,
+    // two 64-byte positions per 128-byte bank window: 4-way conflicted stores and loads)
     if (PS > 1 && ps > 0) {
-      float* dst = red + (wave * 64 + lane) * 16;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) *(f32x4*)(dst + (i * 2 + j) * 4) = v4[i][j];
+        for (int j = 0; j < 2; ++j) *(f32x4*)(red + ((i * 2 + j) * NTHR + wave * 64 + lane) * 4) = v4[i][j];
     }
     __syncthreads();
     if (ps == 0) {
@@ -868,7 +877,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
         for (int j = 0; j < 2; ++j) {
           f32x4 v = v4[i][j];
 #pragma unroll
-          for (int o = 1; o < PS; ++o) v += *(const f32x4*)(red + ((qo + QO * o) * 64 + lane) * 16 + (i * 2 + j) * 4);
+          for (int o = 1; o < PS; ++o) v += *(const f32x4*)(red + ((i * 2 + j) * NTHR + (qo + QO * o) * 64 + lane) * 4);
           if (t < 9) {
             float* dst = p.slab + (((size_t)split * 9 * KD + 9 * kd + t) * Mtot + m_base + 16 * i) * p.Nc + n_base + 16 * j;
 #pragma unroll
@@ -912,7 +921,10 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
   constexpr int XB = XI * 1024, YB = YI * 1024;
   constexpr int MT = (9 * CIN + 15) / 16;
   constexpr int KS = BMW / 32;
-  constexpr int REDB = 4 * 64 * (MT * 2 + 2) * 16;
+  // (cross-wave reduction rows padded to an odd number of 16-byte units: a lane stride of
+  // NV = 2 MT + 2 units (128 bytes at MT = 3) put all 8 lanes of a 16-byte store group on
+  // the same banks -- 8-way; r5 PMC pass: 14.5 % conflict cycles)
+  constexpr int REDB = 4 * 64 * (MT * 2 + 3) * 16;
   constexpr int LDS_BYTES = (XB + YB > REDB) ? XB + YB : REDB;
   static_assert(W >= 16 && W <= 128, "first-layer window wgrad");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
@@ -1072,9 +1084,9 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
   // acc[mt][j][r] = dW[m = 16 mt + 4 (lane >> 4) + r][co0 + 16 j + (lane & 15)]
   __syncthreads();
   float* red = (float*)smem;
-  constexpr int NV = MT * 2 + 2;
+  constexpr int NV = MT * 2 + 2, NVP = NV | 1;
   {
-    float* dst = red + (wave * 64 + lane) * NV * 4;
+    float* dst = red + (wave * 64 + lane) * NVP * 4;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -1087,7 +1099,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
     const int ln = idx / NV, v = idx - ln * NV;
     f32x4 sum = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int w = 0; w < 4; ++w) sum += *(const f32x4*)(red + ((w * 64 + ln) * NV + v) * 4);
+    for (int w = 0; w < 4; ++w) sum += *(const f32x4*)(red + ((w * 64 + ln) * NVP + v) * 4);
     const int n = co0 + (ln & 15);
     if (v < MT * 2) {
       const int mt = v >> 1, j = v & 1;
@@ -1253,12 +1265,14 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
   float* red = (float*)smem;
   auto reduce_store = [&](const f32x4 (&v4)[2][2], const int t) {
     __syncthreads();
+    // red[fragment (i, j)][wave * 64 + lane]: consecutive lanes 16 bytes apart (a lane-major
+    // [lane][4 fragments] layout puts the 8 lanes of a 16-byte store group 64 bytes apart,
+    // two 64-byte positions per 128-byte bank window: 4-way conflicted stores and loads)
     if (PS > 1 && ps > 0) {
-      float* dst = red + (wave * 64 + lane) * 16;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) *(f32x4*)(dst + (i * 2 + j) * 4) = v4[i][j];
+        for (int j = 0; j < 2; ++j) *(f32x4*)(red + ((i * 2 + j) * NTHR + wave * 64 + lane) * 4) = v4[i][j];
     }
     __syncthreads();
     if (ps == 0) {
@@ -1268,7 +1282,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_tconv_win_kernel(const WgradParams
         for (int j = 0; j < 2; ++j) {
           f32x4 v = v4[i][j];
 #pragma unroll
-          for (int o = 1; o < PS; ++o) v += *(const f32x4*)(red + ((qn + QN * o) * 64 + lane) * 16 + (i * 2 + j) * 4);
+          for (int o = 1; o < PS; ++o) v += *(const f32x4*)(red + ((i * 2 + j) * NTHR + (qn + QN * o) * 64 + lane) * 4);
           const int m = co0 + 16 * i + 4 * (lane >> 4), n = ci0 + 32 * qn + 16 * j + (lane & 15);
           if (t < 4) {
             float* o = p.slab + (((size_t)split * 4 + t) * Mtot + m) * p.Nc + n;
