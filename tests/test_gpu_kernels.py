@@ -233,11 +233,13 @@ def test_conv_row_window_dgrad_dual_dest_mask_dropout(cuda_dev):
 @pytest.mark.parametrize("N,H,Cin,Co,tile", [(2, 32, 4, 32, 0), (3, 128, 4, 32, 9), (5, 16, 4, 64, 9),
                                              (2, 64, 8, 32, 9), (2, 32, 4, 32, 8), (2, 32, 8, 64, 8),
                                              (9, 128, 4, 32, 9), (5, 32, 4, 32, 9), (3, 64, 4, 64, 9),
-                                             (5, 32, 8, 64, 9)])
+                                             (5, 32, 8, 64, 9), (2, 256, 4, 32, 9), (3, 512, 4, 32, 9),
+                                             (2, 512, 8, 64, 9)])
 def test_conv_first_layer_smallc(cuda_dev, N, H, Cin, Co, tile):
     """First layer (padded 4/8 channels): row-window kernel (tile 9, auto; 8 windows per
     workgroup with the next halo prefetched -- full and partial groups, 1-2 channel
-    tiles) and the implicit-GEMM small-C mode (tile 8)."""
+    tiles; rows 16..512 wide, a window of one 512-wide row) and the implicit-GEMM small-C
+    mode (tile 8)."""
     torch.manual_seed(3)
     x = torch.randn(N, H, H, Cin, device=cuda_dev).bfloat16()
     w = (torch.randn(3, 3, Cin, Co, device=cuda_dev) * 0.2).bfloat16()
@@ -251,7 +253,8 @@ def test_conv_first_layer_smallc(cuda_dev, N, H, Cin, Co, tile):
 
 
 @pytest.mark.parametrize("N,H,Ci,Co,tile", [(2, 8, 64, 32, 0), (2, 8, 64, 32, 8), (3, 64, 64, 32, 0),
-                                            (2, 32, 128, 64, 0), (5, 16, 256, 128, 0), (3, 8, 512, 256, 0)])
+                                            (2, 32, 128, 64, 0), (5, 16, 256, 128, 0), (3, 8, 512, 256, 0),
+                                            (2, 128, 128, 64, 0)])
 def test_tconv_fwd_shuffle_and_dgrad(cuda_dev, N, H, Ci, Co, tile):
     """2x2 stride-2 transposed conv: window kernels (auto) and the implicit-GEMM path (tile 8)."""
     torch.manual_seed(4)

@@ -88,11 +88,12 @@ def test_composite_tconv_dgrad(cuda_dev, N, H, K, Cc, Cs, O):
 @pytest.mark.parametrize("N,H,K,Cc,Cs,O,splits,win", [(2, 64, 64, 32, 32, 32, 8, 0), (2, 64, 64, 32, 32, 32, 8, -1),
                                                        (2, 32, 128, 64, 64, 64, 5, 0), (3, 32, 32, 32, 32, 32, 7, 0),
                                                        (2, 32, 128, 64, 64, 64, 70, 0), (3, 16, 64, 32, 32, 32, 3, 0),
-                                                       (3, 16, 64, 32, 32, 32, 3, -1), (2, 16, 128, 64, 64, 64, 5, 0)])
+                                                       (3, 16, 64, 32, 32, 32, 3, -1), (2, 16, 128, 64, 64, 64, 5, 0),
+                                                       (2, 128, 128, 64, 64, 64, 6, 0)])
 def test_composite_tconv_weight_grads(cuda_dev, N, H, K, Cc, Cs, O, splits, win):
-    """4x4-tap stride-2 slab sums H / per-tap bias sums Bs (coarse rows 16..64 wide: the
-    window kernel -- at 16 a 32-pixel step spans two coarse rows --, win -1: the tiled
-    kernel) -> chain rule -> dWt, dbt."""
+    """4x4-tap stride-2 slab sums H / per-tap bias sums Bs (coarse rows 16..128 wide: the
+    window kernel -- at 16 a 32-pixel step spans two coarse rows, at 128 a window is one
+    coarse row --, win -1: the tiled kernel) -> chain rule -> dWt, dbt."""
     b, skip, wt, bt, wa, dz = _problem(cuda_dev, N, H, K, Cc, Cs, O, 12)
     _, ref_wt, ref_bt, ref_wa = _reference(b, skip, wt, bt, wa, dz, with_wa=True)
     dev = cuda_dev

@@ -454,7 +454,7 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) 
   constexpr int KS = (9 * CIN + 31) / 32;                      // MFMA K-steps
   constexpr int EPIB = (EPI == EPI_STATS) ? epi_lds_bytes<BM, BN>() : BM * (BN + 4) * 2;
   constexpr int TPR = W / 16;
-  static_assert((CIN == 4 || CIN == 8) && W >= 16 && W <= 128 && BM % W == 0, "first-layer window");
+  static_assert((CIN == 4 || CIN == 8) && W >= 16 && W <= 512 && BM % W == 0, "first-layer window");
   __shared__ __attribute__((aligned(1024))) char smem[XB + EPIB];
   char* Xs = smem;
   char* Es = smem + XB;                                        // epilogue staging
@@ -614,6 +614,8 @@ hipError_t launch_win_first(const ConvFwdParams& p, hipStream_t s) {
     WF_CASE(32)
     WF_CASE(64)
     WF_CASE(128)
+    WF_CASE(256)
+    WF_CASE(512)
     default:
       return hipErrorInvalidValue;
   }
@@ -847,6 +849,7 @@ hipError_t launch_tconv_fwd(const ConvFwdParams& p, hipStream_t s) {
     case 16: UNET_LAUNCH((tconv_fwd_kernel<16, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
     case 32: UNET_LAUNCH((tconv_fwd_kernel<32, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
     case 64: UNET_LAUNCH((tconv_fwd_kernel<64, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 128: UNET_LAUNCH((tconv_fwd_kernel<128, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
     default: return hipErrorInvalidValue;
   }
   return launch_status();
@@ -895,17 +898,20 @@ static bool win_eligible(const ConvFwdParams& p) {
          (p.C1 % 32) == 0 && (p.C2 % 32) == 0 && p.C1 > 0;
 }
 
-// First layer (4/8 padded input channels) on full rows 16..128 wide.
+// First layer (4/8 padded input channels) on full rows 16..512 wide (256 / 512: a window is
+// two rows / one row; the 512^2 model's first layer ran the tiled implicit GEMM at 15 TF/s,
+// 0.33 ms per half-batch launch -- r5 layer times).
 static bool win_first_eligible(const ConvFwdParams& p) {
-  const bool w_ok = p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128;
+  const bool w_ok = p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128 || p.OW == 256 || p.OW == 512;
   return p.KD == 1 && p.OD == 1 && p.ID == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.pad == 1 &&
          p.up1 == 1 && !p.shuffle && !p.nz && w_ok && p.IW == p.OW && p.IH == p.OH && p.C2 == 0 &&
          (p.C1 == 4 || p.C1 == 8) && p.Cout % 32 == 0 && p.D1 == p.Cout;
 }
 
-// 2D transposed-conv forward (1x1 GEMM + 2x2 pixel shuffle) on coarse rows 8..64 wide.
+// 2D transposed-conv forward (1x1 GEMM + 2x2 pixel shuffle) on coarse rows 8..128 wide
+// (128: a window is one coarse row).
 static bool tconv_fwd_eligible(const ConvFwdParams& p) {
-  const bool w_ok = p.OW == 8 || p.OW == 16 || p.OW == 32 || p.OW == 64;
+  const bool w_ok = p.OW == 8 || p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128;
   return p.shuffle == 2 && p.KD == 1 && p.KH == 1 && p.KW == 1 && p.OD == 1 && w_ok && p.IW == p.OW &&
          p.IH == p.OH && p.C2 == 0 && (p.C1 % 32) == 0 && ((p.Cout >> 2) % 32) == 0 && !p.relu &&
          p.drop_rate == 0.f && !p.mask1 && !p.stats && p.out_scale == 1.f;

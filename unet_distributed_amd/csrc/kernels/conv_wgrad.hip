@@ -1320,7 +1320,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_s2d_win_kernel(const WgradParams p
   constexpr int XI = QN * BMc / 16, YI = (FR * FP + 15) / 16;
   constexpr int XB = XI * 1024, YB = YI * 1024;
   constexpr int KS = BMc / 32;
-  static_assert(W >= 16 && W <= 64, "composite window wgrad");
+  static_assert(W >= 16 && W <= 128, "composite window wgrad");
   __shared__ __attribute__((aligned(1024))) char smem[XB + YB];
   char* Xs = smem;
   char* Ys = smem + XB;
@@ -1527,10 +1527,12 @@ static bool wgrad_tconv_win_eligible(const WgradParams& p) {
          (p.M1 % 32) == 0 && (p.Nc % 32) == 0 && p.bias_mode != 1;
 }
 
-// Composite transposed-conv slab sums (4x4 taps, stride 2, pad 1) on coarse rows 16..64 wide.
+// Composite transposed-conv slab sums (4x4 taps, stride 2, pad 1) on coarse rows 16..128
+// wide (128: the 512^2 model's level-3 -> 2 transposed conv; there the generic one-tap tile
+// ran at 38 TF/s, 0.89 ms of a 14.5 ms step -- r5 layer times).
 static bool wgrad_s2d_win_eligible(const WgradParams& p) {
   const int R = p.QW > 0 ? 128 / p.QW : 1;
-  return p.win >= 0 && (p.QW == 16 || p.QW == 32 || p.QW == 64) && p.QD == 1 && p.KD == 1 && p.KH == 4 && p.KW == 4 &&
+  return p.win >= 0 && (p.QW == 16 || p.QW == 32 || p.QW == 64 || p.QW == 128) && p.QD == 1 && p.KD == 1 && p.KH == 4 && p.KW == 4 &&
          p.stride == 2 && p.pad == 1 && p.upA == 1 && p.AW == 2 * p.QW && p.AH == 2 * p.QH && p.QH % R == 0 &&
          p.M2 == 0 && (p.M1 % 32) == 0 && (p.Nc % 32) == 0 && p.bias_mode != 1;
 }
@@ -1542,7 +1544,9 @@ WgradCfg wgrad_pick(const WgradParams& p) {
   if (wgrad_win_first_eligible(p)) return {p.M1 == 4 ? 48 : 80, 32, 1, 1};      // first-layer window
   if (wgrad_tconv_win_eligible(p))                                                 // transposed-conv window
     return {32, p.Nc % 128 == 0 ? 128 : (p.Nc % 64 == 0 ? 64 : 32), 4, 0};
-  if (wgrad_s2d_win_eligible(p)) return {32, p.Nc % 64 == 0 ? 64 : 32, 16, 0};   // composite window
+  // composite window (128-wide coarse rows: one 32-channel block per workgroup -- the four
+  // staged fine rows of 258 slots + a 64-channel coarse block would exceed two workgroups' LDS)
+  if (wgrad_s2d_win_eligible(p)) return {32, (p.Nc % 64 == 0 && p.QW <= 64) ? 64 : 32, 16, 0};
   if ((p.M1 == 4 || p.M1 == 8) && p.M2 == 0) return {64, 32, 1, 1};
   // composite transposed-conv slab (tconv_fused.hip): 4x4 taps, stride 2, pad 1, one tap
   // per tile so bias mode 2 yields the per-tap sums
@@ -1617,15 +1621,17 @@ hipError_t wgrad_launch(const WgradParams& p0, hipStream_t s) {
     return launch_status();
   }
   if (wgrad_s2d_win_eligible(p)) {
-    const int qn = p.Nc % 64 == 0 ? 2 : 1;
+    const int qn = (p.Nc % 64 == 0 && p.QW <= 64) ? 2 : 1;
     const int grid = (p.M1 / 32) * (p.Nc / (32 * qn)) * launch_splits(p);
 #define SW_CASE(WW, QQ) UNET_LAUNCH((wgrad_s2d_win_kernel<WW, QQ>), dim3(grid), dim3(NTHR), 0, s, p)
     if (p.QW == 16) {
       if (qn == 2) SW_CASE(16, 2); else SW_CASE(16, 1);
     } else if (p.QW == 32) {
       if (qn == 2) SW_CASE(32, 2); else SW_CASE(32, 1);
-    } else {
+    } else if (p.QW == 64) {
       if (qn == 2) SW_CASE(64, 2); else SW_CASE(64, 1);
+    } else {
+      SW_CASE(128, 1);
     }
 #undef SW_CASE
     return launch_status();
