@@ -255,10 +255,12 @@ def test_f32_native_step_matches_aten_fp32(cuda_dev, kw):
         # ReLU flip near zero moves its max-norm error by up to ~1e-4 -- observed 1.3e-4 on
         # conv8a/bias at 3 x 128^2, where the CPU step happened to flip none)
         assert e_nat < 2 * e_aten + 5e-4, (name, e_nat, e_aten)
-    g64_all = torch.cat([g64[e[0]].reshape(-1) for e in fn.entries])
+    # (flat buffers carry alignment padding between entries: compare entry by entry)
+    g64_all = torch.cat([g64[name].reshape(-1) for name, _, _, _ in fn.entries])
 
-    def l2(a):
-        return ((a.double() - g64_all).norm() / g64_all.norm()).item()
+    def l2(flat):
+        a = torch.cat([flat[off:off + n].double() for _, _, off, n in fn.entries])
+        return ((a - g64_all).norm() / g64_all.norm()).item()
     e_all, e_all_aten = l2(fn.grad.cpu()), l2(ft.grad)
     print("fp32 step vs float64: worst per-tensor %.2e, all gradients L2 %.2e (ATen fp32 CPU %.2e)"
           % (worst, e_all, e_all_aten))
