@@ -5,7 +5,11 @@
 #   bash scripts/gpu_r5_ups_dice.sh [steps] [seeds...]
 set -o pipefail
 export TMPDIR=/tmp
-export MIOPEN_FIND_MODE=${MIOPEN_FIND_MODE:-FAST}
+# MIOpen's FAST find mode picks naive fp32 NHWC kernels for this decoder (~70 img/s,
+# profiles/r5_aten_ups_kernels.md); NORMAL searches once (~3 min, cached for later runs) and
+# then runs ~4.7k img/s
+export MIOPEN_FIND_MODE=${MIOPEN_FIND_MODE:-NORMAL}
+arms=${ARMS:-"native_bf16 native_fp32 aten_fp32"}
 steps=${1:-200}; shift || true
 seeds=${@:-1 2 3}
 o=gpurun_out/dice_ups; mkdir -p $o
@@ -18,11 +22,9 @@ run() {   # name timeout args...
     || { echo "$name rc=$?"; tail -20 $o/$name.log; exit 1; }
 }
 for seed in $seeds; do
-  run native_bf16_s$seed 300 python train.py $COMMON --seed $seed --backend native --dtype bf16
-  run native_fp32_s$seed 400 python train.py $COMMON --seed $seed --backend native --dtype fp32
-  # (ATen fp32 runs this 1-channel decoder at ~70 img/s: ATEN_STEPS, default 40, bounds it)
-  run aten_fp32_s$seed 600 python train.py ${COMMON/--steps $steps/--steps ${ATEN_STEPS:-40}} --seed $seed \
-    --backend torch --dtype fp32
+  [[ $arms == *native_bf16* ]] && run native_bf16_s$seed 300 python train.py $COMMON --seed $seed --backend native --dtype bf16
+  [[ $arms == *native_fp32* ]] && run native_fp32_s$seed 400 python train.py $COMMON --seed $seed --backend native --dtype fp32
+  [[ $arms == *aten_fp32* ]] && run aten_fp32_s$seed 600 python train.py $COMMON --seed $seed --backend torch --dtype fp32
   echo seed $seed done
 done
 python scripts/dice_ups_summary.py $o "${LR:-0.0005}" $seeds

@@ -299,12 +299,17 @@ def test_hip_graph_replay_equals_eager(cuda_dev, monkeypatch, norm):
     dict(batch_size=8, img_size=64, in_channels=4, dropout=0.0),
     dict(batch_size=4, img_size=64, in_channels=1, use_upsampling=True, hip_graph=True, dropout=0.0),
     dict(batch_size=4, img_size=64, in_channels=4),
+    dict(batch_size=4, img_size=64, in_channels=4, norm="group", dtype="fp16"),
+    dict(batch_size=6, img_size=128, in_channels=4, norm="group", dtype="fp16", loss="dice_bce"),
+    dict(batch_size=4, img_size=64, in_channels=1, use_upsampling=True, norm="group"),
 ])
 def test_two_stream_forward_equals_one_stream(cuda_dev, monkeypatch, kw):
     """fwd_streams=2 runs the training forward as two half-batch chunks on two
     streams (fused pools / head logits written at the chunk's offset): activations,
     loss sums and gradients are bit-identical to the one-stream forward, dropout
-    included (each chunk hashes its elements' whole-batch indices, drop_idx0)."""
+    included (each chunk hashes its elements' whole-batch indices, drop_idx0 / the
+    norm pass's n0).  GroupNorm: each chunk finalizes its own samples' statistics at
+    its offset, the head input's normalisation + loss sums run on the whole batch."""
     outs = []
     for n in ("1", "2"):
         monkeypatch.setenv("UNET_ENGINE", "fwd_streams=" + n)

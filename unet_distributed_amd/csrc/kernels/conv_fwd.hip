@@ -448,8 +448,13 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) 
   constexpr int ROWB = RS * SB;
   constexpr int CPR = ROWB / 16;                               // 16-byte chunks per halo row
   constexpr int NCH = HR * CPR;                                // halo chunks
-  constexpr int CPT = (NCH + NTHR - 1) / NTHR;                 // chunks per thread
-  constexpr int XB = (NCH * 16 + 1023) / 1024 * 1024;
+  // + a zeroed tail of 16 chunks: a zero tap reads its partner's slot ^ 16, which for the
+  // last halo row's columns W - 1, W lies up to 2 slots past the image (RS = W + 16 at
+  // W >= 128) -- never-written LDS there could hold a NaN pattern (0 x NaN).  (Found at
+  // W = 512: relative error 0.65.)
+  constexpr int NCHZ = NCH + 16;
+  constexpr int CPT = (NCHZ + NTHR - 1) / NTHR;                // chunks per thread
+  constexpr int XB = (NCHZ * 16 + 1023) / 1024 * 1024;
   constexpr int BN = 32, TM = 8, TN = 2;
   constexpr int KS = (9 * CIN + 31) / 32;                      // MFMA K-steps
   constexpr int EPIB = (EPI == EPI_STATS) ? epi_lds_bytes<BM, BN>() : BM * (BN + 4) * 2;
@@ -490,7 +495,7 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) 
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int u = tid + NTHR * c;
-      if (u < NCH) *(u32x4*)(Xs + u * 16) = hv[c];
+      if (u < NCHZ) *(u32x4*)(Xs + u * 16) = hv[c];
     }
   };
   // weight fragments (A operand: k = 32 s + 8 (lane >> 4) .. + 7, m = lane & 15), from global.

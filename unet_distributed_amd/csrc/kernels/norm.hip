@@ -236,7 +236,9 @@ __global__ void __launch_bounds__(NT) norm_apply_kernel(const h16* __restrict__ 
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int relu, float drop_rate,
                                                         uint32_t seed0, const uint32_t* __restrict__ seed_ptr,
-                                                        uint32_t salt, h16* __restrict__ y) {
+                                                        uint32_t salt, int n0, h16* __restrict__ y) {
+  // n0: the launch's first sample in the whole batch (a half-batch chunk of the two-stream
+  // forward): dropout hashes whole-batch element indices, like the conv epilogue's drop_idx0
   const int n = blockIdx.y, nbp = gridDim.x, blk = blockIdx.x;
   const int cpr = C / 8, rstep = NT / cpr;
   const int cc = threadIdx.x % cpr, rs = threadIdx.x / cpr;
@@ -256,7 +258,7 @@ __global__ void __launch_bounds__(NT) norm_apply_kernel(const h16* __restrict__ 
     const float inv_keep = 1.f / (1.f - drop_rate);
     const uint32_t thr = (uint32_t)(drop_rate * 4294967296.0);
     for (int p = p0 + rs; p < p1; p += rstep) {
-      const size_t q = (size_t)n * P + p;
+      const size_t q = (size_t)(n0 + n) * P + p;
       float v[8];
       unpack8(*(const u32x4*)(z + base + (size_t)p * C), v);
 #pragma unroll
@@ -790,9 +792,9 @@ hipError_t norm_rows_launch(const void* A, const void* B, int N, int P, int C, f
 
 hipError_t norm_apply_launch(const void* z, int N, int P, int C, const float* mean, const float* rstd, int cstride,
                              const float* gamma, const float* beta, int relu, float drop_rate, uint32_t seed,
-                             const uint32_t* seed_ptr, uint32_t salt, void* y, hipStream_t s) {
+                             const uint32_t* seed_ptr, uint32_t salt, int n0, void* y, hipStream_t s) {
   UNET_LAUNCH(norm_apply_kernel, dim3(norm_blocks_per_sample(N, P), N), dim3(NT), 0, s, (const h16*)z, P, C,
-                     mean, rstd, cstride, gamma, beta, relu, drop_rate, seed, seed_ptr, salt, (h16*)y);
+                     mean, rstd, cstride, gamma, beta, relu, drop_rate, seed, seed_ptr, salt, n0, (h16*)y);
   return launch_status();
 }
 

@@ -657,7 +657,8 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     return [=](hipStream_t s) { return A->moments_collect_launch(part, n, c, nbp, S, s); };
   }
   if (kind == "norm_apply") {
-    // ptrs: z, mean, rstd, gamma, beta, y   ints: N, P, C, cstride, relu, salt[, seed]   floats: drop_rate
+    // ptrs: z, mean, rstd, gamma, beta, y   ints: N, P, C, cstride, relu, salt[, seed[, n0]]   floats: drop_rate
+    // (n0: first sample of the launch in the whole batch -- dropout hash indices)
     need(6, 6, 1);
     void* z = vp(0);
     const float *mu = (const float*)vp(1), *rs = (const float*)vp(2), *gm = (const float*)vp(3),
@@ -665,11 +666,12 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     void* y = vp(5);
     int n = I[0], np = I[1], c = I[2], cs = I[3], relu = I[4];
     uint32_t salt = (uint32_t)I[5], seed0 = I.size() > 6 ? (uint32_t)I[6] : 0u;
+    const int n0 = I.size() > 7 ? (int)I[7] : 0;
     float dr = (float)F[0];
     check_msg(norm_check(c, 0));
     return [=](hipStream_t s) {
       return A->norm_apply_launch(z, n, np, c, mu, rs, cs, gm, bt, relu, dr, seedp ? *seedp : seed0,
-                               seed_devp ? *seed_devp : nullptr, salt, y, s);
+                               seed_devp ? *seed_devp : nullptr, salt, n0, y, s);
     };
   }
   if (kind == "norm_bwd_apply") {

@@ -117,7 +117,7 @@ FUSIONS: Dict[str, Fusion] = {
                         norm={"none"}, option="head_fuse", when=lambda e: e.tinfo[e.head_in][1] == 32),
     "pool_epilogue": Fusion("2x2 max-pool in the convNb forward epilogue", norm={"none"}),
     "fwd_2streams": Fusion("training forward as two half-batch chunks on two streams",
-                           norm={"none"}, even_batch=True, when=lambda e: e.opts["fwd_streams"] == 2),
+                           norm={"none", "group"}, even_batch=True, when=lambda e: e.opts["fwd_streams"] == 2),
     "tconv_fused": Fusion("composite transposed-conv backward (tconv_fused.hip)", dims={2},
                           option="tconv_fused"),
     "tconv_wa": Fusion("consumer's u-row weight gradient chained from the slab sums", dims={2},
@@ -213,6 +213,7 @@ class NativeUNet:
         self.wgrad_win = 0
         # fusion name -> layers it was applied to (FUSIONS; plan validation and tests)
         self.fusions: Dict[str, List[str]] = {}
+        self._dry = dry_run
         self._alloc_weights()
         self._alloc_activations()
         # (each op's parameters are kept for the static plan validation, runtime/plan_check.py)
@@ -605,13 +606,16 @@ class NativeUNet:
             self._stat_bufs[key] = t
         return t
 
-    def _fuse_stats(self, d, key, C, level):
+    def _fuse_stats(self, d, key, C, level, c=0, nb=None):
         """Let conv dict `d` write per-tile normalisation statistics from its epilogue
         (conv_epilogue.h EPI_STATS / EPI_DGRAD_NORM) if its kernel can.  Returns
-        (rows, per_sample) or None; per_sample: every sample owns rows / B
-        consecutive rows (required by GroupNorm's per-sample statistics)."""
+        (rows, per_sample) or None; per_sample: every sample owns rows / N
+        consecutive rows (required by GroupNorm's per-sample statistics).  Chunk c of
+        nb images (the two-stream forward, d["N"] == nb) writes its rows after the rows
+        of the chunks before it: sample-major, so the whole-batch row order is kept."""
         if not self.fuse_norm_stats:
             return None
+        nb = nb or self.B
         try:
             rows, px = self.C.conv_stat_tiles(dict(d, stats=1))
         except ValueError:
@@ -619,76 +623,108 @@ class NativeUNet:
         if rows == 0:
             return None
         P = self.npix(level) // self.B
-        per_sample = px > 0 and P % px == 0 and rows % self.B == 0
+        per_sample = px > 0 and P % px == 0 and rows % nb == 0
         if self.spec.norm == "group" and not per_sample:
             return None
-        d["stats"] = _ptr(self._stat_buf(key, rows * 2 * C))
+        buf = self._stat_buf(key, (self.B // nb) * rows * 2 * C)
+        d["stats"] = _ptr(buf) + c * rows * 2 * C * 4
         return rows, per_sample
 
-    def _stat_rows(self, key, A, B, l, fused, plan, name):
-        """(rows buffer, row count) of the per-tile / per-block partial sums of layer l:
-        the producer's epilogue rows when `fused`, else a moments pass over (A, A*B)."""
-        C, P, N = l.cout, self.npix(l.level) // self.B, self.B
+    def _stat_rows(self, key, A, B, l, fused, plan, name, c=0, nb=None):
+        """(rows pointer, row count) of the per-tile / per-block partial sums of layer l
+        (images [c nb, (c + 1) nb)): the producer's epilogue rows when `fused`, else a
+        moments pass over (A, A*B) -- A, B: pointers to the chunk's images."""
+        nb = nb or self.B
+        C, P = l.cout, self.npix(l.level) // self.B
         if fused:
-            return self._stat_bufs[key], fused[0]
-        R = N * self.C.norm_blocks_per_sample(N, P)
-        rows = self._stat_buf("m" + key, R * 2 * C)
-        plan.add_generic("norm_rows", [_ptr(A), _ptr(B), _ptr(rows)], [N, P, C], [], name)
+            return _ptr(self._stat_bufs[key]) + c * fused[0] * 2 * C * 4, fused[0]
+        R = nb * self.C.norm_blocks_per_sample(nb, P)
+        rows = _ptr(self._stat_buf("m" + key, (self.B // nb) * R * 2 * C)) + c * R * 2 * C * 4
+        plan.add_generic("norm_rows", [A, B, rows], [nb, P, C], [], name)
         return rows, R
 
-    def _stat_work(self, key, R, C):
+    def _stat_work(self, key, R, C, c=0, nb=None):
         """Workspace of bn_stats / gn_stats (slices of R rows, or GroupNorm's per-sample
-        parameter-gradient rows + their slices)."""
+        parameter-gradient rows + their slices); one per forward chunk (the two chunks'
+        finalizes run concurrently), each sized for the whole batch's rows so the
+        one-stream evaluation plan never regrows (and frees) a buffer a recorded launch
+        points into."""
+        Rw = R * (self.B // (nb or self.B))
         # (+64: the single-launch finalize's hand-off counter past the slices, norm.hip)
-        n = max(self.C.row_slices(R), 1) * 2 * C + self.B * 2 * C + self.C.row_slices(self.B) * 2 * C + 64
-        return self._stat_buf("w" + key, n)
+        n = max(self.C.row_slices(Rw), 1) * 2 * C + self.B * 2 * C + self.C.row_slices(self.B) * 2 * C + 64
+        return self._stat_buf("w" + key + (":%d" % c if c else ""), n)
 
-    def _norm_fwd(self, plan, l, dropout, train, fused=None):
-        """z:<L> -> activation <L> = relu(norm(z)) (+ dropout).  fused: (rows, per_sample)
-        when conv L's epilogue wrote the statistics (no separate moments pass)."""
+    def _norm_fwd(self, plan, l, dropout, train, fused=None, c=0, nb=None):
+        """z:<L> -> activation <L> = relu(norm(z)) (+ dropout) for images [c nb, (c+1) nb)
+        (a chunk of the two-stream forward; GroupNorm only: per-sample statistics).
+        fused: (rows, per_sample) when conv L's epilogue wrote the statistics (no
+        separate moments pass)."""
         b, spec = self.bufs, self.spec
-        C, P, N = l.cout, self.npix(l.level) // self.B, self.B
+        nb = nb or self.B
+        C, P, N = l.cout, self.npix(l.level) // self.B, nb
         z = b["z:" + l.name]
-        mean, rstd = b["mean:" + l.name], b["rstd:" + l.name]
-        fa, fc = b["fa:" + l.name], b["fc:" + l.name]
+        zp = _ptr(z) + c * nb * P * C * z.element_size()
+        mo = 0 if spec.norm == "batch" else c * nb * C * 4            # per-sample [B][C] coefficients
+        mean, rstd = _ptr(b["mean:" + l.name]) + mo, _ptr(b["rstd:" + l.name]) + mo
+        fa, fc = _ptr(b["fa:" + l.name]) + mo, _ptr(b["fc:" + l.name]) + mo
         gamma, beta = self.master_ptr(l.name + "/norm/gamma"), self.master_ptr(l.name + "/norm/beta")
         if spec.norm == "batch":
+            assert nb == self.B, "BatchNorm statistics are whole-batch: no forward chunks"
             rm = self.state[l.name + "/norm/moving_mean"]
             rv = self.state[l.name + "/norm/moving_variance"]
             if train:
-                rows, R = self._stat_rows("st:" + l.name, z, z, l, fused, plan, "bnstat:" + l.name)
+                rows, R = self._stat_rows("st:" + l.name, zp, zp, l, fused, plan, "bnstat:" + l.name)
             else:
-                rows, R = self._stat_buf("st:" + l.name, 64), 1        # inference: running statistics
+                rows, R = _ptr(self._stat_buf("st:" + l.name, 64)), 1     # inference: running statistics
             ws = self._stat_work("st:" + l.name, R, C)
-            plan.add_generic("bn_stats", [_ptr(rows), gamma, beta, _ptr(rm), _ptr(rv), _ptr(mean), _ptr(rstd),
-                                          _ptr(fa), _ptr(fc), 0, 0, 0, 0, 0, _ptr(ws)],
+            plan.add_generic("bn_stats", [rows, gamma, beta, _ptr(rm), _ptr(rv), mean, rstd,
+                                          fa, fc, 0, 0, 0, 0, 0, _ptr(ws)],
                              [R, C, 0 if train else 2], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM],
                              "bnfin:" + l.name)
-            cstride = 0
         else:
-            rows, R = self._stat_rows("st:" + l.name, z, z, l, fused, plan, "gnstat:" + l.name)
-            ws = self._stat_work("st:" + l.name, R, C)
-            plan.add_generic("gn_stats", [_ptr(rows), gamma, beta, _ptr(mean), _ptr(rstd), _ptr(fa), _ptr(fc),
-                                          0, 0, 0, 0, 0, _ptr(ws)],
+            rows, R = self._stat_rows("st:" + l.name, zp, zp, l, fused, plan, "gnstat:" + l.name, c, nb)
+            ws = self._stat_work("st:" + l.name, R, C, c, nb)
+            plan.add_generic("gn_stats", [rows, gamma, beta, mean, rstd, fa, fc, 0, 0, 0, 0, 0, _ptr(ws)],
                              [N, R // N, C, spec.groups, P, 0], [self.NORM_EPS], "gnfin:" + l.name)
-            cstride = C
         if l.name in self._xf_fwd:
             return          # the consumer conv normalises z on load and writes the activation
+        if l.name == self.head_in and nb != self.B:
+            # two-stream forward: the head (its loss sums need every pixel) runs on the
+            # whole batch once both chunks are done (_build_forward_2s)
+            self._deferred_head = (l, dropout, train)
+            return
+        self._norm_out(plan, l, dropout, train, c, nb)
+
+    def _norm_out(self, plan, l, dropout, train, c=0, nb=None):
+        """The pass after a layer's statistics: the normalised activation (with the 2x2
+        max-pool of convNb; with the head logits / loss sums for the head input)."""
+        b, spec = self.bufs, self.spec
+        nb = nb or self.B
+        C, P, N = l.cout, self.npix(l.level) // self.B, nb
+        z = b["z:" + l.name]
+        zp = _ptr(z) + c * nb * P * C * z.element_size()
+        mo = 0 if spec.norm == "batch" else c * nb * C * 4
+        mean, rstd = _ptr(b["mean:" + l.name]) + mo, _ptr(b["rstd:" + l.name]) + mo
+        fa, fc = _ptr(b["fa:" + l.name]) + mo, _ptr(b["fc:" + l.name]) + mo
+        gamma, beta = self.master_ptr(l.name + "/norm/gamma"), self.master_ptr(l.name + "/norm/beta")
+        cstride = 0 if spec.norm == "batch" else C
+        out = _ptr(b[l.name]) + self._toff(l.name, c, nb)
         if l.name == self.head_in and not (l.dropout and dropout) and self.tinfo[l.name][1] in (16, 32, 64):
+            assert nb == self.B
             if train:
                 # training: normalisation, logits, sigmoid, loss sums and the nine per-channel
                 # pixel sums of the head's backward in one pass (head.hip norm_head_loss);
                 # the activation is not stored -- nothing downstream reads it
                 hp = self._stat_buf("hn:part", self.C.hn_partial_floats(N, P, C))
-                plan.add_generic("norm_head_loss", [_ptr(z), _ptr(fa), _ptr(fc), self.master_ptr("Mask/kernel"),
+                plan.add_generic("norm_head_loss", [zp, fa, fc, self.master_ptr("Mask/kernel"),
                                                     self.master_ptr("Mask/bias"), _ptr(self.target), 0,
                                                     _ptr(self.prob), _ptr(hp), _ptr(self.sums)],
                                  [N, P, C, cstride], [], "fwd:Mask")
                 self._norm_head_loss = True
                 return
             # head input: normalisation + the 1x1 head's logits in one pass (head_finish follows)
-            plan.add_generic("norm_head", [_ptr(z), _ptr(fa), _ptr(fc), self.master_ptr("Mask/kernel"),
-                                           self.master_ptr("Mask/bias"), _ptr(b[l.name]), _ptr(self.prob)],
+            plan.add_generic("norm_head", [zp, fa, fc, self.master_ptr("Mask/kernel"),
+                                           self.master_ptr("Mask/bias"), out, _ptr(self.prob)],
                              [self.npix(l.level), C, cstride, P], [], "norm:" + l.name)
             self._norm_head = True
             return
@@ -696,13 +732,13 @@ class NativeUNet:
         if pool is not None and not (l.dropout and dropout):
             # convNb: normalisation and the 2x2 max-pool of its output in one pass
             dd, hh, ww = self.sdims(l.level)
-            plan.add_generic("norm_pool", [_ptr(z), _ptr(fa), _ptr(fc), _ptr(b[l.name]), _ptr(b[pool]),
-                                           _ptr(self.pool_codes[pool])],
+            pcode = _ptr(self.pool_codes[pool]) + c * nb * (self.npix(l.level + 1) // self.B) * (C // 8) * 4
+            plan.add_generic("norm_pool", [zp, fa, fc, out, _ptr(b[pool]) + self._toff(pool, c, nb), pcode],
                              [N, dd, hh, ww, C, int(self.dims == 3), cstride], [], "norm:" + l.name)
             self._pool_fused.add(pool)
             return
-        plan.add_generic("norm_apply", [_ptr(z), _ptr(mean), _ptr(rstd), gamma, beta, _ptr(b[l.name])],
-                         [N, P, C, cstride, 1, self._salt(l.name)],
+        plan.add_generic("norm_apply", [zp, mean, rstd, gamma, beta, out],
+                         [N, P, C, cstride, 1, self._salt(l.name), 0, c * nb],
                          [spec.dropout if (l.dropout and dropout) else 0.0], "norm:" + l.name)
 
     def _norm_bwd_ops(self, l, apply=True):
@@ -723,17 +759,17 @@ class NativeUNet:
 
         def emit(pl):
             if hn:      # rows from the forward's head sums (head_norm_coef)
-                rows, R = self._hn_rows, N * self.C.hn_blocks_per_sample(N, P)
+                rows, R = _ptr(self._hn_rows), N * self.C.hn_blocks_per_sample(N, P)
             else:
-                rows, R = self._stat_rows("bst:" + l.name, g, z, l, fused, pl, "nstat_bwd:" + l.name)
+                rows, R = self._stat_rows("bst:" + l.name, _ptr(g), _ptr(z), l, fused, pl, "nstat_bwd:" + l.name)
             ws = self._stat_work("bst:" + l.name, R, C)
             if spec.norm == "batch":
-                pl.add_generic("bn_stats", [_ptr(rows), gamma, beta, 0, 0, _ptr(mean), _ptr(rstd), 0, 0,
+                pl.add_generic("bn_stats", [rows, gamma, beta, 0, 0, _ptr(mean), _ptr(rstd), 0, 0,
                                             _ptr(ca), _ptr(cb), _ptr(cc), dgam, dbet, _ptr(ws)],
                                [R, C, 1], [float(N * P), self.NORM_EPS, self.BN_MOMENTUM], "bnfin_bwd:" + l.name)
                 cstride = 0
             else:
-                pl.add_generic("gn_stats", [_ptr(rows), gamma, beta, _ptr(mean), _ptr(rstd), 0, 0, _ptr(ca),
+                pl.add_generic("gn_stats", [rows, gamma, beta, _ptr(mean), _ptr(rstd), 0, 0, _ptr(ca),
                                             _ptr(cb), _ptr(cc), dgam, dbet, _ptr(ws)],
                                [N, R // N, C, spec.groups, P, 1], [self.NORM_EPS], "gnfin_bwd:" + l.name)
                 cstride = C
@@ -899,13 +935,17 @@ class NativeUNet:
         d, h, w = self.sdims(lvl)
         return c * nb * d * h * w * ch * self.bufs[tname].element_size()
 
-    def _xf_fwd_fields(self, src):
+    def _xf_fwd_fields(self, src, c=0, nb=None):
         """Operand-transform fields of a conv reading normalised activation `src` as the
-        pre-norm z (conv_params.h xform 1); the conv also writes the activation."""
+        pre-norm z (conv_params.h xform 1) for images [c nb, (c + 1) nb); the conv also
+        writes the activation."""
         b = self.bufs
-        return dict(xform=1, xa=_ptr(b["fa:" + src]), xb=_ptr(b["fc:" + src]),
-                    xcs=0 if self.spec.norm == "batch" else self.tinfo[src][1],
-                    xout=_ptr(b[src]))
+        nb = nb or self.B
+        C = self.tinfo[src][1]
+        mo = 0 if self.spec.norm == "batch" else c * nb * C * 4       # per-sample [B][C] coefficients
+        return dict(xform=1, xa=_ptr(b["fa:" + src]) + mo, xb=_ptr(b["fc:" + src]) + mo,
+                    xcs=0 if self.spec.norm == "batch" else C,
+                    xout=_ptr(b[src]) + self._toff(src, c, nb))
 
     def _plan_xforms(self):
         """Normalised activations whose only consumer is the next conv's first source
@@ -951,12 +991,16 @@ class NativeUNet:
 
     def _fwd_streams(self, train):
         """2: the training forward runs as two half-batch chunks on two HIP streams, the
-        second chunk started once the first has finished its first fwd_offset layers, so kernels of different levels (bandwidth-bound full-resolution ones,
-        MFMA-bound coarse ones) share the GPU.  Norm-free 2D model with an even batch
-        (BatchNorm needs whole-batch statistics); option fwd_streams=1 keeps one stream.
-        Default 2 since round 3: same-box interleaved A/B of the headline step +1.0 / +1.0 /
-        +0.6 % (44.2k -> 44.7k img/s, round 2 measured +0.9 % the same way)."""
-        if not train or not self._fusion_ok("fwd_2streams") or self.device.type != "cuda":
+        second chunk started once the first has finished its first fwd_offset layers, so
+        kernels of different levels (bandwidth-bound full-resolution ones, MFMA-bound
+        coarse ones) share the GPU.  Norm-free or GroupNorm model (per-sample statistics:
+        each chunk finalizes its own samples; the head's loss sums run on the whole batch
+        after both chunks) with an even batch -- BatchNorm needs whole-batch statistics;
+        option fwd_streams=1 keeps one stream.  Default 2 since round 3: same-box
+        interleaved A/B of the headline step +1.0 / +1.0 / +0.6 % (44.2k -> 44.7k img/s,
+        round 2 measured +0.9 % the same way).  (A CPU dry run plans it too, for the
+        static plan validation.)"""
+        if not train or not self._fusion_ok("fwd_2streams") or (self.device.type != "cuda" and not self._dry):
             return 1
         return 2
 
@@ -993,6 +1037,7 @@ class NativeUNet:
         nb = self.B // 2
         off = self.opts["fwd_offset"]
         self._fwd2 = []                      # (first op, op after the offset layers, end) per chunk
+        self._deferred_head = None
         for c in range(2):
             start = plan.size()
             mark = start
@@ -1001,6 +1046,11 @@ class NativeUNet:
                 if k + 1 == off:
                     mark = plan.size()
             self._fwd2.append((start, mark, plan.size()))
+        if self._deferred_head is not None:
+            # GroupNorm: the head input's normalisation with the head logits / loss sums on
+            # the whole batch (both chunks' per-sample statistics are in place by now)
+            self._norm_out(plan, *self._deferred_head)
+            self._deferred_head = None
         for l in spec.layers:
             if l.kind == "mask":
                 self._fwd_layer(plan, l, dropout, train, 0, self.B)
@@ -1035,13 +1085,13 @@ class NativeUNet:
                 d.update(self._ut_fields(tl, P(self.inputs[ut][0])))
                 s1 = d["ut_x"]
             if src1 in self._xf_fwd:
-                d.update(self._xf_fwd_fields(src1))
-                s1 = _ptr(b["z:" + src1])
+                d.update(self._xf_fwd_fields(src1, c, nb))
+                s1 = _ptr(b["z:" + src1]) + self._toff(src1, c, nb)
             d.update(name="fwd:" + l.name, C1=c1, C2=self.tinfo[skip][1] if skip else 0, up1=up1,
                      src1=s1, src2=P(skip) if skip else None,
                      wgt=self.wptr(l.name), bias=self.master_ptr(l.name + "/bias"),
                      Cout=l.cout, relu=0 if normed else 1,
-                     dst1=_ptr(b["z:" + l.name]) if normed else P(l.name),
+                     dst1=_ptr(b["z:" + l.name]) + self._toff(l.name, c, nb) if normed else P(l.name),
                      drop_rate=spec.dropout if (l.dropout and dropout and not normed) else 0.0,
                      salt=self._salt(l.name), drop_idx0=c * nb * (self.npix(l.level) // self.B) * l.cout)
             bits = self.relu_bits.get(l.name)
@@ -1069,10 +1119,10 @@ class NativeUNet:
             self._rev_order(d, src1, l.name, pool if pool in self._pool_fused else None)
             fused = None
             if normed and (train or spec.norm == "group"):
-                fused = self._fuse_stats(d, "st:" + l.name, l.cout, l.level)
+                fused = self._fuse_stats(d, "st:" + l.name, l.cout, l.level, c, nb)
             plan.add_conv_fwd(d)
             if normed:
-                self._norm_fwd(plan, l, dropout, train, fused)
+                self._norm_fwd(plan, l, dropout, train, fused, c, nb)
         elif l.kind == "pool" and l.name in self._pool_fused:
             pass                                 # written by its source conv's epilogue
         elif l.kind == "pool":
