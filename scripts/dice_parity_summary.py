@@ -30,7 +30,11 @@ def loss_gap(a, b):
         out.append(statistics.mean(abs(la[s] - lb[s]) for s in steps) / statistics.mean(lb[s] for s in steps))
     return statistics.mean(out)
 
-out = ["# Dice parity, hard synthetic task (1x MI355X, 128x128x4, global batch 32, lr 5e-4, seeds %s)" % seeds, "",
+# (the header names what was run: the upsampling pair is 1-channel at UPS_LR, default 1e-4)
+only_ups = all(f in ("native_ups", "aten_ups") for _, f in runs)
+desc = ("upsampling decoder, 128x128x1, global batch 32, lr %s" % os.environ.get("UPS_LR", "1e-4") if only_ups else
+        "128x128x4, global batch 32, lr 5e-4; upsampling pair: 1 channel, lr %s" % os.environ.get("UPS_LR", "1e-4"))
+out = ["# Dice parity, hard synthetic task (1x MI355X, %s, seeds %s)" % (desc, seeds), "",
        "`scripts/gpu_dice_parity.sh`: per seed the same run (init, data order, dropout streams) through five",
        "paths; test Dice from `Trainer.evaluate` (all full test batches, sharded and allreduced).", "",
        "| run | seed | test Dice per epoch (step: dice) | final test Dice |", "|---|---|---|---|"] + rows

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 b512=${1-16 32 64 128}; b3=${2-8 12 16}
 o=gpurun_out/r5cfg; mkdir -p $o; : > $o/configs.jsonl
 run() { tag=$1; shift
-  timeout -k 10 300 python bench.py "$@" > $o/$tag.log 2>&1 || { echo "bench $tag rc=$?"; tail -20 $o/$tag.log; exit 1; }
+  timeout -k 10 600 python bench.py "$@" > $o/$tag.log 2>&1 || { echo "bench $tag rc=$?"; tail -20 $o/$tag.log; exit 1; }
   python - "$tag" "$o/$tag.log" "$*" >> $o/configs.jsonl <<'PY'
 import json, sys
 sys.path.insert(0, "tools")
@@ -29,3 +29,6 @@ run gn16 --norm group --dtype fp16 --steps 10 --warmup 3
 run ups --use_upsampling --in_channels 1 --steps 10 --warmup 3; }
 for b in $b512; do run s512_b$b --img_size 512 --in_channels 1 --per_gpu_batch $b --steps 8 --warmup 3; done
 for b in $b3; do run d3_b$b --dims 3 --per_gpu_batch $b --steps 5 --warmup 2; done
+[ -n "$SKIP_FP32" ] || { run fp32_native --dtype fp32 --per_gpu_batch 128 --steps 5 --warmup 2
+export MIOPEN_FIND_MODE=NORMAL   # (FAST picks naive fp32 NHWC kernels: profiles/r5_aten_ups_kernels.md)
+run fp32_aten --dtype fp32 --backend torch --per_gpu_batch 128 --steps 5 --warmup 2; }

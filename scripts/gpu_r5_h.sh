@@ -9,7 +9,7 @@ o=gpurun_out/r5h; mkdir -p $o
 hb=$!
 trap "kill $hb 2>/dev/null" EXIT
 timeout -k 10 600 python -u -m pytest "tests/test_gpu_kernels.py::test_conv_first_layer_smallc" \
-  "tests/test_gpu_model.py::test_two_stream_forward_equals_one_stream" tests/test_gpu_norm_fused.py \
+  "tests/test_gpu_model.py::test_two_stream_forward_equals_one_stream" tests/test_gpu_norm_fused.py tests/test_gpu_f32.py \
   -q -s --timeout 300 --timeout-method thread > $o/tests.log 2>&1; rc=$?
 grep -E "passed|failed" $o/tests.log | tail -4
 [ $rc -gt 1 ] && { echo "tests crashed rc=$rc"; tail -30 $o/tests.log; exit 1; }
@@ -24,6 +24,12 @@ done
 timeout -k 10 300 python bench.py --img_size 512 --in_channels 1 --per_gpu_batch 32 --steps 8 --warmup 3 > $o/s512.log 2>&1 \
   || { echo "s512 rc=$?"; tail -20 $o/s512.log; exit 1; }
 grep '^{' $o/s512.log | cut -c1-160
+for cfg in "" "--use_upsampling --in_channels 1"; do
+  timeout -k 10 300 python bench.py --dtype fp32 --per_gpu_batch 128 --steps 5 --warmup 2 $cfg > $o/f32.log 2>&1 \
+    || { echo "native fp32 rc=$?"; tail -20 $o/f32.log; exit 1; }
+  echo "native fp32 [$cfg]: $(grep '^{' $o/f32.log | cut -c1-120)"
+  cp $o/f32.log "$o/f32_${cfg// /_}.log"
+done
 export MIOPEN_FIND_MODE=NORMAL
 timeout -k 10 600 python bench.py --dtype fp32 --backend torch --per_gpu_batch 128 --steps 5 --warmup 2 > $o/aten32_normal.log 2>&1 \
   || { echo "aten fp32 normal rc=$?"; tail -20 $o/aten32_normal.log; exit 1; }

@@ -1,0 +1,104 @@
+"""Per-layer oracle at the benched shape (per-GPU batch 1024, 128x128x4, bf16): one native
+training step, then every conv layer whose operands the plan materialises is recomputed
+from the captured tensors in fp32 (shifted-tap GEMMs on rocBLAS, no MIOpen): forward
+outputs (first 64 images) and weight gradients over the whole batch -- the split-K sizing
+(`wg_target`), window choices and 2 GiB chunking of the bench shape, which the whole-step
+ATen parity (B <= 256) never reaches.  Dropout off (the oracle has no mask stream); the
+kernels and plan are otherwise the benched ones."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from test_gpu_model import _setup
+
+pytestmark = pytest.mark.gpu
+NS = 64                      # images of the forward check
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-30)).item()
+
+
+def _taps(x):
+    """3x3 'same' taps of NHWC x as [(dh, dw, [P, C] shifted copy)]."""
+    N, H, W, C = x.shape
+    xp = F.pad(x, (0, 0, 1, 1, 1, 1))
+    for dh in range(3):
+        for dw in range(3):
+            yield dh, dw, xp[:, dh:dh + H, dw:dw + W, :].reshape(-1, C)
+
+
+@pytest.fixture(scope="module")
+def stepped(cuda_dev):
+    spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, batch_size=1024, img_size=128, in_channels=4, dropout=0.0)
+    nb.fwd_bwd(x, y, seed=11)
+    torch.cuda.synchronize()
+    return spec, fn, nb.engine
+
+
+def _inputs(e, spec, name):
+    """The conv's input as an NHWC fp32 tensor (u first, then the skip), or None when the
+    plan does not materialise it (a transposed conv formed on load)."""
+    src1, up1, skip = e.inputs[name]
+    if up1 != 1 or src1 not in e.bufs or src1 in getattr(e, "_ut_onload", {}).values():
+        return None
+    if name in getattr(e, "_ut_onload", {}):
+        return None
+    parts = [e.bufs[src1]] + ([e.bufs[skip]] if skip else [])
+    return parts
+
+
+def test_bench_shape_forward_per_layer(stepped):
+    spec, fn, e = stepped
+    checked = 0
+    for l in spec.layers:
+        if l.kind != "conv":
+            continue
+        parts = _inputs(e, spec, l.name)
+        if parts is None:
+            continue
+        xin = torch.cat([p[:NS].float() for p in parts], -1)
+        w = fn.view(fn.master, l.name + "/kernel").bfloat16().float()          # [3, 3, Cin, Cout]
+        b = fn.view(fn.master, l.name + "/bias").float()
+        Cin = w.shape[2]
+        xin = xin[..., :Cin] if xin.shape[-1] > Cin else xin
+        if xin.shape[-1] < Cin:      # first layer: channel-padded input buffer
+            xin = F.pad(xin, (0, Cin - xin.shape[-1]))
+        out = torch.zeros(xin.shape[0] * xin.shape[1] * xin.shape[2], w.shape[3], device=xin.device)
+        for dh, dw, xs in _taps(xin):
+            out += xs @ w[dh, dw]
+        ref = F.relu(out + b).reshape(*xin.shape[:3], -1)
+        got = e.bufs[l.name][:NS].float()
+        err = _rel(got, ref)
+        assert err < 2e-2, (l.name, err)
+        checked += 1
+    assert checked >= 12
+
+
+def test_bench_shape_weight_gradients_per_layer(stepped):
+    spec, fn, e = stepped
+    checked = []
+    for l in spec.layers:
+        if l.kind != "conv" or ("d:" + l.name) not in e.bufs:
+            continue
+        parts = _inputs(e, spec, l.name)
+        if parts is None:
+            continue
+        g = fn.view(fn.grad, l.name + "/kernel").float()                       # [3, 3, Cin, Cout]
+        Cin, Cout = g.shape[2], g.shape[3]
+        dy = e.bufs["d:" + l.name].float().reshape(-1, Cout)
+        xin = torch.cat([p.float() for p in parts], -1)
+        if xin.shape[-1] < Cin:
+            xin = F.pad(xin, (0, Cin - xin.shape[-1]))
+        ref = torch.zeros_like(g)
+        for dh, dw, xs in _taps(xin[..., :Cin]):
+            ref[dh, dw] = xs.t() @ dy
+        err = _rel(g, ref)
+        assert err < 2e-2, (l.name, err)
+        gb = fn.view(fn.grad, l.name + "/bias").float()
+        assert _rel(gb, dy.sum(0)) < 2e-2, l.name
+        checked.append(l.name)
+        del xin, dy
+    print("bench-shape weight gradients checked:", checked)
+    assert len(checked) >= 8

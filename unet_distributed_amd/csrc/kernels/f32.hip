@@ -60,22 +60,24 @@ __global__ void __launch_bounds__(FT) f32_conv_kernel(const F32Conv p) {
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const bool vec = (Cin % 4) == 0 && (p.C1 % 4) == 0;
   const bool wvec = (p.ldw % 4) == 0 && (((uintptr_t)p.wgt) & 15) == 0;
-  for (int k0 = 0; k0 < K; k0 += FBK) {
-    float av[4];
+  // A loader state of this thread's k = k0 + ak: (tap, c) advanced incrementally by FBK per
+  // step (no per-step divisions), tap -> (kd, kh, kw) likewise
+  int a_tap = ak / Cin, a_c = ak - (ak / Cin) * Cin;
+  int a_kw = a_tap % p.KW, a_kh = (a_tap / p.KW) % p.KH, a_kd = a_tap / (p.KW * p.KH);
+  const int padd = p.KD > 1 ? p.pad : 0;
+  float av[4], bv[4];
+  auto load = [&](const int k0) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) av[e] = 0.f;
+    for (int e = 0; e < 4; ++e) av[e] = bv[e] = 0.f;
     if (q < M) {
       if (vec) {
-        const int k = k0 + ak;
-        if (k < K) {
-          const int tap = k / Cin, c = k - tap * Cin;
-          const int kw = tap % p.KW, kh = (tap / p.KW) % p.KH, kd = tap / (p.KW * p.KH);
-          const int id = qd * p.stride + kd - (p.KD > 1 ? p.pad : 0);
-          const int ih = qh * p.stride + kh - p.pad, iw = qw * p.stride + kw - p.pad;
+        if (k0 + ak < K) {
+          const int id = qd * p.stride + a_kd - padd;
+          const int ih = qh * p.stride + a_kh - p.pad, iw = qw * p.stride + a_kw - p.pad;
           if ((unsigned)id < (unsigned)p.ID && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW) {
             const size_t pix = (((size_t)qn * p.ID + id) * p.IH + ih) * p.IW + iw;
-            const f32x4 v = c < p.C1 ? *(const f32x4*)(p.src1 + pix * p.C1 + c)
-                                     : *(const f32x4*)(p.src2 + pix * p.C2 + (c - p.C1));
+            const f32x4 v = a_c < p.C1 ? *(const f32x4*)(p.src1 + pix * p.C1 + a_c)
+                                       : *(const f32x4*)(p.src2 + pix * p.C2 + (a_c - p.C1));
 #pragma unroll
             for (int e = 0; e < 4; ++e) av[e] = v[e];
           }
@@ -87,7 +89,7 @@ __global__ void __launch_bounds__(FT) f32_conv_kernel(const F32Conv p) {
           if (k >= K) continue;
           const int tap = k / Cin, c = k - tap * Cin;
           const int kw = tap % p.KW, kh = (tap / p.KW) % p.KH, kd = tap / (p.KW * p.KH);
-          const int id = qd * p.stride + kd - (p.KD > 1 ? p.pad : 0);
+          const int id = qd * p.stride + kd - padd;
           const int ih = qh * p.stride + kh - p.pad, iw = qw * p.stride + kw - p.pad;
           if ((unsigned)id < (unsigned)p.ID && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW) {
             const size_t pix = (((size_t)qn * p.ID + id) * p.IH + ih) * p.IW + iw;
@@ -96,28 +98,44 @@ __global__ void __launch_bounds__(FT) f32_conv_kernel(const F32Conv p) {
         }
       }
     }
-    float bv[4];
-    {
-      const int k = k0 + bk;
+    const int k = k0 + bk;
+    if (k < K) {
+      if (wvec && n0 + bn + 4 <= p.Cout) {
+        const f32x4 v = *(const f32x4*)(p.wgt + (size_t)k * p.ldw + n0 + bn);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bv[e] = 0.f;
-      if (k < K) {
-        if (wvec && n0 + bn + 4 <= p.Cout) {
-          const f32x4 v = *(const f32x4*)(p.wgt + (size_t)k * p.ldw + n0 + bn);
+        for (int e = 0; e < 4; ++e) bv[e] = v[e];
+      } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) bv[e] = v[e];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (n0 + bn + e < p.Cout) bv[e] = p.wgt[(size_t)k * p.ldw + n0 + bn + e];
+        for (int e = 0; e < 4; ++e)
+          if (n0 + bn + e < p.Cout) bv[e] = p.wgt[(size_t)k * p.ldw + n0 + bn + e];
+      }
+    }
+  };
+  auto advance = [&]() {
+    a_c += FBK;
+    while (a_c >= Cin) {
+      a_c -= Cin;
+      if (++a_kw == p.KW) {
+        a_kw = 0;
+        if (++a_kh == p.KH) {
+          a_kh = 0;
+          ++a_kd;
         }
       }
     }
+  };
+  // register prefetch: the next K step's global loads are in flight under this step's MFMAs
+  load(0);
+  for (int k0 = 0; k0 < K; k0 += FBK) {
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < 4; ++e) As[am][ak + e] = av[e];
     *(f32x4*)&Bs[bk][bn] = (f32x4){bv[0], bv[1], bv[2], bv[3]};
     __syncthreads();
+    if (k0 + FBK < K) {
+      advance();
+      load(k0 + FBK);
+    }
 #pragma unroll
     for (int ks = 0; ks < FBK / 4; ++ks) {
       const int kk = ks * 4 + (lane >> 4);
@@ -199,20 +217,28 @@ __global__ void __launch_bounds__(FT) f32_wgrad_kernel(const F32Wgrad p) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int q0 = q_begin; q0 < q_end; q0 += FBK) {
+  // this thread's pixel q = q0 + lr as (n, d, h, w), advanced incrementally by FBK per step
+  int qw_ = 0, qh_ = 0, qd_ = 0, qn_ = 0;
+  {
+    int t = q_begin + lr;
+    qw_ = t % p.QW;
+    t /= p.QW;
+    qh_ = t % p.QH;
+    t /= p.QH;
+    qd_ = t % p.QD;
+    qn_ = t / p.QD;
+  }
+  const int padd = p.KD > 1 ? p.pad : 0;
+  float av[4], bv[4];
+  auto load = [&](const int q0) {
     const int q = q0 + lr;
-    float av[4] = {0.f, 0.f, 0.f, 0.f}, bv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) av[e] = bv[e] = 0.f;
     if (q < q_end) {
-      int t = q;
-      const int w = t % p.QW;
-      t /= p.QW;
-      const int h = t % p.QH;
-      t /= p.QH;
-      const int d = t % p.QD, n = t / p.QD;
-      const int ad = d * p.stride + kd - (p.KD > 1 ? p.pad : 0);
-      const int ah = h * p.stride + kh - p.pad, aw = w * p.stride + kw - p.pad;
+      const int ad = qd_ * p.stride + kd - padd;
+      const int ah = qh_ * p.stride + kh - p.pad, aw = qw_ * p.stride + kw - p.pad;
       if ((unsigned)ad < (unsigned)p.AD && (unsigned)ah < (unsigned)p.AH && (unsigned)aw < (unsigned)p.AW) {
-        const size_t pix = (((size_t)n * p.AD + ad) * p.AH + ah) * p.AW + aw;
+        const size_t pix = (((size_t)qn_ * p.AD + ad) * p.AH + ah) * p.AW + aw;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int m = m0 + lc + e;
@@ -226,10 +252,31 @@ __global__ void __launch_bounds__(FT) f32_wgrad_kernel(const F32Wgrad p) {
         if (n < p.Nc) bv[e] = p.b[(size_t)q * p.Nc + n];
       }
     }
+  };
+  auto advance = [&]() {
+    qw_ += FBK;
+    while (qw_ >= p.QW) {
+      qw_ -= p.QW;
+      if (++qh_ == p.QH) {
+        qh_ = 0;
+        if (++qd_ == p.QD) {
+          qd_ = 0;
+          ++qn_;
+        }
+      }
+    }
+  };
+  // register prefetch: the next pixel step's loads are in flight under this step's MFMAs
+  if (q_begin < q_end) load(q_begin);
+  for (int q0 = q_begin; q0 < q_end; q0 += FBK) {
     __syncthreads();
     *(f32x4*)&As[lr][lc] = (f32x4){av[0], av[1], av[2], av[3]};
     *(f32x4*)&Bs[lr][lc] = (f32x4){bv[0], bv[1], bv[2], bv[3]};
     __syncthreads();
+    if (q0 + FBK < q_end) {
+      advance();
+      load(q0 + FBK);
+    }
 #pragma unroll
     for (int ks = 0; ks < FBK / 4; ++ks) {
       const int kk = ks * 4 + (lane >> 4);
