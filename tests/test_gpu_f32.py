@@ -24,8 +24,11 @@ def transpose(w, T, A, B, flip):
 
 
 @pytest.mark.parametrize("N,H,C1,C2,Co,relu", [(2, 16, 32, 32, 64, 1), (1, 32, 4, 0, 32, 1), (2, 8, 1, 0, 32, 0),
-                                               (3, 16, 64, 0, 48, 1)])
+                                               (3, 16, 64, 0, 48, 1), (4, 128, 32, 32, 64, 1), (4, 128, 64, 0, 128, 0),
+                                               (5, 128, 32, 0, 32, 1)])
 def test_f32_conv3x3_fwd(cuda_dev, N, H, C1, C2, Co, relu):
+    """Tiles: 128 x 32 (Cout <= 32), 128 x 64 / 128 x 128 (M >= 64k pixels), 64 x 64; the
+    large shapes against the CPU (MIOpen's fp32 algorithms are no exact oracle there)."""
     torch.manual_seed(H + C1)
     dev = cuda_dev
     a = torch.randn(N, H, H, C1, device=dev)
@@ -37,10 +40,12 @@ def test_f32_conv3x3_fwd(cuda_dev, N, H, C1, C2, Co, relu):
                       src2=ptr(b) if C2 else None, wgt=ptr(w), bias=ptr(bias), Cout=Co, relu=relu, dst1=ptr(out)),
                  stream())
     xin = nchw(a) if not C2 else torch.cat([nchw(a), nchw(b)], 1)
-    ref = nhwc(F.conv2d(xin, w.permute(3, 2, 0, 1), bias, padding=1))
+    cpu = H >= 128
+    dv = "cpu" if cpu else dev
+    ref = nhwc(F.conv2d(xin.to(dv), w.permute(3, 2, 0, 1).to(dv), bias.to(dv), padding=1))
     if relu:
         ref = F.relu(ref)
-    assert rel(out, ref) < TOL
+    assert rel(out.to(dv), ref) < TOL
 
 
 def test_f32_conv3d_fwd(cuda_dev):
@@ -56,13 +61,16 @@ def test_f32_conv3d_fwd(cuda_dev):
     assert rel(out, ref) < TOL
 
 
-def test_f32_conv_dgrad_and_wgrad(cuda_dev):
+@pytest.mark.parametrize("C1,C2,Co", [(32, 32, 32), (32, 0, 32), (32, 0, 64), (64, 0, 64), (64, 64, 128),
+                                      (4, 0, 32), (1, 0, 32)])
+def test_f32_conv_dgrad_and_wgrad(cuda_dev, C1, C2, Co):
     """Data gradient = conv of dY with the flipped, transposed kernel (f32_transpose) and the
     ReLU mask of the producer; weight gradient = per-tap split-K slabs (+ the fixed-order
-    slab reduction)."""
+    slab reduction): channel-sized tiles 32 / 64 (f32_wgrad_cs_kernel, K split over the
+    waves) and the generic 64 x 64 tile (channel counts not multiples of 4)."""
     torch.manual_seed(4)
     dev = cuda_dev
-    N, H, C1, C2, Co = 2, 32, 32, 32, 32
+    N, H = 2, 32
     xa = F.relu(torch.randn(N, H, H, C1, device=dev))
     xb = F.relu(torch.randn(N, H, H, C2, device=dev))
     w = torch.randn(3, 3, C1 + C2, Co, device=dev) * 0.1

@@ -28,36 +28,46 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// A tile = im2col rows (pixels) x K slice; B tile = weight rows [k][Cout]
+// A tile = im2col rows (pixels) x K slice; B tile = weight rows [k][Cout].  Tiles (BM, BN)
+// with 4 waves in a WGM x WGN grid, each wave MI x NJ 16 x 16 MFMA tiles: (128, 32) for
+// Cout <= 32 (4 x 1 waves of 32 x 32 -- the 64-wide N tile left half of its MFMAs on zero
+// columns at the level-1 convs), (128, 64) / (128, 128) (2 x 2 waves of 64 x 32 / 64 x 64:
+// 2-4x the MFMAs per LDS and global byte of the 64 x 64 tile), (64, 64) for small M.
+template <int BM, int BN>
 __global__ void __launch_bounds__(FT) f32_conv_kernel(const F32Conv p) {
-  __shared__ float As[FBM][FBK + 1];
-  __shared__ float Bs[FBK][FBN];
+  constexpr int RA = BM / 64;                  // pixel rows per thread in the A loader
+  constexpr int WGN = BN == 32 ? 1 : 2, WGM = 4 / WGN;
+  constexpr int MI = BM / WGM / 16, NJ = BN / WGN / 16;
+  constexpr int BVN = BN / 16;                 // B floats per thread (k row tid >> 4)
+  __shared__ float As[BM][FBK + 1];
+  __shared__ float Bs[FBK][BN];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave - wm * WGN;
   const int M = p.N * p.OD * p.OH * p.OW;
   const int Cin = p.C1 + p.C2;
   const int K = p.KD * p.KH * p.KW * Cin;
-  const int m0 = blockIdx.x * FBM, n0 = blockIdx.y * FBN;
-  // A loader: thread -> (pixel row, 4 consecutive k)
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  // A loader: thread -> (pixel rows am + 64 r, 4 consecutive k)
   const int am = tid >> 2, ak = (tid & 3) * 4;
-  const int q = m0 + am;
-  int qn = 0, qd = 0, qh = 0, qw = 0;
-  {
-    int t = q < M ? q : 0;
-    qw = t % p.OW;
+  int qv[RA], qn[RA], qd[RA], qh[RA], qw[RA];
+#pragma unroll
+  for (int r = 0; r < RA; ++r) {
+    qv[r] = m0 + am + 64 * r;
+    int t = qv[r] < M ? qv[r] : 0;
+    qw[r] = t % p.OW;
     t /= p.OW;
-    qh = t % p.OH;
+    qh[r] = t % p.OH;
     t /= p.OH;
-    qd = t % p.OD;
-    qn = t / p.OD;
+    qd[r] = t % p.OD;
+    qn[r] = t / p.OD;
   }
-  // B loader: thread -> (k row, 4 consecutive n)
-  const int bk = tid >> 4, bn = (tid & 15) * 4;
-  f32x4 acc[2][2];
+  // B loader: thread -> (k row, BVN consecutive n)
+  const int bk = tid >> 4, bn = (tid & 15) * BVN;
+  f32x4 acc[MI][NJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const bool vec = (Cin % 4) == 0 && (p.C1 % 4) == 0;
   const bool wvec = (p.ldw % 4) == 0 && (((uintptr_t)p.wgt) & 15) == 0;
   // A loader state of this thread's k = k0 + ak: (tap, c) advanced incrementally by FBK per
@@ -65,21 +75,23 @@ __global__ void __launch_bounds__(FT) f32_conv_kernel(const F32Conv p) {
   int a_tap = ak / Cin, a_c = ak - (ak / Cin) * Cin;
   int a_kw = a_tap % p.KW, a_kh = (a_tap / p.KW) % p.KH, a_kd = a_tap / (p.KW * p.KH);
   const int padd = p.KD > 1 ? p.pad : 0;
-  float av[4], bv[4];
+  float av[RA][4], bv[BVN];
   auto load = [&](const int k0) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) av[e] = bv[e] = 0.f;
-    if (q < M) {
+    for (int r = 0; r < RA; ++r) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) av[r][e] = 0.f;
+      if (qv[r] >= M) continue;
       if (vec) {
         if (k0 + ak < K) {
-          const int id = qd * p.stride + a_kd - padd;
-          const int ih = qh * p.stride + a_kh - p.pad, iw = qw * p.stride + a_kw - p.pad;
+          const int id = qd[r] * p.stride + a_kd - padd;
+          const int ih = qh[r] * p.stride + a_kh - p.pad, iw = qw[r] * p.stride + a_kw - p.pad;
           if ((unsigned)id < (unsigned)p.ID && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW) {
-            const size_t pix = (((size_t)qn * p.ID + id) * p.IH + ih) * p.IW + iw;
+            const size_t pix = (((size_t)qn[r] * p.ID + id) * p.IH + ih) * p.IW + iw;
             const f32x4 v = a_c < p.C1 ? *(const f32x4*)(p.src1 + pix * p.C1 + a_c)
                                        : *(const f32x4*)(p.src2 + pix * p.C2 + (a_c - p.C1));
 #pragma unroll
-            for (int e = 0; e < 4; ++e) av[e] = v[e];
+            for (int e = 0; e < 4; ++e) av[r][e] = v[e];
           }
         }
       } else {
@@ -89,24 +101,29 @@ __global__ void __launch_bounds__(FT) f32_conv_kernel(const F32Conv p) {
           if (k >= K) continue;
           const int tap = k / Cin, c = k - tap * Cin;
           const int kw = tap % p.KW, kh = (tap / p.KW) % p.KH, kd = tap / (p.KW * p.KH);
-          const int id = qd * p.stride + kd - padd;
-          const int ih = qh * p.stride + kh - p.pad, iw = qw * p.stride + kw - p.pad;
+          const int id = qd[r] * p.stride + kd - padd;
+          const int ih = qh[r] * p.stride + kh - p.pad, iw = qw[r] * p.stride + kw - p.pad;
           if ((unsigned)id < (unsigned)p.ID && (unsigned)ih < (unsigned)p.IH && (unsigned)iw < (unsigned)p.IW) {
-            const size_t pix = (((size_t)qn * p.ID + id) * p.IH + ih) * p.IW + iw;
-            av[e] = c < p.C1 ? p.src1[pix * p.C1 + c] : p.src2[pix * p.C2 + (c - p.C1)];
+            const size_t pix = (((size_t)qn[r] * p.ID + id) * p.IH + ih) * p.IW + iw;
+            av[r][e] = c < p.C1 ? p.src1[pix * p.C1 + c] : p.src2[pix * p.C2 + (c - p.C1)];
           }
         }
       }
     }
+#pragma unroll
+    for (int e = 0; e < BVN; ++e) bv[e] = 0.f;
     const int k = k0 + bk;
     if (k < K) {
-      if (wvec && n0 + bn + 4 <= p.Cout) {
-        const f32x4 v = *(const f32x4*)(p.wgt + (size_t)k * p.ldw + n0 + bn);
+      if (wvec && BVN >= 4 && n0 + bn + BVN <= p.Cout) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) bv[e] = v[e];
+        for (int h = 0; h < BVN / 4; ++h) {
+          const f32x4 v = *(const f32x4*)(p.wgt + (size_t)k * p.ldw + n0 + bn + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bv[4 * h + e] = v[e];
+        }
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int e = 0; e < BVN; ++e)
           if (n0 + bn + e < p.Cout) bv[e] = p.wgt[(size_t)k * p.ldw + n0 + bn + e];
       }
     }
@@ -129,8 +146,11 @@ __global__ void __launch_bounds__(FT) f32_conv_kernel(const F32Conv p) {
   for (int k0 = 0; k0 < K; k0 += FBK) {
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < 4; ++e) As[am][ak + e] = av[e];
-    *(f32x4*)&Bs[bk][bn] = (f32x4){bv[0], bv[1], bv[2], bv[3]};
+    for (int r = 0; r < RA; ++r)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) As[am + 64 * r][ak + e] = av[r][e];
+#pragma unroll
+    for (int e = 0; e < BVN; ++e) Bs[bk][bn + e] = bv[e];
     __syncthreads();
     if (k0 + FBK < K) {
       advance();
@@ -139,32 +159,32 @@ __global__ void __launch_bounds__(FT) f32_conv_kernel(const F32Conv p) {
 #pragma unroll
     for (int ks = 0; ks < FBK / 4; ++ks) {
       const int kk = ks * 4 + (lane >> 4);
-      float a[2], b[2];
+      float a[MI], b[NJ];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = As[wm * 32 + i * 16 + (lane & 15)][kk];
+      for (int i = 0; i < MI; ++i) a[i] = As[wm * (16 * MI) + i * 16 + (lane & 15)][kk];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = Bs[kk][wn * 32 + j * 16 + (lane & 15)];
+      for (int j = 0; j < NJ; ++j) b[j] = Bs[kk][wn * (16 * NJ) + j * 16 + (lane & 15)];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma4(a[i], b[j], acc[i][j]);
     }
   }
-  // epilogue: acc[i][j][r] = out[pixel m0 + wm 32 + 16 i + 4 (lane >> 4) + r][chan n0 + wn 32 + 16 j + (lane & 15)]
+  // epilogue: acc[i][j][r] = out[pixel m0 + wm 16 MI + 16 i + 4 (lane >> 4) + r][chan n0 + wn 16 NJ + 16 j + (lane & 15)]
   const float inv_keep = p.drop_rate > 0.f ? 1.f / (1.f - p.drop_rate) : 1.f;
   const uint32_t thr = (uint32_t)(p.drop_rate * 4294967296.0);
   const uint32_t seed = p.seed_ptr ? *p.seed_ptr : p.seed;
   const int Dt = p.shuffle ? p.Cout >> p.shuffle : p.Cout;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+  for (int j = 0; j < NJ; ++j) {
+    const int n = n0 + wn * (16 * NJ) + j * 16 + (lane & 15);
     if (n >= p.Cout) continue;
     const float bias = p.bias ? p.bias[p.shuffle ? n % Dt : n] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int qq = m0 + wm * 32 + i * 16 + 4 * (lane >> 4) + r;
+        const int qq = m0 + wm * (16 * MI) + i * 16 + 4 * (lane >> 4) + r;
         if (qq >= M) continue;
         float v = acc[i][j][r] + bias;
         if (p.relu) v = fmaxf(v, 0.f);
@@ -300,6 +320,146 @@ __global__ void __launch_bounds__(FT) f32_wgrad_kernel(const F32Wgrad p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * 32 + i * 16 + 4 * (lane >> 4) + r;
+        if (m < Mt && n < p.Nc) p.slab[(((size_t)split * taps + tap) * Mt + m) * p.Nc + n] = acc[i][j][r];
+      }
+    }
+}
+
+// Weight gradient with channel-sized tiles (BM, BN in {32, 64}; every channel count % 4 == 0):
+// the 64 x 64 tile of f32_wgrad_kernel leaves 3/4 of its MFMAs on zeros at 32 x 32 (the
+// level-1 convs -- 2.2 ms per launch, round-5 fp32 profile).  The 4 waves form a
+// (BM / 32) x (BN / 32) grid of 32 x 32 sub-tiles and split each step's KR = 16 WK pixels
+// WK ways; the WK partial tiles are summed in fixed order through LDS at the end.  One
+// pixel state per thread: thread t loads row t / TPR, its 1 / TPR share of the A row (BM
+// channels) and of the B row (BN channels) as float4s; the row's pixel is advanced by KR
+// per step without divisions; the next step's loads are in flight under the MFMAs.
+template <int BM, int BN>
+__global__ void __launch_bounds__(FT) f32_wgrad_cs_kernel(const F32Wgrad p) {
+  // wave sub-tiles SM x SN (64 x 64 in the 128 x 128 tile: 4x the MFMAs per LDS read of 32 x 32)
+  constexpr int SM = BM == 128 ? 64 : 32, SN = BN == 128 ? 64 : 32, MI = SM / 16, NJ = SN / 16;
+  constexpr int WGM = BM / SM, WGN = BN / SN, WK = 4 / (WGM * WGN), KR = FBK * WK, TPR = FT / KR;
+  constexpr int AV = BM / TPR / 4, BV = BN / TPR / 4;        // float4s per thread and row
+  static_assert(AV >= 1 && BV >= 1, "channel share per thread");
+  __shared__ float As[KR][BM + 4];
+  __shared__ float Bs[KR][BN + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wk = wave / (WGM * WGN), wr = wave - wk * (WGM * WGN), wm = wr / WGN, wn = wr - wm * WGN;
+  const int Mt = p.M1 + p.M2;
+  const int ntn = (p.Nc + BN - 1) / BN;
+  const int m0 = (blockIdx.x / ntn) * BM, n0 = (blockIdx.x % ntn) * BN;
+  const int tap = blockIdx.y, split = blockIdx.z;
+  const int kw = tap % p.KW, kh = (tap / p.KW) % p.KH, kd = tap / (p.KW * p.KH);
+  const int Q = p.N * p.QD * p.QH * p.QW;
+  const int q_begin = (int)((long long)split * Q / p.splits), q_end = (int)((long long)(split + 1) * Q / p.splits);
+  const int lr = tid / TPR, sub = tid - lr * TPR;
+  int qw_ = 0, qh_ = 0, qd_ = 0, qn_ = 0;
+  {
+    int t = q_begin + lr;
+    qw_ = t % p.QW;
+    t /= p.QW;
+    qh_ = t % p.QH;
+    t /= p.QH;
+    qd_ = t % p.QD;
+    qn_ = t / p.QD;
+  }
+  const int padd = p.KD > 1 ? p.pad : 0;
+  f32x4 av[AV], bv[BV];
+  auto load = [&](const int q0) {
+    const int q = q0 + lr;
+#pragma unroll
+    for (int v = 0; v < AV; ++v) av[v] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int v = 0; v < BV; ++v) bv[v] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (q < q_end) {
+      const int ad = qd_ * p.stride + kd - padd;
+      const int ah = qh_ * p.stride + kh - p.pad, aw = qw_ * p.stride + kw - p.pad;
+      if ((unsigned)ad < (unsigned)p.AD && (unsigned)ah < (unsigned)p.AH && (unsigned)aw < (unsigned)p.AW) {
+        const size_t pix = (((size_t)qn_ * p.AD + ad) * p.AH + ah) * p.AW + aw;
+#pragma unroll
+        for (int v = 0; v < AV; ++v) {
+          const int m = m0 + (sub * AV + v) * 4;
+          if (m < p.M1) av[v] = *(const f32x4*)(p.a1 + pix * p.M1 + m);
+          else if (m < Mt) av[v] = *(const f32x4*)(p.a2 + pix * p.M2 + (m - p.M1));
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < BV; ++v) {
+        const int n = n0 + (sub * BV + v) * 4;
+        if (n < p.Nc) bv[v] = *(const f32x4*)(p.b + (size_t)q * p.Nc + n);
+      }
+    }
+  };
+  auto advance = [&]() {
+    qw_ += KR;
+    while (qw_ >= p.QW) {
+      qw_ -= p.QW;
+      if (++qh_ == p.QH) {
+        qh_ = 0;
+        if (++qd_ == p.QD) {
+          qd_ = 0;
+          ++qn_;
+        }
+      }
+    }
+  };
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (q_begin < q_end) load(q_begin);
+  for (int q0 = q_begin; q0 < q_end; q0 += KR) {
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < AV; ++v) *(f32x4*)&As[lr][(sub * AV + v) * 4] = av[v];
+#pragma unroll
+    for (int v = 0; v < BV; ++v) *(f32x4*)&Bs[lr][(sub * BV + v) * 4] = bv[v];
+    __syncthreads();
+    if (q0 + KR < q_end) {
+      advance();
+      load(q0 + KR);
+    }
+#pragma unroll
+    for (int ks = 0; ks < FBK / 4; ++ks) {
+      const int kk = wk * FBK + ks * 4 + (lane >> 4);
+      float a[MI], b[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = As[kk][wm * SM + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) b[j] = Bs[kk][wn * SN + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma4(a[i], b[j], acc[i][j]);
+    }
+  }
+  if constexpr (WK > 1) {
+    static_assert(MI == 2 && NJ == 2, "K-split tiles are 32 x 32 per wave");
+    // the K-split partial tiles: red[fragment][wave][lane] (fragment-major: lanes 16 B apart)
+    __shared__ f32x4 red[4][4][64];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) red[i * 2 + j][wave][lane] = acc[i][j];
+    __syncthreads();
+    if (wk != 0) return;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int o = 1; o < WK; ++o) acc[i][j] += red[i * 2 + j][o * (WGM * WGN) + wr][lane];
+  }
+  const int taps = p.KD * p.KH * p.KW;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = n0 + wn * SN + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * SM + i * 16 + 4 * (lane >> 4) + r;
         if (m < Mt && n < p.Nc) p.slab[(((size_t)split * taps + tap) * Mt + m) * p.Nc + n] = acc[i][j][r];
       }
     }
@@ -461,47 +621,75 @@ __global__ void __launch_bounds__(FT) f32_head_bwd_kernel(const float* __restric
                                                           const float* __restrict__ sums, int P,
                                                           float inv_total, float bce_w, float* __restrict__ dx,
                                                           float* __restrict__ partial) {
-  __shared__ float sh[FT / 64][C + 1];
+  // G = C / 4 consecutive threads per pixel, one float4 channel group each: the pixel's
+  // row is read and written as contiguous 16-byte pieces (one thread per pixel walking its
+  // C channels made every load a 64-line gather: 1.7 ms for 268 MB, round-5 fp32 profile)
+  constexpr int G = C / 4, PPB = FT / G;
+  __shared__ f32x4 red[FT];
+  __shared__ float redb[FT];
   const float I = sums[0], St = sums[1], Sp = sums[2];
   const float a = -2.f / (2.f * I + 1.f), bb = 1.f / (St + Sp + 1.f);
-  float gw[C];
-#pragma unroll
-  for (int c = 0; c < C; ++c) gw[c] = 0.f;
+  const int g = threadIdx.x % G, pl = threadIdx.x / G;
+  const f32x4 wg = *(const f32x4*)(w + 4 * g);
+  f32x4 gw = (f32x4){0.f, 0.f, 0.f, 0.f};
   float gb = 0.f;
-  for (int px = blockIdx.x * FT + threadIdx.x; px < P; px += gridDim.x * FT) {
+  for (long long px = (long long)blockIdx.x * PPB + pl; px < P; px += (long long)gridDim.x * PPB) {
     const float pr = prob[px], tv = t[px];
     const float dice = fmaf(a, tv, bb) * pr * (1.f - pr);
     const float dz = fmaf(bce_w * (pr - tv), inv_total, dice);
-    gb += dz;
+    if (g == 0) gb += dz;
+    const f32x4 xv = *(const f32x4*)(x + px * C + 4 * g);
+    gw += dz * xv;
+    if (dx) {
+      f32x4 o;
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const float xv = x[(size_t)px * C + c];
-      gw[c] = fmaf(dz, xv, gw[c]);
-      if (dx) dx[(size_t)px * C + c] = xv > 0.f ? dz * w[c] : 0.f;
+      for (int e = 0; e < 4; ++e) o[e] = xv[e] > 0.f ? dz * wg[e] : 0.f;
+      *(f32x4*)(dx + px * C + 4 * g) = o;
     }
   }
-  const int wv = threadIdx.x >> 6;
-#pragma unroll
-  for (int c = 0; c <= C; ++c) {
-    float v = wave_sum(c < C ? gw[c] : gb);
-    if ((threadIdx.x & 63) == 0) sh[wv][c] = v;
-  }
+  red[threadIdx.x] = gw;
+  redb[threadIdx.x] = gb;
   __syncthreads();
-  for (int c = threadIdx.x; c <= C; c += FT) {
-    float s = 0.f;
-    for (int k = 0; k < FT / 64; ++k) s += sh[k][c];
-    partial[(size_t)blockIdx.x * (C + 1) + c] = s;
+  // fixed-order sums over the threads of each channel group
+  if (threadIdx.x < G) {
+    f32x4 s4 = red[threadIdx.x];
+    for (int k = 1; k < PPB; ++k) s4 += red[k * G + threadIdx.x];
+    *(f32x4*)(partial + (size_t)blockIdx.x * (C + 1) + 4 * threadIdx.x) = s4;
+  } else if (threadIdx.x == G) {
+    float sb = 0.f;
+    for (int k = 0; k < PPB; ++k) sb += redb[k * G];
+    partial[(size_t)blockIdx.x * (C + 1) + C] = sb;
   }
 }
 
 // per-block column sums of x [rows][C] (bias gradients): partial[blk][C]
 __global__ void __launch_bounds__(FT) f32_colsum_kernel(const float* __restrict__ x, long long rows, int C,
                                                         float* __restrict__ partial) {
+  // C % 4 == 0, C <= 4 FT: a thread owns one float4 column group cg of row lane rl; the
+  // FT / (C / 4) row lanes stride the block's row range (4 rows in flight each), then the
+  // lanes' sums are added in fixed order through LDS.  (Round-5 profile: the previous
+  // one-thread-per-column loop -- C of 256 threads busy, one dependent load per row --
+  // took 3 ms per level-1 bias gradient, 28 % of the fp32 step.)
+  __shared__ f32x4 red[FT];
+  const int G = C >> 2, RL = FT / G;
+  const int cg = threadIdx.x % G, rl = threadIdx.x / G;
   const long long r0 = (long long)blockIdx.x * rows / gridDim.x, r1 = (long long)(blockIdx.x + 1) * rows / gridDim.x;
-  for (int c = threadIdx.x; c < C; c += FT) {
-    float s = 0.f;
-    for (long long r = r0; r < r1; ++r) s += x[r * C + c];
-    partial[(size_t)blockIdx.x * C + c] = s;
+  f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (rl < RL) {
+    long long r = r0 + rl;
+    for (; r + 3 * RL < r1; r += 4 * RL) {
+      const f32x4 a = *(const f32x4*)(x + r * C + 4 * cg), b = *(const f32x4*)(x + (r + RL) * C + 4 * cg);
+      const f32x4 c = *(const f32x4*)(x + (r + 2 * RL) * C + 4 * cg), d = *(const f32x4*)(x + (r + 3 * RL) * C + 4 * cg);
+      acc += (a + b) + (c + d);
+    }
+    for (; r < r1; r += RL) acc += *(const f32x4*)(x + r * C + 4 * cg);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x < G) {
+    f32x4 s = red[threadIdx.x];
+    for (int k = 1; k < RL; ++k) s += red[k * G + threadIdx.x];
+    *(f32x4*)(partial + (size_t)blockIdx.x * C + 4 * threadIdx.x) = s;
   }
 }
 
@@ -546,14 +734,45 @@ const char* f32_wgrad_check(const F32Wgrad& p) {
 
 hipError_t f32_conv_launch(const F32Conv& p, hipStream_t s) {
   const int M = p.N * p.OD * p.OH * p.OW;
-  UNET_LAUNCH(f32_conv_kernel, dim3((M + FBM - 1) / FBM, (p.Cout + FBN - 1) / FBN), dim3(FT), 0, s, p);
+  // (128-row tiles while they still give >= 2 workgroups per CU)
+  const int gm = (M + 127) / 128;
+  if (p.Cout <= 32)
+    UNET_LAUNCH((f32_conv_kernel<128, 32>), dim3(gm, 1), dim3(FT), 0, s, p);
+  else if (p.Cout <= 64 && gm >= 512)
+    UNET_LAUNCH((f32_conv_kernel<128, 64>), dim3(gm, 1), dim3(FT), 0, s, p);
+  else if (p.Cout % 128 == 0 && gm * (p.Cout / 128) >= 512)
+    UNET_LAUNCH((f32_conv_kernel<128, 128>), dim3(gm, p.Cout / 128), dim3(FT), 0, s, p);
+  else
+    UNET_LAUNCH((f32_conv_kernel<64, 64>), dim3((M + FBM - 1) / FBM, (p.Cout + FBN - 1) / FBN), dim3(FT), 0, s, p);
   return launch_status();
+}
+
+// tile of the weight gradient: (BM, BN) of f32_wgrad_cs_kernel when every channel count is a
+// multiple of 4 (float4 operand loads), else (0, 0): the generic 64 x 64 kernel
+void f32_wgrad_tile(int M1, int M2, int Nc, int* bm, int* bn) {
+  const bool vec = M1 % 4 == 0 && M2 % 4 == 0 && Nc % 4 == 0;
+  const bool big = (M1 + M2) % 128 == 0 && Nc % 128 == 0;     // 128 x 128: 4x4 MFMA tiles per wave
+  *bm = vec ? (big ? 128 : (M1 + M2 <= 32 ? 32 : 64)) : 0;
+  *bn = vec ? (big ? 128 : (Nc <= 32 ? 32 : 64)) : 0;
 }
 
 hipError_t f32_wgrad_launch(const F32Wgrad& p, hipStream_t s) {
   const int Mt = p.M1 + p.M2;
+  int bm, bn;
+  f32_wgrad_tile(p.M1, p.M2, p.Nc, &bm, &bn);
+  const dim3 gy(1, p.KD * p.KH * p.KW, p.splits);
+  if (bm) {
+    const int tiles = ((Mt + bm - 1) / bm) * ((p.Nc + bn - 1) / bn);
+    const dim3 g(tiles, gy.y, gy.z);
+    if (bm == 128) UNET_LAUNCH((f32_wgrad_cs_kernel<128, 128>), g, dim3(FT), 0, s, p);
+    else if (bm == 32 && bn == 32) UNET_LAUNCH((f32_wgrad_cs_kernel<32, 32>), g, dim3(FT), 0, s, p);
+    else if (bm == 32) UNET_LAUNCH((f32_wgrad_cs_kernel<32, 64>), g, dim3(FT), 0, s, p);
+    else if (bn == 32) UNET_LAUNCH((f32_wgrad_cs_kernel<64, 32>), g, dim3(FT), 0, s, p);
+    else UNET_LAUNCH((f32_wgrad_cs_kernel<64, 64>), g, dim3(FT), 0, s, p);
+    return launch_status();
+  }
   const int tiles = ((Mt + FBM - 1) / FBM) * ((p.Nc + FBN - 1) / FBN);
-  UNET_LAUNCH(f32_wgrad_kernel, dim3(tiles, p.KD * p.KH * p.KW, p.splits), dim3(FT), 0, s, p);
+  UNET_LAUNCH(f32_wgrad_kernel, dim3(tiles, gy.y, gy.z), dim3(FT), 0, s, p);
   return launch_status();
 }
 
@@ -624,7 +843,8 @@ hipError_t f32_head_bwd_launch(const float* x, const float* w, const float* prob
 hipError_t f32_colsum_launch(const float* x, long long rows, int C, int blocks, float* partial, float* out,
                              hipStream_t s) {
   UNET_LAUNCH(f32_colsum_kernel, dim3(blocks), dim3(FT), 0, s, x, rows, C, partial);
-  UNET_LAUNCH(f32_rows_sum_kernel, dim3((C + 255) / 256), dim3(256), 0, s, partial, blocks, C, out);
+  // stage 2: the same fixed-order kernel over the block partials, one block
+  UNET_LAUNCH(f32_colsum_kernel, dim3(1), dim3(FT), 0, s, (const float*)partial, (long long)blocks, C, out);
   return launch_status();
 }
 

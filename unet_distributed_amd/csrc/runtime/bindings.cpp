@@ -742,6 +742,7 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     float *pa = fp(1), *out = fp(2);
     long long rows = I[0];
     int c = I[1], nb = I[2];
+    if (c % 4 || c <= 0 || c > 1024 || nb < 1) throw std::invalid_argument("f32_colsum: C % 4 == 0, C <= 1024, blocks >= 1");
     return [=](hipStream_t s) { return unet::f32_colsum_launch(x, rows, c, nb, pa, out, s); };
   }
   if (kind == "f32_transpose") {
@@ -909,6 +910,11 @@ PYBIND11_MODULE(_C, m) {
     check(unet::f32_wgrad_launch(p, as_stream(stream)), "f32_wgrad");
   }, py::arg("params"), py::arg("stream") = 0);
   m.def("f32_head_blocks", &unet::f32_head_blocks);
+  m.def("f32_wgrad_tile", [](int M1, int M2, int Nc) {
+    int bm, bn;
+    unet::f32_wgrad_tile(M1, M2, Nc, &bm, &bn);
+    return py::make_tuple(bm, bn);
+  });
   m.def("head_blocks", &head_blocks_py);
   m.def("norm_blocks_per_sample", &norm_blocks_per_sample);
   m.def("sample_slices", &sample_slices);

@@ -232,7 +232,9 @@ class NativeUNetF32:
         """Weight gradient slabs -> fixed-order reduction into the kernel gradient; bias
         gradient by fixed-order column sums."""
         Q = geo["N"] * geo["QD"] * geo["QH"] * geo["QW"]
-        tiles = -(-(M1 + M2) // 64) * -(-Nc // 64) * taps
+        bm, bn = self.C.f32_wgrad_tile(M1, M2, Nc)      # (0, 0): the generic 64 x 64 tile
+        bm, bn = bm or 64, bn or 64
+        tiles = -(-(M1 + M2) // bm) * -(-Nc // bn) * taps
         splits = max(1, min(self.WG_SPLIT_TARGET // max(1, tiles) * 4, Q // 256, 512))
         slab = torch.empty(splits * taps * (M1 + M2) * Nc, dtype=torch.float32, device=self.device)
         self._keep.append(slab)
@@ -246,7 +248,7 @@ class NativeUNetF32:
                          [splits, taps, M1 + M2, M1 + M2, Nc], [1.0], "reduce:" + name)
         plan.annotate(reads=[_ptr(slab)], writes=[self.grad(kernel_var)])
         cw = self.flat.view(self.flat.master, bias_var).numel()
-        nblk = max(1, min(256, bias_rows // 256))
+        nblk = max(1, min(1024, bias_rows // 2048, self._colsum_part.numel() // cw))
         assert nblk * cw <= self._colsum_part.numel()
         plan.add_generic("f32_colsum", [_ptr(bias_src), _ptr(self._colsum_part), self.grad(bias_var)],
                          [bias_rows, cw, nblk], [], "bsum:" + name)
