@@ -384,7 +384,9 @@ def test_wgrad3d_row_window(cuda_dev, N, D, H, C1, C2, Cout, splits):
 
 @pytest.mark.parametrize("N,H,Creal,Cpad,Co,splits,win", [(2, 32, 1, 4, 32, 3, -1), (2, 32, 1, 4, 32, 3, 0),
                                                            (3, 128, 4, 4, 32, 7, 0), (2, 16, 3, 4, 64, 40, 0),
-                                                           (2, 64, 8, 8, 32, 5, 0), (2, 32, 5, 8, 32, 3, -1)])
+                                                           (2, 64, 8, 8, 32, 5, 0), (2, 32, 5, 8, 32, 3, -1),
+                                                           (2, 256, 1, 4, 32, 6, 0), (2, 512, 4, 4, 32, 9, 0),
+                                                           (1, 512, 8, 8, 64, 4, 0)])
 def test_wgrad_first_layer_smallc(cuda_dev, N, H, Creal, Cpad, Co, splits, win):
     """First-layer weight gradient: row-window kernel (win=0) and the tiled small-C mode
     (win=-1); padded channels dropped by the slab reduction's row remap."""

@@ -914,7 +914,8 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
   // neighbour RS slots on lands 64 bytes x 2 away from the row's own slots), and GEMM rows
   // past the ninth tap (discarded) read 16 slots on instead of the broadcast zero slot
   // (round 4: W + 4 = 132 -- 37.5 % of the kernel's LDS cycles were conflicts).
-  constexpr int BMW = 256, R = BMW / W, HR = R + 2, SB = 2 * CIN;
+  // (256-pixel windows; a window is one row on rows 512 wide -- the 512^2 model)
+  constexpr int BMW = W > 256 ? W : 256, R = BMW / W, HR = R + 2, SB = 2 * CIN;
   constexpr int RS = CIN == 4 ? ((W + 4 + 15) / 32) * 32 + 16 : W + 4, ROWB = RS * SB;
   constexpr int CPR = ROWB / 16;
   constexpr int XI = (HR * CPR + 63) / 64, YI = BMW / 16;
@@ -926,7 +927,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
   // the same banks -- 8-way; r5 PMC pass: 14.5 % conflict cycles)
   constexpr int REDB = 4 * 64 * (MT * 2 + 3) * 16;
   constexpr int LDS_BYTES = (XB + YB > REDB) ? XB + YB : REDB;
-  static_assert(W >= 16 && W <= 128, "first-layer window wgrad");
+  static_assert(W >= 16 && W <= 512, "first-layer window wgrad");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   char* Xs = smem;
   char* Ys = smem + XB;
@@ -1121,6 +1122,8 @@ hipError_t launch_wgrad_win_first(const WgradParams& p, hipStream_t s) {
       case 16: UNET_LAUNCH((wgrad_win_first_kernel<16, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
       case 32: UNET_LAUNCH((wgrad_win_first_kernel<32, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
       case 64: UNET_LAUNCH((wgrad_win_first_kernel<64, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      case 256: UNET_LAUNCH((wgrad_win_first_kernel<256, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      case 512: UNET_LAUNCH((wgrad_win_first_kernel<512, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
       default: UNET_LAUNCH((wgrad_win_first_kernel<128, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
     }
     return launch_status();
@@ -1129,6 +1132,8 @@ hipError_t launch_wgrad_win_first(const WgradParams& p, hipStream_t s) {
     case 16: UNET_LAUNCH((wgrad_win_first_kernel<16, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
     case 32: UNET_LAUNCH((wgrad_win_first_kernel<32, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
     case 64: UNET_LAUNCH((wgrad_win_first_kernel<64, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 256: UNET_LAUNCH((wgrad_win_first_kernel<256, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case 512: UNET_LAUNCH((wgrad_win_first_kernel<512, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
     default: UNET_LAUNCH((wgrad_win_first_kernel<128, CIN>), dim3(grid), dim3(NTHR), 0, s, p); break;
   }
   return launch_status();
@@ -1514,7 +1519,7 @@ static bool wgrad_win_eligible(const WgradParams& p) {
 
 // First layer (CIN 4/8, padded channels) on full rows 16..128 wide.
 static bool wgrad_win_first_eligible(const WgradParams& p) {
-  const bool w_ok = p.QW == 16 || p.QW == 32 || p.QW == 64 || p.QW == 128;
+  const bool w_ok = p.QW == 16 || p.QW == 32 || p.QW == 64 || p.QW == 128 || p.QW == 256 || p.QW == 512;
   return p.win >= 0 && w_ok && p.QD == 1 && p.KD == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.pad == 1 &&
          p.upA == 1 && p.AW == p.QW && p.AH == p.QH && (p.M1 == 4 || p.M1 == 8) && p.M2 == 0 &&
          (p.Nc % 32) == 0 && p.bias_mode != 2;
@@ -1573,7 +1578,7 @@ const char* wgrad_check(const WgradParams& p) {
   }
   if (p.xform != 0 && p.xform != 2) return "wgrad: xform must be 0 or 2";
   if (p.xform == 2 && (!wgrad_win_first_eligible(p) || !p.xa || !p.xb || !p.xc || !p.xz ||
-                       (p.xcs != 0 && p.xcs != p.Nc) || (p.xcs && p.QH % (256 / p.QW))))
+                       (p.xcs != 0 && p.xcs != p.Nc) || (p.xcs && p.QH % ((p.QW > 256 ? p.QW : 256) / p.QW))))
     return "wgrad: B transform (dz on load) needs the first-layer window wgrad";
   if (p.upA != 1) return "wgrad: upA must be 1 (nearest upsampling is materialised)";
   // (the head-on-load instantiation is the 2D full-row window, launch_wgrad_win_g<W, 1,
