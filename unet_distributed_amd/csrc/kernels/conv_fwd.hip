@@ -767,7 +767,7 @@ __global__ void __launch_bounds__(NTHR) tconv_dgrad_kernel(const ConvFwdParams p
   constexpr int EPIB = (EPI == EPI_DGRAD_NORM) ? epi_lds_bytes<BMc, BN>() : BMc * (BN + 4) * 2;
   constexpr int LDS_BYTES = (YB + WB > EPIB) ? YB + WB : EPIB;
   constexpr int TM = BMc / 4 / 16, TN = BN / 16;
-  static_assert(BMc % W == 0 && W >= 8 && W <= 128, "tconv window");
+  static_assert(BMc % W == 0 && W >= 8 && W <= 256, "tconv window");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   char* Ys = smem;
   char* Ws = smem + YB;
@@ -881,6 +881,8 @@ hipError_t launch_tconv_dgrad(const ConvFwdParams& p, hipStream_t s) {
     TD_CASE(16)
     TD_CASE(32)
     TD_CASE(64)
+    TD_CASE(128)
+    TD_CASE(256)
     default:
       return hipErrorInvalidValue;
   }
@@ -925,7 +927,8 @@ static bool tconv_fwd_eligible(const ConvFwdParams& p) {
 // 2D transposed-conv data gradient (2x2 stride-2 conv of the fine gradient); coarse rows
 // 32 / 64 wide (narrower levels measured faster on the implicit-GEMM kernel).
 static bool tconv_dgrad_eligible(const ConvFwdParams& p) {
-  const bool w_ok = p.OW == 8 || p.OW == 16 || p.OW == 32 || p.OW == 64;
+  // (coarse rows 128 / 256 wide: the 512^2 model; 80 KB of LDS, still two workgroups per CU)
+  const bool w_ok = p.OW == 8 || p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128 || p.OW == 256;
   return !p.shuffle && p.KD == 1 && p.KH == 2 && p.KW == 2 && p.stride == 2 && p.pad == 0 && p.OD == 1 &&
          p.ID == 1 && w_ok && p.IW == 2 * p.OW && p.IH == 2 * p.OH && p.up1 == 1 && p.C2 == 0 &&
          (p.C1 % 32) == 0 && (p.Cout % 64) == 0 && (!p.stats || p.nz) && p.drop_rate == 0.f;
