@@ -252,6 +252,24 @@ def test_conv_first_layer_smallc(cuda_dev, N, H, Cin, Co, tile):
     assert rel_err(out, ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,D,H,Cin,Co,tile", [(1, 4, 32, 4, 32, 9), (2, 3, 64, 4, 64, 9), (1, 5, 128, 8, 32, 9),
+                                               (1, 4, 32, 4, 32, 0), (1, 3, 32, 4, 32, 8)])
+def test_conv3d_first_layer_window(cuda_dev, N, D, H, Cin, Co, tile):
+    """3D first layer (padded 4/8 channels) on the first-layer window (tile 9 / auto): per
+    depth tap the halo of slice d + kd - 1 (zeros past the volume) and that tap's weights,
+    the next (window, depth tap)'s halo prefetched; tile 8 = the implicit-GEMM small-C mode."""
+    torch.manual_seed(D + H + Cin)
+    x = torch.randn(N, D, H, H, Cin, device=cuda_dev).bfloat16()
+    w = (torch.randn(3, 3, 3, Cin, Co, device=cuda_dev) * 0.1).bfloat16()
+    b = torch.randn(Co, device=cuda_dev)
+    wp = pad64(w.permute(4, 0, 1, 2, 3).reshape(Co, -1))
+    out = torch.empty(N, D, H, H, Co, device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(N=N, OD=D, OH=H, OW=H, ID=D, IH=H, IW=H, KD=3, KH=3, KW=3, pad=1, C1=Cin, src1=ptr(x),
+                      wgt=ptr(wp), bias=ptr(b), Cout=Co, relu=1, dst1=ptr(out), tile=tile), stream())
+    ref = ndhwc(F.relu(F.conv3d(ncdhw(x.float()), w.float().permute(4, 3, 0, 1, 2), b, padding=1)))
+    assert rel_err(out, ref) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,Ci,Co,tile", [(2, 8, 64, 32, 0), (2, 8, 64, 32, 8), (3, 64, 64, 32, 0),
                                             (2, 32, 128, 64, 0), (5, 16, 256, 128, 0), (3, 8, 512, 256, 0),
                                             (2, 128, 128, 64, 0), (1, 256, 64, 32, 0)])
@@ -406,6 +424,32 @@ def test_wgrad_first_layer_smallc(cuda_dev, N, H, Creal, Cpad, Co, splits, win):
     gwr, gbr = torch.autograd.grad(F.conv2d(nchw(x.float()[..., :Creal]), w, bb, padding=1), [w, bb],
                                    nchw(dy.float()))
     assert rel_err(gw, gwr.permute(2, 3, 1, 0).reshape(-1)) < 2e-3
+    assert rel_err(gb, gbr) < 2e-3
+
+
+@pytest.mark.parametrize("N,D,H,Creal,Co,splits,win", [(1, 4, 32, 4, 32, 3, 0), (2, 3, 64, 1, 32, 5, 0),
+                                                         (1, 5, 128, 4, 64, 7, 0), (1, 4, 32, 4, 32, 3, -1)])
+def test_wgrad_first_layer_3d(cuda_dev, N, D, H, Creal, Co, splits, win):
+    """3D first-layer weight gradient (4 padded channels): the window kernel staging the three
+    depth slices' halos (win = 0) and the tiled small-C mode (win = -1), rows remapped like
+    the engine's (taps x padded channels -> taps x real channels)."""
+    torch.manual_seed(9)
+    Cpad = 4
+    x = torch.zeros(N, D, H, H, Cpad, device=cuda_dev)
+    x[..., :Creal] = torch.randn(N, D, H, H, Creal, device=cuda_dev)
+    x = x.bfloat16()
+    dy = torch.randn(N, D, H, H, Co, device=cuda_dev).bfloat16()
+    BM, BN, NTAP, smallc = C().wgrad_pick(Cpad, 0, Co, 27, QW=H, win=win, QH=H, QD=D)
+    assert smallc
+    Mtot = (27 * Cpad + BM - 1) // BM * BM
+    d = dict(N=N, QD=D, QH=H, QW=H, AD=D, AH=H, AW=H, KD=3, KH=3, KW=3, pad=1, M1=Cpad, a1=ptr(x), b=ptr(dy),
+             Nc=Co, bias_mode=1, win=win)
+    gw, gb = _wgrad(d, splits, 1, Mtot, 27 * Creal, Co, 27 * Creal * Co, bias_w=(splits, Co), rows=(Cpad, Creal))
+    w = torch.zeros(Co, Creal, 3, 3, 3, device=cuda_dev, requires_grad=True)
+    bb = torch.zeros(Co, device=cuda_dev, requires_grad=True)
+    gwr, gbr = torch.autograd.grad(F.conv3d(ncdhw(x.float()[..., :Creal]), w, bb, padding=1), [w, bb],
+                                   ncdhw(dy.float()))
+    assert rel_err(gw, gwr.permute(2, 3, 4, 1, 0).reshape(-1)) < 2e-3
     assert rel_err(gb, gbr) < 2e-3
 
 

@@ -434,8 +434,14 @@ hipError_t launch_img8(const ConvFwdParams& p, hipStream_t s) {
 // hidden, and the epilogue's stores stream back to back.  (Register staging, not LDS-DMA:
 // the compiler then counts the loads past the epilogue's stores itself.)
 constexpr int FWPW = 8;
-template <int W, int CIN, int EPI>
-__global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) conv_win_first_kernel(const ConvFwdParams p) {
+// D3: 3D (3x3x3 'same'): rows of the flattened (n, d, h) space; each depth tap kd stages the
+// window's halo from the depth slice d + kd - 1 (zeros past the volume) and runs the 2D tap
+// set with that depth tap's weights, accumulating into the same tile.  The next (window,
+// depth tap)'s halo is in registers under the current one's MFMAs.
+// (3D holds three depth taps' weight fragments: two waves per SIMD, no spills)
+template <int W, int CIN, int EPI, bool D3 = false>
+__global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(D3 ? 2 : 3)))
+conv_win_first_kernel(const ConvFwdParams p) {
   // Row pitch in slots.  CIN 4 (8-byte slots): a half-wave's two 16-lane groups read 128
   // consecutive bytes each, at taps whose slots differ by Delta; they share no bank iff
   // 8 Delta == 128 (mod 256).  With the pitch == 16 (mod 32) slots and the K order below
@@ -464,9 +470,10 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) 
   char* Xs = smem;
   char* Es = smem + XB;                                        // epilogue staging
 
+  constexpr int NKD = D3 ? 3 : 1;                              // depth taps
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int H = p.OH;
-  const int rows_total = p.N * H;
+  const int H = p.OH, D = D3 ? p.OD : 1;
+  const int rows_total = p.N * D * H;
   const int M = rows_total * W;
   const int tiles_n = p.Cout / BN;
   const int nwin = ((rows_total + R - 1) / R) * tiles_n;
@@ -479,16 +486,28 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) 
   // halo chunk u = row u / CPR, 16 bytes = slots covering columns (CIN 4) 2c - 2, 2c - 1
   // or (CIN 8) c - 2, c = u % CPR; out-of-range chunks load zeros
   u32x4 hv[CPT];
-  auto load_halo = [&](const int w) {
+  // a window never spans two depth slices (host check: H % R == 0)
+  auto slice_ok = [&](const int w, const int kd) -> bool {
+    if constexpr (!D3) return true;
+    const int dd = ((w / tiles_n) * R / H) % D + kd - 1;
+    return (unsigned)dd < (unsigned)D;
+  };
+  auto load_halo = [&](const int w, const int kd) {
     const int g0 = (w / tiles_n) * R;
+    const bool sok = slice_ok(w, kd);
+    const int shift = D3 ? (kd - 1) * H : 0;                  // rows of the depth-shifted slice
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int u = tid + NTHR * c;
       const int hr = u / CPR, cc = u - hr * CPR;
       const int gr = g0 - 1 + hr;
       const int col = CIN == 4 ? 2 * cc - 2 : cc - 2;
-      const bool ok = u < NCH && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
-      hv[c] = __builtin_amdgcn_raw_buffer_load_b128(rs1, ok ? ((gr * W + col) * CIN) * 2 : OOB, 0, 0);
+      // (the SHIFTED row is range-checked: a halo row of the window's last slice row plus the
+      // depth shift lies in the next volume -- past the tensor for the last one, where the
+      // 2 GiB buffer range would not stop the load; run P faulted on exactly that)
+      const bool ok = sok && u < NCH && (unsigned)gr < (unsigned)rows_total &&
+                      (unsigned)(gr + shift) < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+      hv[c] = __builtin_amdgcn_raw_buffer_load_b128(rs1, ok ? (((gr + shift) * W + col) * CIN) * 2 : OOB, 0, 0);
     }
   };
   auto store_halo = [&]() {
@@ -507,8 +526,10 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) 
   constexpr unsigned long long KPERM = 0xFEDCBA87'95624310ull;
   auto ktap = [](const int i) -> int { return CIN == 4 ? (int)((KPERM >> (4 * i)) & 15ull) : i; };
   const int fsub = lane >> 4, fr = lane & 15;
-  h16x8 wf[KS][TN];
+  h16x8 wf[NKD][KS][TN];
   auto load_w = [&](const int n0) {
+#pragma unroll
+    for (int kd = 0; kd < NKD; ++kd)
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
@@ -519,21 +540,23 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) 
           for (int hh = 0; hh < 2; ++hh) {
             const int t = ktap(8 * s + 2 * fsub + hh);
             const u32x2 h2 = __builtin_bit_cast(
-                u32x2, __builtin_amdgcn_raw_buffer_load_b64(rsw, t < 9 ? ((n0 + 16 * j + fr) * p.Kpad + 4 * t) * 2 : OOB,
-                                                            0, 0));
+                u32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                           rsw, t < 9 ? ((n0 + 16 * j + fr) * p.Kpad + 4 * (9 * kd + t)) * 2 : OOB, 0, 0));
             v[2 * hh] = h2[0];
             v[2 * hh + 1] = h2[1];
           }
-          wf[s][j] = __builtin_bit_cast(h16x8, v);
+          wf[kd][s][j] = __builtin_bit_cast(h16x8, v);
         } else {
+          // (taps 9..11 of the last K step read the next depth tap's weights: their halo
+          // operand is the zero slot)
           const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
-              rsw, ((n0 + 16 * j + fr) * p.Kpad + 32 * s + 8 * fsub) * 2, 0, 0);
-          wf[s][j] = __builtin_bit_cast(h16x8, v);
+              rsw, ((n0 + 16 * j + fr) * p.Kpad + 72 * kd + 32 * s + 8 * fsub) * 2, 0, 0);
+          wf[kd][s][j] = __builtin_bit_cast(h16x8, v);
         }
       }
   };
   if (w_lo >= w_hi) return;
-  load_halo(w_lo);
+  load_halo(w_lo, 0);
   load_w((w_lo % tiles_n) * BN);
   store_halo();
   __syncthreads();
@@ -542,7 +565,6 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) 
     const int tm = w / tiles_n, tn = w - tm * tiles_n;
     const int g0 = tm * R, m0 = g0 * W, n0 = tn * BN;
     if (w > w_lo && tiles_n > 1) load_w(n0);
-    if (w + 1 < w_hi) load_halo(w + 1);                      // lands under this window's work
     uint32_t top_ok = 0, bot_ok = 0, live = 0;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -558,37 +580,50 @@ __global__ void __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) 
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      if (!((live >> i) & 1u)) continue;
-      const int rr = rw0 + i / TPR;                       // window row of this 16-pixel tile
-      const int cw = ((128 * wave) % W) + (i % TPR) * 16 + fr;   // this lane's output column
-      const bool tok = (top_ok >> i) & 1u, bok = (bot_ok >> i) & 1u;
+    for (int kd = 0; kd < NKD; ++kd) {
+      // the next (window, depth tap)'s halo lands under this one's MFMAs
+      if (kd + 1 < NKD) load_halo(w, kd + 1);
+      else if (w + 1 < w_hi) load_halo(w + 1, 0);
+      if (slice_ok(w, kd)) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        u32x4 v;
-        if constexpr (CIN == 4) {
+        for (int i = 0; i < TM; ++i) {
+          if (!((live >> i) & 1u)) continue;
+          const int rr = rw0 + i / TPR;                       // window row of this 16-pixel tile
+          const int cw = ((128 * wave) % W) + (i % TPR) * 16 + fr;   // this lane's output column
+          const bool tok = (top_ok >> i) & 1u, bok = (bot_ok >> i) & 1u;
 #pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            int t = ktap(8 * s + 2 * fsub + hh);            // tap of this 4-channel half
-            const bool zt = t >= 9;                         // zero tap: the partner's tap, other banks
-            if (zt) t = ktap(8 * s + 2 * (fsub ^ 1) + hh);
-            const int dh = t / 3, dw = t - 3 * dh;
-            const bool ok = t < 9 && (dh != 0 || tok) && (dh != 2 || bok);
-            const int slot = ((rr + dh) * RS + cw + dw + 1) ^ (zt ? 16 : 0);
-            const u32x2 h2 = *(const u32x2*)(Xs + (ok ? slot * SB : 0));
-            v[2 * hh] = h2[0];
-            v[2 * hh + 1] = h2[1];
+          for (int s = 0; s < KS; ++s) {
+            u32x4 v;
+            if constexpr (CIN == 4) {
+#pragma unroll
+              for (int hh = 0; hh < 2; ++hh) {
+                int t = ktap(8 * s + 2 * fsub + hh);            // tap of this 4-channel half
+                const bool zt = t >= 9;                         // zero tap: the partner's tap, other banks
+                if (zt) t = ktap(8 * s + 2 * (fsub ^ 1) + hh);
+                const int dh = t / 3, dw = t - 3 * dh;
+                const bool ok = t < 9 && (dh != 0 || tok) && (dh != 2 || bok);
+                const int slot = ((rr + dh) * RS + cw + dw + 1) ^ (zt ? 16 : 0);
+                const u32x2 h2 = *(const u32x2*)(Xs + (ok ? slot * SB : 0));
+                v[2 * hh] = h2[0];
+                v[2 * hh + 1] = h2[1];
+              }
+            } else {
+              const int t = 4 * s + fsub;
+              const int dh = t / 3, dw = t - 3 * dh;
+              const bool ok = t < 9 && (dh != 0 || tok) && (dh != 2 || bok);
+              const int slot = (rr + dh) * RS + cw + dw + 1;
+              v = *(const u32x4*)(Xs + (ok ? slot * SB : 0));
+            }
+            const h16x8 xf = __builtin_bit_cast(h16x8, v);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[kd][s][j], xf, acc[i][j]);
           }
-        } else {
-          const int t = 4 * s + fsub;
-          const int dh = t / 3, dw = t - 3 * dh;
-          const bool ok = t < 9 && (dh != 0 || tok) && (dh != 2 || bok);
-          const int slot = (rr + dh) * RS + cw + dw + 1;
-          v = *(const u32x4*)(Xs + (ok ? slot * SB : 0));
         }
-        const h16x8 xf = __builtin_bit_cast(h16x8, v);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[s][j], xf, acc[i][j]);
+      }
+      if (kd + 1 < NKD) {                                  // next depth tap's halo
+        __syncthreads();
+        store_halo();
+        __syncthreads();
       }
     }
     __syncthreads();                                     // halo reads done; previous epilogue's staging reads done
@@ -602,17 +637,24 @@ template <int CIN>
 hipError_t launch_win_first(const ConvFwdParams& p, hipStream_t s) {
   const int W = p.OW;
   const int R = 512 / W;
-  const int grid = (((p.N * p.OH + R - 1) / R) * (p.Cout / 32) + FWPW - 1) / FWPW;
+  const bool d3 = p.KD == 3;
+  const int grid = (((p.N * p.OD * p.OH + R - 1) / R) * (p.Cout / 32) + FWPW - 1) / FWPW;
   const int epi = conv_epi_mode(p);
   const bool fwd = epi == EPI_FWD;
+#define WF_GEO(WW, G3)                                                                                        \
+    if (fwd)                                                                                                  \
+      UNET_LAUNCH((conv_win_first_kernel<WW, CIN, EPI_FWD, G3>), dim3(grid), dim3(NTHR), 0, s, p);    \
+    else if (epi == EPI_STATS)                                                                                \
+      UNET_LAUNCH((conv_win_first_kernel<WW, CIN, EPI_STATS, G3>), dim3(grid), dim3(NTHR), 0, s, p);  \
+    else                                                                                                      \
+      UNET_LAUNCH((conv_win_first_kernel<WW, CIN, EPI_GENERIC, G3>), dim3(grid), dim3(NTHR), 0, s, p);
 #define WF_CASE(WW)                                                                                        \
   case WW:                                                                                                 \
-    if (fwd)                                                                                               \
-      UNET_LAUNCH((conv_win_first_kernel<WW, CIN, EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p);     \
-    else if (epi == EPI_STATS)                                                                             \
-      UNET_LAUNCH((conv_win_first_kernel<WW, CIN, EPI_STATS>), dim3(grid), dim3(NTHR), 0, s, p);   \
-    else                                                                                                   \
-      UNET_LAUNCH((conv_win_first_kernel<WW, CIN, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p); \
+    if (d3) {                                                                                              \
+      if constexpr (WW <= 128) { WF_GEO(WW, true) } else { return hipErrorInvalidValue; }                  \
+    } else {                                                                                               \
+      WF_GEO(WW, false)                                                                                    \
+    }                                                                                                      \
     break;
   switch (W) {
     WF_CASE(16)
@@ -625,6 +667,7 @@ hipError_t launch_win_first(const ConvFwdParams& p, hipStream_t s) {
       return hipErrorInvalidValue;
   }
 #undef WF_CASE
+#undef WF_GEO
   return launch_status();
 }
 
@@ -910,6 +953,11 @@ static bool win_eligible(const ConvFwdParams& p) {
 // 0.33 ms per half-batch launch -- r5 layer times).
 static bool win_first_eligible(const ConvFwdParams& p) {
   const bool w_ok = p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128 || p.OW == 256 || p.OW == 512;
+  // 3D (3x3x3 'same', rows <= 128 wide, windows inside one depth slice)
+  if (p.KD == 3 && p.OD > 1 && p.ID == p.OD && p.OW <= 128 && w_ok && p.OH % (512 / p.OW) == 0 && p.KH == 3 &&
+      p.KW == 3 && p.stride == 1 && p.pad == 1 && p.up1 == 1 && !p.shuffle && !p.nz && p.IW == p.OW &&
+      p.IH == p.OH && p.C2 == 0 && (p.C1 == 4 || p.C1 == 8) && p.Cout % 32 == 0 && p.D1 == p.Cout)
+    return true;
   return p.KD == 1 && p.OD == 1 && p.ID == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.pad == 1 &&
          p.up1 == 1 && !p.shuffle && !p.nz && w_ok && p.IW == p.OW && p.IH == p.OH && p.C2 == 0 &&
          (p.C1 == 4 || p.C1 == 8) && p.Cout % 32 == 0 && p.D1 == p.Cout;
@@ -1115,7 +1163,7 @@ void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
     case 9: {
       const int R = 512 / p.OW;
       if (p.nz) return;
-      *rows = (p.N * p.OH + R - 1) / R;
+      *rows = (p.N * p.OD * p.OH + R - 1) / R;
       *tile_px = 512;
       return;
     }

@@ -907,7 +907,11 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
 // supplies pixel q's slot for tap 4mt + pp (CIN 4) or tap 2mt + pp/2 and channel half
 // pp & 1 (CIN 8), so the transpose hands lane i the (tap, channel) row 16 mt + i; taps
 // past the ninth and taps whose input row leaves the pixel's image address slot 0.
-template <int W, int CIN, bool XF = false>
+// D3 (3x3x3, CIN 4): the halos of the three depth slices d - 1, d, d + 1 of the window are
+// staged together (zeros past the volume), GEMM rows m = (9 kd + t) CIN + c over the 27 taps
+// (MT = 7 row tiles); a row tile may span two depth slices, its lanes just address their own
+// slice's halo.
+template <int W, int CIN, bool XF = false, bool D3 = false>
 __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams p) {
   // Row pitch in slots: CIN 4 (8-byte slots) pads it to == 16 (mod 32) -- the four taps of
   // an A fragment (4 mt .. 4 mt + 3) then read slot sets that never share banks (a vertical
@@ -918,9 +922,12 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
   constexpr int BMW = W > 256 ? W : 256, R = BMW / W, HR = R + 2, SB = 2 * CIN;
   constexpr int RS = CIN == 4 ? ((W + 4 + 15) / 32) * 32 + 16 : W + 4, ROWB = RS * SB;
   constexpr int CPR = ROWB / 16;
-  constexpr int XI = (HR * CPR + 63) / 64, YI = BMW / 16;
+  constexpr int NS = D3 ? 3 : 1;                      // staged depth slices
+  constexpr int XI = (NS * HR * CPR + 63) / 64, YI = BMW / 16;
   constexpr int XB = XI * 1024, YB = YI * 1024;
-  constexpr int MT = (9 * CIN + 15) / 16;
+  constexpr int NT = D3 ? 27 : 9;                     // taps
+  constexpr int MT = (NT * CIN + 15) / 16;
+  static_assert(!D3 || (CIN == 4 && !XF), "3D first-layer window wgrad: 4 padded channels");
   constexpr int KS = BMW / 32;
   // (cross-wave reduction rows padded to an odd number of 16-byte units: a lane stride of
   // NV = 2 MT + 2 units (128 bytes at MT = 3) put all 8 lanes of a 16-byte store group on
@@ -933,8 +940,8 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
   char* Ys = smem + XB;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int H = p.QH;
-  const int rows_total = p.N * H;
+  const int H = p.QH, D = D3 ? p.QD : 1;
+  const int rows_total = p.N * D * H;
   const int Mq = rows_total * W;
   const int nwin = (rows_total + R - 1) / R;
   const int Mtot = MT * 16;
@@ -1002,10 +1009,13 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
       const int k = wave + 4 * qq;
       if (k < XI) {
         const int u = 64 * k + lane;
-        const int hr = u / CPR, c = u - hr * CPR;
-        const int gr = g0 - 1 + hr;
+        const int hr3 = u / CPR, c = u - hr3 * CPR;
+        const int kd = D3 ? hr3 / HR : 0, hr = hr3 - kd * HR;     // (3D: slice d + kd - 1)
+        const int gr = g0 - 1 + hr + (D3 ? (kd - 1) * H : 0);
         const int col = CIN == 4 ? 2 * c - 2 : c - 2;
-        const bool ok = hr < HR && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+        const int dd = D3 ? (g0 / H) % D + kd - 1 : 0;
+        const bool ok = hr3 < NS * HR && (unsigned)dd < (unsigned)D && (unsigned)gr < (unsigned)rows_total &&
+                        (unsigned)col < (unsigned)W;
         const int off = ok ? ((gr * W + col) * CIN) * 2 : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
                                                  off, 0, 0, 0);
@@ -1065,14 +1075,16 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const int t = CIN == 4 ? 4 * mt + pp : 2 * mt + (pp >> 1);
+        const int t3 = CIN == 4 ? 4 * mt + pp : 2 * mt + (pp >> 1);
+        const int kd = D3 ? t3 / 9 : 0, t = t3 - 9 * kd;
         const int chb = CIN == 4 ? 0 : (pp & 1) * 8;
         const int dh = t / 3, dw = t - 3 * dh;
         int a[2];
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
-          const bool ok = t < 9 && !(dh == 0 && hlp[hh] == 0) && !(dh == 2 && hlp[hh] == H - 1);
-          a[hh] = ok ? (slotp[hh] + dh * RS + dw) * SB + chb : (t >= 9 && CIN == 4 ? (slotp[hh] + 16) * SB : 0);
+          const bool ok = t3 < NT && !(dh == 0 && hlp[hh] == 0) && !(dh == 2 && hlp[hh] == H - 1);
+          a[hh] = ok ? (slotp[hh] + (kd * HR + dh) * RS + dw) * SB + chb
+                     : (t3 >= NT && CIN == 4 ? (slotp[hh] + 16) * SB : 0);
         }
         const h16x8 af = tr8(Xs + a[0], Xs + a[1]);
 #pragma unroll
@@ -1117,6 +1129,17 @@ __global__ void __launch_bounds__(NTHR) wgrad_win_first_kernel(const WgradParams
 template <int CIN>
 hipError_t launch_wgrad_win_first(const WgradParams& p, hipStream_t s) {
   const int grid = (p.Nc / 32) * launch_splits(p);
+  if constexpr (CIN == 4) {
+    if (p.KD == 3) {          // (wgrad_win_first3_eligible: the caller checked)
+      switch (p.QW) {
+        case 16: UNET_LAUNCH((wgrad_win_first_kernel<16, 4, false, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+        case 32: UNET_LAUNCH((wgrad_win_first_kernel<32, 4, false, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+        case 64: UNET_LAUNCH((wgrad_win_first_kernel<64, 4, false, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+        default: UNET_LAUNCH((wgrad_win_first_kernel<128, 4, false, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      }
+      return launch_status();
+    }
+  }
   if (p.xform == 2) {         // dz formed on load (norm backward of the first layer)
     switch (p.QW) {
       case 16: UNET_LAUNCH((wgrad_win_first_kernel<16, CIN, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
@@ -1518,7 +1541,15 @@ static bool wgrad_win_eligible(const WgradParams& p) {
 }
 
 // First layer (CIN 4/8, padded channels) on full rows 16..128 wide.
+static bool wgrad_win_first3_eligible(const WgradParams& p) {
+  const bool w_ok = p.QW == 16 || p.QW == 32 || p.QW == 64 || p.QW == 128;
+  return p.win >= 0 && w_ok && p.KD == 3 && p.QD > 1 && p.AD == p.QD && p.KH == 3 && p.KW == 3 && p.stride == 1 &&
+         p.pad == 1 && p.upA == 1 && p.AW == p.QW && p.AH == p.QH && p.QH % (256 / p.QW) == 0 && p.M1 == 4 &&
+         p.M2 == 0 && (p.Nc % 32) == 0 && p.bias_mode != 2 && p.xform == 0;
+}
+
 static bool wgrad_win_first_eligible(const WgradParams& p) {
+  if (wgrad_win_first3_eligible(p)) return true;
   const bool w_ok = p.QW == 16 || p.QW == 32 || p.QW == 64 || p.QW == 128 || p.QW == 256 || p.QW == 512;
   return p.win >= 0 && w_ok && p.QD == 1 && p.KD == 1 && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.pad == 1 &&
          p.upA == 1 && p.AW == p.QW && p.AH == p.QH && (p.M1 == 4 || p.M1 == 8) && p.M2 == 0 &&
@@ -1546,6 +1577,7 @@ WgradCfg wgrad_pick(const WgradParams& p) {
   const int KT = p.KD * p.KH * p.KW;
   const int M = p.M1 + p.M2;
   if (wgrad_win_eligible(p)) return {32, (p.Nc % 64 == 0) ? 64 : 32, 9, 0};   // row-window tile
+  if (wgrad_win_first3_eligible(p)) return {112, 32, 1, 1};                     // 3D first-layer window
   if (wgrad_win_first_eligible(p)) return {p.M1 == 4 ? 48 : 80, 32, 1, 1};      // first-layer window
   if (wgrad_tconv_win_eligible(p))                                                 // transposed-conv window
     return {32, p.Nc % 128 == 0 ? 128 : (p.Nc % 64 == 0 ? 64 : 32), 4, 0};
