@@ -81,6 +81,17 @@ struct StripTiles {
   }
 };
 
+// Epilogue constants a persistent caller loads once (conv_win.h conv_win_pf_kernel): the
+// lane's bias values bias[j][r] (channel n0 + 16 j + 4 (lane >> 4) + r) and the fused head's
+// weights.  With them the EPI_FWD epilogue issues no global loads, so the caller's
+// prefetch of the next window -- issued before it -- is never waited on behind them.
+template <int TN>
+struct EpiConst {
+  float bias[TN][4];
+  float hw[8];
+  float hb;
+};
+
 // SEGW > 0: the tile is a row window of SEGW-wide row segments (window kernels on rows
 // wider than one window, or any row-window kernel): tile pixel ml is at row
 // m0 + ml / SEGW (m0 = first row), column col0 + ml % SEGW of rows `pitch` pixels wide.
@@ -92,7 +103,8 @@ template <int BM, int BN, int WM, int WN, int TM, int TN, int NTHR, int EPI = EP
 __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc)[TM][TN], char* smem,
                                               const int m0, const int n0, const int M, const int wm,
                                               const int wn, const int lane, const int tid,
-                                              const int pitch = 0, const int col0 = 0, const int stat_row = 0) {
+                                              const int pitch = 0, const int col0 = 0, const int stat_row = 0,
+                                              const EpiConst<TN>* ec = nullptr) {
   auto qof = [&](int ml) -> int {
     if constexpr (SEGW > 0) return (m0 + ml / SEGW) * pitch + col0 + (ml % SEGW);
     else return m0 + ml;
@@ -149,7 +161,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
     float bsv[4], msc[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      bsv[r] = kBias ? p.bias[kShuffle ? (n + r) % Dtb : n + r] : 0.f;
+      bsv[r] = ec ? ec->bias[j][r] : (kBias ? p.bias[kShuffle ? (n + r) % Dtb : n + r] : 0.f);
       msc[r] = kMaskScale ? ((n + r < p.D1) ? p.mask_scale1 : p.mask_scale2) : 1.f;
     }
     if constexpr (EPI == EPI_FWD) {
@@ -423,8 +435,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
   }
   if (kHeadable && kHead) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) hw[e] = p.head_w[(tid % CPR) * 8 + e];
-    hb = p.head_b[0];
+    for (int e = 0; e < 8; ++e) hw[e] = ec ? ec->hw[e] : p.head_w[(tid % CPR) * 8 + e];
+    hb = ec ? ec->hb : p.head_b[0];
   }
   // (fully unrolled with the fused head, whose per-iteration logits live in registers)
   constexpr int NITER = (NCHUNK + NTHR - 1) / NTHR;

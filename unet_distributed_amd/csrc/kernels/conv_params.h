@@ -144,6 +144,8 @@ struct ConvFwdParams {
   float* head_logit;
   int rev;                    // row-window kernels: windows in reverse order (the consumer starts
                               // where its producer ended, on the tail still in the Infinity Cache)
+  int win_pf;                 // > 0: 2D 128-wide 32 -> 32 channel row windows run persistently,
+                              // win_pf consecutive windows per workgroup (conv_win_pf_kernel)
   HeadGrad hg;                // 2D row-window data gradient of the head input: src1 (dY) formed
                               // on load (one 32-channel chunk), see HeadGrad
   // Space-to-depth source (2D row-window, composite transposed-conv data gradient):

@@ -42,10 +42,20 @@ inline int win_rows(const ConvFwdParams& p) {
   const int W = p.OW > 128 ? 128 : p.OW;
   return win_bm(p) / W;
 }
+// Persistent prefetching window (conv_win_pf_kernel): 2D, 128-wide rows, one 32-channel
+// input chunk, 32 output channels, bias + ReLU forward or data-gradient epilogue (level 1
+// of the 128^2 UNet: the forward of conv1b / conv9b, the skip data gradient of conv9a).
+// (every epilogue mode; the head-on-load data gradient of the head input too)
+inline bool win_pf_eligible(const ConvFwdParams& p) {
+  return p.win_pf > 0 && p.OW == 128 && p.KD == 1 && p.OD == 1 && p.C1 == 32 && p.C2 == 0 && p.Cout == 32 &&
+         p.tile != 12 && !p.xform && !p.s2d && !p.ut.x && !p.fw.x && p.OH % 4 == 0 &&
+         (!p.hg.prob || conv_epi_mode(p) == EPI_DGRAD);
+}
 inline int win_grid(const ConvFwdParams& p) {
   const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
   const int rows = p.N * p.OD * p.OH;
   const int R = win_rows(p);
+  if (win_pf_eligible(p)) return (rows / 4 + p.win_pf - 1) / p.win_pf;
   return ((rows + R - 1) / R) * (p.OW / W) * (p.Cout / win_bn(p));
 }
 // (BN, BM, row width) combinations win_bn / win_bm can select (the 64-channel tile also
@@ -557,10 +567,223 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
     conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0, 0, tm);
 }
 
+// ---------------------------------------------------------------------------------
+// Persistent prefetching row window (win_pf_eligible): level 1 of the 128^2 UNet has one
+// 32-channel input chunk per window, so conv_win_kernel's workgroup is a serial chain --
+// DMA the 55 KB halo, wait, 144 MFMAs per wave, epilogue, exit -- and two workgroups per
+// CU leave HBM idle for much of it (3.6 TB/s, 18 % MFMA busy on conv1b's forward, r5 PMC).
+// Here a workgroup runs win_pf consecutive windows: the weights are staged once, and the
+// next window's halo is loaded into registers (13 x 16 bytes per thread) while the
+// current one's MFMAs and epilogue run, then written to LDS (XF 3, head-on-load: the
+// next window's per-pixel probability, target and ReLU bits -- 12 registers -- and the
+// halo is formed from them).  The epilogue's constants
+// (bias, head weights) are loaded once too (EpiConst), so its only memory operations are
+// stores and the prefetch is never waited on behind a load (the data-gradient epilogue's
+// mask / pool-route loads still are).  Same operands, tap order and epilogue as
+// conv_win_kernel<128, 32, 512, false, EPI, GEO_2D, XF>: bit-identical outputs.
+constexpr int PF_HWP = 144;                   // halo row pitch in 64-byte slots (ALR's)
+constexpr int PF_ROWB = PF_HWP * 64;
+constexpr int PF_CPT = 6 * 128 * 4 / NTHR;    // 16-byte granules of the 6 halo rows' pixels per thread
+constexpr int PF_XB = 6 * PF_ROWB, PF_WB = 9 * 32 * 64;
+static_assert(512 * 36 * 2 <= PF_XB, "epilogue staging aliases the halo image");
+
+template <int EPI, int XF>
+__global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParams p) {
+  static_assert(XF == 0 || (XF == 3 && EPI == EPI_DGRAD), "plain source or head-on-load data gradient");
+  constexpr int W = 128, R = 4, BM = 512, BN = 32, ROWB = PF_ROWB;
+  constexpr int TC = 2, NCS = 4, RW = 4, TM = RW * TC, TN = 2, WMP = BM / 4;
+  using Map = StripTiles<W, RW, TC, NCS>;
+  __shared__ __attribute__((aligned(1024))) char smem[PF_XB + PF_WB];
+  char* Xs = smem;
+  char* Ws = smem + PF_XB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = p.OH;
+  const int rows_total = p.N * H;
+  const int M = rows_total * W;
+  const int nwin = rows_total / R;                   // H % R == 0 (win_pf_eligible)
+  const int w_lo = (int)blockIdx.x * p.win_pf;
+  const int w_hi = w_lo + p.win_pf < nwin ? w_lo + p.win_pf : nwin;
+  if (w_lo >= w_hi) return;
+  constexpr int OOB = 0x7fffffff;
+  const char* src = (const char*)p.src1;
+
+  // Halo pixels: granule c of thread t = halo row c / 2, column (t >> 2) + 64 (c & 1),
+  // logical chunk t & 3 -- a 512-granule row is two 256-thread passes, so a thread's
+  // global and LDS offsets are its own base plus compile-time constants and a row's
+  // validity is wave-uniform.  LDS slot = column + 1, physical chunk = logical ^
+  // ((slot >> 1) & 3), as conv_win_kernel's DMA leaves it; the zero columns -1 / 128
+  // (slots 0 / 129) are rewritten per window (the epilogue's staging overwrites them).
+  u32x4 hv[PF_CPT];
+  const int gl_t = tid * 16;
+  const int lds_t = (1 + (tid >> 2)) * 64 + 16 * ((tid & 3) ^ (((1 + (tid >> 2)) >> 1) & 3));
+  // XF 3: slot sl = tid + 256 j of the 6 x 144-slot image (conv_win_kernel's XF 3 map)
+  constexpr int NSL = 6 * PF_HWP, HJ = (NSL + NTHR - 1) / NTHR;
+  float hpr[HJ], htv[HJ];
+  uint32_t hbits[HJ];
+  HeadGradCtx hctx{};
+  if constexpr (XF == 3) hctx = head_grad_ctx(p.hg);
+  auto load_halo = [&](const int w) {
+    const int g0 = (p.rev ? nwin - 1 - w : w) * R;
+    if constexpr (XF == 3) {
+      const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
+#pragma unroll
+      for (int j = 0; j < HJ; ++j) {
+        const int sl = tid + NTHR * j;
+        const int hr = sl / PF_HWP, hc = sl - hr * PF_HWP;
+        const int gr = g0 - 1 + hr, col = hc - 1;
+        const bool ok = sl < NSL && (hr > 0 || top_in) && (hr < R + 1 || bot_in) &&
+                        (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+        const int pix = ok ? gr * W + col : 0;
+        hpr[j] = p.hg.prob[pix];
+        htv[j] = bits2f(((const uint16_t*)p.hg.t)[pix]);
+        hbits[j] = ok ? ((const uint32_t*)p.hg.bits)[pix] : 0u;
+      }
+      return;
+    }
+    const int grow0 = (g0 / H) * H;                  // the window's image (32-bit offsets from it)
+    const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)grow0 * W * 64), (short)0, OOB, 0x00020000);
+    const int rowoff = (g0 - 1 - grow0) * W * 64;    // byte offset of halo row 0 (may be -8 KB: row 0 then off)
+#pragma unroll
+    for (int c = 0; c < PF_CPT; ++c) {
+      const int hr = c >> 1;
+      const bool ok = (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)(g0 - 1 + hr) < (unsigned)rows_total;
+      hv[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? rowoff + hr * W * 64 + (c & 1) * 4096 + gl_t : OOB, 0, 0);
+    }
+  };
+  auto store_halo = [&]() {
+    if constexpr (XF == 3) {
+      // dY = dlogit w (x > 0) per slot (zeros outside the image: bits 0), as conv_win_kernel
+#pragma unroll
+      for (int j = 0; j < HJ; ++j) {
+        const int sl = tid + NTHR * j;
+        if (sl >= NSL) continue;
+        const int hc = sl % PF_HWP;
+        const float dz = head_dlogit(hpr[j], htv[j], hctx.a, hctx.bb, hctx.inv_total, hctx.bce_w, hctx.gscale);
+        const int sw = (hc >> 1) & 3;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = dz * hctx.w[8 * k + e];
+            o[e] = ((hbits[j] >> (8 * k + e)) & 1u) ? v : 0.f;
+          }
+          *(u32x4*)(Xs + sl * 64 + 16 * (k ^ sw)) = pack8(o);
+        }
+      }
+      return;
+    }
+#pragma unroll
+    for (int c = 0; c < PF_CPT; ++c) *(u32x4*)(Xs + lds_t + (c >> 1) * ROWB + (c & 1) * 4096) = hv[c];
+    if (tid < 48) *(u32x4*)(Xs + (tid >> 3) * ROWB + ((tid >> 2) & 1) * 129 * 64 + 16 * (tid & 3)) = (u32x4){0u, 0u, 0u, 0u};
+  };
+  load_halo(w_lo);
+  {
+    // weight image (once): row tap * 32 + n, 64 bytes = the 32 input channels
+    const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
+    const int lslot = lane >> 2;
+    const int lchunk = (lane & 3) ^ ((lslot >> 1) & 3);
+    const int wl = (lslot * p.Kpad + lchunk * 8) * 2;
+    constexpr int WI = 9 * BN / 16;
+#pragma unroll
+    for (int q = 0; q < (WI + 3) / 4; ++q) {
+      const int k = wave + 4 * q;
+      if (k < WI) {
+        const int tap = k / (BN / 16), nb = (k % (BN / 16)) * 16;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(Ws + k * 1024), 16,
+                                                 (nb * p.Kpad + tap * 32) * 2 + wl, 0, 0, 0);
+      }
+    }
+  }
+  const int fsub = lane >> 4, fr = lane & 15;
+  EpiConst<TN> ec;
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      ec.bias[j][r] = (EPI != EPI_DGRAD && EPI != EPI_DGRAD_NORM && p.bias) ? p.bias[16 * j + 4 * fsub + r] : 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ec.hw[e] = (EPI == EPI_FWD && p.head_w) ? p.head_w[(tid % 4) * 8 + e] : 0.f;
+  ec.hb = (EPI == EPI_FWD && p.head_w) ? p.head_b[0] : 0.f;
+  store_halo();
+  __syncthreads();
+
+  const int r0 = (wave / NCS) * RW, c0 = (wave % NCS) * 16 * TC;
+  int xbase[3];
+#pragma unroll
+  for (int dw = 0; dw < 3; ++dw) {
+    const int hc = fr + dw;
+    xbase[dw] = r0 * ROWB + c0 * 64 + hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3));
+  }
+  const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
+  for (int w = w_lo; w < w_hi; ++w) {
+    const int tm = p.rev ? nwin - 1 - w : w;
+    const int g0 = tm * R;
+    if (w + 1 < w_hi) load_halo(w + 1);             // in flight under this window's MFMAs + epilogue
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw) {
+      h16x8 wf[3][TN];
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) wf[dh][j] = *(const h16x8*)(Ws + ((3 * dh + dw) * BN + 16 * j) * 64 + wbase);
+#pragma unroll
+      for (int hr = 0; hr < RW + 2; ++hr) {
+#pragma unroll
+        for (int ci = 0; ci < TC; ++ci) {
+          const h16x8 xf = *(const h16x8*)(Xs + xbase[dw] + hr * ROWB + ci * 16 * 64);
+#pragma unroll
+          for (int dh = 0; dh < 3; ++dh) {
+            const int ri = hr - dh;
+            if (ri < 0 || ri >= RW) continue;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[ri * TC + ci][j] = mfma16(wf[dh][j], xf, acc[ri * TC + ci][j]);
+          }
+        }
+      }
+    }
+    __syncthreads();                                 // fragment reads done: the epilogue stages in Xs
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(p, acc, smem, g0 * W, 0, M, wave, 0, lane, tid, 0,
+                                                                  0, tm, &ec);
+    if (w + 1 < w_hi) {
+      __syncthreads();                               // staging reads done
+      store_halo();
+      __syncthreads();
+    }
+  }
+}
+
+hipError_t launch_win_pf(const ConvFwdParams& p, hipStream_t s) {
+  const int grid = win_grid(p);
+  switch (conv_epi_mode(p)) {
+    case EPI_FWD: UNET_LAUNCH((conv_win_pf_kernel<EPI_FWD, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case EPI_DGRAD:
+      if (p.hg.prob)
+        UNET_LAUNCH((conv_win_pf_kernel<EPI_DGRAD, 3>), dim3(grid), dim3(NTHR), 0, s, p);
+      else
+        UNET_LAUNCH((conv_win_pf_kernel<EPI_DGRAD, 0>), dim3(grid), dim3(NTHR), 0, s, p);
+      break;
+    case EPI_STATS: UNET_LAUNCH((conv_win_pf_kernel<EPI_STATS, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    case EPI_DGRAD_NORM: UNET_LAUNCH((conv_win_pf_kernel<EPI_DGRAD_NORM, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    default: UNET_LAUNCH((conv_win_pf_kernel<EPI_GENERIC, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
+  }
+  return launch_status();
+}
+
 }  // namespace
 
 template <int BN, int BM>
 hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
+  if constexpr (BN == 32 && BM == 512) {
+    if (win_pf_eligible(p)) return launch_win_pf(p, s);
+  }
   const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
   const int grid = win_grid(p);
   const bool cc = p.C2 > 0;

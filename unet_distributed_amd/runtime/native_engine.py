@@ -67,8 +67,10 @@ def _r64(k: int) -> int:
 #   dw_fuse      data + weight gradient of a 32 -> 32 channel conv on 128-wide rows in one kernel
 #                reading dY once (conv_dw.hip) (1)
 #   dw_wgs       workgroups (= slab rows) per fused data + weight gradient launch (512)
+#   win_pf       windows per workgroup of the persistent prefetching row window on 128-wide
+#                32 -> 32 channel convs (conv_win.h conv_win_pf_kernel) (8; 0 off)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
-                       tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512)
+                       tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8)
 
 
 class Fusion:
@@ -924,7 +926,7 @@ class NativeUNet:
         idd, ih, iw = self.sdims(in_level or level)
         kd = K if self.dims == 3 else 1
         return dict(N=self.B, OD=od, OH=oh, OW=ow, ID=idd, IH=ih, IW=iw, KD=kd, KH=K, KW=K,
-                    stride=stride, pad=pad, tile=0)
+                    stride=stride, pad=pad, tile=0, win_pf=self.opts["win_pf"])
 
     def _salt(self, lname):
         return [l.name for l in self.spec.layers].index(lname)
