@@ -146,6 +146,10 @@ struct ConvFwdParams {
                               // where its producer ended, on the tail still in the Infinity Cache)
   int win_pf;                 // > 0: 2D 128-wide 32 -> 32 channel row windows run persistently,
                               // win_pf consecutive windows per workgroup (conv_win_pf_kernel)
+  int win_cp;                 // >= 1: 64-channel row windows of 64-wide rows with two or more input
+                              // chunks load the next chunk under the current one's MFMAs
+                              // (conv_win_cp_kernel); >= 2: also 128-wide rows, 3D or two or more
+                              // chunks (conv_win_cp128_kernel)
   HeadGrad hg;                // 2D row-window data gradient of the head input: src1 (dY) formed
                               // on load (one 32-channel chunk), see HeadGrad
   // Space-to-depth source (2D row-window, composite transposed-conv data gradient):

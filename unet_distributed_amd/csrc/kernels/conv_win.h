@@ -51,6 +51,23 @@ inline bool win_pf_eligible(const ConvFwdParams& p) {
          p.tile != 12 && !p.xform && !p.s2d && !p.ut.x && !p.fw.x && p.OH % 4 == 0 &&
          (!p.hg.prob || conv_epi_mode(p) == EPI_DGRAD);
 }
+// Chunk-pipelined window (conv_win_cp_kernel): 2D 64-wide full rows, the 64-channel tile,
+// plain or concat source, no operand transform, two or more 32-channel input chunks (level 2
+// of the 128^2 UNet).  (At levels 3-4 -- 32 / 16-wide rows, 4..16 chunks -- the per-launch
+// times rose 0.016-0.034 ms against the DMA chunk loop, run V: not used there.)
+inline bool win_cp_eligible(const ConvFwdParams& p) {
+  return p.win_cp > 0 && p.OW == 64 && p.KD == 1 && p.OD == 1 &&
+         p.C1 + p.C2 >= 64 && p.Cout % 64 == 0 && !p.head_w && p.tile != 6 && !p.xform && !p.hg.prob &&
+         !p.s2d && !p.ut.x && !p.fw.x;
+}
+// Chunk-pipelined window on 128-wide rows (conv_win_cp128_kernel): 2D with two or more input
+// chunks, or 3D (3x3x3: depth taps x chunks), the 32-channel tile, no operand transform
+// (the 3D level 1 of the 128^3 UNet, the 512^2 model's 128-wide level).
+inline bool win_cp128_eligible(const ConvFwdParams& p) {
+  const bool d3 = p.KD == 3 && p.OD > 1;
+  return p.win_cp > 1 && p.OW == 128 && (d3 || (p.KD == 1 && p.OD == 1 && p.C1 + p.C2 >= 64)) && p.tile != 12 &&
+         !p.xform && !p.hg.prob && !p.s2d && !p.ut.x && !p.fw.x && !win_pf_eligible(p);
+}
 inline int win_grid(const ConvFwdParams& p) {
   const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
   const int rows = p.N * p.OD * p.OH;
@@ -760,6 +777,329 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Chunk-pipelined row window (win_cp_eligible): at levels 2-4 a window runs 2..16 input
+// chunks, and conv_win_kernel's chunk step is serial -- LDS-DMA the chunk's halo image and
+// 36 KB of weights, wait, MFMAs -- with two workgroups per CU to cover one's wait with the
+// other's MFMAs (27-49 % MFMA busy, r5 PMC).  Here the next chunk's halo and weight images
+// are loaded into registers (6-7 + 9 x 16 bytes per thread) while the current chunk's MFMAs
+// run, and written to LDS after them: one barrier pair per chunk, no exposed load latency
+// past the first chunk.  Same LDS images (pitch W + 4, chunk swizzle), operands, tap order
+// and epilogue as conv_win_kernel<W, 64, 256, CONCAT, EPI, GEO_2D>: bit-identical outputs.
+template <int W, bool CONCAT, int EPI>
+__global__ void __launch_bounds__(NTHR, 2) conv_win_cp_kernel(const ConvFwdParams p) {
+  constexpr int BN = 64, BM = 256, R = BM / W, HR = R + 2;
+  constexpr int HWP = W + 4, ROWB = HWP * 64;
+  constexpr int NSLOT = HR * HWP;
+  constexpr int XB = (NSLOT + 15) / 16 * 1024, WB = 9 * BN * 64;
+  constexpr int XG = (NSLOT * 4 + NTHR - 1) / NTHR;     // halo granules per thread
+  constexpr int WG = 9 * BN * 4 / NTHR;                 // weight granules per thread (9)
+  constexpr int EPIB = (EPI == EPI_STATS || EPI == EPI_DGRAD_NORM) ? epi_lds_bytes<BM, BN>() : BM * (BN + 4) * 2;
+  constexpr int LDS_BYTES = (XB + WB > EPIB) ? XB + WB : EPIB;
+  constexpr int WMP = BM / 4, TM = WMP / 16, TN = BN / 16;
+  constexpr int TC = 1, NCS = W / 16, RW = R / (4 / NCS);
+  static_assert(W >= 16 && W <= 64 && RW * TC == TM && 9 * BN * 4 % NTHR == 0, "chunk-pipelined window shape");
+  using Map = StripTiles<W, RW, TC, NCS>;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  char* Xs = smem;
+  char* Ws = smem + XB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = p.OH;
+  const int rows_total = p.N * H;
+  const int M = rows_total * W;
+  const int tiles_n = p.Cout / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm0 = bid / tiles_n, tn = bid % tiles_n;
+  const int tm = p.rev ? (int)(gridDim.x / tiles_n) - 1 - tm0 : tm0;
+  const int g0 = tm * R, n0 = tn * BN;
+  const int Cin = p.C1 + p.C2;
+  const int nchunks = Cin >> 5;
+  constexpr int OOB = 0x7fffffff;
+  const int grow0 = (g0 / H) * H;                       // the window's image (32-bit offsets from it)
+  const size_t img_px = (size_t)grow0 * W;
+  const char* s1b = (const char*)p.src1 + img_px * p.C1 * 2;
+  const char* s2b = p.src2 ? (const char*)p.src2 + img_px * p.C2 * 2 : s1b;
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)s1b, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc((void*)s2b, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
+  const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
+
+  // halo granule u = tid + 256 c: slot u / 4 (row slot / HWP, column slot % HWP - 1), logical
+  // chunk u % 4 at physical chunk ^ ((column slot >> 1) & 3); weight granule u: row u / 4 =
+  // tap c x BN + n (n = tid / 4), logical chunk u % 4 at ^ ((row >> 1) & 3)
+  u32x4 xv[XG], wv[WG];
+  auto load_chunk = [&](const int kc) {
+    const bool from1 = !CONCAT || (kc << 5) < p.C1;
+    const int C = from1 ? p.C1 : p.C2;
+    const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
+    const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
+#pragma unroll
+    for (int c = 0; c < XG; ++c) {
+      const int u = tid + NTHR * c;
+      const int sl = u >> 2, hr = sl / HWP, hc = sl - hr * HWP;
+      const int gr = g0 - 1 + hr, col = hc - 1;
+      const bool ok = sl < NSLOT && (hr > 0 || top_in) && (hr < R + 1 || bot_in) &&
+                      (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+      xv[c] = __builtin_amdgcn_raw_buffer_load_b128(
+          rs, ok ? (((gr - grow0) * W + col) * C + cb + (u & 3) * 8) * 2 : OOB, 0, 0);
+    }
+#pragma unroll
+    for (int c = 0; c < WG; ++c)
+      wv[c] = __builtin_amdgcn_raw_buffer_load_b128(
+          rsw, ((n0 + (tid >> 2)) * p.Kpad + c * Cin + (kc << 5) + (tid & 3) * 8) * 2, 0, 0);
+  };
+  auto store_chunk = [&]() {
+#pragma unroll
+    for (int c = 0; c < XG; ++c) {
+      const int u = tid + NTHR * c;
+      const int sl = u >> 2, hc = sl % HWP;
+      if (sl < NSLOT) *(u32x4*)(Xs + sl * 64 + 16 * ((u & 3) ^ ((hc >> 1) & 3))) = xv[c];
+    }
+    const int wrow = tid >> 2;
+#pragma unroll
+    for (int c = 0; c < WG; ++c)
+      *(u32x4*)(Ws + (c * BN + wrow) * 64 + 16 * ((tid & 3) ^ ((wrow >> 1) & 3))) = wv[c];
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int fsub = lane >> 4, fr = lane & 15;
+  const int r0 = (wave / NCS) * RW, c0 = (wave % NCS) * 16 * TC;
+  int xbase[3];
+#pragma unroll
+  for (int dw = 0; dw < 3; ++dw) {
+    const int hc = fr + dw;
+    xbase[dw] = r0 * ROWB + c0 * 64 + hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3));
+  }
+  const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
+  load_chunk(0);
+  store_chunk();
+  __syncthreads();
+  for (int kc = 0; kc < nchunks; ++kc) {
+    if (kc + 1 < nchunks) load_chunk(kc + 1);          // in flight under this chunk's MFMAs
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw) {
+      h16x8 wf[3][TN];
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) wf[dh][j] = *(const h16x8*)(Ws + ((3 * dh + dw) * BN + 16 * j) * 64 + wbase);
+#pragma unroll
+      for (int hr = 0; hr < RW + 2; ++hr) {
+        const h16x8 xf = *(const h16x8*)(Xs + xbase[dw] + hr * ROWB);
+#pragma unroll
+        for (int dh = 0; dh < 3; ++dh) {
+          const int ri = hr - dh;
+          if (ri < 0 || ri >= RW) continue;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[ri][j] = mfma16(wf[dh][j], xf, acc[ri][j]);
+        }
+      }
+    }
+    __syncthreads();                                    // fragment reads done
+    if (kc + 1 < nchunks) {
+      store_chunk();
+      __syncthreads();
+    }
+  }
+  conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0, 0,
+                                                                tm);
+}
+
+template <int W>
+hipError_t launch_win_cp_w(const ConvFwdParams& p, hipStream_t s) {
+  const int grid = win_grid(p);
+  const bool cc = p.C2 > 0;
+#define CP_EPI(CC)                                                                                           \
+  switch (conv_epi_mode(p)) {                                                                                \
+    case EPI_FWD: UNET_LAUNCH((conv_win_cp_kernel<W, CC, EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p); break;     \
+    case EPI_DGRAD: UNET_LAUNCH((conv_win_cp_kernel<W, CC, EPI_DGRAD>), dim3(grid), dim3(NTHR), 0, s, p); break; \
+    case EPI_STATS: UNET_LAUNCH((conv_win_cp_kernel<W, CC, EPI_STATS>), dim3(grid), dim3(NTHR), 0, s, p); break; \
+    case EPI_DGRAD_NORM:                                                                                     \
+      if (CC) return hipErrorInvalidValue;                                                                   \
+      UNET_LAUNCH((conv_win_cp_kernel<W, false, EPI_DGRAD_NORM>), dim3(grid), dim3(NTHR), 0, s, p);          \
+      break;                                                                                                 \
+    default: UNET_LAUNCH((conv_win_cp_kernel<W, CC, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p); break;     \
+  }
+  if (cc) {
+    CP_EPI(true)
+  } else {
+    CP_EPI(false)
+  }
+#undef CP_EPI
+  return launch_status();
+}
+
+hipError_t launch_win_cp(const ConvFwdParams& p, hipStream_t s) {
+  return p.OW == 64 ? launch_win_cp_w<64>(p, s) : hipErrorInvalidValue;
+}
+
+// Chunk-pipelined window on 128-wide rows (win_cp128_eligible): items = (depth tap, input
+// chunk) pairs; the next item's halo (12 x 16 bytes per thread, conv_win_pf_kernel's affine
+// map, the depth-shifted slice in 3D) and weight rows (5 x 16 bytes) are loaded into
+// registers under the current item's MFMAs.  Same images, operands, order and epilogue as
+// conv_win_kernel<128, 32, 512, CONCAT, EPI, GEO>: bit-identical outputs.
+template <int GEO, bool CONCAT, int EPI>
+__global__ void __launch_bounds__(NTHR, 2) conv_win_cp128_kernel(const ConvFwdParams p) {
+  constexpr int W = 128, R = 4, BM = 512, BN = 32, ROWB = PF_ROWB;
+  constexpr int TC = 2, NCS = 4, RW = 4, TM = RW * TC, TN = 2, WMP = BM / 4;
+  constexpr int NWG = 9 * BN * 4, WGR = (NWG + NTHR - 1) / NTHR;
+  constexpr bool D3 = GEO == GEO_3D;
+  using Map = StripTiles<W, RW, TC, NCS>;
+  static_assert(epi_lds_bytes<BM, BN>() <= PF_XB, "epilogue staging aliases the halo image");
+  __shared__ __attribute__((aligned(1024))) char smem[PF_XB + PF_WB];
+  char* Xs = smem;
+  char* Ws = smem + PF_XB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = p.OH;
+  const int D = D3 ? p.OD : 1;
+  const int rows_total = p.N * D * H;
+  const int M = rows_total * W;
+  const int tiles_n = p.Cout / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm0 = bid / tiles_n, tn = bid % tiles_n;
+  const int tm = p.rev ? (int)(gridDim.x / tiles_n) - 1 - tm0 : tm0;
+  const int g0 = tm * R, n0 = tn * BN;
+  const int dsl = D3 ? (g0 / H) % D : 0;
+  const int Cin = p.C1 + p.C2;
+  const int nchunks = Cin >> 5;
+  constexpr int OOB = 0x7fffffff;
+  const int grow0 = (g0 / (D * H)) * (D * H);          // the window's image / volume
+  const size_t img_px = (size_t)grow0 * W;
+  const char* s1b = (const char*)p.src1 + img_px * p.C1 * 2;
+  const char* s2b = p.src2 ? (const char*)p.src2 + img_px * p.C2 * 2 : s1b;
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc((void*)s1b, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc((void*)s2b, (short)0, OOB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
+  const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
+  // depth taps whose input slice is padding contribute nothing: skipped
+  const int kd_lo = (D3 && dsl == 0) ? 1 : 0, kd_hi = D3 ? (dsl == D - 1 ? 2 : 3) : 1;
+  const int nitems = (kd_hi - kd_lo) * nchunks;
+
+  u32x4 xv[12], wv[WGR];
+  const int lds_t = (1 + (tid >> 2)) * 64 + 16 * ((tid & 3) ^ (((1 + (tid >> 2)) >> 1) & 3));
+  auto load_item = [&](const int it) {
+    const int kd = kd_lo + it / nchunks, kc = it - (it / nchunks) * nchunks;
+    const bool from1 = !CONCAT || (kc << 5) < p.C1;
+    const int C = from1 ? p.C1 : p.C2;
+    const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
+    const __amdgpu_buffer_rsrc_t rs = from1 ? rs1 : rs2;
+    const int shift = D3 ? (kd - 1) * H : 0;
+    const int tb = ((tid >> 2) * C + cb + (tid & 3) * 8) * 2;   // the thread's column / chunk part
+#pragma unroll
+    for (int c = 0; c < 12; ++c) {
+      const int hr = c >> 1;
+      const int gr = g0 - 1 + hr;
+      const bool ok = (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)gr < (unsigned)rows_total &&
+                      (unsigned)(gr + shift) < (unsigned)rows_total;
+      xv[c] = __builtin_amdgcn_raw_buffer_load_b128(
+          rs, ok ? ((gr + shift - grow0) * W + 64 * (c & 1)) * C * 2 + tb : OOB, 0, 0);
+    }
+#pragma unroll
+    for (int c = 0; c < WGR; ++c) {
+      const int u = tid + NTHR * c;
+      const int row = u >> 2, tap = row / BN, n = row - tap * BN;
+      wv[c] = __builtin_amdgcn_raw_buffer_load_b128(
+          rsw, u < NWG ? ((n0 + n) * p.Kpad + (kd * 9 + tap) * Cin + (kc << 5) + (tid & 3) * 8) * 2 : OOB, 0, 0);
+    }
+  };
+  auto store_item = [&]() {
+#pragma unroll
+    for (int c = 0; c < 12; ++c) *(u32x4*)(Xs + lds_t + (c >> 1) * ROWB + (c & 1) * 4096) = xv[c];
+    if (tid < 48) *(u32x4*)(Xs + (tid >> 3) * ROWB + ((tid >> 2) & 1) * 129 * 64 + 16 * (tid & 3)) = (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int c = 0; c < WGR; ++c) {
+      const int u = tid + NTHR * c;
+      const int row = u >> 2;
+      if (u < NWG) *(u32x4*)(Ws + row * 64 + 16 * ((tid & 3) ^ ((row >> 1) & 3))) = wv[c];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int fsub = lane >> 4, fr = lane & 15;
+  const int r0 = (wave / NCS) * RW, c0 = (wave % NCS) * 16 * TC;
+  int xbase[3];
+#pragma unroll
+  for (int dw = 0; dw < 3; ++dw) {
+    const int hc = fr + dw;
+    xbase[dw] = r0 * ROWB + c0 * 64 + hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3));
+  }
+  const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
+  load_item(0);
+  store_item();
+  __syncthreads();
+  for (int it = 0; it < nitems; ++it) {
+    if (it + 1 < nitems) load_item(it + 1);            // in flight under this item's MFMAs
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw) {
+      h16x8 wf[3][TN];
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) wf[dh][j] = *(const h16x8*)(Ws + ((3 * dh + dw) * BN + 16 * j) * 64 + wbase);
+#pragma unroll
+      for (int hr = 0; hr < RW + 2; ++hr) {
+#pragma unroll
+        for (int ci = 0; ci < TC; ++ci) {
+          const h16x8 xf = *(const h16x8*)(Xs + xbase[dw] + hr * ROWB + ci * 16 * 64);
+#pragma unroll
+          for (int dh = 0; dh < 3; ++dh) {
+            const int ri = hr - dh;
+            if (ri < 0 || ri >= RW) continue;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[ri * TC + ci][j] = mfma16(wf[dh][j], xf, acc[ri * TC + ci][j]);
+          }
+        }
+      }
+    }
+    __syncthreads();                                    // fragment reads done
+    if (it + 1 < nitems) {
+      store_item();
+      __syncthreads();
+    }
+  }
+  if constexpr (D3)
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0, 0, tm);
+  else
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0, 0,
+                                                                  tm);
+}
+
+template <int GEO>
+hipError_t launch_win_cp128_g(const ConvFwdParams& p, hipStream_t s) {
+  const int grid = win_grid(p);
+  const bool cc = p.C2 > 0;
+#define CP1_EPI(CC)                                                                                                \
+  switch (conv_epi_mode(p)) {                                                                                     \
+    case EPI_FWD: UNET_LAUNCH((conv_win_cp128_kernel<GEO, CC, EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p); break;     \
+    case EPI_DGRAD: UNET_LAUNCH((conv_win_cp128_kernel<GEO, CC, EPI_DGRAD>), dim3(grid), dim3(NTHR), 0, s, p); break; \
+    case EPI_STATS: UNET_LAUNCH((conv_win_cp128_kernel<GEO, CC, EPI_STATS>), dim3(grid), dim3(NTHR), 0, s, p); break; \
+    case EPI_DGRAD_NORM:                                                                                          \
+      if (CC) return hipErrorInvalidValue;                                                                        \
+      UNET_LAUNCH((conv_win_cp128_kernel<GEO, false, EPI_DGRAD_NORM>), dim3(grid), dim3(NTHR), 0, s, p);          \
+      break;                                                                                                      \
+    default: UNET_LAUNCH((conv_win_cp128_kernel<GEO, CC, EPI_GENERIC>), dim3(grid), dim3(NTHR), 0, s, p); break;     \
+  }
+  if (cc) {
+    CP1_EPI(true)
+  } else {
+    CP1_EPI(false)
+  }
+#undef CP1_EPI
+  return launch_status();
+}
+
+hipError_t launch_win_cp128(const ConvFwdParams& p, hipStream_t s) {
+  return (p.KD == 3) ? launch_win_cp128_g<GEO_3D>(p, s) : launch_win_cp128_g<GEO_2D>(p, s);
+}
+
 hipError_t launch_win_pf(const ConvFwdParams& p, hipStream_t s) {
   const int grid = win_grid(p);
   switch (conv_epi_mode(p)) {
@@ -783,6 +1123,10 @@ template <int BN, int BM>
 hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
   if constexpr (BN == 32 && BM == 512) {
     if (win_pf_eligible(p)) return launch_win_pf(p, s);
+    if (win_cp128_eligible(p)) return launch_win_cp128(p, s);
+  }
+  if constexpr (BN == 64 && BM == 256) {
+    if (win_cp_eligible(p)) return launch_win_cp(p, s);
   }
   const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
   const int grid = win_grid(p);

@@ -103,6 +103,7 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.drop_idx0 = get<unsigned long long>(d, "drop_idx0", 0ull);
   p.rev = get<int>(d, "rev", 0);
   p.win_pf = get<int>(d, "win_pf", 0);
+  p.win_cp = get<int>(d, "win_cp", 0);
   p.dst1 = const_cast<void*>(getp(d, "dst1"));
   p.dst2 = const_cast<void*>(getp(d, "dst2"));
   p.D1 = get<int>(d, "D1", p.Cout);

@@ -69,8 +69,10 @@ def _r64(k: int) -> int:
 #   dw_wgs       workgroups (= slab rows) per fused data + weight gradient launch (512)
 #   win_pf       windows per workgroup of the persistent prefetching row window on 128-wide
 #                32 -> 32 channel convs (conv_win.h conv_win_pf_kernel) (8; 0 off)
+#   win_cp       64-channel row windows on 64-wide rows load the next input chunk under the
+#                current chunk's MFMAs (conv_win.h conv_win_cp_kernel) (1; 0 off)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
-                       tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8)
+                       tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8, win_cp=1)
 
 
 class Fusion:
@@ -926,7 +928,8 @@ class NativeUNet:
         idd, ih, iw = self.sdims(in_level or level)
         kd = K if self.dims == 3 else 1
         return dict(N=self.B, OD=od, OH=oh, OW=ow, ID=idd, IH=ih, IW=iw, KD=kd, KH=K, KW=K,
-                    stride=stride, pad=pad, tile=0, win_pf=self.opts["win_pf"])
+                    stride=stride, pad=pad, tile=0, win_pf=self.opts["win_pf"],
+                    win_cp=self.opts["win_cp"])
 
     def _salt(self, lname):
         return [l.name for l in self.spec.layers].index(lname)
