@@ -154,11 +154,12 @@ def test_win_cp128_3d_equals_window_kernel(cuda_dev, N, D, C1, C2, Cout, rev):
     ref = F.relu(F.conv3d(xin.float().permute(0, 4, 1, 2, 3), w.float().permute(4, 3, 0, 1, 2), bias, padding=1))
     assert rel_err(got[0], ref.permute(0, 2, 3, 4, 1)) < 1e-2
     z = torch.empty_like(out)
-    rows, _ = C().conv_stat_tiles(dict(geo, C1=C1, C2=C2, Cout=Cout, stats=1))
-    st = torch.empty(rows * 2 * Cout, device=cuda_dev)
-    ds = dict(geo, C1=C1, C2=C2, src1=ptr(a), wgt=ptr(wp), bias=ptr(bias), Cout=Cout, dst1=ptr(z), stats=ptr(st))
+    ds = dict(geo, C1=C1, C2=C2, src1=ptr(a), wgt=ptr(wp), bias=ptr(bias), Cout=Cout, dst1=ptr(z))
     if C2:
         ds["src2"] = ptr(b2)
+    rows, _ = C().conv_stat_tiles(dict(ds, stats=1))
+    st = torch.empty(rows * 2 * Cout, device=cuda_dev)
+    ds["stats"] = ptr(st)
     _run(ds, [z, st])
     dy = torch.randn(N, D, H, H, Cout, device=cuda_dev).bfloat16()
     wdg = _pad64(w.flip(0, 1, 2).permute(3, 0, 1, 2, 4).reshape(C1 + C2, -1))

@@ -183,3 +183,19 @@ def test_fused_dgrad_wgrad_host_checks():
                 dict(relu=1, bias=1)):
         with pytest.raises(ValueError):
             C.conv_fwd_grid(dict(base, **bad))
+
+
+def test_persistent_window_grid():
+    """win_pf > 0: the 2D 128-wide 32 -> 32 channel window runs win_pf consecutive windows
+    per workgroup (grid = ceil(windows / win_pf)); any other shape keeps one window per
+    workgroup, and the engine's plans carry the option on every conv launch."""
+    C = native.require()
+    base = dict(N=3, OH=128, OW=128, IH=128, IW=128, KH=3, KW=3, pad=1, C1=32, src1=1, wgt=1, Cout=32, relu=1,
+                dst1=1)
+    nwin = 3 * 128 // 4
+    assert C.conv_fwd_grid(base) == nwin
+    for pf in (1, 5, 8, 200):
+        assert C.conv_fwd_grid(dict(base, win_pf=pf)) == (nwin + pf - 1) // pf
+    for other in (dict(C1=64), dict(Cout=64), dict(OW=64, IW=64, OH=64, IH=64), dict(tile=12, Cout=64)):
+        d = dict(base, **other)
+        assert C.conv_fwd_grid(dict(d, win_pf=8)) == C.conv_fwd_grid(d)
