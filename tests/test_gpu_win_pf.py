@@ -162,3 +162,52 @@ def test_win_pf_head_onload_dgrad_equals_window_kernel(cuda_dev, N, pf, rev, bce
         outs.append(dx)
     assert torch.isfinite(outs[1]).all()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("N,HW,pf,rev,mode", [(1, 256, 8, 0, "pool"), (2, 256, 3, 1, "dgrad"), (1, 512, 8, 1, "pool"),
+                                              (1, 512, 5, 0, "dgrad"), (1, 512, 8, 0, "stats")])
+def test_win_pf_segmented_rows_equal_window_kernel(cuda_dev, N, HW, pf, rev, mode):
+    """Rows wider than 128 (the 512^2 / 256^2 models' level 1) as 128-wide segments: the
+    halo columns -1 / 128 come from the neighbouring segments."""
+    torch.manual_seed(85)
+    x = F.relu(torch.randn(N, HW, HW, 32, device=cuda_dev)).bfloat16()
+    w = (torch.randn(3, 3, 32, 32, device=cuda_dev) * 0.1).bfloat16()
+    b = torch.randn(32, device=cuda_dev) * 0.1
+    geo = dict(N=N, OH=HW, OW=HW, IH=HW, IW=HW, KH=3, KW=3, pad=1, C1=32, Cout=32, rev=rev)
+    y = torch.empty(N, HW, HW, 32, device=cuda_dev, dtype=torch.bfloat16)
+    if mode == "pool":
+        bits = torch.empty(N * HW * HW * 4, device=cuda_dev, dtype=torch.uint8)
+        pooled = torch.empty(N, HW // 2, HW // 2, 32, device=cuda_dev, dtype=torch.bfloat16)
+        codes = torch.empty(N * (HW // 2) ** 2 * 4, device=cuda_dev, dtype=torch.int32)
+        wp = pack_fwd(w)
+        d = dict(geo, src1=ptr(x), wgt=ptr(wp), bias=ptr(b), relu=1, dst1=ptr(y), relu_bits=ptr(bits),
+                 pool_dst=ptr(pooled), pool_code=ptr(codes))
+        outs = [y, bits, pooled, codes]
+    elif mode == "stats":
+        wp = pack_fwd(w)
+        d = dict(geo, src1=ptr(x), wgt=ptr(wp), bias=ptr(b), dst1=ptr(y))
+        rows, _ = C().conv_stat_tiles(dict(d, stats=1))
+        st = torch.empty(rows * 2 * 32, device=cuda_dev)
+        d["stats"] = ptr(st)
+        outs = [y, st]
+    else:
+        wp = pack_dgrad(w)
+        mk = _pack_bits(torch.randn(N, HW, HW, 32, device=cuda_dev))
+        d = dict(geo, src1=ptr(x), wgt=ptr(wp), dst1=ptr(y), mask1=ptr(mk), mask_bits=1)
+        outs = [y]
+    res = []
+    for p in (0, pf):
+        for t in outs:
+            t.fill_(float("nan") if t.is_floating_point() else 0)
+        g = C().conv_fwd_grid(dict(d, win_pf=p))
+        C().conv_fwd(dict(d, win_pf=p), stream())
+        torch.cuda.synchronize()
+        res.append([t.clone() for t in outs])
+        if p:
+            nwin = N * HW // 4 * (HW // 128)
+            assert g == (nwin + p - 1) // p
+    for a, bb in zip(*res):
+        assert torch.equal(a, bb)
+    if mode == "pool":
+        exp = nhwc(F.relu(F.conv2d(nchw(x.float()), w.float().permute(3, 2, 0, 1), b, padding=1)))
+        assert rel_err(res[1][0], exp) < 1e-2

@@ -46,8 +46,10 @@ inline int win_rows(const ConvFwdParams& p) {
 // input chunk, 32 output channels, bias + ReLU forward or data-gradient epilogue (level 1
 // of the 128^2 UNet: the forward of conv1b / conv9b, the skip data gradient of conv9a).
 // (every epilogue mode; the head-on-load data gradient of the head input too)
+// (rows wider than 128 -- the 512^2 / 256^2 models' level 1 -- as 128-wide segments)
 inline bool win_pf_eligible(const ConvFwdParams& p) {
-  return p.win_pf > 0 && p.OW == 128 && p.KD == 1 && p.OD == 1 && p.C1 == 32 && p.C2 == 0 && p.Cout == 32 &&
+  const bool w_ok = p.OW == 128 || (p.OW % 128 == 0 && p.OW > 128 && p.OW <= 8192 && !p.hg.prob);
+  return p.win_pf > 0 && w_ok && p.KD == 1 && p.OD == 1 && p.C1 == 32 && p.C2 == 0 && p.Cout == 32 &&
          p.tile != 12 && !p.xform && !p.s2d && !p.ut.x && !p.fw.x && p.OH % 4 == 0 &&
          (!p.hg.prob || conv_epi_mode(p) == EPI_DGRAD);
 }
@@ -72,7 +74,7 @@ inline int win_grid(const ConvFwdParams& p) {
   const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
   const int rows = p.N * p.OD * p.OH;
   const int R = win_rows(p);
-  if (win_pf_eligible(p)) return (rows / 4 + p.win_pf - 1) / p.win_pf;
+  if (win_pf_eligible(p)) return (rows / 4 * (p.OW / 128) + p.win_pf - 1) / p.win_pf;
   return ((rows + R - 1) / R) * (p.OW / W) * (p.Cout / win_bn(p));
 }
 // (BN, BM, row width) combinations win_bn / win_bm can select (the 64-channel tile also
@@ -604,9 +606,15 @@ constexpr int PF_CPT = 6 * 128 * 4 / NTHR;    // 16-byte granules of the 6 halo 
 constexpr int PF_XB = 6 * PF_ROWB, PF_WB = 9 * 32 * 64;
 static_assert(512 * 36 * 2 <= PF_XB, "epilogue staging aliases the halo image");
 
-template <int EPI, int XF>
+// GEO_SEG: rows of Wf = p.OW > 128 pixels as 128-wide segments (window = 4 rows x one
+// segment, windows in (row group, segment) order as conv_win_kernel's); the halo columns
+// -1 / 128 are the neighbouring segments' pixels (zeros only at the row ends), loaded by 48
+// threads beside the affine part.
+template <int EPI, int XF, int GEO = GEO_2D>
 __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParams p) {
-  static_assert(XF == 0 || (XF == 3 && EPI == EPI_DGRAD), "plain source or head-on-load data gradient");
+  static_assert(XF == 0 || (XF == 3 && EPI == EPI_DGRAD && GEO == GEO_2D), "plain source or head-on-load data gradient");
+  static_assert(GEO == GEO_2D || GEO == GEO_SEG, "2D rows");
+  constexpr bool SEG = GEO == GEO_SEG;
   constexpr int W = 128, R = 4, BM = 512, BN = 32, ROWB = PF_ROWB;
   constexpr int TC = 2, NCS = 4, RW = 4, TM = RW * TC, TN = 2, WMP = BM / 4;
   using Map = StripTiles<W, RW, TC, NCS>;
@@ -615,9 +623,11 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
   char* Ws = smem + PF_XB;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = p.OH;
+  const int Wf = SEG ? p.OW : W;
+  const int nseg = SEG ? p.OW / W : 1;
   const int rows_total = p.N * H;
-  const int M = rows_total * W;
-  const int nwin = rows_total / R;                   // H % R == 0 (win_pf_eligible)
+  const int M = rows_total * Wf;
+  const int nwin = rows_total / R * nseg;            // H % R == 0 (win_pf_eligible)
   const int w_lo = (int)blockIdx.x * p.win_pf;
   const int w_hi = w_lo + p.win_pf < nwin ? w_lo + p.win_pf : nwin;
   if (w_lo >= w_hi) return;
@@ -630,7 +640,7 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
   // validity is wave-uniform.  LDS slot = column + 1, physical chunk = logical ^
   // ((slot >> 1) & 3), as conv_win_kernel's DMA leaves it; the zero columns -1 / 128
   // (slots 0 / 129) are rewritten per window (the epilogue's staging overwrites them).
-  u32x4 hv[PF_CPT];
+  u32x4 hv[PF_CPT], ev = {0u, 0u, 0u, 0u};
   const int gl_t = tid * 16;
   const int lds_t = (1 + (tid >> 2)) * 64 + 16 * ((tid & 3) ^ (((1 + (tid >> 2)) >> 1) & 3));
   // XF 3: slot sl = tid + 256 j of the 6 x 144-slot image (conv_win_kernel's XF 3 map)
@@ -640,7 +650,8 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
   HeadGradCtx hctx{};
   if constexpr (XF == 3) hctx = head_grad_ctx(p.hg);
   auto load_halo = [&](const int w) {
-    const int g0 = (p.rev ? nwin - 1 - w : w) * R;
+    const int tmw = p.rev ? nwin - 1 - w : w;
+    const int g0 = (tmw / nseg) * R, col0 = (tmw % nseg) * W;
     if constexpr (XF == 3) {
       const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
 #pragma unroll
@@ -660,13 +671,22 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
     const int grow0 = (g0 / H) * H;                  // the window's image (32-bit offsets from it)
     const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)grow0 * W * 64), (short)0, OOB, 0x00020000);
-    const int rowoff = (g0 - 1 - grow0) * W * 64;    // byte offset of halo row 0 (may be -8 KB: row 0 then off)
+        __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)grow0 * Wf * 64), (short)0, OOB, 0x00020000);
+    // byte offset of halo row 0's first pixel (negative at the image top: row 0 is then off)
+    const int rowoff = ((g0 - 1 - grow0) * Wf + col0) * 64;
 #pragma unroll
     for (int c = 0; c < PF_CPT; ++c) {
       const int hr = c >> 1;
       const bool ok = (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)(g0 - 1 + hr) < (unsigned)rows_total;
-      hv[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? rowoff + hr * W * 64 + (c & 1) * 4096 + gl_t : OOB, 0, 0);
+      hv[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? rowoff + hr * Wf * 64 + (c & 1) * 4096 + gl_t : OOB, 0, 0);
+    }
+    if constexpr (SEG) {
+      // halo columns -1 / 128 of the segment: thread t < 48 -> row t / 8, side (t / 4) & 1, chunk t & 3
+      const int hr = tid >> 3, col = ((tid >> 2) & 1) ? col0 + W : col0 - 1;
+      const bool ok = tid < 48 && (hr > 0 || top_in) && (hr < R + 1 || bot_in) &&
+                      (unsigned)(g0 - 1 + hr) < (unsigned)rows_total && (unsigned)col < (unsigned)Wf;
+      ev = __builtin_amdgcn_raw_buffer_load_b128(
+          rs, ok ? ((g0 - 1 + hr - grow0) * Wf + col) * 64 + (tid & 3) * 16 : OOB, 0, 0);
     }
   };
   auto store_halo = [&]() {
@@ -694,7 +714,8 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
     }
 #pragma unroll
     for (int c = 0; c < PF_CPT; ++c) *(u32x4*)(Xs + lds_t + (c >> 1) * ROWB + (c & 1) * 4096) = hv[c];
-    if (tid < 48) *(u32x4*)(Xs + (tid >> 3) * ROWB + ((tid >> 2) & 1) * 129 * 64 + 16 * (tid & 3)) = (u32x4){0u, 0u, 0u, 0u};
+    // (slot 0 / 129: chunk swizzle (slot >> 1) & 3 = 0 / 0)
+    if (tid < 48) *(u32x4*)(Xs + (tid >> 3) * ROWB + ((tid >> 2) & 1) * 129 * 64 + 16 * (tid & 3)) = ev;
   };
   load_halo(w_lo);
   {
@@ -737,7 +758,7 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
   const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
   for (int w = w_lo; w < w_hi; ++w) {
     const int tm = p.rev ? nwin - 1 - w : w;
-    const int g0 = tm * R;
+    const int g0 = (tm / nseg) * R, col0 = (tm % nseg) * W;
     if (w + 1 < w_hi) load_halo(w + 1);             // in flight under this window's MFMAs + epilogue
     f32x4 acc[TM][TN];
 #pragma unroll
@@ -767,8 +788,12 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
       }
     }
     __syncthreads();                                 // fragment reads done: the epilogue stages in Xs
-    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(p, acc, smem, g0 * W, 0, M, wave, 0, lane, tid, 0,
-                                                                  0, tm, &ec);
+    if constexpr (SEG)
+      conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, W, W>(p, acc, smem, g0, 0, M, wave, 0, lane, tid, Wf,
+                                                                    col0, tm, &ec);
+    else
+      conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(p, acc, smem, g0 * W, 0, M, wave, 0, lane, tid, 0,
+                                                                    0, tm, &ec);
     if (w + 1 < w_hi) {
       __syncthreads();                               // staging reads done
       store_halo();
@@ -1102,6 +1127,18 @@ hipError_t launch_win_cp128(const ConvFwdParams& p, hipStream_t s) {
 
 hipError_t launch_win_pf(const ConvFwdParams& p, hipStream_t s) {
   const int grid = win_grid(p);
+  if (p.OW > 128) {
+    switch (conv_epi_mode(p)) {
+      case EPI_FWD: UNET_LAUNCH((conv_win_pf_kernel<EPI_FWD, 0, GEO_SEG>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      case EPI_DGRAD: UNET_LAUNCH((conv_win_pf_kernel<EPI_DGRAD, 0, GEO_SEG>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      case EPI_STATS: UNET_LAUNCH((conv_win_pf_kernel<EPI_STATS, 0, GEO_SEG>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      case EPI_DGRAD_NORM:
+        UNET_LAUNCH((conv_win_pf_kernel<EPI_DGRAD_NORM, 0, GEO_SEG>), dim3(grid), dim3(NTHR), 0, s, p);
+        break;
+      default: UNET_LAUNCH((conv_win_pf_kernel<EPI_GENERIC, 0, GEO_SEG>), dim3(grid), dim3(NTHR), 0, s, p); break;
+    }
+    return launch_status();
+  }
   switch (conv_epi_mode(p)) {
     case EPI_FWD: UNET_LAUNCH((conv_win_pf_kernel<EPI_FWD, 0>), dim3(grid), dim3(NTHR), 0, s, p); break;
     case EPI_DGRAD:
