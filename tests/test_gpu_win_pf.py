@@ -211,3 +211,40 @@ def test_win_pf_segmented_rows_equal_window_kernel(cuda_dev, N, HW, pf, rev, mod
     if mode == "pool":
         exp = nhwc(F.relu(F.conv2d(nchw(x.float()), w.float().permute(3, 2, 0, 1), b, padding=1)))
         assert rel_err(res[1][0], exp) < 1e-2
+
+
+@pytest.mark.parametrize("N,pf,rev,gn,stats", [(3, 8, 0, False, True), (2, 5, 1, True, True), (2, 8, 0, True, False)])
+def test_win_pf_normalise_on_load_equals_window_kernel(cuda_dev, N, pf, rev, gn, stats):
+    """Normalised-input convs (norm configs' conv1b / conv9b, xform 1): the persistent
+    window applies y = relu(a z + b) to the prefetched halo in registers and writes the
+    window's own rows to xout -- the same conv output, statistics rows and y."""
+    torch.manual_seed(86)
+    z = torch.randn(N, H, H, 32, device=cuda_dev).bfloat16()
+    a = torch.rand(N if gn else 1, 32, device=cuda_dev) + 0.5
+    b = torch.randn(N if gn else 1, 32, device=cuda_dev) * 0.2
+    w = (torch.randn(3, 3, 32, 32, device=cuda_dev) * 0.1).bfloat16()
+    bias = torch.randn(32, device=cuda_dev) * 0.1
+    wp = pack_fwd(w)
+    out = torch.empty(N, H, H, 32, device=cuda_dev, dtype=torch.bfloat16)
+    yo = torch.empty_like(z)
+    d = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=32, src1=ptr(z), wgt=ptr(wp), bias=ptr(bias),
+             Cout=32, relu=0, dst1=ptr(out), xform=1, xa=ptr(a), xb=ptr(b), xcs=32 if gn else 0, xout=ptr(yo), rev=rev)
+    outs = [out, yo]
+    if stats:
+        nr, _ = C().conv_stat_tiles(dict(d, stats=1))
+        st = torch.empty(nr * 2 * 32, device=cuda_dev)
+        d["stats"] = ptr(st)
+        outs.append(st)
+    else:
+        d.update(relu=1, drop_rate=0.2, seed=3, salt=7)
+    res = []
+    for p in (0, pf):
+        for t in outs:
+            t.fill_(float("nan"))
+        C().conv_fwd(dict(d, win_pf=p), stream())
+        torch.cuda.synchronize()
+        res.append([t.clone() for t in outs])
+    for x0, x1 in zip(*res):
+        assert torch.equal(x0, x1)
+    y_ref = F.relu(z.float() * (a[:, None, None, :] if gn else a) + (b[:, None, None, :] if gn else b))
+    assert (res[1][1].float() - y_ref).abs().max() <= 1e-2 * y_ref.abs().max()

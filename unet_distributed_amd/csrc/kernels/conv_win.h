@@ -50,8 +50,8 @@ inline int win_rows(const ConvFwdParams& p) {
 inline bool win_pf_eligible(const ConvFwdParams& p) {
   const bool w_ok = p.OW == 128 || (p.OW % 128 == 0 && p.OW > 128 && p.OW <= 8192 && !p.hg.prob);
   return p.win_pf > 0 && w_ok && p.KD == 1 && p.OD == 1 && p.C1 == 32 && p.C2 == 0 && p.Cout == 32 &&
-         p.tile != 12 && !p.xform && !p.s2d && !p.ut.x && !p.fw.x && p.OH % 4 == 0 &&
-         (!p.hg.prob || conv_epi_mode(p) == EPI_DGRAD);
+         p.tile != 12 && !p.s2d && !p.ut.x && !p.fw.x && p.OH % 4 == 0 &&
+         (!p.hg.prob || conv_epi_mode(p) == EPI_DGRAD) && (!p.xform || (p.xform == 1 && p.OW == 128 && !p.hg.prob));
 }
 // Chunk-pipelined window (conv_win_cp_kernel): 2D 64-wide full rows, the 64-channel tile,
 // plain or concat source, no operand transform, two or more 32-channel input chunks (level 2
@@ -612,7 +612,8 @@ static_assert(512 * 36 * 2 <= PF_XB, "epilogue staging aliases the halo image");
 // threads beside the affine part.
 template <int EPI, int XF, int GEO = GEO_2D>
 __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParams p) {
-  static_assert(XF == 0 || (XF == 3 && EPI == EPI_DGRAD && GEO == GEO_2D), "plain source or head-on-load data gradient");
+  static_assert(XF == 0 || (XF == 3 && EPI == EPI_DGRAD && GEO == GEO_2D) || (XF == 1 && GEO == GEO_2D),
+                "plain source, head-on-load data gradient or normalise on load");
   static_assert(GEO == GEO_2D || GEO == GEO_SEG, "2D rows");
   constexpr bool SEG = GEO == GEO_SEG;
   constexpr int W = 128, R = 4, BM = 512, BN = 32, ROWB = PF_ROWB;
@@ -649,6 +650,12 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
   uint32_t hbits[HJ];
   HeadGradCtx hctx{};
   if constexpr (XF == 3) hctx = head_grad_ctx(p.hg);
+  // XF 1 (normalise on load, conv_win_kernel's XF 1): y = relu(xa z + xb) with the thread's
+  // 8 channels' coefficients of the prefetched window's sample, applied in registers before
+  // the LDS store (padding rows stay zero); the window's own rows also go to xout
+  float xan[8], xbn[8];
+  int pf_g0 = 0;
+  bool pf_top = false, pf_bot = false;
   auto load_halo = [&](const int w) {
     const int tmw = p.rev ? nwin - 1 - w : w;
     const int g0 = (tmw / nseg) * R, col0 = (tmw % nseg) * W;
@@ -670,6 +677,17 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
     }
     const int grow0 = (g0 / H) * H;                  // the window's image (32-bit offsets from it)
     const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
+    if constexpr (XF == 1) {
+      const size_t cs = (size_t)(g0 / H) * p.xcs + (tid & 3) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        xan[e] = p.xa[cs + e];
+        xbn[e] = p.xb[cs + e];
+      }
+      pf_g0 = g0;
+      pf_top = top_in;
+      pf_bot = bot_in;
+    }
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)(src + (size_t)grow0 * Wf * 64), (short)0, OOB, 0x00020000);
     // byte offset of halo row 0's first pixel (negative at the image top: row 0 is then off)
@@ -712,8 +730,27 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
       }
       return;
     }
+    if constexpr (XF == 1) {
 #pragma unroll
-    for (int c = 0; c < PF_CPT; ++c) *(u32x4*)(Xs + lds_t + (c >> 1) * ROWB + (c & 1) * 4096) = hv[c];
+      for (int c = 0; c < PF_CPT; ++c) {
+        const int hr = c >> 1;
+        const int gr = pf_g0 - 1 + hr;
+        u32x4 v = hv[c];
+        if ((hr > 0 || pf_top) && (hr < R + 1 || pf_bot) && (unsigned)gr < (unsigned)rows_total) {
+          float f[8];
+          unpack8(v, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(xan[e], f[e], xbn[e]), 0.f);
+          v = pack8(f);
+          if (p.xout && hr >= 1 && hr <= R)
+            *(u32x4*)((h16*)p.xout + ((size_t)gr * W + (tid >> 2) + 64 * (c & 1)) * 32 + (tid & 3) * 8) = v;
+        }
+        *(u32x4*)(Xs + lds_t + hr * ROWB + (c & 1) * 4096) = v;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < PF_CPT; ++c) *(u32x4*)(Xs + lds_t + (c >> 1) * ROWB + (c & 1) * 4096) = hv[c];
+    }
     // (slot 0 / 129: chunk swizzle (slot >> 1) & 3 = 0 / 0)
     if (tid < 48) *(u32x4*)(Xs + (tid >> 3) * ROWB + ((tid >> 2) & 1) * 129 * 64 + 16 * (tid & 3)) = ev;
   };
@@ -1137,6 +1174,15 @@ hipError_t launch_win_pf(const ConvFwdParams& p, hipStream_t s) {
         break;
       default: UNET_LAUNCH((conv_win_pf_kernel<EPI_GENERIC, 0, GEO_SEG>), dim3(grid), dim3(NTHR), 0, s, p); break;
     }
+    return launch_status();
+  }
+  if (p.xform) {                        // normalise on load (conv_fwd_prepare: statistics / generic epilogue)
+    if (conv_epi_mode(p) == EPI_STATS)
+      UNET_LAUNCH((conv_win_pf_kernel<EPI_STATS, 1>), dim3(grid), dim3(NTHR), 0, s, p);
+    else if (conv_epi_mode(p) == EPI_GENERIC)
+      UNET_LAUNCH((conv_win_pf_kernel<EPI_GENERIC, 1>), dim3(grid), dim3(NTHR), 0, s, p);
+    else
+      return hipErrorInvalidValue;
     return launch_status();
   }
   switch (conv_epi_mode(p)) {
