@@ -100,3 +100,13 @@ def test_dry_dispatch_reports_a_missing_kernel():
         pytest.skip("host check rejects this combination up front")
     bad = p.check_dispatch(0, p.size())
     assert [b[1] for b in bad] == ["bad"]
+
+
+@pytest.mark.parametrize("dims,img,batch,cin", [(2, 512, 128, 1), (2, 512, 64, 1), (3, 128, 16, 4), (2, 128, 2048, 4)])
+def test_largest_benched_batches_plan(dims, img, batch, cin):
+    """The largest per-GPU batches the config sweeps run (512^2 b128: a 2.1 GB fine gradient;
+    3D b16; 2D b2048) plan without a launch refusing a > 2 GiB operand: kernels that count
+    32-bit offsets from the tensor start (the transposed-conv windows) step aside for the
+    per-tile-based ones there (round 5: 512^2 b128 failed after the 256-wide tconv dgrad)."""
+    e = _engine("none", False, dims, img, batch=batch, in_channels=cin)
+    check_engine(e)

@@ -969,7 +969,8 @@ static bool tconv_fwd_eligible(const ConvFwdParams& p) {
   const bool w_ok = p.OW == 8 || p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128;
   return p.shuffle == 2 && p.KD == 1 && p.KH == 1 && p.KW == 1 && p.OD == 1 && w_ok && p.IW == p.OW &&
          p.IH == p.OH && p.C2 == 0 && (p.C1 % 32) == 0 && ((p.Cout >> 2) % 32) == 0 && !p.relu &&
-         p.drop_rate == 0.f && !p.mask1 && !p.stats && p.out_scale == 1.f;
+         p.drop_rate == 0.f && !p.mask1 && !p.stats && p.out_scale == 1.f &&
+         (long long)p.N * p.IH * p.IW * p.C1 * 2 < (1LL << 31) - 64;      // (offsets from the tensor start)
 }
 
 // 2D transposed-conv data gradient (2x2 stride-2 conv of the fine gradient); coarse rows
@@ -979,7 +980,10 @@ static bool tconv_dgrad_eligible(const ConvFwdParams& p) {
   const bool w_ok = p.OW == 8 || p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128 || p.OW == 256;
   return !p.shuffle && p.KD == 1 && p.KH == 2 && p.KW == 2 && p.stride == 2 && p.pad == 0 && p.OD == 1 &&
          p.ID == 1 && w_ok && p.IW == 2 * p.OW && p.IH == 2 * p.OH && p.up1 == 1 && p.C2 == 0 &&
-         (p.C1 % 32) == 0 && (p.Cout % 64) == 0 && (!p.stats || p.nz) && p.drop_rate == 0.f;
+         (p.C1 % 32) == 0 && (p.Cout % 64) == 0 && (!p.stats || p.nz) && p.drop_rate == 0.f &&
+         // (32-bit offsets from the tensor start: the 512^2 model at batch 128 has a 2.1 GB fine
+         // gradient and takes the implicit GEMM, whose offsets count from each tile's images)
+         (long long)p.N * p.IH * p.IW * p.C1 * 2 < (1LL << 31) - 64;
 }
 
 int conv_fwd_pick(const ConvFwdParams& p);
