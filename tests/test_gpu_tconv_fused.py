@@ -200,3 +200,34 @@ def test_tconv_onload_forward(cuda_dev, N, H, K, Cc, Cs, O, epi):
         kept = z != 0
         assert rel_err(z[kept] * 0.75, nhwc(F.relu(ref))[kept]) < 2e-2
 
+
+
+@pytest.mark.parametrize("N,K,pf,rev", [(2, 64, 8, 0), (3, 64, 5, 1), (2, 32, 8, 1), (1, 64, 1, 0)])
+def test_tconv_onload_persistent_window(cuda_dev, N, K, pf, rev):
+    """conv9a's forward on the persistent tconv-on-load window (conv_win.h conv_win_pfu_kernel,
+    win_pf > 0: 256-pixel windows, each wave forming one u halo row from its coarse row with
+    tap-row weights held across the walk, the next window's coarse row and skip halo
+    prefetched): bit-identical to the one-window XF 5 kernel -- output and ReLU bits."""
+    H = 64
+    b, skip, wt, bt, wa, _ = _problem(cuda_dev, N, H, K, 32, 32, 32, 22)
+    dev = cuda_dev
+    F2 = 2 * H
+    wtp = _pad64(wt.reshape(4 * 32, K).bfloat16())
+    wap = _pad64(wa.bfloat16().permute(3, 0, 1, 2).reshape(32, 9 * 64))
+    ba = torch.randn(32, device=dev) * 0.1
+    d0 = dict(N=N, OH=F2, OW=F2, IH=F2, IW=F2, KH=3, KW=3, pad=1, C1=32, C2=32, src1=ptr(b), src2=ptr(skip),
+              wgt=ptr(wap), bias=ptr(ba), Cout=32, relu=1, ut_x=ptr(b), ut_w=ptr(wtp), ut_b=ptr(bt), ut_C=K,
+              ut_kpad=wtp.shape[1], rev=rev)
+    outs = []
+    for p in (0, pf):
+        z = torch.full((N, F2, F2, 32), float("nan"), device=dev, dtype=torch.bfloat16)
+        bits = torch.zeros(N * F2 * F2 * 4, device=dev, dtype=torch.uint8)
+        d = dict(d0, dst1=ptr(z), relu_bits=ptr(bits), win_pf=p)
+        g = C().conv_fwd_grid(d)
+        C().conv_fwd(d, stream())
+        torch.cuda.synchronize()
+        outs.append((z, bits))
+        if p:
+            assert g == (N * F2 // 2 + p - 1) // p
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert torch.isfinite(outs[1][0].float()).all()

@@ -70,11 +70,20 @@ inline bool win_cp128_eligible(const ConvFwdParams& p) {
   return p.win_cp > 1 && p.OW == 128 && (d3 || (p.KD == 1 && p.OD == 1 && p.C1 + p.C2 >= 64)) && p.tile != 12 &&
          !p.xform && !p.hg.prob && !p.s2d && !p.ut.x && !p.fw.x && !win_pf_eligible(p);
 }
+// Persistent prefetching tconv-on-load window (conv_win_pfu_kernel): conv9a of the 128^2 UNet --
+// 2D 128-wide rows, u (32 channels) = tconv2x2s2 of a 32 / 64-channel coarse input formed on
+// load + a 32-channel skip source, 32 output channels, bias + ReLU epilogue.
+inline bool win_pfu_eligible(const ConvFwdParams& p) {
+  return p.win_pf > 0 && p.ut.x && p.OW == 128 && p.KD == 1 && p.OD == 1 && p.C1 == 32 && p.C2 == 32 &&
+         p.Cout == 32 && (p.ut.C == 32 || p.ut.C == 64) && p.tile != 12 && conv_epi_mode(p) == EPI_FWD &&
+         !p.pool_dst && !p.head_w && p.OH % 2 == 0;
+}
 inline int win_grid(const ConvFwdParams& p) {
   const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
   const int rows = p.N * p.OD * p.OH;
   const int R = win_rows(p);
   if (win_pf_eligible(p)) return (rows / 4 * (p.OW / 128) + p.win_pf - 1) / p.win_pf;
+  if (win_pfu_eligible(p)) return (rows / 2 + p.win_pf - 1) / p.win_pf;
   return ((rows + R - 1) / R) * (p.OW / W) * (p.Cout / win_bn(p));
 }
 // (BN, BM, row width) combinations win_bn / win_bm can select (the 64-channel tile also
@@ -1162,6 +1171,216 @@ hipError_t launch_win_cp128(const ConvFwdParams& p, hipStream_t s) {
   return (p.KD == 3) ? launch_win_cp128_g<GEO_3D>(p, s) : launch_win_cp128_g<GEO_2D>(p, s);
 }
 
+// ---------------------------------------------------------------------------------
+// Persistent prefetching tconv-on-load window (win_pfu_eligible; conv9a's forward).  The
+// one-window XF 5 kernel is a serial chain per 512-pixel window -- coarse rows and tconv
+// weights from memory, u MFMAs, LDS stores, u-chunk MFMAs, skip-chunk DMA, wait, MFMAs,
+// epilogue -- at ~18 us per window for ~2.3 us of MFMA (r5 PMC: 25 % MFMA busy).  Here a
+// workgroup walks win_pf consecutive 256-pixel windows (R = 2: a 4-row halo, 37 KB, beside
+// both chunks' weights, 37 KB, staged once): wave w forms halo row w from coarse row
+// g0 / 2 - 1 + (w + 1) / 2 with tap row (w + 1) & 1, whose tconv weight rows it holds in
+// registers for the whole walk; the next window's coarse row (8 x 16 bytes per lane) is loaded
+// under this window's u-chunk MFMAs, its skip halo (8 x 16 bytes per thread, the affine map
+// of conv_win_pf_kernel) under the skip-chunk MFMAs and epilogue.  Same operands and
+// accumulation order as conv_win_kernel's XF 5 (u bit-identical to tconv_fwd_kernel's),
+// same epilogue: bit-identical outputs.
+template <int KS>
+__global__ void __launch_bounds__(NTHR, 2) conv_win_pfu_kernel(const ConvFwdParams p) {
+  constexpr int W = 128, R = 2, HR = R + 2, BM = 256, BN = 32, ROWB = PF_ROWB;
+  constexpr int TC = 2, NCS = 4, RW = 2, TM = RW * TC, TN = 2, WMP = BM / 4;
+  constexpr int CW = W / 2, PB = CW / 16, Cc = KS * 32;
+  constexpr int XB = HR * ROWB, WB = 9 * BN * 64;
+  static_assert(BM * 64 + 4 * 2 * BN * 4 <= XB, "epilogue staging aliases the halo image");
+  using Map = StripTiles<W, RW, TC, NCS>;
+  __shared__ __attribute__((aligned(1024))) char smem[XB + 2 * WB];
+  char* Xs = smem;
+  char* Wu = smem + XB;                       // u-chunk weights
+  char* Wk = smem + XB + WB;                  // skip-chunk weights
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fsub = lane >> 4, fr = lane & 15;
+  const int H = p.OH;
+  const int rows_total = p.N * H;
+  const int M = rows_total * W;
+  const int nwin = rows_total / R;
+  const int w_lo = (int)blockIdx.x * p.win_pf;
+  const int w_hi = w_lo + p.win_pf < nwin ? w_lo + p.win_pf : nwin;
+  if (w_lo >= w_hi) return;
+  constexpr int OOB = 0x7fffffff;
+
+  // ---- once: both chunks' weight images (row tap * 32 + n: the chunk's 32 input channels)
+  {
+    const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
+    const int lslot = lane >> 2;
+    const int lchunk = (lane & 3) ^ ((lslot >> 1) & 3);
+    constexpr int WI = 9 * BN / 16;
+#pragma unroll
+    for (int q = 0; q < (2 * WI + 3) / 4; ++q) {
+      const int k = wave + 4 * q;
+      if (k < 2 * WI) {
+        const int kc = k / WI, kk = k - kc * WI;
+        const int tap = kk / (BN / 16), nb = (kk % (BN / 16)) * 16;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsw, (__attribute__((address_space(3))) void*)((kc ? Wk : Wu) + kk * 1024), 16,
+            ((nb + lslot) * p.Kpad + tap * 64 + (kc << 5) + lchunk * 8) * 2, 0, 0, 0);
+      }
+    }
+  }
+  // ---- this wave's halo row: tap row th of coarse row offset cq (u = tconv weights x coarse x + b)
+  const int cq = (wave + 1) >> 1, th = (wave + 1) & 1;
+  h16x8 wa[2][2][KS];                          // [tw][j][ks]: both column phases of tap row th
+  {
+    const h16* wt = (const h16*)p.ut.w + (size_t)(8 * (fr >> 2) + (fr & 3)) * p.ut.kpad + 8 * fsub;
+#pragma unroll
+    for (int tw = 0; tw < 2; ++tw)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          wa[tw][j][ks] = *(const h16x8*)(wt + (size_t)((2 * th + tw) * 32 + 4 * j) * p.ut.kpad + 32 * ks);
+  }
+  float bs[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) bs[i] = p.ut.b[8 * fsub + i];
+  EpiConst<TN> ec;
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ec.bias[j][r] = p.bias ? p.bias[16 * j + 4 * fsub + r] : 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ec.hw[e] = 0.f;
+  ec.hb = 0.f;
+
+  h16x8 xb[PB][KS];                            // the wave's coarse row (16 px x 32 ch per fragment)
+  bool xin = false;                            // (of the window the registers hold)
+  auto load_coarse = [&](const int w) {
+    const int g0 = (p.rev ? nwin - 1 - w : w) * R;
+    const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
+    const int hr = wave;                       // halo row = fine row g0 - 1 + hr
+    xin = (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)(g0 - 1 + hr) < (unsigned)rows_total;
+    const int crow = (g0 >> 1) - 1 + cq;       // coarse row (H even: fine row g -> g / 2)
+    const h16* rp = (const h16*)p.ut.x + ((size_t)(xin ? crow : 0) * CW + fr) * Cc + 8 * fsub;
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) xb[pb][ks] = *(const h16x8*)(rp + (size_t)(16 * pb) * Cc + 32 * ks);
+  };
+  // skip halo: granule c of thread t = halo row c / 2, column (t >> 2) + 64 (c & 1), chunk t & 3
+  u32x4 sv[8];
+  const int lds_t = (1 + (tid >> 2)) * 64 + 16 * ((tid & 3) ^ (((1 + (tid >> 2)) >> 1) & 3));
+  auto load_skip = [&](const int w) {
+    const int g0 = (p.rev ? nwin - 1 - w : w) * R;
+    const int grow0 = (g0 / H) * H;
+    const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.src2 + (size_t)grow0 * W * 64), (short)0, OOB, 0x00020000);
+    const int rowoff = (g0 - 1 - grow0) * W * 64;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int hr = c >> 1;
+      const bool ok = (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)(g0 - 1 + hr) < (unsigned)rows_total;
+      sv[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? rowoff + hr * W * 64 + (c & 1) * 4096 + tid * 16 : OOB, 0, 0);
+    }
+  };
+  const int tsel = (fr >> 2) & 1;
+  auto form_u = [&]() {                        // halo row `wave` of u, zero columns included
+    char* xrow = Xs + wave * ROWB;
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) {
+      u32x4 pk[2] = {(u32x4){0u, 0u, 0u, 0u}, (u32x4){0u, 0u, 0u, 0u}};
+      if (xin) {
+#pragma unroll
+        for (int tw = 0; tw < 2; ++tw)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) a = mfma16(wa[tw][j][ks], xb[pb][ks], a);
+            pk[tw][2 * j] = pack2h(a[0] + bs[4 * j], a[1] + bs[4 * j + 1]);
+            pk[tw][2 * j + 1] = pack2h(a[2] + bs[4 * j + 2], a[3] + bs[4 * j + 3]);
+          }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int tw = s ^ tsel;
+        const int hc = 2 * (16 * pb + fr) + tw + 1;
+        *(u32x4*)(xrow + hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3))) = tw ? pk[1] : pk[0];
+      }
+    }
+    if (lane < 8) *(u32x4*)(xrow + ((lane >> 2) ? W + 1 : 0) * 64 + 16 * (lane & 3)) = (u32x4){0u, 0u, 0u, 0u};
+  };
+  auto store_skip = [&]() {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) *(u32x4*)(Xs + lds_t + (c >> 1) * ROWB + (c & 1) * 4096) = sv[c];
+    if (tid < 32) *(u32x4*)(Xs + (tid >> 3) * ROWB + ((tid >> 2) & 1) * 129 * 64 + 16 * (tid & 3)) = (u32x4){0u, 0u, 0u, 0u};
+  };
+
+  const int r0 = (wave / NCS) * RW, c0 = (wave % NCS) * 16 * TC;
+  int xbase[3];
+#pragma unroll
+  for (int dw = 0; dw < 3; ++dw) {
+    const int hc = fr + dw;
+    xbase[dw] = r0 * ROWB + c0 * 64 + hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3));
+  }
+  const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
+  f32x4 acc[TM][TN];
+  auto chunk_mfmas = [&](const char* Ws) {
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw) {
+      h16x8 wf[3][TN];
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) wf[dh][j] = *(const h16x8*)(Ws + ((3 * dh + dw) * BN + 16 * j) * 64 + wbase);
+#pragma unroll
+      for (int hr = 0; hr < RW + 2; ++hr) {
+#pragma unroll
+        for (int ci = 0; ci < TC; ++ci) {
+          const h16x8 xf = *(const h16x8*)(Xs + xbase[dw] + hr * ROWB + ci * 16 * 64);
+#pragma unroll
+          for (int dh = 0; dh < 3; ++dh) {
+            const int ri = hr - dh;
+            if (ri < 0 || ri >= RW) continue;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[ri * TC + ci][j] = mfma16(wf[dh][j], xf, acc[ri * TC + ci][j]);
+          }
+        }
+      }
+    }
+  };
+  load_coarse(w_lo);
+  load_skip(w_lo);
+  for (int w = w_lo; w < w_hi; ++w) {
+    const int tm = p.rev ? nwin - 1 - w : w;
+    const int g0 = tm * R;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    form_u();
+    if (w + 1 < w_hi) load_coarse(w + 1);          // under the u-chunk MFMAs and the rest
+    __syncthreads();                               // u halo (and, first time, the weights) in LDS
+    chunk_mfmas(Wu);
+    __syncthreads();
+    store_skip();
+    if (w + 1 < w_hi) load_skip(w + 1);            // under the skip-chunk MFMAs and the epilogue
+    __syncthreads();
+    chunk_mfmas(Wk);
+    __syncthreads();                               // fragment reads done: the epilogue stages in Xs
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI_FWD, Map, 0, W>(p, acc, smem, g0 * W, 0, M, wave, 0, lane, tid,
+                                                                      0, 0, tm, &ec);
+    __syncthreads();                               // staging reads done before the next u rows
+  }
+}
+
+hipError_t launch_win_pfu(const ConvFwdParams& p, hipStream_t s) {
+  const int grid = win_grid(p);
+  if (p.ut.C == 64)
+    UNET_LAUNCH((conv_win_pfu_kernel<2>), dim3(grid), dim3(NTHR), 0, s, p);
+  else
+    UNET_LAUNCH((conv_win_pfu_kernel<1>), dim3(grid), dim3(NTHR), 0, s, p);
+  return launch_status();
+}
+
 hipError_t launch_win_pf(const ConvFwdParams& p, hipStream_t s) {
   const int grid = win_grid(p);
   if (p.OW > 128) {
@@ -1206,6 +1425,7 @@ template <int BN, int BM>
 hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
   if constexpr (BN == 32 && BM == 512) {
     if (win_pf_eligible(p)) return launch_win_pf(p, s);
+    if (win_pfu_eligible(p)) return launch_win_pfu(p, s);
     if (win_cp128_eligible(p)) return launch_win_cp128(p, s);
   }
   if constexpr (BN == 64 && BM == 256) {
