@@ -79,7 +79,10 @@ PARITY_BOUNDS = {
     "step:batch_size=2,dims=3,img_size=32,in_channels=4": (0.02, 0.03, 0.045, 5e-4),
     "step:batch_size=4,img_size=64,in_channels=4": (0.02, 0.037, 0.1, 3e-4),
     "step:batch_size=4,img_size=64,in_channels=4,loss=dice_bce": (0.02, 0.037, 0.062, 4e-4),
-    "step:batch_size=2,img_size=64,in_channels=1,use_upsampling=True": (0.02, 0.037, 0.1, 0.0125),
+    # the 1-channel upsampling step at batch 2 sits at ATen's own bf16 noise floor: total
+    # distance native 0.0062 vs ATen bf16 autocast 0.0057 on the same step, 0.0021 / 0.0018
+    # at batch 8, native fp32 1e-12 (scripts/ups_parity_diag.py, profiles/r5_ups_parity_diag.md)
+    "step:batch_size=2,img_size=64,in_channels=1,use_upsampling=True": (0.02, 0.037, 0.1, 0.01),
 }
 
 

@@ -296,7 +296,9 @@ __global__ void __launch_bounds__(NT) norm_apply_kernel(const h16* __restrict__ 
   }
 }
 
-// dz = a g + b z + c  (coefficients [C] or [N][C])
+// dz = a g + b z + c  (coefficients [C] or [N][C]); U pixel steps of loads in flight per
+// thread, NTL: non-temporal (read-once) loads
+template <int U, bool NTL>
 __global__ void __launch_bounds__(NT) norm_bwd_apply_kernel(const h16* __restrict__ g, const h16* __restrict__ z,
                                                             int P, int C, const float* __restrict__ ca,
                                                             const float* __restrict__ cb,
@@ -317,18 +319,23 @@ __global__ void __launch_bounds__(NT) norm_bwd_apply_kernel(const h16* __restric
   }
   const int p0 = (int)((long long)blk * P / nbp), p1 = (int)((long long)(blk + 1) * P / nbp);
   const size_t base = (size_t)n * P * C + c0;
+  auto ld = [&](const h16* src, int px) {
+    const u32x4* a = (const u32x4*)(src + base + (size_t)px * C);
+    if constexpr (NTL) return __builtin_nontemporal_load(a);
+    else return *a;
+  };
   int p = p0 + rs;
-  for (; p + (kUnroll - 1) * rstep < p1; p += kUnroll * rstep) {
-    u32x4 rg[kUnroll], rz[kUnroll];
+  for (; p + (U - 1) * rstep < p1; p += U * rstep) {
+    u32x4 rg[U], rz[U];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       // streaming reads (read once): non-temporal, so they do not evict the freshly
       // written tensors the next kernels read from the last-level cache
-      rg[u] = __builtin_nontemporal_load((const u32x4*)(g + base + (size_t)(p + u * rstep) * C));
-      rz[u] = __builtin_nontemporal_load((const u32x4*)(z + base + (size_t)(p + u * rstep) * C));
+      rg[u] = ld(g, p + u * rstep);
+      rz[u] = ld(z, p + u * rstep);
     }
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       float gv[8], zv[8];
       unpack8(rg[u], gv);
       unpack8(rz[u], zv);
@@ -476,9 +483,13 @@ __device__ __forceinline__ void bn_final_channel(const int c, const float s1, co
 }
 
 // Single-launch BatchNorm statistics (forward / backward / plain column sums, modes 0 / 1
-// / 3): phase 1 as row_slices (block (sl, cb) sums rpb rows of 64 columns into slice sl),
-// then the LAST block to finish -- told by the value its agent-scope counter add returns
-// -- sums the slices of every column and finalises all channels (bn_final_channel).
+// / 3).  Block (sl, cb) owns 32 channels -- lane cl < 64 is column (cl >> 5) * C + 32 cb +
+// (cl & 31), i.e. both moments of its channels -- and sums rpb rows of them into slice sl;
+// then the LAST of the nsl blocks of column block cb to finish -- told by the value its
+// agent-scope add on counter[cb] returns -- sums the slices of those 64 columns and
+// finalises its 32 channels (bn_final_channel).  The column blocks finalise in parallel
+// (one block finalising every channel serialised C / 32 rounds of dependent slice loads:
+// ~30 us per launch at C = 128).
 // Hand-off (HIP scoped memory model, no reliance on undocumented hardware ordering):
 //   * every slice value is stored by an agent-scope atomic store (written through to the
 //     device-coherent level: the 8 XCDs have separate L2s, so a plain store could sit in
@@ -489,9 +500,8 @@ __device__ __forceinline__ void bn_final_channel(const int c, const float s1, co
 //   * the last block's lane observes the final count (its add acquires every earlier
 //     block's release), the barrier hands that to the block, and every thread executes an
 //     agent-scope ACQUIRE fence before its agent-scope atomic loads of the slices.
-// The last block resets the counter (graph replays).  Fixed summation order:
-// deterministic, no float atomics.  Replaces the row_slices + bn_final pair (72 -> 36
-// launches per BatchNorm step).
+// The last block resets its counter (graph replays).  Fixed summation order:
+// deterministic, no float atomics.  counter: ceil(C / 32) <= 64 ints.
 __global__ void __launch_bounds__(NT) bn_stats_fused_kernel(const float* __restrict__ rows, int R, int C, int rpb,
                                                             float* __restrict__ slices, int* __restrict__ counter,
                                                             float count, int mode, const float* __restrict__ gamma,
@@ -506,11 +516,14 @@ __global__ void __launch_bounds__(NT) bn_stats_fused_kernel(const float* __restr
   __shared__ int last;
   const int W = 2 * C;
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.y * 32 + (cl & 31);
+  const bool valid = c < C;
+  const int col = (cl >> 5) * C + c;
   {
-    const int col = blockIdx.y * 64 + cl, sl = blockIdx.x;
+    const int sl = blockIdx.x;
     const int r0 = sl * rpb, r1 = min(R, r0 + rpb);
     float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (col < W) {
+    if (valid) {
       int r = r0 + rl;
       for (; r + 28 < r1; r += 32)
 #pragma unroll
@@ -519,45 +532,44 @@ __global__ void __launch_bounds__(NT) bn_stats_fused_kernel(const float* __restr
     }
     red[rl][cl] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     __syncthreads();
-    if (rl == 0 && col < W)
+    if (rl == 0 && valid)
       __hip_atomic_store(slices + (size_t)sl * W + col, red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl],
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int done = __hip_atomic_fetch_add(counter, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = done == (int)(gridDim.x * gridDim.y) - 1;
+    const int done = __hip_atomic_fetch_add(counter + blockIdx.y, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = done == (int)gridDim.x - 1;
   }
   __syncthreads();
   if (!last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const int nsl = gridDim.x;
-  const int t = threadIdx.x & 63;
-  const int mom = t >> 5;
-  for (int c0 = 0; c0 < C; c0 += 32) {
-    const int c = c0 + (t & 31);
-    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (c < C) {
-      const float* sp = slices + mom * C + c;
-      int sl = rl;
-      for (; sl + 28 < nsl; sl += 32)
+  float a[16];
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          a[k] += __hip_atomic_load(sp + (size_t)(sl + 4 * k) * W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (; sl < nsl; sl += 4) a[0] += __hip_atomic_load(sp + (size_t)sl * W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();                                   // (previous channel block's red reads done)
-    red[rl][t] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-    __syncthreads();
-    if (threadIdx.x < 32 && c < C) {
-      const float s1 = red[0][t] + red[1][t] + red[2][t] + red[3][t];
-      const float s2 = red[0][t + 32] + red[1][t + 32] + red[2][t + 32] + red[3][t + 32];
-      bn_final_channel(c, s1, s2, count, mode, gamma, beta, eps, momentum, run_mean, run_var, mean, rstd, fa, fc, ca,
-                       cb, cc, dgamma, dbeta);
-    }
+  for (int k = 0; k < 16; ++k) a[k] = 0.f;
+  if (valid) {
+    const float* sp = slices + col;
+    int sl = rl;
+    for (; sl + 60 < nsl; sl += 64)
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        a[k] += __hip_atomic_load(sp + (size_t)(sl + 4 * k) * W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (; sl < nsl; sl += 4) a[0] += __hip_atomic_load(sp + (size_t)sl * W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (threadIdx.x == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();                                     // (phase-1 red reads done)
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] += a[k + 8];
+  red[rl][cl] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (threadIdx.x < 32 && valid) {
+    const float s1 = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    const float s2 = red[0][cl + 32] + red[1][cl + 32] + red[2][cl + 32] + red[3][cl + 32];
+    bn_final_channel(c, s1, s2, count, mode, gamma, beta, eps, momentum, run_mean, run_var, mean, rstd, fa, fc, ca,
+                     cb, cc, dgamma, dbeta);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(counter + blockIdx.y, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // rows per phase-1 block of bn_stats_fused: at most 128 slices for the last block to sum
@@ -680,6 +692,15 @@ int norm_blocks_per_sample(int N, int P) {
   return nbp < 1 ? 1 : nbp;
 }
 
+// grid width (blocks per sample) of the streaming passes norm_apply / norm_bwd_apply: at
+// least 16 (batch 1024: 16k blocks; one block per sample left the level-2 / 3 passes 5-8 %
+// slower, profiles/r5_norm_ew_grid.md)
+static int ew_blocks_per_sample(int N, int P) {
+  const int maxb = (P + 63) / 64;
+  const int nbp = norm_blocks_per_sample(N, P);
+  return nbp >= 16 ? nbp : (maxb < 16 ? maxb : 16);
+}
+
 const char* norm_check(int C, int G) {
   if (C % 8) return "norm: channels must be a multiple of 8";
   if (C > 2048) return "norm: at most 2048 channels";
@@ -748,12 +769,13 @@ hipError_t bn_stats_launch(const float* rows, int R, int C, float count, int mod
                        eps, momentum, run_mean, run_var, mean, rstd, fa, fc, ca, cb, cc, dgamma, dbeta);
     return launch_status();
   }
-  // one launch: slices, then the finalize by the last block; the counter lives just past
-  // the row_slices(R) * 2C slice floats of the workspace (zeroed once, reset every use)
+  // one launch: slices, then the finalize by the last block of each 32-channel column
+  // block; the ceil(C / 32) <= 64 counters live just past the row_slices(R) * 2C slice
+  // floats of the workspace (zeroed once, reset every use)
   const int rpb = fused_rows_per_block(R);
   const int nsl = (R + rpb - 1) / rpb;
   int* counter = (int*)(slices + (size_t)row_slices(R) * 2 * C);
-  UNET_LAUNCH(bn_stats_fused_kernel, dim3(nsl, (2 * C + 63) / 64), dim3(NT), 0, s, rows, R, C, rpb, slices,
+  UNET_LAUNCH(bn_stats_fused_kernel, dim3(nsl, (C + 31) / 32), dim3(NT), 0, s, rows, R, C, rpb, slices,
                      counter, count, mode, gamma, beta, eps, momentum, run_mean, run_var, mean, rstd, fa, fc, ca, cb, cc,
                      dgamma, dbeta);
   return launch_status();
@@ -774,7 +796,7 @@ hipError_t gn_stats_launch(const float* rows, int N, int rps, int C, int G, int 
     const int rpb = fused_rows_per_block(N);
     const int nsl = (N + rpb - 1) / rpb;
     int* counter = (int*)(slices + (size_t)row_slices(N) * 2 * C);
-    UNET_LAUNCH(bn_stats_fused_kernel, dim3(nsl, (2 * C + 63) / 64), dim3(NT), 0, s, (const float*)work, N, C,
+    UNET_LAUNCH(bn_stats_fused_kernel, dim3(nsl, (C + 31) / 32), dim3(NT), 0, s, (const float*)work, N, C,
                        rpb, slices, counter, 1.f, 3, gamma, beta, eps, 0.f, (float*)nullptr, (float*)nullptr,
                        (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr, (float*)nullptr,
                        (float*)nullptr, (float*)nullptr, dgamma, dbeta);
@@ -793,15 +815,17 @@ hipError_t norm_rows_launch(const void* A, const void* B, int N, int P, int C, f
 hipError_t norm_apply_launch(const void* z, int N, int P, int C, const float* mean, const float* rstd, int cstride,
                              const float* gamma, const float* beta, int relu, float drop_rate, uint32_t seed,
                              const uint32_t* seed_ptr, uint32_t salt, int n0, void* y, hipStream_t s) {
-  UNET_LAUNCH(norm_apply_kernel, dim3(norm_blocks_per_sample(N, P), N), dim3(NT), 0, s, (const h16*)z, P, C,
+  UNET_LAUNCH(norm_apply_kernel, dim3(ew_blocks_per_sample(N, P), N), dim3(NT), 0, s, (const h16*)z, P, C,
                      mean, rstd, cstride, gamma, beta, relu, drop_rate, seed, seed_ptr, salt, n0, (h16*)y);
   return launch_status();
 }
 
 hipError_t norm_bwd_apply_launch(const void* g, const void* z, int N, int P, int C, const float* ca, const float* cb,
                                  const float* cc, int cstride, void* dz, hipStream_t s) {
-  UNET_LAUNCH(norm_bwd_apply_kernel, dim3(norm_blocks_per_sample(N, P), N), dim3(NT), 0, s, (const h16*)g,
-                     (const h16*)z, P, C, ca, cb, cc, cstride, (h16*)dz);
+  // unroll 4 with non-temporal loads: unroll 8 and / or plain loads measured equal or up to
+  // 20 % slower (profiles/r5_norm_ew_grid.md)
+  UNET_LAUNCH((norm_bwd_apply_kernel<4, true>), dim3(ew_blocks_per_sample(N, P), N), dim3(NT), 0, s,
+              (const h16*)g, (const h16*)z, P, C, ca, cb, cc, cstride, (h16*)dz);
   return launch_status();
 }
 
