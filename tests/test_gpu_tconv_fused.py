@@ -231,3 +231,38 @@ def test_tconv_onload_persistent_window(cuda_dev, N, K, pf, rev):
             assert g == (N * F2 // 2 + p - 1) // p
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     assert torch.isfinite(outs[1][0].float()).all()
+
+
+@pytest.mark.parametrize("N,K,pf", [(2, 64, 8), (3, 32, 5)])
+def test_tconv_onload_persistent_window_stats(cuda_dev, N, K, pf):
+    """The normalised configs' conv9a forward on the persistent tconv-on-load window
+    (statistics epilogue: pre-norm z + one {sum z, sum z^2} row per 256-pixel window):
+    z bit-identical to the one-window XF 5 kernel, its per-512-pixel rows equal to the sums
+    of row pairs, and the column sums equal to fp64 sums of z."""
+    H = 64
+    b, skip, wt, bt, wa, _ = _problem(cuda_dev, N, H, K, 32, 32, 32, 23)
+    dev = cuda_dev
+    F2 = 2 * H
+    wtp = _pad64(wt.reshape(4 * 32, K).bfloat16())
+    wap = _pad64(wa.bfloat16().permute(3, 0, 1, 2).reshape(32, 9 * 64))
+    d0 = dict(N=N, OH=F2, OW=F2, IH=F2, IW=F2, KH=3, KW=3, pad=1, C1=32, C2=32, src1=ptr(b), src2=ptr(skip),
+              wgt=ptr(wap), bias=0, Cout=32, relu=0, ut_x=ptr(b), ut_w=ptr(wtp), ut_b=ptr(bt), ut_C=K,
+              ut_kpad=wtp.shape[1])
+    outs = []
+    for p in (0, pf):
+        z = torch.full((N, F2, F2, 32), float("nan"), device=dev, dtype=torch.bfloat16)
+        d = dict(d0, dst1=ptr(z), win_pf=p)
+        rows, px = C().conv_stat_tiles(dict(d, stats=1))
+        assert rows * px == N * F2 * F2 and px == (256 if p else 512)
+        st = torch.full((rows * 2 * 32,), float("nan"), device=dev)
+        d["stats"] = ptr(st)
+        C().conv_fwd(d, stream())
+        torch.cuda.synchronize()
+        outs.append((z, st.view(rows, 2, 32)))
+    assert torch.equal(outs[0][0], outs[1][0])
+    s_one, s_pf = outs[0][1], outs[1][1]
+    assert torch.isfinite(s_pf).all()
+    assert torch.allclose(s_pf.view(-1, 2, 2, 32).sum(1), s_one, rtol=1e-4, atol=1e-2)
+    zf = outs[1][0].double().reshape(-1, 32)
+    ref = torch.stack([zf.sum(0), (zf * zf).sum(0)])
+    assert torch.allclose(s_pf.double().sum(0), ref, rtol=1e-4, atol=1e-1)

@@ -1158,7 +1158,7 @@ void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
     case 6:
     case 12: {       // row window: R rows x (segment) width, tiles in (row group, segment) order
       const int W = p.OW > 128 ? 128 : p.OW;
-      const int R = win_rows(p);
+      const int R = win_pfu_eligible(p) ? 2 : win_rows(p);   // (the persistent tconv-on-load window: 2 rows)
       if (p.nz && p.C2) return;
       *rows = ((p.N * p.OD * p.OH + R - 1) / R) * (p.OW / W);
       *tile_px = R * W;

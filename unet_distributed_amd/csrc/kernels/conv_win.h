@@ -72,11 +72,14 @@ inline bool win_cp128_eligible(const ConvFwdParams& p) {
 }
 // Persistent prefetching tconv-on-load window (conv_win_pfu_kernel): conv9a of the 128^2 UNet --
 // 2D 128-wide rows, u (32 channels) = tconv2x2s2 of a 32 / 64-channel coarse input formed on
-// load + a 32-channel skip source, 32 output channels, bias + ReLU epilogue.
+// load + a 32-channel skip source, 32 output channels, bias + ReLU epilogue or the
+// normalised configs' statistics epilogue (pre-norm z + one {sum z, sum z^2} row per
+// 256-pixel window: conv_stat_tiles).
 inline bool win_pfu_eligible(const ConvFwdParams& p) {
   return p.win_pf > 0 && p.ut.x && p.OW == 128 && p.KD == 1 && p.OD == 1 && p.C1 == 32 && p.C2 == 32 &&
-         p.Cout == 32 && (p.ut.C == 32 || p.ut.C == 64) && p.tile != 12 && conv_epi_mode(p) == EPI_FWD &&
-         !p.pool_dst && !p.head_w && p.OH % 2 == 0;
+         p.Cout == 32 && (p.ut.C == 32 || p.ut.C == 64) && p.tile != 12 &&
+         (conv_epi_mode(p) == EPI_FWD || conv_epi_mode(p) == EPI_STATS) && !p.pool_dst && !p.head_w &&
+         p.OH % 2 == 0;
 }
 inline int win_grid(const ConvFwdParams& p) {
   const int W = p.OW > 128 ? 128 : p.OW;          // window segment width
@@ -1184,8 +1187,9 @@ hipError_t launch_win_cp128(const ConvFwdParams& p, hipStream_t s) {
 // of conv_win_pf_kernel) under the skip-chunk MFMAs and epilogue.  Same operands and
 // accumulation order as conv_win_kernel's XF 5 (u bit-identical to tconv_fwd_kernel's),
 // same epilogue: bit-identical outputs.
-template <int KS>
+template <int KS, int EPI>
 __global__ void __launch_bounds__(NTHR, 2) conv_win_pfu_kernel(const ConvFwdParams p) {
+  static_assert(EPI == EPI_FWD || EPI == EPI_STATS, "persistent tconv-on-load epilogues");
   constexpr int W = 128, R = 2, HR = R + 2, BM = 256, BN = 32, ROWB = PF_ROWB;
   constexpr int TC = 2, NCS = 4, RW = 2, TM = RW * TC, TN = 2, WMP = BM / 4;
   constexpr int CW = W / 2, PB = CW / 16, Cc = KS * 32;
@@ -1366,18 +1370,23 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pfu_kernel(const ConvFwdPara
     __syncthreads();
     chunk_mfmas(Wk);
     __syncthreads();                               // fragment reads done: the epilogue stages in Xs
-    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI_FWD, Map, 0, W>(p, acc, smem, g0 * W, 0, M, wave, 0, lane, tid,
-                                                                      0, 0, tm, &ec);
+    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(p, acc, smem, g0 * W, 0, M, wave, 0, lane, tid, 0, 0,
+                                                                  tm, &ec);
     __syncthreads();                               // staging reads done before the next u rows
   }
 }
 
 hipError_t launch_win_pfu(const ConvFwdParams& p, hipStream_t s) {
   const int grid = win_grid(p);
-  if (p.ut.C == 64)
-    UNET_LAUNCH((conv_win_pfu_kernel<2>), dim3(grid), dim3(NTHR), 0, s, p);
+  const bool st = conv_epi_mode(p) == EPI_STATS;
+  if (p.ut.C == 64 && st)
+    UNET_LAUNCH((conv_win_pfu_kernel<2, EPI_STATS>), dim3(grid), dim3(NTHR), 0, s, p);
+  else if (p.ut.C == 64)
+    UNET_LAUNCH((conv_win_pfu_kernel<2, EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p);
+  else if (st)
+    UNET_LAUNCH((conv_win_pfu_kernel<1, EPI_STATS>), dim3(grid), dim3(NTHR), 0, s, p);
   else
-    UNET_LAUNCH((conv_win_pfu_kernel<1>), dim3(grid), dim3(NTHR), 0, s, p);
+    UNET_LAUNCH((conv_win_pfu_kernel<1, EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p);
   return launch_status();
 }
 
