@@ -83,3 +83,149 @@ def test_fused_dgrad_wgrad_with_pool_route(cuda_dev):
     torch.cuda.synchronize()
     assert torch.equal(dx, ref_dx)
     assert rel_err(slab.double().sum(0).float(), _ref_wgrad(x, dy, w).reshape(9, 32, 32)) < 1e-4
+
+
+def _norm_bwd_apply(g, z, ca, cb, cc, gn):
+    """dz through the split path's own kernel (norm.hip::norm_bwd_apply)."""
+    N, H, W, Ch = g.shape
+    dz = torch.empty_like(g)
+    C().generic("norm_bwd_apply", [ptr(g), ptr(z), ptr(ca), ptr(cb), ptr(cc), ptr(dz)],
+                [N, H * W, Ch, Ch if gn else 0], [], stream())
+    return dz
+
+
+@pytest.mark.parametrize("N,nsplit,gn", [(2, 7, False), (3, 64, True), (1, 1, True), (4, 512, False)])
+def test_fused_dgrad_wgrad_norm_backward_on_load(cuda_dev, N, nsplit, gn):
+    """XF 2: the halo is dz = ca g + cb z + cc formed from g and z in LDS -- the data
+    gradient and the slab rows must equal the fused kernel fed the materialised dz
+    (norm_bwd_apply) bit for bit, and the weight gradient the fp32 reference."""
+    torch.manual_seed(N * 7 + nsplit)
+    H = W = 128
+    dev = cuda_dev
+    g = torch.randn(N, H, W, 32, device=dev).bfloat16()
+    z = torch.randn(N, H, W, 32, device=dev).bfloat16()
+    rows = N if gn else 1
+    ca = 0.5 + torch.rand(rows, 32, device=dev)
+    cb = 0.2 * torch.randn(rows, 32, device=dev)
+    cc = 0.1 * torch.randn(rows, 32, device=dev)
+    x = F.relu(torch.randn(N, H, W, 32, device=dev)).bfloat16()
+    act = F.relu(torch.randn(N, H, W, 32, device=dev)).bfloat16()
+    w = (torch.randn(3, 3, 32, 32, device=dev) * 0.1).bfloat16()
+    wp = pack_dgrad(w)
+    dz = _norm_bwd_apply(g, z, ca, cb, cc, gn)
+    outs = []
+    for xf in (False, True):
+        dx = torch.full((N, H, W, 32), 7.0, device=dev, dtype=torch.bfloat16)
+        slab = torch.full((nsplit, 9, 32, 32), float("nan"), device=dev)
+        bslab = torch.full((nsplit, 32), float("nan"), device=dev)
+        d = dict(N=N, OH=H, OW=W, IH=H, IW=W, KH=3, KW=3, pad=1, C1=32, src1=ptr(dz), wgt=ptr(wp), Cout=32,
+                 relu=0, mask1=ptr(act), dst1=ptr(dx), fw_x=ptr(x), fw_slab=ptr(slab), fw_bias_slab=ptr(bslab),
+                 fw_Cx=32, fw_nsplit=nsplit)
+        if xf:
+            d.update(src1=ptr(g), xform=2, xa=ptr(ca), xb=ptr(cb), xc=ptr(cc), xz=ptr(z), xcs=32 if gn else 0)
+        assert C().conv_fwd_grid(d) == nsplit
+        C().conv_fwd(d, stream())
+        outs.append((dx, slab, bslab))
+    torch.cuda.synchronize()
+    (dx0, s0, b0), (dx1, s1, b1) = outs
+    assert torch.equal(dx1, dx0)
+    assert torch.equal(s1, s0) and torch.equal(b1, b0)
+    ref_w = _ref_wgrad(x, dz, w).reshape(9, 32, 32)
+    assert rel_err(s1.double().sum(0).float(), ref_w) < 1e-4
+    assert rel_err(b1.double().sum(0).float(), dz.float().sum((0, 1, 2))) < 1e-4
+
+
+@pytest.mark.parametrize("N,gn,xf", [(2, False, False), (3, True, True), (2, False, True)])
+def test_fused_dgrad_wgrad_dgrad_norm_epilogue(cuda_dev, N, gn, xf):
+    """EPI_DGRAD_NORM in the fused kernel (the destination is itself a normalised
+    activation's gradient): dX equals the split row-window dgrad's (same epilogue), the
+    per-window {sum g, sum g z} rows sum to the split kernel's per-sample statistics."""
+    torch.manual_seed(31 + N)
+    H = W = 128
+    dev = cuda_dev
+    rows = N if gn else 1
+    dy = torch.randn(N, H, W, 32, device=dev).bfloat16()
+    z = torch.randn(N, H, W, 32, device=dev).bfloat16()
+    ca = 0.5 + torch.rand(rows, 32, device=dev)
+    cb = 0.2 * torch.randn(rows, 32, device=dev)
+    cc = 0.1 * torch.randn(rows, 32, device=dev)
+    x = F.relu(torch.randn(N, H, W, 32, device=dev)).bfloat16()
+    zd = torch.randn(N, H, W, 32, device=dev).bfloat16()            # pre-norm z of the destination
+    na = 0.5 + torch.rand(rows, 32, device=dev)
+    nc = 0.3 * torch.randn(rows, 32, device=dev)
+    w = (torch.randn(3, 3, 32, 32, device=dev) * 0.1).bfloat16()
+    wp = pack_dgrad(w)
+    src = _norm_bwd_apply(dy, z, ca, cb, cc, gn) if xf else dy
+    base = dict(N=N, OH=H, OW=W, IH=H, IW=W, KH=3, KW=3, pad=1, C1=32, src1=ptr(src), wgt=ptr(wp), Cout=32,
+                relu=0, nz=ptr(zd), na=ptr(na), nc=ptr(nc), ncs=32 if gn else 0, npix=H * W)
+    g0 = torch.empty(N, H, W, 32, device=dev, dtype=torch.bfloat16)
+    r0, _ = C().conv_stat_tiles(dict(base, stats=1, dst1=ptr(g0)))
+    st0 = torch.full((r0, 2, 32), float("nan"), device=dev)
+    C().conv_fwd(dict(base, dst1=ptr(g0), stats=ptr(st0)), stream())
+    slab = torch.zeros(64, 9, 32, 32, device=dev)
+    bslab = torch.zeros(64, 32, device=dev)
+    fd = dict(base, fw_x=ptr(x), fw_slab=ptr(slab), fw_bias_slab=ptr(bslab), fw_Cx=32, fw_nsplit=64)
+    if xf:
+        fd.update(src1=ptr(dy), xform=2, xa=ptr(ca), xb=ptr(cb), xc=ptr(cc), xz=ptr(z), xcs=32 if gn else 0)
+    r1, px = C().conv_stat_tiles(dict(fd, stats=1, dst1=ptr(g0)))
+    assert r1 == N * H // 2 and px == 256
+    st1 = torch.full((r1, 2, 32), float("nan"), device=dev)
+    g1 = torch.empty_like(g0)
+    C().conv_fwd(dict(fd, dst1=ptr(g1), stats=ptr(st1)), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(g1, g0)
+    per0 = st0.double().view(N, -1, 2, 32).sum(1)
+    per1 = st1.double().view(N, -1, 2, 32).sum(1)
+    assert (per1 - per0).abs().max() <= 1e-4 * per0.abs().max()
+    assert rel_err(slab.double().sum(0).float(), _ref_wgrad(x, src, w).reshape(9, 32, 32)) < 1e-4
+
+
+@pytest.mark.parametrize("N,gn,bce", [(2, False, 0.0), (3, True, 0.5)])
+def test_fused_dgrad_wgrad_normalised_head_on_load(cuda_dev, N, gn, bce):
+    """XF 3 (the normalised head input conv9b): the halo's dz = (fa z + fc > 0 ? ca w
+    dlogit : 0) + cb z + cc is formed from z, the probability and the target -- the data
+    gradient and slab rows equal the fused kernel fed head_norm_bwd's materialised dz."""
+    torch.manual_seed(77 + N)
+    H = W = 128
+    dev = cuda_dev
+    P = H * W
+    rows = N if gn else 1
+    z = torch.randn(N, H, W, 32, device=dev).bfloat16()
+    prob = torch.rand(N * P, device=dev) * 0.98 + 0.01
+    t = (torch.rand(N * P, device=dev) > 0.7).bfloat16()
+    sums = torch.tensor([(prob * t.float()).sum().item(), t.float().sum().item(), prob.sum().item(), 0.0],
+                        device=dev)
+    hw = 0.3 * torch.randn(32, device=dev)
+    fa, fc = 0.5 + torch.rand(rows, 32, device=dev), 0.2 * torch.randn(rows, 32, device=dev)
+    ca, cb = 0.5 + torch.rand(rows, 32, device=dev), 0.2 * torch.randn(rows, 32, device=dev)
+    cc = 0.1 * torch.randn(rows, 32, device=dev)
+    gsc = torch.full((1,), 4.0, device=dev)
+    x = F.relu(torch.randn(N, H, W, 32, device=dev)).bfloat16()
+    zd = torch.randn(N, H, W, 32, device=dev).bfloat16()            # the destination's pre-norm z
+    na, nc = 0.5 + torch.rand(rows, 32, device=dev), 0.3 * torch.randn(rows, 32, device=dev)
+    w = (torch.randn(3, 3, 32, 32, device=dev) * 0.1).bfloat16()
+    wp = pack_dgrad(w)
+    dz = torch.empty_like(z)
+    C().generic("head_norm_bwd", [ptr(z), ptr(prob), ptr(t), ptr(sums), ptr(hw), ptr(fa), ptr(fc), ptr(ca), ptr(cb),
+                                  ptr(cc), ptr(dz), ptr(gsc)], [N, P, 32, 32 if gn else 0], [1.0 / (N * P), bce, 1.0],
+                stream())
+    outs = []
+    for xf in (False, True):
+        dx = torch.full((N, H, W, 32), 7.0, device=dev, dtype=torch.bfloat16)
+        slab = torch.full((32, 9, 32, 32), float("nan"), device=dev)
+        bslab = torch.full((32, 32), float("nan"), device=dev)
+        st = torch.full((N * H // 2, 2, 32), float("nan"), device=dev)
+        d = dict(N=N, OH=H, OW=W, IH=H, IW=W, KH=3, KW=3, pad=1, C1=32, src1=ptr(dz), wgt=ptr(wp), Cout=32,
+                 relu=0, nz=ptr(zd), na=ptr(na), nc=ptr(nc), ncs=32 if gn else 0, npix=P, stats=ptr(st),
+                 dst1=ptr(dx), fw_x=ptr(x), fw_slab=ptr(slab), fw_bias_slab=ptr(bslab), fw_Cx=32, fw_nsplit=32)
+        if xf:
+            d.update(src1=ptr(z), xform=2, xa=ptr(ca), xb=ptr(cb), xc=ptr(cc), xz=ptr(z), xcs=32 if gn else 0,
+                     hg_prob=ptr(prob), hg_t=ptr(t), hg_sums=ptr(sums), hg_w=ptr(hw), hg_gscale=ptr(gsc),
+                     hg_inv_total=1.0 / (N * P), hg_bce_w=bce, hg_fa=ptr(fa), hg_fc=ptr(fc))
+        assert C().conv_fwd_grid(d) == 32
+        C().conv_fwd(d, stream())
+        outs.append((dx, slab, bslab, st))
+    torch.cuda.synchronize()
+    (dx0, s0, b0, t0), (dx1, s1, b1, t1) = outs
+    assert torch.equal(dx1, dx0) and torch.equal(t1, t0)
+    assert torch.equal(s1, s0) and torch.equal(b1, b0)

@@ -535,3 +535,31 @@ def test_fused_dgrad_wgrad_step(cuda_dev, monkeypatch, kw):
 def rel_err_(a, b):
     a, b = a.double(), b.double()
     return ((a - b).abs().max() / (b.abs().max() + 1e-30)).item()
+
+
+@pytest.mark.parametrize("norm,dtype", [("batch", "bf16"), ("group", "fp16")])
+def test_fused_dgrad_wgrad_norm_step(cuda_dev, monkeypatch, norm, dtype):
+    """Normalised configs at 128^2: dw_fuse=1 runs conv1b / conv9b's data + weight gradients
+    in one kernel with their norm backward's dz formed on load (conv_dw XF 2 / XF 3: no
+    norm_bwd_apply / head_norm_bwd pass) vs dw_fuse=0 (split kernels, materialised dz).
+    The forward is bit-identical; the backward differs only by the statistics rows'
+    summation order (per 256-pixel window instead of per split-kernel tile)."""
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("UNET_ENGINE", "dw_fuse=" + v)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, batch_size=4, img_size=128, in_channels=4, norm=norm,
+                                                 groups=8, dtype=dtype)
+        e = nb.engine
+        assert sorted(e.fusions.get("dz_onload", [])) == (["conv1b", "conv9b"] if v == "1" else []), e.fusions
+        names = e.plan.names()
+        assert ("norm_bwd:conv1b" in names) == (v == "0") and ("norm_bwd:conv9b" in names) == (v == "0")
+        nb.fwd_bwd(x, y, seed=41)
+        torch.cuda.synchronize()
+        outs.append((nb.sums().cpu(), e.prob.clone(), {k: fn.view(fn.grad, k).clone() for k, *_ in fn.entries}))
+    (s0, p0, g0), (s1, p1, g1) = outs
+    assert torch.equal(s0, s1) and torch.equal(p0, p1)
+    for k in g0:
+        if norm == "batch" and k.endswith("/bias") and not k.startswith("Mask"):
+            continue       # (a conv bias before BatchNorm: analytically zero gradient, rounding noise)
+        if g0[k].norm() > 1e-6:
+            assert _cos(g1[k], g0[k]) > 0.999, (k, _cos(g1[k], g0[k]))

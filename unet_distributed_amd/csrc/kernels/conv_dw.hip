@@ -16,9 +16,9 @@
 //
 // Shape: 2D, W = 128, R = 2 rows per window (256 pixels), C1 = Cx = Cout = 32.  LDS:
 // weights 18 KB (staged once per workgroup), dY halo 36 KB (4 rows x 144 slots), x 16 KB:
-// 70 KB, two workgroups per CU.  Registers: the 9 x 32 x 32 dW partial is 144 per lane,
-// the data-gradient tile 32; the weight-gradient MFMAs run before the data-gradient ones
-// so their operands are never live together.
+// 70 KB, two workgroups per CU.  Registers: a wave's 9 x 32 x 16 dW partial is 72 per
+// lane, the data-gradient tile 32; the weight-gradient MFMAs run before the data-gradient
+// ones so their operands are never live together.
 //
 // One LDS image, two read patterns: the data gradient reads 16 consecutive pixels x one
 // 16-byte chunk per lane group (b128), the weight gradient 8 pixels x 4 channels per lane
@@ -27,10 +27,23 @@
 // k -> pixel order of an MFMA K step is free: with each half-wave reading 8 CONSECUTIVE
 // pixels (k = 8 G + 4 hh + q -> pixel 16 (G >> 1) + 8 hh + 4 (G & 1) + q), conv_win's
 // swizzle chunk ^ ((col >> 1) & 3) is conflict-free for both at every column shift.
+//
+// Normalised convs (BatchNorm / GroupNorm, round 6): the conv's pre-activation gradient is
+// dz = ca g + cb z + cc per channel (norm.hip::norm_bwd_apply_kernel), g the masked
+// gradient of the normalised output, z the pre-norm output.  XF 2 forms dz IN the halo
+// image -- each thread loads the g and z granules of its slots into registers and writes
+// fmaf(ca, g, fmaf(cb, z, cc)) rounded to 16 bits (the same values norm_bwd_apply would
+// have stored), zeros outside the image -- so the dz tensor is never written or read.
+// With p.hg.prob set as well (the head input conv9b), g itself is formed per pixel from
+// the probability, the target and the ReLU mask [fa z + fc > 0] (head.hip
+// head_norm_bwd_kernel's formula): neither g nor dz exists in memory.  The data gradient's
+// destination is itself a normalised activation's gradient (EPI_DGRAD_NORM: mask from its
+// pre-norm z, one {sum g, sum g z} statistics row per window).
 #include "common.h"
 #include "conv_params.h"
 #include "conv_epilogue.h"
 #include "conv_win.h"
+#include "head_grad.h"
 
 namespace unet {
 namespace {
@@ -44,12 +57,20 @@ constexpr int DW_XI = DW_HR * DW_PPR;                 // dY halo pieces (1 KB ea
 constexpr int DW_WI = 9 * DW_BN / 16;                 // weight pieces
 constexpr int DW_AI = DW_BM / 16;                     // x image pieces
 constexpr int DW_WB = DW_WI * 1024, DW_XB = DW_XI * 1024, DW_AB = DW_AI * 1024;
-constexpr int DW_LDS = DW_WB + DW_XB + DW_AB;
+constexpr int DW_KB = 6 * 32 * 4;                     // XF 2 / 3 coefficients
+constexpr int DW_LDS = DW_WB + DW_XB + DW_AB + DW_KB;
 static_assert(epi_lds_bytes<DW_BM, DW_BN>() <= DW_XB, "epilogue staging aliases the dY halo image");
 static_assert(4 * 64 * 16 * 4 <= DW_LDS, "slab reduction scratch");
+// XF 2: granule k = tid + 256 j of the HR x 144-slot x 4-chunk halo (slots 130..143 are
+// padding, stored as zeros) -> LDS byte 16 k with the chunk swizzled; a thread's chunk is
+// tid & 3 for every j, so it holds one 8-channel set of coefficients
+constexpr int DW_HG = DW_HR * DW_HWP * 4;
+constexpr int DW_HJ = DW_HG / DW_NTHR;
+static_assert(DW_HG == DW_HJ * DW_NTHR, "whole granule passes");
 
-template <int EPI>
+template <int EPI, int XF>
 __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams p) {
+  static_assert(XF == 0 || XF == 2 || XF == 3, "plain dY, norm backward on load (of the normalised head)");
   constexpr int W = DW_W, R = DW_R, HR = DW_HR, ROWB = DW_ROWB, BN = DW_BN;
   constexpr int TM = 4, TN = 2, TC = 2, RW = 2, NCS = 4;   // data-gradient strip: 2 rows x 32 columns per wave
   __shared__ __attribute__((aligned(1024))) char smem[DW_LDS];
@@ -71,7 +92,7 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
   const int lslot = lane >> 2;
   const int lchunk = (lane & 3) ^ ((lslot >> 1) & 3);
   const int fsub = lane >> 4, fr = lane & 15;
-  const int c0 = wave * 32;           // this wave's column strip (both gradients)
+  const int c0 = wave * 32;           // this wave's data-gradient column strip
   static_assert(DW_HR == 4 && DW_AI % 4 == 0, "one halo row per wave");
   // lane part of the DMA offsets: slot lslot of a 16-slot piece = column lslot - 1 of the
   // halo row (x image: column lslot), physical chunk lane & 3 = logical chunk lchunk
@@ -106,21 +127,26 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
 
   // weight-gradient transposed-read lane roles: lane (G, q, pp) supplies pixel
   // kp(hh) = 16 (G >> 1) + 8 hh + 4 (G & 1) + q of the 32-pixel step and channels
-  // 4 pp .. 4 pp + 3 of a 16-channel block
+  // 4 pp .. 4 pp + 3 of a 16-channel block.  Wave w owns the dY channel block jw = w & 1
+  // of column strips 2 (w >> 1) and 2 (w >> 1) + 1: its dW partial is 9 x 32 x 16 (72
+  // registers; a whole 9 x 32 x 32 partial per wave left no room for the XF 2 halo
+  // staging), at the price of reading each strip's x fragments twice (8 of 56 reads).
   const int G = lane >> 4, tq = (lane >> 2) & 3, pp = lane & 3;
+  const int jw = wave & 1, sw0 = (wave >> 1) * 2;
   auto saddr = [](const int slot, const int col, const int ch) -> int {
     return slot * 64 + (((ch >> 3) ^ ((col >> 1) & 3)) << 4) + ((ch & 7) << 1);
   };
-  // One base register per image and shift: the second read of a pair (hh = 1) is 8
-  // pixels on, +512 bytes with the same swizzle ((col + 8) >> 1 & 3 == col >> 1 & 3); the
-  // second 16-channel block flips chunk bit 1, i.e. the address's bit 5 (XOR 32).
+  // One base register per image and shift (strip 0; strip s is s * 2048 bytes on, the
+  // same swizzle): the second read of a pair (hh = 1) is 8 pixels on, +512 bytes with the
+  // same swizzle ((col + 8) >> 1 & 3 == col >> 1 & 3); the second 16-channel block flips
+  // chunk bit 1, i.e. the address's bit 5 (XOR 32).
   const int kp0 = 16 * (G >> 1) + 4 * (G & 1) + tq;
-  const int abase = saddr(c0 + kp0, c0 + kp0, 4 * pp);            // x image (+ y * W * 64)
+  const int abase = saddr(kp0, kp0, 4 * pp);                      // x image (+ y * W * 64)
   int dbase[3];                                                    // dY halo (+ hr * ROWB)
 #pragma unroll
   for (int dw = 0; dw < 3; ++dw) {
-    const int hc = c0 + kp0 + 2 - dw;                              // dW tap (dh, dw): halo column col + 2 - dw
-    dbase[dw] = saddr(hc, hc, 4 * pp);
+    const int hc = kp0 + 2 - dw;                                   // dW tap (dh, dw): halo column col + 2 - dw
+    dbase[dw] = saddr(hc, hc, 4 * pp) ^ (32 * jw);
   }
   auto tr8 = [&](const char* b0, const char* b1) -> h16x8 {
     const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, b0));
@@ -130,16 +156,19 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
     return __builtin_bit_cast(h16x8, v);
   };
 
-  f32x4 wacc[9][2][2];
+  f32x4 wacc[9][2];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) wacc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  f32x4 bacc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+    for (int i = 0; i < 2; ++i) wacc[t][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 bacc = (f32x4){0.f, 0.f, 0.f, 0.f};
   const u32x4 ones_u = {kOnes2, kOnes2, kOnes2, kOnes2};
   const h16x8 ones = __builtin_bit_cast(h16x8, ones_u);
+  // XF 2: the window sample's backward coefficients ca / cb / cc [3][32] in LDS (written
+  // per window by threads 0..95, read by each thread for its 8 channels in the halo pass:
+  // registers only while the halo is formed)
+  float* Ks = (float*)(As + DW_AB);
+  const int kch = (tid & 3) * 8;
 
   for (int win = w_begin; win < w_end; ++win) {
     const int g0 = win * R;
@@ -150,10 +179,60 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
         (void*)((const char*)p.src1 + img_px * C * 2), (short)0, OOB, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((const char*)p.fw.x + (size_t)g0 * W * Cx * 2), (short)0, OOB, 0x00020000);
+    // XF 2: the z granules of the halo (and the coefficients) are loaded into registers
+    // before the barrier, so they fly while the previous window's epilogue stores drain; g
+    // arrives through the dY halo DMA below and is turned into dz in place.  XF 3: the
+    // DMA brings z (src1 = z), g = w dlogit [fa z + fc > 0] per pixel with dlogit from the
+    // probability and target loaded here
+    u32x4 zv[XF == 2 ? DW_HJ : 1];
+    float dl[XF == 3 ? DW_HJ : 1];
+    uint32_t okm = 0;
+    if constexpr (XF >= 2) {
+      // Ks: ca cb cc [fa fc ca*w] of the window's sample
+      float kv = 0.f;
+      constexpr int NK = XF == 3 ? 192 : 96;
+      if (tid < NK) {
+        const int m = tid >> 5, c = tid & 31;
+        const float* src = m == 0 ? p.xa : m == 1 ? p.xb : m == 2 ? p.xc : m == 3 ? p.hg.fa : m == 4 ? p.hg.fc : p.xa;
+        const size_t ci = (size_t)(g0 / H) * p.xcs + c;
+        kv = src[ci];
+        if (XF == 3 && m == 5) kv *= p.hg.w[c];
+      }
+      const __amdgpu_buffer_rsrc_t rsz = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)((const char*)p.xz + img_px * C * 2), (short)0, OOB, 0x00020000);
+      float pr[XF == 3 ? DW_HJ : 1], tv[XF == 3 ? DW_HJ : 1];
+#pragma unroll
+      for (int j = 0; j < DW_HJ; ++j) {
+        const int k = tid + DW_NTHR * j;
+        const int hr = k / (DW_HWP * 4), s = (k >> 2) - hr * DW_HWP;
+        const int gr = g0 - 1 + hr, col = s - 1;
+        const bool ok = (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)gr < (unsigned)rows_total &&
+                        (unsigned)col < (unsigned)W;
+        okm |= (ok ? 1u : 0u) << j;
+        if constexpr (XF == 3) {
+          const int pix = ok ? gr * W + col : 0;
+          pr[j] = p.hg.prob[pix];
+          tv[j] = bits2f(((const uint16_t*)p.hg.t)[pix]);
+        }
+        if constexpr (XF == 2)
+          zv[j] = __builtin_amdgcn_raw_buffer_load_b128(rsz, ok ? ((gr - grow0) * W + col) * C * 2 + kch * 2 : OOB,
+                                                        0, 0);
+      }
+      if constexpr (XF == 3) {
+        // the batch scalars of the logit gradient (head.hip hn_scalars)
+        const float gs = p.hg.gscale ? *p.hg.gscale : 1.f;
+        const float al = -2.f * gs / (2.f * p.hg.sums[0] + 1.f);
+        const float be = gs / (p.hg.sums[1] + p.hg.sums[2] + 1.f);
+        const float ga = gs * p.hg.bce_w * p.hg.inv_total;
+#pragma unroll
+        for (int j = 0; j < DW_HJ; ++j) dl[j] = hn_dlogit(pr[j], tv[j], al, be, ga);
+      }
+      if (tid < NK) Ks[tid] = kv;    // (the previous window read them before its MFMAs)
+    }
     __syncthreads();      // the previous window's epilogue is done with the staging tile
-    // dY halo image: wave w fills halo row hr = w (pixel row g0 - 1 + w), slot hc =
-    // column hc - 1, as 9 pieces of 16 slots; rows of another image and columns outside
-    // [0, W) load zeros (out-of-range offsets).  Per piece only an immediate changes.
+    // dY (XF 2: g, XF 3: z) halo image: wave w fills halo row hr = w (pixel row g0 - 1 + w), slot
+    // hc = column hc - 1, as 9 pieces of 16 slots; rows of another image and columns
+    // outside [0, W) load zeros (out-of-range offsets).  Per piece only an immediate changes.
     {
       const int gr = g0 - 1 + wave;
       const bool row_ok = (wave > 0 || top_in) && (wave < R + 1 || bot_in) && (unsigned)gr < (unsigned)rows_total;
@@ -173,39 +252,74 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsx, (__attribute__((address_space(3))) void*)(As + (4 * wave + i) * 1024),
                                                16, xdma_lane + (4 * wave + i) * 1024, 0, 0, 0);
     __syncthreads();
+    if constexpr (XF >= 2) {
+      // dz = fmaf(ca, g, fmaf(cb, z, cc)) in place (16-byte granule k of the halo: LDS
+      // slot k >> 2, logical chunk tid & 3), zeros outside the image.  XF 3: dz =
+      // (fa z + fc > 0 ? ca w dlogit : 0) + fmaf(cb, z, cc) (head.hip head_norm_bwd_kernel)
+      float ka[8], kb[8], kc[8], kf[8], kg[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ka[e] = Ks[(XF == 3 ? 160 : 0) + kch + e];
+        kb[e] = Ks[32 + kch + e];
+        kc[e] = Ks[64 + kch + e];
+        if constexpr (XF == 3) {
+          kf[e] = Ks[96 + kch + e];
+          kg[e] = Ks[128 + kch + e];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < DW_HJ; ++j) {
+        const int k = tid + DW_NTHR * j;
+        const int s = (k >> 2) % DW_HWP;
+        u32x4* slot = (u32x4*)(Xs + (k >> 2) * 64 + 16 * ((tid & 3) ^ ((s >> 1) & 3)));
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if ((okm >> j) & 1u) {
+          float gf[8], zf[8];
+          if constexpr (XF == 3) {
+            unpack8(*slot, zf);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float g = fmaf(kf[e], zf[e], kg[e]) > 0.f ? ka[e] * dl[j] : 0.f;
+              gf[e] = g + fmaf(kb[e], zf[e], kc[e]);
+            }
+          } else {
+            unpack8(zv[j], zf);
+            unpack8(*slot, gf);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) gf[e] = fmaf(ka[e], gf[e], fmaf(kb[e], zf[e], kc[e]));
+          }
+          v = pack8(gf);
+        }
+        *slot = v;
+      }
+      __syncthreads();
+    }
 
     // ---- weight gradient: halo row hr at shift dw feeds x rows y = hr - 2 + dh
-    {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int so = (sw0 + st) * 32 * 64;
       h16x8 xa[R][2];
 #pragma unroll
       for (int y = 0; y < R; ++y)
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const int a = (abase ^ (32 * i)) + y * W * 64;
+          const int a = (abase ^ (32 * i)) + y * W * 64 + so;
           xa[y][i] = tr8(As + a, As + a + 512);
         }
 #pragma unroll
       for (int hr = 0; hr < HR; ++hr) {
 #pragma unroll
         for (int dw = 0; dw < 3; ++dw) {
-          h16x8 yb[2];
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int a = (dbase[dw] ^ (32 * j)) + hr * ROWB;
-            yb[j] = tr8(Xs + a, Xs + a + 512);
-          }
-          if (dw == 1 && hr >= 1 && hr <= R) {        // the window's own dY pixels: bias sums
-#pragma unroll
-            for (int j = 0; j < 2; ++j) bacc[j] = mfma16(ones, yb[j], bacc[j]);
-          }
+          const int a = dbase[dw] + hr * ROWB + so;
+          const h16x8 yb = tr8(Xs + a, Xs + a + 512);
+          if (dw == 1 && hr >= 1 && hr <= R) bacc = mfma16(ones, yb, bacc);   // the window's own dY: bias sums
 #pragma unroll
           for (int dh = 0; dh < 3; ++dh) {
             const int y = hr - 2 + dh;
             if (y < 0 || y >= R) continue;
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-              for (int j = 0; j < 2; ++j) wacc[3 * dh + dw][i][j] = mfma16(xa[y][i], yb[j], wacc[3 * dh + dw][i][j]);
+            for (int i = 0; i < 2; ++i) wacc[3 * dh + dw][i] = mfma16(xa[y][i], yb, wacc[3 * dh + dw][i]);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -246,41 +360,35 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
                                                                             tid, 0, 0, win);
   }
 
-  // ---- sum the four waves' partials (different column strips) and write the slab row
+  // ---- sum the partials of the two waves of each dY channel block (waves jw, jw + 2:
+  // different column strips) and write the slab row
   float* red = (float*)smem;
   const int row = p.fw.split_lo + split;
   const int n_base = lane & 15, m_base = 4 * (lane >> 4);
-  auto reduce_store = [&](const f32x4 (&v4)[2][2], const int t) {
+  auto reduce_store = [&](const f32x4 (&v4)[2], const int t) {
     __syncthreads();
-    if (wave > 0) {     // red[fragment][wave * 64 + lane]: lanes 16 bytes apart, conflict-free
+    if (wave >= 2) {    // red[fragment][wave * 64 + lane]: lanes 16 bytes apart, conflict-free
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) *(f32x4*)(red + ((i * 2 + j) * 256 + wave * 64 + lane) * 4) = v4[i][j];
+      for (int i = 0; i < 2; ++i) *(f32x4*)(red + ((i * 2 + jw) * 64 + lane) * 4) = v4[i];
     }
     __syncthreads();
-    if (wave == 0) {
+    if (wave < 2) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i) {
+        const f32x4 v = v4[i] + *(const f32x4*)(red + ((i * 2 + jw) * 64 + lane) * 4);
+        if (t < 9) {
+          float* dst = p.fw.slab + (((size_t)row * 9 + t) * Cx + m_base + 16 * i) * C + n_base + 16 * jw;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          f32x4 v = v4[i][j];
-#pragma unroll
-          for (int o = 1; o < 4; ++o) v += *(const f32x4*)(red + ((i * 2 + j) * 256 + o * 64 + lane) * 4);
-          if (t < 9) {
-            float* dst = p.fw.slab + (((size_t)row * 9 + t) * Cx + m_base + 16 * i) * C + n_base + 16 * j;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dst[(size_t)r * C] = v[r];
-          } else if (i == 0 && lane < 16) {
-            p.fw.bias_slab[(size_t)row * C + n_base + 16 * j] = v[0];
-          }
+          for (int r = 0; r < 4; ++r) dst[(size_t)r * C] = v[r];
+        } else if (i == 0 && lane < 16) {
+          p.fw.bias_slab[(size_t)row * C + n_base + 16 * jw] = v[0];
         }
+      }
     }
   };
 #pragma unroll
   for (int t = 0; t < 9; ++t) reduce_store(wacc[t], t);
-  const f32x4 z = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const f32x4 bv[2][2] = {{bacc[0], bacc[1]}, {z, z}};
+  const f32x4 bv[2] = {bacc, (f32x4){0.f, 0.f, 0.f, 0.f}};
   reduce_store(bv, 9);
 }
 
@@ -292,9 +400,15 @@ const char* conv_dw_check(const ConvFwdParams& p) {
   const int ep = conv_epi_mode(p);
   if (p.OW != DW_W || p.IW != DW_W || p.OH != p.IH || p.OH % DW_R || p.KD != 1 || p.OD != 1 || p.ID != 1 ||
       p.KH != 3 || p.KW != 3 || p.stride != 1 || p.pad != 1 || p.C1 != 32 || p.C2 || p.Cout != DW_BN ||
-      p.D1 != p.Cout || p.fw.Cx != 32 || ep != EPI_DGRAD || p.xform || p.hg.prob || p.s2d || p.ut.x ||
-      p.pool_dst || p.head_w || p.rev)
+      p.D1 != p.Cout || p.fw.Cx != 32 || (ep != EPI_DGRAD && ep != EPI_DGRAD_NORM) || p.s2d ||
+      p.ut.x || p.pool_dst || p.head_w || p.rev)
     return "conv_fwd: fused weight gradient needs a 2D 32 -> 32 channel data gradient on 128-wide rows";
+  if (p.xform && (p.xform != 2 || !p.xa || !p.xb || !p.xc || !p.xz || (p.xcs != 0 && p.xcs != p.C1) || p.xout))
+    return "conv_fwd: fused weight gradient: norm backward on load (xform 2) needs xa / xb / xc / xz, xcs 0 or C";
+  if (p.hg.prob && (p.xform != 2 || p.hg.bits || !p.hg.fa || !p.hg.fc || !p.hg.t || !p.hg.sums || !p.hg.w ||
+                    p.route_gy))
+    return "conv_fwd: fused weight gradient: the normalised head's gradient on load needs xform 2, "
+           "fa / fc (no bits), t, sums, w";
   if (!p.fw.slab || !p.fw.bias_slab || p.fw.nsplit < 1 || p.fw.split_lo < 0)
     return "conv_fwd: fused weight gradient needs slab / bias_slab and nsplit >= 1";
   if ((long long)p.OH * p.OW * 32 * 2 >= (1LL << 31) - 64) return "conv_fwd: one image exceeds 2 GiB";
@@ -303,9 +417,24 @@ const char* conv_dw_check(const ConvFwdParams& p) {
 
 int conv_dw_grid(const ConvFwdParams& p) { return p.fw.nsplit; }
 
+// statistics rows of the EPI_DGRAD_NORM epilogue: one per 2-row window (256 pixels)
+int conv_dw_stat_rows(const ConvFwdParams& p) { return p.N * p.OH / DW_R; }
+
 hipError_t launch_conv_dw(const ConvFwdParams& p, hipStream_t s) {
-  if (conv_epi_mode(p) != EPI_DGRAD) return hipErrorInvalidValue;
-  UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD>), dim3(p.fw.nsplit), dim3(DW_NTHR), 0, s, p);
+  const int ep = conv_epi_mode(p);
+  const dim3 grid(p.fw.nsplit), blk(DW_NTHR);
+  if (ep == EPI_DGRAD && !p.xform)
+    UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD, 0>), grid, blk, 0, s, p);
+  else if (ep == EPI_DGRAD && p.xform == 2 && !p.hg.prob)
+    UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD, 2>), grid, blk, 0, s, p);
+  else if (ep == EPI_DGRAD_NORM && !p.xform)
+    UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD_NORM, 0>), grid, blk, 0, s, p);
+  else if (ep == EPI_DGRAD_NORM && p.xform == 2 && !p.hg.prob)
+    UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD_NORM, 2>), grid, blk, 0, s, p);
+  else if (ep == EPI_DGRAD_NORM && p.xform == 2)
+    UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD_NORM, 3>), grid, blk, 0, s, p);
+  else
+    return hipErrorInvalidValue;
   return launch_status();
 }
 

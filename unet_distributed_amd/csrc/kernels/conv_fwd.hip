@@ -1030,13 +1030,13 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     return "conv_fwd: relu_bits needs an unsplit ReLU forward";
   if ((p.mask_bits & ~3) || ((p.mask_bits & 1) && !p.mask1) || ((p.mask_bits & 2) && !p.mask2))
     return "conv_fwd: mask_bits marks a missing mask";
-  if (p.xform) {
+  if (p.xform && !p.fw.x) {          // (the fused weight gradient's xform 2: conv_dw_check)
     const int ep = conv_epi_mode(p), t = conv_fwd_pick(p);
     if (p.xform != 1 || p.C2 || !p.xa || !p.xb || p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) ||
         (t != 6 && t != 12) || (p.xcs != 0 && p.xcs != p.C1) || p.head_w || (ep != EPI_STATS && ep != EPI_GENERIC))
       return "conv_fwd: operand transform needs a 2D single-source row-window forward of a normalised input";
   }
-  if (p.hg.prob && (!p.hg.t || !p.hg.sums || !p.hg.w || !p.hg.bits || p.C1 != 32 || p.C2 || p.xform ||
+  if (p.hg.prob && !p.fw.x && (!p.hg.t || !p.hg.sums || !p.hg.w || !p.hg.bits || p.C1 != 32 || p.C2 || p.xform ||
                     p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) || conv_epi_mode(p) != EPI_DGRAD ||
                     p.route_gy || !win_tile(conv_fwd_pick(p))))
     return "conv_fwd: head-on-load needs a 2D 32-channel row-window data gradient";
@@ -1178,8 +1178,12 @@ void conv_stat_tiles(const ConvFwdParams& p, int* rows, int* tile_px) {
       *tile_px = 256;
       return;
     }
+    case 14:                 // fused data + weight gradient: one row per 256-pixel window
+      if (!p.nz) return;
+      *rows = conv_dw_stat_rows(p);
+      *tile_px = 256;
+      return;
     case 10:
-    case 14:
       return;
     case 13:               // 8x8 image window: 4 whole images per tile
       *rows = (p.N + IMG8 - 1) / IMG8;

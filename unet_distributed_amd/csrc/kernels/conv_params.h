@@ -27,6 +27,10 @@ struct HeadGrad {
   const uint8_t* bits;        // [P][C / 8] ReLU bits of the head input
   const float* gscale;        // device loss scale (nullptr: 1)
   float inv_total, bce_w;     // 1 / (pixels of the batch), BCE weight (0: Dice only)
+  // normalised head input (conv_dw.hip, xform 2 + prob, bits == nullptr): the ReLU mask is
+  // [fa z + fc > 0] of the pre-norm z (p.xz) instead of bits; [C] or [N][C] (p.xcs)
+  const float* fa;
+  const float* fc;
 };
 
 // Transposed-conv source on load (2D row-window forward of a decoder conv whose first

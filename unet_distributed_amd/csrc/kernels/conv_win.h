@@ -102,6 +102,7 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s);
 // fused data + weight gradient window (conv_dw.hip, tile 14; conv_params.h FusedWgrad)
 const char* conv_dw_check(const ConvFwdParams& p);
 int conv_dw_grid(const ConvFwdParams& p);
+int conv_dw_stat_rows(const ConvFwdParams& p);
 hipError_t launch_conv_dw(const ConvFwdParams& p, hipStream_t s);
 
 #ifdef UNET_WIN_IMPL

@@ -605,9 +605,7 @@ __global__ void __launch_bounds__(256) head_norm_bwd_kernel(
     const size_t q = sb + p;
     float zf[8];
     unpack8(*(const u32x4*)(z + q * C + c0), zf);
-    const float pr = prob[q], tv = (float)t[q];
-    const float vv = pr * (1.f - pr);
-    const float dl = al * tv * vv + be * vv + ga * (pr - tv);
+    const float dl = hn_dlogit(prob[q], (float)t[q], al, be, ga);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float g = fmaf(A[e], zf[e], B[e]) > 0.f ? aw[e] * dl : 0.f;

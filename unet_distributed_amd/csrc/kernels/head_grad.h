@@ -20,6 +20,14 @@ __device__ __forceinline__ float head_dlogit(float pr, float tv, float a, float 
   return __builtin_fmaf(bce_w * (pr - tv), inv_total, dice) * gscale;
 }
 
+// Normalised head input (head.hip norm_head_loss / head_norm_bwd): the logit gradient as
+// al u + be v + ga w with u = t p (1 - p), v = p (1 - p), w = p - t and the batch scalars of
+// hn_scalars -- explicit fused multiply-adds, so every kernel inlining it rounds alike
+__device__ __forceinline__ float hn_dlogit(float pr, float tv, float al, float be, float ga) {
+  const float vv = pr * (1.f - pr);
+  return __builtin_fmaf(al * tv, vv, __builtin_fmaf(be, vv, ga * (pr - tv)));
+}
+
 // Per-launch constants (wave-uniform: scalar registers).  The head weights are loaded
 // here, unconditionally: a load under the per-element ReLU-bit select compiles to a
 // branch + scalar load + wait per element (a 128-deep serialised chain per window).

@@ -70,6 +70,8 @@ HeadGrad head_grad(const py::dict& d) {
   h.gscale = (const float*)getp(d, "hg_gscale");
   h.inv_total = get<float>(d, "hg_inv_total", 0.f);
   h.bce_w = get<float>(d, "hg_bce_w", 0.f);
+  h.fa = (const float*)getp(d, "hg_fa");
+  h.fc = (const float*)getp(d, "hg_fc");
   return h;
 }
 

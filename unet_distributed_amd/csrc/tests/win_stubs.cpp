@@ -20,5 +20,6 @@ const char* conv_dw_check(const ConvFwdParams& p) {
   return p.fw.x ? "host-check build: no fused weight-gradient kernel" : nullptr;
 }
 int conv_dw_grid(const ConvFwdParams& p) { return p.fw.nsplit; }
+int conv_dw_stat_rows(const ConvFwdParams& p) { return p.N * p.OH / 2; }
 hipError_t launch_conv_dw(const ConvFwdParams&, hipStream_t) { return hipErrorNotSupported; }
 }  // namespace unet

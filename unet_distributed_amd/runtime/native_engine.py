@@ -134,8 +134,11 @@ FUSIONS: Dict[str, Fusion] = {
     "tail_halves": Fusion("last data gradient in two batch halves (first-layer wgrad overlap)",
                           norm={"none"}, dims={2}, img=_ROW_IMGS, even_batch=True, cpad=(4, 8),
                           when=lambda e: e.wgrad_win >= 0),
-    "dw_fused": Fusion("data + weight gradient from one staged dY halo (conv_dw.hip)", norm={"none"}, dims={2},
+    "dw_fused": Fusion("data + weight gradient from one staged dY halo (conv_dw.hip)", dims={2},
                        img=(128,), option="dw_fuse", when=lambda e: e.wgrad_win >= 0),
+    "dz_onload": Fusion("norm backward dz = ca g + cb z + cc formed in the fused data + weight gradient's "
+                        "halo (conv_dw.hip XF 2): no norm_bwd_apply pass, dz never stored",
+                        norm={"batch", "group"}, dims={2}, img=(128,), option="dw_fuse", needs=("dw_fused",)),
     "first_dz_onload": Fusion("first layer's norm-backward dz formed by its window wgrad (XF 2)",
                               norm={"batch", "group"}, dims={2}, img=_ROW_IMGS, cpad=(4, 8),
                               when=lambda e: e.wgrad_win >= 0),
@@ -583,7 +586,9 @@ class NativeUNet:
         self.norm_layers = []
         # fused statistics (conv epilogues write per-tile partial sums): name -> buffer
         self._stat_bufs: Dict[str, torch.Tensor] = {}
+        self._stat_retired: List[torch.Tensor] = []
         self._bwd_fused: Dict[str, Tuple[int, bool]] = {}
+        self._dz_onload = set()              # norm layers whose dz the fused dgrad + wgrad forms on load
         self.fuse_norm_stats = True
         if self.spec.norm == "none":
             return
@@ -604,8 +609,13 @@ class NativeUNet:
                 self.state[l.name + "/norm/moving_variance"] = torch.ones(l.cout, dtype=f32, device=self.device)
 
     def _stat_buf(self, key, floats):
+        """Statistics buffer `key` of at least `floats` floats.  A buffer that has to grow is
+        replaced, and the superseded one is kept alive (never freed under a recorded op) but
+        is no named region: an op still pointing into it fails the plan's def-use check."""
         t = self._stat_bufs.get(key)
         if t is None or t.numel() < floats:
+            if t is not None:
+                self._stat_retired.append(t)
             t = torch.zeros(max(floats, 64), dtype=torch.float32, device=self.device)
             self._stat_bufs[key] = t
         return t
@@ -777,8 +787,8 @@ class NativeUNet:
                                             _ptr(cb), _ptr(cc), dgam, dbet, _ptr(ws)],
                                [N, R // N, C, spec.groups, P, 1], [self.NORM_EPS], "gnfin_bwd:" + l.name)
                 cstride = C
-            if not apply:
-                return
+            if not apply or l.name in self._dz_onload:
+                return          # (dz formed on load by its consumers: conv_dw XF 2 / first-layer wgrad)
             if hn:      # dz = a w dlogit m + b z + c: g formed per pixel from prob and t
                 fa, fc = b["fa:" + l.name], b["fc:" + l.name]
                 pl.add_generic("head_norm_bwd", [_ptr(z), _ptr(self.prob), _ptr(self.target), _ptr(self.sums),
@@ -795,7 +805,8 @@ class NativeUNet:
     def _head_grad_fields(self):
         """hg_* fields (conv_params.h HeadGrad) of the head input's gradient consumers."""
         return dict(hg_prob=_ptr(self.prob), hg_t=_ptr(self.target), hg_sums=_ptr(self.sums),
-                    hg_w=self.master_ptr("Mask/kernel"), hg_bits=_ptr(self.relu_bits[self.head_in]),
+                    hg_w=self.master_ptr("Mask/kernel"),
+                    hg_bits=_ptr(self.relu_bits[self.head_in]) if self.head_in in self.relu_bits else None,
                     hg_gscale=_ptr(self.loss_scale_dev), hg_inv_total=1.0 / float(self.npix(1)),
                     hg_bce_w=self.bce_weight)
 
@@ -837,12 +848,16 @@ class NativeUNet:
         nsplit = self.opts["dw_wgs"]
         b = self.bufs
         half = b[src1].numel() * b[src1].element_size() // len(parts)
+        if len(parts) > 1 and parts[0].get("nz"):
+            return None          # (the statistics rows of the dgrad-norm epilogue are per whole launch)
         out = []
         for k, d in enumerate(parts):
-            if d.get("nz") or d.get("hg_prob") or d.get("route_gy"):
+            if d.get("hg_prob") or d.get("route_gy"):
                 return None
             f = dict(d, rev=0, fw_x=_ptr(b[src1]) + k * half, fw_Cx=l.cin, fw_nsplit=nsplit, fw_split_lo=k * nsplit,
                      name=d["name"])
+            if f.get("nz") and not self._restat_dgrad_norm(f, src1):
+                return None
             try:
                 if self.C.conv_fwd_grid(dict(f, fw_slab=1, fw_bias_slab=1)) != nsplit:
                     return None
@@ -851,7 +866,42 @@ class NativeUNet:
             out.append(f)
         wspec["dw"] = dict(rows=nsplit * len(parts))
         self._fusion_on("dw_fused", l.name)
+        if len(out) == 1 and l.name in self.norm_layers and self._fusion_ok("dz_onload", l.name):
+            # the conv's own norm backward on load: the halo is formed from g and z (XF 2), or
+            # for the normalised head input from z, the probability and the target (XF 3: g
+            # is never formed either -- head_norm_bwd's pass disappears)
+            C = l.cout
+            xf = dict(out[0], xform=2, src1=_ptr(b["d:" + l.name]), xz=_ptr(b["z:" + l.name]),
+                      xa=_ptr(b["ca:" + l.name]), xb=_ptr(b["cb:" + l.name]), xc=_ptr(b["cc:" + l.name]),
+                      xcs=0 if self.spec.norm == "batch" else C)
+            if self._norm_head_loss and l.name == self.head_in:
+                hg = self._head_grad_fields()
+                hg.pop("hg_bits")
+                xf.update(hg, src1=_ptr(b["z:" + l.name]), hg_fa=_ptr(b["fa:" + l.name]),
+                          hg_fc=_ptr(b["fc:" + l.name]))
+            try:
+                ok = self.C.conv_fwd_grid(dict(xf, fw_slab=1, fw_bias_slab=1)) == nsplit
+            except ValueError:
+                ok = False
+            if ok:
+                out = [xf]
+                self._dz_onload.add(l.name)
+                self._fusion_on("dz_onload", l.name)
         return out
+
+    def _restat_dgrad_norm(self, f, tname):
+        """Fused data + weight gradient `f` whose epilogue is the dgrad-norm one (gradient of
+        normalised activation `tname`): its statistics rows are per 256-pixel window, not
+        the split kernel's tiles -- re-plan them (rows + buffer) for the fused launch."""
+        l = next(x for x in self.spec.layers if x.name == tname)
+        d = dict(f, fw_slab=1, fw_bias_slab=1)       # (slab pointers: filled at emission)
+        d.pop("stats", None)
+        fused = self._fuse_stats(d, "bst:" + tname, l.cout, l.level)
+        if fused is None:
+            return False
+        f["stats"] = d["stats"]
+        self._bwd_fused[tname] = fused
+        return True
 
     def _skip_route(self, l, skip, c1, c2, dy):
         """(pool name, dgrad dict) of the deferred skip half of decoder conv l's data
@@ -1654,6 +1704,10 @@ class NativeUNet:
                     if sf is not None:
                         self._layer_done_at[tf["consumer"]] = plan.size()
         flush()
+        for name in self._dz_onload:
+            # formed on load by the fused data + weight gradient: never stored (kept aside so
+            # the plan validation flags any op that would still read it)
+            self._dropped["dz:" + name] = self.bufs.pop("dz:" + name, None)
 
     def _add_wgrad_chunked(self, plan, d, row_floats, brow_floats):
         """plan.add_wgrad(d); a tiled (non-window) weight gradient whose operand tensors

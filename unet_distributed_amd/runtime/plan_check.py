@@ -25,7 +25,7 @@ from typing import Dict, List, Tuple
 
 import torch
 
-_HG = ("hg_prob", "hg_t", "hg_sums", "hg_w", "hg_bits", "hg_gscale")
+_HG = ("hg_prob", "hg_t", "hg_sums", "hg_w", "hg_bits", "hg_gscale", "hg_fa", "hg_fc")
 CONV_READS = ("src1", "src2", "wgt", "bias", "mask1", "mask2", "route_gy", "nz", "na", "nc", "xa", "xb", "xc", "xz",
               "ut_x", "ut_w", "ut_b", "head_w", "head_b", "fw_x") + _HG
 CONV_WRITES = ("dst1", "dst2", "stats", "relu_bits", "pool_dst", "head_logit", "xout", "fw_slab", "fw_bias_slab")
