@@ -14,3 +14,6 @@ done
 UNET_ENGINE="fwd_streams=1" timeout -k 10 300 python tools/layer_times.py --batch 1024 --img 128 --norm batch \
   --out $o/lt_bn.md > $o/lt_bn.log 2>&1 || { echo "lt rc=$?"; tail -20 $o/lt_bn.log; exit 1; }
 head -3 $o/lt_bn.md
+UNET_ENGINE="fwd_streams=1" timeout -k 10 300 python tools/layer_times.py --batch 1024 --img 128 \
+  --out $o/lt_head.md > $o/lt_head.log 2>&1 || { echo "lt rc=$?"; tail -20 $o/lt_head.log; exit 1; }
+head -3 $o/lt_head.md

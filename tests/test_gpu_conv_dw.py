@@ -229,3 +229,53 @@ def test_fused_dgrad_wgrad_normalised_head_on_load(cuda_dev, N, gn, bce):
     (dx0, s0, b0, t0), (dx1, s1, b1, t1) = outs
     assert torch.equal(dx1, dx0) and torch.equal(t1, t0)
     assert torch.equal(s1, s0) and torch.equal(b1, b0)
+
+
+@pytest.mark.parametrize("N,nsplit,bce", [(2, 16, 0.0), (3, 96, 0.5)])
+def test_fused_dgrad_wgrad_head_on_load(cuda_dev, N, nsplit, bce):
+    """XF 4 (the norm-free head input conv9b): dY = dlogit w (y > 0) is formed in the halo
+    from the probability, the target and the head input's ReLU bits -- the data gradient
+    and slab rows equal the fused kernel fed head_bwd's materialised dY bit for bit."""
+    torch.manual_seed(90 + N)
+    H = W = 128
+    dev = cuda_dev
+    P = N * H * W
+    y = F.relu(torch.randn(N, H, W, 32, device=dev)).bfloat16()      # the head input (conv9b output)
+    v = (y.float() > 0).reshape(-1, 8).to(torch.int32)
+    bits = (v << torch.arange(8, device=dev, dtype=torch.int32)).sum(1).to(torch.uint8)
+    hw = 0.3 * torch.randn(32, device=dev)
+    hb = torch.randn(1, device=dev)
+    t = (torch.rand(P, device=dev) > 0.7).bfloat16()
+    prob = torch.empty(P, device=dev)
+    nb = C().head_blocks(P)
+    part = torch.empty(nb * 33 + 4 * nb, device=dev)
+    sums = torch.empty(4, device=dev)
+    C().generic("head_fwd", [ptr(y), ptr(hw), ptr(hb), ptr(t), ptr(prob), ptr(part), ptr(sums)], [P, 32], [], stream())
+    dy = torch.empty_like(y)
+    ow, ob = torch.empty(32, device=dev), torch.empty(1, device=dev)
+    gsc = torch.full((1,), 2.0, device=dev)
+    C().generic("head_bwd", [ptr(y), ptr(hw), ptr(prob), ptr(t), ptr(sums), ptr(dy), ptr(part), ptr(ow), ptr(ob),
+                             ptr(gsc)], [P, 32], [1.0 / P, bce, 1.0], stream())
+    x = F.relu(torch.randn(N, H, W, 32, device=dev)).bfloat16()
+    act = F.relu(torch.randn(N, H, W, 32, device=dev)).bfloat16()
+    w = (torch.randn(3, 3, 32, 32, device=dev) * 0.1).bfloat16()
+    wp = pack_dgrad(w)
+    outs = []
+    for xf in (False, True):
+        dx = torch.full((N, H, W, 32), 7.0, device=dev, dtype=torch.bfloat16)
+        slab = torch.full((nsplit, 9, 32, 32), float("nan"), device=dev)
+        bslab = torch.full((nsplit, 32), float("nan"), device=dev)
+        d = dict(N=N, OH=H, OW=W, IH=H, IW=W, KH=3, KW=3, pad=1, C1=32, src1=ptr(dy), wgt=ptr(wp), Cout=32,
+                 relu=0, mask1=ptr(act), dst1=ptr(dx), fw_x=ptr(x), fw_slab=ptr(slab), fw_bias_slab=ptr(bslab),
+                 fw_Cx=32, fw_nsplit=nsplit)
+        if xf:
+            d.update(hg_prob=ptr(prob), hg_t=ptr(t), hg_sums=ptr(sums), hg_w=ptr(hw), hg_bits=ptr(bits),
+                     hg_gscale=ptr(gsc), hg_inv_total=1.0 / P, hg_bce_w=bce)
+        assert C().conv_fwd_grid(d) == nsplit
+        C().conv_fwd(d, stream())
+        outs.append((dx, slab, bslab))
+    torch.cuda.synchronize()
+    (dx0, s0, b0), (dx1, s1, b1) = outs
+    assert torch.equal(dx1, dx0)
+    assert torch.equal(s1, s0) and torch.equal(b1, b0)
+    assert rel_err(s1.double().sum(0).float(), _ref_wgrad(x, dy, w).reshape(9, 32, 32)) < 1e-4

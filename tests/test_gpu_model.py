@@ -507,8 +507,8 @@ def test_tconv_fused_norm_step(cuda_dev, monkeypatch, norm):
     dict(batch_size=3, img_size=128, in_channels=4, loss="dice_bce", hip_graph=True),
 ])
 def test_fused_dgrad_wgrad_step(cuda_dev, monkeypatch, kw):
-    """dw_fuse=1 (default: conv1b's data and weight gradients from one staged dY halo,
-    conv_dw.hip) vs dw_fuse=0: the forward, every data gradient and every other parameter
+    """dw_fuse=1 (default: conv1b's and conv9b's data and weight gradients from one staged
+    dY halo -- conv9b's formed on load from the head, conv_dw.hip XF 4) vs dw_fuse=0: the forward, every data gradient and every other parameter
     gradient are bit-identical; the fused layers' weight / bias gradients differ only by
     fp32 summation order."""
     outs = []
@@ -516,8 +516,8 @@ def test_fused_dgrad_wgrad_step(cuda_dev, monkeypatch, kw):
         monkeypatch.setenv("UNET_ENGINE", "dw_fuse=" + v)
         spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
         e = nb.engine
-        fused = e.fusions.get("dw_fused", [])
-        assert (fused == ["conv1b"]) == (v == "1"), fused
+        fused = sorted(e.fusions.get("dw_fused", []))
+        assert (fused == ["conv1b", "conv9b"]) == (v == "1"), fused
         for seed in (31, 32):
             nb.fwd_bwd(x, y, seed=seed)
         torch.cuda.synchronize()
@@ -526,7 +526,7 @@ def test_fused_dgrad_wgrad_step(cuda_dev, monkeypatch, kw):
     (s0, p0, d0, g0), (s1, p1, d1, g1) = outs
     assert torch.equal(s0, s1) and torch.equal(p0, p1) and torch.equal(d0, d1)
     for k in g0:
-        if k.startswith("conv1b/"):
+        if k.startswith(("conv1b/", "conv9b/")):
             assert rel_err_(g1[k], g0[k]) < 1e-5, (k, rel_err_(g1[k], g0[k]))
         else:
             assert torch.equal(g0[k], g1[k]), k

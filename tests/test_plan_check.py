@@ -109,4 +109,34 @@ def test_largest_benched_batches_plan(dims, img, batch, cin):
     32-bit offsets from the tensor start (the transposed-conv windows) step aside for the
     per-tile-based ones there (round 5: 512^2 b128 failed after the 256-wide tconv dgrad)."""
     e = _engine("none", False, dims, img, batch=batch, in_channels=cin)
-    check_engine(e)
+    errs = check_engine(e)
+    assert errs == {"train": [], "eval": []}, errs
+
+
+@pytest.mark.parametrize("dims,img,ups", [(2, 64, False), (2, 64, True), (2, 128, False), (3, 16, False),
+                                          (3, 16, True)])
+def test_fp32_executor_plans_validate(dims, img, ups):
+    """The fp32 executor (runtime/f32_engine.py, what 'auto' picks for every fp32 GPU config)
+    gets the same static dispatch / def-use / gradient-coverage validation; its dry-run
+    plans refuse to run."""
+    from unet_distributed_amd.runtime.f32_engine import NativeUNetF32
+    spec = UNetSpec(in_channels=1 if ups else 4, use_upsampling=ups, dims=dims)
+    flat = FlatParams(spec)
+    e = NativeUNetF32(spec, flat, 2, img, "cpu", bucket_bounds=plan_buckets(flat, 4.0), dry_run=True)
+    errs = check_engine(e)
+    assert errs == {"train": [], "eval": []}, errs
+    with pytest.raises(RuntimeError):
+        e.forward(1)
+
+
+def test_write_extent_overrun_is_flagged():
+    """A write span (from the op's shape: batch chunk / channel split / slab-row offsets)
+    that runs past the end of its buffer is an error, not silently accepted."""
+    from unet_distributed_amd.runtime.plan_check import check_plan
+    e = _engine("batch", False, 2, 64)
+    assert check_plan(e, e.plan, True) == []
+    k = next(i for i, op in enumerate(e.plan.ops) if op.get("spans") and op["name"].startswith("dgrad:"))
+    p, n = e.plan.ops[k]["spans"][0]
+    e.plan.ops[k]["spans"][0] = (p + 64, n)
+    errs = check_plan(e, e.plan, True)
+    assert any("past its end" in m for m in errs), errs

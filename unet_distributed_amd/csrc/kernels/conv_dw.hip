@@ -59,7 +59,10 @@ constexpr int DW_AI = DW_BM / 16;                     // x image pieces
 constexpr int DW_WB = DW_WI * 1024, DW_XB = DW_XI * 1024, DW_AB = DW_AI * 1024;
 constexpr int DW_KB = 6 * 32 * 4;                     // XF 2 / 3 coefficients
 constexpr int DW_LDS = DW_WB + DW_XB + DW_AB + DW_KB;
-static_assert(epi_lds_bytes<DW_BM, DW_BN>() <= DW_XB, "epilogue staging aliases the dY halo image");
+// the epilogue's staging tile (BN = 32: unpadded 64-byte rows + [4][2][BN] statistics
+// partials, conv_epilogue.h) aliases the two physical halo rows of the window's first two
+// logical rows, which the next window does not carry
+static_assert(DW_BM * 64 + 4 * 2 * DW_BN * 4 <= 2 * DW_ROWB, "epilogue staging aliases two halo rows");
 static_assert(4 * 64 * 16 * 4 <= DW_LDS, "slab reduction scratch");
 // XF 2: granule k = tid + 256 j of the HR x 144-slot x 4-chunk halo (slots 130..143 are
 // padding, stored as zeros) -> LDS byte 16 k with the chunk swizzled; a thread's chunk is
@@ -68,9 +71,31 @@ constexpr int DW_HG = DW_HR * DW_HWP * 4;
 constexpr int DW_HJ = DW_HG / DW_NTHR;
 static_assert(DW_HG == DW_HJ * DW_NTHR, "whole granule passes");
 
+// per-pixel logit gradients of the halo granules (XF 4: head_grad.h, head.hip
+// head_bwd_kernel's formula; XF 3: the normalised head's, head.hip hn_scalars)
+template <int XF>
+__device__ __forceinline__ void dw_dlogit(const ConvFwdParams& p, const float (&pr)[DW_HJ], const float (&tv)[DW_HJ],
+                                          float (&dl)[DW_HJ]) {
+  if constexpr (XF == 4) {
+    const float I = p.hg.sums[0], St = p.hg.sums[1], Sp = p.hg.sums[2];
+    const float a = -2.f / (2.f * I + 1.f), bb = 1.f / (St + Sp + 1.f);
+    const float gs = p.hg.gscale ? *p.hg.gscale : 1.f;
+#pragma unroll
+    for (int j = 0; j < DW_HJ; ++j) dl[j] = head_dlogit(pr[j], tv[j], a, bb, p.hg.inv_total, p.hg.bce_w, gs);
+  } else {
+    const float gs = p.hg.gscale ? *p.hg.gscale : 1.f;
+    const float al = -2.f * gs / (2.f * p.hg.sums[0] + 1.f);
+    const float be = gs / (p.hg.sums[1] + p.hg.sums[2] + 1.f);
+    const float ga = gs * p.hg.bce_w * p.hg.inv_total;
+#pragma unroll
+    for (int j = 0; j < DW_HJ; ++j) dl[j] = hn_dlogit(pr[j], tv[j], al, be, ga);
+  }
+}
+
 template <int EPI, int XF>
 __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams p) {
-  static_assert(XF == 0 || XF == 2 || XF == 3, "plain dY, norm backward on load (of the normalised head)");
+  static_assert(XF == 0 || XF == 2 || XF == 3 || XF == 4,
+                "plain dY, norm backward on load (of the normalised head), head gradient on load");
   constexpr int W = DW_W, R = DW_R, HR = DW_HR, ROWB = DW_ROWB, BN = DW_BN;
   constexpr int TM = 4, TN = 2, TC = 2, RW = 2, NCS = 4;   // data-gradient strip: 2 rows x 32 columns per wave
   __shared__ __attribute__((aligned(1024))) char smem[DW_LDS];
@@ -169,11 +194,22 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
   // registers only while the halo is formed)
   float* Ks = (float*)(As + DW_AB);
   const int kch = (tid & 3) * 8;
+  // Halo row carry: the next window of the same image needs halo rows g0 + 1, g0 + 2 --
+  // this window's logical rows 2, 3 (already formed: XF 2 / 3 transformed).  Logical row r
+  // lives in physical row r ^ 2 fl; a carried window flips fl and loads (forms) only its
+  // rows 2, 3, into the physical rows the previous epilogue staged its tile in.  Halves the
+  // halo's loads (and the XF 2 / 3 transform work); the MFMA address offsets become
+  // hr ROWB +- 2 fl ROWB.
+  int fl = 0;
 
   for (int win = w_begin; win < w_end; ++win) {
     const int g0 = win * R;
     const int grow0 = (g0 / H) * H;                    // the window's image (H % R == 0)
     const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
+    const bool carry = win > w_begin && top_in;       // (wave-uniform)
+    if (carry) fl ^= 1;
+    const int fo = fl * 2 * ROWB;                       // physical offset of logical rows 0, 1 (rows 2, 3: -fo)
+    const int k0 = carry ? 2 * DW_HWP * 4 : 0;          // first halo granule to form
     const size_t img_px = (size_t)grow0 * W;
     const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((const char*)p.src1 + img_px * C * 2), (short)0, OOB, 0x00020000);
@@ -183,65 +219,71 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
     // before the barrier, so they fly while the previous window's epilogue stores drain; g
     // arrives through the dY halo DMA below and is turned into dz in place.  XF 3: the
     // DMA brings z (src1 = z), g = w dlogit [fa z + fc > 0] per pixel with dlogit from the
-    // probability and target loaded here
+    // probability and target loaded here (XF 4: dY = w dlogit [y > 0] from the ReLU bits)
     u32x4 zv[XF == 2 ? DW_HJ : 1];
-    float dl[XF == 3 ? DW_HJ : 1];
+    // XF 3 / 4: each lane loads its granule's pixel probability / target (XF 4: the byte
+    // of ReLU bits of its 8 channels); the logit gradients are formed after the DMA barrier.
+    // (Measured against one load per lane + DPP quad broadcasts, and against forming the
+    // logit gradients before the first barrier: per launch 0.855 vs 0.90 / 0.87 ms, XF 4.)
+    float dl[XF >= 3 ? DW_HJ : 1];
+    uint32_t hbits[XF == 4 ? DW_HJ : 1];
+    float pr[XF >= 3 ? DW_HJ : 1], tv[XF >= 3 ? DW_HJ : 1];
     uint32_t okm = 0;
     if constexpr (XF >= 2) {
-      // Ks: ca cb cc [fa fc ca*w] of the window's sample
+      // Ks: ca cb cc [fa fc ca*w] of the window's sample (XF 4: the head weights w)
       float kv = 0.f;
-      constexpr int NK = XF == 3 ? 192 : 96;
+      constexpr int NK = XF == 4 ? 32 : XF == 3 ? 192 : 96;
       if (tid < NK) {
         const int m = tid >> 5, c = tid & 31;
-        const float* src = m == 0 ? p.xa : m == 1 ? p.xb : m == 2 ? p.xc : m == 3 ? p.hg.fa : m == 4 ? p.hg.fc : p.xa;
-        const size_t ci = (size_t)(g0 / H) * p.xcs + c;
-        kv = src[ci];
-        if (XF == 3 && m == 5) kv *= p.hg.w[c];
+        if constexpr (XF == 4) {
+          kv = p.hg.w[c];
+        } else {
+          const float* src = m == 0 ? p.xa : m == 1 ? p.xb : m == 2 ? p.xc : m == 3 ? p.hg.fa : m == 4 ? p.hg.fc : p.xa;
+          const size_t ci = (size_t)(g0 / H) * p.xcs + c;
+          kv = src[ci];
+          if (XF == 3 && m == 5) kv *= p.hg.w[c];
+        }
       }
       const __amdgpu_buffer_rsrc_t rsz = __builtin_amdgcn_make_buffer_rsrc(
           (void*)((const char*)p.xz + img_px * C * 2), (short)0, OOB, 0x00020000);
-      float pr[XF == 3 ? DW_HJ : 1], tv[XF == 3 ? DW_HJ : 1];
 #pragma unroll
       for (int j = 0; j < DW_HJ; ++j) {
-        const int k = tid + DW_NTHR * j;
+        const int k = k0 + tid + DW_NTHR * j;
         const int hr = k / (DW_HWP * 4), s = (k >> 2) - hr * DW_HWP;
         const int gr = g0 - 1 + hr, col = s - 1;
-        const bool ok = (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)gr < (unsigned)rows_total &&
-                        (unsigned)col < (unsigned)W;
+        const bool ok = k < DW_HG && (hr > 0 || top_in) && (hr < R + 1 || bot_in) &&
+                        (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
         okm |= (ok ? 1u : 0u) << j;
-        if constexpr (XF == 3) {
+        if constexpr (XF >= 3) {
           const int pix = ok ? gr * W + col : 0;
           pr[j] = p.hg.prob[pix];
           tv[j] = bits2f(((const uint16_t*)p.hg.t)[pix]);
+          if constexpr (XF == 4) hbits[j] = ok ? ((const uint8_t*)p.hg.bits)[(size_t)pix * 4 + (tid & 3)] : 0u;
         }
         if constexpr (XF == 2)
           zv[j] = __builtin_amdgcn_raw_buffer_load_b128(rsz, ok ? ((gr - grow0) * W + col) * C * 2 + kch * 2 : OOB,
                                                         0, 0);
       }
-      if constexpr (XF == 3) {
-        // the batch scalars of the logit gradient (head.hip hn_scalars)
-        const float gs = p.hg.gscale ? *p.hg.gscale : 1.f;
-        const float al = -2.f * gs / (2.f * p.hg.sums[0] + 1.f);
-        const float be = gs / (p.hg.sums[1] + p.hg.sums[2] + 1.f);
-        const float ga = gs * p.hg.bce_w * p.hg.inv_total;
-#pragma unroll
-        for (int j = 0; j < DW_HJ; ++j) dl[j] = hn_dlogit(pr[j], tv[j], al, be, ga);
-      }
       if (tid < NK) Ks[tid] = kv;    // (the previous window read them before its MFMAs)
     }
     __syncthreads();      // the previous window's epilogue is done with the staging tile
-    // dY (XF 2: g, XF 3: z) halo image: wave w fills halo row hr = w (pixel row g0 - 1 + w), slot
-    // hc = column hc - 1, as 9 pieces of 16 slots; rows of another image and columns
-    // outside [0, W) load zeros (out-of-range offsets).  Per piece only an immediate changes.
-    {
-      const int gr = g0 - 1 + wave;
-      const bool row_ok = (wave > 0 || top_in) && (wave < R + 1 || bot_in) && (unsigned)gr < (unsigned)rows_total;
+    // dY (XF 2: g, XF 3: z) halo image: wave w fills halo row hr = w (pixel row g0 - 1 + w)
+    // -- carried: waves 2 i, 2 i + 1 the two halves of row 2 + i -- slot hc = column hc - 1,
+    // as 16-slot pieces; rows of another image and columns outside [0, W) load zeros
+    // (out-of-range offsets).  Per piece only an immediate changes.
+    if constexpr (XF != 4) {
+      const int hr = carry ? 2 + (wave >> 1) : wave;
+      const int jlo = carry ? 5 * (wave & 1) : 0, jhi = carry && !(wave & 1) ? 5 : DW_PPR;
+      const int gr = g0 - 1 + hr;
+      const bool row_ok = (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)gr < (unsigned)rows_total;
       const int rowoff = (gr - grow0) * W * C * 2;
+      char* hdst = Xs + (hr ^ (2 * fl)) * ROWB;
 #pragma unroll
       for (int j = 0; j < DW_PPR; ++j) {
+        if (j < jlo || j >= jhi) continue;
         const bool ok = row_ok && (j > 0 || lslot > 0) && (16 * j + lslot - 1 < W);
         const int off = ok ? rowoff + dma_lane + j * 1024 : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs1, (__attribute__((address_space(3))) void*)(Xs + wave * ROWB + j * 1024),
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs1, (__attribute__((address_space(3))) void*)(hdst + j * 1024),
                                                  16, off, 0, 0, 0);
       }
     }
@@ -252,7 +294,29 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsx, (__attribute__((address_space(3))) void*)(As + (4 * wave + i) * 1024),
                                                16, xdma_lane + (4 * wave + i) * 1024, 0, 0, 0);
     __syncthreads();
-    if constexpr (XF >= 2) {
+    // (the per-pixel logit gradients: formed here, after the barrier, so the probability /
+    // target loads overlap the x image DMA instead of being waited on before it)
+    if constexpr (XF >= 3) dw_dlogit<XF>(p, pr, tv, dl);
+    if constexpr (XF == 4) {
+      // dY = dlogit w (x > 0) per slot (head_grad.h head_grad_pixel), zeros outside the image
+      float hw[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) hw[e] = Ks[kch + e];
+#pragma unroll
+      for (int j = 0; j < DW_HJ; ++j) {
+        const int k = k0 + tid + DW_NTHR * j;
+        if (k >= DW_HG) continue;
+        const int hr = k / (DW_HWP * 4), s = (k >> 2) - hr * DW_HWP;
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = dl[j] * hw[e];
+          o[e] = ((hbits[j] >> e) & 1u) ? v : 0.f;
+        }
+        *(u32x4*)(Xs + ((hr ^ (2 * fl)) * DW_HWP + s) * 64 + 16 * ((tid & 3) ^ ((s >> 1) & 3))) = pack8(o);
+      }
+      __syncthreads();
+    } else if constexpr (XF >= 2) {
       // dz = fmaf(ca, g, fmaf(cb, z, cc)) in place (16-byte granule k of the halo: LDS
       // slot k >> 2, logical chunk tid & 3), zeros outside the image.  XF 3: dz =
       // (fa z + fc > 0 ? ca w dlogit : 0) + fmaf(cb, z, cc) (head.hip head_norm_bwd_kernel)
@@ -269,9 +333,10 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
       }
 #pragma unroll
       for (int j = 0; j < DW_HJ; ++j) {
-        const int k = tid + DW_NTHR * j;
-        const int s = (k >> 2) % DW_HWP;
-        u32x4* slot = (u32x4*)(Xs + (k >> 2) * 64 + 16 * ((tid & 3) ^ ((s >> 1) & 3)));
+        const int k = k0 + tid + DW_NTHR * j;
+        if (k >= DW_HG) continue;
+        const int hr = k / (DW_HWP * 4), s = (k >> 2) - hr * DW_HWP;
+        u32x4* slot = (u32x4*)(Xs + ((hr ^ (2 * fl)) * DW_HWP + s) * 64 + 16 * ((tid & 3) ^ ((s >> 1) & 3)));
         u32x4 v = {0u, 0u, 0u, 0u};
         if ((okm >> j) & 1u) {
           float gf[8], zf[8];
@@ -311,7 +376,7 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
       for (int hr = 0; hr < HR; ++hr) {
 #pragma unroll
         for (int dw = 0; dw < 3; ++dw) {
-          const int a = dbase[dw] + hr * ROWB + so;
+          const int a = dbase[dw] + hr * ROWB + so + (hr < 2 ? fo : -fo);
           const h16x8 yb = tr8(Xs + a, Xs + a + 512);
           if (dw == 1 && hr >= 1 && hr <= R) bacc = mfma16(ones, yb, bacc);   // the window's own dY: bias sums
 #pragma unroll
@@ -343,7 +408,7 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
       for (int hr = 0; hr < RW + 2; ++hr) {
 #pragma unroll
         for (int ci = 0; ci < TC; ++ci) {
-          const h16x8 xf = *(const h16x8*)(Xs + xbase[dw] + hr * ROWB + ci * 16 * 64);
+          const h16x8 xf = *(const h16x8*)(Xs + xbase[dw] + hr * ROWB + ci * 16 * 64 + (hr < 2 ? fo : -fo));
 #pragma unroll
           for (int dh = 0; dh < 3; ++dh) {
             const int ri = hr - dh;
@@ -354,10 +419,10 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
         }
       }
     }
-    __syncthreads();      // every wave is done reading the halo image (the staging tile aliases it)
+    __syncthreads();      // every wave is done reading the halo image (the staging tile aliases rows 0, 1)
     using Map = StripTiles<W, RW, TC, NCS>;
-    conv_epilogue<DW_BM, BN, DW_BM / 4, BN, TM, TN, DW_NTHR, EPI, Map, 0, W>(p, acc, Xs, g0 * W, 0, M, wave, 0, lane,
-                                                                            tid, 0, 0, win);
+    conv_epilogue<DW_BM, BN, DW_BM / 4, BN, TM, TN, DW_NTHR, EPI, Map, 0, W>(p, acc, Xs + fo, g0 * W, 0, M, wave, 0,
+                                                                            lane, tid, 0, 0, win);
   }
 
   // ---- sum the partials of the two waves of each dY channel block (waves jw, jw + 2:
@@ -405,10 +470,12 @@ const char* conv_dw_check(const ConvFwdParams& p) {
     return "conv_fwd: fused weight gradient needs a 2D 32 -> 32 channel data gradient on 128-wide rows";
   if (p.xform && (p.xform != 2 || !p.xa || !p.xb || !p.xc || !p.xz || (p.xcs != 0 && p.xcs != p.C1) || p.xout))
     return "conv_fwd: fused weight gradient: norm backward on load (xform 2) needs xa / xb / xc / xz, xcs 0 or C";
-  if (p.hg.prob && (p.xform != 2 || p.hg.bits || !p.hg.fa || !p.hg.fc || !p.hg.t || !p.hg.sums || !p.hg.w ||
-                    p.route_gy))
+  if (p.hg.prob && p.xform && (p.xform != 2 || p.hg.bits || !p.hg.fa || !p.hg.fc || !p.hg.t || !p.hg.sums ||
+                                !p.hg.w || p.route_gy))
     return "conv_fwd: fused weight gradient: the normalised head's gradient on load needs xform 2, "
            "fa / fc (no bits), t, sums, w";
+  if (p.hg.prob && !p.xform && (!p.hg.bits || !p.hg.t || !p.hg.sums || !p.hg.w || p.route_gy || ep != EPI_DGRAD))
+    return "conv_fwd: fused weight gradient: the head gradient on load needs bits, t, sums, w";
   if (!p.fw.slab || !p.fw.bias_slab || p.fw.nsplit < 1 || p.fw.split_lo < 0)
     return "conv_fwd: fused weight gradient needs slab / bias_slab and nsplit >= 1";
   if ((long long)p.OH * p.OW * 32 * 2 >= (1LL << 31) - 64) return "conv_fwd: one image exceeds 2 GiB";
@@ -423,11 +490,13 @@ int conv_dw_stat_rows(const ConvFwdParams& p) { return p.N * p.OH / DW_R; }
 hipError_t launch_conv_dw(const ConvFwdParams& p, hipStream_t s) {
   const int ep = conv_epi_mode(p);
   const dim3 grid(p.fw.nsplit), blk(DW_NTHR);
-  if (ep == EPI_DGRAD && !p.xform)
+  if (ep == EPI_DGRAD && !p.xform && !p.hg.prob)
     UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD, 0>), grid, blk, 0, s, p);
+  else if (ep == EPI_DGRAD && !p.xform)
+    UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD, 4>), grid, blk, 0, s, p);
   else if (ep == EPI_DGRAD && p.xform == 2 && !p.hg.prob)
     UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD, 2>), grid, blk, 0, s, p);
-  else if (ep == EPI_DGRAD_NORM && !p.xform)
+  else if (ep == EPI_DGRAD_NORM && !p.xform && !p.hg.prob)
     UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD_NORM, 0>), grid, blk, 0, s, p);
   else if (ep == EPI_DGRAD_NORM && p.xform == 2 && !p.hg.prob)
     UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD_NORM, 2>), grid, blk, 0, s, p);

@@ -57,6 +57,10 @@ class NativeUNetF32:
         if spec.n_cl_out != 1:
             raise NotImplementedError("fp32 native executor: n_cl_out must be 1")
         self.spec, self.flat = spec, flat
+        # dry_run: plan construction only (plan construction itself launches nothing); the
+        # static plan validation (runtime/plan_check.py) runs on such an executor on a CPU
+        # host, and running its plans is refused
+        self._dry = dry_run
         self.B, self.img, self.dims = batch, img, spec.dims
         self.device = torch.device(device)
         self.loss = loss
@@ -378,11 +382,17 @@ class NativeUNetF32:
         self.bufs["x"].copy_(x_all.index_select(0, idx).view_as(self.bufs["x"]))
         self.target.copy_(y_all.index_select(0, idx).reshape(-1))
 
+    def _live(self):
+        if self._dry:
+            raise RuntimeError("fp32 executor built with dry_run=True: its plans are for validation only")
+
     def forward(self, seed: int, stream=None):
+        self._live()
         self.plan.set_seed(seed & 0xFFFFFFFF)
         self.plan.run(0, self.fwd_end, native.stream_handle(stream))
 
     def backward(self, on_segment=None, stream=None):
+        self._live()
         s = native.stream_handle(stream)
         begin = self.fwd_end
         for i, end in enumerate(self.seg_ends):
@@ -393,6 +403,7 @@ class NativeUNetF32:
                 on_segment(i)
 
     def evaluate_batch(self, stream=None):
+        self._live()
         self.eval_plan.set_seed(0)
         self.eval_plan.run(0, self.eval_plan.size(), native.stream_handle(stream))
 

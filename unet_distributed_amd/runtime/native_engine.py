@@ -224,8 +224,8 @@ class NativeUNet:
         self._alloc_weights()
         self._alloc_activations()
         # (each op's parameters are kept for the static plan validation, runtime/plan_check.py)
-        self.plan = RecordingPlan(self.C.Plan(self.dt_id))
-        self.eval_plan = RecordingPlan(self.C.Plan(self.dt_id))
+        self.plan = RecordingPlan(self.C.Plan(self.dt_id), self._stat_rows_of)
+        self.eval_plan = RecordingPlan(self.C.Plan(self.dt_id), self._stat_rows_of)
         self._plan_xforms()
         self._norm_head_loss = False
         self._build_forward(self.plan, dropout=True)
@@ -238,6 +238,13 @@ class NativeUNet:
         self.set_buckets(bucket_bounds)
         if not dry_run:          # dry_run: plan construction only (CPU tests, no GPU launches)
             self.repack()
+
+    def _stat_rows_of(self, d):
+        """Statistics rows a conv launch writes (plan validation of the stats extents)."""
+        try:
+            return self.C.conv_stat_tiles(dict(d, stats=1))[0]
+        except ValueError:
+            return 0
 
     # ------------------------------------------------------------------ fusion preconditions
     def _fusion_ok(self, name: str, layer: Optional[str] = None) -> bool:
@@ -842,7 +849,7 @@ class NativeUNet:
         dY (1 GiB at level 1, b1024) is read once instead of twice.  Returns the dicts with
         the fw_* fields (slab pointers filled at emission), or None."""
         if (not self._fusion_ok("dw_fused") or skip is not None or l.cin != 32 or l.cout != 32
-                or wspec.get("kernel_out") or wspec["kd"].get("xform") or wspec["kd"].get("hg_prob")
+                or wspec.get("kernel_out") or wspec["kd"].get("xform")
                 or wspec["M1"] != 32 or wspec["M2"] or src1 not in self.bufs):
             return None
         nsplit = self.opts["dw_wgs"]
@@ -852,8 +859,8 @@ class NativeUNet:
             return None          # (the statistics rows of the dgrad-norm epilogue are per whole launch)
         out = []
         for k, d in enumerate(parts):
-            if d.get("hg_prob") or d.get("route_gy"):
-                return None
+            if d.get("route_gy") or (d.get("hg_prob") and len(parts) > 1):
+                return None       # (head-on-load: the head input's dY formed from prob / target / bits, XF 4)
             f = dict(d, rev=0, fw_x=_ptr(b[src1]) + k * half, fw_Cx=l.cin, fw_nsplit=nsplit, fw_split_lo=k * nsplit,
                      name=d["name"])
             if f.get("nz") and not self._restat_dgrad_norm(f, src1):

@@ -37,6 +37,49 @@ def _sel(p, idx):
     return [p[i] for i in idx if i < len(p)]
 
 
+def _conv_write_spans(d, stat_tiles=None) -> List[Tuple[int, int]]:
+    """(pointer, bytes) of the writes of 16-bit conv dict `d` whose extent follows from its
+    shape (the executor's offset arithmetic -- batch chunks, tail halves, channel splits,
+    slab rows -- must keep each inside its buffer)."""
+    g = d.get
+    N, OD, OH, OW = g("N", 1), g("OD", 1) or 1, g("OH", 1), g("OW", 1)
+    M = N * OD * OH * OW
+    Cout = g("Cout", 0)
+    D1 = g("D1") or Cout
+    out = []
+    if g("shuffle"):
+        out.append((g("dst1"), M * Cout * 2))
+    else:
+        out.append((g("dst1"), M * D1 * 2))
+        if g("dst2"):
+            out.append((g("dst2"), M * (Cout - D1) * 2))
+    if g("relu_bits"):
+        out.append((g("relu_bits"), M * Cout // 8))
+    if g("head_logit"):
+        out.append((g("head_logit"), M * 4))
+    if g("pool_dst"):
+        out.append((g("pool_dst"), M // 4 * Cout * 2))
+        out.append((g("pool_code"), M // 4 * Cout // 8 * 4))
+    if g("xout"):
+        out.append((g("xout"), M * g("C1", 0) * 2))
+    if g("fw_x"):
+        rows = g("fw_split_lo", 0) + g("fw_nsplit", 0)
+        out.append((g("fw_slab"), rows * 9 * g("fw_Cx", 0) * g("C1", 0) * 4))
+        out.append((g("fw_bias_slab"), rows * g("C1", 0) * 4))
+    if g("stats") and stat_tiles is not None:
+        rows = stat_tiles(d)
+        if rows:
+            out.append((g("stats"), rows * 2 * Cout * 4))
+    return [(p, n) for p, n in out if p]
+
+
+def _generic_write_spans(kind: str, p: List[int], ints: List[int]) -> List[Tuple[int, int]]:
+    """(pointer, bytes) of the writes of the streaming norm passes (N, P, C in ints)."""
+    if kind in ("norm_apply", "norm_bwd_apply") and len(p) > 5 and len(ints) >= 3:
+        return [(p[5], ints[0] * ints[1] * ints[2] * 2)]
+    return []
+
+
 def _generic_rw(kind: str, p: List[int], ints: List[int]) -> Tuple[List[int], List[int]]:
     """(read pointers, written pointers) of one generic op (layouts: bindings.cpp)."""
     if kind == "ups_fwd":
@@ -108,8 +151,9 @@ def _generic_rw(kind: str, p: List[int], ints: List[int]) -> Tuple[List[int], Li
 class RecordingPlan:
     """A native `_C.Plan` that also keeps each op's parameters for `check_plan`."""
 
-    def __init__(self, plan):
+    def __init__(self, plan, stat_tiles=None):
         self._plan = plan
+        self._stat_tiles = stat_tiles        # conv dict -> statistics rows (extent of `stats`)
         self.ops: List[dict] = []
 
     def add_conv_fwd(self, d):
@@ -117,7 +161,8 @@ class RecordingPlan:
         reads = [d.get(k) for k in CONV_READS]
         writes = [d.get(k) for k in CONV_WRITES]
         (reads if d.get("route_gy") else writes).append(d.get("pool_code"))
-        self.ops.append(dict(name=d.get("name", "conv_fwd"), reads=reads, writes=writes))
+        self.ops.append(dict(name=d.get("name", "conv_fwd"), reads=reads, writes=writes,
+                             spans=_conv_write_spans(d, self._stat_tiles)))
         return i
 
     def add_wgrad(self, d):
@@ -142,7 +187,8 @@ class RecordingPlan:
     def add_generic(self, kind, ptrs, ints, floats, name=""):
         i = self._plan.add_generic(kind, ptrs, ints, floats, name)
         r, w = _generic_rw(kind, list(ptrs), list(ints))
-        self.ops.append(dict(name=name or kind, reads=r, writes=w))
+        self.ops.append(dict(name=name or kind, reads=r, writes=w,
+                             spans=_generic_write_spans(kind, list(ptrs), list(ints))))
         return i
 
     def annotate(self, reads=(), writes=()):
@@ -164,11 +210,15 @@ class _Regions:
             self.spans.append((a, a + t.numel() * t.element_size(), name))
 
     def find(self, ptr):
+        s = self.find_span(ptr)
+        return None if s is None else s[2]
+
+    def find_span(self, ptr):
         best = None
         for a, b, n in self.spans:
             if a <= ptr < b and (best is None or b - a < best[1] - best[0]):
                 best = (a, b, n)
-        return None if best is None else best[2]
+        return best
 
 
 def engine_regions(e) -> Tuple[_Regions, set]:
@@ -242,6 +292,11 @@ def check_plan(e, plan, train: bool) -> List[str]:
                 errs.append("op %d %s: writes %s" % (i, op["name"], r or "unknown pointer 0x%x" % p))
             else:
                 written.add(r)
+        for p, n in op.get("spans", ()):
+            sp = R.find_span(int(p))
+            if sp is not None and int(p) + n > sp[1]:
+                errs.append("op %d %s: writes %d bytes at %s+%d, past its end (%d bytes)"
+                            % (i, op["name"], n, sp[2], int(p) - sp[0], sp[1] - sp[0]))
     if train:
         for name, shape, off, n in e.flat.entries:
             if "grad:" + name not in written:
