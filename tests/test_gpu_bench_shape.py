@@ -102,3 +102,56 @@ def test_bench_shape_weight_gradients_per_layer(stepped):
         del xin, dy
     print("bench-shape weight gradients checked:", checked)
     assert len(checked) >= 8
+
+
+def _dgrad(dy, w):
+    """Data gradient of a 3x3 'same' conv: dX[q] = sum_tap dY[q - tap + 1] W[tap]^T
+    (shifted-tap GEMMs on the padded dY, fp32)."""
+    N, H, W, Co = dy.shape
+    dyp = F.pad(dy, (0, 0, 1, 1, 1, 1))
+    out = torch.zeros(N * H * W, w.shape[2], device=dy.device)
+    for dh in range(3):
+        for dw in range(3):
+            out += dyp[:, 2 - dh:2 - dh + H, 2 - dw:2 - dw + W, :].reshape(-1, Co) @ w[dh, dw].t()
+    return out.reshape(N, H, W, -1)
+
+
+def test_bench_shape_data_gradients(stepped):
+    """Data gradients at the bench shape (first NS images; a conv's data gradient is per
+    image): conv1b's (the fused data + weight gradient, conv_dw.hip, in two batch halves),
+    conv5b's (8x8 image window), conv9b's (its dY formed on load from the head: conv_dw
+    XF 4) and conv9a's skip half (deferred, with the max-pool backward of pool1 routed in
+    its epilogue)."""
+    spec, fn, e = stepped
+    b = e.bufs
+    kern = lambda n: fn.view(fn.master, n + "/kernel").bfloat16().float()
+    # conv1b -> d:conv1a, conv5b -> d:conv5a: masked by the source activation
+    for lname, src in (("conv1b", "conv1a"), ("conv5b", "conv5a")):
+        ref = _dgrad(b["d:" + lname][:NS].float(), kern(lname)) * (b[src][:NS].float() > 0)
+        err = _rel(b["d:" + src][:NS].float(), ref)
+        assert err < 2e-2, (lname, err)
+    # conv9b: dY = dlogit w (y > 0) from the head's probability / target / loss sums
+    P = e.npix(1)
+    pr = e.prob.view(e.B, -1)[:NS].float()
+    t = e.target.view(e.B, -1)[:NS].float()
+    I, St, Sp = [v.item() for v in e.sums[:3]]
+    dl = (-2.0 * t / (2 * I + 1) + 1.0 / (St + Sp + 1)) * pr * (1 - pr) + e.bce_weight * (pr - t) / P
+    hw = fn.view(fn.master, "Mask/kernel").float().reshape(-1)
+    y9b = b["conv9b"][:NS].float()
+    dy9b = dl.reshape(NS, 128, 128, 1) * hw * (y9b > 0)
+    ref = _dgrad(dy9b, kern("conv9b")) * (b["conv9a"][:NS].float() > 0)
+    err = _rel(b["d:conv9a"][:NS].float(), ref)
+    assert err < 2e-2, ("conv9b", err)
+    # conv9a skip half: masked skip gradient + pool1's gradient routed to its first argmax
+    w9a = kern("conv9a")
+    cu = w9a.shape[2] - b["conv1b"].shape[-1]
+    skip_g = _dgrad(b["d:conv9a"][:NS].float(), w9a[:, :, cu:, :])
+    y1b = b["conv1b"][:NS].float()
+    win = y1b.reshape(NS, 64, 2, 64, 2, 32).permute(0, 1, 3, 5, 2, 4).reshape(NS, 64, 64, 32, 4)
+    mx, am = win.max(-1)
+    route = torch.zeros_like(win)
+    route.scatter_(-1, am.unsqueeze(-1), (b["d:pool1"][:NS].float() * (mx > 0)).unsqueeze(-1))
+    route = route.reshape(NS, 64, 64, 32, 2, 2).permute(0, 1, 4, 2, 5, 3).reshape(NS, 128, 128, 32)
+    ref = skip_g * (y1b > 0) + route
+    err = _rel(b["d:conv1b"][:NS].float(), ref)
+    assert err < 2e-2, ("conv9a skip", err)

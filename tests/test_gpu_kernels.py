@@ -272,7 +272,7 @@ def test_conv3d_first_layer_window(cuda_dev, N, D, H, Cin, Co, tile):
 
 @pytest.mark.parametrize("N,H,Ci,Co,tile", [(2, 8, 64, 32, 0), (2, 8, 64, 32, 8), (3, 64, 64, 32, 0),
                                             (2, 32, 128, 64, 0), (5, 16, 256, 128, 0), (3, 8, 512, 256, 0),
-                                            (2, 128, 128, 64, 0), (1, 256, 64, 32, 0)])
+                                            (2, 128, 128, 64, 0), (1, 256, 64, 32, 0), (1, 512, 64, 32, 0)])
 def test_tconv_fwd_shuffle_and_dgrad(cuda_dev, N, H, Ci, Co, tile):
     """2x2 stride-2 transposed conv: window kernels (auto) and the implicit-GEMM path (tile 8)."""
     torch.manual_seed(4)

@@ -685,9 +685,12 @@ hipError_t launch_win_first(const ConvFwdParams& p, hipStream_t s) {
 //   256 coarse pixels x 32 input channels per workgroup; per 32-channel chunk of dy the
 //   2R fine rows are LDS-DMA'd once with even / odd columns de-interleaved, so the
 //   four taps' A fragments are 16 consecutive slots (conflict free) of the same image.
-template <int W, int EPI>
+// SEG (coarse rows wider than 128, the 512^2 model's transConv9: 256-wide): a window is a
+// 128-pixel segment of one coarse row, its fine tile two 256-pixel segments of fine rows.
+template <int W, int EPI, bool SEG = false>
 __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) {
   constexpr int BMc = 128, R = BMc / W;
+  static_assert(!SEG || W == 128, "segmented coarse rows: 128-pixel windows");
   constexpr int XI = BMc / 16, WI = 4 * 32 / 16;   // 1 KB DMA instructions per chunk
   constexpr int XB = XI * 1024, WB = WI * 1024;
   constexpr int EPIB = 4 * BMc * 64;                // fine staging: 64-byte pixel rows
@@ -701,12 +704,15 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = p.OH;
   const int rows_total = p.N * H;
-  const int Mc = rows_total * W;
+  const int Wc = SEG ? p.OW : W;                 // coarse row width
+  const int nseg = SEG ? p.OW / W : 1;
+  const int Mc = rows_total * Wc;
   const int cof = p.Cout >> 2;                   // fine output channels
   const int tiles_n = cof / 32;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
-  const int g0 = tm * R, m0 = g0 * W, n0 = tn * 32;
+  const int g0 = (tm / nseg) * R, seg = tm - (tm / nseg) * nseg;
+  const int m0 = g0 * Wc + seg * W, n0 = tn * 32;
   const int Cin = p.C1;
   constexpr int OOB = 0x7fffffff;
   const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc((void*)p.src1, (short)0, OOB, 0x00020000);
@@ -786,14 +792,15 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
     }
   }
   __syncthreads();
-  // coalesced phase: the window's 2R fine rows are contiguous in the output
-  const size_t fine0 = (size_t)(2 * g0) * (2 * W);
-  const size_t fine_total = (size_t)(2 * rows_total) * (2 * W);
+  // coalesced phase: the window's 2R fine rows (SEG: two 2W-pixel segments of fine rows
+  // 2 Wc wide) are contiguous runs of the output
+  const size_t fine_total = (size_t)(2 * rows_total) * (2 * Wc);
 #pragma unroll
   for (int it = 0; it < (4 * BMc * 4) / NTHR; ++it) {
     const int c = tid + it * NTHR;
     const int fp = c >> 2, q = c & 3;
-    const size_t gp = fine0 + fp;
+    const int frow = fp / (2 * W), fcol = fp - frow * (2 * W);
+    const size_t gp = (size_t)(2 * g0 + frow) * (2 * Wc) + 2 * seg * W + fcol;
     if (gp >= fine_total) continue;
     u32x4 v = *(const u32x4*)(E + tc_off(fp, q));
     if (tc_half(fp)) v = (u32x4){v[2], v[3], v[0], v[1]};
@@ -890,6 +897,11 @@ __global__ void __launch_bounds__(NTHR) tconv_dgrad_kernel(const ConvFwdParams p
 
 hipError_t launch_tconv_fwd(const ConvFwdParams& p, hipStream_t s) {
   const int W = p.OW;
+  if (W > 128) {
+    const int grid = p.N * p.OH * (W / 128) * ((p.Cout >> 2) / 32);
+    UNET_LAUNCH((tconv_fwd_kernel<128, 0, true>), dim3(grid), dim3(NTHR), 0, s, p);
+    return launch_status();
+  }
   const int R = 128 / W;
   const int grid = ((p.N * p.OH + R - 1) / R) * ((p.Cout >> 2) / 32);
   switch (W) {
@@ -966,7 +978,8 @@ static bool win_first_eligible(const ConvFwdParams& p) {
 // 2D transposed-conv forward (1x1 GEMM + 2x2 pixel shuffle) on coarse rows 8..128 wide
 // (128: a window is one coarse row).
 static bool tconv_fwd_eligible(const ConvFwdParams& p) {
-  const bool w_ok = p.OW == 8 || p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128;
+  const bool w_ok = p.OW == 8 || p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128 ||
+                    (p.OW % 128 == 0 && p.OW <= 8192);       // (wider: 128-pixel row segments)
   return p.shuffle == 2 && p.KD == 1 && p.KH == 1 && p.KW == 1 && p.OD == 1 && w_ok && p.IW == p.OW &&
          p.IH == p.OH && p.C2 == 0 && (p.C1 % 32) == 0 && ((p.Cout >> 2) % 32) == 0 && !p.relu &&
          p.drop_rate == 0.f && !p.mask1 && !p.stats && p.out_scale == 1.f &&
