@@ -137,12 +137,14 @@ def test_conv3d_first_layer_window_bounds(cuda_dev, N, D, H, Cin):
     _check(d, outs, ["src1", "wgt", "bias"])
 
 
-@pytest.mark.parametrize("xf,N,nsplit", [(0, 3, 7), (2, 3, 7), (3, 2, 5), (4, 3, 96), (0, 2, 512)])
-def test_conv_dw_bounds(cuda_dev, xf, N, nsplit):
+@pytest.mark.parametrize("xf,N,nsplit,W", [(0, 3, 7, 128), (2, 3, 7, 128), (3, 2, 5, 128), (4, 3, 96, 128),
+                                           (0, 2, 512, 128), (0, 1, 5, 512)])
+def test_conv_dw_bounds(cuda_dev, xf, N, nsplit, W):
     """The fused data + weight gradient: halo rows of the first / last image, the carried
-    halo rows of consecutive windows, the last workgroup's window range."""
+    halo rows of consecutive windows, the last workgroup's window range (W = 512: the
+    segmented rows' neighbour-segment halo columns)."""
     torch.manual_seed(6 + xf)
-    H = W = 128
+    H = 128 if W == 128 else 32
     dev = cuda_dev
     P = N * H * W
     x = F.relu(torch.randn(N, H, W, 32, device=dev)).bfloat16()

@@ -279,3 +279,36 @@ def test_fused_dgrad_wgrad_head_on_load(cuda_dev, N, nsplit, bce):
     assert torch.equal(dx1, dx0)
     assert torch.equal(s1, s0) and torch.equal(b1, b0)
     assert rel_err(s1.double().sum(0).float(), _ref_wgrad(x, dy, w).reshape(9, 32, 32)) < 1e-4
+
+
+@pytest.mark.parametrize("N,W,nsplit", [(2, 256, 9), (1, 512, 64)])
+def test_fused_dgrad_wgrad_segmented_rows(cuda_dev, N, W, nsplit):
+    """Rows wider than 128 (the 512^2 model) as 128-pixel segments walked segment-major
+    (halo columns -1 / 128 from the neighbour segments, the halo-row carry within a
+    segment): dX equals the split row-window data gradient, the slabs the fp32 weight /
+    bias gradients."""
+    torch.manual_seed(W + N)
+    H = 64
+    dev = cuda_dev
+    dy = torch.randn(N, H, W, 32, device=dev).bfloat16()
+    x = F.relu(torch.randn(N, H, W, 32, device=dev)).bfloat16()
+    act = F.relu(torch.randn(N, H, W, 32, device=dev)).bfloat16()
+    w = (torch.randn(3, 3, 32, 32, device=dev) * 0.1).bfloat16()
+    wp = pack_dgrad(w)
+    v = (act.float() > 0).reshape(-1, 8).to(torch.int32)
+    bits = (v << torch.arange(8, device=dev, dtype=torch.int32)).sum(1).to(torch.uint8)
+    base = dict(N=N, OH=H, OW=W, IH=H, IW=W, KH=3, KW=3, pad=1, C1=32, src1=ptr(dy), wgt=ptr(wp), Cout=32, relu=0,
+                mask1=ptr(bits), mask_bits=1)
+    ref_dx = torch.empty(N, H, W, 32, device=dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(base, dst1=ptr(ref_dx)), stream())
+    dx = torch.full_like(ref_dx, 7.0)
+    slab = torch.full((nsplit, 9, 32, 32), float("nan"), device=dev)
+    bslab = torch.full((nsplit, 32), float("nan"), device=dev)
+    d = dict(base, dst1=ptr(dx), fw_x=ptr(x), fw_slab=ptr(slab), fw_bias_slab=ptr(bslab), fw_Cx=32,
+             fw_nsplit=nsplit)
+    assert C().conv_fwd_grid(d) == nsplit
+    C().conv_fwd(d, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx, ref_dx)
+    assert rel_err(slab.double().sum(0).float(), _ref_wgrad(x, dy, w).reshape(9, 32, 32)) < 1e-4
+    assert rel_err(bslab.double().sum(0).float(), dy.float().sum((0, 1, 2))) < 1e-4

@@ -92,7 +92,11 @@ __device__ __forceinline__ void dw_dlogit(const ConvFwdParams& p, const float (&
   }
 }
 
-template <int EPI, int XF>
+// SEG: rows of Wf = p.OW > 128 pixels (the 512^2 model) as 128-pixel segments; windows are
+// walked segment-major (segment s = window / (rows / R)), so consecutive windows of a
+// workgroup are consecutive row pairs of one segment and the halo-row carry still holds;
+// the halo columns -1 / 128 are the neighbouring segments' pixels (zeros at the row ends).
+template <int EPI, int XF, bool SEG = false>
 __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams p) {
   static_assert(XF == 0 || XF == 2 || XF == 3 || XF == 4,
                 "plain dY, norm backward on load (of the normalised head), head gradient on load");
@@ -106,8 +110,10 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = p.OH;
   const int rows_total = p.N * H;
-  const int M = rows_total * W;
-  const int nwin = rows_total / R;
+  const int Wf = SEG ? p.OW : W;                       // row width (SEG: > 128)
+  const int M = rows_total * Wf;
+  const int nrp = rows_total / R;                      // row pairs per segment
+  const int nwin = nrp * (SEG ? Wf / W : 1);
   const int split = blockIdx.x;
   const int w_begin = (int)((long long)split * nwin / p.fw.nsplit);
   const int w_end = (int)((long long)(split + 1) * nwin / p.fw.nsplit);
@@ -203,18 +209,20 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
   int fl = 0;
 
   for (int win = w_begin; win < w_end; ++win) {
-    const int g0 = win * R;
+    const int seg = SEG ? win / nrp : 0;
+    const int col0 = seg * W;                          // the window's first column
+    const int g0 = (SEG ? win - seg * nrp : win) * R;
     const int grow0 = (g0 / H) * H;                    // the window's image (H % R == 0)
     const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
     const bool carry = win > w_begin && top_in;       // (wave-uniform)
     if (carry) fl ^= 1;
     const int fo = fl * 2 * ROWB;                       // physical offset of logical rows 0, 1 (rows 2, 3: -fo)
     const int k0 = carry ? 2 * DW_HWP * 4 : 0;          // first halo granule to form
-    const size_t img_px = (size_t)grow0 * W;
+    const size_t img_px = (size_t)grow0 * Wf;
     const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((const char*)p.src1 + img_px * C * 2), (short)0, OOB, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((const char*)p.fw.x + (size_t)g0 * W * Cx * 2), (short)0, OOB, 0x00020000);
+        (void*)((const char*)p.fw.x + ((size_t)g0 * Wf + col0) * Cx * 2), (short)0, OOB, 0x00020000);
     // XF 2: the z granules of the halo (and the coefficients) are loaded into registers
     // before the barrier, so they fly while the previous window's epilogue stores drain; g
     // arrives through the dY halo DMA below and is turned into dz in place.  XF 3: the
@@ -250,18 +258,18 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
       for (int j = 0; j < DW_HJ; ++j) {
         const int k = k0 + tid + DW_NTHR * j;
         const int hr = k / (DW_HWP * 4), s = (k >> 2) - hr * DW_HWP;
-        const int gr = g0 - 1 + hr, col = s - 1;
+        const int gr = g0 - 1 + hr, col = col0 + s - 1;
         const bool ok = k < DW_HG && (hr > 0 || top_in) && (hr < R + 1 || bot_in) &&
-                        (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+                        (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)Wf && s <= W + 1;
         okm |= (ok ? 1u : 0u) << j;
         if constexpr (XF >= 3) {
-          const int pix = ok ? gr * W + col : 0;
+          const int pix = ok ? gr * Wf + col : 0;
           pr[j] = p.hg.prob[pix];
           tv[j] = bits2f(((const uint16_t*)p.hg.t)[pix]);
           if constexpr (XF == 4) hbits[j] = ok ? ((const uint8_t*)p.hg.bits)[(size_t)pix * 4 + (tid & 3)] : 0u;
         }
         if constexpr (XF == 2)
-          zv[j] = __builtin_amdgcn_raw_buffer_load_b128(rsz, ok ? ((gr - grow0) * W + col) * C * 2 + kch * 2 : OOB,
+          zv[j] = __builtin_amdgcn_raw_buffer_load_b128(rsz, ok ? ((gr - grow0) * Wf + col) * C * 2 + kch * 2 : OOB,
                                                         0, 0);
       }
       if (tid < NK) Ks[tid] = kv;    // (the previous window read them before its MFMAs)
@@ -276,23 +284,28 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
       const int jlo = carry ? 5 * (wave & 1) : 0, jhi = carry && !(wave & 1) ? 5 : DW_PPR;
       const int gr = g0 - 1 + hr;
       const bool row_ok = (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)gr < (unsigned)rows_total;
-      const int rowoff = (gr - grow0) * W * C * 2;
+      const int rowoff = ((gr - grow0) * Wf + col0) * C * 2;
       char* hdst = Xs + (hr ^ (2 * fl)) * ROWB;
 #pragma unroll
       for (int j = 0; j < DW_PPR; ++j) {
         if (j < jlo || j >= jhi) continue;
-        const bool ok = row_ok && (j > 0 || lslot > 0) && (16 * j + lslot - 1 < W);
+        // (SEG: slot 16 j + lslot = column col0 + 16 j + lslot - 1, the neighbour segments'
+        // pixels at slots 0 / 129; slots past 129 are never read)
+        const bool ok = row_ok && (unsigned)(col0 + 16 * j + lslot - 1) < (unsigned)Wf && 16 * j + lslot <= W + 1;
         const int off = ok ? rowoff + dma_lane + j * 1024 : OOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs1, (__attribute__((address_space(3))) void*)(hdst + j * 1024),
                                                  16, off, 0, 0, 0);
       }
     }
-    // x image: slot y * W + col = pixel (g0 + y, col), the same swizzle; wave w fills slots
-    // 64 w .. 64 w + 63
+    // x image: slot y * W + col = pixel (g0 + y, col0 + col), the same swizzle; wave w fills
+    // slots 64 w .. 64 w + 63 (row w >> 1: SEG rows are Wf apart)
 #pragma unroll
-    for (int i = 0; i < DW_AI / 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsx, (__attribute__((address_space(3))) void*)(As + (4 * wave + i) * 1024),
-                                               16, xdma_lane + (4 * wave + i) * 1024, 0, 0, 0);
+    for (int i = 0; i < DW_AI / 4; ++i) {
+      const int k = 4 * wave + i;
+      const int xo = SEG ? ((k >> 3) * Wf + 16 * (k & 7)) * Cx * 2 : k * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsx, (__attribute__((address_space(3))) void*)(As + k * 1024), 16,
+                                               xdma_lane + xo, 0, 0, 0);
+    }
     __syncthreads();
     // (the per-pixel logit gradients: formed here, after the barrier, so the probability /
     // target loads overlap the x image DMA instead of being waited on before it)
@@ -421,8 +434,12 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
     }
     __syncthreads();      // every wave is done reading the halo image (the staging tile aliases rows 0, 1)
     using Map = StripTiles<W, RW, TC, NCS>;
-    conv_epilogue<DW_BM, BN, DW_BM / 4, BN, TM, TN, DW_NTHR, EPI, Map, 0, W>(p, acc, Xs + fo, g0 * W, 0, M, wave, 0,
-                                                                            lane, tid, 0, 0, win);
+    if constexpr (SEG)
+      conv_epilogue<DW_BM, BN, DW_BM / 4, BN, TM, TN, DW_NTHR, EPI, Map, W, W>(p, acc, Xs + fo, g0, 0, M, wave, 0,
+                                                                              lane, tid, Wf, col0, win);
+    else
+      conv_epilogue<DW_BM, BN, DW_BM / 4, BN, TM, TN, DW_NTHR, EPI, Map, 0, W>(p, acc, Xs + fo, g0 * W, 0, M, wave, 0,
+                                                                              lane, tid, 0, 0, win);
   }
 
   // ---- sum the partials of the two waves of each dY channel block (waves jw, jw + 2:
@@ -463,7 +480,8 @@ __global__ void __launch_bounds__(DW_NTHR, 2) conv_dw_kernel(const ConvFwdParams
 const char* conv_dw_check(const ConvFwdParams& p) {
   if (!p.fw.x) return nullptr;
   const int ep = conv_epi_mode(p);
-  if (p.OW != DW_W || p.IW != DW_W || p.OH != p.IH || p.OH % DW_R || p.KD != 1 || p.OD != 1 || p.ID != 1 ||
+  const bool w_ok = p.OW == DW_W || (p.OW % DW_W == 0 && p.OW <= 8192);
+  if (!w_ok || p.IW != p.OW || p.OH != p.IH || p.OH % DW_R || p.KD != 1 || p.OD != 1 || p.ID != 1 ||
       p.KH != 3 || p.KW != 3 || p.stride != 1 || p.pad != 1 || p.C1 != 32 || p.C2 || p.Cout != DW_BN ||
       p.D1 != p.Cout || p.fw.Cx != 32 || (ep != EPI_DGRAD && ep != EPI_DGRAD_NORM) || p.s2d ||
       p.ut.x || p.pool_dst || p.head_w || p.rev)
@@ -479,6 +497,8 @@ const char* conv_dw_check(const ConvFwdParams& p) {
   if (!p.fw.slab || !p.fw.bias_slab || p.fw.nsplit < 1 || p.fw.split_lo < 0)
     return "conv_fwd: fused weight gradient needs slab / bias_slab and nsplit >= 1";
   if ((long long)p.OH * p.OW * 32 * 2 >= (1LL << 31) - 64) return "conv_fwd: one image exceeds 2 GiB";
+  if (p.OW > DW_W && (p.xform || p.hg.prob || p.nz))
+    return "conv_fwd: fused weight gradient on segmented rows: plain dY source, EPI_DGRAD only";
   return nullptr;
 }
 
@@ -490,7 +510,10 @@ int conv_dw_stat_rows(const ConvFwdParams& p) { return p.N * p.OH / DW_R; }
 hipError_t launch_conv_dw(const ConvFwdParams& p, hipStream_t s) {
   const int ep = conv_epi_mode(p);
   const dim3 grid(p.fw.nsplit), blk(DW_NTHR);
-  if (ep == EPI_DGRAD && !p.xform && !p.hg.prob)
+  if (p.OW > DW_W) {
+    if (ep != EPI_DGRAD || p.xform || p.hg.prob) return hipErrorInvalidValue;
+    UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD, 0, true>), grid, blk, 0, s, p);
+  } else if (ep == EPI_DGRAD && !p.xform && !p.hg.prob)
     UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD, 0>), grid, blk, 0, s, p);
   else if (ep == EPI_DGRAD && !p.xform)
     UNET_LAUNCH((conv_dw_kernel<EPI_DGRAD, 4>), grid, blk, 0, s, p);

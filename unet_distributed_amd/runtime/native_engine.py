@@ -134,8 +134,9 @@ FUSIONS: Dict[str, Fusion] = {
     "tail_halves": Fusion("last data gradient in two batch halves (first-layer wgrad overlap)",
                           norm={"none"}, dims={2}, img=_ROW_IMGS, even_batch=True, cpad=(4, 8),
                           when=lambda e: e.wgrad_win >= 0),
-    "dw_fused": Fusion("data + weight gradient from one staged dY halo (conv_dw.hip)", dims={2},
-                       img=(128,), option="dw_fuse", when=lambda e: e.wgrad_win >= 0),
+    "dw_fused": Fusion("data + weight gradient from one staged dY halo (conv_dw.hip; 128-pixel segments of "
+                       "wider rows)", dims={2}, img=(128, 256, 512, 1024), option="dw_fuse",
+                       when=lambda e: e.wgrad_win >= 0),
     "dz_onload": Fusion("norm backward dz = ca g + cb z + cc formed in the fused data + weight gradient's "
                         "halo (conv_dw.hip XF 2): no norm_bwd_apply pass, dz never stored",
                         norm={"batch", "group"}, dims={2}, img=(128,), option="dw_fuse", needs=("dw_fused",)),
