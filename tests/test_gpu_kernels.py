@@ -1068,3 +1068,22 @@ def test_conv_img8_norm_statistics(cuda_dev):
     zf = z0.float().reshape(-1, Co)
     assert rel_err(s0[0], zf.sum(0)) < 1e-3 and rel_err(s0[1], (zf * zf).sum(0)) < 1e-3
 
+
+
+@pytest.mark.parametrize("N,D,Ci,Co,tile", [(2, 16, 64, 32, 0), (1, 32, 128, 64, 0), (1, 64, 64, 32, 0),
+                                           (2, 16, 64, 32, 8), (1, 8, 256, 128, 0)])
+def test_tconv3d_fwd_window(cuda_dev, N, D, Ci, Co, tile):
+    """2x2x2 stride-2 transposed conv forward (3D model): the transposed-conv window kernel
+    (eight taps, two per wave; coarse rows 16..128 wide) against fp32 ATen, and equal to the
+    implicit-GEMM shuffle path (tile 8) within rounding."""
+    torch.manual_seed(D + Ci)
+    x = F.relu(torch.randn(N, D, D, D, Ci, device=cuda_dev)).bfloat16()
+    k = (torch.randn(2, 2, 2, Co, Ci, device=cuda_dev) * 0.1).bfloat16()   # (kd, kh, kw, Cout, Cin)
+    b = torch.randn(Co, device=cuda_dev)
+    out = torch.empty(N, 2 * D, 2 * D, 2 * D, Co, device=cuda_dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(N=N, OD=D, OH=D, OW=D, ID=D, IH=D, IW=D, C1=Ci, src1=ptr(x),
+                      wgt=ptr(pad64(k.reshape(8 * Co, Ci))), bias=ptr(b), Cout=8 * Co, shuffle=3, dst1=ptr(out),
+                      tile=tile), stream())
+    wt = k.float().permute(4, 3, 0, 1, 2)     # (Cin, Cout, kd, kh, kw)
+    ref = ndhwc(F.conv_transpose3d(ncdhw(x.float()), wt, b, stride=2))
+    assert rel_err(out, ref) < 1e-2

@@ -687,11 +687,16 @@ hipError_t launch_win_first(const ConvFwdParams& p, hipStream_t s) {
 //   four taps' A fragments are 16 consecutive slots (conflict free) of the same image.
 // SEG (coarse rows wider than 128, the 512^2 model's transConv9: 256-wide): a window is a
 // 128-pixel segment of one coarse row, its fine tile two 256-pixel segments of fine rows.
-template <int W, int EPI, bool SEG = false>
+// D3 (2x2x2 stride-2, the 3D model): eight taps -- wave w computes taps w (td = 0) and
+// w + 4 (td = 1) from the same x image; a window's R coarse rows lie in one depth slice
+// (OH % R == 0), so per td its 2R fine rows are one contiguous run of fine slice 2 sd + td.
+template <int W, int EPI, bool SEG = false, bool D3 = false>
 __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) {
   constexpr int BMc = 128, R = BMc / W;
   static_assert(!SEG || W == 128, "segmented coarse rows: 128-pixel windows");
-  constexpr int XI = BMc / 16, WI = 4 * 32 / 16;   // 1 KB DMA instructions per chunk
+  static_assert(!(SEG && D3), "3D: rows <= 128 wide");
+  constexpr int NTD = D3 ? 2 : 1;                  // depth taps
+  constexpr int XI = BMc / 16, WI = 4 * NTD * 32 / 16;   // 1 KB DMA instructions per chunk
   constexpr int XB = XI * 1024, WB = WI * 1024;
   constexpr int EPIB = 4 * BMc * 64;                // fine staging: 64-byte pixel rows
   constexpr int LDS_BYTES = (XB + WB > EPIB) ? XB + WB : EPIB;
@@ -703,11 +708,11 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = p.OH;
-  const int rows_total = p.N * H;
+  const int rows_total = p.N * (D3 ? p.OD : 1) * H;    // coarse rows (n, d, h)
   const int Wc = SEG ? p.OW : W;                 // coarse row width
   const int nseg = SEG ? p.OW / W : 1;
   const int Mc = rows_total * Wc;
-  const int cof = p.Cout >> 2;                   // fine output channels
+  const int cof = p.Cout >> (D3 ? 3 : 2);        // fine output channels
   const int tiles_n = cof / 32;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = bid / tiles_n, tn = bid - tm * tiles_n;
@@ -722,9 +727,11 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
   const int fsub = lane >> 4, fr = lane & 15;
   const int fbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
 
-  f32x4 acc[TM][TN];
+  f32x4 acc[NTD][TM][TN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) acc[i][0] = acc[i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int td = 0; td < NTD; ++td)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[td][i][0] = acc[td][i][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   for (int kc = 0; kc < (Cin >> 5); ++kc) {
     if (kc) __syncthreads();
@@ -750,18 +757,21 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
       }
     }
     __syncthreads();
-    h16x8 wf[TN];
+    h16x8 wf[NTD][TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) wf[j] = *(const h16x8*)(Ws + (wave * 32 + 16 * j) * 64 + fbase);
+    for (int td = 0; td < NTD; ++td)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) wf[td][j] = *(const h16x8*)(Ws + ((wave + 4 * td) * 32 + 16 * j) * 64 + fbase);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const h16x8 xf = *(const h16x8*)(Xs + (16 * i) * 64 + fbase);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(wf[j], xf, acc[i][j]);
+      for (int td = 0; td < NTD; ++td)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[td][i][j] = mfma16(wf[td][j], xf, acc[td][i][j]);
     }
   }
-  __syncthreads();
-  // register phase: acc[i][j][r] = out(coarse px 16i + (lane&15), tap = wave)[co = 16j + 4(lane>>4) + r]
+  // register phase: acc[td][i][j][r] = out(coarse px 16i + (lane&15), tap = (td, wave))[co = 16j + 4(lane>>4) + r]
   // Staging: fine pixel fp in 64-byte row fp ^ ((fp >> 1) & 1), 16-byte chunk c at
   // c ^ ((fp >> 2) & 3), its 8-byte halves swapped when ((fp >> 4) ^ (fp >> 5)) & 1.  A
   // register-phase store group (16 lanes, fine pixels 2 apart: fp bits 1-4 = the lane, bit 0
@@ -774,37 +784,43 @@ __global__ void __launch_bounds__(NTHR) tconv_fwd_kernel(const ConvFwdParams p) 
   auto tc_off = [](const int fp, const int c) { return (fp ^ ((fp >> 1) & 1)) * 64 + 16 * (c ^ ((fp >> 2) & 3)); };
   auto tc_half = [](const int fp) { return ((fp >> 4) ^ (fp >> 5)) & 1; };
   const int th = wave >> 1, tw = wave & 1;
+  const size_t fine_total = (size_t)(2 * rows_total) * (2 * Wc) * (D3 ? 2 : 1);
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int nl = 16 * j + 4 * (lane >> 4);
-    float bs[4];
+  for (int td = 0; td < NTD; ++td) {
+    __syncthreads();        // (td 0: the MFMAs' LDS reads; td 1: the previous tile's stores)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bs[r] = p.bias ? p.bias[n0 + nl + r] : 0.f;
+    for (int j = 0; j < TN; ++j) {
+      const int nl = 16 * j + 4 * (lane >> 4);
+      float bs[4];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int pl = 16 * i + (lane & 15);
-      const int rr = pl / W, w = pl - rr * W;
-      const int fp = (2 * rr + th) * (2 * W) + 2 * w + tw;
-      u32x2 pk;
-      pk[0] = pack2h(acc[i][j][0] + bs[0], acc[i][j][1] + bs[1]);
-      pk[1] = pack2h(acc[i][j][2] + bs[2], acc[i][j][3] + bs[3]);
-      *(u32x2*)(E + tc_off(fp, nl >> 3) + 8 * (((nl >> 2) & 1) ^ tc_half(fp))) = pk;
+      for (int r = 0; r < 4; ++r) bs[r] = p.bias ? p.bias[n0 + nl + r] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int pl = 16 * i + (lane & 15);
+        const int rr = pl / W, w = pl - rr * W;
+        const int fp = (2 * rr + th) * (2 * W) + 2 * w + tw;
+        u32x2 pk;
+        pk[0] = pack2h(acc[td][i][j][0] + bs[0], acc[td][i][j][1] + bs[1]);
+        pk[1] = pack2h(acc[td][i][j][2] + bs[2], acc[td][i][j][3] + bs[3]);
+        *(u32x2*)(E + tc_off(fp, nl >> 3) + 8 * (((nl >> 2) & 1) ^ tc_half(fp))) = pk;
+      }
     }
-  }
-  __syncthreads();
-  // coalesced phase: the window's 2R fine rows (SEG: two 2W-pixel segments of fine rows
-  // 2 Wc wide) are contiguous runs of the output
-  const size_t fine_total = (size_t)(2 * rows_total) * (2 * Wc);
+    __syncthreads();
+    // coalesced phase: the window's 2R fine rows (SEG: two 2W-pixel segments of fine rows
+    // 2 Wc wide; D3: rows of fine slice 2 sd + td) are contiguous runs of the output
+    const int sd = D3 ? g0 / H : 0, h0 = D3 ? g0 - sd * H : 0;
+    const size_t frow0 = D3 ? (size_t)(2 * sd + td) * (2 * H) + 2 * h0 : (size_t)(2 * g0);
 #pragma unroll
-  for (int it = 0; it < (4 * BMc * 4) / NTHR; ++it) {
-    const int c = tid + it * NTHR;
-    const int fp = c >> 2, q = c & 3;
-    const int frow = fp / (2 * W), fcol = fp - frow * (2 * W);
-    const size_t gp = (size_t)(2 * g0 + frow) * (2 * Wc) + 2 * seg * W + fcol;
-    if (gp >= fine_total) continue;
-    u32x4 v = *(const u32x4*)(E + tc_off(fp, q));
-    if (tc_half(fp)) v = (u32x4){v[2], v[3], v[0], v[1]};
-    *(u32x4*)((h16*)p.dst1 + gp * cof + n0 + q * 8) = v;
+    for (int it = 0; it < (4 * BMc * 4) / NTHR; ++it) {
+      const int c = tid + it * NTHR;
+      const int fp = c >> 2, q = c & 3;
+      const int frow = fp / (2 * W), fcol = fp - frow * (2 * W);
+      const size_t gp = (frow0 + frow) * (2 * Wc) + 2 * seg * W + fcol;
+      if (gp >= fine_total) continue;
+      u32x4 v = *(const u32x4*)(E + tc_off(fp, q));
+      if (tc_half(fp)) v = (u32x4){v[2], v[3], v[0], v[1]};
+      *(u32x4*)((h16*)p.dst1 + gp * cof + n0 + q * 8) = v;
+    }
   }
 }
 
@@ -897,6 +913,17 @@ __global__ void __launch_bounds__(NTHR) tconv_dgrad_kernel(const ConvFwdParams p
 
 hipError_t launch_tconv_fwd(const ConvFwdParams& p, hipStream_t s) {
   const int W = p.OW;
+  if (p.shuffle == 3) {
+    const int grid = (p.N * p.OD * p.OH / (128 / W)) * ((p.Cout >> 3) / 32);
+    switch (W) {
+      case 16: UNET_LAUNCH((tconv_fwd_kernel<16, 0, false, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      case 32: UNET_LAUNCH((tconv_fwd_kernel<32, 0, false, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      case 64: UNET_LAUNCH((tconv_fwd_kernel<64, 0, false, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      case 128: UNET_LAUNCH((tconv_fwd_kernel<128, 0, false, true>), dim3(grid), dim3(NTHR), 0, s, p); break;
+      default: return hipErrorInvalidValue;
+    }
+    return launch_status();
+  }
   if (W > 128) {
     const int grid = p.N * p.OH * (W / 128) * ((p.Cout >> 2) / 32);
     UNET_LAUNCH((tconv_fwd_kernel<128, 0, true>), dim3(grid), dim3(NTHR), 0, s, p);
@@ -980,6 +1007,12 @@ static bool win_first_eligible(const ConvFwdParams& p) {
 static bool tconv_fwd_eligible(const ConvFwdParams& p) {
   const bool w_ok = p.OW == 8 || p.OW == 16 || p.OW == 32 || p.OW == 64 || p.OW == 128 ||
                     (p.OW % 128 == 0 && p.OW <= 8192);       // (wider: 128-pixel row segments)
+  // 3D (2x2x2): rows 16..128 wide, a window's 128 / W coarse rows inside one depth slice
+  if (p.shuffle == 3)
+    return p.KD == 1 && p.KH == 1 && p.KW == 1 && p.OD == p.ID && p.OD > 1 && p.OW >= 16 && p.OW <= 128 && w_ok &&
+           p.OH % (128 / p.OW) == 0 && p.IW == p.OW && p.IH == p.OH && p.C2 == 0 && (p.C1 % 32) == 0 &&
+           ((p.Cout >> 3) % 32) == 0 && !p.relu && p.drop_rate == 0.f && !p.mask1 && !p.stats &&
+           p.out_scale == 1.f && (long long)p.N * p.ID * p.IH * p.IW * p.C1 * 2 < (1LL << 31) - 64;
   return p.shuffle == 2 && p.KD == 1 && p.KH == 1 && p.KW == 1 && p.OD == 1 && w_ok && p.IW == p.OW &&
          p.IH == p.OH && p.C2 == 0 && (p.C1 % 32) == 0 && ((p.Cout >> 2) % 32) == 0 && !p.relu &&
          p.drop_rate == 0.f && !p.mask1 && !p.stats && p.out_scale == 1.f &&
