@@ -5,7 +5,7 @@ import sys
 
 src, out = sys.argv[1], sys.argv[2]
 rows = [json.loads(l) for l in open(src) if l.strip()]
-L = ["# Every BASELINE config on the round-5 tree (1x MI355X, `scripts/gpu_r5_configs.sh`)", "",
+L = ["# Every BASELINE config (1x MI355X, `scripts/gpu_r<N>_configs.sh`)", "",
      "One `bench.py` line per config (full training step: forward, loss, backward, TF-Adam; synthetic data, "
      "random init). TF/s = img/s x the step's conv / transposed-conv FLOPs per image (`tools/config_flops.py`, "
      "3 x forward MACs x 2).", "",
