@@ -1087,3 +1087,33 @@ def test_tconv3d_fwd_window(cuda_dev, N, D, Ci, Co, tile):
     wt = k.float().permute(4, 3, 0, 1, 2)     # (Cin, Cout, kd, kh, kw)
     ref = ndhwc(F.conv_transpose3d(ncdhw(x.float()), wt, b, stride=2))
     assert rel_err(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,D,H,C1,C2,Cout,splits", [(1, 4, 32, 32, 0, 32, 3), (2, 3, 64, 32, 32, 32, 5),
+                                                      (1, 3, 128, 32, 0, 32, 4), (1, 4, 128, 32, 32, 64, 7),
+                                                      (3, 1, 128, 32, 0, 32, 5), (2, 1, 64, 64, 0, 32, 3),
+                                                      (2, 1, 32, 32, 32, 64, 4), (1, 1, 256, 32, 0, 32, 6)])
+def test_wgrad_window_wave_pair(cuda_dev, N, D, H, C1, C2, Cout, splits):
+    """Wave-pair partials (pair=1: each wave one 16-channel half of its 32-channel output
+    block, three workgroups per CU) against the fp32 reference: 3D (D > 1) and 2D rows,
+    concat sources, segmented 256-wide rows."""
+    torch.manual_seed(N + D + H + C1 + C2 + 11)
+    d3 = D > 1
+    shp = (N, D, H, H) if d3 else (N, H, H)
+    a = F.relu(torch.randn(*shp, C1, device=cuda_dev)).bfloat16()
+    b2 = F.relu(torch.randn(*shp, max(C2, 1), device=cuda_dev)).bfloat16()
+    dy = torch.randn(*shp, Cout, device=cuda_dev).bfloat16()
+    Mt = C1 + C2
+    T = 27 if d3 else 9
+    d = dict(N=N, QD=D, QH=H, QW=H, AD=D, AH=H, AW=H, KD=3 if d3 else 1, KH=3, KW=3, pad=1, M1=C1, M2=C2,
+             a1=ptr(a), a2=ptr(b2) if C2 else None, b=ptr(dy), Nc=Cout, bias_mode=1, pair=1)
+    gw, gb = _wgrad(d, splits, T, Mt, Mt, Cout, T * Mt * Cout, bias_w=(splits, Cout))
+    conv, to_nc = (F.conv3d, ncdhw) if d3 else (F.conv2d, nchw)
+    inp = to_nc(a.float()) if not C2 else torch.cat([to_nc(a.float()), to_nc(b2.float())], 1)
+    ks = (3, 3, 3) if d3 else (3, 3)
+    w = torch.zeros(Cout, Mt, *ks, device=cuda_dev, requires_grad=True)
+    bb = torch.zeros(Cout, device=cuda_dev, requires_grad=True)
+    gwr, gbr = torch.autograd.grad(conv(inp, w, bb, padding=1), [w, bb], to_nc(dy.float()))
+    perm = (2, 3, 4, 1, 0) if d3 else (2, 3, 1, 0)
+    assert rel_err(gw, gwr.permute(*perm).reshape(-1)) < 2e-3
+    assert rel_err(gb, gbr) < 2e-3

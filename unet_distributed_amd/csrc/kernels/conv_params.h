@@ -207,6 +207,8 @@ struct WgradParams {
   const void* xz;
   HeadGrad hg;                // window wgrad of the head input conv: the B operand (dY, 32 channels)
                               // formed on load, see HeadGrad
+  int pair;                   // window wgrad, 32-channel output blocks on column-unit rows: wave-pair
+                              // partials (conv_wgrad.hip wgrad_win_kernel PAIR, three workgroups per CU)
   // filled by the launcher
   int lqw, lqh, lqd;          // log2 of the pixel grid (power-of-two fast path)
   signed char tap_d[27], tap_h[27], tap_w[27];

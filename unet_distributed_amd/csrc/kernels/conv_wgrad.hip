@@ -517,8 +517,12 @@ enum { WGEO_2D = 0, WGEO_SEG = 1, WGEO_3D = 2 };
 // HG: head-on-load (conv_params.h HeadGrad): the B operand (dY of the head input, 32
 // channels, 2D full rows) is formed per window from the head's per-pixel probability,
 // target and ReLU bits instead of being read from memory.
-template <int W, int QO, bool CONCAT, int GEO, bool HG = false>
-__global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p) {
+// PAIR (round 6, column-unit path): wave w owns the 16-channel half jh = w & 1 of its
+// 32-channel output block, so its dW partial is 9 x 32 x 16 (72 registers instead of 144)
+// and the kernel fits three workgroups per CU (the 3D level-1 weight gradients were half
+// waits at two); the pixel splits halve and each x fragment feeds two waves.
+template <int W, int QO, bool CONCAT, int GEO, bool HG = false, bool PAIR = false>
+__global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const WgradParams p) {
   constexpr int BMW = 256, R = BMW / W, HR = R + 2;
   constexpr int HWP = ((W + 2 + 15) / 16) * 16, IPR = HWP / 16, ROWB = HWP * 64;
   constexpr int XI = HR * IPR, YI = QO * BMW / 16;
@@ -528,12 +532,16 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   constexpr int LDS_BYTES = (XB + YB > REDB) ? XB + YB : REDB;
   static_assert(W >= 8 && W <= 128 && (QO == 1 || QO == 2), "window wgrad shape");
   static_assert(!HG || (QO == 1 && !CONCAT && GEO == WGEO_2D && BMW == NTHR), "head-on-load B: one 32-channel image");
+  static_assert(!PAIR || (W >= 32 && !HG), "wave-pair partials: column-unit path");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   char* Xs = smem;
   char* Ys = smem + XB;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int qo = wave % QO, ps = wave / QO;
+  // PAIR: wave = (ps, qo, jh) from the top bit down; pixel splits PSP = 2 / QO
+  constexpr int PSP = PAIR ? 2 / QO : PS;
+  const int jh = PAIR ? wave & 1 : 0;
+  const int qo = PAIR ? (wave >> 1) % QO : wave % QO, ps = PAIR ? (wave >> 1) / QO : wave / QO;
   // Row space g = (n, d, h), rows of Wf pixels cut into nseg W-wide segments (Wf > 128);
   // a window is R rows x one segment.  3D: tap group kd (grid dimension) computes the
   // nine (dh, dw) taps of depth tap kd from the halo rows of slice d + kd - 1.
@@ -571,14 +579,17 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   const bool do_bias = p.bias_mode == 1 && ci_blk == 0 && kd == (KD >> 1);
   const int gsh = (kd - (KD >> 1)) * H;
 
-  f32x4 acc[9][2][2];
+  constexpr int NJ = PAIR ? 1 : 2;                      // 16-channel output halves per wave
+  f32x4 acc[9][2][NJ];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  f32x4 bacc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+      for (int j = 0; j < NJ; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 bacc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) bacc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const u32x4 ones_u = {kOnes2, kOnes2, kOnes2, kOnes2};
   const h16x8 ones = __builtin_bit_cast(h16x8, ones_u);
 
@@ -692,19 +703,19 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
       // and feeds the output rows hr - dh of all three vertical taps, so a unit reads
       // 3 (RWG + 2) A fragment pairs instead of 9 RWG.
       constexpr int NCOL = W / 32;
-      constexpr int RG = PS > NCOL ? PS / NCOL : 1;
+      constexpr int RG = PSP > NCOL ? PSP / NCOL : 1;
       constexpr int RWG = R / RG;
       constexpr int UNITS = NCOL * RG;
       static_assert(R % RG == 0 && RWG >= 1, "wgrad column units");
       const int lp = 8 * G + q;
 #pragma unroll 1
-      for (int u = ps; u < UNITS; u += PS) {
+      for (int u = ps; u < UNITS; u += PSP) {
         const int cu = u % NCOL, rr0 = (u / NCOL) * RWG;
         const int c0 = cu * 32;
         // Per-lane LDS byte bases (the swizzle depends only on lp + dw because c0 and
         // the row pitches are multiples of 32 slots): halo row hr and dY row y are
         // compile-time immediates on top of these 16 registers.
-        int ab[3][2][2], yb[2][2];
+        int ab[3][2][2], yb[NJ][2];
 #pragma unroll
         for (int dw = 0; dw < 3; ++dw)
 #pragma unroll
@@ -715,24 +726,24 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
               ab[dw][i][hh] = tr_addr(rr0 * HWP + col, col, 16 * i + 4 * pp);
             }
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
             const int sl = rr0 * W + c0 + lp + 4 * hh;
-            yb[j][hh] = tr_addr(sl, sl, 16 * j + 4 * pp);
+            yb[j][hh] = tr_addr(sl, sl, 16 * (PAIR ? jh : j) + 4 * pp);
           }
         // dY fragments of the unit's rows, loaded when first needed (halo row hr = y
         // feeds output row y through dh = 0) and live for three halo rows; pixels past
         // the tensor were DMA'd as zeros
-        h16x8 bf[RWG][2];
+        h16x8 bf[RWG][NJ];
 #pragma unroll
         for (int hr = 0; hr < RWG + 2; ++hr) {
           if (hr < RWG) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) bf[hr][j] = tr8(Yq + yb[j][0] + hr * W * 64, Yq + yb[j][1] + hr * W * 64);
+            for (int j = 0; j < NJ; ++j) bf[hr][j] = tr8(Yq + yb[j][0] + hr * W * 64, Yq + yb[j][1] + hr * W * 64);
             if (do_bias) {
 #pragma unroll
-              for (int j = 0; j < 2; ++j) bacc[j] = mfma16(ones, bf[hr][j], bacc[j]);
+              for (int j = 0; j < NJ; ++j) bacc[j] = mfma16(ones, bf[hr][j], bacc[j]);
             }
           }
 #pragma unroll
@@ -747,7 +758,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
 #pragma unroll
               for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) acc[3 * dh + dw][i][j] = mfma16(af[i], bf[y][j], acc[3 * dh + dw][i][j]);
+                for (int j = 0; j < NJ; ++j) acc[3 * dh + dw][i][j] = mfma16(af[i], bf[y][j], acc[3 * dh + dw][i][j]);
             }
           }
           // keep the scheduler from hoisting every row's fragment reads to the top
@@ -776,17 +787,17 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
             }
         // dY fragments of output pair k: loaded at hr = 2k (first use, dh = 0), last
         // used at hr = 2k + 2 (dh = 2) -- at most two pairs live
-        h16x8 bf[NP][2];
+        h16x8 bf[NP][NJ];
 #pragma unroll
         for (int hr = 0; hr <= 2 * NP; ++hr) {
           if (!(hr & 1) && hr < 2 * NP) {
             const int s0 = (y0 + hr) * W + lp, s1 = s0 + 4;
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < NJ; ++j)
               bf[hr >> 1][j] = tr8(Yq + tr_addr(s0, s0, 16 * j + 4 * pp), Yq + tr_addr(s1, s1, 16 * j + 4 * pp));
             if (do_bias) {
 #pragma unroll
-              for (int j = 0; j < 2; ++j) bacc[j] = mfma16(ones, bf[hr >> 1][j], bacc[j]);
+              for (int j = 0; j < NJ; ++j) bacc[j] = mfma16(ones, bf[hr >> 1][j], bacc[j]);
             }
           }
 #pragma unroll
@@ -801,7 +812,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
 #pragma unroll
               for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
+                for (int j = 0; j < NJ; ++j)
                   acc[3 * dh + dw][i][j] = mfma16(af[i], bf[y >> 1][j], acc[3 * dh + dw][i][j]);
             }
           }
@@ -818,15 +829,15 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
       if (g >= rows_total) break;
       const int h = g % H;
       // dY fragments (B operand: k = pixels, n = output channels)
-      h16x8 bf[2];
+      h16x8 bf[NJ];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const int s0 = px0 + 8 * G + q, s1 = s0 + 4;
         bf[j] = tr8(Yq + tr_addr(s0, s0, 16 * j + 4 * pp), Yq + tr_addr(s1, s1, 16 * j + 4 * pp));
       }
       if (do_bias) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bacc[j] = mfma16(ones, bf[j], bacc[j]);
+        for (int j = 0; j < NJ; ++j) bacc[j] = mfma16(ones, bf[j], bacc[j]);
       }
       // lane pixel 8G + q (+4 for the second transposed read): for rows narrower than
       // a 32-pixel step it lies lr rows below the step's first row, at column lc
@@ -847,7 +858,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
                           Xs + tr_addr(slotA + 4, colA + 4, 16 * i + 4 * pp, rowA));
           if (W < 32 && !lane_ok) af = __builtin_bit_cast(h16x8, (u32x4){0u, 0u, 0u, 0u});
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[t][i][j] = mfma16(af, bf[j], acc[t][i][j]);
+          for (int j = 0; j < NJ; ++j) acc[t][i][j] = mfma16(af, bf[j], acc[t][i][j]);
         }
       }
     }
@@ -856,28 +867,30 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   // ---- reduce the pixel-split partials (waves with the same qo) and write the slab
   // acc[t][i][j][r] = dW[t][ci0 + 16i + 4(lane>>4) + r][co0 + 32qo + 16j + (lane&15)]
   float* red = (float*)smem;
-  const int n_base = co0 + 32 * qo + (lane & 15);
+  const int n_base = co0 + 32 * qo + (lane & 15) + 16 * jh;
   const int m_base = ci0 + 4 * (lane >> 4);
-  auto reduce_store = [&](const f32x4 (&v4)[2][2], const int t) {
+  // (PAIR: the partner waves of (qo, jh) are ((o QO + qo) 2 + jh), o < PSP)
+  auto partner = [&](const int o) { return PAIR ? (o * QO + qo) * 2 + jh : qo + QO * o; };
+  auto reduce_store = [&](const f32x4 (&v4)[2][NJ], const int t) {
     __syncthreads();
     // red[fragment (i, j)][wave * 64 + lane]: consecutive lanes 16 bytes apart (a lane-major
     // [lane][4 fragments] layout puts the 8 lanes of a 16-byte store group 64 bytes apart,
     // two 64-byte positions per 128-byte bank window: 4-way conflicted stores and loads)
-    if (PS > 1 && ps > 0) {
+    if (PSP > 1 && ps > 0) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) *(f32x4*)(red + ((i * 2 + j) * NTHR + wave * 64 + lane) * 4) = v4[i][j];
+        for (int j = 0; j < NJ; ++j) *(f32x4*)(red + ((i * 2 + j) * NTHR + wave * 64 + lane) * 4) = v4[i][j];
     }
     __syncthreads();
     if (ps == 0) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           f32x4 v = v4[i][j];
 #pragma unroll
-          for (int o = 1; o < PS; ++o) v += *(const f32x4*)(red + ((i * 2 + j) * NTHR + (qo + QO * o) * 64 + lane) * 4);
+          for (int o = 1; o < PSP; ++o) v += *(const f32x4*)(red + ((i * 2 + j) * NTHR + partner(o) * 64 + lane) * 4);
           if (t < 9) {
             float* dst = p.slab + (((size_t)split * 9 * KD + 9 * kd + t) * Mtot + m_base + 16 * i) * p.Nc + n_base + 16 * j;
 #pragma unroll
@@ -892,7 +905,12 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_win_kernel(const WgradParams p)
   for (int t = 0; t < 9; ++t) reduce_store(acc[t], t);
   if (do_bias) {
     const f32x4 z = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const f32x4 bv[2][2] = {{bacc[0], bacc[1]}, {z, z}};
+    f32x4 bv[2][NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      bv[0][j] = bacc[j];
+      bv[1][j] = z;
+    }
     reduce_store(bv, 9);
   }
 }
@@ -1500,6 +1518,15 @@ hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
     }
   }
   if (p.hg.prob) return hipErrorInvalidValue;
+  if constexpr (QO == 1 && W >= 32) {
+    if (p.pair) {
+      if (p.M2 > 0)
+        UNET_LAUNCH((wgrad_win_kernel<W, QO, true, GEO, false, true>), dim3(grid), dim3(NTHR), 0, s, p);
+      else
+        UNET_LAUNCH((wgrad_win_kernel<W, QO, false, GEO, false, true>), dim3(grid), dim3(NTHR), 0, s, p);
+      return launch_status();
+    }
+  }
   if (p.M2 > 0)
     UNET_LAUNCH((wgrad_win_kernel<W, QO, true, GEO>), dim3(grid), dim3(NTHR), 0, s, p);
   else

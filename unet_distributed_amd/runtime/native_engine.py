@@ -71,8 +71,12 @@ def _r64(k: int) -> int:
 #                32 -> 32 channel convs (conv_win.h conv_win_pf_kernel) (8; 0 off)
 #   win_cp       64-channel row windows on 64-wide rows load the next input chunk under the
 #                current chunk's MFMAs (conv_win.h conv_win_cp_kernel) (1; 0 off)
+#   wg_pair      row-window weight gradients of 32-channel output blocks with wave-pair partials
+#                (conv_wgrad.hip wgrad_win_kernel PAIR: three workgroups per CU): 1 = 3D only,
+#                2 = 2D as well, 0 off (0)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
-                       tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8, win_cp=1)
+                       tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8, win_cp=1,
+                       wg_pair=0)
 
 
 class Fusion:
@@ -1658,7 +1662,7 @@ class NativeUNet:
                                        "tile (its dY is never materialised for a column-sum pass)")
                 d.update(name="wgrad:" + w["lname"], M1=w["M1"], M2=w["M2"], Nc=w["Nc"], splits=splits,
                          win=self.wgrad_win, slab=slab, bias_mode=w["bias_mode"] if fused_bias else 0,
-                         bias_slab=bslab)
+                         bias_slab=bslab, pair=int(self.opts["wg_pair"] >= (1 if self.dims == 3 else 2)))
                 if part is not None:
                     d.update(split_lo=part * splits // 2, split_n=splits // 2)
                 if "dw" in w:
