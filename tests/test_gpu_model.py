@@ -392,6 +392,8 @@ def test_native_inference_export_roundtrip_norm(cuda_dev, tmp_path, norm):
 @pytest.mark.parametrize("kw", [
     dict(batch_size=4, img_size=64, in_channels=4),
     dict(batch_size=4, img_size=128, in_channels=4, loss="dice_bce", hip_graph=True),
+    dict(batch_size=2, img_size=32, in_channels=4, dims=3),
+    dict(batch_size=1, img_size=64, in_channels=4, dims=3, loss="dice_bce"),
 ])
 def test_head_onload_step_equals_materialised(cuda_dev, monkeypatch, kw):
     """head_onload=1 (default: the head input's gradient formed on load by its

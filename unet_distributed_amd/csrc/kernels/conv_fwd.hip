@@ -1083,9 +1083,9 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
       return "conv_fwd: operand transform needs a 2D single-source row-window forward of a normalised input";
   }
   if (p.hg.prob && !p.fw.x && (!p.hg.t || !p.hg.sums || !p.hg.w || !p.hg.bits || p.C1 != 32 || p.C2 || p.xform ||
-                    p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) || conv_epi_mode(p) != EPI_DGRAD ||
+                    (p.KD != 1 && p.KD != 3) || p.OW > 128 || !win_eligible(p) || conv_epi_mode(p) != EPI_DGRAD ||
                     p.route_gy || !win_tile(conv_fwd_pick(p))))
-    return "conv_fwd: head-on-load needs a 2D 32-channel row-window data gradient";
+    return "conv_fwd: head-on-load needs a 2D / 3D 32-channel row-window data gradient";
   if (p.s2d && (p.s2d % 32 || p.C1 != 4 * p.s2d || p.C2 || p.xform || p.hg.prob || p.route_gy || p.KD != 1 ||
                 p.OD != 1 || p.OW > 128 || !win_eligible(p) ||
                 (conv_epi_mode(p) != EPI_DGRAD && conv_epi_mode(p) != EPI_DGRAD_NORM) ||

@@ -531,7 +531,8 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
   constexpr int REDB = 4 * 64 * 16 * 4;                 // one tap of every wave's partials
   constexpr int LDS_BYTES = (XB + YB > REDB) ? XB + YB : REDB;
   static_assert(W >= 8 && W <= 128 && (QO == 1 || QO == 2), "window wgrad shape");
-  static_assert(!HG || (QO == 1 && !CONCAT && GEO == WGEO_2D && BMW == NTHR), "head-on-load B: one 32-channel image");
+  static_assert(!HG || (QO == 1 && !CONCAT && (GEO == WGEO_2D || GEO == WGEO_3D) && BMW == NTHR),
+                "head-on-load B: one 32-channel image (2D rows or 3D slices)");
   static_assert(!PAIR || (W >= 32 && !HG), "wave-pair partials: column-unit path");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   char* Xs = smem;
@@ -1511,7 +1512,7 @@ __global__ void __launch_bounds__(NTHR) wgrad_s2d_win_kernel(const WgradParams p
 template <int W, int QO, int GEO>
 hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
   const int grid = ((p.M1 + p.M2) / 32) * (p.Nc / (32 * QO)) * p.KD * launch_splits(p);
-  if constexpr (GEO == WGEO_2D && QO == 1) {
+  if constexpr ((GEO == WGEO_2D || GEO == WGEO_3D) && QO == 1) {
     if (p.hg.prob) {
       UNET_LAUNCH((wgrad_win_kernel<W, QO, false, GEO, true>), dim3(grid), dim3(NTHR), 0, s, p);
       return launch_status();
@@ -1640,12 +1641,13 @@ const char* wgrad_check(const WgradParams& p) {
                        (p.xcs != 0 && p.xcs != p.Nc) || (p.xcs && p.QH % ((p.QW > 256 ? p.QW : 256) / p.QW))))
     return "wgrad: B transform (dz on load) needs the first-layer window wgrad";
   if (p.upA != 1) return "wgrad: upA must be 1 (nearest upsampling is materialised)";
-  // (the head-on-load instantiation is the 2D full-row window, launch_wgrad_win_g<W, 1,
-  // WGEO_2D>, on the 16..128-wide rows the executor plans it for)
+  // (the head-on-load instantiations are the 2D full-row and the 3D windows,
+  // launch_wgrad_win_g<W, 1, WGEO_2D / WGEO_3D>, on the rows the executor plans them for)
   if (p.hg.prob && (!p.hg.t || !p.hg.sums || !p.hg.w || !p.hg.bits || !wgrad_win_eligible(p) || p.Nc != 32 ||
-                    p.M2 != 0 || p.KD != 1 || p.QD != 1 || p.QW < 16 || p.QW > 128 || p.xform))
-    return "wgrad: head-on-load B needs a 2D single-source row-window wgrad with 32 output channels on rows "
-           "16..128 wide";
+                    p.M2 != 0 || (p.KD == 1 && p.QD != 1) || p.QW < 16 || p.QW > 128 || p.xform ||
+                    (p.KD == 3 && p.QW < 32)))
+    return "wgrad: head-on-load B needs a 2D / 3D single-source row-window wgrad with 32 output channels on rows "
+           "16..128 wide (3D: 32..128)";
   // 32-bit buffer offsets: the window kernels count them from each window's rows (one
   // image must stay below 2 GiB), the tiled kernel from the tensor starts
   {

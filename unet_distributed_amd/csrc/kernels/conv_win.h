@@ -143,8 +143,8 @@ template <int W, int BN, int BM, bool CONCAT, int EPI, int GEO, int XF = 0>
 __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   static_assert(BN == 32 || BN == 64, "row-window tile is 32 or 64 output channels wide");
   static_assert(XF == 0 || ((XF == 1 || XF == 3 || XF == 4) && GEO == GEO_2D && !CONCAT) ||
-                    (XF == 5 && GEO == GEO_2D && CONCAT),
-                "operand transform: 2D single-source windows (tconv on load: 2D concat)");
+                    (XF == 5 && GEO == GEO_2D && CONCAT) || (XF == 3 && GEO == GEO_3D && !CONCAT),
+                "operand transform: 2D single-source windows (tconv on load: 2D concat; head on load: 3D too)");
   constexpr int R = BM / W, HR = R + 2;
   // halo row pitch in 64-byte pixel slots: W + 2 columns rounded up to a multiple of 4
   // (every row starts on a 256-byte bank row); the DMA fills the image as one linear
@@ -278,6 +278,45 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
       const bool from1 = !CONCAT || (kc << 5) < p.C1;
       const int C = from1 ? p.C1 : p.C2;
       const int cb = from1 ? (kc << 5) : (kc << 5) - p.C1;
+      if constexpr (XF == 3) {
+        // head-on-load halo of depth tap kd (3D): slot (hr, hc) holds dY of pixel
+        // (g0 - 1 + hr + gsh, hc - 1) formed from the head (the 2D path's formula); the
+        // depth-shifted slice is inside the volume (the caller skips padding taps)
+        constexpr int NSL = XI * 16, HJ = (NSL + NTHR - 1) / NTHR;
+        const HeadGradCtx hctx = head_grad_ctx(p.hg);
+        float hpr[HJ], htv[HJ];
+        uint32_t hbits[HJ];
+#pragma unroll
+        for (int j = 0; j < HJ; ++j) {
+          const int sl = tid + NTHR * j;
+          const int hr = sl / HWP, hc = sl - hr * HWP;
+          const int gr = g0 - 1 + hr + gsh, col = hc - 1;
+          const bool ok = sl < NSL && hr < HR && (hr > 0 || top_in) && (hr < R + 1 || bot_in) &&
+                          (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+          const int pix = ok ? gr * W + col : 0;
+          hpr[j] = p.hg.prob[pix];
+          htv[j] = bits2f(((const uint16_t*)p.hg.t)[pix]);
+          hbits[j] = ok ? ((const uint32_t*)p.hg.bits)[pix] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < HJ; ++j) {
+          const int sl = tid + NTHR * j;
+          if (sl >= NSL) continue;
+          const int hc = sl % HWP;
+          const float dz = head_dlogit(hpr[j], htv[j], hctx.a, hctx.bb, hctx.inv_total, hctx.bce_w, hctx.gscale);
+          const int sw = (hc >> 1) & 3;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float o[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float v = dz * hctx.w[8 * k + e];
+              o[e] = ((hbits[j] >> (8 * k + e)) & 1u) ? v : 0.f;
+            }
+            *(u32x4*)(Xs + sl * 64 + 16 * (k ^ sw)) = pack8(o);
+          }
+        }
+      }
       {
         // halo image: row hr, slot hc holds pixel (g0 - 1 + hr + gsh, col0 + hc - 1);
         // instruction (hr, j) covers slots 16j .. 16j + 15 of row hr.  Rows outside the
@@ -286,7 +325,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
 #pragma unroll
         for (int q = 0; q < (XI + 3) / 4; ++q) {
           const int k = wave + 4 * q;
-          if (k < XI) {
+          if (XF != 3 && k < XI) {
             const int sl = 16 * k + lslot;                  // this lane's halo slot
             const int hr = sl / HWP, hc = sl - hr * HWP;    // its row / column
             const int gr = g0 - 1 + hr + gsh;
@@ -1491,14 +1530,18 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
     }                                                                                                         \
     break;
   if (p.hg.prob) {                      // head-on-load data gradient (conv_fwd_prepare checks the shape)
-    if (epi != EPI_DGRAD || geo != GEO_2D) return hipErrorInvalidValue;
+    if (epi != EPI_DGRAD || (geo != GEO_2D && geo != GEO_3D)) return hipErrorInvalidValue;
     switch (W) {
 #define HG_CASE(WW)                                                                                       \
   case WW:                                                                                                \
-    if constexpr (win_tile_built<BN, BM>(WW))                                                             \
-      UNET_LAUNCH((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_2D, 3>), dim3(grid), dim3(NTHR), 0, s, p); \
-    else                                                                                                  \
+    if constexpr (win_tile_built<BN, BM>(WW)) {                                                           \
+      if (geo == GEO_3D)                                                                                  \
+        UNET_LAUNCH((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_3D, 3>), dim3(grid), dim3(NTHR), 0, s, p); \
+      else                                                                                                \
+        UNET_LAUNCH((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_2D, 3>), dim3(grid), dim3(NTHR), 0, s, p); \
+    } else {                                                                                              \
       return hipErrorInvalidValue;                                                                        \
+    }                                                                                                     \
     break;
       HG_CASE(16)
       HG_CASE(32)

@@ -119,7 +119,7 @@ class Fusion:
 _ROW_IMGS = (16, 32, 64, 128)       # 2D images whose rows the row-window kernels take whole
 FUSIONS: Dict[str, Fusion] = {
     "head_onload": Fusion("head input gradient formed on load by its consumers (head_grad.h)",
-                          norm={"none"}, dims={2}, img=_ROW_IMGS, option="head_onload",
+                          norm={"none"}, img=_ROW_IMGS, option="head_onload",
                           when=lambda e: e.tinfo[e.head_in][1] == 32 and e.wgrad_win >= 0),
     "head_fuse": Fusion("Mask head in the epilogue of its input conv's forward",
                         norm={"none"}, option="head_fuse", when=lambda e: e.tinfo[e.head_in][1] == 32),
