@@ -120,7 +120,8 @@ _ROW_IMGS = (16, 32, 64, 128)       # 2D images whose rows the row-window kernel
 FUSIONS: Dict[str, Fusion] = {
     "head_onload": Fusion("head input gradient formed on load by its consumers (head_grad.h)",
                           norm={"none"}, img=_ROW_IMGS, option="head_onload",
-                          when=lambda e: e.tinfo[e.head_in][1] == 32 and e.wgrad_win >= 0),
+                          when=lambda e: e.tinfo[e.head_in][1] == 32 and e.wgrad_win >= 0 and
+                          (e.dims == 2 or e.img >= 32)),     # (3D: the column-unit window wgrad)
     "head_fuse": Fusion("Mask head in the epilogue of its input conv's forward",
                         norm={"none"}, option="head_fuse", when=lambda e: e.tinfo[e.head_in][1] == 32),
     "pool_epilogue": Fusion("2x2 max-pool in the convNb forward epilogue", norm={"none"}),
