@@ -400,14 +400,14 @@ def test_head_onload_step_equals_materialised(cuda_dev, monkeypatch, kw):
     consumers, no dY tensor) gives the materialised-dY step bit for bit: loss sums,
     probabilities and every parameter gradient."""
     outs = []
-    for v in ("0", "1"):
-        # (dw_fuse=0: with head_onload=0 the head input conv's weight gradient would run in
+    for v in ("0", "2"):
+        # (head_onload=2: 3D too; dw_fuse=0: with head_onload=0 the head input conv's weight gradient would run in
         # the fused data + weight gradient kernel, a different fp32 summation order)
         monkeypatch.setenv("UNET_ENGINE", "dw_fuse=0,head_onload=" + v)
         spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
         e = nb.engine
-        assert e.head_onload == (v == "1")
-        assert ("wgrad:Mask" in e.plan.names()) == (v == "1")
+        assert e.head_onload == (v == "2")
+        assert ("wgrad:Mask" in e.plan.names()) == (v == "2")
         for seed in (77, 78):
             nb.fwd_bwd(x, y, seed=seed)
         torch.cuda.synchronize()

@@ -56,7 +56,7 @@ def _r64(k: int) -> int:
 #   dual_stream  weight-gradient launches on a side stream during the backward (1)
 #   fwd_streams  training forward as two half-batch chunks on two streams (2)
 #   head_fuse    Mask head in the epilogue of its input conv's forward (1)
-#   head_onload  the head input's gradient formed on load by its consumers (1)
+#   head_onload  the head input's gradient formed on load by its consumers (1: 2D; 2: 3D too)
 #   tconv_fused  deepest fine level whose transposed conv runs the composite backward (2; 0 off)
 #   tconv_wa     the consumer conv's u-row weight gradient from the composite backward's
 #                slab sums (1; 0: full weight gradient over u)
@@ -121,7 +121,9 @@ FUSIONS: Dict[str, Fusion] = {
     "head_onload": Fusion("head input gradient formed on load by its consumers (head_grad.h)",
                           norm={"none"}, img=_ROW_IMGS, option="head_onload",
                           when=lambda e: e.tinfo[e.head_in][1] == 32 and e.wgrad_win >= 0 and
-                          (e.dims == 2 or e.img >= 32)),     # (3D: the column-unit window wgrad)
+                          (e.dims == 2 or (e.img >= 32 and e.opts["head_onload"] >= 2))),
+                          # (3D: opt-in, the column-unit window wgrad; measured 0.6 ms slower at b8 --
+                          # the 3D weight gradient re-forms each depth tap's head gradient)
     "head_fuse": Fusion("Mask head in the epilogue of its input conv's forward",
                         norm={"none"}, option="head_fuse", when=lambda e: e.tinfo[e.head_in][1] == 32),
     "pool_epilogue": Fusion("2x2 max-pool in the convNb forward epilogue", norm={"none"}),
