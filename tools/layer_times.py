@@ -20,25 +20,53 @@ from unet_distributed_amd.runtime.native_engine import NativeUNet  # noqa: E402
 from unet_distributed_amd.runtime.params import FlatParams  # noqa: E402
 
 
-def layer_flops(spec, B, img, dims):
-    """GEMM FLOPs per plan-entry name (fwd:, dgrad:, wgrad:)."""
+def layer_flops(spec, B, img, dims, e=None, names=()):
+    """GEMM FLOPs per plan-entry name (fwd:, dgrad:, dgrad_skip:, wgrad:), attributed to
+    the launch that does them: a concat conv's data gradient split into its u and skip
+    halves, the u-row weight gradient chained into the transposed conv's composite
+    weight gradient (tconv_wa), data + weight gradient in one fused launch (dw_fused), and
+    a layer's work split over several launches of one name (halves) divided among them."""
     out = {}
+    tcon = {}                                   # concat conv -> its transposed conv
+    for l in spec.layers:
+        if l.kind == "tconv":
+            for c in spec.layers:
+                if c.kind == "conv" and c.skip_from is not None and c.level == l.level:
+                    tcon[c.name] = l
+    wa = getattr(e, "_wa_chain_of", {}) if e is not None else {}
+    fused = set(getattr(e, "fusions", {}).get("dw_fused", ())) if e is not None else set()
     for l in spec.layers:
         s = img >> (l.level - 1)
         pix = B * s ** dims
         if l.kind == "conv":
             f = 2.0 * pix * l.cout * l.cin * 3 ** dims
             out["fwd:" + l.name] = f
-            out["wgrad:" + l.name] = f
+            cs = l.cin - tcon[l.name].cout if l.name in tcon else 0       # skip channels
+            fw = f * cs / l.cin if l.name in wa else f
+            if l.name in wa:
+                out["wgrad:" + wa[l.name]] = out.get("wgrad:" + wa[l.name], 0.0) + f - fw
+            fd = 0.0
             if l.level > 1 or l.skip_from is not None or l.cin > 8:
-                out["dgrad:" + l.name] = f
+                fd = f
+                if "dgrad_skip:" + l.name in names:
+                    fd = f * (l.cin - cs) / l.cin
+                    out["dgrad_skip:" + l.name] = f * cs / l.cin
+            if l.name in fused and "wgrad:" + l.name not in names:
+                fd += fw
+            else:
+                out["wgrad:" + l.name] = fw
+            if fd:
+                out["dgrad:" + l.name] = fd
         elif l.kind == "tconv":
-            f = 2.0 * pix * l.cout * l.cin      # pix at the output (finer) level... see below
             s2 = img >> l.level
             f = 2.0 * B * s2 ** dims * l.cin * l.cout * 2 ** dims
             out["fwd:" + l.name] = f
-            out["wgrad:" + l.name] = f
+            out["wgrad:" + l.name] = out.get("wgrad:" + l.name, 0.0) + f
             out["dgrad:" + l.name] = f
+    for n in set(names):
+        k = list(names).count(n)
+        if k > 1 and n in out:
+            out[n] /= k
     return out
 
 
@@ -72,7 +100,7 @@ def main():
         e.backward()
     torch.cuda.synchronize()
     names = e.plan.names()
-    fl = layer_flops(spec, a.batch, a.img, a.dims)
+    fl = layer_flops(spec, a.batch, a.img, a.dims, e, names)
     s = torch.cuda.current_stream().cuda_stream
     rows = []
     total = 0.0
