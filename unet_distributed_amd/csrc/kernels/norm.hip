@@ -513,6 +513,7 @@ __global__ void __launch_bounds__(NT) bn_stats_fused_kernel(const float* __restr
                                                             float* __restrict__ cc, float* __restrict__ dgamma,
                                                             float* __restrict__ dbeta) {
   __shared__ float red[4][64];
+  __shared__ f32x4 red4[16][17];
   __shared__ int last;
   const int W = 2 * C;
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
@@ -520,21 +521,37 @@ __global__ void __launch_bounds__(NT) bn_stats_fused_kernel(const float* __restr
   const bool valid = c < C;
   const int col = (cl >> 5) * C + c;
   {
+    // phase 1: thread (row lane r4 = t >> 4, float4 column f = t & 15) sums float4 f of
+    // the block's 64 columns (f < 8: first moments of channels 32 cb + 4 f .., f >= 8:
+    // second) over rows r0 + r4, + 16, ..: 16-byte loads, 8 in flight (the scalar-load
+    // version kept one float per load and ~32 dependent load rounds at level 1)
+    const int f = threadIdx.x & 15, r4 = threadIdx.x >> 4;
+    const int c4 = blockIdx.y * 32 + 4 * (f & 7);
+    const bool v4 = c4 < C;
+    const int col4 = (f >> 3) * C + c4;
     const int sl = blockIdx.x;
     const int r0 = sl * rpb, r1 = min(R, r0 + rpb);
-    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (valid) {
-      int r = r0 + rl;
-      for (; r + 28 < r1; r += 32)
+    f32x4 a[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) a[k] += rows[(size_t)(r + 4 * k) * W + col];
-      for (; r < r1; r += 4) a[0] += rows[(size_t)r * W + col];
+    for (int k = 0; k < 8; ++k) a[k] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (v4) {
+      int r = r0 + r4;
+      for (; r + 112 < r1; r += 128)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] += *(const f32x4*)(rows + (size_t)(r + 16 * k) * W + col4);
+      for (; r < r1; r += 16) a[0] += *(const f32x4*)(rows + (size_t)r * W + col4);
     }
-    red[rl][cl] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    red4[r4][f] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     __syncthreads();
-    if (rl == 0 && valid)
-      __hip_atomic_store(slices + (size_t)sl * W + col, red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl],
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 64) {
+      // thread cl: column (cl >> 5) * C + 32 cb + (cl & 31) = element (cl & 3) of float4
+      // (cl >> 5) * 8 + ((cl & 31) >> 2)
+      const int ff = (cl >> 5) * 8 + ((cl & 31) >> 2), e = cl & 3;
+      float sm = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) sm += red4[k][ff][e];
+      if (valid) __hip_atomic_store(slices + (size_t)sl * W + col, sm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
@@ -572,10 +589,17 @@ __global__ void __launch_bounds__(NT) bn_stats_fused_kernel(const float* __restr
   if (threadIdx.x == 0) __hip_atomic_store(counter + blockIdx.y, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// rows per phase-1 block of bn_stats_fused: at most 128 slices for the last block to sum
-int fused_rows_per_block(int R) {
-  int rpb = (R + 127) / 128;
-  rpb = (rpb + 15) / 16 * 16;
+// rows per phase-1 block of bn_stats_fused: a multiple of 32 rows (so at most row_slices(R)
+// slices, the workspace's count) and at most min(64, 128 / column blocks) slices -- the
+// launch's cost follows its block count (every block's agent-scope release and counter add):
+// slice-count A/B on the BN step (r6_bench_history.md), 128 blocks for 64..128 channels,
+// 64 slices at 32 channels; the 16-byte phase-1 loads cover the longer slices
+int fused_rows_per_block(int R, int C) {
+  const int ncb = (C + 31) / 32;
+  int ms = 128 / ncb;
+  ms = ms > 64 ? 64 : (ms < 8 ? 8 : ms);
+  int rpb = (R + ms - 1) / ms;
+  rpb = (rpb + 31) / 32 * 32;
   return rpb < 32 ? 32 : rpb;
 }
 
@@ -772,7 +796,7 @@ hipError_t bn_stats_launch(const float* rows, int R, int C, float count, int mod
   // one launch: slices, then the finalize by the last block of each 32-channel column
   // block; the ceil(C / 32) <= 64 counters live just past the row_slices(R) * 2C slice
   // floats of the workspace (zeroed once, reset every use)
-  const int rpb = fused_rows_per_block(R);
+  const int rpb = fused_rows_per_block(R, C);
   const int nsl = (R + rpb - 1) / rpb;
   int* counter = (int*)(slices + (size_t)row_slices(R) * 2 * C);
   UNET_LAUNCH(bn_stats_fused_kernel, dim3(nsl, (C + 31) / 32), dim3(NT), 0, s, rows, R, C, rpb, slices,
@@ -793,7 +817,7 @@ hipError_t gn_stats_launch(const float* rows, int N, int rps, int C, int G, int 
   if (mode == 1) {
     // dgamma / dbeta = column sums of the per-sample contributions (fused single launch)
     float* slices = work + (size_t)N * 2 * C;
-    const int rpb = fused_rows_per_block(N);
+    const int rpb = fused_rows_per_block(N, C);
     const int nsl = (N + rpb - 1) / rpb;
     int* counter = (int*)(slices + (size_t)row_slices(N) * 2 * C);
     UNET_LAUNCH(bn_stats_fused_kernel, dim3(nsl, (C + 31) / 32), dim3(NT), 0, s, (const float*)work, N, C,
