@@ -1076,7 +1076,15 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
     return "conv_fwd: relu_bits needs an unsplit ReLU forward";
   if ((p.mask_bits & ~3) || ((p.mask_bits & 1) && !p.mask1) || ((p.mask_bits & 2) && !p.mask2))
     return "conv_fwd: mask_bits marks a missing mask";
-  if (p.xform && !p.fw.x) {          // (the fused weight gradient's xform 2: conv_dw_check)
+  if (p.xform == 2 && !p.fw.x) {     // data gradient of a normalised layer, dz formed on load
+    const int ep = conv_epi_mode(p), t = conv_fwd_pick(p);
+    if (p.C2 || !p.xa || !p.xb || !p.xc || !p.xz || p.KD != 1 || p.OD != 1 || p.OW < 16 || p.OW > 64 ||
+        !win_eligible(p) || t != 6 || (win_bn(p) != 64 && p.OW != 64) || (p.xcs != 0 && p.xcs != p.C1) ||
+        (p.OW == 64 && p.C1 > 128) ||
+        p.head_w || p.hg.prob || p.s2d || p.ut.x || p.route_gy || p.pool_dst || (ep != EPI_DGRAD && ep != EPI_DGRAD_NORM))
+      return "conv_fwd: dz on load needs a 2D single-source row-window data gradient (rows 16..64 wide; the 32-channel "
+             "tile on 64-wide rows only)";
+  } else if (p.xform && !p.fw.x) {   // (the fused weight gradient's xform 2: conv_dw_check)
     const int ep = conv_epi_mode(p), t = conv_fwd_pick(p);
     if (p.xform != 1 || p.C2 || !p.xa || !p.xb || p.KD != 1 || p.OD != 1 || p.OW > 128 || !win_eligible(p) ||
         (t != 6 && t != 12) || (p.xcs != 0 && p.xcs != p.C1) || p.head_w || (ep != EPI_STATS && ep != EPI_GENERIC))

@@ -521,7 +521,11 @@ enum { WGEO_2D = 0, WGEO_SEG = 1, WGEO_3D = 2 };
 // 32-channel output block, so its dW partial is 9 x 32 x 16 (72 registers instead of 144)
 // and the kernel fits three workgroups per CU (the 3D level-1 weight gradients were half
 // waits at two); the pixel splits halve and each x fragment feeds two waves.
-template <int W, int QO, bool CONCAT, int GEO, bool HG = false, bool PAIR = false>
+// DZ (xform 2, 2D single source, rows 16..64 wide): the B operand is the layer's norm
+// backward dz = ca g + cb z + cc formed on load -- p.b = g is DMA'd as usual, each thread's
+// z granules are loaded with it and the staged g image is rewritten in place (the
+// norm_bwd_apply formula and rounding; coefficients of the window's sample in LDS, Ks).
+template <int W, int QO, bool CONCAT, int GEO, bool HG = false, bool PAIR = false, bool DZ = false>
 __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const WgradParams p) {
   constexpr int BMW = 256, R = BMW / W, HR = R + 2;
   constexpr int HWP = ((W + 2 + 15) / 16) * 16, IPR = HWP / 16, ROWB = HWP * 64;
@@ -529,8 +533,11 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
   constexpr int XB = XI * 1024, YB = YI * 1024;
   constexpr int PS = 4 / QO, KS = BMW / 32;
   constexpr int REDB = 4 * 64 * 16 * 4;                 // one tap of every wave's partials
-  constexpr int LDS_BYTES = (XB + YB > REDB) ? XB + YB : REDB;
+  constexpr int KB = DZ ? 3 * 32 * QO * 4 : 0;         // DZ: ca / cb / cc of the block's channels
+  constexpr int LDS_BYTES = (XB + YB + KB > REDB) ? XB + YB + KB : REDB;
   static_assert(W >= 8 && W <= 128 && (QO == 1 || QO == 2), "window wgrad shape");
+  static_assert(!DZ || (GEO == WGEO_2D && !HG && !PAIR && !CONCAT && W >= 16 && W <= 64 && QO == 1),
+                "dz on load: 2D single-source full rows 16..64 wide");
   static_assert(!HG || (QO == 1 && !CONCAT && (GEO == WGEO_2D || GEO == WGEO_3D) && BMW == NTHR),
                 "head-on-load B: one 32-channel image (2D rows or 3D slices)");
   static_assert(!PAIR || (W >= 32 && !HG), "wave-pair partials: column-unit path");
@@ -635,6 +642,12 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
   constexpr bool pair_ok = PAIR_PATH;   // wgrad_win_eligible: QH % 16 == 0 for 16-wide rows
   HeadGradCtx hctx{};
   if constexpr (HG) hctx = head_grad_ctx(p.hg);
+  // DZ: thread t rewrites granules u = t + 256 c of the B image: image o = c / 4, slot
+  // (t >> 2) + 64 (c & 3), physical chunk t & 3 = logical chunk dzl (the slot swizzle bit
+  // (slot >> 3) & 1 is (t >> 5) & 1 for every c): channels co0 + 32 o + 8 dzl ..
+  float* Ks = (float*)(smem + XB + YB);
+  const int dzl = (tid & 3) ^ (((tid >> 5) & 1) << 1);
+  int ks_n = -1;                                        // sample whose coefficients Ks holds
   for (int win = w_begin; win < w_end; ++win) {
     const int g0 = (GEO == WGEO_SEG ? win / nseg : win) * R;
     const int col0 = GEO == WGEO_SEG ? (win % nseg) * W : 0;
@@ -648,6 +661,8 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
         (void*)(abase + (size_t)rb * Wf * CA * 2), (short)0, OOB, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(bbase + (size_t)g0 * Wf * p.Nc * 2), (short)0, OOB, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsz = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((DZ ? (const char*)p.xz : bbase) + (size_t)g0 * Wf * p.Nc * 2), (short)0, OOB, 0x00020000);
     __syncthreads();   // the previous window's fragment reads are done
 #pragma unroll
     for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
@@ -695,7 +710,50 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
                                                  off, 0, 0, 0);
       }
     }
+    u32x4 zq[DZ ? 4 * QO : 1];
+    if constexpr (DZ) {
+      const int n = p.xcs ? g0 / H : 0;                 // (windows never span two images: rows_ok)
+      if (n != ks_n) {                                  // (the loop-top barrier ordered the old reads)
+        ks_n = n;
+        if (tid < 3 * 32 * QO) {
+          const int m = tid / (32 * QO), c = tid - m * 32 * QO;
+          Ks[tid] = (m == 0 ? p.xa : m == 1 ? p.xb : p.xc)[(size_t)n * p.xcs + co0 + c];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4 * QO; ++c) {
+        const int pix = g0 * W + (tid >> 2) + 64 * (c & 3);
+        zq[c] = __builtin_amdgcn_raw_buffer_load_b128(
+            rsz, pix < Mq ? ((pix - g0 * W) * p.Nc + co0 + 32 * (c >> 2) + 8 * dzl) * 2 : OOB, 0, 0);
+      }
+    }
     __syncthreads();
+    if constexpr (DZ) {
+#pragma unroll
+      for (int o = 0; o < QO; ++o) {
+        float ka[8], kz[8], kk[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int ch = 32 * o + 8 * dzl + e;
+          ka[e] = Ks[ch];
+          kz[e] = Ks[32 * QO + ch];
+          kk[e] = Ks[64 * QO + ch];
+        }
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+          const int c = 4 * o + c4;
+          if (g0 * W + (tid >> 2) + 64 * c4 >= Mq) continue;   // past the tensor: stays zero
+          u32x4* a = (u32x4*)(Ys + (tid + NTHR * c) * 16);
+          float gv[8], zv[8];
+          unpack8(*a, gv);
+          unpack8(zq[c], zv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) gv[e] = fmaf(ka[e], gv[e], fmaf(kz[e], zv[e], kk[e]));
+          *a = pack8(gv);
+        }
+      }
+      __syncthreads();
+    }
     const char* Yq = Ys + qo * (BMW * 64);
     // (one column unit per wave: with two, the 128-wide QO = 2 case spills)
     if constexpr (UNITS_PATH) {
@@ -1519,6 +1577,14 @@ hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
     }
   }
   if (p.hg.prob) return hipErrorInvalidValue;
+  if (p.xform == 2) {                                   // dz on load (wgrad_check: 2D single source)
+    if constexpr (GEO == WGEO_2D && W >= 16 && W <= 64 && QO == 1) {
+      if (p.M2 > 0) return hipErrorInvalidValue;
+      UNET_LAUNCH((wgrad_win_kernel<W, QO, false, GEO, false, false, true>), dim3(grid), dim3(NTHR), 0, s, p);
+      return launch_status();
+    }
+    return hipErrorInvalidValue;
+  }
   if constexpr (QO == 1 && W >= 32) {
     if (p.pair) {
       if (p.M2 > 0)
@@ -1604,7 +1670,9 @@ static bool wgrad_s2d_win_eligible(const WgradParams& p) {
 WgradCfg wgrad_pick(const WgradParams& p) {
   const int KT = p.KD * p.KH * p.KW;
   const int M = p.M1 + p.M2;
-  if (wgrad_win_eligible(p)) return {32, (p.Nc % 64 == 0) ? 64 : 32, 9, 0};   // row-window tile
+  // row-window tile (dz on load: the 32-channel output block -- with two, the z granules in
+  // flight pushed the 64-channel block past 256 VGPRs, 11-17 spilled)
+  if (wgrad_win_eligible(p)) return {32, (p.Nc % 64 == 0 && p.xform != 2) ? 64 : 32, 9, 0};
   if (wgrad_win_first3_eligible(p)) return {112, 32, 1, 1};                     // 3D first-layer window
   if (wgrad_win_first_eligible(p)) return {p.M1 == 4 ? 48 : 80, 32, 1, 1};      // first-layer window
   if (wgrad_tconv_win_eligible(p))                                                 // transposed-conv window
@@ -1637,9 +1705,13 @@ const char* wgrad_check(const WgradParams& p) {
     if (KT % c.NTAP) return "wgrad: taps not divisible by the tap group";
   }
   if (p.xform != 0 && p.xform != 2) return "wgrad: xform must be 0 or 2";
-  if (p.xform == 2 && (!wgrad_win_first_eligible(p) || !p.xa || !p.xb || !p.xc || !p.xz ||
-                       (p.xcs != 0 && p.xcs != p.Nc) || (p.xcs && p.QH % ((p.QW > 256 ? p.QW : 256) / p.QW))))
-    return "wgrad: B transform (dz on load) needs the first-layer window wgrad";
+  if (p.xform == 2 && (!p.xa || !p.xb || !p.xc || !p.xz || (p.xcs != 0 && p.xcs != p.Nc) ||
+                       (wgrad_win_first_eligible(p)
+                            ? (p.xcs && p.QH % ((p.QW > 256 ? p.QW : 256) / p.QW)) != 0
+                            : (!wgrad_win_eligible(p) || p.KD != 1 || p.QD != 1 || p.QW < 16 || p.QW > 64 ||
+                               p.M2 != 0 || p.hg.prob || p.pair))))
+    return "wgrad: B transform (dz on load) needs the first-layer window wgrad or a 2D single-source row-window "
+           "wgrad on rows 16..64 wide";
   if (p.upA != 1) return "wgrad: upA must be 1 (nearest upsampling is materialised)";
   // (the head-on-load instantiations are the 2D full-row and the 3D windows,
   // launch_wgrad_win_g<W, 1, WGEO_2D / WGEO_3D>, on the rows the executor plans them for)

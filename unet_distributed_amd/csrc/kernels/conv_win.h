@@ -53,13 +53,15 @@ inline bool win_pf_eligible(const ConvFwdParams& p) {
          p.tile != 12 && !p.s2d && !p.ut.x && !p.fw.x && p.OH % 4 == 0 &&
          (!p.hg.prob || conv_epi_mode(p) == EPI_DGRAD) && (!p.xform || (p.xform == 1 && p.OW == 128 && !p.hg.prob));
 }
+constexpr int CP_DZ_MAXC = 128;      // conv_win_cp_kernel DZ: input channels in LDS coefficients
 // Chunk-pipelined window (conv_win_cp_kernel): 2D 64-wide full rows, the 64-channel tile,
 // plain or concat source, no operand transform, two or more 32-channel input chunks (level 2
 // of the 128^2 UNet).  (At levels 3-4 -- 32 / 16-wide rows, 4..16 chunks -- the per-launch
 // times rose 0.016-0.034 ms against the DMA chunk loop, run V: not used there.)
 inline bool win_cp_eligible(const ConvFwdParams& p) {
   return p.win_cp > 0 && p.OW == 64 && p.KD == 1 && p.OD == 1 &&
-         p.C1 + p.C2 >= 64 && p.Cout % 64 == 0 && !p.head_w && p.tile != 6 && !p.xform && !p.hg.prob &&
+         p.C1 + p.C2 >= 64 && p.Cout % 64 == 0 && !p.head_w && p.tile != 6 &&
+         (!p.xform || (p.xform == 2 && !p.C2 && p.C1 <= CP_DZ_MAXC)) && !p.hg.prob &&
          !p.s2d && !p.ut.x && !p.fw.x;
 }
 // Chunk-pipelined window on 128-wide rows (conv_win_cp128_kernel): 2D with two or more input
@@ -133,7 +135,9 @@ constexpr int NTHR = 256;
 
 // XF (2D, single source): operand transform of the src1 halo image in LDS before the
 // MFMAs -- 1: conv_params.h xform 1, y = relu(xa z + xb) (the window's own rows of the
-// transformed operand go to xout); 3: head-on-load, the halo image of dY (32 channels)
+// transformed operand go to xout); 2: the conv's own norm backward on load (data gradient of a
+// normalised layer: src1 = g, p.xz = z, the halo becomes dz = ca g + cb z + cc, the
+// norm_bwd_apply formula and rounding); 3: head-on-load, the halo image of dY (32 channels)
 // is formed from the head's per-pixel probability, target and ReLU bits (p.hg,
 // head_grad.h) instead of being read from memory; 4: space-to-depth source (p.s2d: the
 // DMA gathers the fine pixels of each coarse slot, structurally zero taps skipped); 5
@@ -142,7 +146,7 @@ constexpr int NTHR = 256;
 template <int W, int BN, int BM, bool CONCAT, int EPI, int GEO, int XF = 0>
 __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
   static_assert(BN == 32 || BN == 64, "row-window tile is 32 or 64 output channels wide");
-  static_assert(XF == 0 || ((XF == 1 || XF == 3 || XF == 4) && GEO == GEO_2D && !CONCAT) ||
+  static_assert(XF == 0 || ((XF == 1 || XF == 2 || XF == 3 || XF == 4) && GEO == GEO_2D && !CONCAT) ||
                     (XF == 5 && GEO == GEO_2D && CONCAT) || (XF == 3 && GEO == GEO_3D && !CONCAT),
                 "operand transform: 2D single-source windows (tconv on load: 2D concat; head on load: 3D too)");
   constexpr int R = BM / W, HR = R + 2;
@@ -377,7 +381,7 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
     // operand transform: thread t owns logical 16-byte chunk xlc = t & 3 (channels
     // cb + 8 xlc ..) of slots (t >> 2) + 64 j, so its 8 channels' coefficients are fixed
     // per chunk; the slot's physical chunk is xlc ^ swizzle(column), as the DMA wrote it
-    constexpr int XNJ = XF == 1 ? (XI * 64 + NTHR - 1) / NTHR : 1;
+    constexpr int XNJ = (XF == 1 || XF == 2) ? (XI * 64 + NTHR - 1) / NTHR : 1;
     const int xlc = tid & 3, xs0 = tid >> 2;
     auto xslot = [&](const int j, int& hr, int& hc, int& gr, bool& ok) {
       const int sl = xs0 + (NTHR / 4) * j;
@@ -388,7 +392,10 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
            (unsigned)(hc - 1) < (unsigned)W;
       return sl;
     };
-    const size_t xsample = XF == 1 ? (size_t)(g0 / H) * p.xcs : 0;   // the window's sample (GroupNorm rows)
+    const size_t xsample = (XF == 1 || XF == 2) ? (size_t)(g0 / H) * p.xcs : 0;   // the window's sample (GroupNorm rows)
+    // XF 2: z of the halo slots (the image-relative base of conv_fwd's src1 layout, C1 channels)
+    const __amdgpu_buffer_rsrc_t rsz = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(XF == 2 ? (const char*)p.xz + img_px * p.C1 * 2 : s1b), (short)0, OOB, 0x00020000);
     // XF 5: u channels cb .. cb + 31 of the halo image from the coarse input.  The HR fine
     // halo rows come from NCR = R / 2 + 2 coarse rows (R even); wave w takes coarse rows
     // cq = w, w + 4, ..: it loads the row's B fragments (16 coarse pixels x 32 coarse
@@ -536,6 +543,26 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
           }
         }
       }
+      // XF 2: the thread's z granules and 8 channels' coefficients, in flight with the DMA
+      u32x4 zq[XF == 2 ? XNJ : 1];
+      float za[8], zb[8], zc[8];
+      if constexpr (XF == 2) {
+#pragma unroll
+        for (int j = 0; j < XNJ; ++j) {
+          int hr, hc, gr;
+          bool ok;
+          xslot(j, hr, hc, gr, ok);
+          zq[j] = __builtin_amdgcn_raw_buffer_load_b128(
+              rsz, ok ? (((gr - grow0) * W + hc - 1) * p.C1 + cb + xlc * 8) * 2 : OOB, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const size_t ci = xsample + cb + xlc * 8 + e;
+          za[e] = p.xa[ci];
+          zb[e] = p.xb[ci];
+          zc[e] = p.xc[ci];
+        }
+      }
       if constexpr (XF == 5) {
         if (from1) {
           if (p.ut.C == 64)
@@ -597,6 +624,23 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
         }
       }
       __syncthreads();
+      if constexpr (XF == 2) {
+#pragma unroll
+        for (int j = 0; j < XNJ; ++j) {
+          int hr, hc, gr;
+          bool ok;
+          const int sl = xslot(j, hr, hc, gr, ok);
+          if (!ok) continue;                              // padding stays the DMA's zeros
+          char* a = Xs + sl * 64 + 16 * (xlc ^ ((hc >> 1) & 3));
+          float v[8], zv[8];
+          unpack8(*(const u32x4*)a, v);
+          unpack8(zq[j], zv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaf(za[e], v[e], fmaf(zb[e], zv[e], zc[e]));
+          *(u32x4*)a = pack8(v);
+        }
+        __syncthreads();
+      }
       if constexpr (XF == 1) {
         float xa[8], xb[8];
 #pragma unroll
@@ -900,7 +944,10 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
 // run, and written to LDS after them: one barrier pair per chunk, no exposed load latency
 // past the first chunk.  Same LDS images (pitch W + 4, chunk swizzle), operands, tap order
 // and epilogue as conv_win_kernel<W, 64, 256, CONCAT, EPI, GEO_2D>: bit-identical outputs.
-template <int W, bool CONCAT, int EPI>
+// DZ (xform 2, conv_win_kernel's XF 2): src1 = g; the z granules ride along with the g
+// granules and each halo granule is stored as dz = ca g + cb z + cc, the window sample's
+// coefficients of every input channel held in LDS (Ks, past the images).
+template <int W, bool CONCAT, int EPI, bool DZ = false>
 __global__ void __launch_bounds__(NTHR, 2) conv_win_cp_kernel(const ConvFwdParams p) {
   constexpr int BN = 64, BM = 256, R = BM / W, HR = R + 2;
   constexpr int HWP = W + 4, ROWB = HWP * 64;
@@ -909,7 +956,8 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_cp_kernel(const ConvFwdParam
   constexpr int XG = (NSLOT * 4 + NTHR - 1) / NTHR;     // halo granules per thread
   constexpr int WG = 9 * BN * 4 / NTHR;                 // weight granules per thread (9)
   constexpr int EPIB = (EPI == EPI_STATS || EPI == EPI_DGRAD_NORM) ? epi_lds_bytes<BM, BN>() : BM * (BN + 4) * 2;
-  constexpr int LDS_BYTES = (XB + WB > EPIB) ? XB + WB : EPIB;
+  constexpr int KB = DZ ? 3 * CP_DZ_MAXC * 4 : 0;       // DZ coefficients (Cin <= CP_DZ_MAXC)
+  constexpr int LDS_BYTES = (XB + WB + KB > EPIB) ? XB + WB + KB : EPIB;
   constexpr int WMP = BM / 4, TM = WMP / 16, TN = BN / 16;
   constexpr int TC = 1, NCS = W / 16, RW = R / (4 / NCS);
   static_assert(W >= 16 && W <= 64 && RW * TC == TM && 9 * BN * 4 % NTHR == 0, "chunk-pipelined window shape");
@@ -937,11 +985,24 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_cp_kernel(const ConvFwdParam
   const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc((void*)s2b, (short)0, OOB, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.wgt, (short)0, OOB, 0x00020000);
   const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
+  float* Ks = (float*)(smem + XB + WB);
+  const __amdgpu_buffer_rsrc_t rsz = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(DZ ? (const char*)p.xz + img_px * p.C1 * 2 : s1b), (short)0, OOB, 0x00020000);
+  if constexpr (DZ) {
+    // ca / cb / cc of the window's sample (GroupNorm: xcs = C1), every input channel
+    const size_t xs = (size_t)(g0 / H) * p.xcs;
+    for (int i = tid; i < 3 * Cin; i += NTHR) {
+      const int m = i / Cin, c = i - m * Cin;
+      Ks[i] = (m == 0 ? p.xa : m == 1 ? p.xb : p.xc)[xs + c];
+    }
+  }
 
   // halo granule u = tid + 256 c: slot u / 4 (row slot / HWP, column slot % HWP - 1), logical
   // chunk u % 4 at physical chunk ^ ((column slot >> 1) & 3); weight granule u: row u / 4 =
   // tap c x BN + n (n = tid / 4), logical chunk u % 4 at ^ ((row >> 1) & 3)
   u32x4 xv[XG], wv[WG];
+  u32x4 zq[DZ ? XG : 1];
+  uint32_t okm = 0;                                     // DZ: granules of real pixels
   auto load_chunk = [&](const int kc) {
     const bool from1 = !CONCAT || (kc << 5) < p.C1;
     const int C = from1 ? p.C1 : p.C2;
@@ -956,13 +1017,39 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_cp_kernel(const ConvFwdParam
                       (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
       xv[c] = __builtin_amdgcn_raw_buffer_load_b128(
           rs, ok ? (((gr - grow0) * W + col) * C + cb + (u & 3) * 8) * 2 : OOB, 0, 0);
+      if constexpr (DZ) {
+        zq[c] = __builtin_amdgcn_raw_buffer_load_b128(
+            rsz, ok ? (((gr - grow0) * W + col) * C + cb + (u & 3) * 8) * 2 : OOB, 0, 0);
+        okm = c ? (okm | ((ok ? 1u : 0u) << c)) : (ok ? 1u : 0u);
+      }
     }
 #pragma unroll
     for (int c = 0; c < WG; ++c)
       wv[c] = __builtin_amdgcn_raw_buffer_load_b128(
           rsw, ((n0 + (tid >> 2)) * p.Kpad + c * Cin + (kc << 5) + (tid & 3) * 8) * 2, 0, 0);
   };
-  auto store_chunk = [&]() {
+  auto store_chunk = [&](const int kc) {
+    if constexpr (DZ) {
+      // dz = ca g + (cb z + cc) of the thread's 8 channels (kc 32 + (tid & 3) 8 ..)
+      const float* kb = Ks + (kc << 5) + (tid & 3) * 8;
+      float ka[8], kz[8], kk[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ka[e] = kb[e];
+        kz[e] = kb[Cin + e];
+        kk[e] = kb[2 * Cin + e];
+      }
+#pragma unroll
+      for (int c = 0; c < XG; ++c) {
+        if (!((okm >> c) & 1u)) continue;               // padding stays zero
+        float gv[8], zv[8];
+        unpack8(xv[c], gv);
+        unpack8(zq[c], zv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gv[e] = fmaf(ka[e], gv[e], fmaf(kz[e], zv[e], kk[e]));
+        xv[c] = pack8(gv);
+      }
+    }
 #pragma unroll
     for (int c = 0; c < XG; ++c) {
       const int u = tid + NTHR * c;
@@ -990,7 +1077,8 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_cp_kernel(const ConvFwdParam
   }
   const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
   load_chunk(0);
-  store_chunk();
+  if constexpr (DZ) __syncthreads();                    // Ks written
+  store_chunk(0);
   __syncthreads();
   for (int kc = 0; kc < nchunks; ++kc) {
     if (kc + 1 < nchunks) load_chunk(kc + 1);          // in flight under this chunk's MFMAs
@@ -1015,7 +1103,7 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_cp_kernel(const ConvFwdParam
     }
     __syncthreads();                                    // fragment reads done
     if (kc + 1 < nchunks) {
-      store_chunk();
+      store_chunk(kc + 1);
       __syncthreads();
     }
   }
@@ -1027,6 +1115,16 @@ template <int W>
 hipError_t launch_win_cp_w(const ConvFwdParams& p, hipStream_t s) {
   const int grid = win_grid(p);
   const bool cc = p.C2 > 0;
+  if (p.xform == 2) {                                   // dz on load (win_cp_eligible: single source)
+    if (cc || p.C1 > CP_DZ_MAXC) return hipErrorInvalidValue;
+    if (conv_epi_mode(p) == EPI_DGRAD_NORM)
+      UNET_LAUNCH((conv_win_cp_kernel<W, false, EPI_DGRAD_NORM, true>), dim3(grid), dim3(NTHR), 0, s, p);
+    else if (conv_epi_mode(p) == EPI_DGRAD)
+      UNET_LAUNCH((conv_win_cp_kernel<W, false, EPI_DGRAD, true>), dim3(grid), dim3(NTHR), 0, s, p);
+    else
+      return hipErrorInvalidValue;
+    return launch_status();
+  }
 #define CP_EPI(CC)                                                                                           \
   switch (conv_epi_mode(p)) {                                                                                \
     case EPI_FWD: UNET_LAUNCH((conv_win_cp_kernel<W, CC, EPI_FWD>), dim3(grid), dim3(NTHR), 0, s, p); break;     \
@@ -1519,7 +1617,19 @@ hipError_t launch_win(const ConvFwdParams& p, hipStream_t s) {
 #define XF_CASE(WW)                                                                                           \
   case WW:                                                                                                    \
     if constexpr (win_tile_built<BN, BM>(WW)) {                                                               \
-      if (epi == EPI_STATS)                                                                                   \
+      if (p.xform == 2) {                                                                                     \
+        if constexpr ((BN == 64 && BM == 256 && WW <= 64) || (BN == 32 && BM == 512 && WW == 64)) {           \
+          if (epi == EPI_DGRAD_NORM)                                                                          \
+            UNET_LAUNCH((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD_NORM, GEO_2D, 2>), dim3(grid), dim3(NTHR), 0, s, \
+                        p);                                                                                   \
+          else if (epi == EPI_DGRAD)                                                                          \
+            UNET_LAUNCH((conv_win_kernel<WW, BN, BM, false, EPI_DGRAD, GEO_2D, 2>), dim3(grid), dim3(NTHR), 0, s, p); \
+          else                                                                                                \
+            return hipErrorInvalidValue;                                                                      \
+        } else {                                                                                              \
+          return hipErrorInvalidValue;                                                                        \
+        }                                                                                                     \
+      } else if (epi == EPI_STATS)                                                                            \
         UNET_LAUNCH((conv_win_kernel<WW, BN, BM, false, EPI_STATS, GEO_2D, 1>), dim3(grid), dim3(NTHR), 0, s, p); \
       else if (epi == EPI_GENERIC)                                                                            \
         UNET_LAUNCH((conv_win_kernel<WW, BN, BM, false, EPI_GENERIC, GEO_2D, 1>), dim3(grid), dim3(NTHR), 0, s, p); \

@@ -886,6 +886,13 @@ PYBIND11_MODULE(_C, m) {
     unet::conv_stat_tiles(conv_params(d), &rows, &px);
     return py::make_tuple(rows, px);
   }, py::arg("params"));
+  // validates a weight-gradient dict before its slabs exist (planning): raises like "wgrad"
+  m.def("wgrad_validate", [](const py::dict& d0) {
+    py::dict d = d0.attr("copy")();           // (a new dict: the caller's is left as is)
+    if (!d.contains("slab") || d["slab"].is_none()) d["slab"] = py::int_(256);
+    if (!d.contains("bias_slab") || d["bias_slab"].is_none()) d["bias_slab"] = py::int_(256);
+    (void)wgrad_params(d);
+  }, py::arg("params"));
   m.def("wgrad", [](const py::dict& d, uintptr_t stream, int dtype) {
     WgradParams p = wgrad_params(d);
     check(api(dtype)->wgrad_launch(p, as_stream(stream)), "wgrad");
@@ -931,8 +938,9 @@ PYBIND11_MODULE(_C, m) {
   // grid (QH, QD default to QW: square / cubic levels), a row-window candidate
   m.def(
       "wgrad_pick",
-      [](int M1, int M2, int Nc, int KT, int QW, int upA, int win, int QH, int QD) {
+      [](int M1, int M2, int Nc, int KT, int QW, int upA, int win, int QH, int QD, int xform) {
         WgradParams p{};
+        p.xform = xform;
         p.M1 = M1;
         p.M2 = M2;
         p.Nc = Nc;
@@ -972,7 +980,7 @@ PYBIND11_MODULE(_C, m) {
         return py::make_tuple(c.BM, c.BN, c.NTAP, c.smallc);
       },
       py::arg("M1"), py::arg("M2"), py::arg("Nc"), py::arg("KT"), py::arg("QW") = 0, py::arg("upA") = 1,
-      py::arg("win") = -1, py::arg("QH") = 0, py::arg("QD") = 0);
+      py::arg("win") = -1, py::arg("QH") = 0, py::arg("QD") = 0, py::arg("xform") = 0);
   m.def("packseg_bytes", []() { return (int)sizeof(PackSeg); });
   m.def("reduce_job_bytes", []() { return (int)sizeof(ReduceJob); });
   m.def("reduce_groups", &reduce_groups);

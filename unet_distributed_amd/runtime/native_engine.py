@@ -71,12 +71,14 @@ def _r64(k: int) -> int:
 #                32 -> 32 channel convs (conv_win.h conv_win_pf_kernel) (8; 0 off)
 #   win_cp       64-channel row windows on 64-wide rows load the next input chunk under the
 #                current chunk's MFMAs (conv_win.h conv_win_cp_kernel) (1; 0 off)
+#   dz_split     normalised layers on 16..64-wide rows whose dz only their own data and weight
+#                gradients read: both form it on load (conv_win.h XF 2, wgrad_win_kernel DZ) (1)
 #   wg_pair      row-window weight gradients of 32-channel output blocks with wave-pair partials
 #                (conv_wgrad.hip wgrad_win_kernel PAIR: three workgroups per CU): 1 = 3D only,
 #                2 = 2D as well, 0 off (0)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
                        tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8, win_cp=1,
-                       wg_pair=0)
+                       wg_pair=0, dz_split=1)
 
 
 class Fusion:
@@ -147,6 +149,10 @@ FUSIONS: Dict[str, Fusion] = {
     "dz_onload": Fusion("norm backward dz = ca g + cb z + cc formed in the fused data + weight gradient's "
                         "halo (conv_dw.hip XF 2): no norm_bwd_apply pass, dz never stored",
                         norm={"batch", "group"}, dims={2}, img=(128,), option="dw_fuse", needs=("dw_fused",)),
+    "dz_split": Fusion("norm backward dz formed on load by both of the layer's split consumers -- the "
+                       "row-window data gradient (conv_win.h XF 2 / chunk-pipelined DZ) and the window weight "
+                       "gradient's B operand (wgrad_win_kernel DZ): no norm_bwd_apply pass, dz never stored",
+                       norm={"batch", "group"}, dims={2}, option="dz_split", when=lambda e: e.wgrad_win >= 0),
     "first_dz_onload": Fusion("first layer's norm-backward dz formed by its window wgrad (XF 2)",
                               norm={"batch", "group"}, dims={2}, img=_ROW_IMGS, cpad=(4, 8),
                               when=lambda e: e.wgrad_win >= 0),
@@ -904,6 +910,43 @@ class NativeUNet:
                 self._fusion_on("dz_onload", l.name)
         return out
 
+    def _dz_split_fields(self, l, src1, skip):
+        """xform-2 fields (dz = ca g + cb z + cc formed on load from g = d:<l>) when conv `l`'s
+        dz is read by nothing but its own data gradient and weight gradient and both kernels
+        take the transform (FUSIONS['dz_split']): single-source 2D conv on 16..64-wide rows,
+        no fused data + weight gradient, no chained / composite consumer; else None.  The
+        decision is recorded (_dz_onload): no norm_bwd_apply pass, dz is never stored."""
+        if (not self._fusion_ok("dz_split") or skip is not None or l.name not in self.norm_layers
+                or self.inputs.get(l.name, ("",))[1] != 1 or l.name in self._wa_chain_of
+                or l.name in self._tf_consumer or (self._norm_head_loss and l.name == self.head_in)):
+            return None
+        W = self.sdims(l.level)[2]
+        if W < 16 or W > 64 or l.cin % 32 or l.cout % 32:
+            return None
+        b = self.bufs
+        xf = dict(xform=2, xa=_ptr(b["ca:" + l.name]), xb=_ptr(b["cb:" + l.name]), xc=_ptr(b["cc:" + l.name]),
+                  xz=_ptr(b["z:" + l.name]), xcs=0 if self.spec.norm == "batch" else l.cout)
+        # kernel probes: the data gradient (with its dgrad-norm epilogue, as planned) and the
+        # weight gradient, both with the transform
+        d = self._conv_common(l.level, 3, 1, 1)
+        lvl, ch, relu_src, drop = self.tinfo[src1]
+        m1, mb = self._relu_mask(src1) if relu_src else (None, 0)
+        d.update(name="dgrad:" + l.name, C1=l.cout, src1=_ptr(b["d:" + l.name]), wgt=self.wptr(l.name, "dg"),
+                 Cout=l.cin, relu=0, dst1=_ptr(b["d:" + src1]), D1=l.cin, mask1=m1, mask_bits=mb)
+        d.update(xf)                  # (the planned dgrad may carry the dgrad-norm epilogue: both take XF 2)
+        sd = self.sdims(l.level)
+        kd = dict(N=self.B, QD=sd[0], QH=sd[1], QW=sd[2], AD=sd[0], AH=sd[1], AW=sd[2], KD=1, KH=3, KW=3,
+                  stride=1, pad=1, upA=1, a1=_ptr(b[src1]), b=_ptr(b["d:" + l.name]), M1=l.cin, M2=0, Nc=l.cout,
+                  splits=1, win=self.wgrad_win, bias_mode=1, **xf)
+        try:
+            self.C.conv_fwd_grid(d)
+            self.C.wgrad_validate(kd)
+        except ValueError:
+            return None
+        self._dz_onload.add(l.name)
+        self._fusion_on("dz_split", l.name)
+        return xf
+
     def _restat_dgrad_norm(self, f, tname):
         """Fused data + weight gradient `f` whose epilogue is the dgrad-norm one (gradient of
         normalised activation `tname`): its statistics rows are per 256-pixel window, not
@@ -1270,7 +1313,8 @@ class NativeUNet:
     def _wgrad_pick(self, w):
         """Tile config of a wgrad spec; QW marks 2D 3x3 convs (row-window candidates)."""
         return self.C.wgrad_pick(w["M1"], w["M2"], w["Nc"], w["KT"], QW=w.get("QW", 0), upA=w.get("upA", 1),
-                                 win=self.wgrad_win, QH=w.get("QH", 0), QD=w.get("QD", 0))
+                                 win=self.wgrad_win, QH=w.get("QH", 0), QD=w.get("QD", 0),
+                                 xform=w["kd"].get("xform", 0) if "kd" in w else 0)
 
     def _wgrad_splits(self, w):
         M1, M2, Nc, KT, Q = w["M1"], w["M2"], w["Nc"], w["KT"], w["Q"]
@@ -1370,8 +1414,11 @@ class NativeUNet:
                         first_xf = dict(xform=2, xa=_ptr(b["ca:" + l.name]), xb=_ptr(b["cb:" + l.name]),
                                         xc=_ptr(b["cc:" + l.name]), xz=_ptr(b["z:" + l.name]),
                                         xcs=0 if spec.norm == "batch" else l.cout)
-                    ops.extend(self._norm_bwd_ops(l, apply=first_xf is None))
-                    dy = b["dz:" + l.name] if first_xf is None else b["d:" + l.name]
+                    split_xf = None
+                    if first_xf is None and not first:
+                        split_xf = self._dz_split_fields(l, src1, skip)
+                    ops.extend(self._norm_bwd_ops(l, apply=first_xf is None and split_xf is None))
+                    dy = b["dz:" + l.name] if first_xf is None and split_xf is None else b["d:" + l.name]
                 Q = self.npix(l.level)
                 # --- weight + bias gradient (fused column sums); the upsampling decoder's
                 # A operand is the materialised upsample when there is one
@@ -1391,6 +1438,8 @@ class NativeUNet:
                           b=_ptr(dy))
                 if first_xf is not None:
                     kd.update(first_xf)
+                if spec.norm != "none" and split_xf is not None:
+                    kd.update(split_xf)
                 if l.name == self.head_in and self.head_onload:
                     kd.update(self._head_grad_fields())
                 wspec = dict(lname=l.name, kd=kd, M1=c1w, M2=c2w, Nc=l.cout, KT=KT3, Q=Q,
@@ -1463,6 +1512,8 @@ class NativeUNet:
                             self._rev_order(d, "g:" + l.name, "g:" + src1)
                         return d
                     dd_ = mk()                 # built now: it decides the fused norm backward
+                    if spec.norm != "none" and split_xf is not None:
+                        dd_.update(split_xf)
                     halves = self._tail_halves(dd_, l, src1, skip, dy)
                     parts = self._plan_dw_fuse(l, src1, skip, [dd_] if halves is None else list(halves), wspec)
                     if parts is not None:
