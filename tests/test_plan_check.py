@@ -140,3 +140,20 @@ def test_write_extent_overrun_is_flagged():
     e.plan.ops[k]["spans"][0] = (p + 64, n)
     errs = check_plan(e, e.plan, True)
     assert any("past its end" in m for m in errs), errs
+
+
+@pytest.mark.parametrize("norm,img", [("batch", 128), ("group", 128), ("batch", 64), ("group", 32)])
+def test_dz_split_option_plans_validate(norm, img):
+    """Option dz_split=1 (measured slower, off by default): the normalised layers on 16..64-wide
+    rows whose dz only their own data / weight gradients read form it on load; their
+    norm_bwd_apply passes and dz buffers are gone and the plan still validates (no op reads
+    a dropped dz)."""
+    e0 = _engine(norm, False, 2, img, batch=8)
+    e1 = _engine(norm, False, 2, img, batch=8, opts=dict(dz_split=1))
+    assert check_engine(e1) == {"train": [], "eval": []}
+    lay = e1.fusions.get("dz_split", [])
+    assert lay and not e0.fusions.get("dz_split")
+    n0 = [n for n in e0.plan.names() if n.startswith("norm_bwd:")]
+    n1 = [n for n in e1.plan.names() if n.startswith("norm_bwd:")]
+    assert sorted(set(n0) - set(n1)) == sorted("norm_bwd:" + l for l in lay)
+    assert all("dz:" + l not in e1.bufs for l in lay)

@@ -648,6 +648,12 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
   float* Ks = (float*)(smem + XB + YB);
   const int dzl = (tid & 3) ^ (((tid >> 5) & 1) << 1);
   int ks_n = -1;                                        // sample whose coefficients Ks holds
+  // CARRY (128-wide rows, 2D / 3D: two-row windows, four halo rows): consecutive windows of
+  // one image share two halo rows -- the previous window's logical rows 2, 3 are the next
+  // one's 0, 1 -- so only two new rows are DMA'd (18 of 36 KB) and logical row r lives at
+  // physical row r ^ 2 fl, fl flipping with every carry (conv_dw.hip's halo-row carry)
+  constexpr bool CARRY = UNITS_PATH && W == 128 && (GEO == WGEO_2D || GEO == WGEO_3D);
+  int fl = 0, prev = -2;
   for (int win = w_begin; win < w_end; ++win) {
     const int g0 = (GEO == WGEO_SEG ? win / nseg : win) * R;
     const int col0 = GEO == WGEO_SEG ? (win % nseg) * W : 0;
@@ -656,6 +662,13 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
     if (GEO == WGEO_3D && (unsigned)((g0 / H) % D + kd - 1) >= (unsigned)D) continue;
     const bool zero_halo = UNITS_PATH || pair_ok;
     const bool top_in = !zero_halo || (g0 % H) != 0, bot_in = !zero_halo || ((g0 + R) % H) != 0;
+    // (top_in: the previous window's bottom halo rows are this image's rows, not zeros)
+    const bool carry = CARRY && prev == win - 1 && top_in;
+    if constexpr (CARRY) {
+      fl = carry ? fl ^ 1 : 0;
+      prev = win;
+    }
+    const int kb = carry ? 2 * IPR : 0;                 // first halo piece to load
     const int rb = max(g0 - 1 + gsh, 0);             // first halo row held by rsa
     const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(abase + (size_t)rb * Wf * CA * 2), (short)0, OOB, 0x00020000);
@@ -666,7 +679,7 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
     __syncthreads();   // the previous window's fragment reads are done
 #pragma unroll
     for (int qq = 0; qq < (XI + 3) / 4; ++qq) {
-      const int k = wave + 4 * qq;
+      const int k = kb + wave + 4 * qq;
       if (k < XI) {
         const int hr = k / IPR, j = k - hr * IPR;
         const int gr = g0 - 1 + hr + gsh;
@@ -675,7 +688,8 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
         const bool ok = row_in && (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)Wf &&
                         (GEO != WGEO_SEG || 16 * j + lslot <= W + 1);
         const int off = ok ? ((gr - rb) * Wf + col0 + 16 * j) * CA * 2 + ((ROWSWZ && (hr & 1)) ? xl_odd : xl) : OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (__attribute__((address_space(3))) void*)(Xs + k * 1024), 16,
+        const int pk = CARRY && fl ? k + (hr < 2 ? 2 * IPR : -2 * IPR) : k;   // (CARRY: physical row hr ^ 2 fl)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (__attribute__((address_space(3))) void*)(Xs + pk * 1024), 16,
                                                  off, 0, 0, 0);
       }
     }
@@ -766,6 +780,9 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
       constexpr int RWG = R / RG;
       constexpr int UNITS = NCOL * RG;
       static_assert(R % RG == 0 && RWG >= 1, "wgrad column units");
+      static_assert(!CARRY || (RWG == R && R == 2), "halo-row carry: one two-row unit per column");
+      // CARRY: logical halo row hr at physical hr ^ 2 fl -- rows 0, 1 shifted by +xsh, 2, 3 by -xsh
+      const int xsh = (CARRY && fl) ? 2 * ROWB : 0;
       const int lp = 8 * G + q;
 #pragma unroll 1
       for (int u = ps; u < UNITS; u += PSP) {
@@ -809,7 +826,10 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
           for (int dw = 0; dw < 3; ++dw) {
             h16x8 af[2];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) af[i] = tr8(Xs + ab[dw][i][0] + hr * ROWB, Xs + ab[dw][i][1] + hr * ROWB);
+            for (int i = 0; i < 2; ++i) {
+              const int ro = hr * ROWB + (CARRY ? (hr < 2 ? xsh : -xsh) : 0);
+              af[i] = tr8(Xs + ab[dw][i][0] + ro, Xs + ab[dw][i][1] + ro);
+            }
 #pragma unroll
             for (int dh = 0; dh < 3; ++dh) {
               const int y = hr - dh;
@@ -1585,7 +1605,7 @@ hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
     }
     return hipErrorInvalidValue;
   }
-  if constexpr (QO == 1 && W >= 32) {
+  if constexpr (QO == 1 && W >= 32 && W <= 64) {      // (128-wide rows: 61 VGPRs spilled, 2x slower)
     if (p.pair) {
       if (p.M2 > 0)
         UNET_LAUNCH((wgrad_win_kernel<W, QO, true, GEO, false, true>), dim3(grid), dim3(NTHR), 0, s, p);

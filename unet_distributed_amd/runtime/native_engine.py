@@ -72,13 +72,15 @@ def _r64(k: int) -> int:
 #   win_cp       64-channel row windows on 64-wide rows load the next input chunk under the
 #                current chunk's MFMAs (conv_win.h conv_win_cp_kernel) (1; 0 off)
 #   dz_split     normalised layers on 16..64-wide rows whose dz only their own data and weight
-#                gradients read: both form it on load (conv_win.h XF 2, wgrad_win_kernel DZ) (1)
+#                gradients read: both form it on load (conv_win.h XF 2, wgrad_win_kernel DZ) (0:
+#                measured slower, r6_bench_history.md -- the consumers' per-window z loads and
+#                transform cost more than the norm_bwd_apply pass they replace)
 #   wg_pair      row-window weight gradients of 32-channel output blocks with wave-pair partials
 #                (conv_wgrad.hip wgrad_win_kernel PAIR: three workgroups per CU): 1 = 3D only,
 #                2 = 2D as well, 0 off (0)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
                        tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8, win_cp=1,
-                       wg_pair=0, dz_split=1)
+                       wg_pair=0, dz_split=0)
 
 
 class Fusion:
@@ -1067,7 +1069,9 @@ class NativeUNet:
         separate norm_apply pass).  Decided once, for the training and the evaluation
         plans alike.  (Measured and dropped in round 2: the consumer's weight gradient
         normalising on load too, -1.3 % BN / -1.5 % GN; dz formed on load by the data
-        gradient, -1.1 % BN; level-1 dgrad + wgrad both forming dz, -1.2 % BN.)"""
+        gradient, -1.1 % BN; level-1 dgrad + wgrad both forming dz, -1.2 % BN.  Round 6 rebuilt
+        the last two: level 1 in the fused conv_dw window (kept), levels 2-4 in the split
+        consumers -- option dz_split, -3.2 % BN, off.)"""
         self._xf_fwd = set()
         if not self._fusion_ok("norm_onload"):
             return
