@@ -403,7 +403,9 @@ def test_head_onload_step_equals_materialised(cuda_dev, monkeypatch, kw):
     for v in ("0", "2"):
         # (head_onload=2: 3D too; dw_fuse=0: with head_onload=0 the head input conv's weight gradient would run in
         # the fused data + weight gradient kernel, a different fp32 summation order)
-        monkeypatch.setenv("UNET_ENGINE", "dw_fuse=0,head_onload=" + v)
+        # (head_wsum=0: the Mask gradients from head_bwd on both sides -- the forward sums
+        # of head_wsum round differently, test_head_wsum_step_matches below)
+        monkeypatch.setenv("UNET_ENGINE", "dw_fuse=0,head_wsum=0,head_onload=" + v)
         spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
         e = nb.engine
         assert e.head_onload == (v == "2")
@@ -415,6 +417,36 @@ def test_head_onload_step_equals_materialised(cuda_dev, monkeypatch, kw):
     (s0, p0, g0), (s1, p1, g1) = outs
     assert torch.equal(s0, s1) and torch.equal(p0, p1)
     assert torch.equal(g0, g1)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(batch_size=4, img_size=128, in_channels=4),
+    dict(batch_size=6, img_size=128, in_channels=4, loss="dice_bce", hip_graph=True),
+    dict(batch_size=2, img_size=128, in_channels=4, dtype="fp16"),
+])
+def test_head_wsum_step_matches(cuda_dev, monkeypatch, kw):
+    """head_wsum=1 (default: the Mask gradients from per-workgroup sums of the fused-head
+    forward, the head input never stored) vs head_wsum=0 (head_bwd re-reads the stored head
+    input): identical loss sums, probabilities and every other gradient bit for bit; the
+    Mask weight / bias gradients equal up to fp32 summation order."""
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("UNET_ENGINE", "head_wsum=" + v)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
+        e = nb.engine
+        assert bool(e.fusions.get("head_wsum")) == (v == "1")
+        for seed in (61, 62):
+            nb.fwd_bwd(x, y, seed=seed)
+        torch.cuda.synchronize()
+        outs.append((nb.sums().cpu(), e.prob.clone(), {k: fn.view(fn.grad, k).clone() for k, *_ in fn.entries}))
+    (s0, p0, g0), (s1, p1, g1) = outs
+    assert torch.equal(s0, s1) and torch.equal(p0, p1)
+    for k in g0:
+        if k.startswith("Mask/"):
+            err = ((g1[k] - g0[k]).abs().max() / (g0[k].abs().max() + 1e-12)).item()
+            assert err < 1e-4, (k, err)
+        else:
+            assert torch.equal(g0[k], g1[k]), k
 
 
 @pytest.mark.parametrize("kw", [

@@ -43,7 +43,7 @@ def test_every_plan_validates(norm, ups, dims, img):
 
 def test_headline_plan_applies_the_measured_fusions():
     e = _engine("none", False, 2, 128)
-    assert sorted(e.fusions) == sorted(["head_onload", "head_fuse", "pool_epilogue", "tconv_fused", "tconv_wa", "dw_fused",
+    assert sorted(e.fusions) == sorted(["head_onload", "head_fuse", "head_wsum", "pool_epilogue", "tconv_fused", "tconv_wa", "dw_fused",
                                         "tconv_onload", "skip_route", "tail_halves"])
     assert e.fusions["tconv_onload"] == ["transConv9"]
 

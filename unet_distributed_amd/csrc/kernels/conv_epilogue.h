@@ -92,6 +92,14 @@ struct EpiConst {
   float hb;
 };
 
+// Mask weight-gradient sums a persistent fused-head caller accumulates over its windows
+// (conv_params.h head_ws): the thread's 8 channels' {sum u y, sum v y, sum w y} and, on the
+// pixel's chunk-0 lane, {sum u, sum v, sum w}
+struct HeadWsum {
+  float s[3][8];
+  float u, v, w;
+};
+
 // SEGW > 0: the tile is a row window of SEGW-wide row segments (window kernels on rows
 // wider than one window, or any row-window kernel): tile pixel ml is at row
 // m0 + ml / SEGW (m0 = first row), column col0 + ml % SEGW of rows `pitch` pixels wide.
@@ -104,7 +112,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
                                               const int m0, const int n0, const int M, const int wm,
                                               const int wn, const int lane, const int tid,
                                               const int pitch = 0, const int col0 = 0, const int stat_row = 0,
-                                              const EpiConst<TN>* ec = nullptr) {
+                                              const EpiConst<TN>* ec = nullptr, HeadWsum* hws = nullptr) {
   auto qof = [&](int ml) -> int {
     if constexpr (SEGW > 0) return (m0 + ml / SEGW) * pitch + col0 + (ml % SEGW);
     else return m0 + ml;
@@ -492,7 +500,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       // (off is a multiple of 8: the bit tensor's byte of these 8 channels is off / 8)
       v = mbit ? keep_bits(v, ((const uint8_t*)mk)[off >> 3]) : keep_pos(v, *(const u32x4*)((const h16*)mk + off));
     }
-    *(u32x4*)(dst + off) = v;
+    if (!(kHeadable && kHead && p.head_nostore)) *(u32x4*)(dst + off) = v;
     // (EPI_FWD: ReLU outputs from relu2h, never -0 -- the cheap form)
     if (EPI == EPI_FWD && p.relu_bits) p.relu_bits[off >> 3] = (uint8_t)pos_bits_relu(v);
     if (G && p.relu_bits) p.relu_bits[off >> 3] = (uint8_t)pos_bits(v);
@@ -507,6 +515,25 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
         z += __shfl_xor(z, 2, 64);
         hz[it] = z + hb;
         hq[it] = q;
+        if (hws) {
+          // the probability head_finish will form from this logit, the target: the Mask
+          // weight gradient's per-pixel factors (head_grad.h head_dlogit = A u + B v + G w)
+          const float zl = z + hb;
+          const float pr = 1.f / (1.f + __expf(-zl));
+          const float tv = bits2f(((const uint16_t*)p.head_t)[q]);
+          const float vv = pr * (1.f - pr), uu = tv * vv, ww = pr - tv;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            hws->s[0][e] = fmaf(uu, f[e], hws->s[0][e]);
+            hws->s[1][e] = fmaf(vv, f[e], hws->s[1][e]);
+            hws->s[2][e] = fmaf(ww, f[e], hws->s[2][e]);
+          }
+          if (cb == 0) {
+            hws->u += uu;
+            hws->v += vv;
+            hws->w += ww;
+          }
+        }
       }
     }
   }

@@ -1146,6 +1146,10 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
         conv_epi_mode(p) != EPI_FWD || conv_fwd_pick(p) != 6)
       return "conv_fwd: fused head needs a 32-channel ReLU row-window forward";
   }
+  if ((p.head_ws || p.head_nostore) &&
+      (!p.head_w || !win_pf_eligible(p) || p.OW != 128 || (p.head_ws && !p.head_t) || !p.relu_bits))
+    return "conv_fwd: Mask weight sums / an unstored head input need the persistent 128-wide fused-head window "
+           "with ReLU bits";
   if ((long long)p.N * p.ID * p.IH * p.IW >= (1LL << 31) || (long long)p.N * p.OD * p.OH * p.OW >= (1LL << 31))
     return "conv_fwd: too many pixels";
   // buffer loads use 32-bit byte offsets: the row-window kernels count them from the

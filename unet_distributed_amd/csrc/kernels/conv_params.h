@@ -146,6 +146,15 @@ struct ConvFwdParams {
   const float* head_w;
   const float* head_b;
   float* head_logit;
+  // Mask weight-gradient sums in the forward (conv_win_pf_kernel with the fused head): per
+  // pixel u = t p (1 - p), v = p (1 - p), w = p - t (p = sigmoid(logit), t = head_t) and
+  // one row per workgroup of head_ws: {sum u y_c, sum v y_c, sum w y_c} (3 x 32 channel-major
+  // blocks), sum u, sum v, sum w, pad -- head.hip head_wsum_grad turns them into the Mask
+  // gradients once the loss sums are known.  head_nostore: the activation itself is not
+  // stored (its ReLU bits are): nothing else reads it.
+  const void* head_t;
+  float* head_ws;
+  int head_nostore;
   int rev;                    // row-window kernels: windows in reverse order (the consumer starts
                               // where its producer ended, on the tail still in the Infinity Cache)
   int win_pf;                 // > 0: 2D 128-wide 32 -> 32 channel row windows run persistently,

@@ -878,6 +878,13 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
 #pragma unroll
   for (int e = 0; e < 8; ++e) ec.hw[e] = (EPI == EPI_FWD && p.head_w) ? p.head_w[(tid % 4) * 8 + e] : 0.f;
   ec.hb = (EPI == EPI_FWD && p.head_w) ? p.head_b[0] : 0.f;
+  HeadWsum hws;
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) hws.s[k][e] = 0.f;
+  hws.u = hws.v = hws.w = 0.f;
+  HeadWsum* hwp = (EPI == EPI_FWD && !SEG && p.head_ws) ? &hws : nullptr;
   store_halo();
   __syncthreads();
 
@@ -926,11 +933,44 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
                                                                     col0, tm, &ec);
     else
       conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(p, acc, smem, g0 * W, 0, M, wave, 0, lane, tid, 0,
-                                                                    0, tm, &ec);
+                                                                    0, tm, &ec, hwp);
     if (w + 1 < w_hi) {
       __syncthreads();                               // staging reads done
       store_halo();
       __syncthreads();
+    }
+  }
+  if constexpr (EPI == EPI_FWD && !SEG) {
+    if (p.head_ws) {
+      // the workgroup's Mask weight sums -> row blockIdx.x: lanes l, l ^ 4, .. hold the same 8
+      // channels (chunk tid & 3), folded in a fixed order, then the 4 waves through LDS
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+          for (int o = 4; o < 64; o <<= 1) hws.s[k][e] += __shfl_xor(hws.s[k][e], o, 64);
+      hws.u = wave_sum(hws.u);
+      hws.v = wave_sum(hws.v);
+      hws.w = wave_sum(hws.w);
+      float* red = (float*)smem;                     // [wave][100]
+      __syncthreads();                               // the last epilogue's staging reads are done
+      if (lane < 4) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) red[wave * 100 + k * 32 + lane * 8 + e] = hws.s[k][e];
+      }
+      if (lane == 0) {
+        red[wave * 100 + 96] = hws.u;
+        red[wave * 100 + 97] = hws.v;
+        red[wave * 100 + 98] = hws.w;
+        red[wave * 100 + 99] = 0.f;
+      }
+      __syncthreads();
+      if (tid < 100)
+        p.head_ws[(size_t)blockIdx.x * 100 + tid] =
+            (red[tid] + red[100 + tid]) + (red[200 + tid] + red[300 + tid]);
     }
   }
 }

@@ -197,6 +197,47 @@ __global__ void __launch_bounds__(HT) head_bwd_kernel(const h16* __restrict__ x,
   }
 }
 
+// Mask gradients from the forward's sums (conv_params.h head_ws; conv_win_pf_kernel with the
+// fused head): head_grad.h's dlogit = A u + B v + G w per pixel with the batch scalars
+// A = a gs, B = bb gs, G = bce_w inv_total gs, so
+//   grad_w[c] = A sum u y_c + B sum v y_c + G sum w y_c,   grad_b = A sum u + B sum v + G sum w
+// -- the head input need not be re-read (nor stored).  Block j < 32: channel j, block 32:
+// the bias; fixed-order column sums over the rows.
+__global__ void __launch_bounds__(256) head_wsum_grad_kernel(const float* __restrict__ rows, int nr,
+                                                             const float* __restrict__ sums, float inv_total,
+                                                             float bce_w, float gscale,
+                                                             const float* __restrict__ gscale_ptr,
+                                                             float* __restrict__ gw, float* __restrict__ gb) {
+  __shared__ float red[3][256];
+  if (gscale_ptr) gscale = *gscale_ptr;
+  const int j = blockIdx.x;
+  float s[3] = {0.f, 0.f, 0.f};
+  for (int k = threadIdx.x; k < nr; k += 256) {
+#pragma unroll
+    for (int m = 0; m < 3; ++m) s[m] += rows[(size_t)k * 100 + (j < 32 ? 32 * m + j : 96 + m)];
+  }
+#pragma unroll
+  for (int m = 0; m < 3; ++m) red[m][threadIdx.x] = s[m];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+#pragma unroll
+      for (int m = 0; m < 3; ++m) red[m][threadIdx.x] += red[m][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float I = sums[0], St = sums[1], Sp = sums[2];
+    const float a = -2.f / (2.f * I + 1.f);
+    const float bb = 1.f / (St + Sp + 1.f);
+    const float g = (a * gscale) * red[0][0] + (bb * gscale) * red[1][0] + (bce_w * inv_total * gscale) * red[2][0];
+    if (j < 32)
+      gw[j] = g;
+    else
+      gb[0] = g;
+  }
+}
+
 // grad_w[c] = sum_b partial[b][c], grad_b = sum_b partial[b][C]: one block per column
 __global__ void __launch_bounds__(256) head_grad_reduce_kernel(const float* __restrict__ partial, int nb, int C,
                                                                float* __restrict__ gw, float* __restrict__ gb) {
@@ -270,6 +311,13 @@ hipError_t head_bwd_launch(const void* x, const float* w, const float* prob, con
                          sums, P, inv_total, bce_w, gscale, gscale_ptr, (h16*)dx, partial);
   }
   UNET_LAUNCH(head_grad_reduce_kernel, dim3(C + 1), dim3(256), 0, s, partial, nb, C, gw, gb);
+  return launch_status();
+}
+
+hipError_t head_wsum_grad_launch(const float* rows, int nrows, const float* sums, float inv_total, float bce_w,
+                                 float gscale, const float* gscale_ptr, float* gw, float* gb, hipStream_t s) {
+  UNET_LAUNCH(head_wsum_grad_kernel, dim3(33), dim3(256), 0, s, rows, nrows, sums, inv_total, bce_w, gscale,
+              gscale_ptr, gw, gb);
   return launch_status();
 }
 
@@ -446,27 +494,35 @@ __global__ void __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2))) no
   // step u are formed by lane cc = u of each pixel group, so the transcendental tail runs
   // once per pixel across the group instead of on one lane while the other CP - 1 idle
   // (it was most of the kernel's VALU time)
-  constexpr int KU = CP;
+  // (KH groups of KU steps per iteration: 2 KU loads of 16 bytes in flight per lane -- with
+  // one group the pass ran at 2.8 TB/s, latency-bound at two waves per SIMD)
+  constexpr int KU = CP, KH = 2;
   int p = p0 + pr0;
-  for (; p + (KU - 1) * PPB < p1; p += KU * PPB) {
-    u32x4 raw[KU];
-    float tv[KU], zl[KU], pr[KU];
+  for (; p + (KH * KU - 1) * PPB < p1; p += KH * KU * PPB) {
+    u32x4 raw[KH][KU];
+    float tv[KH][KU];
 #pragma unroll
-    for (int u = 0; u < KU; ++u) {
-      const size_t q = sb + p + u * PPB;
-      raw[u] = *(const u32x4*)(z + q * C + c0);
-      tv[u] = (float)t[q];
+    for (int h = 0; h < KH; ++h)
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const size_t q = sb + p + (h * KU + u) * PPB;
+        raw[h][u] = *(const u32x4*)(z + q * C + c0);
+        tv[h][u] = (float)t[q];
+      }
+#pragma unroll
+    for (int h = 0; h < KH; ++h) {
+      float zl[KU], pr[KU];
+#pragma unroll
+      for (int u = 0; u < KU; ++u) pixel(raw[h][u], tv[h][u], sb + p + (h * KU + u) * PPB, zl[u], pr[u]);
+      float zs = zl[0], ps = pr[0], ts = tv[h][0];
+#pragma unroll
+      for (int u = 1; u < KU; ++u) {
+        zs = cc == u ? zl[u] : zs;
+        ps = cc == u ? pr[u] : ps;
+        ts = cc == u ? tv[h][u] : ts;
+      }
+      scalars(zs, ps, ts, sb + p + (h * KU + cc) * PPB);
     }
-#pragma unroll
-    for (int u = 0; u < KU; ++u) pixel(raw[u], tv[u], sb + p + u * PPB, zl[u], pr[u]);
-    float zs = zl[0], ps = pr[0], ts = tv[0];
-#pragma unroll
-    for (int u = 1; u < KU; ++u) {
-      zs = cc == u ? zl[u] : zs;
-      ps = cc == u ? pr[u] : ps;
-      ts = cc == u ? tv[u] : ts;
-    }
-    scalars(zs, ps, ts, sb + p + cc * PPB);
   }
   for (; p < p1; p += PPB) {
     const size_t q = sb + p;

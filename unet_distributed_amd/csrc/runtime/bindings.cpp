@@ -150,8 +150,12 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.head_w = (const float*)getp(d, "head_w");
   p.head_b = (const float*)getp(d, "head_b");
   p.head_logit = (float*)const_cast<void*>(getp(d, "head_logit"));
+  p.head_t = getp(d, "head_t");
+  p.head_ws = (float*)const_cast<void*>(getp(d, "head_ws"));
+  p.head_nostore = get<int>(d, "head_nostore", 0);
   p.hg = head_grad(d);
-  if (!p.src1 || !p.wgt || !p.dst1) throw std::invalid_argument("conv_fwd: src1/wgt/dst1 required");
+  if (!p.src1 || !p.wgt || (!p.dst1 && !(p.head_nostore && p.head_w)))
+    throw std::invalid_argument("conv_fwd: src1/wgt/dst1 required");
   check_msg(conv_fwd_prepare(p));
   return p;
 }
@@ -279,6 +283,7 @@ F32Wgrad f32_wgrad_params(const py::dict& d) {
   X(upsample2_fwd_launch) \
   X(head_fwd_launch) \
   X(head_bwd_launch) \
+  X(head_wsum_grad_launch) \
   X(partial_reduce_launch) \
   X(head_finish_launch) \
   X(norm_head_launch) \
@@ -565,6 +570,16 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     return [=](hipStream_t s) {
       return A->head_bwd_launch(x, w, prob, t, sums, P_, C, it, bw, gs, gsp, dx, part, gw, gb, s);
     };
+  }
+  if (kind == "head_wsum_grad") {
+    // ptrs: rows (head_ws), sums, gw, gb [, device loss scale]   ints: nrows   floats: inv_total, bce_w, gscale
+    need(4, 1, 3);
+    const float *rows = (const float*)vp(0), *sums = (const float*)vp(1);
+    float *gw = (float*)vp(2), *gb = (float*)vp(3);
+    const float* gsp = P.size() > 4 ? (const float*)vp(4) : nullptr;
+    const int nr = (int)I[0];
+    const float it = (float)F[0], bw = (float)F[1], gs = (float)F[2];
+    return [=](hipStream_t s) { return A->head_wsum_grad_launch(rows, nr, sums, it, bw, gs, gsp, gw, gb, s); };
   }
   if (kind == "norm_moments") {
     // ptrs: A, B, partial, S   ints: N, P, C    (S[n][2][C] = per-sample sums of A and A*B)

@@ -57,6 +57,8 @@ def _r64(k: int) -> int:
 #   fwd_streams  training forward as two half-batch chunks on two streams (2)
 #   head_fuse    Mask head in the epilogue of its input conv's forward (1)
 #   head_onload  the head input's gradient formed on load by its consumers (1: 2D; 2: 3D too)
+#   head_wsum    the Mask gradients from per-workgroup sums of the fused-head forward; the head
+#                input is not stored (1)
 #   tconv_fused  deepest fine level whose transposed conv runs the composite backward (2; 0 off)
 #   tconv_wa     the consumer conv's u-row weight gradient from the composite backward's
 #                slab sums (1; 0: full weight gradient over u)
@@ -80,7 +82,7 @@ def _r64(k: int) -> int:
 #                2 = 2D as well, 0 off (0)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
                        tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8, win_cp=1,
-                       wg_pair=0, dz_split=0)
+                       wg_pair=0, dz_split=0, head_wsum=1)
 
 
 class Fusion:
@@ -130,6 +132,9 @@ FUSIONS: Dict[str, Fusion] = {
                           # the 3D weight gradient re-forms each depth tap's head gradient)
     "head_fuse": Fusion("Mask head in the epilogue of its input conv's forward",
                         norm={"none"}, option="head_fuse", when=lambda e: e.tinfo[e.head_in][1] == 32),
+    "head_wsum": Fusion("Mask weight / bias gradients from sums the head-input conv's forward accumulates "
+                        "(conv_params.h head_ws): no backward pass over the head input, which is never stored",
+                        norm={"none"}, dims={2}, option="head_wsum", needs=("head_fuse", "head_onload")),
     "pool_epilogue": Fusion("2x2 max-pool in the convNb forward epilogue", norm={"none"}),
     "fwd_2streams": Fusion("training forward as two half-batch chunks on two streams",
                            norm={"none", "group"}, even_batch=True, when=lambda e: e.opts["fwd_streams"] == 2),
@@ -1233,6 +1238,8 @@ class NativeUNet:
                     d.update(head_w=self.master_ptr("Mask/kernel"), head_b=self.master_ptr("Mask/bias"),
                              head_logit=_ptr(self.prob) + 4 * c * nb * (self.npix(1) // self.B))
                     self._head_fused_blocks = nbk
+                    if train:
+                        self._plan_head_wsum(d, l, c, nb, nch)
             self._rev_order(d, src1, l.name, pool if pool in self._pool_fused else None)
             fused = None
             if normed and (train or spec.norm == "group"):
@@ -1299,6 +1306,30 @@ class NativeUNet:
 
     def _fwd2_active(self, plan):
         return plan is self.plan and getattr(self, "_fwd2", None) is not None and self._fwd_streams(True) == 2
+
+    def _plan_head_wsum(self, d, l, c, nb, nch):
+        """FUSIONS['head_wsum']: the fused-head forward of chunk c also accumulates the Mask
+        weight-gradient sums (one 100-float row per workgroup into self.head_ws) and does not
+        store the head input -- its only other reader was the head backward's weight
+        gradient (head-on-load: the data gradients form dY from the probability, target and
+        ReLU bits).  `d` is updated in place when the kernel takes it."""
+        if not self._fusion_ok("head_wsum", l.name):
+            return
+        P = self.npix(1) // self.B
+        probe = dict(d, head_t=_ptr(self.target), head_ws=1, head_nostore=1, dst1=None)
+        try:
+            grid = int(self.C.conv_fwd_grid(probe))
+        except ValueError:
+            return
+        if grid <= 0:
+            return
+        if getattr(self, "head_ws", None) is None or self.head_ws.numel() < nch * grid * 100:
+            self.head_ws = torch.zeros(nch * grid * 100, dtype=torch.float32, device=self.device)
+            self._head_ws_rows = 0
+        d.update(head_t=_ptr(self.target) + 2 * c * nb * P, head_ws=_ptr(self.head_ws) + 4 * c * grid * 100,
+                 head_ws_rows=grid, head_nostore=1, dst1=None)
+        self._head_ws_rows = max(self._head_ws_rows, (c + 1) * grid)
+        self._fusion_on("head_wsum", l.name)
 
     def _head_grid(self, d):
         """Workgroups of the head-input conv when its forward can carry the fused
@@ -1387,6 +1418,13 @@ class NativeUNet:
                                             _ptr(self.loss_scale_dev)],
                              [Nb, Pb, hc, 0 if spec.norm == "batch" else hc], [inv_total, self.bce_weight, 1.0],
                              "bwd:Mask")
+                done("Mask")
+            elif l.kind == "mask" and self.fusions.get("head_wsum"):
+                # the Mask gradients from the forward's per-workgroup sums (head_ws)
+                emit_generic("head_wsum_grad",
+                             lambda: [_ptr(self.head_ws), _ptr(self.sums), self.grad_ptr("Mask/kernel"),
+                                      self.grad_ptr("Mask/bias"), _ptr(self.loss_scale_dev)],
+                             [self._head_ws_rows], [inv_total, self.bce_weight, 1.0], "wgrad:Mask")
                 done("Mask")
             elif l.kind == "mask":
                 hc = self.tinfo[self.head_in][1]

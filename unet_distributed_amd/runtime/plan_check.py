@@ -27,8 +27,9 @@ import torch
 
 _HG = ("hg_prob", "hg_t", "hg_sums", "hg_w", "hg_bits", "hg_gscale", "hg_fa", "hg_fc")
 CONV_READS = ("src1", "src2", "wgt", "bias", "mask1", "mask2", "route_gy", "nz", "na", "nc", "xa", "xb", "xc", "xz",
-              "ut_x", "ut_w", "ut_b", "head_w", "head_b", "fw_x") + _HG
-CONV_WRITES = ("dst1", "dst2", "stats", "relu_bits", "pool_dst", "head_logit", "xout", "fw_slab", "fw_bias_slab")
+              "ut_x", "ut_w", "ut_b", "head_w", "head_b", "head_t", "fw_x") + _HG
+CONV_WRITES = ("dst1", "dst2", "stats", "relu_bits", "pool_dst", "head_logit", "head_ws", "xout", "fw_slab",
+               "fw_bias_slab")
 WGRAD_READS = ("a1", "a2", "b", "xa", "xb", "xc", "xz") + _HG
 WGRAD_WRITES = ("slab", "bias_slab")
 
@@ -57,6 +58,8 @@ def _conv_write_spans(d, stat_tiles=None) -> List[Tuple[int, int]]:
         out.append((g("relu_bits"), M * Cout // 8))
     if g("head_logit"):
         out.append((g("head_logit"), M * 4))
+    if g("head_ws"):
+        out.append((g("head_ws"), g("head_ws_rows", 0) * 100 * 4))
     if g("pool_dst"):
         out.append((g("pool_dst"), M // 4 * Cout * 2))
         out.append((g("pool_code"), M // 4 * Cout // 8 * 4))
@@ -113,6 +116,8 @@ def _generic_rw(kind: str, p: List[int], ints: List[int]) -> Tuple[List[int], Li
         return _sel(p, [0, 1]), _sel(p, [0, 2, 3])
     if kind == "head_fwd":
         return _sel(p, [0, 1, 2, 3]), _sel(p, [4, 5, 6])
+    if kind == "head_wsum_grad":
+        return _sel(p, [0, 1, 4]), _sel(p, [2, 3])
     if kind == "head_bwd":
         return _sel(p, [0, 1, 2, 3, 4, 9]), _sel(p, [5, 6, 7, 8])
     if kind == "norm_head":
@@ -241,7 +246,7 @@ def engine_regions(e) -> Tuple[_Regions, set]:
         R.add("stat:" + k, t)
         if k.startswith("w"):                    # bn/gn_stats workspaces (self-contained)
             inputs.add("stat:" + k)
-    for k in ("prob", "target", "sums", "head_partial", "slab", "bias_slab", "red_stage", "arena",
+    for k in ("prob", "target", "sums", "head_partial", "head_ws", "slab", "bias_slab", "red_stage", "arena",
               "loss_scale_dev", "_no_dy"):
         R.add(k, getattr(e, k, None))
     inputs |= {"target", "arena", "loss_scale_dev", "_no_dy"}
