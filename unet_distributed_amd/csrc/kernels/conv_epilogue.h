@@ -92,12 +92,19 @@ struct EpiConst {
   float hb;
 };
 
-// Mask weight-gradient sums a persistent fused-head caller accumulates over its windows
-// (conv_params.h head_ws): the thread's 8 channels' {sum u y, sum v y, sum w y} and, on the
-// pixel's chunk-0 lane, {sum u, sum v, sum w}
+// Mask weight-gradient sums of one tile (conv_params.h head_ws), returned by the fused-head
+// epilogue when HeadT::on: the thread's 8 channels' {sum u y, sum v y, sum w y} and, on the
+// pixel's chunk-0 lane, {sum u, sum v, sum w}.  HeadT::t: the targets of the thread's pixels
+// of the tile (chunk iteration it: pixel tid / 4 + 64 it), prefetched by the persistent caller
+// with the window's halo (a global load in the epilogue would wait on that prefetch).  Both
+// travel by value: a pointer to the caller's accumulators kept them in scratch.
 struct HeadWsum {
   float s[3][8];
   float u, v, w;
+};
+struct HeadT {
+  float t[8];
+  bool on;
 };
 
 // SEGW > 0: the tile is a row window of SEGW-wide row segments (window kernels on rows
@@ -108,11 +115,17 @@ struct HeadWsum {
 // whole rows of TROW pixels (row-window kernels; enables the fused max-pool).
 template <int BM, int BN, int WM, int WN, int TM, int TN, int NTHR, int EPI = EPI_GENERIC,
           class MapM = LinearTiles<WM>, int SEGW = 0, int TROW = 0>
-__device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc)[TM][TN], char* smem,
-                                              const int m0, const int n0, const int M, const int wm,
-                                              const int wn, const int lane, const int tid,
-                                              const int pitch = 0, const int col0 = 0, const int stat_row = 0,
-                                              const EpiConst<TN>* ec = nullptr, HeadWsum* hws = nullptr) {
+__device__ __forceinline__ HeadWsum conv_epilogue(const ConvFwdParams p, f32x4 (&acc)[TM][TN], char* smem,
+                                                  const int m0, const int n0, const int M, const int wm,
+                                                  const int wn, const int lane, const int tid,
+                                                  const int pitch = 0, const int col0 = 0, const int stat_row = 0,
+                                                  const EpiConst<TN>* ec = nullptr, const HeadT ht = HeadT{}) {
+  HeadWsum hws;
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) hws.s[k][e] = 0.f;
+  hws.u = hws.v = hws.w = 0.f;
   auto qof = [&](int ml) -> int {
     if constexpr (SEGW > 0) return (m0 + ml / SEGW) * pitch + col0 + (ml % SEGW);
     else return m0 + ml;
@@ -270,7 +283,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       }
     }
     stats_out(s1, s2, cb);
-    return;
+    return hws;
   }
   if constexpr (kNormG) {
     // gradient of y = dropout(relu(na z + nc)): mask recomputed from the pre-norm z the
@@ -353,7 +366,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       }
     }
     stats_out(s1, s2, cb);
-    return;
+    return hws;
   }
   if constexpr (EPI == EPI_DGRAD && NCHUNK % NTHR == 0 && NTHR % CPR == 0) {
     // a thread's channel chunk (hence destination tensor, row stride and mask) is the
@@ -421,7 +434,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       }
       *(u32x4*)(dst + (size_t)q * rs + co) = v;
     }
-    return;
+    return hws;
   }
   const int Dt = kShuffle ? (p.Cout >> p.shuffle) : 0;
   // Fused segmentation head (forward of conv9b, BN == Cout == 32): the CPR = 4
@@ -433,7 +446,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
   const bool kHead = kHeadable && p.head_w != nullptr;
   float hw[8], hb = 0.f;
   constexpr int HIT = kHeadable ? NCHUNK / NTHR : 1;     // chunk iterations per thread
-  static_assert(!kHeadable || (NCHUNK % NTHR == 0 && HIT % CPR == 0), "fused head tiling");
+  static_assert(!kHeadable || (NCHUNK % NTHR == 0 && HIT % CPR == 0 && HIT <= 8), "fused head tiling");
   float hz[HIT];
   int hq[HIT];
 #pragma unroll
@@ -515,23 +528,25 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
         z += __shfl_xor(z, 2, 64);
         hz[it] = z + hb;
         hq[it] = q;
-        if (hws) {
-          // the probability head_finish will form from this logit, the target: the Mask
-          // weight gradient's per-pixel factors (head_grad.h head_dlogit = A u + B v + G w)
+        if (ht.on) {
+          // the probability head_finish forms from this logit, the target: the Mask weight
+          // gradient's per-pixel factors (head_grad.h head_dlogit = A u + B v + G w)
           const float zl = z + hb;
-          const float pr = 1.f / (1.f + __expf(-zl));
-          const float tv = bits2f(((const uint16_t*)p.head_t)[q]);
+          // (hardware reciprocal: the IEEE division made the forward +12 %; the sums feed only
+          // the Mask gradient, within fp32 rounding of head_finish's probability)
+          const float pr = __builtin_amdgcn_rcpf(1.f + __expf(-zl));
+          const float tv = ht.t[it];
           const float vv = pr * (1.f - pr), uu = tv * vv, ww = pr - tv;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            hws->s[0][e] = fmaf(uu, f[e], hws->s[0][e]);
-            hws->s[1][e] = fmaf(vv, f[e], hws->s[1][e]);
-            hws->s[2][e] = fmaf(ww, f[e], hws->s[2][e]);
+            hws.s[0][e] = fmaf(uu, f[e], hws.s[0][e]);
+            hws.s[1][e] = fmaf(vv, f[e], hws.s[1][e]);
+            hws.s[2][e] = fmaf(ww, f[e], hws.s[2][e]);
           }
           if (cb == 0) {
-            hws->u += uu;
-            hws->v += vv;
-            hws->w += ww;
+            hws.u += uu;
+            hws.v += vv;
+            hws.w += ww;
           }
         }
       }
@@ -601,6 +616,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdParams p, f32x4 (&acc
       }
     }
   }
+  return hws;
 }
 
 }  // namespace unet

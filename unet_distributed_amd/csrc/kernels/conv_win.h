@@ -752,9 +752,19 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
   float xan[8], xbn[8];
   int pf_g0 = 0;
   bool pf_top = false, pf_bot = false;
+  // head_ws: the targets of the thread's 8 epilogue pixels (tid / 4 + 64 it) of the prefetched
+  // window (conv_epilogue.h HeadWsum::t), loaded with its halo
+  constexpr bool HWS = EPI == EPI_FWD && !SEG;
+  float tnext[HWS ? 8 : 1];
   auto load_halo = [&](const int w) {
     const int tmw = p.rev ? nwin - 1 - w : w;
     const int g0 = (tmw / nseg) * R, col0 = (tmw % nseg) * W;
+    if constexpr (HWS) {
+      if (p.head_ws) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) tnext[it] = bits2f(((const uint16_t*)p.head_t)[g0 * W + (tid >> 2) + 64 * it]);
+      }
+    }
     if constexpr (XF == 3) {
       const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
 #pragma unroll
@@ -878,13 +888,16 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
 #pragma unroll
   for (int e = 0; e < 8; ++e) ec.hw[e] = (EPI == EPI_FWD && p.head_w) ? p.head_w[(tid % 4) * 8 + e] : 0.f;
   ec.hb = (EPI == EPI_FWD && p.head_w) ? p.head_b[0] : 0.f;
-  HeadWsum hws;
+  HeadWsum hws;                                      // the walk's Mask weight sums (head_ws)
 #pragma unroll
   for (int k = 0; k < 3; ++k)
 #pragma unroll
     for (int e = 0; e < 8; ++e) hws.s[k][e] = 0.f;
   hws.u = hws.v = hws.w = 0.f;
-  HeadWsum* hwp = (EPI == EPI_FWD && !SEG && p.head_ws) ? &hws : nullptr;
+  HeadT ht;                                          // the current window's targets
+  ht.on = HWS && p.head_ws;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) ht.t[it] = HWS ? tnext[it] : 0.f;
   store_halo();
   __syncthreads();
 
@@ -931,12 +944,26 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
     if constexpr (SEG)
       conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, W, W>(p, acc, smem, g0, 0, M, wave, 0, lane, tid, Wf,
                                                                     col0, tm, &ec);
-    else
-      conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(p, acc, smem, g0 * W, 0, M, wave, 0, lane, tid, 0,
-                                                                    0, tm, &ec, hwp);
+    else {
+      const HeadWsum r = conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(
+          p, acc, smem, g0 * W, 0, M, wave, 0, lane, tid, 0, 0, tm, &ec, ht);
+      if constexpr (HWS) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hws.s[k][e] += r.s[k][e];
+        hws.u += r.u;
+        hws.v += r.v;
+        hws.w += r.w;
+      }
+    }
     if (w + 1 < w_hi) {
       __syncthreads();                               // staging reads done
       store_halo();
+      if constexpr (HWS) {
+#pragma unroll
+        for (int it = 0; it < 8; ++it) ht.t[it] = tnext[it];
+      }
       __syncthreads();
     }
   }
