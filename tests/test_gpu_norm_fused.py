@@ -531,3 +531,39 @@ def test_gn_stats_backward_parameter_grads_many_samples(cuda_dev, N, rps, Ch, G)
         assert torch.allclose(db.double(), db_ref, rtol=1e-4, atol=1e-2), rep
         assert torch.allclose(dg.double(), dg_ref, rtol=1e-4, atol=1e-2), rep
         assert torch.allclose(ca.double().view(N, Ch), gamma.double() * r, rtol=1e-5), rep
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,tile,n0", [(2, 32, 128, 128, 0, 0), (4, 16, 128, 256, 0, 3),
+                                                 (2, 64, 64, 64, 0, 0), (2, 128, 32, 32, 6, 1)])
+def test_conv_fwd_operand_norm_on_load_with_dropout(cuda_dev, N, H, Cin, Cout, tile, n0):
+    """xform 1 with the source layer's inverted dropout (xd_rate / xd_salt / xd_idx0, the
+    planner's conv3a / conv4a): xout equals norm_apply's dropout(relu(a z + b)) bit for bit
+    (same hash of the whole-batch element index, n0: the chunk's first image), and the conv
+    output equals the same window conv of that materialised activation."""
+    torch.manual_seed(51 + N + H)
+    dev = cuda_dev
+    z = torch.randn(N, H, H, Cin, device=dev).bfloat16()
+    a = 0.5 + torch.rand(Cin, device=dev)
+    b = 0.3 * torch.randn(Cin, device=dev)
+    # norm_apply with gamma = a, rstd = 1, beta = b, mean = 0: its A = a, B = b exactly
+    one, zero = torch.ones(Cin, device=dev), torch.zeros(Cin, device=dev)
+    y_ap = torch.empty_like(z)
+    seed, salt, rate = 1234567, 7, 0.3
+    C().generic("norm_apply", [ptr(z), ptr(zero), ptr(one), ptr(a), ptr(b), ptr(y_ap)],
+                [N, H * H, Cin, 0, 1, salt, seed, n0], [rate], stream())
+    w = (torch.randn(3, 3, Cin, Cout, device=dev) * 0.05).bfloat16()
+    bias = torch.randn(Cout, device=dev) * 0.1
+    wp = pack_fwd(w)
+    base = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, wgt=ptr(wp), bias=ptr(bias), Cout=Cout,
+                relu=1, tile=tile)
+    ref = torch.empty(N, H, H, Cout, device=dev, dtype=torch.bfloat16)
+    C().conv_fwd(dict(base, src1=ptr(y_ap), dst1=ptr(ref)), stream())
+    out = torch.empty_like(ref)
+    yo = torch.full_like(z, float("nan"))
+    C().conv_fwd(dict(base, src1=ptr(z), dst1=ptr(out), xform=1, xa=ptr(a), xb=ptr(b), xcs=0, xout=ptr(yo),
+                      xd_rate=rate, xd_salt=salt, xd_idx0=n0 * H * H * Cin, seed=seed), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(yo, y_ap)
+    assert torch.equal(out, ref)
+    kept = (y_ap.float() != 0).float().mean().item()
+    assert 0.2 < kept < 0.5, kept                      # (about (1 - rate) of the positive half)

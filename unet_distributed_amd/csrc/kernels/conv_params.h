@@ -140,6 +140,12 @@ struct ConvFwdParams {
   const float* xc;
   const void* xz;
   void* xout;
+  // xform 1 with the source layer's inverted dropout (its keep mask from drop_hash of the
+  // element index xd_idx0 + pixel * C1 + channel, seed / seed_ptr, salt xd_salt): the
+  // operand is dropout(relu(xa z + xb)), what norm_apply would have stored
+  float xd_rate;
+  uint32_t xd_salt;
+  unsigned long long xd_idx0;
   int tile;                  // 0 = auto, else forced tile config id (tuning / A-B tests)
   // Fused segmentation head (row-window forward, Cout == 32, EPI_FWD only): per pixel
   // z = sum_c out[c] head_w[c] + head_b -> head_logit (fp32) for head_finish

@@ -51,7 +51,8 @@ inline bool win_pf_eligible(const ConvFwdParams& p) {
   const bool w_ok = p.OW == 128 || (p.OW % 128 == 0 && p.OW > 128 && p.OW <= 8192 && !p.hg.prob);
   return p.win_pf > 0 && w_ok && p.KD == 1 && p.OD == 1 && p.C1 == 32 && p.C2 == 0 && p.Cout == 32 &&
          p.tile != 12 && !p.s2d && !p.ut.x && !p.fw.x && p.OH % 4 == 0 &&
-         (!p.hg.prob || conv_epi_mode(p) == EPI_DGRAD) && (!p.xform || (p.xform == 1 && p.OW == 128 && !p.hg.prob));
+         (!p.hg.prob || conv_epi_mode(p) == EPI_DGRAD) &&
+         (!p.xform || (p.xform == 1 && p.OW == 128 && !p.hg.prob && !(p.xd_rate > 0.f)));
 }
 constexpr int CP_DZ_MAXC = 128;      // conv_win_cp_kernel DZ: input channels in LDS coefficients
 // Chunk-pipelined window (conv_win_cp_kernel): 2D 64-wide full rows, the 64-channel tile,
@@ -649,6 +650,11 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
           xa[e] = p.xa[ci];
           xb[e] = p.xb[ci];
         }
+        // the source's dropout (xd_rate): norm.hip norm_apply's keep test and scale
+        const bool xdrop = p.xd_rate > 0.f;
+        const uint32_t xseed = xdrop ? (p.seed_ptr ? *p.seed_ptr : p.seed) : 0u;
+        const float xinv = xdrop ? 1.f / (1.f - p.xd_rate) : 1.f;
+        const uint32_t xthr = (uint32_t)(p.xd_rate * 4294967296.0);
 #pragma unroll
         for (int j = 0; j < XNJ; ++j) {
           int hr, hc, gr;
@@ -660,6 +666,11 @@ __global__ void __launch_bounds__(NTHR) conv_win_kernel(const ConvFwdParams p) {
           unpack8(*(const u32x4*)a, v);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(fmaf(xa[e], v[e], xb[e]), 0.f);
+          if (xdrop) {
+            const unsigned long long e0 = p.xd_idx0 + (unsigned long long)(gr * W + hc - 1) * C + cb + xlc * 8;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = drop_hash(e0 + e, xseed, p.xd_salt) >= xthr ? v[e] * xinv : 0.f;
+          }
           const u32x4 o = pack8(v);
           *(u32x4*)a = o;
           // the window's own rows (once: output-channel tile 0) -> xout

@@ -146,6 +146,9 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.fw.nsplit = get<int>(d, "fw_nsplit", 0);
   p.fw.split_lo = get<int>(d, "fw_split_lo", 0);
   p.xout = const_cast<void*>(getp(d, "xout"));
+  p.xd_rate = get<float>(d, "xd_rate", 0.f);
+  p.xd_salt = get<uint32_t>(d, "xd_salt", 0u);
+  p.xd_idx0 = get<unsigned long long>(d, "xd_idx0", 0ull);
   p.tile = get<int>(d, "tile", 0);
   p.head_w = (const float*)getp(d, "head_w");
   p.head_b = (const float*)getp(d, "head_b");
@@ -791,7 +794,7 @@ class Plan {
   explicit Plan(int dtype = 0) : A_(api(dtype)) {}
   int add_conv_fwd(const py::dict& d) {
     ConvFwdParams p = conv_params(d);
-    const bool seeded = p.drop_rate > 0.f || p.nd_rate > 0.f;
+    const bool seeded = p.drop_rate > 0.f || p.nd_rate > 0.f || p.xd_rate > 0.f;
     const uint32_t* seedp = &seed_;
     const uint32_t* const* seed_devp = &seed_dev_;
     const KernelApi* A = A_;

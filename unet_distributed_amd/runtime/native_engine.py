@@ -1055,21 +1055,26 @@ class NativeUNet:
         d, h, w = self.sdims(lvl)
         return c * nb * d * h * w * ch * self.bufs[tname].element_size()
 
-    def _xf_fwd_fields(self, src, c=0, nb=None):
+    def _xf_fwd_fields(self, src, c=0, nb=None, dropout=False):
         """Operand-transform fields of a conv reading normalised activation `src` as the
         pre-norm z (conv_params.h xform 1) for images [c nb, (c + 1) nb); the conv also
-        writes the activation."""
+        writes the activation (with `src`'s dropout when `dropout`: xd_*, norm_apply's keep
+        mask of the whole-batch element index)."""
         b = self.bufs
         nb = nb or self.B
         C = self.tinfo[src][1]
         mo = 0 if self.spec.norm == "batch" else c * nb * C * 4       # per-sample [B][C] coefficients
-        return dict(xform=1, xa=_ptr(b["fa:" + src]) + mo, xb=_ptr(b["fc:" + src]) + mo,
-                    xcs=0 if self.spec.norm == "batch" else C,
-                    xout=_ptr(b[src]) + self._toff(src, c, nb))
+        out = dict(xform=1, xa=_ptr(b["fa:" + src]) + mo, xb=_ptr(b["fc:" + src]) + mo,
+                   xcs=0 if self.spec.norm == "batch" else C,
+                   xout=_ptr(b[src]) + self._toff(src, c, nb))
+        if dropout and self.tinfo[src][3] and self.spec.dropout > 0:
+            P = self.npix(self.tinfo[src][0]) // self.B
+            out.update(xd_rate=self.spec.dropout, xd_salt=self._salt(src), xd_idx0=c * nb * P * C)
+        return out
 
     def _plan_xforms(self):
         """Normalised activations whose only consumer is the next conv's first source
-        (the 'a' convs of each block, no dropout): that conv normalises z on load and
+        (the 'a' convs of each block, with their dropout): that conv normalises z on load and
         also stores the activation for its weight gradient (+0.4 % BN b1024 over a
         separate norm_apply pass).  Decided once, for the training and the evaluation
         plans alike.  (Measured and dropped in round 2: the consumer's weight gradient
@@ -1088,7 +1093,7 @@ class NativeUNet:
         users.setdefault(self.head_in, []).append(("Mask", 0))
         kinds = {l.name: l.kind for l in self.spec.layers}
         for l in self.spec.layers:
-            if l.kind != "conv" or l.name not in self.norm_layers or self.tinfo[l.name][3]:
+            if l.kind != "conv" or l.name not in self.norm_layers:
                 continue
             u = users.get(l.name, [])
             if len(u) != 1 or u[0][1] != 0 or kinds.get(u[0][0]) != "conv":
@@ -1100,7 +1105,7 @@ class NativeUNet:
             d = self._conv_common(l2.level, 3, 1, 1)
             d.update(C1=l.cout, src1=_ptr(self.bufs["z:" + l.name]), wgt=self.wptr(l2.name), Cout=l2.cout,
                      relu=0, dst1=_ptr(self.bufs["z:" + l2.name]), bias=self.master_ptr(l2.name + "/bias"))
-            d.update(self._xf_fwd_fields(l.name))
+            d.update(self._xf_fwd_fields(l.name, dropout=True))
             try:
                 self.C.conv_fwd_grid(d)
             except ValueError:
@@ -1207,7 +1212,7 @@ class NativeUNet:
                 d.update(self._ut_fields(tl, P(self.inputs[ut][0])))
                 s1 = d["ut_x"]
             if src1 in self._xf_fwd:
-                d.update(self._xf_fwd_fields(src1, c, nb))
+                d.update(self._xf_fwd_fields(src1, c, nb, dropout))
                 s1 = _ptr(b["z:" + src1]) + self._toff(src1, c, nb)
             d.update(name="fwd:" + l.name, C1=c1, C2=self.tinfo[skip][1] if skip else 0, up1=up1,
                      src1=s1, src2=P(skip) if skip else None,
