@@ -49,6 +49,16 @@ def _inputs(e, spec, name):
     return parts
 
 
+def _relu_mask(e, name, n):
+    """[n, H, W, C] bool: the ReLU bits the forward stored for `name` (first n images)."""
+    bits = e.relu_bits[name]
+    C = e.tinfo[name][1]
+    per = bits.numel() // e.B
+    v = bits[:n * per].to(torch.int32)
+    m = (v.unsqueeze(-1) >> torch.arange(8, device=v.device, dtype=torch.int32)) & 1
+    return m.reshape(n, -1, C).bool().reshape(n, 128, 128, C)
+
+
 def test_bench_shape_forward_per_layer(stepped):
     spec, fn, e = stepped
     checked = 0
@@ -69,6 +79,17 @@ def test_bench_shape_forward_per_layer(stepped):
         for dh, dw, xs in _taps(xin):
             out += xs @ w[dh, dw]
         ref = F.relu(out + b).reshape(*xin.shape[:3], -1)
+        if l.name == e.head_in and e.fusions.get("head_wsum"):
+            # (head_wsum: the head input is not stored -- its ReLU bits and the head's
+            # probabilities are what the step keeps)
+            mism = (_relu_mask(e, l.name, NS) != (ref > 0)).float().mean().item()
+            assert mism < 1e-3, (l.name, mism)
+            hw = fn.view(fn.master, "Mask/kernel").float().reshape(-1)
+            hb = fn.view(fn.master, "Mask/bias").float()
+            pref = torch.sigmoid(ref.bfloat16().float() @ hw + hb)
+            assert _rel(e.prob.view(e.B, -1)[:NS].reshape(pref.shape), pref) < 2e-2
+            checked += 1
+            continue
         got = e.bufs[l.name][:NS].float()
         err = _rel(got, ref)
         assert err < 2e-2, (l.name, err)
@@ -137,8 +158,8 @@ def test_bench_shape_data_gradients(stepped):
     I, St, Sp = [v.item() for v in e.sums[:3]]
     dl = (-2.0 * t / (2 * I + 1) + 1.0 / (St + Sp + 1)) * pr * (1 - pr) + e.bce_weight * (pr - t) / P
     hw = fn.view(fn.master, "Mask/kernel").float().reshape(-1)
-    y9b = b["conv9b"][:NS].float()
-    dy9b = dl.reshape(NS, 128, 128, 1) * hw * (y9b > 0)
+    pos9b = _relu_mask(e, "conv9b", NS) if e.fusions.get("head_wsum") else b["conv9b"][:NS].float() > 0
+    dy9b = dl.reshape(NS, 128, 128, 1) * hw * pos9b
     ref = _dgrad(dy9b, kern("conv9b")) * (b["conv9a"][:NS].float() > 0)
     err = _rel(b["d:conv9a"][:NS].float(), ref)
     assert err < 2e-2, ("conv9b", err)
