@@ -555,7 +555,7 @@ def test_conv_fwd_operand_norm_on_load_with_dropout(cuda_dev, N, H, Cin, Cout, t
     bias = torch.randn(Cout, device=dev) * 0.1
     wp = pack_fwd(w)
     base = dict(N=N, OH=H, OW=H, IH=H, IW=H, KH=3, KW=3, pad=1, C1=Cin, wgt=ptr(wp), bias=ptr(bias), Cout=Cout,
-                relu=1, tile=tile)
+                relu=0, tile=tile)           # (the normalised consumer's pre-norm output, generic epilogue)
     ref = torch.empty(N, H, H, Cout, device=dev, dtype=torch.bfloat16)
     C().conv_fwd(dict(base, src1=ptr(y_ap), dst1=ptr(ref)), stream())
     out = torch.empty_like(ref)
