@@ -59,6 +59,8 @@ def _r64(k: int) -> int:
 #   head_onload  the head input's gradient formed on load by its consumers (1: 2D; 2: 3D too)
 #   head_wsum    the Mask gradients from per-workgroup sums of the fused-head forward; the head
 #                input is not stored (1)
+#   xf_drop      dropout layers' outputs normalised on load too (xform 1 with xd_*) (0: measured
+#                slower -- the per-element hash on the consumer's chunk path, r6_bench_history.md)
 #   tconv_fused  deepest fine level whose transposed conv runs the composite backward (2; 0 off)
 #   tconv_wa     the consumer conv's u-row weight gradient from the composite backward's
 #                slab sums (1; 0: full weight gradient over u)
@@ -82,7 +84,7 @@ def _r64(k: int) -> int:
 #                2 = 2D as well, 0 off (0)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
                        tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8, win_cp=1,
-                       wg_pair=0, dz_split=0, head_wsum=1)
+                       wg_pair=0, dz_split=0, head_wsum=1, xf_drop=0)
 
 
 class Fusion:
@@ -1074,7 +1076,7 @@ class NativeUNet:
 
     def _plan_xforms(self):
         """Normalised activations whose only consumer is the next conv's first source
-        (the 'a' convs of each block, with their dropout): that conv normalises z on load and
+        (the 'a' convs of each block; with dropout only under option xf_drop): that conv normalises z on load and
         also stores the activation for its weight gradient (+0.4 % BN b1024 over a
         separate norm_apply pass).  Decided once, for the training and the evaluation
         plans alike.  (Measured and dropped in round 2: the consumer's weight gradient
@@ -1093,7 +1095,8 @@ class NativeUNet:
         users.setdefault(self.head_in, []).append(("Mask", 0))
         kinds = {l.name: l.kind for l in self.spec.layers}
         for l in self.spec.layers:
-            if l.kind != "conv" or l.name not in self.norm_layers:
+            if l.kind != "conv" or l.name not in self.norm_layers or (self.tinfo[l.name][3] and not
+                                                                      self.opts["xf_drop"]):
                 continue
             u = users.get(l.name, [])
             if len(u) != 1 or u[0][1] != 0 or kinds.get(u[0][0]) != "conv":
