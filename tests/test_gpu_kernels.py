@@ -1117,3 +1117,37 @@ def test_wgrad_window_wave_pair(cuda_dev, N, D, H, C1, C2, Cout, splits):
     perm = (2, 3, 4, 1, 0) if d3 else (2, 3, 1, 0)
     assert rel_err(gw, gwr.permute(*perm).reshape(-1)) < 2e-3
     assert rel_err(gb, gbr) < 2e-3
+
+
+@pytest.mark.parametrize("N,D,H,C1,C2,Cout,splits", [(2, 1, 128, 32, 0, 32, 7), (3, 1, 128, 32, 32, 64, 5),
+                                                      (1, 8, 128, 32, 0, 32, 6), (1, 6, 128, 32, 32, 32, 4),
+                                                      (2, 1, 128, 64, 0, 32, 64)])
+def test_wgrad_window_prefetch_equals_dma(cuda_dev, N, D, H, C1, C2, Cout, splits):
+    """Prefetching 128-wide window weight gradient (pf=1: the next window's new halo rows and
+    dY in registers under the current window's MFMAs) equals the LDS-DMA window kernel bit
+    for bit (same images, fragment reads, MFMA order, reduction); 2D and 3D rows, concat
+    sources, windows at image / slice starts (no carry) and split ranges that start inside
+    an image."""
+    torch.manual_seed(N + D + C1 + C2 + splits)
+    d3 = D > 1
+    shp = (N, D, H, H) if d3 else (N, H, H)
+    a = F.relu(torch.randn(*shp, C1, device=cuda_dev)).bfloat16()
+    b2 = F.relu(torch.randn(*shp, max(C2, 1), device=cuda_dev)).bfloat16()
+    dy = torch.randn(*shp, Cout, device=cuda_dev).bfloat16()
+    Mt = C1 + C2
+    T = 27 if d3 else 9
+    d = dict(N=N, QD=D, QH=H, QW=H, AD=D, AH=H, AW=H, KD=3 if d3 else 1, KH=3, KW=3, pad=1, M1=C1, M2=C2,
+             a1=ptr(a), a2=ptr(b2) if C2 else None, b=ptr(dy), Nc=Cout, bias_mode=1)
+    out = []
+    for pf in (0, 1):
+        gw, gb = _wgrad(dict(d, pf=pf), splits, T, Mt, Mt, Cout, T * Mt * Cout, bias_w=(splits, Cout))
+        out.append((gw, gb))
+    torch.cuda.synchronize()
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    conv, to_nc = (F.conv3d, ncdhw) if d3 else (F.conv2d, nchw)
+    inp = to_nc(a.float()) if not C2 else torch.cat([to_nc(a.float()), to_nc(b2.float())], 1)
+    ks = (3, 3, 3) if d3 else (3, 3)
+    w = torch.zeros(Cout, Mt, *ks, device=cuda_dev, requires_grad=True)
+    gwr, = torch.autograd.grad(conv(inp, w, padding=1), [w], to_nc(dy.float()))
+    perm = (2, 3, 4, 1, 0) if d3 else (2, 3, 1, 0)
+    assert rel_err(out[1][0], gwr.permute(*perm).reshape(-1)) < 2e-3

@@ -222,7 +222,10 @@ struct WgradParams {
   const void* xz;
   HeadGrad hg;                // window wgrad of the head input conv: the B operand (dY, 32 channels)
                               // formed on load, see HeadGrad
-  int pair;                   // window wgrad, 32-channel output blocks on column-unit rows: wave-pair
+  int pair;
+  // 128-wide row-window weight gradient with register prefetch of the next window
+  // (conv_wgrad.hip wgrad_pf128_kernel; option wg_pf)
+  int pf;                   // window wgrad, 32-channel output blocks on column-unit rows: wave-pair
                               // partials (conv_wgrad.hip wgrad_win_kernel PAIR, three workgroups per CU)
   // filled by the launcher
   int lqw, lqh, lqd;          // log2 of the pixel grid (power-of-two fast path)

@@ -996,6 +996,264 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
 
 
 // ---------------------------------------------------------------------------------
+// Prefetching 128-wide window weight gradient (option wg_pf; 2D / 3D, 32-channel output
+// block).  wgrad_win_kernel<128, 1> stages each window by LDS-DMA and waits for it: at two
+// workgroups per CU the 3D level-1 weight gradients ran ~4.5 us per window against ~0.5 us
+// of MFMA work -- one HBM round trip per window, exposed.  Here the halo-row carry leaves
+// two new input rows (18 KB) + the dY image (16 KB) per window, 9 x 16 bytes per thread:
+// they are loaded into registers right after the current window's data is in LDS, fly under
+// its MFMAs, and are written to LDS after them (one barrier pair per window, as before).  A
+// window that cannot carry (the first of a workgroup or of an image) loads synchronously.
+// Same LDS images, swizzles, fragment reads, MFMA order and reduction as wgrad_win_kernel
+// with CARRY: bit-identical slabs.
+template <bool CONCAT, int GEO>
+__global__ void __launch_bounds__(NTHR, 2) wgrad_pf128_kernel(const WgradParams p) {
+  constexpr int W = 128, BMW = 256, R = 2, HWP = 144, IPR = 9, ROWB = HWP * 64;
+  constexpr int XI = (R + 2) * IPR, YI = BMW / 16, XB = XI * 1024, YB = YI * 1024;
+  constexpr int REDB = 4 * 64 * 16 * 4;
+  constexpr int LDS_BYTES = (XB + YB > REDB) ? XB + YB : REDB;
+  constexpr int NX = (2 * IPR + 3) / 4, NY = YI / 4;    // pieces per wave: new rows, dY
+  static_assert(GEO == WGEO_2D || GEO == WGEO_3D, "2D / 3D full rows");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  char* Xs = smem;
+  char* Ys = smem + XB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ps = wave;                                  // pixel split = column unit (QO = 1)
+  constexpr int KD = GEO == WGEO_3D ? 3 : 1;
+  const int H = p.QH;
+  const int D = GEO == WGEO_3D ? p.QD : 1;
+  const int rows_total = p.N * D * H;
+  const int Mq = rows_total * W;
+  const int nwin = rows_total / R;
+  const int Mtot = p.M1 + p.M2;
+  const int cob = p.Nc / 32;
+  const int ntile = (Mtot / 32) * cob * KD;
+  const int bid = (p.xcd & 1) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int lsplit = bid / ntile;
+  const int split = p.split_lo + lsplit;
+  int tile = bid - lsplit * ntile;
+  const int kd = tile % KD;
+  tile /= KD;
+  const int ci_blk = tile / cob, co_blk = tile - ci_blk * cob;
+  const int ci0 = ci_blk * 32, co0 = co_blk * 32;
+  const bool from1 = !CONCAT || ci0 < p.M1;
+  const int CA = from1 ? p.M1 : p.M2, ca0 = from1 ? ci0 : ci0 - p.M1;
+  constexpr int OOB = 0x7fffffff;
+  const char* abase = (const char*)(from1 ? p.a1 : p.a2);
+  const char* bbase = (const char*)p.b;
+  const int w_begin = (int)((long long)split * nwin / p.splits);
+  const int w_end = (int)((long long)(split + 1) * nwin / p.splits);
+  const bool do_bias = p.bias_mode == 1 && ci_blk == 0 && kd == (KD >> 1);
+  const int gsh = (kd - (KD >> 1)) * H;
+
+  f32x4 acc[9][2][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 bacc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+  const u32x4 ones_u = {kOnes2, kOnes2, kOnes2, kOnes2};
+  const h16x8 ones = __builtin_bit_cast(h16x8, ones_u);
+
+  // lane roles of wgrad_win_kernel's LDS-DMA (slot 16k + lslot, physical chunk lane & 3)
+  const int lslot = lane >> 2;
+  const int lchunk = (lane & 3) ^ (((lslot >> 3) & 1) << 1);
+  const int xl = ((lslot - 1) * CA + ca0 + lchunk * 8) * 2;
+  const int yl = (lslot * p.Nc + co0 + lchunk * 8) * 2;
+  const int G = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  auto tr_addr = [&](int slot, int col, int ch) -> int {
+    const int swz = ((col >> 3) & 1) << 1;
+    return slot * 64 + (((ch >> 3) ^ swz) << 4) + ((ch & 7) << 1);
+  };
+  auto tr8 = [&](const char* base0, const char* base1) -> h16x8 {
+    const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base0));
+    const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4v, base1));
+    const u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+    const u32x4 v = {l2[0], l2[1], h2[0], h2[1]};
+    return __builtin_bit_cast(h16x8, v);
+  };
+
+  // halo pieces k = kb + wave + 4 i (i < NX) of window `win` (input rows g0 - 1 + hr + gsh)
+  u32x4 xr[NX], yr[NY];
+  auto load_x = [&](const int win, const int kb) {
+    const int g0 = win * R;
+    const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
+    const int rb = max(g0 - 1 + gsh, 0);
+    const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(abase + (size_t)rb * W * CA * 2), (short)0, OOB, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int k = kb + wave + 4 * i;
+      const int hr = k / IPR, j = k - hr * IPR;
+      const int gr = g0 - 1 + hr + gsh;
+      const int col = 16 * j + lslot - 1;
+      const bool ok = k < kb + 2 * IPR && (hr > 0 || top_in) && (hr < R + 1 || bot_in) &&
+                      (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+      xr[i] = __builtin_amdgcn_raw_buffer_load_b128(rsa, ok ? ((gr - rb) * W + 16 * j) * CA * 2 + xl : OOB, 0, 0);
+    }
+  };
+  auto load_y = [&](const int win) {
+    const int g0 = win * R;
+    const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(bbase + (size_t)g0 * W * p.Nc * 2), (short)0, OOB, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < NY; ++i) {
+      const int sb = (wave + 4 * i) * 16;
+      const int pix = g0 * W + sb;
+      yr[i] = __builtin_amdgcn_raw_buffer_load_b128(rsb, pix + lslot < Mq ? sb * p.Nc * 2 + yl : OOB, 0, 0);
+    }
+  };
+  // (logical halo row hr at physical row hr ^ 2 fl; every slot of the row pieces is written:
+  // out-of-range loads return zeros, as the DMA leaves them)
+  auto store_x = [&](const int kb, const int fl) {
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int k = kb + wave + 4 * i;
+      if (k < kb + 2 * IPR) {
+        const int hr = k / IPR;
+        const int pk = fl ? k + (hr < 2 ? 2 * IPR : -2 * IPR) : k;
+        *(u32x4*)(Xs + pk * 1024 + lane * 16) = xr[i];
+      }
+    }
+  };
+  auto store_y = [&]() {
+#pragma unroll
+    for (int i = 0; i < NY; ++i) *(u32x4*)(Ys + (wave + 4 * i) * 1024 + lane * 16) = yr[i];
+  };
+
+  int fl = 0, prev = -2, pwin = -1;
+  for (int win = w_begin; win < w_end; ++win) {
+    const int g0 = win * R;
+    if (GEO == WGEO_3D && (unsigned)((g0 / H) % D + kd - 1) >= (unsigned)D) continue;
+    const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
+    const bool carry = prev == win - 1 && top_in;
+    fl = carry ? fl ^ 1 : 0;
+    prev = win;
+    __syncthreads();                                   // the previous window's fragment reads are done
+    if (!(carry && pwin == win)) {
+      // not prefetched: this window's rows (all four unless it carries) and dY, synchronously
+      if (!carry) {
+        load_x(win, 0);
+        store_x(0, fl);
+      }
+      load_x(win, 2 * IPR);
+      load_y(win);
+    }
+    store_x(2 * IPR, fl);
+    store_y();
+    pwin = -1;
+    if (win + 1 < w_end && bot_in) {
+      // the next window carries (same image, not a depth-padding window: same slice): its
+      // two new rows and dY fly under this window's MFMAs
+      load_x(win + 1, 2 * IPR);
+      load_y(win + 1);
+      pwin = win + 1;
+    }
+    __syncthreads();
+    {
+      const int c0 = ps * 32;
+      const int lp = 8 * G + q;
+      const int xsh = fl ? 2 * ROWB : 0;
+      int ab[3][2][2], yb[2][2];
+#pragma unroll
+      for (int dw = 0; dw < 3; ++dw)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int col = c0 + dw + lp + 4 * hh;
+            ab[dw][i][hh] = tr_addr(col, col, 16 * i + 4 * pp);
+          }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int sl = c0 + lp + 4 * hh;
+          yb[j][hh] = tr_addr(sl, sl, 16 * j + 4 * pp);
+        }
+      h16x8 bf[R][2];
+#pragma unroll
+      for (int hr = 0; hr < R + 2; ++hr) {
+        if (hr < R) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) bf[hr][j] = tr8(Ys + yb[j][0] + hr * W * 64, Ys + yb[j][1] + hr * W * 64);
+          if (do_bias) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bacc[j] = mfma16(ones, bf[hr][j], bacc[j]);
+          }
+        }
+#pragma unroll
+        for (int dw = 0; dw < 3; ++dw) {
+          h16x8 af[2];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int ro = hr * ROWB + (hr < 2 ? xsh : -xsh);
+            af[i] = tr8(Xs + ab[dw][i][0] + ro, Xs + ab[dw][i][1] + ro);
+          }
+#pragma unroll
+          for (int dh = 0; dh < 3; ++dh) {
+            const int y = hr - dh;
+            if (y < 0 || y >= R) continue;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+              for (int j = 0; j < 2; ++j) acc[3 * dh + dw][i][j] = mfma16(af[i], bf[y][j], acc[3 * dh + dw][i][j]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+
+  // ---- reduce the pixel-split partials of the four waves and write the slab (as wgrad_win_kernel)
+  float* red = (float*)smem;
+  const int n_base = co0 + (lane & 15);
+  const int m_base = ci0 + 4 * (lane >> 4);
+  auto reduce_store = [&](const f32x4 (&v4)[2][2], const int t) {
+    __syncthreads();
+    if (ps > 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) *(f32x4*)(red + ((i * 2 + j) * NTHR + wave * 64 + lane) * 4) = v4[i][j];
+    }
+    __syncthreads();
+    if (ps == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x4 v = v4[i][j];
+#pragma unroll
+          for (int o = 1; o < 4; ++o) v += *(const f32x4*)(red + ((i * 2 + j) * NTHR + o * 64 + lane) * 4);
+          if (t < 9) {
+            float* dst = p.slab + (((size_t)split * 9 * KD + 9 * kd + t) * Mtot + m_base + 16 * i) * p.Nc + n_base + 16 * j;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dst[(size_t)r * p.Nc] = v[r];
+          } else if (i == 0 && lane < 16) {
+            p.bias_slab[(size_t)split * p.Nc + n_base + 16 * j] = v[0];
+          }
+        }
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < 9; ++t) reduce_store(acc[t], t);
+  if (do_bias) {
+    const f32x4 z = (f32x4){0.f, 0.f, 0.f, 0.f};
+    f32x4 bv[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bv[0][j] = bacc[j];
+      bv[1][j] = z;
+    }
+    reduce_store(bv, 9);
+  }
+}
+
+
+// ---------------------------------------------------------------------------------
 // First-layer row-window weight gradient (CIN = 4 or 8 padded input channels).
 // GEMM rows m = (tap, channel) (36 or 72, padded to MT x 16), columns = 32 output
 // channels, K = pixels.  The halo image uses the first-layer forward's slot layout
@@ -1597,6 +1855,15 @@ hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
     }
   }
   if (p.hg.prob) return hipErrorInvalidValue;
+  if constexpr (W == 128 && QO == 1 && (GEO == WGEO_2D || GEO == WGEO_3D)) {
+    if (p.pf && !p.xform && !p.pair) {                  // prefetching window (option wg_pf)
+      if (p.M2 > 0)
+        UNET_LAUNCH((wgrad_pf128_kernel<true, GEO>), dim3(grid), dim3(NTHR), 0, s, p);
+      else
+        UNET_LAUNCH((wgrad_pf128_kernel<false, GEO>), dim3(grid), dim3(NTHR), 0, s, p);
+      return launch_status();
+    }
+  }
   if (p.xform == 2) {                                   // dz on load (wgrad_check: 2D single source)
     if constexpr (GEO == WGEO_2D && W >= 16 && W <= 64 && QO == 1) {
       if (p.M2 > 0) return hipErrorInvalidValue;

@@ -199,6 +199,7 @@ WgradParams wgrad_params(const py::dict& d) {
   p.xc = (const float*)getp(d, "xc");
   p.xz = getp(d, "xz");
   p.pair = get<int>(d, "pair", 0);
+  p.pf = get<int>(d, "pf", 0);
   p.hg = head_grad(d);
   if (p.bias_mode && !p.bias_slab) throw std::invalid_argument("wgrad: bias_slab required");
   if (!p.a1 || !p.b || !p.slab) throw std::invalid_argument("wgrad: a1/b/slab required");

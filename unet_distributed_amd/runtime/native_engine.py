@@ -59,6 +59,9 @@ def _r64(k: int) -> int:
 #   head_onload  the head input's gradient formed on load by its consumers (1: 2D; 2: 3D too)
 #   head_wsum    the Mask gradients from per-workgroup sums of the fused-head forward; the head
 #                input is not stored (1)
+#   wg_pf        128-wide window weight gradients with the next window's rows + dY prefetched in
+#                registers (conv_wgrad.hip wgrad_pf128_kernel): 1 = 3D, 2 = 2D as well (1: the 3D
+#                level-1 weight gradients -19..-21 % per launch; 2D neutral)
 #   xf_drop      dropout layers' outputs normalised on load too (xform 1 with xd_*) (0: measured
 #                slower -- the per-element hash on the consumer's chunk path, r6_bench_history.md)
 #   tconv_fused  deepest fine level whose transposed conv runs the composite backward (2; 0 off)
@@ -84,7 +87,7 @@ def _r64(k: int) -> int:
 #                2 = 2D as well, 0 off (0)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
                        tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8, win_cp=1,
-                       wg_pair=0, dz_split=0, head_wsum=1, xf_drop=0)
+                       wg_pair=0, dz_split=0, head_wsum=1, xf_drop=0, wg_pf=1)
 
 
 class Fusion:
@@ -1766,7 +1769,8 @@ class NativeUNet:
                                        "tile (its dY is never materialised for a column-sum pass)")
                 d.update(name="wgrad:" + w["lname"], M1=w["M1"], M2=w["M2"], Nc=w["Nc"], splits=splits,
                          win=self.wgrad_win, slab=slab, bias_mode=w["bias_mode"] if fused_bias else 0,
-                         bias_slab=bslab, pair=int(self.opts["wg_pair"] >= (1 if self.dims == 3 else 2)))
+                         bias_slab=bslab, pair=int(self.opts["wg_pair"] >= (1 if self.dims == 3 else 2)),
+                         pf=int(self.opts["wg_pf"] >= (1 if self.dims == 3 else 2)))
                 if part is not None:
                     d.update(split_lo=part * splits // 2, split_n=splits // 2)
                 if "dw" in w:
