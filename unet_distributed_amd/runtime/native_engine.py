@@ -59,6 +59,9 @@ def _r64(k: int) -> int:
 #   head_onload  the head input's gradient formed on load by its consumers (1: 2D; 2: 3D too)
 #   head_wsum    the Mask gradients from per-workgroup sums of the fused-head forward; the head
 #                input is not stored (1)
+#   win_cp3      win_cp of the 3D model (2: the 3D level-1 convs on the chunk-pipelined 128-wide
+#                window, conv_win_cp128_kernel -- -10..-12 % per launch, +2 % on the 3D step in
+#                round 6; neutral in round 5, before the 3D weight-gradient prefetch)
 #   wg_pf        128-wide window weight gradients with the next window's rows + dY prefetched in
 #                registers (conv_wgrad.hip wgrad_pf128_kernel): 1 = 3D, 2 = 2D as well (1: the 3D
 #                level-1 weight gradients -19..-21 % per launch; 2D neutral)
@@ -87,7 +90,7 @@ def _r64(k: int) -> int:
 #                2 = 2D as well, 0 off (0)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
                        tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8, win_cp=1,
-                       wg_pair=0, dz_split=0, head_wsum=1, xf_drop=0, wg_pf=1)
+                       wg_pair=0, dz_split=0, head_wsum=1, xf_drop=0, wg_pf=1, win_cp3=2)
 
 
 class Fusion:
@@ -1049,7 +1052,7 @@ class NativeUNet:
         kd = K if self.dims == 3 else 1
         return dict(N=self.B, OD=od, OH=oh, OW=ow, ID=idd, IH=ih, IW=iw, KD=kd, KH=K, KW=K,
                     stride=stride, pad=pad, tile=0, win_pf=self.opts["win_pf"],
-                    win_cp=self.opts["win_cp"])
+                    win_cp=self.opts["win_cp3"] if self.dims == 3 else self.opts["win_cp"])
 
     def _salt(self, lname):
         return [l.name for l in self.spec.layers].index(lname)
