@@ -20,6 +20,9 @@ Bucket sizing for MI355X xGMI: 8 GPUs are fully connected by 7 links of
 so per-message latency (~10-30 us) rather than bandwidth dominates for these
 sizes; a handful of 4-16 MB buckets keeps launches few while still leaving
 only a small exposed tail (the encoder's last ~4.5 MB).
+Status: this sizing is reasoned, not tuned -- no multi-rank RCCL run on xGMI hardware exists yet
+(one-rank runs time the per-bucket collectives: 0.014-0.017 ms each, `bench.py --dist_force 1`,
+profiles/r6_configs.md); `--bucket_mb` is the knob once an 8-GPU node measures it.
 """
 
 from typing import List
