@@ -597,3 +597,27 @@ def test_fused_dgrad_wgrad_norm_step(cuda_dev, monkeypatch, norm, dtype):
             continue       # (a conv bias before BatchNorm: analytically zero gradient, rounding noise)
         if g0[k].norm() > 1e-6:
             assert _cos(g1[k], g0[k]) > 0.999, (k, _cos(g1[k], g0[k]))
+
+
+@pytest.mark.parametrize("kw", [
+    dict(batch_size=4, img_size=128, in_channels=4, norm="batch"),
+    dict(batch_size=3, img_size=128, in_channels=4, norm="batch", loss="dice_bce", hip_graph=True),
+])
+def test_skip_onload_step_equals_materialised(cuda_dev, monkeypatch, kw):
+    """skip_onload=1 (BatchNorm default: conv9a's skip source conv1b is never stored in
+    training -- the tconv-on-load forward and the chained skip-row weight gradient normalise
+    its pre-norm z on load with norm_pool's formula) gives the materialised step bit for bit:
+    loss sums, probabilities, every parameter gradient."""
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("UNET_ENGINE", "skip_onload=" + v)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
+        e = nb.engine
+        assert bool(e.fusions.get("skip_onload")) == (v == "1")
+        for seed in (41, 42):
+            nb.fwd_bwd(x, y, seed=seed)
+        torch.cuda.synchronize()
+        outs.append((nb.sums().cpu(), e.prob.clone(), fn.grad.clone()))
+    (s0, p0, g0), (s1, p1, g1) = outs
+    assert torch.equal(s0, s1) and torch.equal(p0, p1)
+    assert torch.equal(g0, g1)

@@ -1146,6 +1146,8 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
         conv_epi_mode(p) != EPI_FWD || conv_fwd_pick(p) != 6)
       return "conv_fwd: fused head needs a 32-channel ReLU row-window forward";
   }
+  if ((p.x2a || p.x2b) && (!p.x2a || !p.x2b || !win_pfu_eligible(p) || (p.x2cs != 0 && p.x2cs != p.C2)))
+    return "conv_fwd: the skip source normalised on load needs the persistent tconv-on-load window";
   if ((p.head_ws || p.head_nostore) &&
       (!p.head_w || !win_pf_eligible(p) || p.OW != 128 || (p.head_ws && !p.head_t) || !p.relu_bits))
     return "conv_fwd: Mask weight sums / an unstored head input need the persistent 128-wide fused-head window "

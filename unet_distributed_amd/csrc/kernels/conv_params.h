@@ -146,6 +146,12 @@ struct ConvFwdParams {
   float xd_rate;
   uint32_t xd_salt;
   unsigned long long xd_idx0;
+  // skip source (src2) normalised on load, y2 = relu(x2a z2 + x2b) ([C2] or [N][C2], x2cs):
+  // the persistent tconv-on-load window only (conv_win_pfu_kernel; conv9a of the normalised
+  // configs, whose skip activation is then never stored)
+  const float* x2a;
+  const float* x2b;
+  int x2cs;
   int tile;                  // 0 = auto, else forced tile config id (tuning / A-B tests)
   // Fused segmentation head (row-window forward, Cout == 32, EPI_FWD only): per pixel
   // z = sum_c out[c] head_w[c] + head_b -> head_logit (fp32) for head_finish

@@ -1005,13 +1005,16 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
 // its MFMAs, and are written to LDS after them (one barrier pair per window, as before).  A
 // window that cannot carry (the first of a workgroup or of an image) loads synchronously.
 // Same LDS images, swizzles, fragment reads, MFMA order and reduction as wgrad_win_kernel
-// with CARRY: bit-identical slabs.
-template <bool CONCAT, int GEO>
+// with CARRY: bit-identical slabs.  xform 1 (BatchNorm, single source): the A operand is the
+// pre-norm z of a normalised activation, relu(xa z + xb) formed in registers before the LDS
+// store (padding stays zero) -- the activation itself need not be stored (norm_pool's y).
+template <bool CONCAT, int GEO, bool AXF = false>
 __global__ void __launch_bounds__(NTHR, 2) wgrad_pf128_kernel(const WgradParams p) {
   constexpr int W = 128, BMW = 256, R = 2, HWP = 144, IPR = 9, ROWB = HWP * 64;
   constexpr int XI = (R + 2) * IPR, YI = BMW / 16, XB = XI * 1024, YB = YI * 1024;
   constexpr int REDB = 4 * 64 * 16 * 4;
-  constexpr int LDS_BYTES = (XB + YB > REDB) ? XB + YB : REDB;
+  constexpr int LDS_BYTES = (XB + YB + 256 > REDB) ? XB + YB + 256 : REDB;
+  static_assert(!AXF || (!CONCAT && GEO == WGEO_2D), "A on load: 2D single source");
   constexpr int NX = (2 * IPR + 3) / 4, NY = YI / 4;    // pieces per wave: new rows, dY
   static_assert(GEO == WGEO_2D || GEO == WGEO_3D, "2D / 3D full rows");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
@@ -1075,8 +1078,13 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_pf128_kernel(const WgradParams 
     return __builtin_bit_cast(h16x8, v);
   };
 
+  // xform 1: the block's 32 channels' xa / xb in LDS (BatchNorm: one set for the launch)
+  float* Kx = (float*)(smem + XB + YB);
+  constexpr bool axf = AXF;
+  if (axf && tid < 64) Kx[tid] = (tid < 32 ? p.xa : p.xb)[ca0 + (tid & 31)];
   // halo pieces k = kb + wave + 4 i (i < NX) of window `win` (input rows g0 - 1 + hr + gsh)
   u32x4 xr[NX], yr[NY];
+  uint32_t xokm = 0;
   auto load_x = [&](const int win, const int kb) {
     const int g0 = win * R;
     const bool top_in = (g0 % H) != 0, bot_in = ((g0 + R) % H) != 0;
@@ -1091,6 +1099,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_pf128_kernel(const WgradParams 
       const int col = 16 * j + lslot - 1;
       const bool ok = k < kb + 2 * IPR && (hr > 0 || top_in) && (hr < R + 1 || bot_in) &&
                       (unsigned)gr < (unsigned)rows_total && (unsigned)col < (unsigned)W;
+      xokm = i ? (xokm | ((ok ? 1u : 0u) << i)) : (ok ? 1u : 0u);
       xr[i] = __builtin_amdgcn_raw_buffer_load_b128(rsa, ok ? ((gr - rb) * W + 16 * j) * CA * 2 + xl : OOB, 0, 0);
     }
   };
@@ -1108,6 +1117,18 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_pf128_kernel(const WgradParams 
   // (logical halo row hr at physical row hr ^ 2 fl; every slot of the row pieces is written:
   // out-of-range loads return zeros, as the DMA leaves them)
   auto store_x = [&](const int kb, const int fl) {
+    if (axf) {
+      const float* ka = Kx + lchunk * 8;
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        if (!((xokm >> i) & 1u)) continue;
+        float f[8];
+        unpack8(xr[i], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(ka[e], f[e], ka[32 + e]), 0.f);
+        xr[i] = pack8(f);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
       const int k = kb + wave + 4 * i;
@@ -1856,7 +1877,14 @@ hipError_t launch_wgrad_win_g(const WgradParams& p, hipStream_t s) {
   }
   if (p.hg.prob) return hipErrorInvalidValue;
   if constexpr (W == 128 && QO == 1 && (GEO == WGEO_2D || GEO == WGEO_3D)) {
-    if (p.pf && !p.xform && !p.pair) {                  // prefetching window (option wg_pf)
+    if (p.pf && p.xform != 2 && !p.pair) {              // prefetching window (option wg_pf; xform 1: A on load)
+      if (p.xform == 1) {
+        if constexpr (GEO == WGEO_2D) {
+          UNET_LAUNCH((wgrad_pf128_kernel<false, GEO, true>), dim3(grid), dim3(NTHR), 0, s, p);
+          return launch_status();
+        }
+        return hipErrorInvalidValue;
+      }
       if (p.M2 > 0)
         UNET_LAUNCH((wgrad_pf128_kernel<true, GEO>), dim3(grid), dim3(NTHR), 0, s, p);
       else
@@ -1991,7 +2019,11 @@ const char* wgrad_check(const WgradParams& p) {
     if (p.M1 % 8 || p.M2 % 8) return "wgrad: channel split must be a multiple of 8";
     if (KT % c.NTAP) return "wgrad: taps not divisible by the tap group";
   }
-  if (p.xform != 0 && p.xform != 2) return "wgrad: xform must be 0 or 2";
+  if (p.xform != 0 && p.xform != 1 && p.xform != 2) return "wgrad: xform must be 0, 1 or 2";
+  if (p.xform == 1 && (!p.pf || !wgrad_win_eligible(p) || p.QW != 128 || p.KD != 1 || p.QD != 1 || p.M2 != 0 ||
+                       p.M1 != 32 || p.xcs != 0 || !p.xa || !p.xb || p.hg.prob || p.pair))
+    return "wgrad: A normalised on load needs the prefetching 128-wide window (2D, one 32-channel source, "
+           "BatchNorm coefficients)";
   if (p.xform == 2 && (!p.xa || !p.xb || !p.xc || !p.xz || (p.xcs != 0 && p.xcs != p.Nc) ||
                        (wgrad_win_first_eligible(p)
                             ? (p.xcs && p.QH % ((p.QW > 256 ? p.QW : 256) / p.QW)) != 0

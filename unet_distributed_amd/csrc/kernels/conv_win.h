@@ -1485,7 +1485,11 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pfu_kernel(const ConvFwdPara
       for (int ks = 0; ks < KS; ++ks) xb[pb][ks] = *(const h16x8*)(rp + (size_t)(16 * pb) * Cc + 32 * ks);
   };
   // skip halo: granule c of thread t = halo row c / 2, column (t >> 2) + 64 (c & 1), chunk t & 3
+  // (x2a: normalised on load, relu(x2a z + x2b) of the thread's 8 channels (t & 3) * 8 .. of the
+  // window's sample; padding granules -- sok bit clear -- stay zero)
   u32x4 sv[8];
+  uint32_t sok = 0;
+  float s2a[8], s2b[8];
   const int lds_t = (1 + (tid >> 2)) * 64 + 16 * ((tid & 3) ^ (((1 + (tid >> 2)) >> 1) & 3));
   auto load_skip = [&](const int w) {
     const int g0 = (p.rev ? nwin - 1 - w : w) * R;
@@ -1494,11 +1498,21 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pfu_kernel(const ConvFwdPara
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.src2 + (size_t)grow0 * W * 64), (short)0, OOB, 0x00020000);
     const int rowoff = (g0 - 1 - grow0) * W * 64;
+    sok = 0;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       const int hr = c >> 1;
       const bool ok = (hr > 0 || top_in) && (hr < R + 1 || bot_in) && (unsigned)(g0 - 1 + hr) < (unsigned)rows_total;
+      sok |= (ok ? 1u : 0u) << c;
       sv[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? rowoff + hr * W * 64 + (c & 1) * 4096 + tid * 16 : OOB, 0, 0);
+    }
+    if (p.x2a) {
+      const size_t cs = (size_t)(g0 / H) * p.x2cs + (tid & 3) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s2a[e] = p.x2a[cs + e];
+        s2b[e] = p.x2b[cs + e];
+      }
     }
   };
   const int tsel = (fr >> 2) & 1;
@@ -1529,6 +1543,17 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pfu_kernel(const ConvFwdPara
     if (lane < 8) *(u32x4*)(xrow + ((lane >> 2) ? W + 1 : 0) * 64 + 16 * (lane & 3)) = (u32x4){0u, 0u, 0u, 0u};
   };
   auto store_skip = [&]() {
+    if (p.x2a) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        if (!((sok >> c) & 1u)) continue;
+        float f[8];
+        unpack8(sv[c], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(s2a[e], f[e], s2b[e]), 0.f);
+        sv[c] = pack8(f);
+      }
+    }
 #pragma unroll
     for (int c = 0; c < 8; ++c) *(u32x4*)(Xs + lds_t + (c >> 1) * ROWB + (c & 1) * 4096) = sv[c];
     if (tid < 32) *(u32x4*)(Xs + (tid >> 3) * ROWB + ((tid >> 2) & 1) * 129 * 64 + 16 * (tid & 3)) = (u32x4){0u, 0u, 0u, 0u};

@@ -184,7 +184,8 @@ __global__ void __launch_bounds__(256) norm_pool_kernel(const h16* __restrict__ 
 #pragma unroll
       for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(A[e], f[e], B[e]), 0.f);
       const u32x4 v = pack8(f);
-      *(u32x4*)(y + (size_t)(pi.base + (dz * H + dy) * W + dx) * C + pi.cc * 8) = v;
+      // (y == nullptr: the activation's readers normalise z on load -- only the pool is stored)
+      if (y) *(u32x4*)(y + (size_t)(pi.base + (dz * H + dy) * W + dx) * C + pi.cc * 8) = v;
       unpack8(v, f);                                 // the stored (rounded) activation
 #pragma unroll
       for (int e = 0; e < 8; ++e) {

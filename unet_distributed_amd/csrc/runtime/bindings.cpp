@@ -149,6 +149,9 @@ ConvFwdParams conv_params(const py::dict& d) {
   p.xd_rate = get<float>(d, "xd_rate", 0.f);
   p.xd_salt = get<uint32_t>(d, "xd_salt", 0u);
   p.xd_idx0 = get<unsigned long long>(d, "xd_idx0", 0ull);
+  p.x2a = (const float*)getp(d, "x2a");
+  p.x2b = (const float*)getp(d, "x2b");
+  p.x2cs = get<int>(d, "x2cs", 0);
   p.tile = get<int>(d, "tile", 0);
   p.head_w = (const float*)getp(d, "head_w");
   p.head_b = (const float*)getp(d, "head_b");

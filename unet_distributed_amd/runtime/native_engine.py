@@ -59,6 +59,8 @@ def _r64(k: int) -> int:
 #   head_onload  the head input's gradient formed on load by its consumers (1: 2D; 2: 3D too)
 #   head_wsum    the Mask gradients from per-workgroup sums of the fused-head forward; the head
 #                input is not stored (1)
+#   skip_onload  BatchNorm: conv9a's skip source read as pre-norm z by its consumers, never stored
+#                in training (1)
 #   win_cp3      win_cp of the 3D model (2: the 3D level-1 convs on the chunk-pipelined 128-wide
 #                window, conv_win_cp128_kernel -- -10..-12 % per launch, +2 % on the 3D step in
 #                round 6; neutral in round 5, before the 3D weight-gradient prefetch)
@@ -90,7 +92,7 @@ def _r64(k: int) -> int:
 #                2 = 2D as well, 0 off (0)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
                        tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8, win_cp=1,
-                       wg_pair=0, dz_split=0, head_wsum=1, xf_drop=0, wg_pf=1, win_cp3=2)
+                       wg_pair=0, dz_split=0, head_wsum=1, xf_drop=0, wg_pf=1, win_cp3=2, skip_onload=1)
 
 
 class Fusion:
@@ -152,6 +154,9 @@ FUSIONS: Dict[str, Fusion] = {
                        option="tconv_wa", needs=("tconv_fused",)),
     "tconv_onload": Fusion("transposed conv formed on load by its consumer's forward (XF 5)", dims={2},
                            option="tconv_onload", needs=("tconv_wa",)),
+    "skip_onload": Fusion("a normalised skip source normalised on load by its tconv-on-load consumer and the "
+                          "chained skip-row weight gradient: never stored in training (x2a / xform 1)",
+                          norm={"batch"}, dims={2}, option="skip_onload", when=lambda e: e.wgrad_win >= 0),
     "norm_onload": Fusion("normalisation of an 'a' conv's output on load by its consumer (XF 1)",
                           norm={"batch", "group"}, dims={2}),
     "skip_route": Fusion("skip-half data gradient with the pool backward in its epilogue", dims={2}),
@@ -255,6 +260,8 @@ class NativeUNet:
         # (each op's parameters are kept for the static plan validation, runtime/plan_check.py)
         self.plan = RecordingPlan(self.C.Plan(self.dt_id), self._stat_rows_of)
         self.eval_plan = RecordingPlan(self.C.Plan(self.dt_id), self._stat_rows_of)
+        for cname, d in self._ut_probe.items():
+            self._plan_skip_onload(next(x for x in self.spec.layers if x.name == cname), d)
         self._plan_xforms()
         self._norm_head_loss = False
         self._build_forward(self.plan, dropout=True)
@@ -518,6 +525,8 @@ class NativeUNet:
         self._tf_consumer: Dict[str, str] = {}
         self._wa_chain_of: Dict[str, str] = {}  # consumer conv whose u-row wgrad is chained -> tconv
         self._ut_onload: Dict[str, str] = {}    # consumer conv that forms u on load -> tconv
+        self._skip_onload: Dict[str, str] = {}  # skip source normalised on load (never stored) -> consumer
+        self._ut_probe: Dict[str, dict] = {}
         top = self.opts["tconv_fused"]
         if not self._fusion_ok("tconv_fused") or (self.spec.norm != "none" and not self.fuse_norm_stats_planned()):
             return
@@ -605,9 +614,44 @@ class NativeUNet:
         tf["ut"] = True
         self._ut_onload[c.name] = l.name
         self._fusion_on("tconv_onload", l.name)
+        self._ut_probe[c.name] = d                # (skip_onload: decided once the norm buffers exist)
         # the fine output is never formed (no forward writes it, no backward reads it);
         # kept aside so the plan validation can flag any op that would still read it
         self._dropped[l.name] = self.bufs.pop(l.name, None)
+
+    def _plan_skip_onload(self, c, d):
+        """FUSIONS['skip_onload']: the normalised skip source S of the tconv-on-load consumer
+        `c` (conv9a: BatchNorm, 128-wide rows) is never stored in training -- the consumer's
+        persistent window normalises S's pre-norm z on load (conv_params.h x2a / x2b) and so
+        does the chained skip-row weight gradient (the prefetching 128-wide window, xform 1);
+        S's data gradient masks from z already (dgrad-norm epilogue), and norm_pool keeps only
+        the pooled tensor.  Recorded in self._skip_onload {S: c}; the plan validation flags
+        any op that would still read S's activation."""
+        src1, up1, skip = self.inputs[c.name]
+        if (skip is None or skip not in self.norm_layers or not self._fusion_ok("skip_onload", skip)
+                or self.spec.norm != "batch" or self.tinfo[skip][3] or self.tinfo[skip][1] != 32):
+            return
+        b = self.bufs
+        probe = dict(d, src2=1, x2a=_ptr(b["fa:" + skip]), x2b=_ptr(b["fc:" + skip]), x2cs=0)
+        sd = self.sdims(c.level)
+        wk = dict(N=self.B, QD=sd[0], QH=sd[1], QW=sd[2], AD=sd[0], AH=sd[1], AW=sd[2], KD=1, KH=3, KW=3,
+                  stride=1, pad=1, upA=1, a1=_ptr(b["z:" + skip]), b=_ptr(b[skip]), M1=32, M2=0, Nc=c.cout,
+                  splits=1, win=self.wgrad_win, bias_mode=1, pf=1, xform=1, xa=_ptr(b["fa:" + skip]),
+                  xb=_ptr(b["fc:" + skip]), xcs=0)
+        try:
+            if self.C.conv_fwd_grid(probe) <= 0:
+                return
+            self.C.wgrad_validate(wk)
+        except ValueError:
+            return
+        self._skip_onload[skip] = c.name
+        self._fusion_on("skip_onload", skip)
+
+    def _skip_xf_fields(self, skip, c, nb):
+        """x2* fields of the tconv-on-load consumer reading skip source `skip` as pre-norm z."""
+        b = self.bufs
+        return dict(src2=_ptr(b["z:" + skip]) + self._toff(skip, c, nb), x2a=_ptr(b["fa:" + skip]),
+                    x2b=_ptr(b["fc:" + skip]), x2cs=0)
 
     # ------------------------------------------------------------------ normalisation
     NORM_EPS = 1e-3          # models/reference.py::_norm (Keras default epsilon)
@@ -783,6 +827,8 @@ class NativeUNet:
             # convNb: normalisation and the 2x2 max-pool of its output in one pass
             dd, hh, ww = self.sdims(l.level)
             pcode = _ptr(self.pool_codes[pool]) + c * nb * (self.npix(l.level + 1) // self.B) * (C // 8) * 4
+            if train and l.name in self._skip_onload:
+                out = 0                      # (skip_onload: its consumers read z)
             plan.add_generic("norm_pool", [zp, fa, fc, out, _ptr(b[pool]) + self._toff(pool, c, nb), pcode],
                              [N, dd, hh, ww, C, int(self.dims == 3), cstride], [], "norm:" + l.name)
             self._pool_fused.add(pool)
@@ -1220,6 +1266,7 @@ class NativeUNet:
                 tl = next(x for x in spec.layers if x.name == ut)
                 d.update(self._ut_fields(tl, P(self.inputs[ut][0])))
                 s1 = d["ut_x"]
+            skip_xf = train and skip is not None and self._skip_onload.get(skip) == l.name
             if src1 in self._xf_fwd:
                 d.update(self._xf_fwd_fields(src1, c, nb, dropout))
                 s1 = _ptr(b["z:" + src1]) + self._toff(src1, c, nb)
@@ -1230,6 +1277,8 @@ class NativeUNet:
                      dst1=_ptr(b["z:" + l.name]) + self._toff(l.name, c, nb) if normed else P(l.name),
                      drop_rate=spec.dropout if (l.dropout and dropout and not normed) else 0.0,
                      salt=self._salt(l.name), drop_idx0=c * nb * (self.npix(l.level) // self.B) * l.cout)
+            if skip_xf:
+                d.update(self._skip_xf_fields(skip, c, nb))
             bits = self.relu_bits.get(l.name)
             if bits is not None and not normed:
                 d["relu_bits"] = _ptr(bits) + c * nb * (self.npix(l.level) // self.B) * l.cout // 8
@@ -1483,6 +1532,8 @@ class NativeUNet:
                     # chained u rows: the weight gradient runs over the skip source only;
                     # tconv_chain forms the u rows from H / Bs
                     a1, upA, c1w, c2w, skw = b[skip], 1, c2, 0, None
+                    if self._skip_onload.get(skip) == l.name:
+                        a1 = b["z:" + skip]          # (normalised on load: xform 1 below)
                 else:
                     a1, upA, c1w, c2w, skw = (b[src1] if src1 in b else None), up1, c1, c2, skip
                 if up1 == 2 and self.ups_materialize:
@@ -1496,6 +1547,8 @@ class NativeUNet:
                     kd.update(first_xf)
                 if spec.norm != "none" and split_xf is not None:
                     kd.update(split_xf)
+                if wa_t is not None and self._skip_onload.get(skip) == l.name:
+                    kd.update(xform=1, xa=_ptr(b["fa:" + skip]), xb=_ptr(b["fc:" + skip]), xcs=0)
                 if l.name == self.head_in and self.head_onload:
                     kd.update(self._head_grad_fields())
                 wspec = dict(lname=l.name, kd=kd, M1=c1w, M2=c2w, Nc=l.cout, KT=KT3, Q=Q,
@@ -1773,7 +1826,7 @@ class NativeUNet:
                 d.update(name="wgrad:" + w["lname"], M1=w["M1"], M2=w["M2"], Nc=w["Nc"], splits=splits,
                          win=self.wgrad_win, slab=slab, bias_mode=w["bias_mode"] if fused_bias else 0,
                          bias_slab=bslab, pair=int(self.opts["wg_pair"] >= (1 if self.dims == 3 else 2)),
-                         pf=int(self.opts["wg_pf"] >= (1 if self.dims == 3 else 2)))
+                         pf=int(self.opts["wg_pf"] >= (1 if self.dims == 3 else 2) or d.get("xform") == 1))
                 if part is not None:
                     d.update(split_lo=part * splits // 2, split_n=splits // 2)
                 if "dw" in w:
