@@ -602,9 +602,11 @@ def test_fused_dgrad_wgrad_norm_step(cuda_dev, monkeypatch, norm, dtype):
 @pytest.mark.parametrize("kw", [
     dict(batch_size=4, img_size=128, in_channels=4, norm="batch"),
     dict(batch_size=3, img_size=128, in_channels=4, norm="batch", loss="dice_bce", hip_graph=True),
+    dict(batch_size=4, img_size=128, in_channels=4, norm="group", dtype="fp16"),
+    dict(batch_size=6, img_size=128, in_channels=4, norm="group", hip_graph=True),
 ])
 def test_skip_onload_step_equals_materialised(cuda_dev, monkeypatch, kw):
-    """skip_onload=1 (BatchNorm default: conv9a's skip source conv1b is never stored in
+    """skip_onload=1 (normalised configs' default: conv9a's skip source conv1b is never stored in
     training -- the tconv-on-load forward and the chained skip-row weight gradient normalise
     its pre-norm z on load with norm_pool's formula) gives the materialised step bit for bit:
     loss sums, probabilities, every parameter gradient."""

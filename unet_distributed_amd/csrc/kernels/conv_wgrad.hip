@@ -1007,7 +1007,8 @@ __global__ void __launch_bounds__(NTHR, PAIR ? 3 : 2) wgrad_win_kernel(const Wgr
 // Same LDS images, swizzles, fragment reads, MFMA order and reduction as wgrad_win_kernel
 // with CARRY: bit-identical slabs.  xform 1 (BatchNorm, single source): the A operand is the
 // pre-norm z of a normalised activation, relu(xa z + xb) formed in registers before the LDS
-// store (padding stays zero) -- the activation itself need not be stored (norm_pool's y).
+// store (padding stays zero) -- the activation itself need not be stored (norm_pool's y);
+// coefficients [C] (BatchNorm) or [N][C] (GroupNorm, xcs = C: refreshed per image).
 template <bool CONCAT, int GEO, bool AXF = false>
 __global__ void __launch_bounds__(NTHR, 2) wgrad_pf128_kernel(const WgradParams p) {
   constexpr int W = 128, BMW = 256, R = 2, HWP = 144, IPR = 9, ROWB = HWP * 64;
@@ -1081,7 +1082,7 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_pf128_kernel(const WgradParams 
   // xform 1: the block's 32 channels' xa / xb in LDS (BatchNorm: one set for the launch)
   float* Kx = (float*)(smem + XB + YB);
   constexpr bool axf = AXF;
-  if (axf && tid < 64) Kx[tid] = (tid < 32 ? p.xa : p.xb)[ca0 + (tid & 31)];
+  if (axf && tid < 64 && !p.xcs) Kx[tid] = (tid < 32 ? p.xa : p.xb)[ca0 + (tid & 31)];
   // halo pieces k = kb + wave + 4 i (i < NX) of window `win` (input rows g0 - 1 + hr + gsh)
   u32x4 xr[NX], yr[NY];
   uint32_t xokm = 0;
@@ -1157,6 +1158,14 @@ __global__ void __launch_bounds__(NTHR, 2) wgrad_pf128_kernel(const WgradParams 
       // not prefetched: this window's rows (all four unless it carries) and dY, synchronously
       if (!carry) {
         load_x(win, 0);
+        if constexpr (AXF) {
+          if (p.xcs) {
+            // GroupNorm: the coefficients of this image's sample (a carried window never
+            // changes image, so only these windows refresh them)
+            if (tid < 64) Kx[tid] = (tid < 32 ? p.xa : p.xb)[(size_t)(g0 / H) * p.xcs + ca0 + (tid & 31)];
+            __syncthreads();
+          }
+        }
         store_x(0, fl);
       }
       load_x(win, 2 * IPR);
@@ -2021,9 +2030,8 @@ const char* wgrad_check(const WgradParams& p) {
   }
   if (p.xform != 0 && p.xform != 1 && p.xform != 2) return "wgrad: xform must be 0, 1 or 2";
   if (p.xform == 1 && (!p.pf || !wgrad_win_eligible(p) || p.QW != 128 || p.KD != 1 || p.QD != 1 || p.M2 != 0 ||
-                       p.M1 != 32 || p.xcs != 0 || !p.xa || !p.xb || p.hg.prob || p.pair))
-    return "wgrad: A normalised on load needs the prefetching 128-wide window (2D, one 32-channel source, "
-           "BatchNorm coefficients)";
+                       p.M1 != 32 || (p.xcs != 0 && p.xcs != p.M1) || !p.xa || !p.xb || p.hg.prob || p.pair))
+    return "wgrad: A normalised on load needs the prefetching 128-wide window (2D, one 32-channel source)";
   if (p.xform == 2 && (!p.xa || !p.xb || !p.xc || !p.xz || (p.xcs != 0 && p.xcs != p.Nc) ||
                        (wgrad_win_first_eligible(p)
                             ? (p.xcs && p.QH % ((p.QW > 256 ? p.QW : 256) / p.QW)) != 0

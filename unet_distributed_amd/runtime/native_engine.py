@@ -59,8 +59,8 @@ def _r64(k: int) -> int:
 #   head_onload  the head input's gradient formed on load by its consumers (1: 2D; 2: 3D too)
 #   head_wsum    the Mask gradients from per-workgroup sums of the fused-head forward; the head
 #                input is not stored (1)
-#   skip_onload  BatchNorm: conv9a's skip source read as pre-norm z by its consumers, never stored
-#                in training (1)
+#   skip_onload  normalised configs: conv9a's skip source read as pre-norm z by its consumers, never
+#                stored in training (1)
 #   win_cp3      win_cp of the 3D model (2: the 3D level-1 convs on the chunk-pipelined 128-wide
 #                window, conv_win_cp128_kernel -- -10..-12 % per launch, +2 % on the 3D step in
 #                round 6; neutral in round 5, before the 3D weight-gradient prefetch)
@@ -156,7 +156,7 @@ FUSIONS: Dict[str, Fusion] = {
                            option="tconv_onload", needs=("tconv_wa",)),
     "skip_onload": Fusion("a normalised skip source normalised on load by its tconv-on-load consumer and the "
                           "chained skip-row weight gradient: never stored in training (x2a / xform 1)",
-                          norm={"batch"}, dims={2}, option="skip_onload", when=lambda e: e.wgrad_win >= 0),
+                          norm={"batch", "group"}, dims={2}, option="skip_onload", when=lambda e: e.wgrad_win >= 0),
     "norm_onload": Fusion("normalisation of an 'a' conv's output on load by its consumer (XF 1)",
                           norm={"batch", "group"}, dims={2}),
     "skip_route": Fusion("skip-half data gradient with the pool backward in its epilogue", dims={2}),
@@ -629,15 +629,16 @@ class NativeUNet:
         any op that would still read S's activation."""
         src1, up1, skip = self.inputs[c.name]
         if (skip is None or skip not in self.norm_layers or not self._fusion_ok("skip_onload", skip)
-                or self.spec.norm != "batch" or self.tinfo[skip][3] or self.tinfo[skip][1] != 32):
+                or self.tinfo[skip][3] or self.tinfo[skip][1] != 32):
             return
         b = self.bufs
-        probe = dict(d, src2=1, x2a=_ptr(b["fa:" + skip]), x2b=_ptr(b["fc:" + skip]), x2cs=0)
+        xcs = 0 if self.spec.norm == "batch" else 32
+        probe = dict(d, src2=1, x2a=_ptr(b["fa:" + skip]), x2b=_ptr(b["fc:" + skip]), x2cs=xcs)
         sd = self.sdims(c.level)
         wk = dict(N=self.B, QD=sd[0], QH=sd[1], QW=sd[2], AD=sd[0], AH=sd[1], AW=sd[2], KD=1, KH=3, KW=3,
                   stride=1, pad=1, upA=1, a1=_ptr(b["z:" + skip]), b=_ptr(b[skip]), M1=32, M2=0, Nc=c.cout,
                   splits=1, win=self.wgrad_win, bias_mode=1, pf=1, xform=1, xa=_ptr(b["fa:" + skip]),
-                  xb=_ptr(b["fc:" + skip]), xcs=0)
+                  xb=_ptr(b["fc:" + skip]), xcs=xcs)
         try:
             if self.C.conv_fwd_grid(probe) <= 0:
                 return
@@ -650,8 +651,10 @@ class NativeUNet:
     def _skip_xf_fields(self, skip, c, nb):
         """x2* fields of the tconv-on-load consumer reading skip source `skip` as pre-norm z."""
         b = self.bufs
-        return dict(src2=_ptr(b["z:" + skip]) + self._toff(skip, c, nb), x2a=_ptr(b["fa:" + skip]),
-                    x2b=_ptr(b["fc:" + skip]), x2cs=0)
+        C = self.tinfo[skip][1]
+        mo = 0 if self.spec.norm == "batch" else c * nb * C * 4       # per-sample [B][C] coefficients
+        return dict(src2=_ptr(b["z:" + skip]) + self._toff(skip, c, nb), x2a=_ptr(b["fa:" + skip]) + mo,
+                    x2b=_ptr(b["fc:" + skip]) + mo, x2cs=0 if self.spec.norm == "batch" else C)
 
     # ------------------------------------------------------------------ normalisation
     NORM_EPS = 1e-3          # models/reference.py::_norm (Keras default epsilon)
@@ -1548,7 +1551,8 @@ class NativeUNet:
                 if spec.norm != "none" and split_xf is not None:
                     kd.update(split_xf)
                 if wa_t is not None and self._skip_onload.get(skip) == l.name:
-                    kd.update(xform=1, xa=_ptr(b["fa:" + skip]), xb=_ptr(b["fc:" + skip]), xcs=0)
+                    kd.update(xform=1, xa=_ptr(b["fa:" + skip]), xb=_ptr(b["fc:" + skip]),
+                              xcs=0 if spec.norm == "batch" else self.tinfo[skip][1])
                 if l.name == self.head_in and self.head_onload:
                     kd.update(self._head_grad_fields())
                 wspec = dict(lname=l.name, kd=kd, M1=c1w, M2=c2w, Nc=l.cout, KT=KT3, Q=Q,
