@@ -623,3 +623,31 @@ def test_skip_onload_step_equals_materialised(cuda_dev, monkeypatch, kw):
     (s0, p0, g0), (s1, p1, g1) = outs
     assert torch.equal(s0, s1) and torch.equal(p0, p1)
     assert torch.equal(g0, g1)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(batch_size=2, img_size=32, in_channels=4, dims=3),
+    dict(batch_size=1, img_size=64, in_channels=4, dims=3, loss="dice_bce"),
+    dict(batch_size=2, img_size=32, in_channels=4, dims=3, norm="batch"),
+])
+def test_route3_step_equals_separate_pool_bwd(cuda_dev, monkeypatch, kw):
+    """3D skip_route (route3=1: the decoder data gradients split, the skip half deferred and
+    carrying the pool backward in its epilogue with 3-bit window codes) vs the dual-destination
+    data gradient + separate pool backward: loss sums and probabilities bit for bit, parameter
+    gradients to rounding (the split halves' MFMA tiles may differ)."""
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("UNET_ENGINE", "route3=" + v)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
+        e = nb.engine
+        assert bool(e.fusions.get("skip_route")) == (v == "1")
+        nb.fwd_bwd(x, y, seed=41)
+        torch.cuda.synchronize()
+        outs.append((nb.sums().cpu(), e.prob.clone(), {k: fn.view(fn.grad, k).clone() for k, *_ in fn.entries}))
+    (s0, p0, g0), (s1, p1, g1) = outs
+    assert torch.equal(s0, s1) and torch.equal(p0, p1)
+    for k in g0:
+        if kw.get("norm") == "batch" and k.endswith("/bias") and not k.startswith("Mask"):
+            continue
+        if g0[k].norm() > 1e-6:
+            assert rel_err_(g1[k], g0[k]) < 2e-3, (k, rel_err_(g1[k], g0[k]))

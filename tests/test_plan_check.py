@@ -157,3 +157,20 @@ def test_dz_split_option_plans_validate(norm, img):
     n1 = [n for n in e1.plan.names() if n.startswith("norm_bwd:")]
     assert sorted(set(n0) - set(n1)) == sorted("norm_bwd:" + l for l in lay)
     assert all("dz:" + l not in e1.bufs for l in lay)
+
+
+@pytest.mark.parametrize("norm,ups,img", [("none", False, 32), ("none", True, 32), ("batch", False, 32),
+                                          ("none", False, 128)])
+def test_route3_option_plans_validate(norm, ups, img):
+    """Option route3=1: 3D decoder data gradients split, their skip half deferred to the
+    pool backward's slot carrying it in the epilogue (conv_epilogue.h route_pix, 3-bit
+    codes); every bwd:pool launch of the routed skips is gone and the plan validates."""
+    e0 = _engine(norm, ups, 3, img, opts=dict(route3=0))
+    e1 = _engine(norm, ups, 3, img, opts=dict(route3=1))
+    assert check_engine(e1) == {"train": [], "eval": []}
+    assert not e0.fusions.get("skip_route")
+    lay = e1.fusions.get("skip_route", [])
+    assert lay
+    names = e1.plan.names()
+    assert sum(n.startswith("dgrad_skip:") for n in names) == len(lay)
+    assert sum(n.startswith("bwd:pool") for n in names) == sum(n.startswith("bwd:pool") for n in e0.plan.names()) - len(lay)

@@ -45,6 +45,25 @@ constexpr int epi_lds_bytes() {
   return BM * (BN + 4) * 2 + (NTHR / 64) * 2 * BN * 4;
 }
 
+// Fused max-pool backward (route_gy): pooled pixel of output pixel q, and in rk the
+// window corner q is, in elementwise.hip::maxpool2_fwd_kernel's order -- 2D k =
+// 2 (h & 1) + (w & 1), 3D k = 4 (d & 1) + 2 (h & 1) + (w & 1) (q = ((n D + d) H + h) W + w)
+__device__ __forceinline__ size_t route_pix(const ConvFwdParams& p, int q, uint32_t& rk) {
+  const int g = q / p.OW, w = q - g * p.OW;
+  if (p.OD > 1) {
+    const int s = g / p.OH, h = g - s * p.OH;
+    rk = ((uint32_t)(s & 1) << 2) | ((uint32_t)(h & 1) << 1) | (uint32_t)(w & 1);
+    return ((size_t)(s >> 1) * (p.OH >> 1) + (h >> 1)) * (p.OW >> 1) + (w >> 1);
+  }
+  rk = ((uint32_t)(g & 1) << 1) | (uint32_t)(w & 1);
+  return (size_t)(g >> 1) * (p.OW >> 1) + (w >> 1);
+}
+// channel e of a pool code word routes to corner rk (its first maximum, and positive)
+__device__ __forceinline__ bool route_hit(uint32_t cw, int e, uint32_t rk, bool d3) {
+  const uint32_t k = d3 ? (cw >> (3 * e)) & 7u : (cw >> (2 * e)) & 3u;
+  return k == rk && ((cw >> (24 + e)) & 1u);
+}
+
 // nullptr when the normalisation fields of p form a supported epilogue
 __host__ __device__ inline const char* conv_norm_epi_check(const ConvFwdParams& p) {
   if (!p.stats && !p.nz) return nullptr;
@@ -310,20 +329,18 @@ __device__ __forceinline__ HeadWsum conv_epilogue(const ConvFwdParams p, f32x4 (
     }
     // fused max-pool backward (route_gy; the skip half of a decoder data gradient): the
     // pooled gradient is added at each window's recorded argmax before the mask
-    const bool route = p.route_gy != nullptr;
+    const bool route = p.route_gy != nullptr, d3 = p.OD > 1;
     u32x4 rg[NIT];
     uint32_t rc[NIT], rk[NIT];
     if (route) {
-      const int OW = p.OW, cpp = p.Cout >> 3;
+      const int cpp = p.Cout >> 3;
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
         const int q = qof(ml0 + it * RPI);
         if (q < M) {
-          const int gr = q / OW, w = q - gr * OW;
-          const size_t pq = (size_t)(gr >> 1) * (OW >> 1) + (w >> 1);
+          const size_t pq = route_pix(p, q, rk[it]);
           rc[it] = p.pool_code[pq * cpp + (n >> 3)];
           rg[it] = *(const u32x4*)((const h16*)p.route_gy + pq * p.Cout + n);
-          rk[it] = ((uint32_t)(gr & 1) << 1) | (uint32_t)(w & 1);
         }
       }
     }
@@ -348,7 +365,7 @@ __device__ __forceinline__ HeadWsum conv_epilogue(const ConvFwdParams p, f32x4 (
         const uint32_t cw = rc[it];
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          if (((cw >> (2 * e)) & 3u) == rk[it] && ((cw >> (24 + e)) & 1u)) g[e] += gg[e];
+          if (route_hit(cw, e, rk[it], d3)) g[e] += gg[e];
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -394,22 +411,19 @@ __device__ __forceinline__ HeadWsum conv_epilogue(const ConvFwdParams p, f32x4 (
         }
       }
     }
-    // fused pool backward (route_gy, 2D, one destination): pixel q = (row g, column w)
-    // is window position k = 2 (g & 1) + (w & 1) of pooled pixel (g / 2, w / 2)
-    const bool route = p.route_gy != nullptr;
+    // fused pool backward (route_gy, one destination; route_pix / route_hit)
+    const bool route = p.route_gy != nullptr, d3 = p.OD > 1;
     u32x4 rg[NIT];
     uint32_t rc[NIT], rk[NIT];
     if (route) {
-      const int OW = p.OW, cpp = p.Cout >> 3;
+      const int cpp = p.Cout >> 3;
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
         const int q = qof(ml0 + it * RPI);
         if (q < M) {
-          const int g = q / OW, w = q - g * OW;
-          const size_t pq = (size_t)(g >> 1) * (OW >> 1) + (w >> 1);
+          const size_t pq = route_pix(p, q, rk[it]);
           rc[it] = p.pool_code[pq * cpp + (n >> 3)];
           rg[it] = *(const u32x4*)((const h16*)p.route_gy + pq * p.Cout + n);
-          rk[it] = ((uint32_t)(g & 1) << 1) | (uint32_t)(w & 1);
         }
       }
     }
@@ -429,7 +443,7 @@ __device__ __forceinline__ HeadWsum conv_epilogue(const ConvFwdParams p, f32x4 (
         const uint32_t cw = rc[it];
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          if (((cw >> (2 * e)) & 3u) == rk[it] && ((cw >> (24 + e)) & 1u)) o[e] += gg[e];
+          if (route_hit(cw, e, rk[it], d3)) o[e] += gg[e];
         v = pack8(o);
       }
       *(u32x4*)(dst + (size_t)q * rs + co) = v;

@@ -1110,10 +1110,10 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
              "32 / 64 / 128 coarse channels, (W / 32) (C / 32) <= 8)";
   }
   if (p.route_gy && (!p.pool_code || (conv_epi_mode(p) != EPI_DGRAD && conv_epi_mode(p) != EPI_DGRAD_NORM) ||
-                     !win_eligible(p) || p.KD != 1 || p.OD != 1 ||
+                     !win_eligible(p) || (p.OD == 1 ? p.KD != 1 : p.OD % 2 != 0) ||
                      p.OH % 2 || p.OW % 2 || p.D1 != p.Cout || p.pool_dst || p.mask_scale1 != 1.f ||
                      !(win_tile(conv_fwd_pick(p)) || conv_fwd_pick(p) == 14)))
-    return "conv_fwd: fused pool backward needs a 2D row-window data gradient (even dims, one destination, codes)";
+    return "conv_fwd: fused pool backward needs a row-window data gradient (even dims, one destination, codes)";
   if (p.pool_dst) {
     const int W = p.OW > 128 ? 128 : p.OW;
     const int R = win_rows(p);

@@ -90,9 +90,13 @@ def _r64(k: int) -> int:
 #   wg_pair      row-window weight gradients of 32-channel output blocks with wave-pair partials
 #                (conv_wgrad.hip wgrad_win_kernel PAIR: three workgroups per CU): 1 = 3D only,
 #                2 = 2D as well, 0 off (0)
+#   route3       3D: the decoder's skip-half data gradient carries the pool backward in its
+#                epilogue (skip_route; the data gradient splits in two launches) (1: measured
+#                -0.26 ms launch sum, +1.5..3 % 3D b8 bench, r6_bench_history.md)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
                        tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8, win_cp=1,
-                       wg_pair=0, dz_split=0, head_wsum=1, xf_drop=0, wg_pf=1, win_cp3=2, skip_onload=1)
+                       wg_pair=0, dz_split=0, head_wsum=1, xf_drop=0, wg_pf=1, win_cp3=2, skip_onload=1,
+                       route3=1)
 
 
 class Fusion:
@@ -159,7 +163,8 @@ FUSIONS: Dict[str, Fusion] = {
                           norm={"batch", "group"}, dims={2}, option="skip_onload", when=lambda e: e.wgrad_win >= 0),
     "norm_onload": Fusion("normalisation of an 'a' conv's output on load by its consumer (XF 1)",
                           norm={"batch", "group"}, dims={2}),
-    "skip_route": Fusion("skip-half data gradient with the pool backward in its epilogue", dims={2}),
+    "skip_route": Fusion("skip-half data gradient with the pool backward in its epilogue",
+                         when=lambda e: e.dims == 2 or e.opts["route3"] >= 1),
     "tail_halves": Fusion("last data gradient in two batch halves (first-layer wgrad overlap)",
                           norm={"none"}, dims={2}, img=_ROW_IMGS, even_batch=True, cpad=(4, 8),
                           when=lambda e: e.wgrad_win >= 0),
@@ -1027,8 +1032,8 @@ class NativeUNet:
 
     def _skip_route(self, l, skip, c1, c2, dy):
         """(pool name, dgrad dict) of the deferred skip half of decoder conv l's data
-        gradient when it can carry the pool backward of its skip source (2D row-window
-        data gradient), else None (the dual-destination dgrad + separate pool backward).  Saves the skip-gradient tensor's
+        gradient when it can carry the pool backward of its skip source (row-window
+        data gradient; 3D with option route3), else None (the dual-destination dgrad + separate pool backward).  Saves the skip-gradient tensor's
         write and re-read: the pool backward's read of it becomes a second read of dy."""
         if not self._fusion_ok("skip_route"):
             return None
