@@ -651,3 +651,34 @@ def test_route3_step_equals_separate_pool_bwd(cuda_dev, monkeypatch, kw):
             continue
         if g0[k].norm() > 1e-6:
             assert rel_err_(g1[k], g0[k]) < 2e-3, (k, rel_err_(g1[k], g0[k]))
+
+
+@pytest.mark.parametrize("kw", [
+    dict(batch_size=1, img_size=128, in_channels=4, dims=3),
+    dict(batch_size=2, img_size=128, in_channels=4, dims=3, loss="dice_bce"),
+])
+def test_head_wsum3d_step_matches(cuda_dev, monkeypatch, kw):
+    """3D head_wsum=2 (the 128-wide chunk-pipelined fused-head forward accumulates the Mask
+    weight sums and does not store the head input; head_dy forms the head input's dY from its
+    ReLU bits) vs head_wsum=1 (3D: head_bwd re-reads the stored head input): identical loss
+    sums, probabilities and every other gradient bit for bit; the Mask gradients equal up to
+    fp32 summation order."""
+    outs = []
+    for v in ("1", "2"):
+        monkeypatch.setenv("UNET_ENGINE", "head_wsum=" + v)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
+        e = nb.engine
+        assert bool(e.fusions.get("head_wsum")) == (v == "2")
+        assert ("wgrad:Mask" in e.plan.names()) == (v == "2")
+        for seed in (61, 62):
+            nb.fwd_bwd(x, y, seed=seed)
+        torch.cuda.synchronize()
+        outs.append((nb.sums().cpu(), e.prob.clone(), {k: fn.view(fn.grad, k).clone() for k, *_ in fn.entries}))
+    (s0, p0, g0), (s1, p1, g1) = outs
+    assert torch.equal(s0, s1) and torch.equal(p0, p1)
+    for k in g0:
+        if k.startswith("Mask/"):
+            err = ((g1[k] - g0[k]).abs().max() / (g0[k].abs().max() + 1e-12)).item()
+            assert err < 1e-4, (k, err)
+        else:
+            assert torch.equal(g0[k], g1[k]), k

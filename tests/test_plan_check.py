@@ -174,3 +174,15 @@ def test_route3_option_plans_validate(norm, ups, img):
     names = e1.plan.names()
     assert sum(n.startswith("dgrad_skip:") for n in names) == len(lay)
     assert sum(n.startswith("bwd:pool") for n in names) == sum(n.startswith("bwd:pool") for n in e0.plan.names()) - len(lay)
+
+
+def test_head_wsum3d_option_plans_validate():
+    """Option head_wsum=2 on the 3D 128^3 model: the fused-head forward accumulates the Mask
+    weight sums and stores no head input; the backward forms its dY from the ReLU bits
+    (head_dy) and finishes the Mask gradients from the sums; the plan validates."""
+    e1 = _engine("none", False, 3, 128, batch=2, opts=dict(head_wsum=2))
+    assert check_engine(e1) == {"train": [], "eval": []}
+    assert e1.fusions.get("head_wsum") == ["conv9b"]
+    assert "wgrad:Mask" in e1.plan.names() and "bwd:Mask" in e1.plan.names()
+    e0 = _engine("none", False, 3, 128, batch=2)
+    assert not e0.fusions.get("head_wsum") and "wgrad:Mask" not in e0.plan.names()

@@ -1149,9 +1149,11 @@ const char* conv_fwd_prepare(ConvFwdParams& p) {
   if ((p.x2a || p.x2b) && (!p.x2a || !p.x2b || !win_pfu_eligible(p) || (p.x2cs != 0 && p.x2cs != p.C2)))
     return "conv_fwd: the skip source normalised on load needs the persistent tconv-on-load window";
   if ((p.head_ws || p.head_nostore) &&
-      (!p.head_w || !win_pf_eligible(p) || p.OW != 128 || (p.head_ws && !p.head_t) || !p.relu_bits))
+      (!p.head_w || p.OW != 128 || (p.head_ws && !p.head_t) || !p.relu_bits ||
+       !(win_pf_eligible(p) || (p.KD == 3 && p.OD > 1 && p.Cout == 32 && win_tile(conv_fwd_pick(p)) &&
+                                win_bn(p) == 32 && win_bm(p) == 512 && win_cp128_eligible(p)))))
     return "conv_fwd: Mask weight sums / an unstored head input need the persistent 128-wide fused-head window "
-           "with ReLU bits";
+           "(3D: the 128-wide chunk-pipelined window) with ReLU bits";
   if ((long long)p.N * p.ID * p.IH * p.IW >= (1LL << 31) || (long long)p.N * p.OD * p.OH * p.OW >= (1LL << 31))
     return "conv_fwd: too many pixels";
   // buffer loads use 32-bit byte offsets: the row-window kernels count them from the

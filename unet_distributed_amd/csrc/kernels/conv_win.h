@@ -713,6 +713,38 @@ constexpr int PF_CPT = 6 * 128 * 4 / NTHR;    // 16-byte granules of the 6 halo 
 constexpr int PF_XB = 6 * PF_ROWB, PF_WB = 9 * 32 * 64;
 static_assert(512 * 36 * 2 <= PF_XB, "epilogue staging aliases the halo image");
 
+// The workgroup's Mask weight sums (conv_params.h head_ws) -> one 100-float row: lanes l,
+// l ^ 4, .. hold the same 8 channels (chunk tid & 3), folded in a fixed order, then the 4
+// waves through LDS (smem: the epilogue's staging, free after a barrier)
+__device__ __forceinline__ void head_ws_store(HeadWsum& hws, char* smem, const int wave, const int lane,
+                                              const int tid, float* row) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) hws.s[k][e] += __shfl_xor(hws.s[k][e], o, 64);
+  hws.u = wave_sum(hws.u);
+  hws.v = wave_sum(hws.v);
+  hws.w = wave_sum(hws.w);
+  float* red = (float*)smem;                         // [wave][100]
+  __syncthreads();                                   // the last epilogue's staging reads are done
+  if (lane < 4) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wave * 100 + k * 32 + lane * 8 + e] = hws.s[k][e];
+  }
+  if (lane == 0) {
+    red[wave * 100 + 96] = hws.u;
+    red[wave * 100 + 97] = hws.v;
+    red[wave * 100 + 98] = hws.w;
+    red[wave * 100 + 99] = 0.f;
+  }
+  __syncthreads();
+  if (tid < 100) row[tid] = (red[tid] + red[100 + tid]) + (red[200 + tid] + red[300 + tid]);
+}
+
 // GEO_SEG: rows of Wf = p.OW > 128 pixels as 128-wide segments (window = 4 rows x one
 // segment, windows in (row group, segment) order as conv_win_kernel's); the halo columns
 // -1 / 128 are the neighbouring segments' pixels (zeros only at the row ends), loaded by 48
@@ -979,37 +1011,7 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_pf_kernel(const ConvFwdParam
     }
   }
   if constexpr (EPI == EPI_FWD && !SEG) {
-    if (p.head_ws) {
-      // the workgroup's Mask weight sums -> row blockIdx.x: lanes l, l ^ 4, .. hold the same 8
-      // channels (chunk tid & 3), folded in a fixed order, then the 4 waves through LDS
-#pragma unroll
-      for (int k = 0; k < 3; ++k)
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-#pragma unroll
-          for (int o = 4; o < 64; o <<= 1) hws.s[k][e] += __shfl_xor(hws.s[k][e], o, 64);
-      hws.u = wave_sum(hws.u);
-      hws.v = wave_sum(hws.v);
-      hws.w = wave_sum(hws.w);
-      float* red = (float*)smem;                     // [wave][100]
-      __syncthreads();                               // the last epilogue's staging reads are done
-      if (lane < 4) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) red[wave * 100 + k * 32 + lane * 8 + e] = hws.s[k][e];
-      }
-      if (lane == 0) {
-        red[wave * 100 + 96] = hws.u;
-        red[wave * 100 + 97] = hws.v;
-        red[wave * 100 + 98] = hws.w;
-        red[wave * 100 + 99] = 0.f;
-      }
-      __syncthreads();
-      if (tid < 100)
-        p.head_ws[(size_t)blockIdx.x * 100 + tid] =
-            (red[tid] + red[100 + tid]) + (red[200 + tid] + red[300 + tid]);
-    }
+    if (p.head_ws) head_ws_store(hws, smem, wave, lane, tid, p.head_ws + (size_t)blockIdx.x * 100);
   }
 }
 
@@ -1322,6 +1324,13 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_cp128_kernel(const ConvFwdPa
     xbase[dw] = r0 * ROWB + c0 * 64 + hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3));
   }
   const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
+  // head_ws (fused head): the targets of the thread's 8 epilogue pixels (tid / 4 + 64 it),
+  // loaded here and waited on only by the epilogue
+  HeadT ht;
+  ht.on = EPI == EPI_FWD && p.head_ws;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    ht.t[i] = (EPI == EPI_FWD && p.head_ws) ? bits2f(((const uint16_t*)p.head_t)[g0 * W + (tid >> 2) + 64 * i]) : 0.f;
   load_item(0);
   store_item();
   __syncthreads();
@@ -1355,9 +1364,13 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_cp128_kernel(const ConvFwdPa
       __syncthreads();
     }
   }
-  if constexpr (D3)
-    conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0, 0, tm);
-  else
+  if constexpr (D3) {
+    HeadWsum hws = conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map>(p, acc, smem, g0 * W, n0, M, wave, 0, lane,
+                                                                          tid, 0, 0, tm, nullptr, ht);
+    if constexpr (EPI == EPI_FWD) {
+      if (p.head_ws) head_ws_store(hws, smem, wave, lane, tid, p.head_ws + (size_t)blockIdx.x * 100);
+    }
+  } else
     conv_epilogue<BM, BN, WMP, BN, TM, TN, NTHR, EPI, Map, 0, W>(p, acc, smem, g0 * W, n0, M, wave, 0, lane, tid, 0, 0,
                                                                   tm);
 }

@@ -197,6 +197,37 @@ __global__ void __launch_bounds__(HT) head_bwd_kernel(const h16* __restrict__ x,
   }
 }
 
+// dY of the head input from its ReLU bits (head_wsum without head-on-load: the fused-head
+// forward stores neither the head input nor needs it here -- the Mask gradients come from its
+// sums): dx[p][c] = dlogit(p) w[c] where bit c of pixel p is set, head_bwd_kernel's values.
+// bits: C / 8 bytes per pixel (byte = channel chunk, bit e = channel 8 chunk + e).
+template <int C>
+__global__ void __launch_bounds__(HT) head_dy_kernel(const uint8_t* __restrict__ bits, const float* __restrict__ w,
+                                                     const float* __restrict__ prob, const h16* __restrict__ t,
+                                                     const float* __restrict__ sums, int P, float inv_total,
+                                                     float bce_w, float gscale, const float* __restrict__ gscale_ptr,
+                                                     h16* __restrict__ dx) {
+  constexpr int CP = C / 8;
+  if (gscale_ptr) gscale = *gscale_ptr;
+  const int cc = threadIdx.x % CP;
+  float wr[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) wr[e] = w[cc * 8 + e];
+  const float I = sums[0], St = sums[1], Sp = sums[2];
+  const float a = -2.f / (2.f * I + 1.f);
+  const float bb = 1.f / (St + Sp + 1.f);
+  const int total = P * CP;                            // < 2^31 (head_check / planner)
+  for (int i = blockIdx.x * HT + threadIdx.x; i < total; i += gridDim.x * HT) {
+    const int p = i / CP;
+    const float dz = head_dlogit(prob[p], (float)t[p], a, bb, inv_total, bce_w, gscale);
+    const uint32_t m = bits[i];
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = ((m >> e) & 1u) ? dz * wr[e] : 0.f;
+    *(u32x4*)(dx + (size_t)i * 8) = pack8(o);
+  }
+}
+
 // Mask gradients from the forward's sums (conv_params.h head_ws; conv_win_pf_kernel with the
 // fused head): head_grad.h's dlogit = A u + B v + G w per pixel with the batch scalars
 // A = a gs, B = bb gs, G = bce_w inv_total gs, so
@@ -311,6 +342,27 @@ hipError_t head_bwd_launch(const void* x, const float* w, const float* prob, con
                          sums, P, inv_total, bce_w, gscale, gscale_ptr, (h16*)dx, partial);
   }
   UNET_LAUNCH(head_grad_reduce_kernel, dim3(C + 1), dim3(256), 0, s, partial, nb, C, gw, gb);
+  return launch_status();
+}
+
+hipError_t head_dy_launch(const void* bits, const float* w, const float* prob, const void* t, const float* sums, int P,
+                          int C, float inv_total, float bce_w, float gscale, const float* gscale_ptr, void* dx,
+                          hipStream_t s) {
+  if ((long long)P * (C / 8) >= (1LL << 31)) return hipErrorInvalidValue;
+  const int nb = head_blocks(P);
+  switch (C) {
+    case 16:
+      UNET_LAUNCH(head_dy_kernel<16>, dim3(nb), dim3(HT), 0, s, (const uint8_t*)bits, w, prob, (const h16*)t, sums,
+                  P, inv_total, bce_w, gscale, gscale_ptr, (h16*)dx);
+      break;
+    case 32:
+      UNET_LAUNCH(head_dy_kernel<32>, dim3(nb), dim3(HT), 0, s, (const uint8_t*)bits, w, prob, (const h16*)t, sums,
+                  P, inv_total, bce_w, gscale, gscale_ptr, (h16*)dx);
+      break;
+    default:
+      UNET_LAUNCH(head_dy_kernel<64>, dim3(nb), dim3(HT), 0, s, (const uint8_t*)bits, w, prob, (const h16*)t, sums,
+                  P, inv_total, bce_w, gscale, gscale_ptr, (h16*)dx);
+  }
   return launch_status();
 }
 

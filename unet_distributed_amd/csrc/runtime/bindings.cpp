@@ -291,6 +291,7 @@ F32Wgrad f32_wgrad_params(const py::dict& d) {
   X(head_fwd_launch) \
   X(head_bwd_launch) \
   X(head_wsum_grad_launch) \
+  X(head_dy_launch) \
   X(partial_reduce_launch) \
   X(head_finish_launch) \
   X(norm_head_launch) \
@@ -577,6 +578,17 @@ Launcher make_generic(const KernelApi* A, const std::string& kind, const std::ve
     return [=](hipStream_t s) {
       return A->head_bwd_launch(x, w, prob, t, sums, P_, C, it, bw, gs, gsp, dx, part, gw, gb, s);
     };
+  }
+  if (kind == "head_dy") {
+    // ptrs: relu bits, w, prob, t, sums, dx [, device loss scale]   ints: P, C   floats: inv_total, bce_w, gscale
+    need(6, 2, 3);
+    void *bits = vp(0), *t = vp(3), *dx = vp(5);
+    const float *w = (const float*)vp(1), *prob = (const float*)vp(2), *sums = (const float*)vp(4);
+    const float* gsp = P.size() > 6 ? (const float*)vp(6) : nullptr;
+    const int P_ = (int)I[0], C = (int)I[1];
+    const float it = (float)F[0], bw = (float)F[1], gs = (float)F[2];
+    check_msg(head_check(C));
+    return [=](hipStream_t s) { return A->head_dy_launch(bits, w, prob, t, sums, P_, C, it, bw, gs, gsp, dx, s); };
   }
   if (kind == "head_wsum_grad") {
     // ptrs: rows (head_ws), sums, gw, gb [, device loss scale]   ints: nrows   floats: inv_total, bce_w, gscale

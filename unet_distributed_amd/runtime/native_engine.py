@@ -90,6 +90,8 @@ def _r64(k: int) -> int:
 #   wg_pair      row-window weight gradients of 32-channel output blocks with wave-pair partials
 #                (conv_wgrad.hip wgrad_win_kernel PAIR: three workgroups per CU): 1 = 3D only,
 #                2 = 2D as well, 0 off (0)
+#   head_wsum    Mask weight gradients from the fused-head forward's sums: 1 = 2D (with head-on-load),
+#                2 = 3D as well (head_dy forms dY from the ReLU bits; measured neutral on 3D b8), 0 off (1)
 #   route3       3D: the decoder's skip-half data gradient carries the pool backward in its
 #                epilogue (skip_route; the data gradient splits in two launches) (1: measured
 #                -0.26 ms launch sum, +1.5..3 % 3D b8 bench, r6_bench_history.md)
@@ -147,8 +149,10 @@ FUSIONS: Dict[str, Fusion] = {
     "head_fuse": Fusion("Mask head in the epilogue of its input conv's forward",
                         norm={"none"}, option="head_fuse", when=lambda e: e.tinfo[e.head_in][1] == 32),
     "head_wsum": Fusion("Mask weight / bias gradients from sums the head-input conv's forward accumulates "
-                        "(conv_params.h head_ws): no backward pass over the head input, which is never stored",
-                        norm={"none"}, dims={2}, option="head_wsum", needs=("head_fuse", "head_onload")),
+                        "(conv_params.h head_ws): the head input is never stored -- 2D: with head-on-load, no "
+                        "backward pass over it; 3D (option head_wsum=2): its dY from the ReLU bits (head_dy)",
+                        norm={"none"}, option="head_wsum", needs=("head_fuse",),
+                        when=lambda e: (e.dims == 2 and e.head_onload) or (e.dims == 3 and e.opts["head_wsum"] >= 2)),
     "pool_epilogue": Fusion("2x2 max-pool in the convNb forward epilogue", norm={"none"}),
     "fwd_2streams": Fusion("training forward as two half-batch chunks on two streams",
                            norm={"none", "group"}, even_batch=True, when=lambda e: e.opts["fwd_streams"] == 2),
@@ -477,9 +481,12 @@ class NativeUNet:
         self.head_onload = self._fusion_ok("head_onload")
         if self.head_onload:
             self._fusion_on("head_onload", self.head_in)
+        # head_wsum without head-on-load (3D): the head backward forms dY from the head
+        # input's ReLU bits (head_dy), the input itself is not stored
+        self._head_dy = not self.head_onload and not FUSIONS["head_wsum"].unmet(self)
         if spec.norm == "none":
             for l in spec.layers:
-                if l.kind == "conv" and (l.name != self.head_in or self.head_onload):
+                if l.kind == "conv" and (l.name != self.head_in or self.head_onload or self._head_dy):
                     self.relu_bits[l.name] = torch.zeros(self.npix(l.level) * l.cout // 8, dtype=torch.uint8,
                                                          device=self.device)
         self._plan_tconv_fused()
@@ -1491,6 +1498,14 @@ class NativeUNet:
                              "bwd:Mask")
                 done("Mask")
             elif l.kind == "mask" and self.fusions.get("head_wsum"):
+                if not self.head_onload:
+                    # the head input's dY from its ReLU bits (the input was not stored)
+                    hc = self.tinfo[self.head_in][1]
+                    emit_generic("head_dy",
+                                 lambda: [_ptr(self.relu_bits[self.head_in]), self.master_ptr("Mask/kernel"),
+                                          _ptr(self.prob), _ptr(self.target), _ptr(self.sums),
+                                          _ptr(b["d:" + self.head_in]), _ptr(self.loss_scale_dev)],
+                                 [self.npix(1), hc], [inv_total, self.bce_weight, 1.0], "bwd:Mask")
                 # the Mask gradients from the forward's per-workgroup sums (head_ws)
                 emit_generic("head_wsum_grad",
                              lambda: [_ptr(self.head_ws), _ptr(self.sums), self.grad_ptr("Mask/kernel"),

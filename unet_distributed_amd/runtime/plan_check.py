@@ -77,9 +77,12 @@ def _conv_write_spans(d, stat_tiles=None) -> List[Tuple[int, int]]:
 
 
 def _generic_write_spans(kind: str, p: List[int], ints: List[int]) -> List[Tuple[int, int]]:
-    """(pointer, bytes) of the writes of the streaming norm passes (N, P, C in ints)."""
+    """(pointer, bytes) of the writes of the streaming norm passes (N, P, C in ints) and
+    the head dY pass (P, C)."""
     if kind in ("norm_apply", "norm_bwd_apply") and len(p) > 5 and len(ints) >= 3:
         return [(p[5], ints[0] * ints[1] * ints[2] * 2)]
+    if kind == "head_dy" and len(p) > 5 and len(ints) >= 2:
+        return [(p[5], ints[0] * ints[1] * 2)]
     return []
 
 
@@ -118,6 +121,8 @@ def _generic_rw(kind: str, p: List[int], ints: List[int]) -> Tuple[List[int], Li
         return _sel(p, [0, 1, 2, 3]), _sel(p, [4, 5, 6])
     if kind == "head_wsum_grad":
         return _sel(p, [0, 1, 4]), _sel(p, [2, 3])
+    if kind == "head_dy":
+        return _sel(p, [0, 1, 2, 3, 4, 6]), _sel(p, [5])
     if kind == "head_bwd":
         return _sel(p, [0, 1, 2, 3, 4, 9]), _sel(p, [5, 6, 7, 8])
     if kind == "norm_head":
