@@ -682,3 +682,28 @@ def test_head_wsum3d_step_matches(cuda_dev, monkeypatch, kw):
             assert err < 1e-4, (k, err)
         else:
             assert torch.equal(g0[k], g1[k]), k
+
+
+@pytest.mark.parametrize("kw", [
+    dict(batch_size=2, img_size=32, in_channels=4, dims=3),
+    dict(batch_size=2, img_size=128, in_channels=4, dims=3, loss="dice_bce"),
+])
+def test_tail3_step_matches(cuda_dev, monkeypatch, kw):
+    """3D tail halves (tail3=1: the last data gradient in two batch halves, the first layer's
+    weight gradient split at the same volume boundary so its first half overlaps the second
+    data-gradient half) vs one launch each: loss sums and probabilities bit for bit, gradients to
+    split-K summation order."""
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("UNET_ENGINE", "tail3=" + v)
+        spec, cfg, x, y, fn, nb, ft, tb = _setup(cuda_dev, **kw)
+        e = nb.engine
+        assert bool(e.fusions.get("tail_halves")) == (v == "1")
+        nb.fwd_bwd(x, y, seed=41)
+        torch.cuda.synchronize()
+        outs.append((nb.sums().cpu(), e.prob.clone(), {k: fn.view(fn.grad, k).clone() for k, *_ in fn.entries}))
+    (s0, p0, g0), (s1, p1, g1) = outs
+    assert torch.equal(s0, s1) and torch.equal(p0, p1)
+    for k in g0:
+        if g0[k].norm() > 1e-6:
+            assert rel_err_(g1[k], g0[k]) < 1e-3, (k, rel_err_(g1[k], g0[k]))

@@ -186,3 +186,13 @@ def test_head_wsum3d_option_plans_validate():
     assert "wgrad:Mask" in e1.plan.names() and "bwd:Mask" in e1.plan.names()
     e0 = _engine("none", False, 3, 128, batch=2)
     assert not e0.fusions.get("head_wsum") and "wgrad:Mask" not in e0.plan.names()
+
+
+@pytest.mark.parametrize("img,batch", [(32, 2), (128, 8)])
+def test_tail3_option_plans_validate(img, batch):
+    """Option tail3=1: the 3D model's last data gradient runs in two volume halves with the
+    first layer's weight gradient split between them; the plan validates."""
+    e = _engine("none", False, 3, img, batch=batch, opts=dict(tail3=1))
+    assert check_engine(e) == {"train": [], "eval": []}
+    assert e.fusions.get("tail_halves") == ["conv1b"]
+    assert e.plan.names().count("dgrad:conv1b") == 2 and e.plan.names().count("wgrad:conv1a") == 2

@@ -92,13 +92,14 @@ def _r64(k: int) -> int:
 #                2 = 2D as well, 0 off (0)
 #   head_wsum    Mask weight gradients from the fused-head forward's sums: 1 = 2D (with head-on-load),
 #                2 = 3D as well (head_dy forms dY from the ReLU bits; measured neutral on 3D b8), 0 off (1)
+#   tail3        3D: the last data gradient in two volume halves (tail_halves) (0: measured neutral)
 #   route3       3D: the decoder's skip-half data gradient carries the pool backward in its
 #                epilogue (skip_route; the data gradient splits in two launches) (1: measured
 #                -0.26 ms launch sum, +1.5..3 % 3D b8 bench, r6_bench_history.md)
 ENGINE_DEFAULTS = dict(dual_stream=1, fwd_streams=2, head_fuse=1, head_onload=1, tconv_fused=2, tconv_wa=1,
                        tconv_onload=1, fwd_offset=6, wg_target=512, dw_fuse=1, dw_wgs=512, win_pf=8, win_cp=1,
                        wg_pair=0, dz_split=0, head_wsum=1, xf_drop=0, wg_pf=1, win_cp3=2, skip_onload=1,
-                       route3=1)
+                       route3=1, tail3=0)
 
 
 class Fusion:
@@ -170,8 +171,8 @@ FUSIONS: Dict[str, Fusion] = {
     "skip_route": Fusion("skip-half data gradient with the pool backward in its epilogue",
                          when=lambda e: e.dims == 2 or e.opts["route3"] >= 1),
     "tail_halves": Fusion("last data gradient in two batch halves (first-layer wgrad overlap)",
-                          norm={"none"}, dims={2}, img=_ROW_IMGS, even_batch=True, cpad=(4, 8),
-                          when=lambda e: e.wgrad_win >= 0),
+                          norm={"none"}, img=_ROW_IMGS, even_batch=True, cpad=(4, 8),
+                          when=lambda e: e.wgrad_win >= 0 and (e.dims == 2 or e.opts["tail3"] >= 1)),
     "dw_fused": Fusion("data + weight gradient from one staged dY halo (conv_dw.hip; 128-pixel segments of "
                        "wider rows)", dims={2}, img=(128, 256, 512, 1024), option="dw_fuse",
                        when=lambda e: e.wgrad_win >= 0),
