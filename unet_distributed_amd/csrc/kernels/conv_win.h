@@ -1324,16 +1324,30 @@ __global__ void __launch_bounds__(NTHR, 2) conv_win_cp128_kernel(const ConvFwdPa
     xbase[dw] = r0 * ROWB + c0 * 64 + hc * 64 + 16 * (fsub ^ ((hc >> 1) & 3));
   }
   const int wbase = fr * 64 + 16 * (fsub ^ ((fr >> 1) & 3));
+  load_item(0);
   // head_ws (fused head): the targets of the thread's 8 epilogue pixels (tid / 4 + 64 it),
-  // loaded here and waited on only by the epilogue
+  // loaded behind item 0's halo (whose wait they share)
   HeadT ht;
   ht.on = EPI == EPI_FWD && p.head_ws;
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
-    ht.t[i] = (EPI == EPI_FWD && p.head_ws) ? bits2f(((const uint16_t*)p.head_t)[g0 * W + (tid >> 2) + 64 * i]) : 0.f;
-  load_item(0);
+  for (int i = 0; i < 8; ++i) ht.t[i] = 0.f;
+  if (EPI == EPI_FWD && p.head_ws) {
+    // one block of 8 loads (a per-element select became 8 branches, each waiting on its load)
+    const uint16_t* tp = (const uint16_t*)p.head_t + g0 * W + (tid >> 2);
+    uint16_t tv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tv[i] = tp[64 * i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ht.t[i] = bits2f(tv[i]);
+  }
   store_item();
   __syncthreads();
+  if constexpr (EPI == EPI_FWD) {
+    // the targets are complete here (item 0's halo wait covers them): keep the loads from
+    // being scheduled into the epilogue, where their round trip would be exposed
+#pragma unroll
+    for (int i = 0; i < 8; ++i) asm volatile("" : : "v"(ht.t[i]));
+  }
   for (int it = 0; it < nitems; ++it) {
     if (it + 1 < nitems) load_item(it + 1);            // in flight under this item's MFMAs
 #pragma unroll
